@@ -1,0 +1,348 @@
+"""TEST INFRASTRUCTURE ONLY — numpy/ctypes front-end of the CPU oracle.
+
+This module is the *checker* and the CPU baseline.  Only ``tests/``,
+``__graft_entry__.smoke()`` and ``bench.py``'s ``cpu_baseline`` leg may import
+it; the product package (``orpcd_amd``) never does.
+
+It wraps ``oracle/build/liborpcd_oracle.so`` (a C++ restatement of the
+Open3D 0.18.0 algorithms the reference delegates to — see the header of
+``orpcd_oracle.cpp``) and restates, in plain Python, the reference's own
+control flow for the hot path:
+
+* ``OracleGeneralizedICP.optimize``  — ``generalizedICP.py:47-83``
+* ``OracleAligner``                  — ``Aligner.py:36-317`` (refine excluded)
+* ``radius_scale`` / ``random_downsample`` — ``radiusScaler.py:18-30``,
+  ``randomDownsampler.py:29-37``
+
+Parity status: the Python control flow is pinned by golden vectors produced
+by importing the reference (``tests/golden/make_golden.py``).  The Open3D
+arithmetic (GICP / normals / FPFH / FGR) is **parity unpinned** against real
+Open3D, which is absent from this image.
+"""
+from __future__ import annotations
+
+import ctypes
+import math
+import os
+import subprocess
+from typing import List, Optional, Tuple
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "build", "liborpcd_oracle.so")
+
+_f64p = np.ctypeslib.ndpointer(dtype=np.float64, flags="C_CONTIGUOUS")
+_i32p = np.ctypeslib.ndpointer(dtype=np.int32, flags="C_CONTIGUOUS")
+_i64p = np.ctypeslib.ndpointer(dtype=np.int64, flags="C_CONTIGUOUS")
+_lib = None
+
+
+def build() -> str:
+    """Compile the oracle with its Makefile (gcc/OpenMP)."""
+    subprocess.run(["make", "-s", "-C", _HERE], check=True)
+    return LIB_PATH
+
+
+def lib():
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        build()
+    L = ctypes.CDLL(LIB_PATH)
+    c_i64, c_int, c_dbl = ctypes.c_int64, ctypes.c_int, ctypes.c_double
+    vp = ctypes.c_void_p
+    L.oracle_num_threads.restype = c_int
+    L.oracle_set_num_threads.argtypes = [c_int]
+    L.oracle_fast_eigen3x3.argtypes = [_f64p, _f64p]
+    L.oracle_gicp_cov_from_normal.argtypes = [_f64p, c_dbl, _f64p]
+    L.oracle_solve_psd6.argtypes = [_f64p, _f64p, _f64p, _f64p]
+    L.oracle_vec6_to_m4.argtypes = [_f64p, _f64p]
+    L.oracle_nn1_radius.argtypes = [_f64p, c_i64, _f64p, c_i64, c_dbl, _i32p, _f64p]
+    L.oracle_knn.argtypes = [_f64p, c_i64, c_int, _f64p, c_i64, c_int, c_dbl, _i32p, _f64p, _i32p]
+    L.oracle_estimate_normals.argtypes = [_f64p, c_i64, c_int, c_dbl, c_dbl, _f64p, _f64p, _f64p]
+    L.oracle_gicp.argtypes = [_f64p, c_i64, _f64p, c_i64, c_dbl, c_int, c_dbl, c_dbl, c_dbl,
+                              _f64p, _f64p, _f64p, _i32p, _i64p, vp, vp, vp]
+    L.oracle_gicp_step.argtypes = [_f64p, _f64p, c_i64, _f64p, _f64p, c_i64, _i32p, _f64p, _f64p, _f64p]
+    if hasattr(L, "oracle_fpfh"):
+        L.oracle_fpfh.argtypes = [_f64p, c_i64, c_dbl, c_int, c_dbl, c_int, _f64p, _f64p]
+        L.oracle_fgr.argtypes = [_f64p, c_i64, _f64p, c_i64, _f64p, _f64p, c_dbl, c_dbl, c_dbl, c_int, c_int,
+                                 c_int, ctypes.c_uint64, _f64p, _f64p, _f64p, _i64p, _i64p]
+    _lib = L
+    return L
+
+
+def _c3(a) -> np.ndarray:
+    a = np.ascontiguousarray(a, dtype=np.float64)
+    if a.ndim != 2 or a.shape[1] != 3:
+        raise ValueError(f"expected (N,3) array, got {a.shape}")
+    return a
+
+
+def set_num_threads(n: int) -> None:
+    lib().oracle_set_num_threads(int(n))
+
+
+def num_threads() -> int:
+    return int(lib().oracle_num_threads())
+
+
+# ---------------------------------------------------------------- primitives
+def fast_eigen3x3(cov: np.ndarray) -> np.ndarray:
+    out = np.zeros(3)
+    lib().oracle_fast_eigen3x3(np.ascontiguousarray(cov, dtype=np.float64).reshape(9), out)
+    return out
+
+
+def gicp_cov_from_normal(n: np.ndarray, eps: float = 1e-3) -> np.ndarray:
+    out = np.zeros(9)
+    lib().oracle_gicp_cov_from_normal(np.ascontiguousarray(n, dtype=np.float64), eps, out)
+    return out.reshape(3, 3)
+
+
+def solve_psd6(A: np.ndarray, b: np.ndarray) -> Tuple[bool, np.ndarray, float]:
+    x = np.zeros(6)
+    det = np.zeros(1)
+    rc = lib().oracle_solve_psd6(np.ascontiguousarray(A, dtype=np.float64).reshape(36),
+                                 np.ascontiguousarray(b, dtype=np.float64), x, det)
+    return rc == 0, x, float(det[0])
+
+
+def vec6_to_m4(x: np.ndarray) -> np.ndarray:
+    T = np.zeros(16)
+    lib().oracle_vec6_to_m4(np.ascontiguousarray(x, dtype=np.float64), T)
+    return T.reshape(4, 4)
+
+
+def nn1_radius(q: np.ndarray, t: np.ndarray, radius: float):
+    q, t = _c3(q), _c3(t)
+    idx = np.empty(len(q), np.int32)
+    d2 = np.empty(len(q))
+    lib().oracle_nn1_radius(q, len(q), t, len(t), float(radius), idx, d2)
+    return idx, d2
+
+
+def knn(pts: np.ndarray, q: np.ndarray, k: int, radius: float = -1.0):
+    pts = np.ascontiguousarray(pts, dtype=np.float64)
+    q = np.ascontiguousarray(q, dtype=np.float64)
+    dim = pts.shape[1]
+    idx = np.empty((len(q), k), np.int32)
+    d2 = np.empty((len(q), k))
+    cnt = np.empty(len(q), np.int32)
+    lib().oracle_knn(pts, len(pts), dim, q, len(q), int(k), float(radius), idx, d2, cnt)
+    return idx, d2, cnt
+
+
+def estimate_normals(pts: np.ndarray, knn_k: int = 20, radius: float = -1.0, eps: float = 1e-3):
+    """O3D EstimateNormals (fast) → (normals, raw covariance, GICP covariance)."""
+    pts = _c3(pts)
+    n = len(pts)
+    normals = np.empty((n, 3))
+    raw = np.empty((n, 3, 3))
+    cov = np.empty((n, 3, 3))
+    lib().oracle_estimate_normals(pts, n, int(knn_k), float(radius), float(eps), normals,
+                                  raw.reshape(-1), cov.reshape(-1))
+    return normals, raw, cov
+
+
+def gicp(source: np.ndarray, target: np.ndarray, max_correspondence_distance: float = 0.5,
+         max_iteration: int = 100, relative_fitness: float = 1e-6, relative_rmse: float = 1e-6,
+         epsilon: float = 1e-3, trace: bool = False) -> dict:
+    """registration_generalized_icp restated (O3D Registration.cpp RegistrationICP).
+
+    Returns Open3D's column-convention transformation (not transposed)."""
+    s, t = _c3(source), _c3(target)
+    T = np.zeros(16)
+    fit, rmse = np.zeros(1), np.zeros(1)
+    it = np.zeros(1, np.int32)
+    nc = np.zeros(1, np.int64)
+    tn = np.zeros(max_iteration + 1, np.int64) if trace else None
+    tf = np.zeros(max_iteration + 1) if trace else None
+    tr = np.zeros(max_iteration + 1) if trace else None
+    ptr = (lambda a: a.ctypes.data_as(ctypes.c_void_p) if a is not None else None)
+    rc = lib().oracle_gicp(s, len(s), t, len(t), float(max_correspondence_distance), int(max_iteration),
+                           float(relative_fitness), float(relative_rmse), float(epsilon), T, fit, rmse, it, nc,
+                           ptr(tn), ptr(tf), ptr(tr))
+    if rc != 0:
+        raise ValueError("oracle_gicp: invalid arguments")
+    out = dict(T=T.reshape(4, 4), fitness=float(fit[0]), rmse=float(rmse[0]), iters=int(it[0]),
+               ncorr=int(nc[0]))
+    if trace:
+        k = out["iters"] + 1
+        out["trace_ncorr"], out["trace_fitness"], out["trace_rmse"] = tn[:k], tf[:k], tr[:k]
+    return out
+
+
+def gicp_step(src, scov, tgt, tcov, corr_tgt):
+    src, tgt = _c3(src), _c3(tgt)
+    JTJ, JTr, upd = np.zeros(36), np.zeros(6), np.zeros(16)
+    lib().oracle_gicp_step(src, np.ascontiguousarray(scov, dtype=np.float64).reshape(-1), len(src), tgt,
+                           np.ascontiguousarray(tcov, dtype=np.float64).reshape(-1), len(tgt),
+                           np.ascontiguousarray(corr_tgt, dtype=np.int32), JTJ, JTr, upd)
+    return JTJ.reshape(6, 6), JTr, upd.reshape(4, 4)
+
+
+def fpfh(points: np.ndarray, normal_radius: float = 0.1, normal_knn: int = 20, fpfh_radius: float = 0.1,
+         fpfh_knn: int = 20):
+    """estimate_normals(Hybrid) + compute_fpfh_feature(Hybrid) → (normals (N,3), features (N,33))."""
+    p = _c3(points)
+    normals = np.empty((len(p), 3))
+    feat = np.empty((len(p), 33))
+    lib().oracle_fpfh(p, len(p), float(normal_radius), int(normal_knn), float(fpfh_radius), int(fpfh_knn),
+                      normals, feat.reshape(-1))
+    return normals, feat
+
+
+def fgr(source, target, source_feat, target_feat, division_factor=1.4, tuple_scale=0.9,
+        maximum_correspondence_distance=0.5, iteration_number=100, decrease_mu=True,
+        maximum_tuple_count=1000, seed=0) -> dict:
+    """registration_fgr_based_on_feature_matching restated (O3D FastGlobalRegistration.cpp)."""
+    s, t = _c3(source), _c3(target)
+    fs = np.ascontiguousarray(source_feat, dtype=np.float64)
+    ft = np.ascontiguousarray(target_feat, dtype=np.float64)
+    T = np.zeros(16)
+    fit, rmse = np.zeros(1), np.zeros(1)
+    nc, nm = np.zeros(1, np.int64), np.zeros(2, np.int64)
+    lib().oracle_fgr(s, len(s), t, len(t), fs.reshape(-1), ft.reshape(-1), float(division_factor),
+                     float(tuple_scale), float(maximum_correspondence_distance), int(iteration_number),
+                     int(bool(decrease_mu)), int(maximum_tuple_count), int(seed) & 0xFFFFFFFFFFFFFFFF, T, fit,
+                     rmse, nc, nm)
+    return dict(T=T.reshape(4, 4), fitness=float(fit[0]), rmse=float(rmse[0]), ncorr=int(nc[0]),
+                n_mutual=int(nm[0]), n_tuple_corr=int(nm[1]))
+
+
+# ------------------------------------------------- reference plugin restated
+class OracleGeneralizedICP:
+    """generalizedICP.py:15-83 restated on the oracle (an IOptimizer)."""
+
+    def __init__(self, max_correspondence_distance: float = 0.5, max_iterations: int = 100):
+        self._max_correspondence_distance = max_correspondence_distance if max_correspondence_distance > 0 else 0.5
+        self._max_iterations = max_iterations if max_iterations > 0 else 100
+        self.last = None
+
+    def optimize(self, source: np.ndarray, target: np.ndarray, **kwargs):
+        r = gicp(source, target, self._max_correspondence_distance, self._max_iterations)
+        self.last = r
+        roto_translation = np.copy(r["T"])                       # generalizedICP.py:72
+        roto_translation[:3, :3] = roto_translation[:3, :3].T    # generalizedICP.py:73-74
+        if r["rmse"] == 0:                                       # generalizedICP.py:77-81
+            raise ValueError("Optimization failed with loss = 0.")
+        return roto_translation, r["rmse"]
+
+
+class OracleFastGlobalOptimizer:
+    """fastGlobalOptimizer.py:23-190 restated on the oracle, including Q4:
+    the target features are computed from the SOURCE cloud (:137-142)."""
+
+    def __init__(self, division_factor=1.4, tuple_scale=0.9, maximum_correspondence_distance=0.5,
+                 iteration_number=100, decrease_mu=True, normal_estimate_radius=0.1, normal_estimate_knn=20,
+                 fpfh_radius=0.1, fpfh_knn=20, seed=0, compat_q4=True):
+        self.opt = dict(division_factor=division_factor, tuple_scale=tuple_scale,
+                        maximum_correspondence_distance=maximum_correspondence_distance,
+                        iteration_number=iteration_number, decrease_mu=decrease_mu)
+        self.nr, self.nk, self.fr, self.fk = normal_estimate_radius, normal_estimate_knn, fpfh_radius, fpfh_knn
+        self.seed = seed
+        self.compat_q4 = compat_q4
+
+    def optimize(self, source, target, **kwargs):
+        _, fs = fpfh(source, self.nr, self.nk, self.fr, self.fk)
+        ft = fs if self.compat_q4 else fpfh(target, self.nr, self.nk, self.fr, self.fk)[1]
+        r = fgr(source, target, fs, ft, seed=self.seed, **self.opt)
+        T = np.copy(r["T"])
+        T[:3, :3] = T[:3, :3].T
+        if r["ncorr"] == 0:
+            raise Warning("No correspondences detected from the optimizer.")
+        return T, r["rmse"]
+
+
+# ------------------------------------------------- reference preprocessing
+def radius_scale(cloud: np.ndarray):
+    """radiusScaler.py:18-30: centre on the mean, divide by the max radius."""
+    center = np.mean(cloud, axis=0, keepdims=True)
+    radius = float(np.max(np.sqrt(((cloud - center) ** 2).sum(axis=1))))
+    return (cloud - center) / radius, center, radius
+
+
+def random_downsample(cloud: np.ndarray, sample_size: int, replace: bool = False):
+    """randomDownsampler.py:35-37 (global legacy numpy RNG)."""
+    return cloud[np.random.choice(cloud.shape[0], sample_size, replace=replace)]
+
+
+# ------------------------------------------------- reference Aligner restated
+class OracleAligner:
+    """Aligner.py:36-317 restated (refine_registration excluded, Q5).
+
+    Same RNG consumption (global legacy ``np.random``), same composition and
+    the same strict-< / <= decision rules (Q1, Q2, Q3, Q7)."""
+
+    def __init__(self, optimizer, attempts=30, deg=math.pi / 2, mu=0.0, std=0.1, delta=0.2, max_iter=100,
+                 eps=0.05, preprocess=None):
+        self._optimizer = optimizer
+        self._attempts, self._deg, self._mu, self._std = attempts, deg, mu, std
+        self._delta, self._max_iter, self._eps = delta, max_iter, eps
+        self._preprocess = preprocess or (lambda c: radius_scale(c)[0])
+        self.calls: List[Tuple] = []
+
+    def initialize_rotation(self):  # Aligner.py:125-162
+        t1 = np.random.uniform(low=-self._deg, high=self._deg)
+        t2 = np.random.uniform(low=-self._deg, high=self._deg)
+        t3 = np.random.uniform(low=-self._deg, high=self._deg)
+        r1 = np.array([[1, 0, 0], [0, np.cos(t1), -np.sin(t1)], [0, np.sin(t1), np.cos(t1)]])
+        r2 = np.array([[np.cos(t2), 0, np.sin(t2)], [0, 1, 0], [-np.sin(t2), 0, np.cos(t2)]])
+        r3 = np.array([[np.cos(t3), -np.sin(t3), 0], [np.sin(t3), np.cos(t3), 0], [0, 0, 1]])
+        rot = np.dot(r1, np.dot(r2, r3))
+        trans = self._mu + np.random.randn(3) * self._std
+        return rot, trans
+
+    def multistart_registration(self, source, target):  # Aligner.py:164-204
+        metric = np.inf
+        best = np.eye(4)
+        for _ in range(self._attempts):
+            R0, t0 = self.initialize_rotation()
+            s_init = np.dot(source.copy(), R0) + t0
+            Tc, m = self._optimizer.optimize(s_init, target)
+            self.calls.append((R0, t0, float(m)))
+            if m < metric:
+                metric = m
+                T = np.eye(4)
+                T[:3, :3] = np.dot(R0, Tc[:3, :3])
+                T[:3, 3] = np.dot(t0, Tc[:3, :3]).ravel() + Tc[:3, 3]
+                best = T
+        return best, metric
+
+    def compass_step(self, source, target, sf, delta):  # Aligner.py:206-226
+        new_sf = sf + delta
+        T, m = self.multistart_registration(source, target * new_sf)
+        return new_sf, T, m
+
+    def align(self, source, target, max_compass_iterations: Optional[int] = None):  # Aligner.py:228-317
+        source = self._preprocess(source)
+        target = self._preprocess(target)
+        iteration = 0
+        sf = np.ones((1, 3))
+        T, metric = self.multistart_registration(source, target)
+        errors = [metric]
+        directions = np.eye(3)
+        while self._delta >= self._eps and iteration <= self._max_iter:
+            if max_compass_iterations is not None and iteration >= max_compass_iterations:
+                break
+            iteration += 1
+            for axis in range(3):
+                plus = self._delta * directions[:, axis]
+                _, newT, new_metric = self.compass_step(source, target, sf, plus)
+                if new_metric <= metric:
+                    metric, T = new_metric, newT
+                    sf += plus
+                    errors.append(new_metric)
+                    break
+                neg = -self._delta * directions[:, axis]
+                _, newT, new_metric = self.compass_step(source, target, sf, neg)
+                if new_metric <= metric:
+                    metric, T = new_metric, newT
+                    sf += neg
+                    errors.append(new_metric)
+                    break
+            if new_metric > metric:
+                self._delta = self._delta / 2
+        return T, metric, sf, errors
