@@ -1,0 +1,183 @@
+"""Benchmark: GICP iterations/s of the MI355X inner registration loop (C2).
+
+    python bench.py --gpus N --steps K --warmup W
+
+Workload (BASELINE.json configs[1]): ArmadilloBack_330 ->
+ArmadilloBack_0 densified to 50,000 points each (synthetic: sampling with
+replacement + 5e-5 jitter, workloads.c2_pair), RadiusScaler-normalised
+(Preprocessor([])), GICP defaults (max_corr 0.5, 100 iterations).
+
+One step = one Aligner.multistart_registration over the pair at scale (1,1,1):
+`--attempts` (default 30, as the reference) random starts drawn from the
+global numpy RNG exactly as the reference, each a full GICP run, executed as
+ONE device batch and sharded over ranks (one process per GPU, torch.distributed
+with RCCL); every rank then replays the reference's argmin.  Total work per
+step is fixed as N grows (strong scaling).
+
+value = GICP iterations completed (all starts, all ranks) / max-over-ranks
+wall time of the K timed steps.  Also reported: the dominant kernel's
+roofline (live hipEvent timing inside the library on its own stream), a CPU
+baseline (the oracle: C++/OpenMP KD-tree GICP on the host cores, bounded
+sample of the same starts), and one full Aligner.align() wall-clock on rank 0.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(REPO, "multi-scale-pointcloud-registration_amd"))
+sys.path.insert(0, REPO)
+
+FP32_PEAK_TFLOPS = 157.3    # MI355X FP32 (vector == matrix rate), MI355X_MICROARCH.md
+FLOP_PER_PAIR = 8           # 3 sub + 3 mul/fma(=5) per query-target distance
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=2)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--points", type=int, default=50_000)
+    ap.add_argument("--attempts", type=int, default=30)
+    ap.add_argument("--cpu-seconds", type=float, default=20.0, help="CPU baseline sample budget (0 = skip)")
+    ap.add_argument("--align", type=int, default=1, help="also time one full align() on rank 0 (N=1)")
+    return ap.parse_args()
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch
+        import torch.distributed as dist
+
+        torch.cuda.set_device(local_rank)
+        dist.init_process_group("nccl", init_method="env://")
+
+    from orpcd_amd import Aligner, GeneralizedICP, Preprocessor
+    from workloads import c2_pair
+
+    src_raw, tgt_raw = c2_pair(args.points)
+    source = Preprocessor([]).preprocess(src_raw)
+    target = Preprocessor([]).preprocess(tgt_raw)
+
+    opt = GeneralizedICP(device=local_rank)
+    ctx = opt.context
+    aligner = Aligner(Preprocessor([]), Preprocessor([]), opt, attempts=args.attempts)
+
+    def barrier():
+        if dist is not None:
+            import torch
+            torch.cuda.synchronize()
+            dist.barrier()
+
+    def step(k):
+        np.random.seed(1000 + k)  # identical draws on every rank
+        aligner.multistart_registration(source, target)
+        return aligner.history[-1]["iters"]
+
+    for k in range(args.warmup):
+        step(k)
+    ctx.reset_stats()
+    ctx.profiling(True)
+    barrier()
+    t0 = time.perf_counter()
+    iters = 0
+    for k in range(args.steps):
+        iters += step(args.warmup + k)
+    barrier()
+    elapsed = time.perf_counter() - t0
+    ctx.profiling(False)
+    st = ctx.stats()
+    if dist is not None:
+        import torch
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+        s = torch.tensor([st["ms"], st["launches"], st["pairs"]], dtype=torch.float64, device="cuda")
+        dist.all_reduce(s, op=dist.ReduceOp.SUM)
+        st["ms"], st["launches"], st["pairs"] = (float(x) for x in s.tolist())
+
+    value = iters / elapsed
+    avg_ms = st["ms"] / max(st["launches"], 1)
+    flops_per_launch = st["pairs"] / max(st["launches"], 1) * FLOP_PER_PAIR
+    achieved = flops_per_launch / (avg_ms * 1e-3) / 1e12 if avg_ms > 0 else 0.0
+
+    cpu = None
+    align_s = None
+    if rank == 0 and world == 1:
+        if args.cpu_seconds > 0:
+            cpu = cpu_baseline(source, target, args)
+        if args.align:
+            np.random.seed(0)
+            al = Aligner(Preprocessor([]), Preprocessor([]), opt, attempts=args.attempts)
+            t1 = time.perf_counter()
+            T, metric, sf, errors = al.align(src_raw, tgt_raw, refine_registration=False)
+            align_s = dict(seconds=round(time.perf_counter() - t1, 3), rmse=float(metric),
+                           scale_factors=[round(float(x), 6) for x in sf.ravel()],
+                           multistarts=len(al.history), gicp_iters=int(sum(h["iters"] for h in al.history)))
+
+    if rank == 0:
+        line = {
+            "metric": "GICP iters/sec (Aligner multistart, 50k<->50k)",
+            "value": round(value, 3),
+            "unit": "GICP iterations/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None,
+            "dtype": "f32+f64",
+            "data": "synthetic (Armadillo 330->0 densified to 50k, jitter 5e-5; seeds fixed)",
+            "config": {"workload": "C2: Armadillo pair @50k pts, GeneralizedICP defaults, one multistart/step",
+                       "points": args.points, "attempts_per_step": args.attempts,
+                       "parallelism": f"attempts sharded over {world} GPU(s)"},
+            "roofline": {"bound": "mfma", "achieved": round(achieved, 3), "peak": FP32_PEAK_TFLOPS,
+                         "unit": "TFLOP/s", "frac": round(achieved / FP32_PEAK_TFLOPS, 4), "traffic": None,
+                         "kernel": "gicp_pass_kernel", "avg_launch_ms": round(avg_ms, 4),
+                         "launches": int(st["launches"]), "flop_per_pair": FLOP_PER_PAIR},
+            "cpu_baseline": cpu,
+            "gicp_iterations": int(iters),
+            "align": align_s,
+        }
+        print(json.dumps(line))
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+def cpu_baseline(source, target, args):
+    """The oracle (C++/OpenMP, KD-tree 1-NN, fp64) on the same starts as step 0,
+    attempt by attempt until the time budget is spent."""
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    import oracle as O
+
+    np.random.seed(1000)
+    al = O.OracleAligner(None, attempts=args.attempts)
+    starts = [al.initialize_rotation() for _ in range(args.attempts)]
+    t0 = time.perf_counter()
+    iters = 0
+    done = 0
+    for R0, t0_ in starts:
+        r = O.gicp(np.dot(source, R0) + t0_, target, 0.5, 100)
+        iters += r["iters"]
+        done += 1
+        if time.perf_counter() - t0 > args.cpu_seconds:
+            break
+    el = time.perf_counter() - t0
+    return {"value": round(iters / el, 3), "unit": "GICP iterations/s", "cores": O.num_threads(),
+            "kind": "port",
+            "sample": f"{done} of {args.attempts} starts of step 0 (same R0,t0), {iters} GICP iterations, "
+                      f"{el:.1f} s, {os.cpu_count()} host cpus visible"}
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,133 @@
+/*
+ * orpcd.h — C-ABI of liborpcd_hip.so, the MI355X-native implementation of
+ * OR-PCD's inner registration loop (dpolimeni/Multi-scale-pointcloud-
+ * registration, `or-pcd` 0.0.1-BETA.7).
+ *
+ * Plain pointers and sizes only: no torch, no HIP types in the signatures.
+ * The caller owns every host buffer; a context owns all device memory.
+ * One context per (thread, device); a context is not re-entrant.  No C++
+ * exception crosses this boundary: every entry point returns an orpcd_status
+ * and orpcd_last_error() holds the message of the last failure.
+ *
+ * Reference interfaces each entry point replaces (file:line under
+ * /root/reference/src/or_pcd/):
+ *   orpcd_set_target / orpcd_set_source / orpcd_gicp_batch
+ *       GeneralizedICP.optimize            Optimizer/generalizedICP.py:47-83
+ *       -> o3d registration_generalized_icp Optimizer/generalizedICP.py:59-70
+ *       batched over the multistart loop   Aligner/Aligner.py:178-202
+ *   orpcd_estimate_normals
+ *       o3d EstimateNormals(KNN 20) inside registration_generalized_icp, and
+ *       source_copy.estimate_normals(Hybrid) Optimizer/fastGlobalOptimizer.py:118-127
+ *   orpcd_nn1_radius
+ *       o3d GetRegistrationResultAndCorrespondences (SearchHybrid(r, 1)),
+ *       the correspondence step of every ICP iteration (generalizedICP.py:60)
+ *   orpcd_fpfh
+ *       o3d compute_fpfh_feature           Optimizer/fastGlobalOptimizer.py:130-142
+ *   orpcd_fgr
+ *       o3d registration_fgr_based_on_feature_matching
+ *                                          Optimizer/fastGlobalOptimizer.py:158-174
+ */
+#ifndef ORPCD_H
+#define ORPCD_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define ORPCD_ABI_VERSION 1
+
+typedef enum {
+    ORPCD_OK = 0,
+    ORPCD_EINVAL = 1,  /* invalid argument (maps to the reference's validation) */
+    ORPCD_ENOCORR = 2, /* no correspondences (Python: ValueError / Warning)     */
+    ORPCD_EDEVICE = 3  /* HIP runtime / kernel failure                          */
+} orpcd_status;
+
+typedef struct orpcd_ctx orpcd_ctx;
+
+int orpcd_abi_version(void);
+int orpcd_device_count(int* count);
+int orpcd_ctx_create(int device, orpcd_ctx** out);
+int orpcd_ctx_destroy(orpcd_ctx* ctx);
+const char* orpcd_last_error(const orpcd_ctx* ctx);
+
+/* ------------------------------------------------------------------ clouds
+ * Target: uploaded once per scale candidate (Aligner.compass_step scales the
+ * target, Aligner.py:221-222).  Builds the fp32 search copy and the per-point
+ * GICP covariances C_t = R_{e1->n} diag(eps,1,1) R^T from KNN-20 normals.   */
+int orpcd_set_target(orpcd_ctx* ctx, const double* xyz, int64_t m, double epsilon);
+/* Source: uploaded once per align() (the preprocessed source, unposed).
+ * KNN-20 neighbourhood covariances are computed once; each start's posed
+ * covariances are derived from them (rigid equivariance).     */
+int orpcd_set_source(orpcd_ctx* ctx, const double* xyz, int64_t n);
+
+typedef struct {
+    double max_correspondence_distance; /* generalizedICP.py:15-19, default 0.5  */
+    int32_t max_iteration;              /* ICPConvergenceCriteria(max_iteration)  */
+    double relative_fitness;            /* Open3D default 1e-6                    */
+    double relative_rmse;               /* Open3D default 1e-6                    */
+    double epsilon;                     /* GICP covariance epsilon, default 1e-3  */
+} orpcd_gicp_params;
+
+/* GICP from identity for B starts of the current source posed as
+ *     source_initialized = source @ R0[b] + t0[b]      (Aligner.py:183-185)
+ * against the current target.  Outputs per start b:
+ *   T_out[16*b]   Open3D's column-convention transformation (row-major 4x4),
+ *                 i.e. what registration_generalized_icp returns BEFORE the
+ *                 plugin transposes R (generalizedICP.py:72-74);
+ *   rmse_out[b]   inlier RMSE, fitness_out[b] = |corr| / N,
+ *   iters_out[b]  ICP iterations executed, ncorr_out[b] = |corr|.
+ * Any of the output pointers except T_out/rmse_out may be NULL.             */
+int orpcd_gicp_batch(orpcd_ctx* ctx, const double* R0, const double* t0, int32_t B,
+                     const orpcd_gicp_params* params, double* T_out, double* rmse_out,
+                     double* fitness_out, int32_t* iters_out, int64_t* ncorr_out);
+
+/* ------------------------------------------------------- kernel-level entry
+ * Radius-bounded exact 1-NN (d^2 < r^2 strictly, fp64 re-checked);
+ * idx = -1 when no target lies within radius.                               */
+int orpcd_nn1_radius(orpcd_ctx* ctx, const double* q, int64_t nq, const double* t, int64_t m,
+                     double radius, int32_t* idx_out, double* d2_out);
+/* EstimateNormals: knn neighbours (radius <= 0: pure KNN; > 0: hybrid).
+ * normals (n*3), raw neighbourhood covariance (n*9), GICP covariance (n*9,
+ * only when epsilon >= 0).  Any output may be NULL.                         */
+int orpcd_estimate_normals(orpcd_ctx* ctx, const double* xyz, int64_t n, int32_t knn, double radius,
+                           double epsilon, double* normals_out, double* rawcov_out, double* gicpcov_out);
+
+/* FPFH (33 bins, Open3D layout transposed to n x 33) after Hybrid normals.  */
+int orpcd_fpfh(orpcd_ctx* ctx, const double* xyz, int64_t n, double normal_radius, int32_t normal_knn,
+               double fpfh_radius, int32_t fpfh_knn, double* normals_out, double* feat_out);
+
+typedef struct {
+    double division_factor;                 /* 1.4  fastGlobalOptimizer.py:25 */
+    double tuple_scale;                     /* 0.9                            */
+    double maximum_correspondence_distance; /* 0.5                            */
+    int32_t iteration_number;               /* 100                            */
+    int32_t decrease_mu;                    /* 1                              */
+    int32_t maximum_tuple_count;            /* Open3D default 1000            */
+    uint64_t seed;                          /* tuple-test RNG (mt19937)       */
+} orpcd_fgr_params;
+
+/* FGR on given features (n x 33 and m x 33, row-major).  T_out: Open3D's
+ * column-convention transformation; n_mutual_out[2] = {mutual matches,
+ * tuple correspondences}.                                                   */
+int orpcd_fgr(orpcd_ctx* ctx, const double* src, int64_t n, const double* tgt, int64_t m,
+              const double* src_feat, const double* tgt_feat, const orpcd_fgr_params* params,
+              double* T_out, double* fitness_out, double* rmse_out, int64_t* ncorr_out,
+              int64_t* n_mutual_out);
+
+/* ------------------------------------------------------------ measurement
+ * Live kernel timing (hipEvents on the context's stream).  When enabled,
+ * every launch of the dominant correspondence kernel is bracketed.
+ * stats[0] = launches, [1] = total ms, [2] = query-target pairs evaluated,
+ * [3] = GICP iterations completed, [4] = correspondence passes.             */
+int orpcd_profiling(orpcd_ctx* ctx, int32_t enable);
+int orpcd_stats(orpcd_ctx* ctx, double* stats_out, int32_t n);
+int orpcd_reset_stats(orpcd_ctx* ctx);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* ORPCD_H */

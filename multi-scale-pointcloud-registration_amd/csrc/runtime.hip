@@ -1,0 +1,376 @@
+// runtime.hip — the C-ABI (include/orpcd.h): context, device-resident clouds
+// and the batched GICP driver.  Host orchestration only; all arithmetic on
+// the hot path runs in the kernels of knn_kernels.hip / gicp_kernels.hip.
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <new>
+
+#include "orpcd_internal.h"
+
+using namespace orpcd;
+
+#define CTX_CHECK(ctx, call)                                                                          \
+    do {                                                                                              \
+        hipError_t e_ = (call);                                                                       \
+        if (e_ != hipSuccess) {                                                                       \
+            (ctx)->err = std::string(#call) + ": " + hipGetErrorString(e_);                           \
+            return ORPCD_EDEVICE;                                                                     \
+        }                                                                                             \
+    } while (0)
+
+#define CTX_REQUIRE(ctx, cond, msg)   \
+    do {                              \
+        if (!(cond)) {                \
+            (ctx)->err = (msg);       \
+            return ORPCD_EINVAL;      \
+        }                             \
+    } while (0)
+
+namespace {
+
+int64_t pad_to(int64_t v, int64_t m) { return ((v + m - 1) / m) * m; }
+
+// Upload a target cloud and compute its GICP covariances.
+int upload_target(orpcd_ctx* c, const double* xyz, int64_t m, double eps) {
+    c->M = m;
+    c->Mpad = std::max<int64_t>(kTargetTile, pad_to(m, kTargetTile));
+    CTX_CHECK(c, c->tgt64.ensure((size_t)m * 3));
+    CTX_CHECK(c, c->tgt4.ensure((size_t)c->Mpad));
+    CTX_CHECK(c, c->tcov.ensure((size_t)m * 6));
+    CTX_CHECK(c, c->scratch64a.ensure((size_t)m * 6));
+    CTX_CHECK(c, hipMemcpyAsync(c->tgt64.p, xyz, (size_t)m * 3 * sizeof(double), hipMemcpyHostToDevice, c->stream));
+    CTX_CHECK(c, launch_prep_targets(c->tgt64.p, m, c->Mpad, c->tgt4.p, c->stream));
+    if (eps >= 0.0) {
+        CTX_CHECK(c, launch_knn_cov(c->tgt64.p, m, 20, -1.0, c->scratch64a.p, nullptr, nullptr, c->stream));
+        CTX_CHECK(c, launch_normals_cov(c->scratch64a.p, m, nullptr, 1, eps, nullptr, c->tcov.p, c->stream));
+    }
+    c->tgt_eps = eps;
+    return ORPCD_OK;
+}
+
+bool finite_cloud(const double* xyz, int64_t n) {
+    for (int64_t i = 0; i < 3 * n; ++i)
+        if (!std::isfinite(xyz[i])) return false;
+    return true;
+}
+
+}  // namespace
+
+extern "C" {
+
+int orpcd_abi_version(void) { return ORPCD_ABI_VERSION; }
+
+int orpcd_device_count(int* count) {
+    if (!count) return ORPCD_EINVAL;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) n = 0;
+    *count = n;
+    return ORPCD_OK;
+}
+
+int orpcd_ctx_create(int device, orpcd_ctx** out) {
+    if (!out) return ORPCD_EINVAL;
+    *out = nullptr;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return ORPCD_EDEVICE;
+    if (device < 0 || device >= n) return ORPCD_EINVAL;
+    orpcd_ctx* c = new (std::nothrow) orpcd_ctx();
+    if (!c) return ORPCD_EDEVICE;
+    c->device = device;
+    if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+        delete c;
+        return ORPCD_EDEVICE;
+    }
+    *out = c;
+    return ORPCD_OK;
+}
+
+int orpcd_ctx_destroy(orpcd_ctx* c) {
+    if (!c) return ORPCD_EINVAL;
+    (void)hipSetDevice(c->device);
+    (void)hipStreamSynchronize(c->stream);
+    for (auto* b : {&c->tgt64, &c->tcov, &c->src64, &c->sraw, &c->scov, &c->G, &c->T, &c->Q, &c->R, &c->prev,
+                    &c->partial, &c->out_fit, &c->out_rmse, &c->scratch64a, &c->scratch64b, &c->scratch64c})
+        b->release();
+    c->tgt4.release();
+    c->scratch4.release();
+    c->done.release();
+    c->active.release();
+    c->out_iters.release();
+    c->out_ncorr.release();
+    c->scratch32.release();
+    c->h64.release();
+    c->h32.release();
+    for (hipEvent_t e : c->ev_pool) (void)hipEventDestroy(e);
+    (void)hipStreamDestroy(c->stream);
+    delete c;
+    return ORPCD_OK;
+}
+
+const char* orpcd_last_error(const orpcd_ctx* c) { return c ? c->err.c_str() : "null context"; }
+
+int orpcd_set_target(orpcd_ctx* c, const double* xyz, int64_t m, double epsilon) {
+    if (!c) return ORPCD_EINVAL;
+    CTX_REQUIRE(c, xyz && m > 0, "set_target: empty target cloud");
+    CTX_REQUIRE(c, m < (int64_t)1 << 30, "set_target: too many points");
+    CTX_REQUIRE(c, finite_cloud(xyz, m), "set_target: non-finite coordinates");
+    CTX_CHECK(c, hipSetDevice(c->device));
+    int rc = upload_target(c, xyz, m, epsilon);
+    if (rc) return rc;
+    CTX_CHECK(c, hipStreamSynchronize(c->stream));
+    return ORPCD_OK;
+}
+
+int orpcd_set_source(orpcd_ctx* c, const double* xyz, int64_t n) {
+    if (!c) return ORPCD_EINVAL;
+    CTX_REQUIRE(c, xyz && n > 0, "set_source: empty source cloud");
+    CTX_REQUIRE(c, n < (int64_t)1 << 30, "set_source: too many points");
+    CTX_REQUIRE(c, finite_cloud(xyz, n), "set_source: non-finite coordinates");
+    CTX_CHECK(c, hipSetDevice(c->device));
+    c->N = n;
+    CTX_CHECK(c, c->src64.ensure((size_t)n * 3));
+    CTX_CHECK(c, c->sraw.ensure((size_t)n * 6));
+    CTX_CHECK(c, hipMemcpyAsync(c->src64.p, xyz, (size_t)n * 3 * sizeof(double), hipMemcpyHostToDevice, c->stream));
+    CTX_CHECK(c, launch_knn_cov(c->src64.p, n, 20, -1.0, c->sraw.p, nullptr, nullptr, c->stream));
+    CTX_CHECK(c, hipStreamSynchronize(c->stream));
+    return ORPCD_OK;
+}
+
+int orpcd_gicp_batch(orpcd_ctx* c, const double* R0, const double* t0, int32_t B, const orpcd_gicp_params* p,
+                     double* T_out, double* rmse_out, double* fitness_out, int32_t* iters_out, int64_t* ncorr_out) {
+    if (!c) return ORPCD_EINVAL;
+    CTX_REQUIRE(c, R0 && t0 && p && T_out && rmse_out, "gicp_batch: null argument");
+    CTX_REQUIRE(c, B > 0, "gicp_batch: B must be > 0");
+    CTX_REQUIRE(c, c->N > 0, "gicp_batch: no source (call orpcd_set_source)");
+    CTX_REQUIRE(c, c->M > 0, "gicp_batch: no target (call orpcd_set_target)");
+    CTX_REQUIRE(c, p->max_correspondence_distance > 0, "gicp_batch: max_correspondence_distance must be > 0");
+    CTX_REQUIRE(c, p->max_iteration >= 0, "gicp_batch: max_iteration must be >= 0");
+    CTX_REQUIRE(c, p->epsilon >= 0, "gicp_batch: epsilon must be >= 0");
+    CTX_CHECK(c, hipSetDevice(c->device));
+    if (c->tgt_eps != p->epsilon) {  // target covariances depend on epsilon
+        std::vector<double> host((size_t)c->M * 3);
+        CTX_CHECK(c, hipMemcpy(host.data(), c->tgt64.p, host.size() * sizeof(double), hipMemcpyDeviceToHost));
+        int rc = upload_target(c, host.data(), c->M, p->epsilon);
+        if (rc) return rc;
+    }
+    const int64_t N = c->N;
+    const int nblk = (int)((N + kPassQueries - 1) / kPassQueries);
+    CTX_CHECK(c, c->scov.ensure((size_t)B * N * 6));
+    CTX_CHECK(c, c->G.ensure((size_t)B * 12));
+    CTX_CHECK(c, c->T.ensure((size_t)B * 16));
+    CTX_CHECK(c, c->Q.ensure((size_t)B * 12));
+    CTX_CHECK(c, c->R.ensure((size_t)B * 9));
+    CTX_CHECK(c, c->prev.ensure((size_t)B * 2));
+    CTX_CHECK(c, c->partial.ensure((size_t)B * nblk * kPartialStride));
+    CTX_CHECK(c, c->done.ensure((size_t)B));
+    CTX_CHECK(c, c->active.ensure((size_t)B));
+    CTX_CHECK(c, c->out_fit.ensure((size_t)B));
+    CTX_CHECK(c, c->out_rmse.ensure((size_t)B));
+    CTX_CHECK(c, c->out_iters.ensure((size_t)B));
+    CTX_CHECK(c, c->out_ncorr.ensure((size_t)B));
+    CTX_CHECK(c, c->scratch64b.ensure((size_t)B * 9));
+    const size_t hsz = (size_t)B * (12 + 16 + 12 + 9 + 9 + 2);
+    CTX_CHECK(c, c->h64.ensure(hsz + (size_t)B * 20));
+    CTX_CHECK(c, c->h32.ensure((size_t)B * 4));
+
+    // host: base pose G_b = [R0_b^T | t0_b] (source @ R0 + t0 in column form)
+    double* hG = c->h64.p;
+    double* hT = hG + (size_t)B * 12;
+    double* hQ = hT + (size_t)B * 16;
+    double* hR = hQ + (size_t)B * 12;
+    double* hRc = hR + (size_t)B * 9;
+    double* hPrev = hRc + (size_t)B * 9;
+    for (int b = 0; b < B; ++b) {
+        const double* r = R0 + 9 * b;
+        for (int i = 0; i < 3; ++i) {
+            for (int j = 0; j < 3; ++j) {
+                hG[12 * b + 4 * i + j] = r[3 * j + i];
+                hRc[9 * b + 3 * i + j] = r[3 * j + i];
+            }
+            hG[12 * b + 4 * i + 3] = t0[3 * b + i];
+        }
+        for (int t = 0; t < 16; ++t) hT[16 * b + t] = (t % 5 == 0) ? 1.0 : 0.0;
+        for (int t = 0; t < 12; ++t) hQ[12 * b + t] = hG[12 * b + t];
+        for (int t = 0; t < 9; ++t) hR[9 * b + t] = (t % 4 == 0) ? 1.0 : 0.0;
+        hPrev[2 * b] = hPrev[2 * b + 1] = 0.0;
+    }
+    int32_t* hAct = c->h32.p;
+    int32_t* hDone = hAct + B;
+    for (int b = 0; b < B; ++b) {
+        hAct[b] = b;
+        hDone[b] = 0;
+    }
+    CTX_CHECK(c, hipMemcpyAsync(c->G.p, hG, (size_t)B * 12 * 8, hipMemcpyHostToDevice, c->stream));
+    CTX_CHECK(c, hipMemcpyAsync(c->T.p, hT, (size_t)B * 16 * 8, hipMemcpyHostToDevice, c->stream));
+    CTX_CHECK(c, hipMemcpyAsync(c->Q.p, hQ, (size_t)B * 12 * 8, hipMemcpyHostToDevice, c->stream));
+    CTX_CHECK(c, hipMemcpyAsync(c->R.p, hR, (size_t)B * 9 * 8, hipMemcpyHostToDevice, c->stream));
+    CTX_CHECK(c, hipMemcpyAsync(c->scratch64b.p, hRc, (size_t)B * 9 * 8, hipMemcpyHostToDevice, c->stream));
+    CTX_CHECK(c, hipMemcpyAsync(c->prev.p, hPrev, (size_t)B * 2 * 8, hipMemcpyHostToDevice, c->stream));
+    CTX_CHECK(c, hipMemcpyAsync(c->active.p, hAct, (size_t)B * 4, hipMemcpyHostToDevice, c->stream));
+    CTX_CHECK(c, hipMemcpyAsync(c->done.p, hDone, (size_t)B * 4, hipMemcpyHostToDevice, c->stream));
+
+    // posed-frame source covariances for every start (rigid equivariance)
+    CTX_CHECK(c, launch_normals_cov(c->sraw.p, N, c->scratch64b.p, B, p->epsilon, nullptr, c->scov.p, c->stream));
+
+    const double r2 = p->max_correspondence_distance * p->max_correspondence_distance;
+    int nact = B;
+    for (int pass = 0; pass <= p->max_iteration && nact > 0; ++pass) {
+        hipEvent_t e0 = nullptr, e1 = nullptr;
+        if (c->profiling) {
+            if (c->ev_pool.size() < 2) {
+                for (int t = 0; t < 2; ++t) {
+                    hipEvent_t e;
+                    CTX_CHECK(c, hipEventCreate(&e));
+                    c->ev_pool.push_back(e);
+                }
+            }
+            e0 = c->ev_pool[0];
+            e1 = c->ev_pool[1];
+            CTX_CHECK(c, hipEventRecord(e0, c->stream));
+        }
+        CTX_CHECK(c, launch_gicp_pass(c, nact, nblk, r2, c->stream));
+        if (c->profiling) CTX_CHECK(c, hipEventRecord(e1, c->stream));
+        CTX_CHECK(c, launch_gicp_solve(c, nact, nblk, pass, *p, c->stream));
+        CTX_CHECK(c, hipMemcpyAsync(hDone, c->done.p, (size_t)B * 4, hipMemcpyDeviceToHost, c->stream));
+        CTX_CHECK(c, hipStreamSynchronize(c->stream));
+        if (c->profiling) {
+            float ms = 0.f;
+            CTX_CHECK(c, hipEventElapsedTime(&ms, e0, e1));
+            c->stats.launches += 1;
+            c->stats.ms += ms;
+            c->stats.pairs += (double)nact * (double)N * (double)c->M;
+        }
+        c->stats.passes += nact;
+        int k = 0;
+        for (int b = 0; b < nact; ++b)
+            if (!hDone[hAct[b]]) hAct[k++] = hAct[b];
+        if (k != nact && k > 0)
+            CTX_CHECK(c, hipMemcpyAsync(c->active.p, hAct, (size_t)k * 4, hipMemcpyHostToDevice, c->stream));
+        nact = k;
+    }
+    // outputs
+    double* hFit = hPrev + (size_t)B * 2;
+    double* hRmse = hFit + B;
+    int32_t* hIters = c->h32.p + 2 * B;
+    CTX_CHECK(c, hipMemcpyAsync(hT, c->T.p, (size_t)B * 16 * 8, hipMemcpyDeviceToHost, c->stream));
+    CTX_CHECK(c, hipMemcpyAsync(hFit, c->out_fit.p, (size_t)B * 8, hipMemcpyDeviceToHost, c->stream));
+    CTX_CHECK(c, hipMemcpyAsync(hRmse, c->out_rmse.p, (size_t)B * 8, hipMemcpyDeviceToHost, c->stream));
+    CTX_CHECK(c, hipMemcpyAsync(hIters, c->out_iters.p, (size_t)B * 4, hipMemcpyDeviceToHost, c->stream));
+    std::vector<int64_t> nc((size_t)B);
+    CTX_CHECK(c, hipMemcpyAsync(nc.data(), c->out_ncorr.p, (size_t)B * 8, hipMemcpyDeviceToHost, c->stream));
+    CTX_CHECK(c, hipStreamSynchronize(c->stream));
+    for (int b = 0; b < B; ++b) {
+        std::memcpy(T_out + 16 * b, hT + 16 * b, 16 * sizeof(double));
+        rmse_out[b] = hRmse[b];
+        if (fitness_out) fitness_out[b] = hFit[b];
+        if (iters_out) iters_out[b] = hIters[b];
+        if (ncorr_out) ncorr_out[b] = nc[b];
+        c->stats.iterations += hIters[b];
+    }
+    return ORPCD_OK;
+}
+
+int orpcd_nn1_radius(orpcd_ctx* c, const double* q, int64_t nq, const double* t, int64_t m, double radius,
+                     int32_t* idx_out, double* d2_out) {
+    if (!c) return ORPCD_EINVAL;
+    CTX_REQUIRE(c, q && t && idx_out && d2_out && nq >= 0 && m > 0, "nn1_radius: bad arguments");
+    CTX_REQUIRE(c, radius > 0, "nn1_radius: radius must be > 0");
+    if (nq == 0) return ORPCD_OK;
+    CTX_CHECK(c, hipSetDevice(c->device));
+    const int64_t mpad = std::max<int64_t>(kTargetTile, pad_to(m, kTargetTile));
+    CTX_CHECK(c, c->scratch64a.ensure((size_t)m * 3));
+    CTX_CHECK(c, c->scratch64b.ensure((size_t)nq * 3));
+    CTX_CHECK(c, c->scratch64c.ensure((size_t)nq));
+    CTX_CHECK(c, c->scratch4.ensure((size_t)mpad));
+    CTX_CHECK(c, c->scratch32.ensure((size_t)nq));
+    CTX_CHECK(c, hipMemcpyAsync(c->scratch64a.p, t, (size_t)m * 24, hipMemcpyHostToDevice, c->stream));
+    CTX_CHECK(c, hipMemcpyAsync(c->scratch64b.p, q, (size_t)nq * 24, hipMemcpyHostToDevice, c->stream));
+    CTX_CHECK(c, launch_prep_targets(c->scratch64a.p, m, mpad, c->scratch4.p, c->stream));
+    CTX_CHECK(c, launch_nn1(c->scratch64b.p, nq, c->scratch4.p, c->scratch64a.p, mpad, radius * radius,
+                            c->scratch32.p, c->scratch64c.p, c->stream));
+    CTX_CHECK(c, hipMemcpyAsync(idx_out, c->scratch32.p, (size_t)nq * 4, hipMemcpyDeviceToHost, c->stream));
+    CTX_CHECK(c, hipMemcpyAsync(d2_out, c->scratch64c.p, (size_t)nq * 8, hipMemcpyDeviceToHost, c->stream));
+    CTX_CHECK(c, hipStreamSynchronize(c->stream));
+    return ORPCD_OK;
+}
+
+int orpcd_estimate_normals(orpcd_ctx* c, const double* xyz, int64_t n, int32_t knn, double radius, double epsilon,
+                           double* normals_out, double* rawcov_out, double* gicpcov_out) {
+    if (!c) return ORPCD_EINVAL;
+    CTX_REQUIRE(c, xyz && n > 0, "estimate_normals: empty cloud");
+    CTX_REQUIRE(c, knn > 0 && knn <= 64, "estimate_normals: knn must be in [1, 64]");
+    CTX_CHECK(c, hipSetDevice(c->device));
+    CTX_CHECK(c, c->scratch64a.ensure((size_t)n * 3));
+    CTX_CHECK(c, c->scratch64b.ensure((size_t)n * 6));
+    CTX_CHECK(c, c->scratch64c.ensure((size_t)n * 9));
+    CTX_CHECK(c, hipMemcpyAsync(c->scratch64a.p, xyz, (size_t)n * 24, hipMemcpyHostToDevice, c->stream));
+    CTX_CHECK(c, launch_knn_cov(c->scratch64a.p, n, knn, radius, c->scratch64b.p, nullptr, nullptr, c->stream));
+    // normals -> scratch64c[0:3n], gicp cov -> scratch64c[3n:9n]
+    double* dN = c->scratch64c.p;
+    double* dC = c->scratch64c.p + 3 * n;
+    CTX_CHECK(c, launch_normals_cov(c->scratch64b.p, n, nullptr, 1, epsilon, dN, epsilon >= 0 ? dC : nullptr,
+                                    c->stream));
+    std::vector<double> raw6((size_t)n * 6), cov6;
+    CTX_CHECK(c, hipMemcpyAsync(raw6.data(), c->scratch64b.p, (size_t)n * 48, hipMemcpyDeviceToHost, c->stream));
+    if (normals_out)
+        CTX_CHECK(c, hipMemcpyAsync(normals_out, dN, (size_t)n * 24, hipMemcpyDeviceToHost, c->stream));
+    if (gicpcov_out && epsilon >= 0) {
+        cov6.resize((size_t)n * 6);
+        CTX_CHECK(c, hipMemcpyAsync(cov6.data(), dC, (size_t)n * 48, hipMemcpyDeviceToHost, c->stream));
+    }
+    CTX_CHECK(c, hipStreamSynchronize(c->stream));
+    auto expand = [n](const std::vector<double>& s6, double* o9) {
+        for (int64_t i = 0; i < n; ++i) {
+            const double* s = &s6[(size_t)6 * i];
+            double* o = o9 + 9 * i;
+            o[0] = s[0];
+            o[1] = s[1];
+            o[2] = s[2];
+            o[3] = s[1];
+            o[4] = s[3];
+            o[5] = s[4];
+            o[6] = s[2];
+            o[7] = s[4];
+            o[8] = s[5];
+        }
+    };
+    if (rawcov_out) expand(raw6, rawcov_out);
+    if (gicpcov_out && epsilon >= 0) expand(cov6, gicpcov_out);
+    return ORPCD_OK;
+}
+
+int orpcd_fpfh(orpcd_ctx* c, const double*, int64_t, double, int32_t, double, int32_t, double*, double*) {
+    if (!c) return ORPCD_EINVAL;
+    c->err = "fpfh: not built in this revision";
+    return ORPCD_EINVAL;
+}
+
+int orpcd_fgr(orpcd_ctx* c, const double*, int64_t, const double*, int64_t, const double*, const double*,
+              const orpcd_fgr_params*, double*, double*, double*, int64_t*, int64_t*) {
+    if (!c) return ORPCD_EINVAL;
+    c->err = "fgr: not built in this revision";
+    return ORPCD_EINVAL;
+}
+
+int orpcd_profiling(orpcd_ctx* c, int32_t enable) {
+    if (!c) return ORPCD_EINVAL;
+    c->profiling = enable != 0;
+    return ORPCD_OK;
+}
+
+int orpcd_stats(orpcd_ctx* c, double* out, int32_t n) {
+    if (!c || !out) return ORPCD_EINVAL;
+    const double v[5] = {c->stats.launches, c->stats.ms, c->stats.pairs, c->stats.iterations, c->stats.passes};
+    for (int i = 0; i < n && i < 5; ++i) out[i] = v[i];
+    return ORPCD_OK;
+}
+
+int orpcd_reset_stats(orpcd_ctx* c) {
+    if (!c) return ORPCD_EINVAL;
+    c->stats = KernelStats();
+    return ORPCD_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,232 @@
+"""Aligner — the outer compass (pattern) search over (sx, sy, sz).
+
+Reference: or_pcd/Aligner/Aligner.py:32-408.  Same constructor, defaults,
+validation, RNG consumption (global legacy ``np.random``: three
+``uniform`` + one ``randn(3)`` per attempt, Aligner.py:129-160), the same
+composition T = [R0·Rc, t0·Rc + tc] (:192-202), the strict ``<`` over
+attempts (:192) and the ``<=`` acceptance / δ-halving of the compass (:263-298),
+including the reference's stateful δ (Q3).
+
+What is different is HOW a multistart runs: when the optimizer offers
+``optimize_batch`` (the build's GeneralizedICP), all attempts of one scale run
+as one device batch, sharded over the ranks of an initialised
+``torch.distributed`` group (``orpcd_amd.parallel``), and the per-attempt
+records are replayed through the reference's selection loop in attempt order.
+Any other IOptimizer (including the reference's own) is called per attempt,
+exactly as the reference does.
+"""
+import copy
+import time
+from typing import List, Tuple
+
+import numpy as np
+
+from .. import parallel
+from ..Optimizer.iOptimizer import IOptimizer
+from ..Preprocessor.Scalers.BaseScaler import BaseScaler
+from ..utils.constants import (
+    __ALIGNER_DEG__,
+    __ALIGNER_DELTA__,
+    __ALIGNER_EPS__,
+    __ALIGNER_MAX_ITER__,
+    __ALIGNER_MU__,
+    __ALIGNER_STD__,
+    __MULTISTART_ATTEMPTS__,
+    __REFINER_DISTANCE_THRESHOLD__,
+    __REFINER_MAX_ITER__,
+)
+from ..utils.logger_factory import LoggerFactory
+
+
+class Aligner:
+    transfromation: np.ndarray = np.eye(4)
+    scale_factors: np.ndarray = np.ones((1, 3))
+
+    def __init__(self, source_preprocessor, target_preprocessor, optimizer: IOptimizer,
+                 attempts: int = __MULTISTART_ATTEMPTS__, deg: float = __ALIGNER_DEG__, mu: float = __ALIGNER_MU__,
+                 std: float = __ALIGNER_STD__, delta: float = __ALIGNER_DELTA__, max_iter: int = __ALIGNER_MAX_ITER__,
+                 eps: float = __ALIGNER_EPS__, visualize_intermediate_steps: bool = False):
+        self._LOG = LoggerFactory.get_logger(log_name=self.__class__.__name__)
+        checks = [("attempts", attempts, lambda v: v <= 0, __MULTISTART_ATTEMPTS__),
+                  ("deg", deg, lambda v: v <= 0, __ALIGNER_DEG__),
+                  ("mu", mu, lambda v: v < 0, __ALIGNER_MU__),
+                  ("std", std, lambda v: v <= 0, __ALIGNER_STD__),
+                  ("delta", delta, lambda v: v <= 0, __ALIGNER_DELTA__),
+                  ("max_iter", max_iter, lambda v: v <= 0, __ALIGNER_MAX_ITER__),
+                  ("eps", eps, lambda v: v <= 0, __ALIGNER_EPS__)]
+        vals = {}
+        for name, v, bad, default in checks:  # Aligner.py:69-116
+            if bad(v):
+                self._LOG.warning(f"{name} cannot be 0 or less. Provided: {v}")
+                v = default
+            vals[name] = v
+        self._attempts = vals["attempts"]
+        self._deg = vals["deg"]
+        self._mu = vals["mu"]
+        self._std = vals["std"]
+        self._delta = vals["delta"]
+        self._max_iter = vals["max_iter"]
+        self._eps = vals["eps"]
+        self._visualize_intermediate_steps = visualize_intermediate_steps
+        self._source_preprocessor = source_preprocessor
+        self._target_preprocessor = target_preprocessor
+        self._optimizer = optimizer
+        # instrumentation (not in the reference): per-multistart records
+        self.history: List[dict] = []
+
+    # ----------------------------------------------------------------- RNG
+    def initialize_rotation(self) -> Tuple[np.ndarray, np.ndarray]:
+        """Aligner.py:125-162 (bit-identical draws and matrix products)."""
+        theta_1 = np.random.uniform(low=-self._deg, high=self._deg)
+        theta_2 = np.random.uniform(low=-self._deg, high=self._deg)
+        theta_3 = np.random.uniform(low=-self._deg, high=self._deg)
+        r_1 = np.array([[1, 0, 0], [0, np.cos(theta_1), -np.sin(theta_1)], [0, np.sin(theta_1), np.cos(theta_1)]])
+        r_2 = np.array([[np.cos(theta_2), 0, np.sin(theta_2)], [0, 1, 0], [-np.sin(theta_2), 0, np.cos(theta_2)]])
+        r_3 = np.array([[np.cos(theta_3), -np.sin(theta_3), 0], [np.sin(theta_3), np.cos(theta_3), 0], [0, 0, 1]])
+        rotation_matrix = np.dot(r_1, np.dot(r_2, r_3))
+        translation = self._mu + np.random.randn(3) * self._std
+        return rotation_matrix, translation
+
+    # ----------------------------------------------------------- multistart
+    def multistart_registration(self, source: np.ndarray, target: np.ndarray) -> Tuple[np.ndarray, float]:
+        if hasattr(self._optimizer, "optimize_batch"):
+            return self._multistart_batched(source, target)
+        return self._multistart_sequential(source, target)
+
+    def _multistart_sequential(self, source, target):
+        """Aligner.py:164-204 verbatim in behaviour (one optimize per attempt)."""
+        metric = np.inf
+        best_transformation = np.eye(4)
+        for _ in range(self._attempts):
+            source_copy = copy.deepcopy(source)
+            initial_rotation, initial_translation = self.initialize_rotation()
+            source_initialized = np.dot(source_copy, initial_rotation) + initial_translation
+            current_transform, current_metric = self._optimizer.optimize(source_initialized, target)
+            if current_metric < metric:
+                metric = current_metric
+                best_transformation = self._compose(initial_rotation, initial_translation, current_transform)
+        return best_transformation, metric
+
+    @staticmethod
+    def _compose(R0, t0, Tc):
+        """Aligner.py:196-201."""
+        T = np.eye(4)
+        T[:3, :3] = np.dot(R0, Tc[:3, :3])
+        T[:3, 3] = np.dot(t0, Tc[:3, :3]).ravel() + Tc[:3, 3]
+        return T
+
+    def _multistart_batched(self, source, target):
+        B = self._attempts
+        R0s, t0s, states = [], [], []
+        for _ in range(B):  # same draws, same order as the sequential loop
+            R, t = self.initialize_rotation()
+            R0s.append(R)
+            t0s.append(t)
+            states.append(np.random.get_state())
+        rank, ws = parallel.world()
+        lo, hi = parallel.shard(B, rank, ws)
+        t_start = time.perf_counter()
+        if hi > lo:
+            local = parallel.pack(self._optimizer.optimize_batch(source, target, np.array(R0s[lo:hi]),
+                                                                 np.array(t0s[lo:hi])))
+        else:
+            local = np.zeros((0, parallel.REC))
+        table = parallel.unpack(parallel.allgather_records(local, B))
+        self.history.append(dict(B=B, seconds=time.perf_counter() - t_start, iters=int(table["iters"].sum()),
+                                 rmse=table["rmse"].copy()))
+        metric = np.inf
+        best_transformation = np.eye(4)
+        for n in range(B):
+            current_metric = float(table["rmse"][n])
+            if current_metric == 0 and hasattr(self._optimizer, "zero_rmse_message"):
+                # the reference raises inside optimize() of attempt n, before
+                # drawing attempt n+1: leave the RNG exactly there
+                np.random.set_state(states[n])
+                raise ValueError(self._optimizer.zero_rmse_message)
+            if current_metric < metric:
+                metric = current_metric
+                best_transformation = self._compose(R0s[n], t0s[n], table["T"][n])
+        return best_transformation, metric
+
+    # -------------------------------------------------------------- compass
+    def compass_step(self, source, target, scale_factors, delta):
+        """Aligner.py:206-226."""
+        new_scale_factors = scale_factors + delta
+        target_scaled = target * new_scale_factors
+        current_rotation, current_metric = self.multistart_registration(source, target_scaled)
+        return new_scale_factors, current_rotation, current_metric
+
+    def align(self, source: np.ndarray, target: np.ndarray, refine_registration: bool = True,
+              icp_type: str = "PointToPlane") -> Tuple[np.ndarray, float, np.ndarray, List[float]]:
+        """Aligner.py:228-317."""
+        source = self._source_preprocessor.preprocess(source)
+        target = self._target_preprocessor.preprocess(target)
+        iteration = 0
+        optimal_scale_factors = np.ones((1, 3))
+        start = time.time()
+        optimal_transformation, optimal_metric = self.multistart_registration(source, target)
+        self._LOG.info(f"Multi-start registration time: {time.time() - start}")
+        errors = [optimal_metric]
+        directions = np.eye(3)
+        while self._delta >= self._eps and iteration <= self._max_iter:
+            iteration += 1
+            for axis in range(3):
+                scale_plus = self._delta * directions[:, axis]
+                new_scale_factors, new_rotation, new_metric = self.compass_step(
+                    source, target, optimal_scale_factors, scale_plus)
+                if new_metric <= optimal_metric:
+                    optimal_metric = new_metric
+                    optimal_transformation = new_rotation
+                    optimal_scale_factors += scale_plus
+                    errors.append(new_metric)
+                    break
+                scale_neg = -self._delta * directions[:, axis]
+                new_scale_factors, new_rotation, new_metric = self.compass_step(
+                    source, target, optimal_scale_factors, scale_neg)
+                if new_metric <= optimal_metric:
+                    optimal_metric = new_metric
+                    optimal_transformation = new_rotation
+                    optimal_scale_factors += scale_neg
+                    errors.append(new_metric)
+                    break
+            if new_metric > optimal_metric:
+                self._delta = self._delta / 2
+        if refine_registration:
+            target = target * optimal_scale_factors
+            optimal_transformation, optimal_metric = self.refine_registration(
+                source=source, target=target, initial_transform=optimal_transformation, icp_type=icp_type)
+            errors.append(optimal_metric)
+        self.transfromation = optimal_transformation
+        self.scale_factors = optimal_scale_factors
+        return optimal_transformation, optimal_metric, optimal_scale_factors, errors
+
+    def refine_registration(self, source, target, initial_transform, max_iteration: int = __REFINER_MAX_ITER__,
+                            distance_threshold: float = __REFINER_DISTANCE_THRESHOLD__, icp_type: str = "PointToPoint"):
+        """Aligner.py:319-364 — out of scope for this revision.
+
+        With the reference default ``PointToPlane`` Open3D 0.18 raises because the
+        target cloud carries no normals (Q5); this raises the same error type."""
+        if icp_type == "PointToPlane":
+            raise RuntimeError("TransformationEstimationPointToPlane and TransformationEstimationColoredICP "
+                               "require pre-computed normal vectors for target PointCloud.")
+        raise NotImplementedError("refine_registration(PointToPoint) is not built yet; "
+                                  "call align(..., refine_registration=False)")
+
+    def transfrom(self, source: np.ndarray) -> np.ndarray:
+        """Aligner.py:367-394."""
+        for block in self._source_preprocessor.preprocessor_blocks:
+            if issubclass(block.__class__, BaseScaler):
+                source_mean, source_distance = block.mean, block.scale
+        for block in self._target_preprocessor.preprocessor_blocks:
+            if issubclass(block.__class__, BaseScaler):
+                target_mean, target_distance = block.mean, block.scale
+        source = (source - source_mean) / source_distance
+        source = np.dot(source, self.transfromation[:3, :3]) + self.transfromation[:3, 3]
+        source = source / self.scale_factors
+        return source * target_distance + target_mean
+
+    def __repr__(self):
+        return (f"{self.__class__.__name__}(source_preprocessor={self._source_preprocessor}, "
+                f"target_preprocessor={self._target_preprocessor}, optimizer={self._optimizer}, "
+                f"attempts={self._attempts}, deg={self._deg}, mu={self._mu}, std={self._std}, "
+                f"delta={self._delta}, max_iter={self._max_iter}, eps={self._eps})")

@@ -1,0 +1,244 @@
+"""ctypes binding of liborpcd_hip.so (include/orpcd.h).
+
+The product path has exactly one backend: the HIP library built for gfx950.
+If it is missing or cannot find a GPU, calls fail loudly — there is no CPU
+fallback (the CPU oracle under oracle/ is test infrastructure only).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+from typing import Optional
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("ORPCD_HIP_LIB", os.path.join(_HERE, "_lib", "liborpcd_hip.so"))
+
+ORPCD_OK, ORPCD_EINVAL, ORPCD_ENOCORR, ORPCD_EDEVICE = 0, 1, 2, 3
+
+_f64p = np.ctypeslib.ndpointer(dtype=np.float64, flags="C_CONTIGUOUS")
+_i32p = np.ctypeslib.ndpointer(dtype=np.int32, flags="C_CONTIGUOUS")
+_i64p = np.ctypeslib.ndpointer(dtype=np.int64, flags="C_CONTIGUOUS")
+
+
+class NativeError(RuntimeError):
+    """A HIP runtime / kernel failure or a missing native library."""
+
+
+class GicpParams(ctypes.Structure):
+    _fields_ = [("max_correspondence_distance", ctypes.c_double), ("max_iteration", ctypes.c_int32),
+                ("relative_fitness", ctypes.c_double), ("relative_rmse", ctypes.c_double),
+                ("epsilon", ctypes.c_double)]
+
+
+class FgrParams(ctypes.Structure):
+    _fields_ = [("division_factor", ctypes.c_double), ("tuple_scale", ctypes.c_double),
+                ("maximum_correspondence_distance", ctypes.c_double), ("iteration_number", ctypes.c_int32),
+                ("decrease_mu", ctypes.c_int32), ("maximum_tuple_count", ctypes.c_int32),
+                ("seed", ctypes.c_uint64)]
+
+
+_lib = None
+_lib_lock = threading.Lock()
+
+# every symbol include/orpcd.h declares (checked by tests/test_abi.py)
+EXPORTED = ("orpcd_abi_version", "orpcd_device_count", "orpcd_ctx_create", "orpcd_ctx_destroy",
+            "orpcd_last_error", "orpcd_set_target", "orpcd_set_source", "orpcd_gicp_batch",
+            "orpcd_nn1_radius", "orpcd_estimate_normals", "orpcd_fpfh", "orpcd_fgr", "orpcd_profiling",
+            "orpcd_stats", "orpcd_reset_stats")
+
+
+def load_library():
+    """Load liborpcd_hip.so (raises NativeError if it is not built)."""
+    global _lib
+    with _lib_lock:
+        if _lib is not None:
+            return _lib
+        if not os.path.exists(LIB_PATH):
+            raise NativeError(f"liborpcd_hip.so not found at {LIB_PATH}; build it with "
+                              "`python multi-scale-pointcloud-registration_amd/build_native.py` "
+                              "(or __graft_entry__.build()).  There is no CPU fallback.")
+        L = ctypes.CDLL(LIB_PATH)
+        vp, c_int, c_i64, c_dbl = ctypes.c_void_p, ctypes.c_int, ctypes.c_int64, ctypes.c_double
+        L.orpcd_abi_version.restype = c_int
+        L.orpcd_device_count.argtypes = [ctypes.POINTER(c_int)]
+        L.orpcd_ctx_create.argtypes = [c_int, ctypes.POINTER(vp)]
+        L.orpcd_ctx_destroy.argtypes = [vp]
+        L.orpcd_last_error.argtypes = [vp]
+        L.orpcd_last_error.restype = ctypes.c_char_p
+        L.orpcd_set_target.argtypes = [vp, _f64p, c_i64, c_dbl]
+        L.orpcd_set_source.argtypes = [vp, _f64p, c_i64]
+        L.orpcd_gicp_batch.argtypes = [vp, _f64p, _f64p, ctypes.c_int32, ctypes.POINTER(GicpParams), _f64p, _f64p,
+                                       _f64p, _i32p, _i64p]
+        L.orpcd_nn1_radius.argtypes = [vp, _f64p, c_i64, _f64p, c_i64, c_dbl, _i32p, _f64p]
+        L.orpcd_estimate_normals.argtypes = [vp, _f64p, c_i64, ctypes.c_int32, c_dbl, c_dbl, vp, vp, vp]
+        L.orpcd_fpfh.argtypes = [vp, _f64p, c_i64, c_dbl, ctypes.c_int32, c_dbl, ctypes.c_int32, _f64p, _f64p]
+        L.orpcd_fgr.argtypes = [vp, _f64p, c_i64, _f64p, c_i64, _f64p, _f64p, ctypes.POINTER(FgrParams), _f64p,
+                                _f64p, _f64p, _i64p, _i64p]
+        L.orpcd_profiling.argtypes = [vp, ctypes.c_int32]
+        L.orpcd_stats.argtypes = [vp, _f64p, ctypes.c_int32]
+        L.orpcd_reset_stats.argtypes = [vp]
+        if L.orpcd_abi_version() != 1:
+            raise NativeError("liborpcd_hip.so ABI mismatch")
+        _lib = L
+        return L
+
+
+def device_count() -> int:
+    n = ctypes.c_int(0)
+    load_library().orpcd_device_count(ctypes.byref(n))
+    return int(n.value)
+
+
+def _c3(a) -> np.ndarray:
+    a = np.ascontiguousarray(a, dtype=np.float64)
+    if a.ndim != 2 or a.shape[1] != 3:
+        raise ValueError(f"expected an (N, 3) point array, got shape {a.shape}")
+    return a
+
+
+class Context:
+    """One device context (stream + device-resident clouds).  Not thread-safe."""
+
+    def __init__(self, device: Optional[int] = None):
+        L = load_library()
+        if device is None:
+            device = int(os.environ.get("LOCAL_RANK", "0")) if device_count() > 1 else 0
+        h = ctypes.c_void_p()
+        rc = L.orpcd_ctx_create(int(device), ctypes.byref(h))
+        if rc != ORPCD_OK:
+            raise NativeError(f"orpcd_ctx_create(device={device}) failed with status {rc} "
+                              f"({device_count()} HIP device(s) visible)")
+        self._h = h
+        self._L = L
+        self.device = device
+        self._target_key = None
+        self._source_key = None
+
+    def close(self):
+        if getattr(self, "_h", None):
+            self._L.orpcd_ctx_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _check(self, rc: int, what: str):
+        if rc == ORPCD_OK:
+            return
+        msg = self._L.orpcd_last_error(self._h)
+        msg = msg.decode() if msg else ""
+        if rc == ORPCD_EINVAL:
+            raise ValueError(f"{what}: {msg}")
+        raise NativeError(f"{what} failed (status {rc}): {msg}")
+
+    # ------------------------------------------------------------- clouds
+    @staticmethod
+    def _key(a: np.ndarray):
+        return (a.shape, hash(a.tobytes()))
+
+    def set_target(self, xyz: np.ndarray, epsilon: float = 1e-3, cache: bool = True):
+        xyz = _c3(xyz)
+        key = (self._key(xyz), float(epsilon))
+        if cache and key == self._target_key:
+            return
+        self._check(self._L.orpcd_set_target(self._h, xyz, len(xyz), float(epsilon)), "orpcd_set_target")
+        self._target_key = key
+
+    def set_source(self, xyz: np.ndarray, cache: bool = True):
+        xyz = _c3(xyz)
+        key = self._key(xyz)
+        if cache and key == self._source_key:
+            return
+        self._check(self._L.orpcd_set_source(self._h, xyz, len(xyz)), "orpcd_set_source")
+        self._source_key = key
+
+    # --------------------------------------------------------------- GICP
+    def gicp_batch(self, R0: np.ndarray, t0: np.ndarray, max_correspondence_distance=0.5, max_iteration=100,
+                   relative_fitness=1e-6, relative_rmse=1e-6, epsilon=1e-3) -> dict:
+        R0 = np.ascontiguousarray(R0, dtype=np.float64).reshape(-1, 3, 3)
+        B = R0.shape[0]
+        t0 = np.ascontiguousarray(t0, dtype=np.float64).reshape(B, 3)
+        p = GicpParams(float(max_correspondence_distance), int(max_iteration), float(relative_fitness),
+                       float(relative_rmse), float(epsilon))
+        T = np.zeros((B, 4, 4))
+        rmse, fit = np.zeros(B), np.zeros(B)
+        iters = np.zeros(B, np.int32)
+        ncorr = np.zeros(B, np.int64)
+        self._check(self._L.orpcd_gicp_batch(self._h, R0.reshape(-1), t0.reshape(-1), B, ctypes.byref(p),
+                                             T.reshape(-1), rmse, fit, iters, ncorr), "orpcd_gicp_batch")
+        return dict(T=T, rmse=rmse, fitness=fit, iters=iters, ncorr=ncorr)
+
+    # -------------------------------------------------------- kernel level
+    def nn1_radius(self, q: np.ndarray, t: np.ndarray, radius: float):
+        q, t = _c3(q), _c3(t)
+        idx = np.empty(len(q), np.int32)
+        d2 = np.empty(len(q))
+        self._check(self._L.orpcd_nn1_radius(self._h, q, len(q), t, len(t), float(radius), idx, d2),
+                    "orpcd_nn1_radius")
+        return idx, d2
+
+    def estimate_normals(self, xyz: np.ndarray, knn: int = 20, radius: float = -1.0, epsilon: float = 1e-3):
+        xyz = _c3(xyz)
+        n = len(xyz)
+        normals = np.empty((n, 3))
+        raw = np.empty((n, 3, 3))
+        cov = np.empty((n, 3, 3))
+        ptr = lambda a: a.ctypes.data_as(ctypes.c_void_p)  # noqa: E731
+        self._check(self._L.orpcd_estimate_normals(self._h, xyz, n, int(knn), float(radius), float(epsilon),
+                                                   ptr(normals), ptr(raw), ptr(cov) if epsilon >= 0 else None),
+                    "orpcd_estimate_normals")
+        return normals, raw, (cov if epsilon >= 0 else None)
+
+    def fpfh(self, xyz: np.ndarray, normal_radius=0.1, normal_knn=20, fpfh_radius=0.1, fpfh_knn=20):
+        xyz = _c3(xyz)
+        normals = np.empty((len(xyz), 3))
+        feat = np.empty((len(xyz), 33))
+        self._check(self._L.orpcd_fpfh(self._h, xyz, len(xyz), float(normal_radius), int(normal_knn),
+                                       float(fpfh_radius), int(fpfh_knn), normals, feat.reshape(-1)), "orpcd_fpfh")
+        return normals, feat
+
+    def fgr(self, src, tgt, src_feat, tgt_feat, division_factor=1.4, tuple_scale=0.9,
+            maximum_correspondence_distance=0.5, iteration_number=100, decrease_mu=True,
+            maximum_tuple_count=1000, seed=0) -> dict:
+        src, tgt = _c3(src), _c3(tgt)
+        fs = np.ascontiguousarray(src_feat, dtype=np.float64)
+        ft = np.ascontiguousarray(tgt_feat, dtype=np.float64)
+        p = FgrParams(float(division_factor), float(tuple_scale), float(maximum_correspondence_distance),
+                      int(iteration_number), int(bool(decrease_mu)), int(maximum_tuple_count),
+                      int(seed) & 0xFFFFFFFFFFFFFFFF)
+        T = np.zeros(16)
+        fit, rmse = np.zeros(1), np.zeros(1)
+        nc, nm = np.zeros(1, np.int64), np.zeros(2, np.int64)
+        self._check(self._L.orpcd_fgr(self._h, src, len(src), tgt, len(tgt), fs.reshape(-1), ft.reshape(-1),
+                                      ctypes.byref(p), T, fit, rmse, nc, nm), "orpcd_fgr")
+        return dict(T=T.reshape(4, 4), fitness=float(fit[0]), rmse=float(rmse[0]), ncorr=int(nc[0]),
+                    n_mutual=int(nm[0]), n_tuple_corr=int(nm[1]))
+
+    # ---------------------------------------------------------- measuring
+    def profiling(self, enable: bool = True):
+        self._check(self._L.orpcd_profiling(self._h, int(bool(enable))), "orpcd_profiling")
+
+    def stats(self) -> dict:
+        out = np.zeros(5)
+        self._check(self._L.orpcd_stats(self._h, out, 5), "orpcd_stats")
+        return dict(launches=out[0], ms=out[1], pairs=out[2], iterations=out[3], passes=out[4])
+
+    def reset_stats(self):
+        self._check(self._L.orpcd_reset_stats(self._h), "orpcd_reset_stats")
+
+
+_default_ctx = {}
+
+
+def default_context(device: Optional[int] = None) -> Context:
+    """Process-wide context per device (one process per GPU)."""
+    key = device
+    if key not in _default_ctx:
+        _default_ctx[key] = Context(device)
+    return _default_ctx[key]

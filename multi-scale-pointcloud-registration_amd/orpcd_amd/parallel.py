@@ -1,0 +1,75 @@
+"""Multistart sharding across ranks (one process per GPU).
+
+The attempts of one ``multistart_registration`` (Aligner.py:178-202) are
+independent: every rank replays the identical host RNG stream, runs a
+contiguous block of attempts on its own GPU, and one all-gather of a fixed
+160-byte record per attempt gives every rank the full table, on which each
+applies the reference's strict-< argmin in attempt order.  No other data-path
+collective exists.  Backend: ``torch.distributed`` — "nccl" (= RCCL over
+xGMI on ROCm) on GPUs, "gloo" for CPU tests.
+"""
+from __future__ import annotations
+
+from typing import Tuple
+
+import numpy as np
+
+REC = 20  # rmse, fitness, iters, ncorr, T(16)
+
+
+def world() -> Tuple[int, int]:
+    try:
+        import torch.distributed as dist
+    except Exception:  # pragma: no cover
+        return 0, 1
+    if dist.is_available() and dist.is_initialized():
+        return dist.get_rank(), dist.get_world_size()
+    return 0, 1
+
+
+def shard(B: int, rank: int, world_size: int) -> Tuple[int, int]:
+    """Contiguous block [lo, hi) of attempts for `rank` (sizes differ by <= 1)."""
+    base, rem = divmod(B, world_size)
+    lo = rank * base + min(rank, rem)
+    return lo, lo + base + (1 if rank < rem else 0)
+
+
+def pack(r: dict) -> np.ndarray:
+    b = len(r["rmse"])
+    out = np.zeros((b, REC))
+    out[:, 0] = r["rmse"]
+    out[:, 1] = r["fitness"]
+    out[:, 2] = r["iters"]
+    out[:, 3] = r["ncorr"]
+    out[:, 4:] = np.asarray(r["T"]).reshape(b, 16)
+    return out
+
+
+def unpack(rec: np.ndarray) -> dict:
+    return dict(rmse=rec[:, 0].copy(), fitness=rec[:, 1].copy(), iters=rec[:, 2].astype(np.int64),
+                ncorr=rec[:, 3].astype(np.int64), T=rec[:, 4:].reshape(-1, 4, 4).copy())
+
+
+def allgather_records(local: np.ndarray, B: int) -> np.ndarray:
+    """All-gather per-attempt records; returns the (B, REC) table in attempt order."""
+    rank, ws = world()
+    if ws == 1:
+        return local
+    import torch
+    import torch.distributed as dist
+
+    width = -(-B // ws)  # max block size
+    buf = np.zeros((width, REC))
+    buf[: len(local)] = local
+    if dist.get_backend() == "nccl":
+        dev = torch.device("cuda", torch.cuda.current_device())
+    else:
+        dev = torch.device("cpu")
+    t = torch.from_numpy(buf).to(dev)
+    outs = [torch.empty_like(t) for _ in range(ws)]
+    dist.all_gather(outs, t)
+    table = np.zeros((B, REC))
+    for r in range(ws):
+        lo, hi = shard(B, r, ws)
+        table[lo:hi] = outs[r][: hi - lo].cpu().numpy()
+    return table

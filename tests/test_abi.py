@@ -1,0 +1,72 @@
+"""The C-ABI library loads and exports every symbol include/orpcd.h declares
+(no compute calls: runs on a host without a GPU)."""
+import ctypes
+import os
+import re
+import subprocess
+
+import numpy as np
+import pytest
+
+from conftest import REPO
+
+
+def _declared():
+    src = open(os.path.join(REPO, "include", "orpcd.h")).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(orpcd_[a-z0-9_]+)\s*\(", src)))
+
+
+def test_header_lists_the_python_binding_symbols():
+    from orpcd_amd import _native
+    assert sorted(_native.EXPORTED) == _declared()
+
+
+def test_library_exports_every_declared_symbol():
+    from orpcd_amd import _native
+    lib = _native.LIB_PATH
+    assert os.path.exists(lib), "run __graft_entry__.build() first"
+    out = subprocess.run(["nm", "-D", "--defined-only", lib], capture_output=True, text=True, check=True).stdout
+    exported = set(re.findall(r"\bT (orpcd_[a-z0-9_]+)", out))
+    missing = [s for s in _declared() if s not in exported]
+    assert not missing, missing
+    L = _native.load_library()
+    assert L.orpcd_abi_version() == 1
+
+
+def test_library_is_gfx950_code_object():
+    from orpcd_amd import _native
+    out = subprocess.run(["/opt/rocm/lib/llvm/bin/llvm-objdump", "--offloading", _native.LIB_PATH],
+                         capture_output=True, text=True)
+    text = out.stdout + out.stderr
+    if "gfx" not in text:  # older objdump: fall back to scanning the bundle
+        text = open(_native.LIB_PATH, "rb").read().decode("latin1")
+    assert "gfx950" in text
+
+
+def test_no_gpu_fails_loudly_not_silently():
+    from orpcd_amd import _native
+    if _native.device_count() > 0:
+        pytest.skip("a GPU is visible")
+    L = _native.load_library()
+    h = ctypes.c_void_p()
+    assert L.orpcd_ctx_create(0, ctypes.byref(h)) == _native.ORPCD_EDEVICE
+    with pytest.raises(_native.NativeError):
+        _native.Context(0)
+
+
+def test_null_context_is_rejected():
+    from orpcd_amd import _native
+    L = _native.load_library()
+    assert L.orpcd_ctx_destroy(None) == _native.ORPCD_EINVAL
+    assert L.orpcd_set_source(None, np.zeros(3), 1) == _native.ORPCD_EINVAL
+    assert L.orpcd_last_error(None) == b"null context"
+
+
+def test_product_package_never_imports_the_oracle():
+    pkg = os.path.join(REPO, "multi-scale-pointcloud-registration_amd")
+    for root, _, files in os.walk(pkg):
+        for f in files:
+            if f.endswith((".py", ".hip", ".h", ".cpp")):
+                text = open(os.path.join(root, f)).read()
+                assert "import oracle" not in text and "liborpcd_oracle" not in text, f

@@ -1,0 +1,158 @@
+"""GPU parity: liborpcd_hip.so (through the C-ABI) against the CPU oracle.
+
+Tolerances (north_star "stated float tolerance"):
+  * nearest-neighbour indices: identical, except certified near-ties where the
+    two candidates' exact distances differ by < 1e-6 relative (the fp32 search
+    cannot order them); d^2 of the chosen pair is fp64 (rtol 1e-12);
+  * normals / covariances: fp64 on both sides, same operation order: 1e-10;
+  * per-optimize GICP: T elementwise <= 1e-6, inlier RMSE |delta| <= 1e-7,
+    fitness |delta| <= 1e-4, iteration count within 1;
+  * full align(): final RMSE |delta| <= 1e-5, scale factors identical.
+"""
+import numpy as np
+import pytest
+
+from workloads import rot_xyz, small_pair
+
+pytestmark = pytest.mark.gpu
+
+T_TOL, RMSE_TOL = 1e-6, 1e-7
+
+
+def _certified_nn(oracle_idx, gpu_idx, q, t):
+    bad = np.nonzero(oracle_idx != gpu_idx)[0]
+    for i in bad:
+        a, b = oracle_idx[i], gpu_idx[i]
+        assert a >= 0 and b >= 0, f"query {i}: one side found no neighbour ({a} vs {b})"
+        da = ((q[i] - t[a]) ** 2).sum()
+        db = ((q[i] - t[b]) ** 2).sum()
+        assert abs(da - db) <= 1e-6 * max(da, 1e-30), f"query {i}: not a near-tie ({da} vs {db})"
+    return len(bad)
+
+
+def test_nn1_radius_matches_oracle(ctx, oracle):
+    rng = np.random.default_rng(0)
+    t = rng.normal(size=(7001, 3)) * 0.5          # ragged: not a tile multiple
+    q = rng.normal(size=(5003, 3)) * 0.6
+    for radius in (0.05, 0.3, 10.0):
+        oi, od = oracle.nn1_radius(q, t, radius)
+        gi, gd = ctx.nn1_radius(q, t, radius)
+        flips = _certified_nn(oi, gi, q, t)
+        assert flips <= 2
+        same = oi == gi
+        assert np.allclose(gd[same], od[same], rtol=1e-12, atol=0)
+        assert np.all(gd[gi < 0] == 0)
+
+
+def test_nn1_edge_cases(ctx, oracle):
+    t = np.array([[1.0, 0, 0], [-1.0, 0, 0], [0, 1.0, 0], [1.0, 0, 0]])
+    gi, gd = ctx.nn1_radius(np.zeros((1, 3)), t, 2.0)
+    assert gi[0] == 0 and gd[0] == 1.0                    # exact tie -> lowest index
+    gi, _ = ctx.nn1_radius(np.zeros((1, 3)), t, 1.0)      # strict d^2 < r^2
+    assert gi[0] == -1
+    gi, gd = ctx.nn1_radius(np.zeros((0, 3)), t, 1.0)     # empty query set
+    assert len(gi) == 0
+    gi, gd = ctx.nn1_radius(np.ones((3, 3)), t[:1], 5.0)  # single target
+    assert np.all(gi == 0)
+    with pytest.raises(ValueError):
+        ctx.nn1_radius(np.zeros((1, 3)), t, 0.0)
+
+
+@pytest.mark.parametrize("knn,radius", [(20, -1.0), (20, 0.1), (8, -1.0), (32, 0.2)])
+def test_estimate_normals_matches_oracle(ctx, oracle, knn, radius):
+    src, _ = small_pair(3000, seed=1)
+    on, oraw, ocov = oracle.estimate_normals(src, knn, radius, 1e-3)
+    gn, graw, gcov = ctx.estimate_normals(src, knn, radius, 1e-3)
+    assert np.abs(graw - oraw).max() < 1e-12
+    assert np.abs(gn - on).max() < 1e-10
+    assert np.abs(gcov - ocov).max() < 1e-10
+
+
+def test_estimate_normals_degenerate(ctx, oracle):
+    pts = np.array([[0.0, 0, 0], [1.0, 0, 0]])            # < 3 neighbours -> Identity -> (0,0,1)
+    gn, graw, gcov = ctx.estimate_normals(pts, 20, -1.0, 1e-3)
+    on, oraw, ocov = oracle.estimate_normals(pts, 20, -1.0, 1e-3)
+    assert np.array_equal(gn, on) and np.allclose(gn, [[0, 0, 1], [0, 0, 1]])
+    assert np.allclose(gcov, ocov)
+    line = np.c_[np.linspace(0, 1, 30), np.zeros(30), np.zeros(30)]  # collinear -> planar-degenerate cov
+    gn, _, _ = ctx.estimate_normals(line, 20)
+    on, _, _ = oracle.estimate_normals(line, 20)
+    assert np.allclose(gn, on)
+
+
+def _cmp_gicp(g, o, it_tol=1):
+    assert np.abs(g["T"] - o["T"]).max() <= T_TOL, np.abs(g["T"] - o["T"]).max()
+    assert abs(g["rmse"] - o["rmse"]) <= RMSE_TOL, (g["rmse"], o["rmse"])
+    assert abs(g["fitness"] - o["fitness"]) <= 1e-4
+    assert abs(g["iters"] - o["iters"]) <= it_tol
+
+
+@pytest.mark.parametrize("n,m,seed", [(300, 300, 0), (2000, 2500, 1), (5000, 4000, 2)])
+def test_gicp_single_matches_oracle(ctx, oracle, n, m, seed):
+    src, tgt = small_pair(n, m, seed=seed)
+    o = oracle.gicp(src, tgt, 0.5, 100)
+    ctx.set_target(tgt)
+    ctx.set_source(src)
+    r = ctx.gicp_batch(np.eye(3)[None], np.zeros((1, 3)))
+    g = dict(T=r["T"][0], rmse=r["rmse"][0], fitness=r["fitness"][0], iters=r["iters"][0])
+    _cmp_gicp(g, o)
+
+
+def test_gicp_batch_posed_starts_match_oracle(ctx, oracle):
+    """Multistart semantics: start b runs on source @ R0[b] + t0[b] (Aligner.py:183-185)."""
+    src, tgt = small_pair(1500, 1800, seed=3)
+    rng = np.random.default_rng(7)
+    B = 6
+    R0 = np.array([rot_xyz(*rng.uniform(-90, 90, 3)) for _ in range(B)])
+    t0 = rng.normal(size=(B, 3)) * 0.1
+    ctx.set_target(tgt)
+    ctx.set_source(src)
+    r = ctx.gicp_batch(R0, t0)
+    for b in range(B):
+        o = oracle.gicp(np.dot(src, R0[b]) + t0[b], tgt, 0.5, 100)
+        _cmp_gicp(dict(T=r["T"][b], rmse=r["rmse"][b], fitness=r["fitness"][b], iters=r["iters"][b]), o)
+
+
+def test_gicp_plugin_drop_in(oracle):
+    """GeneralizedICP.optimize: R transposed (generalizedICP.py:72-74), rmse==0 -> ValueError."""
+    from orpcd_amd import GeneralizedICP
+    src, tgt = small_pair(1200, seed=4)
+    T, rmse = GeneralizedICP().optimize(src, tgt)
+    Tr, rr = oracle.OracleGeneralizedICP().optimize(src, tgt)
+    assert np.abs(T - Tr).max() <= T_TOL and abs(rmse - rr) <= RMSE_TOL
+    with pytest.raises(ValueError):
+        GeneralizedICP().optimize(src, tgt + 50.0)  # no correspondences within 0.5
+
+
+def test_gicp_max_iteration_and_tiny_clouds(ctx, oracle):
+    src, tgt = small_pair(400, seed=5)
+    for it in (1, 3):
+        ctx.set_target(tgt)
+        ctx.set_source(src)
+        r = ctx.gicp_batch(np.eye(3)[None], np.zeros((1, 3)), max_iteration=it)
+        o = oracle.gicp(src, tgt, 0.5, it)
+        assert r["iters"][0] == o["iters"] == it
+        _cmp_gicp(dict(T=r["T"][0], rmse=r["rmse"][0], fitness=r["fitness"][0], iters=r["iters"][0]), o, 0)
+    tiny = src[:2]
+    ctx.set_source(tiny)
+    r = ctx.gicp_batch(np.eye(3)[None], np.zeros((1, 3)))
+    o = oracle.gicp(tiny, tgt, 0.5, 100)
+    _cmp_gicp(dict(T=r["T"][0], rmse=r["rmse"][0], fitness=r["fitness"][0], iters=r["iters"][0]), o)
+
+
+def test_align_matches_oracle_aligner(oracle):
+    """Full Aligner.align (refine off) on a small pair: same decisions as the
+    CPU restatement of the reference's control flow."""
+    from orpcd_amd import Aligner, GeneralizedICP, Preprocessor
+    src, tgt = small_pair(800, 900, seed=6)
+    tgt = tgt * np.array([1.15, 1.0, 0.9])
+    np.random.seed(0)
+    o = oracle.OracleAligner(oracle.OracleGeneralizedICP(), attempts=4)
+    To, mo, sfo, eo = o.align(src.copy(), tgt.copy())
+    np.random.seed(0)
+    al = Aligner(Preprocessor([]), Preprocessor([]), GeneralizedICP(), attempts=4)
+    T, m, sf, e = al.align(src.copy(), tgt.copy(), refine_registration=False)
+    assert np.array_equal(sf, sfo)
+    assert len(e) == len(eo)
+    assert abs(m - mo) <= 1e-5
+    assert np.abs(T - To).max() <= 1e-4

@@ -1,0 +1,145 @@
+"""Host logic of the product package against the reference's golden vectors
+(no GPU: the optimizers here are scripted, the native library is not called)."""
+import numpy as np
+import pytest
+
+from conftest import GOLDEN
+
+
+class BatchedScripted:
+    """optimize_batch twin of ScriptedOptimizer: identical values per attempt."""
+
+    zero_rmse_message = "Optimization failed with loss = 0."
+
+    def __init__(self, inner):
+        self.inner = inner
+        self.batches = []
+
+    def optimize_batch(self, source, target, R0, t0):
+        Ts, rm = [], []
+        for R, t in zip(R0, t0):
+            T, m = self.inner.optimize(np.dot(source.copy(), R) + t, target)
+            Ts.append(T)
+            rm.append(m)
+        self.batches.append(len(R0))
+        n = len(R0)
+        return dict(T=np.array(Ts), rmse=np.array(rm), fitness=np.ones(n), iters=np.ones(n, np.int32),
+                    ncorr=np.ones(n, np.int64))
+
+
+def test_rng_replay_matches_reference_G1():
+    from orpcd_amd import Aligner, Preprocessor
+    g = np.load(f"{GOLDEN}/g1_rng.npz")
+    for seed in (0, 1, 42):
+        np.random.seed(seed)
+        al = Aligner(Preprocessor([]), Preprocessor([]), optimizer=None)
+        for n in range(64):
+            R, t = al.initialize_rotation()
+            assert np.array_equal(R, g[f"R_{seed}"][n]) and np.array_equal(t, g[f"t_{seed}"][n])
+
+
+def test_preprocess_matches_reference_G2():
+    from orpcd_amd import Preprocessor
+    from orpcd_amd.Preprocessor.Downsamplers import RandomDownsampler
+    from workloads import armadillo
+    g = np.load(f"{GOLDEN}/g2_preprocess.npz")
+    for name, cloud in zip(("ArmadilloBack_330", "ArmadilloBack_0"), armadillo()):
+        np.random.seed(0)
+        pp = Preprocessor([RandomDownsampler(5000)])
+        out = pp.preprocess(cloud)
+        sc = pp.preprocessor_blocks[0]
+        assert np.array_equal(out, g[f"{name}_out"])
+        assert np.array_equal(sc.mean, g[f"{name}_mean"]) and sc.scale == g[f"{name}_scale"]
+
+
+@pytest.mark.parametrize("batched", [False, True])
+@pytest.mark.parametrize("mode,attempts,seed", [("scripted", 4, 7), ("never_improves", 30, 0), ("constant", 2, 3)])
+def test_aligner_matches_reference_G3(mode, attempts, seed, batched):
+    from orpcd_amd import Aligner, Preprocessor
+    from scripted import ScriptedOptimizer
+    g = np.load(f"{GOLDEN}/g3_aligner_trace.npz")
+    np.random.seed(seed)
+    inner = ScriptedOptimizer(g["goal"], mode=mode)
+    opt = BatchedScripted(inner) if batched else inner
+    al = Aligner(Preprocessor([]), Preprocessor([]), opt, attempts=attempts)
+    T, m, sf, err = al.align(g["src"].copy(), g["tgt"].copy(), refine_registration=False)
+    assert np.array_equal(T, g[f"{mode}_T"]) and m == g[f"{mode}_metric"]
+    assert np.array_equal(sf, g[f"{mode}_sf"]) and np.array_equal(err, g[f"{mode}_errors"])
+    assert np.array_equal(np.array([c[2] for c in inner.calls]), g[f"{mode}_call_rmse"])
+    assert np.array_equal(np.array([c[1] for c in inner.calls]), g[f"{mode}_call_s0"])
+    assert np.array_equal(np.random.uniform(size=4), g[f"{mode}_rng_after"])
+    assert al._delta == g[f"{mode}_delta_after"]  # Q3: delta is instance state
+    if batched:
+        assert all(b == attempts for b in opt.batches)
+
+
+def test_batched_zero_rmse_raises_like_reference():
+    """The reference raises ValueError inside attempt n's optimize(); the RNG
+    is then positioned right after attempt n's draws (not after all B)."""
+    from orpcd_amd import Aligner, Preprocessor
+
+    class Fails(BatchedScripted):
+        def __init__(self):
+            self.batches = []
+
+        def optimize_batch(self, source, target, R0, t0):
+            n = len(R0)
+            rm = np.linspace(1, 2, n)
+            rm[2] = 0.0
+            return dict(T=np.tile(np.eye(4), (n, 1, 1)), rmse=rm, fitness=np.ones(n), iters=np.ones(n),
+                        ncorr=np.ones(n))
+
+    np.random.seed(11)
+    al = Aligner(Preprocessor([]), Preprocessor([]), Fails(), attempts=6)
+    src = np.random.default_rng(0).normal(size=(20, 3))
+    np.random.seed(11)
+    with pytest.raises(ValueError):
+        al.multistart_registration(src, src)
+    after = np.random.uniform(size=3)
+    np.random.seed(11)
+    for _ in range(3):
+        al.initialize_rotation()
+    assert np.array_equal(after, np.random.uniform(size=3))
+
+
+def test_refine_registration_behaviour():
+    from orpcd_amd import Aligner, Preprocessor
+    al = Aligner(Preprocessor([]), Preprocessor([]), None)
+    with pytest.raises(RuntimeError):  # Q5: PointToPlane without target normals
+        al.refine_registration(np.zeros((3, 3)), np.zeros((3, 3)), np.eye(4), icp_type="PointToPlane")
+
+
+def test_constructor_validation_falls_back_to_defaults():
+    from orpcd_amd import Aligner, GeneralizedICP, Preprocessor
+    al = Aligner(Preprocessor([]), Preprocessor([]), None, attempts=0, deg=-1, mu=-1, std=0, delta=0,
+                 max_iter=0, eps=0)
+    assert (al._attempts, al._deg, al._mu, al._std, al._delta, al._max_iter, al._eps) == (
+        30, np.pi / 2, 0.0, 0.1, 0.2, 100, 0.05)
+    g = GeneralizedICP(max_correspondence_distance=-1, max_iterations=0)
+    assert g._max_correspondence_distance == 0.5 and g._max_iterations == 100
+
+
+def test_shard_covers_every_attempt_once():
+    from orpcd_amd.parallel import shard
+    for B in (1, 7, 30, 64, 65):
+        for W in (1, 2, 3, 8):
+            seen = []
+            for r in range(W):
+                lo, hi = shard(B, r, W)
+                seen.extend(range(lo, hi))
+            assert seen == list(range(B))
+
+
+def test_transfrom_matches_reference_formula():
+    from orpcd_amd import Aligner, Preprocessor
+    rng = np.random.default_rng(0)
+    src, tgt = rng.normal(size=(30, 3)), rng.normal(size=(25, 3))
+    ps, pt = Preprocessor([]), Preprocessor([])
+    s, t = ps.preprocess(src), pt.preprocess(tgt)
+    al = Aligner(ps, pt, None)
+    al.transfromation = np.eye(4)
+    al.transfromation[:3, 3] = [0.1, 0, 0]
+    al.scale_factors = np.array([[1.1, 0.9, 1.0]])
+    sc_s, sc_t = ps.preprocessor_blocks[0], pt.preprocessor_blocks[0]
+    expect = (((src - sc_s.mean) / sc_s.scale) + [0.1, 0, 0]) / al.scale_factors * sc_t.scale + sc_t.mean
+    assert np.allclose(al.transfrom(src), expect)
