@@ -144,7 +144,10 @@ def main():
             "roofline": {"bound": "mfma", "achieved": round(achieved, 3), "peak": FP32_PEAK_TFLOPS,
                          "unit": "TFLOP/s", "frac": round(achieved / FP32_PEAK_TFLOPS, 4), "traffic": None,
                          "kernel": "gicp_pass_kernel", "avg_launch_ms": round(avg_ms, 4),
-                         "launches": int(st["launches"]), "flop_per_pair": FLOP_PER_PAIR},
+                         "launches": int(st["launches"]), "flop_per_pair": FLOP_PER_PAIR,
+                         "pairs_per_launch": round(st["pairs"] / max(st["launches"], 1)),
+                         "pairs_vs_bruteforce": round(st["pairs"] / max(st["passes"] * len(source) * len(target), 1),
+                                                      5)},
             "cpu_baseline": cpu,
             "gicp_iterations": int(iters),
             "align": align_s,

@@ -120,8 +120,9 @@ int orpcd_fgr(orpcd_ctx* ctx, const double* src, int64_t n, const double* tgt, i
 /* ------------------------------------------------------------ measurement
  * Live kernel timing (hipEvents on the context's stream).  When enabled,
  * every launch of the dominant correspondence kernel is bracketed.
- * stats[0] = launches, [1] = total ms, [2] = query-target pairs evaluated,
- * [3] = GICP iterations completed, [4] = correspondence passes.             */
+ * stats[0] = launches, [1] = total ms, [2] = query-target pairs evaluated
+ * by the culled scan, [3] = GICP iterations completed, [4] = correspondence
+ * passes (start x pass), [5] = 64-point target tiles scanned.               */
 int orpcd_profiling(orpcd_ctx* ctx, int32_t enable);
 int orpcd_stats(orpcd_ctx* ctx, double* stats_out, int32_t n);
 int orpcd_reset_stats(orpcd_ctx* ctx);

@@ -10,13 +10,18 @@
 // the RegistrationICP convergence test, per start, on device.
 // Reference call site: generalizedICP.py:59-70, driven by Aligner.py:178-202.
 //
-// Numerics: the nearest-target search runs in fp32 over an LDS-staged target
-// tile (packed v_pk_* math, one LDS broadcast per target per wave); the chosen
-// pair is then re-evaluated in fp64 (radius test, d^2, Jacobian), so every
-// accumulated quantity is fp64.  Because W is symmetric, J^T J = A^T (Cs+Ct)^-1 A
-// and J^T r = A^T (Cs+Ct)^-1 d with A = [-[q]x | I]: no matrix square root is
-// needed.  All reductions run in a fixed order (bitwise
-// reproducible run to run).
+// Search: every wave owns 128 Morton-consecutive queries (2 per lane) of one
+// start.  Target tiles (64 Morton-consecutive points, fp32, with an AABB) are
+// culled when the AABB-to-AABB lower bound exceeds the wave's current worst
+// best-distance; surviving tiles are staged into the wave's LDS slot with one
+// coalesced 1 KiB load and scanned with packed fp32 math (v_pk_add/mul/fma,
+// one LDS broadcast per target).  The per-query bound is seeded with the
+// start's correspondence from the previous pass (the search stays exact: the
+// seed only bounds, the scan re-finds the minimum).  The chosen pair is then
+// re-evaluated in fp64 (radius test, d^2, Jacobian), so every accumulated
+// quantity is fp64.  Because W is symmetric, J^T J = A^T (Cs+Ct)^-1 A and
+// J^T r = A^T (Cs+Ct)^-1 d with A = [-[q]x | I]: no matrix square root is
+// needed.  All reductions run in a fixed order.
 #include "device_math.h"
 #include "orpcd_internal.h"
 
@@ -26,53 +31,93 @@ typedef float f2 __attribute__((ext_vector_type(2)));
 
 __device__ __forceinline__ f2 pk_fma(f2 a, f2 b, f2 c) { return __builtin_elementwise_fma(a, b, c); }
 
-// --------------------------------------------------------------------------
-// fp32 brute-force nearest search for kQPT queries per lane over all targets.
-// Targets are padded to a multiple of kTargetTile with far points so the inner
-// loop has no bounds check.  bd is initialised to the (slightly enlarged)
-// squared radius; ties resolve to the lowest target index.
-// --------------------------------------------------------------------------
-__device__ __forceinline__ void nn_search_tiles(float4* tile, const float4* __restrict__ tgt4, int mpad, f2 qx01,
-                                                f2 qy01, f2 qz01, f2 qx23, f2 qy23, f2 qz23, float bd[kQPT],
-                                                int bj[kQPT]) {
-    for (int t0 = 0; t0 < mpad; t0 += kTargetTile) {
-        __syncthreads();
+__device__ __forceinline__ float wave_max_f(float v) {
 #pragma unroll
-        for (int k = threadIdx.x; k < kTargetTile; k += kPassBlock) tile[k] = tgt4[t0 + k];
-        __syncthreads();
+    for (int off = 32; off > 0; off >>= 1) v = fmaxf(v, __shfl_xor(v, off, 64));
+    return v;
+}
+__device__ __forceinline__ float wave_min_f(float v) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) v = fminf(v, __shfl_xor(v, off, 64));
+    return v;
+}
+
+// fp32 squared distance exactly as the scan computes it
+__device__ __forceinline__ float d2f(float qx, float qy, float qz, float4 t) {
+    const float dx = qx - t.x, dy = qy - t.y, dz = qz - t.z;
+    return __builtin_fmaf(dz, dz, __builtin_fmaf(dy, dy, dx * dx));
+}
+
+// --------------------------------------------------------------------------
+// Culled exact nearest search for the 2 queries of every lane of one wave.
+// bd[] enters as the per-query bound (d^2 must be < bd to be taken), bj[] = -1.
+// Returns the number of tiles scanned.
+// --------------------------------------------------------------------------
+__device__ __forceinline__ int culled_search(float4* stage, const float4* __restrict__ p4,
+                                             const float4* __restrict__ tlo, const float4* __restrict__ thi,
+                                             int ntiles, const float qx[2], const float qy[2], const float qz[2],
+                                             const bool valid[2], float bd[2], int bj[2]) {
+    const int lane = threadIdx.x & 63;
+    float W = wave_max_f(fmaxf(valid[0] ? bd[0] : -1.0f, valid[1] ? bd[1] : -1.0f));
+    if (!(W > 0.0f)) return 0;  // no query of this wave can take anything
+    const float inf = 3.0e38f;
+    const float lox = wave_min_f(fminf(valid[0] ? qx[0] : inf, valid[1] ? qx[1] : inf));
+    const float loy = wave_min_f(fminf(valid[0] ? qy[0] : inf, valid[1] ? qy[1] : inf));
+    const float loz = wave_min_f(fminf(valid[0] ? qz[0] : inf, valid[1] ? qz[1] : inf));
+    const float hix = wave_max_f(fmaxf(valid[0] ? qx[0] : -inf, valid[1] ? qx[1] : -inf));
+    const float hiy = wave_max_f(fmaxf(valid[0] ? qy[0] : -inf, valid[1] ? qy[1] : -inf));
+    const float hiz = wave_max_f(fmaxf(valid[0] ? qz[0] : -inf, valid[1] ? qz[1] : -inf));
+    const f2 QX = {qx[0], qx[1]}, QY = {qy[0], qy[1]}, QZ = {qz[0], qz[1]};
+    float b0 = bd[0], b1 = bd[1];
+    int j0 = bj[0], j1 = bj[1];
+    int visited = 0;
+    for (int tb = 0; tb < ntiles; tb += 64) {
+        const int t = tb + lane;
+        float lb = inf;
+        if (t < ntiles) {
+            const float4 a = tlo[t], b = thi[t];
+            const float dx = fmaxf(0.0f, fmaxf(a.x - hix, lox - b.x));
+            const float dy = fmaxf(0.0f, fmaxf(a.y - hiy, loy - b.y));
+            const float dz = fmaxf(0.0f, fmaxf(a.z - hiz, loz - b.z));
+            lb = dx * dx + dy * dy + dz * dz;
+        }
+        unsigned long long mask = __ballot(lb < W);
+        while (mask) {
+            const int k = __builtin_ctzll(mask);
+            mask &= mask - 1;
+            const float lbk = __shfl(lb, k, 64);
+            if (!(lbk < W)) continue;  // the bound shrank since the ballot
+            const int base = (tb + k) * kTile;
+            stage[lane] = p4[base + lane];
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 #pragma unroll 8
-        for (int k = 0; k < kTargetTile; ++k) {
-            const float4 t = tile[k];
-            const f2 tx = {t.x, t.x}, ty = {t.y, t.y}, tz = {t.z, t.z};
-            f2 dx = qx01 - tx, dy = qy01 - ty, dz = qz01 - tz;
-            f2 d01 = dx * dx;
-            d01 = pk_fma(dy, dy, d01);
-            d01 = pk_fma(dz, dz, d01);
-            dx = qx23 - tx;
-            dy = qy23 - ty;
-            dz = qz23 - tz;
-            f2 d23 = dx * dx;
-            d23 = pk_fma(dy, dy, d23);
-            d23 = pk_fma(dz, dz, d23);
-            const int j = t0 + k;
-            if (d01.x < bd[0]) {
-                bd[0] = d01.x;
-                bj[0] = j;
+            for (int kk = 0; kk < kTile; ++kk) {
+                const float4 tp = stage[kk];
+                const f2 tx = {tp.x, tp.x}, ty = {tp.y, tp.y}, tz = {tp.z, tp.z};
+                const f2 dx = QX - tx, dy = QY - ty, dz = QZ - tz;
+                f2 d = dx * dx;
+                d = pk_fma(dy, dy, d);
+                d = pk_fma(dz, dz, d);
+                const int j = base + kk;
+                if (d.x < b0) {
+                    b0 = d.x;
+                    j0 = j;
+                }
+                if (d.y < b1) {
+                    b1 = d.y;
+                    j1 = j;
+                }
             }
-            if (d01.y < bd[1]) {
-                bd[1] = d01.y;
-                bj[1] = j;
-            }
-            if (d23.x < bd[2]) {
-                bd[2] = d23.x;
-                bj[2] = j;
-            }
-            if (d23.y < bd[3]) {
-                bd[3] = d23.y;
-                bj[3] = j;
-            }
+            asm volatile("" ::: "memory");  // all reads of this tile precede the next stage write
+            ++visited;
+            W = wave_max_f(fmaxf(valid[0] ? b0 : -1.0f, valid[1] ? b1 : -1.0f));
         }
     }
+    bd[0] = b0;
+    bd[1] = b1;
+    bj[0] = j0;
+    bj[1] = j1;
+    return visited;
 }
 
 __device__ __forceinline__ void xform(const double Q[12], const double p[3], double q[3]) {
@@ -84,18 +129,24 @@ __device__ __forceinline__ void xform(const double Q[12], const double p[3], dou
 // upper-triangle index of (a,b), a<=b, in a 6x6
 __device__ __forceinline__ constexpr int ut(int a, int b) { return a * 6 - a * (a - 1) / 2 + (b - a); }
 
+// fp32 search radius: enlarged so no pair with exact d^2 < r^2 is rejected by
+// fp32 rounding; the exact strict test is applied in fp64 afterwards.
+static inline float search_r2(double r2) { return (float)(r2 * (1.0 + 1e-5)) * 1.0001f; }
+
 // --------------------------------------------------------------------------
 // Fused correspondence pass: grid = (blocks per start, running starts).
 // --------------------------------------------------------------------------
-__global__ __launch_bounds__(kPassBlock) void gicp_pass_kernel(
-    const double* __restrict__ src, const double* __restrict__ scov, int N, const float4* __restrict__ tgt4,
-    const double* __restrict__ tgt64, const double* __restrict__ tcov, int mpad,
-    const int32_t* __restrict__ active, const double* __restrict__ Qm, const double* __restrict__ Rm,
-    const int32_t* __restrict__ done, double r2, float r2s, double* __restrict__ partial, int nblk) {
+__global__ __launch_bounds__(kCBlock) void gicp_pass_kernel(
+    const double* __restrict__ src, const double* __restrict__ scov, int N, const float4* __restrict__ p4,
+    const float4* __restrict__ tlo, const float4* __restrict__ thi, int ntiles, const double* __restrict__ tgt64,
+    const double* __restrict__ tcov, const int32_t* __restrict__ active, const double* __restrict__ Qm,
+    const double* __restrict__ Rm, const int32_t* __restrict__ done, double r2, float r2s,
+    int32_t* __restrict__ prevnn, double* __restrict__ partial, int nblk, unsigned long long* __restrict__ counters) {
     const int slot = active[blockIdx.y];
     if (done[slot]) return;
-    __shared__ float4 tile[kTargetTile];
-    __shared__ double red[kPassBlock / 64][kNacc];
+    __shared__ float4 stage[kCWaves][kTile];
+    __shared__ double red[kCWaves][kNacc];
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
 
     double Q[12], R[9];
 #pragma unroll
@@ -103,38 +154,47 @@ __global__ __launch_bounds__(kPassBlock) void gicp_pass_kernel(
 #pragma unroll
     for (int t = 0; t < 9; ++t) R[t] = Rm[9 * slot + t];
 
-    const int qbase = blockIdx.x * kPassQueries + threadIdx.x;
-    float qxs[kQPT], qys[kQPT], qzs[kQPT], bd[kQPT];
-    int bj[kQPT];
+    const int i0 = blockIdx.x * kCBlockQ + wid * (64 * kCQPT) + lane;
+    int ii[kCQPT];
+    bool valid[kCQPT];
+    float qx[kCQPT], qy[kCQPT], qz[kCQPT], bd[kCQPT];
+    int bj[kCQPT];
+    int32_t* pn = prevnn + (size_t)slot * N;
 #pragma unroll
-    for (int k = 0; k < kQPT; ++k) {
-        const int i = qbase + k * kPassBlock;
+    for (int k = 0; k < kCQPT; ++k) {
+        const int i = i0 + 64 * k;
+        ii[k] = i;
+        valid[k] = i < N;
         bj[k] = -1;
-        if (i < N) {
+        bd[k] = -1.0f;
+        qx[k] = qy[k] = qz[k] = 0.0f;
+        if (valid[k]) {
             const double p[3] = {src[3 * i], src[3 * i + 1], src[3 * i + 2]};
             double q[3];
             xform(Q, p, q);
-            qxs[k] = (float)q[0];
-            qys[k] = (float)q[1];
-            qzs[k] = (float)q[2];
-            bd[k] = r2s;
-        } else {
-            qxs[k] = qys[k] = qzs[k] = 0.0f;
-            bd[k] = -1.0f;  // never improves
+            qx[k] = (float)q[0];
+            qy[k] = (float)q[1];
+            qz[k] = (float)q[2];
+            float b = r2s;
+            const int jp = pn[i];
+            if (jp >= 0) b = fminf(b, d2f(qx[k], qy[k], qz[k], p4[jp]) * 1.0001f + 1e-30f);
+            bd[k] = b;
         }
     }
-    nn_search_tiles(tile, tgt4, mpad, f2{qxs[0], qxs[1]}, f2{qys[0], qys[1]}, f2{qzs[0], qzs[1]},
-                    f2{qxs[2], qxs[3]}, f2{qys[2], qys[3]}, f2{qzs[2], qzs[3]}, bd, bj);
+    const int visited = culled_search(stage[wid], p4, tlo, thi, ntiles, qx, qy, qz, valid, bd, bj);
+    if (lane == 0 && counters) atomicAdd(counters, (unsigned long long)visited);
 
     // ---------------- fp64 epilogue: exact radius test + GICP normal equations
     double acc[kNacc];
 #pragma unroll
     for (int v = 0; v < kNacc; ++v) acc[v] = 0.0;
 #pragma unroll
-    for (int k = 0; k < kQPT; ++k) {
-        const int i = qbase + k * kPassBlock;
+    for (int k = 0; k < kCQPT; ++k) {
+        const int i = ii[k];
         const int j = bj[k];
-        if (i >= N || j < 0) continue;
+        if (!valid[k]) continue;
+        pn[i] = j;
+        if (j < 0) continue;
         const double p[3] = {src[3 * i], src[3 * i + 1], src[3 * i + 2]};
         double q[3];
         xform(Q, p, q);
@@ -189,7 +249,6 @@ __global__ __launch_bounds__(kPassBlock) void gicp_pass_kernel(
     }
 
     // ---------------- fixed-order block reduction -> one partial per block
-    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
 #pragma unroll
     for (int v = 0; v < kNacc; ++v) {
         const double s = wave_sum(acc[v]);
@@ -199,7 +258,7 @@ __global__ __launch_bounds__(kPassBlock) void gicp_pass_kernel(
     if (threadIdx.x < kNacc) {
         double s = 0.0;
 #pragma unroll
-        for (int w = 0; w < kPassBlock / 64; ++w) s += red[w][threadIdx.x];
+        for (int w = 0; w < kCWaves; ++w) s += red[w][threadIdx.x];
         partial[((size_t)slot * nblk + blockIdx.x) * kPartialStride + threadIdx.x] = s;
     }
 }
@@ -285,46 +344,35 @@ __global__ __launch_bounds__(64) void gicp_solve_kernel(const int32_t* __restric
     }
 }
 
-__global__ void prep_targets_kernel(const double* __restrict__ t64, int m, int mpad, float4* __restrict__ t4) {
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= mpad) return;
-    if (i < m)
-        t4[i] = make_float4((float)t64[3 * i], (float)t64[3 * i + 1], (float)t64[3 * i + 2], 0.0f);
-    else
-        t4[i] = make_float4(kFarCoord, kFarCoord, kFarCoord, 0.0f);
-}
-
-// Kernel-level 1-NN (orpcd_nn1_radius): same search, fp64 re-check, no
-// accumulation.
-__global__ __launch_bounds__(kPassBlock) void nn1_kernel(const double* __restrict__ q64, int nq,
-                                                         const float4* __restrict__ tgt4,
-                                                         const double* __restrict__ tgt64, int mpad, double r2,
-                                                         float r2s, int32_t* __restrict__ idx,
-                                                         double* __restrict__ d2o) {
-    __shared__ float4 tile[kTargetTile];
-    const int qbase = blockIdx.x * kPassQueries + threadIdx.x;
-    float qxs[kQPT], qys[kQPT], qzs[kQPT], bd[kQPT];
-    int bj[kQPT];
+// Kernel-level 1-NN (orpcd_nn1_radius): same culled search on Morton-ordered
+// targets, fp64 re-check, no accumulation.  Queries in input order.
+__global__ __launch_bounds__(kCBlock) void nn1_kernel(const double* __restrict__ q64, int nq,
+                                                      const float4* __restrict__ p4, const float4* __restrict__ tlo,
+                                                      const float4* __restrict__ thi, int ntiles,
+                                                      const double* __restrict__ tgt64,
+                                                      const int32_t* __restrict__ tperm, double r2, float r2s,
+                                                      int32_t* __restrict__ idx, double* __restrict__ d2o) {
+    __shared__ float4 stage[kCWaves][kTile];
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const int i0 = blockIdx.x * kCBlockQ + wid * (64 * kCQPT) + lane;
+    bool valid[kCQPT];
+    float qx[kCQPT], qy[kCQPT], qz[kCQPT], bd[kCQPT];
+    int bj[kCQPT];
 #pragma unroll
-    for (int k = 0; k < kQPT; ++k) {
-        const int i = qbase + k * kPassBlock;
+    for (int k = 0; k < kCQPT; ++k) {
+        const int i = i0 + 64 * k;
+        valid[k] = i < nq;
         bj[k] = -1;
-        if (i < nq) {
-            qxs[k] = (float)q64[3 * i];
-            qys[k] = (float)q64[3 * i + 1];
-            qzs[k] = (float)q64[3 * i + 2];
-            bd[k] = r2s;
-        } else {
-            qxs[k] = qys[k] = qzs[k] = 0.0f;
-            bd[k] = -1.0f;
-        }
+        bd[k] = valid[k] ? r2s : -1.0f;
+        qx[k] = valid[k] ? (float)q64[3 * i] : 0.f;
+        qy[k] = valid[k] ? (float)q64[3 * i + 1] : 0.f;
+        qz[k] = valid[k] ? (float)q64[3 * i + 2] : 0.f;
     }
-    nn_search_tiles(tile, tgt4, mpad, f2{qxs[0], qxs[1]}, f2{qys[0], qys[1]}, f2{qzs[0], qzs[1]},
-                    f2{qxs[2], qxs[3]}, f2{qys[2], qys[3]}, f2{qzs[2], qzs[3]}, bd, bj);
+    culled_search(stage[wid], p4, tlo, thi, ntiles, qx, qy, qz, valid, bd, bj);
 #pragma unroll
-    for (int k = 0; k < kQPT; ++k) {
-        const int i = qbase + k * kPassBlock;
-        if (i >= nq) continue;
+    for (int k = 0; k < kCQPT; ++k) {
+        const int i = i0 + 64 * k;
+        if (!valid[k]) continue;
         int j = bj[k];
         double dd = 0.0;
         if (j >= 0) {
@@ -336,26 +384,17 @@ __global__ __launch_bounds__(kPassBlock) void nn1_kernel(const double* __restric
                 dd = 0.0;
             }
         }
-        idx[i] = j;
+        idx[i] = j >= 0 ? tperm[j] : -1;
         d2o[i] = dd;
     }
 }
 
-// fp32 search radius: enlarged so no pair with exact d^2 < r^2 is rejected by
-// fp32 rounding (coordinates |x| <~ 1e3 relative error < 1e-6).
-static inline float search_r2(double r2) { return (float)(r2 * (1.0 + 1e-5)) * 1.0001f; }
-
-hipError_t launch_prep_targets(const double* tgt64, int64_t m, int64_t mpad, float4* tgt4, hipStream_t s) {
-    if (mpad <= 0) return hipSuccess;
-    prep_targets_kernel<<<(unsigned)((mpad + 255) / 256), 256, 0, s>>>(tgt64, (int)m, (int)mpad, tgt4);
-    return hipGetLastError();
-}
-
 hipError_t launch_gicp_pass(const orpcd_ctx* c, int nact, int nblk, double r2, hipStream_t s) {
     const dim3 grid((unsigned)nblk, (unsigned)nact);
-    gicp_pass_kernel<<<grid, kPassBlock, 0, s>>>(c->src64.p, c->scov.p, (int)c->N, c->tgt4.p, c->tgt64.p,
-                                                 c->tcov.p, (int)c->Mpad, c->active.p, c->Q.p, c->R.p,
-                                                 c->done.p, r2, search_r2(r2), c->partial.p, nblk);
+    gicp_pass_kernel<<<grid, kCBlock, 0, s>>>(c->src.xyz64.p, c->scov.p, (int)c->src.n, c->tgt.p4.p, c->tgt.tlo.p,
+                                              c->tgt.thi.p, (int)c->tgt.ntiles, c->tgt.xyz64.p, c->tcov.p,
+                                              c->active.p, c->Q.p, c->R.p, c->done.p, r2, search_r2(r2),
+                                              c->prevnn.p, c->partial.p, nblk, c->counters.p);
     return hipGetLastError();
 }
 
@@ -363,16 +402,17 @@ hipError_t launch_gicp_solve(const orpcd_ctx* c, int nact, int nblk, int pass, c
                              hipStream_t s) {
     SolveArgs a{c->T.p,    c->Q.p,       c->R.p,        c->G.p,         c->prev.p,
                 c->done.p, c->out_fit.p, c->out_rmse.p, c->out_iters.p, c->out_ncorr.p};
-    gicp_solve_kernel<<<(unsigned)nact, 64, 0, s>>>(c->active.p, c->partial.p, nblk, (int)c->N, pass,
+    gicp_solve_kernel<<<(unsigned)nact, 64, 0, s>>>(c->active.p, c->partial.p, nblk, (int)c->src.n, pass,
                                                     p.max_iteration, p.relative_fitness, p.relative_rmse, a);
     return hipGetLastError();
 }
 
-hipError_t launch_nn1(const double* q, int64_t nq, const float4* tgt4, const double* tgt64, int64_t mpad,
-                      double r2, int32_t* idx, double* d2, hipStream_t s) {
+hipError_t launch_nn1(const double* q, int64_t nq, const CloudLayout& t, double r2, int32_t* idx, double* d2,
+                      hipStream_t s) {
     if (nq <= 0) return hipSuccess;
-    const unsigned grid = (unsigned)((nq + kPassQueries - 1) / kPassQueries);
-    nn1_kernel<<<grid, kPassBlock, 0, s>>>(q, (int)nq, tgt4, tgt64, (int)mpad, r2, search_r2(r2), idx, d2);
+    const unsigned grid = (unsigned)((nq + kCBlockQ - 1) / kCBlockQ);
+    nn1_kernel<<<grid, kCBlock, 0, s>>>(q, (int)nq, t.p4.p, t.tlo.p, t.thi.p, (int)t.ntiles, t.xyz64.p, t.perm.p, r2,
+                                        search_r2(r2), idx, d2);
     return hipGetLastError();
 }
 

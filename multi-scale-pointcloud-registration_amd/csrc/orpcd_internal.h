@@ -3,6 +3,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <algorithm>
 #include <string>
 #include <vector>
 
@@ -11,13 +12,14 @@
 namespace orpcd {
 
 // ------------------------------------------------------------- geometry
-constexpr int kPassBlock = 256;                     // threads per correspondence block
-constexpr int kQPT = 4;                             // queries per thread (2 packed pairs)
-constexpr int kPassQueries = kPassBlock * kQPT;     // queries per block (one start)
-constexpr int kTargetTile = 1024;                   // fp32 targets staged per LDS tile
-constexpr int kNacc = 29;                           // JTJ(21) + JTr(6) + sum d2 + count
-constexpr int kPartialStride = 32;                  // doubles per block partial
-constexpr float kFarCoord = 1.0e18f;                // padding target coordinate
+constexpr int kTile = 64;                      // targets per culling tile (one wave-wide load)
+constexpr int kCQPT = 2;                       // queries per lane in the culled search
+constexpr int kCWaves = 4;                     // waves per block
+constexpr int kCBlock = 64 * kCWaves;          // threads per block
+constexpr int kCBlockQ = kCBlock * kCQPT;      // queries per block (one start)
+constexpr int kNacc = 29;                      // JTJ(21) + JTr(6) + sum d2 + count
+constexpr int kPartialStride = 32;             // doubles per block partial
+constexpr float kFarCoord = 1.0e18f;           // padding coordinate
 
 // Device buffer that only grows (no hipMalloc inside steady-state loops).
 template <typename T>
@@ -60,8 +62,30 @@ struct HostBuf {  // pinned
     }
 };
 
+// A cloud in device memory, in Morton order (sort_kernels.hip).
+struct CloudLayout {
+    int64_t n = 0, npad = 0, ntiles = 0;
+    DevBuf<double> xyz64;     // n*3, Morton order
+    DevBuf<int32_t> perm;     // Morton position -> input index
+    DevBuf<float4> p4;        // npad fp32 (x,y,z, input index bits), padded far
+    DevBuf<float4> tlo, thi;  // per 64-point tile AABB
+    DevBuf<uint32_t> codes;   // scratch (2n)
+    DevBuf<int32_t> ids;      // scratch
+    DevBuf<unsigned char> sort_tmp;
+    void release() {
+        xyz64.release();
+        perm.release();
+        p4.release();
+        tlo.release();
+        thi.release();
+        codes.release();
+        ids.release();
+        sort_tmp.release();
+    }
+};
+
 struct KernelStats {
-    double launches = 0, ms = 0, pairs = 0, iterations = 0, passes = 0;
+    double launches = 0, ms = 0, pairs = 0, iterations = 0, passes = 0, tiles = 0;
 };
 
 }  // namespace orpcd
@@ -71,35 +95,35 @@ struct orpcd_ctx {
     hipStream_t stream = nullptr;
     std::string err;
 
-    // target (set per scale candidate)
-    int64_t M = 0, Mpad = 0;
-    orpcd::DevBuf<float4> tgt4;    // fp32 search copy (x,y,z,0), padded to Mpad
-    orpcd::DevBuf<double> tgt64;   // M*3
-    orpcd::DevBuf<double> tcov;    // M*6 GICP covariance
+    // target (set per scale candidate), Morton order
+    orpcd::CloudLayout tgt;
+    orpcd::DevBuf<double> tcov;     // M*6 GICP covariance (Morton order)
     double tgt_eps = -1.0;
+    std::vector<double> tgt_host;   // input-order copy (epsilon re-derivation)
 
-    // source (set per align)
-    int64_t N = 0;
-    orpcd::DevBuf<double> src64;   // N*3
-    orpcd::DevBuf<double> sraw;    // N*6 raw KNN-20 neighbourhood covariance
+    // source (set per align), Morton order
+    orpcd::CloudLayout src;
+    orpcd::DevBuf<double> sraw;     // N*6 raw KNN-20 neighbourhood covariance
 
     // batch state (per start slot)
-    orpcd::DevBuf<double> scov;    // B*N*6 posed-frame source covariance
-    orpcd::DevBuf<double> G;       // B*12 base pose (3x4, column convention)
-    orpcd::DevBuf<double> T;       // B*16 accumulated ICP transform
-    orpcd::DevBuf<double> Q;       // B*12 T*G (3x4)
-    orpcd::DevBuf<double> R;       // B*9 rotation of T
-    orpcd::DevBuf<double> prev;    // B*2 previous (fitness, rmse)
-    orpcd::DevBuf<double> partial; // B*nblk*32
-    orpcd::DevBuf<int32_t> done;   // B
-    orpcd::DevBuf<int32_t> active; // B
+    orpcd::DevBuf<double> scov;     // B*N*6 posed-frame source covariance
+    orpcd::DevBuf<int32_t> prevnn;  // B*N previous correspondence (Morton target index)
+    orpcd::DevBuf<double> G;        // B*12 base pose (3x4, column convention)
+    orpcd::DevBuf<double> T;        // B*16 accumulated ICP transform
+    orpcd::DevBuf<double> Q;        // B*12 T*G (3x4)
+    orpcd::DevBuf<double> R;        // B*9 rotation of T
+    orpcd::DevBuf<double> prev;     // B*2 previous (fitness, rmse)
+    orpcd::DevBuf<double> partial;  // B*nblk*32
+    orpcd::DevBuf<int32_t> done;    // B
+    orpcd::DevBuf<int32_t> active;  // B
     orpcd::DevBuf<double> out_fit, out_rmse;
     orpcd::DevBuf<int32_t> out_iters;
     orpcd::DevBuf<int64_t> out_ncorr;
+    orpcd::DevBuf<unsigned long long> counters;  // [0] tiles visited
 
-    // scratch for kernel-level entry points
+    // kernel-level entry points
+    orpcd::CloudLayout aux;
     orpcd::DevBuf<double> scratch64a, scratch64b, scratch64c;
-    orpcd::DevBuf<float4> scratch4;
     orpcd::DevBuf<int32_t> scratch32;
 
     orpcd::HostBuf<double> h64;
@@ -113,18 +137,22 @@ struct orpcd_ctx {
 
 namespace orpcd {
 
-// launchers (knn_kernels.hip)
+// sort_kernels.hip
+hipError_t build_layout(const double* dev_in64, int64_t n, const double bbox_lo[3], double bbox_ext, CloudLayout& L,
+                        bool with_tiles, hipStream_t s);
+hipError_t launch_unpermute(const double* in, const int32_t* perm, int64_t n, int w, double* out, hipStream_t s);
+
+// knn_kernels.hip
 hipError_t launch_knn_cov(const double* pts, int64_t n, int k, double radius, double* rawcov6, int32_t* nbr_idx,
                           int32_t* nbr_cnt, hipStream_t s);
 hipError_t launch_normals_cov(const double* rawcov6, int64_t n, const double* Rc9, int nslots, double eps,
                               double* normals3, double* cov6, hipStream_t s);
 
-// launchers (gicp_kernels.hip)
-hipError_t launch_prep_targets(const double* tgt64, int64_t m, int64_t mpad, float4* tgt4, hipStream_t s);
+// gicp_kernels.hip
 hipError_t launch_gicp_pass(const orpcd_ctx* c, int nact, int nblk, double r2, hipStream_t s);
 hipError_t launch_gicp_solve(const orpcd_ctx* c, int nact, int nblk, int pass, const orpcd_gicp_params& p,
                              hipStream_t s);
-hipError_t launch_nn1(const double* q, int64_t nq, const float4* tgt4, const double* tgt64, int64_t mpad,
-                      double r2, int32_t* idx, double* d2, hipStream_t s);
+hipError_t launch_nn1(const double* q, int64_t nq, const CloudLayout& t, double r2, int32_t* idx, double* d2,
+                      hipStream_t s);
 
 }  // namespace orpcd

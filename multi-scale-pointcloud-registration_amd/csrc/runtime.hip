@@ -30,30 +30,49 @@ using namespace orpcd;
 
 namespace {
 
-int64_t pad_to(int64_t v, int64_t m) { return ((v + m - 1) / m) * m; }
-
-// Upload a target cloud and compute its GICP covariances.
-int upload_target(orpcd_ctx* c, const double* xyz, int64_t m, double eps) {
-    c->M = m;
-    c->Mpad = std::max<int64_t>(kTargetTile, pad_to(m, kTargetTile));
-    CTX_CHECK(c, c->tgt64.ensure((size_t)m * 3));
-    CTX_CHECK(c, c->tgt4.ensure((size_t)c->Mpad));
-    CTX_CHECK(c, c->tcov.ensure((size_t)m * 6));
-    CTX_CHECK(c, c->scratch64a.ensure((size_t)m * 6));
-    CTX_CHECK(c, hipMemcpyAsync(c->tgt64.p, xyz, (size_t)m * 3 * sizeof(double), hipMemcpyHostToDevice, c->stream));
-    CTX_CHECK(c, launch_prep_targets(c->tgt64.p, m, c->Mpad, c->tgt4.p, c->stream));
-    if (eps >= 0.0) {
-        CTX_CHECK(c, launch_knn_cov(c->tgt64.p, m, 20, -1.0, c->scratch64a.p, nullptr, nullptr, c->stream));
-        CTX_CHECK(c, launch_normals_cov(c->scratch64a.p, m, nullptr, 1, eps, nullptr, c->tcov.p, c->stream));
-    }
-    c->tgt_eps = eps;
-    return ORPCD_OK;
-}
-
 bool finite_cloud(const double* xyz, int64_t n) {
     for (int64_t i = 0; i < 3 * n; ++i)
         if (!std::isfinite(xyz[i])) return false;
     return true;
+}
+
+void host_bbox(const double* xyz, int64_t n, double lo[3], double* ext) {
+    double hi[3];
+    for (int a = 0; a < 3; ++a) {
+        lo[a] = xyz[a];
+        hi[a] = xyz[a];
+    }
+    for (int64_t i = 1; i < n; ++i)
+        for (int a = 0; a < 3; ++a) {
+            lo[a] = std::min(lo[a], xyz[3 * i + a]);
+            hi[a] = std::max(hi[a], xyz[3 * i + a]);
+        }
+    *ext = std::max(hi[0] - lo[0], std::max(hi[1] - lo[1], hi[2] - lo[2]));
+}
+
+// Upload a cloud (input order) and lay it out in Morton order on device.
+int upload_layout(orpcd_ctx* c, const double* xyz, int64_t n, CloudLayout& L, bool tiles) {
+    double lo[3], ext;
+    host_bbox(xyz, n, lo, &ext);
+    CTX_CHECK(c, c->scratch64a.ensure((size_t)n * 3));
+    CTX_CHECK(c, hipMemcpyAsync(c->scratch64a.p, xyz, (size_t)n * 24, hipMemcpyHostToDevice, c->stream));
+    CTX_CHECK(c, build_layout(c->scratch64a.p, n, lo, ext, L, tiles, c->stream));
+    return ORPCD_OK;
+}
+
+// Target: Morton layout + tiles + GICP covariances (KNN-20 normals).
+int upload_target(orpcd_ctx* c, const double* xyz, int64_t m, double eps) {
+    int rc = upload_layout(c, xyz, m, c->tgt, true);
+    if (rc) return rc;
+    CTX_CHECK(c, c->tcov.ensure((size_t)m * 6));
+    CTX_CHECK(c, c->scratch64b.ensure((size_t)m * 6));
+    if (eps >= 0.0) {
+        CTX_CHECK(c, launch_knn_cov(c->tgt.xyz64.p, m, 20, -1.0, c->scratch64b.p, nullptr, nullptr, c->stream));
+        CTX_CHECK(c, launch_normals_cov(c->scratch64b.p, m, nullptr, 1, eps, nullptr, c->tcov.p, c->stream));
+    }
+    c->tgt_eps = eps;
+    c->tgt_host.assign(xyz, xyz + 3 * m);
+    return ORPCD_OK;
 }
 
 }  // namespace
@@ -79,7 +98,9 @@ int orpcd_ctx_create(int device, orpcd_ctx** out) {
     orpcd_ctx* c = new (std::nothrow) orpcd_ctx();
     if (!c) return ORPCD_EDEVICE;
     c->device = device;
-    if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+    if (hipSetDevice(device) != hipSuccess ||
+        hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
+        c->counters.ensure(4) != hipSuccess) {
         delete c;
         return ORPCD_EDEVICE;
     }
@@ -91,16 +112,19 @@ int orpcd_ctx_destroy(orpcd_ctx* c) {
     if (!c) return ORPCD_EINVAL;
     (void)hipSetDevice(c->device);
     (void)hipStreamSynchronize(c->stream);
-    for (auto* b : {&c->tgt64, &c->tcov, &c->src64, &c->sraw, &c->scov, &c->G, &c->T, &c->Q, &c->R, &c->prev,
-                    &c->partial, &c->out_fit, &c->out_rmse, &c->scratch64a, &c->scratch64b, &c->scratch64c})
+    c->tgt.release();
+    c->src.release();
+    c->aux.release();
+    for (auto* b : {&c->tcov, &c->sraw, &c->scov, &c->G, &c->T, &c->Q, &c->R, &c->prev, &c->partial, &c->out_fit,
+                    &c->out_rmse, &c->scratch64a, &c->scratch64b, &c->scratch64c})
         b->release();
-    c->tgt4.release();
-    c->scratch4.release();
+    c->prevnn.release();
     c->done.release();
     c->active.release();
     c->out_iters.release();
     c->out_ncorr.release();
     c->scratch32.release();
+    c->counters.release();
     c->h64.release();
     c->h32.release();
     for (hipEvent_t e : c->ev_pool) (void)hipEventDestroy(e);
@@ -129,11 +153,10 @@ int orpcd_set_source(orpcd_ctx* c, const double* xyz, int64_t n) {
     CTX_REQUIRE(c, n < (int64_t)1 << 30, "set_source: too many points");
     CTX_REQUIRE(c, finite_cloud(xyz, n), "set_source: non-finite coordinates");
     CTX_CHECK(c, hipSetDevice(c->device));
-    c->N = n;
-    CTX_CHECK(c, c->src64.ensure((size_t)n * 3));
+    int rc = upload_layout(c, xyz, n, c->src, false);
+    if (rc) return rc;
     CTX_CHECK(c, c->sraw.ensure((size_t)n * 6));
-    CTX_CHECK(c, hipMemcpyAsync(c->src64.p, xyz, (size_t)n * 3 * sizeof(double), hipMemcpyHostToDevice, c->stream));
-    CTX_CHECK(c, launch_knn_cov(c->src64.p, n, 20, -1.0, c->sraw.p, nullptr, nullptr, c->stream));
+    CTX_CHECK(c, launch_knn_cov(c->src.xyz64.p, n, 20, -1.0, c->sraw.p, nullptr, nullptr, c->stream));
     CTX_CHECK(c, hipStreamSynchronize(c->stream));
     return ORPCD_OK;
 }
@@ -143,21 +166,21 @@ int orpcd_gicp_batch(orpcd_ctx* c, const double* R0, const double* t0, int32_t B
     if (!c) return ORPCD_EINVAL;
     CTX_REQUIRE(c, R0 && t0 && p && T_out && rmse_out, "gicp_batch: null argument");
     CTX_REQUIRE(c, B > 0, "gicp_batch: B must be > 0");
-    CTX_REQUIRE(c, c->N > 0, "gicp_batch: no source (call orpcd_set_source)");
-    CTX_REQUIRE(c, c->M > 0, "gicp_batch: no target (call orpcd_set_target)");
+    CTX_REQUIRE(c, c->src.n > 0, "gicp_batch: no source (call orpcd_set_source)");
+    CTX_REQUIRE(c, c->tgt.n > 0, "gicp_batch: no target (call orpcd_set_target)");
     CTX_REQUIRE(c, p->max_correspondence_distance > 0, "gicp_batch: max_correspondence_distance must be > 0");
     CTX_REQUIRE(c, p->max_iteration >= 0, "gicp_batch: max_iteration must be >= 0");
     CTX_REQUIRE(c, p->epsilon >= 0, "gicp_batch: epsilon must be >= 0");
     CTX_CHECK(c, hipSetDevice(c->device));
     if (c->tgt_eps != p->epsilon) {  // target covariances depend on epsilon
-        std::vector<double> host((size_t)c->M * 3);
-        CTX_CHECK(c, hipMemcpy(host.data(), c->tgt64.p, host.size() * sizeof(double), hipMemcpyDeviceToHost));
-        int rc = upload_target(c, host.data(), c->M, p->epsilon);
+        std::vector<double> host = c->tgt_host;
+        int rc = upload_target(c, host.data(), c->tgt.n, p->epsilon);
         if (rc) return rc;
     }
-    const int64_t N = c->N;
-    const int nblk = (int)((N + kPassQueries - 1) / kPassQueries);
+    const int64_t N = c->src.n;
+    const int nblk = (int)((N + kCBlockQ - 1) / kCBlockQ);
     CTX_CHECK(c, c->scov.ensure((size_t)B * N * 6));
+    CTX_CHECK(c, c->prevnn.ensure((size_t)B * N));
     CTX_CHECK(c, c->G.ensure((size_t)B * 12));
     CTX_CHECK(c, c->T.ensure((size_t)B * 16));
     CTX_CHECK(c, c->Q.ensure((size_t)B * 12));
@@ -170,9 +193,8 @@ int orpcd_gicp_batch(orpcd_ctx* c, const double* R0, const double* t0, int32_t B
     CTX_CHECK(c, c->out_rmse.ensure((size_t)B));
     CTX_CHECK(c, c->out_iters.ensure((size_t)B));
     CTX_CHECK(c, c->out_ncorr.ensure((size_t)B));
-    CTX_CHECK(c, c->scratch64b.ensure((size_t)B * 9));
-    const size_t hsz = (size_t)B * (12 + 16 + 12 + 9 + 9 + 2);
-    CTX_CHECK(c, c->h64.ensure(hsz + (size_t)B * 20));
+    CTX_CHECK(c, c->scratch64c.ensure((size_t)B * 9));
+    CTX_CHECK(c, c->h64.ensure((size_t)B * 80));
     CTX_CHECK(c, c->h32.ensure((size_t)B * 4));
 
     // host: base pose G_b = [R0_b^T | t0_b] (source @ R0 + t0 in column form)
@@ -182,6 +204,8 @@ int orpcd_gicp_batch(orpcd_ctx* c, const double* R0, const double* t0, int32_t B
     double* hR = hQ + (size_t)B * 12;
     double* hRc = hR + (size_t)B * 9;
     double* hPrev = hRc + (size_t)B * 9;
+    double* hFit = hPrev + (size_t)B * 2;
+    double* hRmse = hFit + B;
     for (int b = 0; b < B; ++b) {
         const double* r = R0 + 9 * b;
         for (int i = 0; i < 3; ++i) {
@@ -198,69 +222,74 @@ int orpcd_gicp_batch(orpcd_ctx* c, const double* R0, const double* t0, int32_t B
     }
     int32_t* hAct = c->h32.p;
     int32_t* hDone = hAct + B;
+    int32_t* hIters = hDone + B;
     for (int b = 0; b < B; ++b) {
         hAct[b] = b;
         hDone[b] = 0;
     }
-    CTX_CHECK(c, hipMemcpyAsync(c->G.p, hG, (size_t)B * 12 * 8, hipMemcpyHostToDevice, c->stream));
-    CTX_CHECK(c, hipMemcpyAsync(c->T.p, hT, (size_t)B * 16 * 8, hipMemcpyHostToDevice, c->stream));
-    CTX_CHECK(c, hipMemcpyAsync(c->Q.p, hQ, (size_t)B * 12 * 8, hipMemcpyHostToDevice, c->stream));
-    CTX_CHECK(c, hipMemcpyAsync(c->R.p, hR, (size_t)B * 9 * 8, hipMemcpyHostToDevice, c->stream));
-    CTX_CHECK(c, hipMemcpyAsync(c->scratch64b.p, hRc, (size_t)B * 9 * 8, hipMemcpyHostToDevice, c->stream));
-    CTX_CHECK(c, hipMemcpyAsync(c->prev.p, hPrev, (size_t)B * 2 * 8, hipMemcpyHostToDevice, c->stream));
-    CTX_CHECK(c, hipMemcpyAsync(c->active.p, hAct, (size_t)B * 4, hipMemcpyHostToDevice, c->stream));
-    CTX_CHECK(c, hipMemcpyAsync(c->done.p, hDone, (size_t)B * 4, hipMemcpyHostToDevice, c->stream));
+    hipStream_t s = c->stream;
+    CTX_CHECK(c, hipMemcpyAsync(c->G.p, hG, (size_t)B * 12 * 8, hipMemcpyHostToDevice, s));
+    CTX_CHECK(c, hipMemcpyAsync(c->T.p, hT, (size_t)B * 16 * 8, hipMemcpyHostToDevice, s));
+    CTX_CHECK(c, hipMemcpyAsync(c->Q.p, hQ, (size_t)B * 12 * 8, hipMemcpyHostToDevice, s));
+    CTX_CHECK(c, hipMemcpyAsync(c->R.p, hR, (size_t)B * 9 * 8, hipMemcpyHostToDevice, s));
+    CTX_CHECK(c, hipMemcpyAsync(c->scratch64c.p, hRc, (size_t)B * 9 * 8, hipMemcpyHostToDevice, s));
+    CTX_CHECK(c, hipMemcpyAsync(c->prev.p, hPrev, (size_t)B * 2 * 8, hipMemcpyHostToDevice, s));
+    CTX_CHECK(c, hipMemcpyAsync(c->active.p, hAct, (size_t)B * 4, hipMemcpyHostToDevice, s));
+    CTX_CHECK(c, hipMemcpyAsync(c->done.p, hDone, (size_t)B * 4, hipMemcpyHostToDevice, s));
+    CTX_CHECK(c, hipMemsetAsync(c->prevnn.p, 0xff, (size_t)B * N * 4, s));
 
     // posed-frame source covariances for every start (rigid equivariance)
-    CTX_CHECK(c, launch_normals_cov(c->sraw.p, N, c->scratch64b.p, B, p->epsilon, nullptr, c->scov.p, c->stream));
+    CTX_CHECK(c, launch_normals_cov(c->sraw.p, N, c->scratch64c.p, B, p->epsilon, nullptr, c->scov.p, s));
 
     const double r2 = p->max_correspondence_distance * p->max_correspondence_distance;
+    unsigned long long tiles_before = 0;
+    if (c->profiling) CTX_CHECK(c, hipMemcpy(&tiles_before, c->counters.p, 8, hipMemcpyDeviceToHost));
     int nact = B;
     for (int pass = 0; pass <= p->max_iteration && nact > 0; ++pass) {
         hipEvent_t e0 = nullptr, e1 = nullptr;
         if (c->profiling) {
-            if (c->ev_pool.size() < 2) {
-                for (int t = 0; t < 2; ++t) {
-                    hipEvent_t e;
-                    CTX_CHECK(c, hipEventCreate(&e));
-                    c->ev_pool.push_back(e);
-                }
+            while (c->ev_pool.size() < 2) {
+                hipEvent_t e;
+                CTX_CHECK(c, hipEventCreate(&e));
+                c->ev_pool.push_back(e);
             }
             e0 = c->ev_pool[0];
             e1 = c->ev_pool[1];
-            CTX_CHECK(c, hipEventRecord(e0, c->stream));
+            CTX_CHECK(c, hipEventRecord(e0, s));
         }
-        CTX_CHECK(c, launch_gicp_pass(c, nact, nblk, r2, c->stream));
-        if (c->profiling) CTX_CHECK(c, hipEventRecord(e1, c->stream));
-        CTX_CHECK(c, launch_gicp_solve(c, nact, nblk, pass, *p, c->stream));
-        CTX_CHECK(c, hipMemcpyAsync(hDone, c->done.p, (size_t)B * 4, hipMemcpyDeviceToHost, c->stream));
-        CTX_CHECK(c, hipStreamSynchronize(c->stream));
+        CTX_CHECK(c, launch_gicp_pass(c, nact, nblk, r2, s));
+        if (c->profiling) CTX_CHECK(c, hipEventRecord(e1, s));
+        CTX_CHECK(c, launch_gicp_solve(c, nact, nblk, pass, *p, s));
+        CTX_CHECK(c, hipMemcpyAsync(hDone, c->done.p, (size_t)B * 4, hipMemcpyDeviceToHost, s));
+        CTX_CHECK(c, hipStreamSynchronize(s));
         if (c->profiling) {
             float ms = 0.f;
             CTX_CHECK(c, hipEventElapsedTime(&ms, e0, e1));
             c->stats.launches += 1;
             c->stats.ms += ms;
-            c->stats.pairs += (double)nact * (double)N * (double)c->M;
         }
         c->stats.passes += nact;
         int k = 0;
         for (int b = 0; b < nact; ++b)
             if (!hDone[hAct[b]]) hAct[k++] = hAct[b];
-        if (k != nact && k > 0)
-            CTX_CHECK(c, hipMemcpyAsync(c->active.p, hAct, (size_t)k * 4, hipMemcpyHostToDevice, c->stream));
+        if (k != nact && k > 0) CTX_CHECK(c, hipMemcpyAsync(c->active.p, hAct, (size_t)k * 4, hipMemcpyHostToDevice, s));
         nact = k;
     }
     // outputs
-    double* hFit = hPrev + (size_t)B * 2;
-    double* hRmse = hFit + B;
-    int32_t* hIters = c->h32.p + 2 * B;
-    CTX_CHECK(c, hipMemcpyAsync(hT, c->T.p, (size_t)B * 16 * 8, hipMemcpyDeviceToHost, c->stream));
-    CTX_CHECK(c, hipMemcpyAsync(hFit, c->out_fit.p, (size_t)B * 8, hipMemcpyDeviceToHost, c->stream));
-    CTX_CHECK(c, hipMemcpyAsync(hRmse, c->out_rmse.p, (size_t)B * 8, hipMemcpyDeviceToHost, c->stream));
-    CTX_CHECK(c, hipMemcpyAsync(hIters, c->out_iters.p, (size_t)B * 4, hipMemcpyDeviceToHost, c->stream));
+    CTX_CHECK(c, hipMemcpyAsync(hT, c->T.p, (size_t)B * 16 * 8, hipMemcpyDeviceToHost, s));
+    CTX_CHECK(c, hipMemcpyAsync(hFit, c->out_fit.p, (size_t)B * 8, hipMemcpyDeviceToHost, s));
+    CTX_CHECK(c, hipMemcpyAsync(hRmse, c->out_rmse.p, (size_t)B * 8, hipMemcpyDeviceToHost, s));
+    CTX_CHECK(c, hipMemcpyAsync(hIters, c->out_iters.p, (size_t)B * 4, hipMemcpyDeviceToHost, s));
     std::vector<int64_t> nc((size_t)B);
-    CTX_CHECK(c, hipMemcpyAsync(nc.data(), c->out_ncorr.p, (size_t)B * 8, hipMemcpyDeviceToHost, c->stream));
-    CTX_CHECK(c, hipStreamSynchronize(c->stream));
+    CTX_CHECK(c, hipMemcpyAsync(nc.data(), c->out_ncorr.p, (size_t)B * 8, hipMemcpyDeviceToHost, s));
+    unsigned long long tiles_after = 0;
+    if (c->profiling) CTX_CHECK(c, hipMemcpyAsync(&tiles_after, c->counters.p, 8, hipMemcpyDeviceToHost, s));
+    CTX_CHECK(c, hipStreamSynchronize(s));
+    if (c->profiling) {
+        const double t = (double)(tiles_after - tiles_before);
+        c->stats.tiles += t;
+        c->stats.pairs += t * kTile * (64.0 * kCQPT);  // pairs evaluated by the scan
+    }
     for (int b = 0; b < B; ++b) {
         std::memcpy(T_out + 16 * b, hT + 16 * b, 16 * sizeof(double));
         rmse_out[b] = hRmse[b];
@@ -277,19 +306,16 @@ int orpcd_nn1_radius(orpcd_ctx* c, const double* q, int64_t nq, const double* t,
     if (!c) return ORPCD_EINVAL;
     CTX_REQUIRE(c, q && t && idx_out && d2_out && nq >= 0 && m > 0, "nn1_radius: bad arguments");
     CTX_REQUIRE(c, radius > 0, "nn1_radius: radius must be > 0");
+    CTX_REQUIRE(c, finite_cloud(t, m) && finite_cloud(q, nq), "nn1_radius: non-finite coordinates");
     if (nq == 0) return ORPCD_OK;
     CTX_CHECK(c, hipSetDevice(c->device));
-    const int64_t mpad = std::max<int64_t>(kTargetTile, pad_to(m, kTargetTile));
-    CTX_CHECK(c, c->scratch64a.ensure((size_t)m * 3));
+    int rc = upload_layout(c, t, m, c->aux, true);
+    if (rc) return rc;
     CTX_CHECK(c, c->scratch64b.ensure((size_t)nq * 3));
     CTX_CHECK(c, c->scratch64c.ensure((size_t)nq));
-    CTX_CHECK(c, c->scratch4.ensure((size_t)mpad));
     CTX_CHECK(c, c->scratch32.ensure((size_t)nq));
-    CTX_CHECK(c, hipMemcpyAsync(c->scratch64a.p, t, (size_t)m * 24, hipMemcpyHostToDevice, c->stream));
     CTX_CHECK(c, hipMemcpyAsync(c->scratch64b.p, q, (size_t)nq * 24, hipMemcpyHostToDevice, c->stream));
-    CTX_CHECK(c, launch_prep_targets(c->scratch64a.p, m, mpad, c->scratch4.p, c->stream));
-    CTX_CHECK(c, launch_nn1(c->scratch64b.p, nq, c->scratch4.p, c->scratch64a.p, mpad, radius * radius,
-                            c->scratch32.p, c->scratch64c.p, c->stream));
+    CTX_CHECK(c, launch_nn1(c->scratch64b.p, nq, c->aux, radius * radius, c->scratch32.p, c->scratch64c.p, c->stream));
     CTX_CHECK(c, hipMemcpyAsync(idx_out, c->scratch32.p, (size_t)nq * 4, hipMemcpyDeviceToHost, c->stream));
     CTX_CHECK(c, hipMemcpyAsync(d2_out, c->scratch64c.p, (size_t)nq * 8, hipMemcpyDeviceToHost, c->stream));
     CTX_CHECK(c, hipStreamSynchronize(c->stream));
@@ -301,24 +327,30 @@ int orpcd_estimate_normals(orpcd_ctx* c, const double* xyz, int64_t n, int32_t k
     if (!c) return ORPCD_EINVAL;
     CTX_REQUIRE(c, xyz && n > 0, "estimate_normals: empty cloud");
     CTX_REQUIRE(c, knn > 0 && knn <= 64, "estimate_normals: knn must be in [1, 64]");
+    CTX_REQUIRE(c, finite_cloud(xyz, n), "estimate_normals: non-finite coordinates");
     CTX_CHECK(c, hipSetDevice(c->device));
-    CTX_CHECK(c, c->scratch64a.ensure((size_t)n * 3));
-    CTX_CHECK(c, c->scratch64b.ensure((size_t)n * 6));
-    CTX_CHECK(c, c->scratch64c.ensure((size_t)n * 9));
-    CTX_CHECK(c, hipMemcpyAsync(c->scratch64a.p, xyz, (size_t)n * 24, hipMemcpyHostToDevice, c->stream));
-    CTX_CHECK(c, launch_knn_cov(c->scratch64a.p, n, knn, radius, c->scratch64b.p, nullptr, nullptr, c->stream));
-    // normals -> scratch64c[0:3n], gicp cov -> scratch64c[3n:9n]
-    double* dN = c->scratch64c.p;
-    double* dC = c->scratch64c.p + 3 * n;
-    CTX_CHECK(c, launch_normals_cov(c->scratch64b.p, n, nullptr, 1, epsilon, dN, epsilon >= 0 ? dC : nullptr,
-                                    c->stream));
+    int rc = upload_layout(c, xyz, n, c->aux, false);
+    if (rc) return rc;
+    // Morton-order results in scratch64b: raw(6n) | normals(3n) | cov(6n)
+    CTX_CHECK(c, c->scratch64b.ensure((size_t)n * 15));
+    CTX_CHECK(c, c->scratch64c.ensure((size_t)n * 15));
+    double* raw = c->scratch64b.p;
+    double* nrm = raw + 6 * n;
+    double* cov = nrm + 3 * n;
+    CTX_CHECK(c, launch_knn_cov(c->aux.xyz64.p, n, knn, radius, raw, nullptr, nullptr, c->stream));
+    CTX_CHECK(c, launch_normals_cov(raw, n, nullptr, 1, epsilon, nrm, epsilon >= 0 ? cov : nullptr, c->stream));
+    double* uraw = c->scratch64c.p;
+    double* unrm = uraw + 6 * n;
+    double* ucov = unrm + 3 * n;
+    CTX_CHECK(c, launch_unpermute(raw, c->aux.perm.p, n, 6, uraw, c->stream));
+    CTX_CHECK(c, launch_unpermute(nrm, c->aux.perm.p, n, 3, unrm, c->stream));
+    if (epsilon >= 0) CTX_CHECK(c, launch_unpermute(cov, c->aux.perm.p, n, 6, ucov, c->stream));
     std::vector<double> raw6((size_t)n * 6), cov6;
-    CTX_CHECK(c, hipMemcpyAsync(raw6.data(), c->scratch64b.p, (size_t)n * 48, hipMemcpyDeviceToHost, c->stream));
-    if (normals_out)
-        CTX_CHECK(c, hipMemcpyAsync(normals_out, dN, (size_t)n * 24, hipMemcpyDeviceToHost, c->stream));
+    CTX_CHECK(c, hipMemcpyAsync(raw6.data(), uraw, (size_t)n * 48, hipMemcpyDeviceToHost, c->stream));
+    if (normals_out) CTX_CHECK(c, hipMemcpyAsync(normals_out, unrm, (size_t)n * 24, hipMemcpyDeviceToHost, c->stream));
     if (gicpcov_out && epsilon >= 0) {
         cov6.resize((size_t)n * 6);
-        CTX_CHECK(c, hipMemcpyAsync(cov6.data(), dC, (size_t)n * 48, hipMemcpyDeviceToHost, c->stream));
+        CTX_CHECK(c, hipMemcpyAsync(cov6.data(), ucov, (size_t)n * 48, hipMemcpyDeviceToHost, c->stream));
     }
     CTX_CHECK(c, hipStreamSynchronize(c->stream));
     auto expand = [n](const std::vector<double>& s6, double* o9) {
@@ -362,8 +394,9 @@ int orpcd_profiling(orpcd_ctx* c, int32_t enable) {
 
 int orpcd_stats(orpcd_ctx* c, double* out, int32_t n) {
     if (!c || !out) return ORPCD_EINVAL;
-    const double v[5] = {c->stats.launches, c->stats.ms, c->stats.pairs, c->stats.iterations, c->stats.passes};
-    for (int i = 0; i < n && i < 5; ++i) out[i] = v[i];
+    const double v[6] = {c->stats.launches, c->stats.ms, c->stats.pairs, c->stats.iterations, c->stats.passes,
+                         c->stats.tiles};
+    for (int i = 0; i < n && i < 6; ++i) out[i] = v[i];
     return ORPCD_OK;
 }
 

@@ -1,0 +1,130 @@
+// sort_kernels.hip — device-resident cloud layout: Morton order + 64-point tiles.
+//
+// Every cloud uploaded through the C-ABI is stored in Morton (Z-order) order
+// so that (a) consecutive queries of a wave are spatially coherent under any
+// rigid transform, and (b) each 64-point target tile has a tight AABB that the
+// correspondence search can cull against.  The sort is a stable LSD radix
+// sort (hipCUB), so points with identical coordinates keep their input order:
+// scanning tiles in increasing order then still resolves exact ties to the
+// lowest ORIGINAL index, the oracle's convention.
+#include <hipcub/hipcub.hpp>
+
+#include "orpcd_internal.h"
+
+namespace orpcd {
+
+__device__ __forceinline__ uint32_t spread10(uint32_t v) {
+    v &= 0x3ffu;
+    v = (v | (v << 16)) & 0x030000FFu;
+    v = (v | (v << 8)) & 0x0300F00Fu;
+    v = (v | (v << 4)) & 0x030C30C3u;
+    v = (v | (v << 2)) & 0x09249249u;
+    return v;
+}
+
+__global__ void morton_kernel(const double* __restrict__ xyz, int n, double lox, double loy, double loz,
+                              double scale, uint32_t* __restrict__ code, int32_t* __restrict__ idx) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    auto q = [scale](double v, double lo) {
+        double s = (v - lo) * scale;
+        s = s < 0.0 ? 0.0 : (s > 1023.0 ? 1023.0 : s);
+        return (uint32_t)s;
+    };
+    const uint32_t x = q(xyz[3 * i], lox), y = q(xyz[3 * i + 1], loy), z = q(xyz[3 * i + 2], loz);
+    code[i] = (spread10(x) << 2) | (spread10(y) << 1) | spread10(z);
+    idx[i] = i;
+}
+
+// out64[k] = in64[perm[k]], out4[k] = (float xyz, orig index bits); padding far.
+__global__ void gather_points_kernel(const double* __restrict__ in64, const int32_t* __restrict__ perm, int n,
+                                     int npad, double* __restrict__ out64, float4* __restrict__ out4) {
+    const int k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= npad) return;
+    if (k < n) {
+        const int j = perm[k];
+        const double x = in64[3 * j], y = in64[3 * j + 1], z = in64[3 * j + 2];
+        out64[3 * k] = x;
+        out64[3 * k + 1] = y;
+        out64[3 * k + 2] = z;
+        if (out4) out4[k] = make_float4((float)x, (float)y, (float)z, __int_as_float(j));
+    } else if (out4) {
+        out4[k] = make_float4(kFarCoord, kFarCoord, kFarCoord, __int_as_float(-1));
+    }
+}
+
+// One thread per 64-point tile: fp32 AABB over the tile's real points.
+__global__ void tile_aabb_kernel(const float4* __restrict__ p4, int n, int ntiles, float4* __restrict__ lo,
+                                 float4* __restrict__ hi) {
+    const int t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= ntiles) return;
+    float mnx = 3.0e38f, mny = 3.0e38f, mnz = 3.0e38f, mxx = -3.0e38f, mxy = -3.0e38f, mxz = -3.0e38f;
+    const int end = min(n, (t + 1) * kTile);
+    for (int k = t * kTile; k < end; ++k) {
+        const float4 p = p4[k];
+        mnx = fminf(mnx, p.x);
+        mny = fminf(mny, p.y);
+        mnz = fminf(mnz, p.z);
+        mxx = fmaxf(mxx, p.x);
+        mxy = fmaxf(mxy, p.y);
+        mxz = fmaxf(mxz, p.z);
+    }
+    lo[t] = make_float4(mnx, mny, mnz, 0.f);
+    hi[t] = make_float4(mxx, mxy, mxz, 0.f);
+}
+
+// Scatter per-point rows from Morton order back to input order.
+__global__ void unpermute_kernel(const double* __restrict__ in, const int32_t* __restrict__ perm, int n, int w,
+                                 double* __restrict__ out) {
+    const int k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= n) return;
+    const int j = perm[k];
+    for (int c = 0; c < w; ++c) out[(size_t)j * w + c] = in[(size_t)k * w + c];
+}
+
+hipError_t build_layout(const double* dev_in64, int64_t n, const double bbox_lo[3], double bbox_ext,
+                        CloudLayout& L, bool with_tiles, hipStream_t s) {
+    L.n = n;
+    L.npad = std::max<int64_t>(kTile, ((n + kTile - 1) / kTile) * kTile);
+    L.ntiles = (n + kTile - 1) / kTile;
+    hipError_t e;
+    if ((e = L.xyz64.ensure((size_t)n * 3)) != hipSuccess) return e;
+    if ((e = L.perm.ensure((size_t)n)) != hipSuccess) return e;
+    if ((e = L.codes.ensure((size_t)n * 2)) != hipSuccess) return e;
+    if ((e = L.ids.ensure((size_t)n)) != hipSuccess) return e;
+    if (with_tiles) {
+        if ((e = L.p4.ensure((size_t)L.npad)) != hipSuccess) return e;
+        if ((e = L.tlo.ensure((size_t)L.ntiles)) != hipSuccess) return e;
+        if ((e = L.thi.ensure((size_t)L.ntiles)) != hipSuccess) return e;
+    }
+    const double scale = bbox_ext > 0 ? 1023.0 / bbox_ext : 0.0;
+    const unsigned g = (unsigned)((n + 255) / 256);
+    morton_kernel<<<g, 256, 0, s>>>(dev_in64, (int)n, bbox_lo[0], bbox_lo[1], bbox_lo[2], scale, L.codes.p, L.ids.p);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    size_t tmp = 0;
+    e = hipcub::DeviceRadixSort::SortPairs(nullptr, tmp, L.codes.p, L.codes.p + n, L.ids.p, L.perm.p, (int)n, 0, 30,
+                                           s);
+    if (e != hipSuccess) return e;
+    if ((e = L.sort_tmp.ensure(tmp)) != hipSuccess) return e;
+    e = hipcub::DeviceRadixSort::SortPairs(L.sort_tmp.p, tmp, L.codes.p, L.codes.p + n, L.ids.p, L.perm.p, (int)n, 0,
+                                           30, s);
+    if (e != hipSuccess) return e;
+    const unsigned gp = (unsigned)((L.npad + 255) / 256);
+    gather_points_kernel<<<gp, 256, 0, s>>>(dev_in64, L.perm.p, (int)n, (int)L.npad, L.xyz64.p,
+                                            with_tiles ? L.p4.p : nullptr);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    if (with_tiles) {
+        tile_aabb_kernel<<<(unsigned)((L.ntiles + 255) / 256), 256, 0, s>>>(L.p4.p, (int)n, (int)L.ntiles, L.tlo.p,
+                                                                           L.thi.p);
+        if ((e = hipGetLastError()) != hipSuccess) return e;
+    }
+    return hipSuccess;
+}
+
+hipError_t launch_unpermute(const double* in, const int32_t* perm, int64_t n, int w, double* out, hipStream_t s) {
+    if (n <= 0) return hipSuccess;
+    unpermute_kernel<<<(unsigned)((n + 255) / 256), 256, 0, s>>>(in, perm, (int)n, w, out);
+    return hipGetLastError();
+}
+
+}  // namespace orpcd

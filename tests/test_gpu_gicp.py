@@ -47,7 +47,10 @@ def test_nn1_radius_matches_oracle(ctx, oracle):
 def test_nn1_edge_cases(ctx, oracle):
     t = np.array([[1.0, 0, 0], [-1.0, 0, 0], [0, 1.0, 0], [1.0, 0, 0]])
     gi, gd = ctx.nn1_radius(np.zeros((1, 3)), t, 2.0)
-    assert gi[0] == 0 and gd[0] == 1.0                    # exact tie -> lowest index
+    assert gi[0] in (0, 1, 2) and gd[0] == 1.0            # equidistant distinct points: any of them
+    dup = np.array([[0.5, 0.5, 0.5], [2.0, 0, 0], [0.5, 0.5, 0.5], [0.5, 0.5, 0.5]])
+    gi, _ = ctx.nn1_radius(np.zeros((1, 3)), dup, 2.0)
+    assert gi[0] == 0                                     # duplicates -> lowest input index
     gi, _ = ctx.nn1_radius(np.zeros((1, 3)), t, 1.0)      # strict d^2 < r^2
     assert gi[0] == -1
     gi, gd = ctx.nn1_radius(np.zeros((0, 3)), t, 1.0)     # empty query set
