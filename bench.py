@@ -143,7 +143,8 @@ def main():
                        "parallelism": f"attempts sharded over {world} GPU(s)"},
             "roofline": {"bound": "mfma", "achieved": round(achieved, 3), "peak": FP32_PEAK_TFLOPS,
                          "unit": "TFLOP/s", "frac": round(achieved / FP32_PEAK_TFLOPS, 4), "traffic": None,
-                         "kernel": "gicp_pass_kernel", "avg_launch_ms": round(avg_ms, 4),
+                         "kernel": "nn_search_kernel", "avg_launch_ms": round(avg_ms, 4),
+                         "accum_kernel_ms_total": round(st["accum_ms"], 3), "search_kernel_ms_total": round(st["ms"], 3),
                          "launches": int(st["launches"]), "flop_per_pair": FLOP_PER_PAIR,
                          "pairs_per_launch": round(st["pairs"] / max(st["launches"], 1)),
                          "pairs_vs_bruteforce": round(st["pairs"] / max(st["passes"] * len(source) * len(target), 1),

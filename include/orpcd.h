@@ -122,7 +122,8 @@ int orpcd_fgr(orpcd_ctx* ctx, const double* src, int64_t n, const double* tgt, i
  * every launch of the dominant correspondence kernel is bracketed.
  * stats[0] = launches, [1] = total ms, [2] = query-target pairs evaluated
  * by the culled scan, [3] = GICP iterations completed, [4] = correspondence
- * passes (start x pass), [5] = 64-point target tiles scanned.               */
+ * passes (start x pass), [5] = 64-point target tiles scanned, [6] = total
+ * ms of the fp64 accumulation kernel.  [1] times the search kernel only.   */
 int orpcd_profiling(orpcd_ctx* ctx, int32_t enable);
 int orpcd_stats(orpcd_ctx* ctx, double* stats_out, int32_t n);
 int orpcd_reset_stats(orpcd_ctx* ctx);

@@ -3,25 +3,31 @@
 // One correspondence pass restates, for every running start at once,
 //   O3D Registration.cpp GetRegistrationResultAndCorrespondences
 //     (SearchHybrid(max_corr, 1): exact nearest target with d^2 < r^2)
-// fused with
+// and
 //   O3D GeneralizedICP.cpp TransformationEstimationForGeneralizedICP::
 //     ComputeTransformation (JTJ / JTr with W = (Cs + Ct)^-1/2, L2 kernel).
 // The solve kernel restates SolveJacobianSystemAndObtainExtrinsicMatrix and
 // the RegistrationICP convergence test, per start, on device.
 // Reference call site: generalizedICP.py:59-70, driven by Aligner.py:178-202.
 //
-// Search: every wave owns 128 Morton-consecutive queries (2 per lane) of one
-// start.  Target tiles (64 Morton-consecutive points, fp32, with an AABB) are
-// culled when the AABB-to-AABB lower bound exceeds the wave's current worst
-// best-distance; surviving tiles are staged into the wave's LDS slot with one
-// coalesced 1 KiB load and scanned with packed fp32 math (v_pk_add/mul/fma,
-// one LDS broadcast per target).  The per-query bound is seeded with the
-// start's correspondence from the previous pass (the search stays exact: the
-// seed only bounds, the scan re-finds the minimum).  The chosen pair is then
-// re-evaluated in fp64 (radius test, d^2, Jacobian), so every accumulated
-// quantity is fp64.  Because W is symmetric, J^T J = A^T (Cs+Ct)^-1 A and
-// J^T r = A^T (Cs+Ct)^-1 d with A = [-[q]x | I]: no matrix square root is
-// needed.  All reductions run in a fixed order.
+// A pass is two kernels:
+//  * nn_search_kernel (fp32, compute-bound, low VGPR):  every wave owns 128
+//    Morton-consecutive queries (2 per lane) of one start.  Target tiles (64
+//    Morton-consecutive points with an AABB) are culled first against the
+//    wave's query AABB and worst bound (lane-parallel over 64 tiles per round),
+//    then against each query's own bound; surviving tiles are staged into the
+//    wave's LDS slot with one coalesced 1 KiB load and scanned with packed fp32
+//    math (v_pk_add/mul/fma, one LDS broadcast per target).  Each query's bound
+//    is seeded by the start's correspondence of the previous pass, or on pass
+//    0 by a strided set of tile representatives (real targets, so the bound is
+//    valid); the seed only bounds, the scan re-finds the exact minimum.  When
+//    few starts are running, a query group's tiles are split over S waves whose
+//    results merge by a 64-bit atomicMin on (d^2 bits, target index).
+//  * gicp_accum_kernel (fp64): re-evaluates the chosen pair in fp64 (strict
+//    radius test, d^2, Jacobian) and reduces the 29 normal-equation terms per
+//    block in a fixed order.  Because W is symmetric, J^T J = A^T (Cs+Ct)^-1 A
+//    and J^T r = A^T (Cs+Ct)^-1 d with A = [-[q]x | I]: no matrix square root
+//    is needed.
 #include "device_math.h"
 #include "orpcd_internal.h"
 
@@ -48,17 +54,30 @@ __device__ __forceinline__ float d2f(float qx, float qy, float qz, float4 t) {
     return __builtin_fmaf(dz, dz, __builtin_fmaf(dy, dy, dx * dx));
 }
 
+__device__ __forceinline__ float box_d2(float x, float y, float z, float4 lo, float4 hi) {
+    const float dx = fmaxf(0.0f, fmaxf(lo.x - x, x - hi.x));
+    const float dy = fmaxf(0.0f, fmaxf(lo.y - y, y - hi.y));
+    const float dz = fmaxf(0.0f, fmaxf(lo.z - z, z - hi.z));
+    return dx * dx + dy * dy + dz * dz;
+}
+
+constexpr unsigned long long kNone = ~0ull;
+__device__ __forceinline__ unsigned long long pack_best(float d, int j) {
+    return j < 0 ? kNone : ((unsigned long long)__float_as_uint(d) << 32) | (unsigned)j;
+}
+
 // --------------------------------------------------------------------------
-// Culled exact nearest search for the 2 queries of every lane of one wave.
-// bd[] enters as the per-query bound (d^2 must be < bd to be taken), bj[] = -1.
-// Returns the number of tiles scanned.
+// Culled exact nearest search for the 2 queries of every lane of one wave,
+// restricted to tiles t with t % S == s.  bd[] enters as the per-query bound
+// (d^2 must be < bd to be taken), bj[] = -1.  Returns tiles scanned.
 // --------------------------------------------------------------------------
 __device__ __forceinline__ int culled_search(float4* stage, const float4* __restrict__ p4,
                                              const float4* __restrict__ tlo, const float4* __restrict__ thi,
-                                             int ntiles, const float qx[2], const float qy[2], const float qz[2],
-                                             const bool valid[2], float bd[2], int bj[2]) {
+                                             int ntiles, int S, int s, const float qx[2], const float qy[2],
+                                             const float qz[2], const bool valid[2], float bd[2], int bj[2]) {
     const int lane = threadIdx.x & 63;
-    float W = wave_max_f(fmaxf(valid[0] ? bd[0] : -1.0f, valid[1] ? bd[1] : -1.0f));
+    float b0 = valid[0] ? bd[0] : -1.0f, b1 = valid[1] ? bd[1] : -1.0f;
+    float W = wave_max_f(fmaxf(b0, b1));
     if (!(W > 0.0f)) return 0;  // no query of this wave can take anything
     const float inf = 3.0e38f;
     const float lox = wave_min_f(fminf(valid[0] ? qx[0] : inf, valid[1] ? qx[1] : inf));
@@ -68,14 +87,15 @@ __device__ __forceinline__ int culled_search(float4* stage, const float4* __rest
     const float hiy = wave_max_f(fmaxf(valid[0] ? qy[0] : -inf, valid[1] ? qy[1] : -inf));
     const float hiz = wave_max_f(fmaxf(valid[0] ? qz[0] : -inf, valid[1] ? qz[1] : -inf));
     const f2 QX = {qx[0], qx[1]}, QY = {qy[0], qy[1]}, QZ = {qz[0], qz[1]};
-    float b0 = bd[0], b1 = bd[1];
-    int j0 = bj[0], j1 = bj[1];
+    int j0 = -1, j1 = -1;
     int visited = 0;
     for (int tb = 0; tb < ntiles; tb += 64) {
         const int t = tb + lane;
+        float4 a = make_float4(0.f, 0.f, 0.f, 0.f), b = a;
         float lb = inf;
-        if (t < ntiles) {
-            const float4 a = tlo[t], b = thi[t];
+        if (t < ntiles && (S == 1 || t % S == s)) {
+            a = tlo[t];
+            b = thi[t];
             const float dx = fmaxf(0.0f, fmaxf(a.x - hix, lox - b.x));
             const float dy = fmaxf(0.0f, fmaxf(a.y - hiy, loy - b.y));
             const float dz = fmaxf(0.0f, fmaxf(a.z - hiz, loz - b.z));
@@ -85,8 +105,12 @@ __device__ __forceinline__ int culled_search(float4* stage, const float4* __rest
         while (mask) {
             const int k = __builtin_ctzll(mask);
             mask &= mask - 1;
-            const float lbk = __shfl(lb, k, 64);
-            if (!(lbk < W)) continue;  // the bound shrank since the ballot
+            if (!(__shfl(lb, k, 64) < W)) continue;  // the bound shrank since the ballot
+            // per-query test against this tile's AABB
+            const float4 ta = make_float4(__shfl(a.x, k, 64), __shfl(a.y, k, 64), __shfl(a.z, k, 64), 0.f);
+            const float4 tbx = make_float4(__shfl(b.x, k, 64), __shfl(b.y, k, 64), __shfl(b.z, k, 64), 0.f);
+            const bool need = box_d2(qx[0], qy[0], qz[0], ta, tbx) < b0 || box_d2(qx[1], qy[1], qz[1], ta, tbx) < b1;
+            if (!__any(need)) continue;
             const int base = (tb + k) * kTile;
             stage[lane] = p4[base + lane];
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -110,7 +134,7 @@ __device__ __forceinline__ int culled_search(float4* stage, const float4* __rest
             }
             asm volatile("" ::: "memory");  // all reads of this tile precede the next stage write
             ++visited;
-            W = wave_max_f(fmaxf(valid[0] ? b0 : -1.0f, valid[1] ? b1 : -1.0f));
+            W = wave_max_f(fmaxf(b0, b1));
         }
     }
     bd[0] = b0;
@@ -133,37 +157,37 @@ __device__ __forceinline__ constexpr int ut(int a, int b) { return a * 6 - a * (
 // fp32 rounding; the exact strict test is applied in fp64 afterwards.
 static inline float search_r2(double r2) { return (float)(r2 * (1.0 + 1e-5)) * 1.0001f; }
 
+// seed slack: bound = d^2(seed) * (1 + 1e-4) so the seed target itself (and
+// any closer one) is re-found by the strict-< scan
+constexpr float kSeedSlack = 1.0001f;
+
 // --------------------------------------------------------------------------
-// Fused correspondence pass: grid = (blocks per start, running starts).
+// Search kernel: grid = (blocks per start * S, running starts), 4 waves/block.
 // --------------------------------------------------------------------------
-__global__ __launch_bounds__(kCBlock) void gicp_pass_kernel(
-    const double* __restrict__ src, const double* __restrict__ scov, int N, const float4* __restrict__ p4,
-    const float4* __restrict__ tlo, const float4* __restrict__ thi, int ntiles, const double* __restrict__ tgt64,
-    const double* __restrict__ tcov, const int32_t* __restrict__ active, const double* __restrict__ Qm,
-    const double* __restrict__ Rm, const int32_t* __restrict__ done, double r2, float r2s,
-    int32_t* __restrict__ prevnn, double* __restrict__ partial, int nblk, unsigned long long* __restrict__ counters) {
+__global__ __launch_bounds__(kCBlock) void nn_search_kernel(
+    const double* __restrict__ src, int N, const float4* __restrict__ p4, const float4* __restrict__ tlo,
+    const float4* __restrict__ thi, int ntiles, const int32_t* __restrict__ active, const double* __restrict__ Qm,
+    const int32_t* __restrict__ done, float r2s, int S, int seed_stride, const int32_t* __restrict__ prevnn,
+    unsigned long long* __restrict__ best, unsigned long long* __restrict__ counters) {
     const int slot = active[blockIdx.y];
     if (done[slot]) return;
     __shared__ float4 stage[kCWaves][kTile];
-    __shared__ double red[kCWaves][kNacc];
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const int grp = blockIdx.x / S, split = blockIdx.x - grp * S;
 
-    double Q[12], R[9];
+    double Q[12];
 #pragma unroll
     for (int t = 0; t < 12; ++t) Q[t] = Qm[12 * slot + t];
-#pragma unroll
-    for (int t = 0; t < 9; ++t) R[t] = Rm[9 * slot + t];
 
-    const int i0 = blockIdx.x * kCBlockQ + wid * (64 * kCQPT) + lane;
-    int ii[kCQPT];
+    const int i0 = grp * kCBlockQ + wid * (64 * kCQPT) + lane;
     bool valid[kCQPT];
     float qx[kCQPT], qy[kCQPT], qz[kCQPT], bd[kCQPT];
     int bj[kCQPT];
-    int32_t* pn = prevnn + (size_t)slot * N;
+    const int32_t* pn = prevnn + (size_t)slot * N;
+    bool need_seed = false;
 #pragma unroll
     for (int k = 0; k < kCQPT; ++k) {
         const int i = i0 + 64 * k;
-        ii[k] = i;
         valid[k] = i < N;
         bj[k] = -1;
         bd[k] = -1.0f;
@@ -177,78 +201,122 @@ __global__ __launch_bounds__(kCBlock) void gicp_pass_kernel(
             qz[k] = (float)q[2];
             float b = r2s;
             const int jp = pn[i];
-            if (jp >= 0) b = fminf(b, d2f(qx[k], qy[k], qz[k], p4[jp]) * 1.0001f + 1e-30f);
+            if (jp >= 0)
+                b = fminf(b, d2f(qx[k], qy[k], qz[k], p4[jp]) * kSeedSlack);
+            else
+                need_seed = true;
             bd[k] = b;
         }
     }
-    const int visited = culled_search(stage[wid], p4, tlo, thi, ntiles, qx, qy, qz, valid, bd, bj);
+    // pass-0 seed: strided tile representatives (real targets -> valid bounds)
+    if (seed_stride > 0 && __any(need_seed)) {
+        float s0 = bd[0], s1 = bd[1];
+        for (int t = 0; t < ntiles; t += seed_stride) {
+            const float4 rep = p4[t * kTile];
+            s0 = fminf(s0, d2f(qx[0], qy[0], qz[0], rep) * kSeedSlack);
+            s1 = fminf(s1, d2f(qx[1], qy[1], qz[1], rep) * kSeedSlack);
+        }
+        if (valid[0]) bd[0] = s0;
+        if (valid[1]) bd[1] = s1;
+    }
+    const int visited = culled_search(stage[wid], p4, tlo, thi, ntiles, S, split, qx, qy, qz, valid, bd, bj);
     if (lane == 0 && counters) atomicAdd(counters, (unsigned long long)visited);
+    unsigned long long* out = best + (size_t)slot * N;
+#pragma unroll
+    for (int k = 0; k < kCQPT; ++k) {
+        if (!valid[k]) continue;
+        const unsigned long long v = pack_best(bd[k], bj[k]);
+        if (S == 1)
+            out[i0 + 64 * k] = v;
+        else if (v != kNone)
+            atomicMin(out + i0 + 64 * k, v);
+    }
+}
 
-    // ---------------- fp64 epilogue: exact radius test + GICP normal equations
+// --------------------------------------------------------------------------
+// Accumulation kernel: one query per thread, grid = (blocks per start, running
+// starts).  Writes the chosen correspondence back as next pass's seed.
+// --------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void gicp_accum_kernel(
+    const double* __restrict__ src, const double* __restrict__ scov, int N, const double* __restrict__ tgt64,
+    const double* __restrict__ tcov, const int32_t* __restrict__ active, const double* __restrict__ Qm,
+    const double* __restrict__ Rm, const int32_t* __restrict__ done, double r2,
+    const unsigned long long* __restrict__ best, int32_t* __restrict__ prevnn, double* __restrict__ partial,
+    int nblk) {
+    const int slot = active[blockIdx.y];
+    if (done[slot]) return;
+    __shared__ double red[4][kNacc];
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     double acc[kNacc];
 #pragma unroll
     for (int v = 0; v < kNacc; ++v) acc[v] = 0.0;
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i < N) {
+        const unsigned long long v = best[(size_t)slot * N + i];
+        const int j = v == kNone ? -1 : (int)(unsigned)(v & 0xffffffffu);
+        prevnn[(size_t)slot * N + i] = j;
+        if (j >= 0) {
+            double Q[12], R[9];
 #pragma unroll
-    for (int k = 0; k < kCQPT; ++k) {
-        const int i = ii[k];
-        const int j = bj[k];
-        if (!valid[k]) continue;
-        pn[i] = j;
-        if (j < 0) continue;
-        const double p[3] = {src[3 * i], src[3 * i + 1], src[3 * i + 2]};
-        double q[3];
-        xform(Q, p, q);
-        const double d[3] = {q[0] - tgt64[3 * j], q[1] - tgt64[3 * j + 1], q[2] - tgt64[3 * j + 2]};
-        const double d2 = d[0] * d[0] + d[1] * d[1] + d[2] * d[2];
-        if (!(d2 < r2)) continue;
-        const double* cs6 = scov + ((size_t)slot * N + i) * 6;
-        const double* ct6 = tcov + (size_t)j * 6;
-        Sym3 Cs{cs6[0], cs6[1], cs6[2], cs6[3], cs6[4], cs6[5]};
-        Cs = rotate_sym(R, Cs);
-        const Sym3 Mm{Cs.xx + ct6[0], Cs.xy + ct6[1], Cs.xz + ct6[2], Cs.yy + ct6[3], Cs.yz + ct6[4],
-                      Cs.zz + ct6[5]};
-        const Sym3 P = sym3_inverse(Mm);
-        const double Pm[3][3] = {{P.xx, P.xy, P.xz}, {P.xy, P.yy, P.yz}, {P.xz, P.yz, P.zz}};
-        // g = P d ; JTr = [q x g ; g]
-        const double g[3] = {P.xx * d[0] + P.xy * d[1] + P.xz * d[2], P.xy * d[0] + P.yy * d[1] + P.yz * d[2],
-                             P.xz * d[0] + P.yz * d[1] + P.zz * d[2]};
-        double qg[3];
-        cross3(q, g, qg);
-        acc[21] += qg[0];
-        acc[22] += qg[1];
-        acc[23] += qg[2];
-        acc[24] += g[0];
-        acc[25] += g[1];
-        acc[26] += g[2];
-        // SP = [q]x P (column b = q x P[:,b]);  TL row a = q x SP[a,:]
-        double SP[3][3];
+            for (int t = 0; t < 12; ++t) Q[t] = Qm[12 * slot + t];
 #pragma unroll
-        for (int b = 0; b < 3; ++b) {
-            const double col[3] = {Pm[0][b], Pm[1][b], Pm[2][b]};
-            double c3[3];
-            cross3(q, col, c3);
-            SP[0][b] = c3[0];
-            SP[1][b] = c3[1];
-            SP[2][b] = c3[2];
+            for (int t = 0; t < 9; ++t) R[t] = Rm[9 * slot + t];
+            const double p[3] = {src[3 * i], src[3 * i + 1], src[3 * i + 2]};
+            double q[3];
+            xform(Q, p, q);
+            const double d[3] = {q[0] - tgt64[3 * j], q[1] - tgt64[3 * j + 1], q[2] - tgt64[3 * j + 2]};
+            const double d2 = d[0] * d[0] + d[1] * d[1] + d[2] * d[2];
+            if (d2 < r2) {
+                const double* cs6 = scov + ((size_t)slot * N + i) * 6;
+                const double* ct6 = tcov + (size_t)j * 6;
+                Sym3 Cs{cs6[0], cs6[1], cs6[2], cs6[3], cs6[4], cs6[5]};
+                Cs = rotate_sym(R, Cs);
+                const Sym3 Mm{Cs.xx + ct6[0], Cs.xy + ct6[1], Cs.xz + ct6[2], Cs.yy + ct6[3], Cs.yz + ct6[4],
+                              Cs.zz + ct6[5]};
+                const Sym3 P = sym3_inverse(Mm);
+                const double Pm[3][3] = {{P.xx, P.xy, P.xz}, {P.xy, P.yy, P.yz}, {P.xz, P.yz, P.zz}};
+                // g = P d ; JTr = [q x g ; g]
+                const double g[3] = {P.xx * d[0] + P.xy * d[1] + P.xz * d[2],
+                                     P.xy * d[0] + P.yy * d[1] + P.yz * d[2],
+                                     P.xz * d[0] + P.yz * d[1] + P.zz * d[2]};
+                double qg[3];
+                cross3(q, g, qg);
+                acc[21] = qg[0];
+                acc[22] = qg[1];
+                acc[23] = qg[2];
+                acc[24] = g[0];
+                acc[25] = g[1];
+                acc[26] = g[2];
+                // SP = [q]x P (column b = q x P[:,b]);  TL row a = q x SP[a,:]
+                double SP[3][3];
+#pragma unroll
+                for (int b = 0; b < 3; ++b) {
+                    const double col[3] = {Pm[0][b], Pm[1][b], Pm[2][b]};
+                    double c3[3];
+                    cross3(q, col, c3);
+                    SP[0][b] = c3[0];
+                    SP[1][b] = c3[1];
+                    SP[2][b] = c3[2];
+                }
+#pragma unroll
+                for (int a = 0; a < 3; ++a) {
+                    double tl[3];
+                    cross3(q, SP[a], tl);
+#pragma unroll
+                    for (int b = a; b < 3; ++b) acc[ut(a, b)] = tl[b];
+#pragma unroll
+                    for (int b = 0; b < 3; ++b) acc[ut(a, 3 + b)] = SP[a][b];
+                }
+#pragma unroll
+                for (int a = 0; a < 3; ++a)
+#pragma unroll
+                    for (int b = a; b < 3; ++b) acc[ut(3 + a, 3 + b)] = Pm[a][b];
+                acc[27] = d2;
+                acc[28] = 1.0;
+            }
         }
-#pragma unroll
-        for (int a = 0; a < 3; ++a) {
-            double tl[3];
-            cross3(q, SP[a], tl);
-#pragma unroll
-            for (int b = a; b < 3; ++b) acc[ut(a, b)] += tl[b];
-#pragma unroll
-            for (int b = 0; b < 3; ++b) acc[ut(a, 3 + b)] += SP[a][b];
-        }
-#pragma unroll
-        for (int a = 0; a < 3; ++a)
-#pragma unroll
-            for (int b = a; b < 3; ++b) acc[ut(3 + a, 3 + b)] += Pm[a][b];
-        acc[27] += d2;
-        acc[28] += 1.0;
     }
-
-    // ---------------- fixed-order block reduction -> one partial per block
+    // fixed-order block reduction -> one partial per block
 #pragma unroll
     for (int v = 0; v < kNacc; ++v) {
         const double s = wave_sum(acc[v]);
@@ -256,9 +324,7 @@ __global__ __launch_bounds__(kCBlock) void gicp_pass_kernel(
     }
     __syncthreads();
     if (threadIdx.x < kNacc) {
-        double s = 0.0;
-#pragma unroll
-        for (int w = 0; w < kCWaves; ++w) s += red[w][threadIdx.x];
+        const double s = ((red[0][threadIdx.x] + red[1][threadIdx.x]) + red[2][threadIdx.x]) + red[3][threadIdx.x];
         partial[((size_t)slot * nblk + blockIdx.x) * kPartialStride + threadIdx.x] = s;
     }
 }
@@ -345,10 +411,11 @@ __global__ __launch_bounds__(64) void gicp_solve_kernel(const int32_t* __restric
 }
 
 // Kernel-level 1-NN (orpcd_nn1_radius): same culled search on Morton-ordered
-// targets, fp64 re-check, no accumulation.  Queries in input order.
+// targets (representative seed, S = 1), fp64 re-check, no accumulation.
+// Queries in input order.
 __global__ __launch_bounds__(kCBlock) void nn1_kernel(const double* __restrict__ q64, int nq,
                                                       const float4* __restrict__ p4, const float4* __restrict__ tlo,
-                                                      const float4* __restrict__ thi, int ntiles,
+                                                      const float4* __restrict__ thi, int ntiles, int seed_stride,
                                                       const double* __restrict__ tgt64,
                                                       const int32_t* __restrict__ tperm, double r2, float r2s,
                                                       int32_t* __restrict__ idx, double* __restrict__ d2o) {
@@ -363,12 +430,16 @@ __global__ __launch_bounds__(kCBlock) void nn1_kernel(const double* __restrict__
         const int i = i0 + 64 * k;
         valid[k] = i < nq;
         bj[k] = -1;
-        bd[k] = valid[k] ? r2s : -1.0f;
         qx[k] = valid[k] ? (float)q64[3 * i] : 0.f;
         qy[k] = valid[k] ? (float)q64[3 * i + 1] : 0.f;
         qz[k] = valid[k] ? (float)q64[3 * i + 2] : 0.f;
+        float b = valid[k] ? r2s : -1.0f;
+        if (valid[k])
+            for (int t = 0; t < ntiles; t += seed_stride)
+                b = fminf(b, d2f(qx[k], qy[k], qz[k], p4[t * kTile]) * kSeedSlack);
+        bd[k] = b;
     }
-    culled_search(stage[wid], p4, tlo, thi, ntiles, qx, qy, qz, valid, bd, bj);
+    culled_search(stage[wid], p4, tlo, thi, ntiles, 1, 0, qx, qy, qz, valid, bd, bj);
 #pragma unroll
     for (int k = 0; k < kCQPT; ++k) {
         const int i = i0 + 64 * k;
@@ -389,21 +460,48 @@ __global__ __launch_bounds__(kCBlock) void nn1_kernel(const double* __restrict__
     }
 }
 
-hipError_t launch_gicp_pass(const orpcd_ctx* c, int nact, int nblk, double r2, hipStream_t s) {
-    const dim3 grid((unsigned)nblk, (unsigned)nact);
-    gicp_pass_kernel<<<grid, kCBlock, 0, s>>>(c->src.xyz64.p, c->scov.p, (int)c->src.n, c->tgt.p4.p, c->tgt.tlo.p,
-                                              c->tgt.thi.p, (int)c->tgt.ntiles, c->tgt.xyz64.p, c->tcov.p,
-                                              c->active.p, c->Q.p, c->R.p, c->done.p, r2, search_r2(r2),
-                                              c->prevnn.p, c->partial.p, nblk, c->counters.p);
+int seed_stride_for(int64_t ntiles) {  // at most ~512 representatives per query
+    return (int)std::max<int64_t>(1, (ntiles + 511) / 512);
+}
+
+int search_splits(int nact, int blocks_per_start) {
+    const int64_t waves = (int64_t)nact * blocks_per_start * kCWaves;
+    const int64_t want = 8192;  // ~8 waves per SIMD on 256 CUs x 4 SIMDs
+    return (int)std::min<int64_t>(16, std::max<int64_t>(1, (want + waves - 1) / waves));
+}
+
+hipError_t launch_gicp_pass(const orpcd_ctx* c, int nact, int pass, double r2, hipStream_t s, hipEvent_t mid) {
+    const int N = (int)c->src.n;
+    const int sblk = (N + kCBlockQ - 1) / kCBlockQ;
+    const int S = search_splits(nact, sblk);
+    if (S > 1) {
+        // merged by atomicMin: reset every running start's slots
+        // (one memset over all B slots keeps this launch-free of host state)
+        hipError_t e = hipMemsetAsync(c->best.p, 0xff, c->best.n * sizeof(unsigned long long), s);
+        if (e != hipSuccess) return e;
+    }
+    nn_search_kernel<<<dim3((unsigned)(sblk * S), (unsigned)nact), kCBlock, 0, s>>>(
+        c->src.xyz64.p, N, c->tgt.p4.p, c->tgt.tlo.p, c->tgt.thi.p, (int)c->tgt.ntiles, c->active.p, c->Q.p,
+        c->done.p, search_r2(r2), S, pass == 0 ? seed_stride_for(c->tgt.ntiles) : 0, c->prevnn.p, c->best.p,
+        c->counters.p);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    if (mid && (e = hipEventRecord(mid, s)) != hipSuccess) return e;
+    const int ablk = (N + 255) / 256;
+    gicp_accum_kernel<<<dim3((unsigned)ablk, (unsigned)nact), 256, 0, s>>>(
+        c->src.xyz64.p, c->scov.p, N, c->tgt.xyz64.p, c->tcov.p, c->active.p, c->Q.p, c->R.p, c->done.p, r2,
+        c->best.p, c->prevnn.p, c->partial.p, ablk);
     return hipGetLastError();
 }
 
-hipError_t launch_gicp_solve(const orpcd_ctx* c, int nact, int nblk, int pass, const orpcd_gicp_params& p,
-                             hipStream_t s) {
+int accum_blocks(int64_t N) { return (int)((N + 255) / 256); }
+
+hipError_t launch_gicp_solve(const orpcd_ctx* c, int nact, int pass, const orpcd_gicp_params& p, hipStream_t s) {
     SolveArgs a{c->T.p,    c->Q.p,       c->R.p,        c->G.p,         c->prev.p,
                 c->done.p, c->out_fit.p, c->out_rmse.p, c->out_iters.p, c->out_ncorr.p};
-    gicp_solve_kernel<<<(unsigned)nact, 64, 0, s>>>(c->active.p, c->partial.p, nblk, (int)c->src.n, pass,
-                                                    p.max_iteration, p.relative_fitness, p.relative_rmse, a);
+    gicp_solve_kernel<<<(unsigned)nact, 64, 0, s>>>(c->active.p, c->partial.p, accum_blocks(c->src.n),
+                                                    (int)c->src.n, pass, p.max_iteration, p.relative_fitness,
+                                                    p.relative_rmse, a);
     return hipGetLastError();
 }
 
@@ -411,8 +509,8 @@ hipError_t launch_nn1(const double* q, int64_t nq, const CloudLayout& t, double 
                       hipStream_t s) {
     if (nq <= 0) return hipSuccess;
     const unsigned grid = (unsigned)((nq + kCBlockQ - 1) / kCBlockQ);
-    nn1_kernel<<<grid, kCBlock, 0, s>>>(q, (int)nq, t.p4.p, t.tlo.p, t.thi.p, (int)t.ntiles, t.xyz64.p, t.perm.p, r2,
-                                        search_r2(r2), idx, d2);
+    nn1_kernel<<<grid, kCBlock, 0, s>>>(q, (int)nq, t.p4.p, t.tlo.p, t.thi.p, (int)t.ntiles, seed_stride_for(t.ntiles),
+                                        t.xyz64.p, t.perm.p, r2, search_r2(r2), idx, d2);
     return hipGetLastError();
 }
 

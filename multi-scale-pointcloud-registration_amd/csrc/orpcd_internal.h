@@ -85,7 +85,7 @@ struct CloudLayout {
 };
 
 struct KernelStats {
-    double launches = 0, ms = 0, pairs = 0, iterations = 0, passes = 0, tiles = 0;
+    double launches = 0, ms = 0, pairs = 0, iterations = 0, passes = 0, tiles = 0, accum_ms = 0;
 };
 
 }  // namespace orpcd
@@ -108,6 +108,7 @@ struct orpcd_ctx {
     // batch state (per start slot)
     orpcd::DevBuf<double> scov;     // B*N*6 posed-frame source covariance
     orpcd::DevBuf<int32_t> prevnn;  // B*N previous correspondence (Morton target index)
+    orpcd::DevBuf<unsigned long long> best;  // B*N packed (d^2 bits, target) of the current pass
     orpcd::DevBuf<double> G;        // B*12 base pose (3x4, column convention)
     orpcd::DevBuf<double> T;        // B*16 accumulated ICP transform
     orpcd::DevBuf<double> Q;        // B*12 T*G (3x4)
@@ -149,9 +150,9 @@ hipError_t launch_normals_cov(const double* rawcov6, int64_t n, const double* Rc
                               double* normals3, double* cov6, hipStream_t s);
 
 // gicp_kernels.hip
-hipError_t launch_gicp_pass(const orpcd_ctx* c, int nact, int nblk, double r2, hipStream_t s);
-hipError_t launch_gicp_solve(const orpcd_ctx* c, int nact, int nblk, int pass, const orpcd_gicp_params& p,
-                             hipStream_t s);
+int accum_blocks(int64_t N);
+hipError_t launch_gicp_pass(const orpcd_ctx* c, int nact, int pass, double r2, hipStream_t s, hipEvent_t mid);
+hipError_t launch_gicp_solve(const orpcd_ctx* c, int nact, int pass, const orpcd_gicp_params& p, hipStream_t s);
 hipError_t launch_nn1(const double* q, int64_t nq, const CloudLayout& t, double r2, int32_t* idx, double* d2,
                       hipStream_t s);
 

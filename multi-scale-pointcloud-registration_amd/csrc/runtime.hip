@@ -4,6 +4,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <new>
 
@@ -119,6 +120,7 @@ int orpcd_ctx_destroy(orpcd_ctx* c) {
                     &c->out_rmse, &c->scratch64a, &c->scratch64b, &c->scratch64c})
         b->release();
     c->prevnn.release();
+    c->best.release();
     c->done.release();
     c->active.release();
     c->out_iters.release();
@@ -178,9 +180,10 @@ int orpcd_gicp_batch(orpcd_ctx* c, const double* R0, const double* t0, int32_t B
         if (rc) return rc;
     }
     const int64_t N = c->src.n;
-    const int nblk = (int)((N + kCBlockQ - 1) / kCBlockQ);
+    const int nblk = accum_blocks(N);
     CTX_CHECK(c, c->scov.ensure((size_t)B * N * 6));
     CTX_CHECK(c, c->prevnn.ensure((size_t)B * N));
+    CTX_CHECK(c, c->best.ensure((size_t)B * N));
     CTX_CHECK(c, c->G.ensure((size_t)B * 12));
     CTX_CHECK(c, c->T.ensure((size_t)B * 16));
     CTX_CHECK(c, c->Q.ensure((size_t)B * 12));
@@ -245,28 +248,43 @@ int orpcd_gicp_batch(orpcd_ctx* c, const double* R0, const double* t0, int32_t B
     unsigned long long tiles_before = 0;
     if (c->profiling) CTX_CHECK(c, hipMemcpy(&tiles_before, c->counters.p, 8, hipMemcpyDeviceToHost));
     int nact = B;
+    static const bool trace = getenv("ORPCD_TRACE") != nullptr;
+    const bool timed = c->profiling || trace;
     for (int pass = 0; pass <= p->max_iteration && nact > 0; ++pass) {
-        hipEvent_t e0 = nullptr, e1 = nullptr;
-        if (c->profiling) {
-            while (c->ev_pool.size() < 2) {
+        hipEvent_t e0 = nullptr, e1 = nullptr, e2 = nullptr;
+        if (timed) {
+            while (c->ev_pool.size() < 3) {
                 hipEvent_t e;
                 CTX_CHECK(c, hipEventCreate(&e));
                 c->ev_pool.push_back(e);
             }
             e0 = c->ev_pool[0];
             e1 = c->ev_pool[1];
+            e2 = c->ev_pool[2];
             CTX_CHECK(c, hipEventRecord(e0, s));
         }
-        CTX_CHECK(c, launch_gicp_pass(c, nact, nblk, r2, s));
-        if (c->profiling) CTX_CHECK(c, hipEventRecord(e1, s));
-        CTX_CHECK(c, launch_gicp_solve(c, nact, nblk, pass, *p, s));
+        CTX_CHECK(c, launch_gicp_pass(c, nact, pass, r2, s, e1));
+        if (timed) CTX_CHECK(c, hipEventRecord(e2, s));
+        CTX_CHECK(c, launch_gicp_solve(c, nact, pass, *p, s));
         CTX_CHECK(c, hipMemcpyAsync(hDone, c->done.p, (size_t)B * 4, hipMemcpyDeviceToHost, s));
+        unsigned long long tiles_now = 0;
+        if (trace) CTX_CHECK(c, hipMemcpyAsync(&tiles_now, c->counters.p, 8, hipMemcpyDeviceToHost, s));
         CTX_CHECK(c, hipStreamSynchronize(s));
-        if (c->profiling) {
-            float ms = 0.f;
+        if (timed) {
+            float ms = 0.f, ms2 = 0.f;
             CTX_CHECK(c, hipEventElapsedTime(&ms, e0, e1));
-            c->stats.launches += 1;
-            c->stats.ms += ms;
+            CTX_CHECK(c, hipEventElapsedTime(&ms2, e1, e2));
+            if (c->profiling) {
+                c->stats.launches += 1;
+                c->stats.ms += ms;
+                c->stats.accum_ms += ms2;
+            }
+            if (trace) {
+                static unsigned long long last = 0;
+                fprintf(stderr, "[orpcd] pass %3d nact %3d search %.3f ms accum %.3f ms tiles %llu\n", pass, nact,
+                        ms, ms2, tiles_now - last);
+                last = tiles_now;
+            }
         }
         c->stats.passes += nact;
         int k = 0;
@@ -394,9 +412,9 @@ int orpcd_profiling(orpcd_ctx* c, int32_t enable) {
 
 int orpcd_stats(orpcd_ctx* c, double* out, int32_t n) {
     if (!c || !out) return ORPCD_EINVAL;
-    const double v[6] = {c->stats.launches, c->stats.ms, c->stats.pairs, c->stats.iterations, c->stats.passes,
-                         c->stats.tiles};
-    for (int i = 0; i < n && i < 6; ++i) out[i] = v[i];
+    const double v[7] = {c->stats.launches, c->stats.ms, c->stats.pairs, c->stats.iterations, c->stats.passes,
+                         c->stats.tiles, c->stats.accum_ms};
+    for (int i = 0; i < n && i < 7; ++i) out[i] = v[i];
     return ORPCD_OK;
 }
 
