@@ -10,24 +10,33 @@
 // the RegistrationICP convergence test, per start, on device.
 // Reference call site: generalizedICP.py:59-70, driven by Aligner.py:178-202.
 //
-// A pass is two kernels:
-//  * nn_search_kernel (fp32, compute-bound, low VGPR):  every wave owns 128
+// A pass is:
+//  * nn_search_kernel (fp32, low VGPR, 8 waves/SIMD): every wave owns 128
 //    Morton-consecutive queries (2 per lane) of one start.  Target tiles (64
 //    Morton-consecutive points with an AABB) are culled first against the
-//    wave's query AABB and worst bound (lane-parallel over 64 tiles per round),
+//    wave's query AABB and worst bound (lane-parallel, 64 tiles per ballot),
 //    then against each query's own bound; surviving tiles are staged into the
-//    wave's LDS slot with one coalesced 1 KiB load and scanned with packed fp32
-//    math (v_pk_add/mul/fma, one LDS broadcast per target).  Each query's bound
-//    is seeded by the start's correspondence of the previous pass, or on pass
-//    0 by a strided set of tile representatives (real targets, so the bound is
-//    valid); the seed only bounds, the scan re-finds the exact minimum.  When
-//    few starts are running, a query group's tiles are split over S waves whose
-//    results merge by a 64-bit atomicMin on (d^2 bits, target index).
+//    wave's LDS slot by one coalesced 1 KiB load (the next candidate's load is
+//    in flight while the current tile is scanned) and scanned with packed fp32
+//    math: per target and lane-pair of queries 6 v_pk ops for the two d^2, then
+//    the key (d^2 bits with the low 6 bits replaced by the tile-local index)
+//    enters a v_min3_u32 running minimum, so one integer min selects distance
+//    AND index.  Candidates whose d^2 agree in the top 26 bits (2^-17 relative)
+//    resolve to the lower Morton position; across tiles the earlier tile wins a
+//    tie (exact duplicates keep the lowest input index: the Morton sort is
+//    stable).  Each query's bound is seeded by the start's correspondence of
+//    the previous pass, or on pass 0 by strided tile representatives (real
+//    targets, so the bound is valid); the seed only bounds the scan.  When few
+//    starts run, a query group's tiles are split over S waves whose results
+//    merge by a 64-bit atomicMin on (d^2 bits, target index).
 //  * gicp_accum_kernel (fp64): re-evaluates the chosen pair in fp64 (strict
 //    radius test, d^2, Jacobian) and reduces the 29 normal-equation terms per
 //    block in a fixed order.  Because W is symmetric, J^T J = A^T (Cs+Ct)^-1 A
 //    and J^T r = A^T (Cs+Ct)^-1 d with A = [-[q]x | I]: no matrix square root
 //    is needed.
+//  * gicp_solve_kernel: per start, fixed-order reduction, convergence test,
+//    6x6 LDLT solve and pose update; then xform_queries_kernel writes the fp32
+//    queries of the next pass (fp64 transform, one rounding).
 #include "device_math.h"
 #include "orpcd_internal.h"
 
@@ -37,110 +46,188 @@ typedef float f2 __attribute__((ext_vector_type(2)));
 
 __device__ __forceinline__ f2 pk_fma(f2 a, f2 b, f2 c) { return __builtin_elementwise_fma(a, b, c); }
 
-__device__ __forceinline__ float wave_max_f(float v) {
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) v = fmaxf(v, __shfl_xor(v, off, 64));
+// ------------------------------------------------ wave reductions (DPP, no LDS)
+// all-reduce within each row of 16 lanes: quad_perm[1,0,3,2], quad_perm[2,3,0,1],
+// row_half_mirror, row_mirror
+template <typename Op>
+__device__ __forceinline__ unsigned row_reduce(unsigned v, Op op) {
+    v = op(v, (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, 0xb1, 0xf, 0xf, false));
+    v = op(v, (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, 0x4e, 0xf, 0xf, false));
+    v = op(v, (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, 0x141, 0xf, 0xf, false));
+    v = op(v, (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, 0x140, 0xf, 0xf, false));
     return v;
 }
-__device__ __forceinline__ float wave_min_f(float v) {
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) v = fminf(v, __shfl_xor(v, off, 64));
-    return v;
+// max of non-negative float bit patterns (or any uint) over the wave -> SGPR
+__device__ __forceinline__ unsigned wave_umax(unsigned v) {
+    v = row_reduce(v, [](unsigned a, unsigned b) { return a > b ? a : b; });
+    const unsigned r0 = __builtin_amdgcn_readlane(v, 0), r1 = __builtin_amdgcn_readlane(v, 16);
+    const unsigned r2 = __builtin_amdgcn_readlane(v, 32), r3 = __builtin_amdgcn_readlane(v, 48);
+    const unsigned a = r0 > r1 ? r0 : r1, b = r2 > r3 ? r2 : r3;
+    return a > b ? a : b;
 }
+__device__ __forceinline__ float wave_fmax(float x) {
+    unsigned v = row_reduce(__float_as_uint(x), [](unsigned a, unsigned b) {
+        return __float_as_uint(fmaxf(__uint_as_float(a), __uint_as_float(b)));
+    });
+    return fmaxf(fmaxf(__uint_as_float(__builtin_amdgcn_readlane(v, 0)), __uint_as_float(__builtin_amdgcn_readlane(v, 16))),
+                 fmaxf(__uint_as_float(__builtin_amdgcn_readlane(v, 32)), __uint_as_float(__builtin_amdgcn_readlane(v, 48))));
+}
+__device__ __forceinline__ float wave_fmin(float x) { return -wave_fmax(-x); }
 
-// fp32 squared distance exactly as the scan computes it
+// fp32 squared distance (seed evaluation)
 __device__ __forceinline__ float d2f(float qx, float qy, float qz, float4 t) {
     const float dx = qx - t.x, dy = qy - t.y, dz = qz - t.z;
     return __builtin_fmaf(dz, dz, __builtin_fmaf(dy, dy, dx * dx));
 }
 
-__device__ __forceinline__ float box_d2(float x, float y, float z, float4 lo, float4 hi) {
-    const float dx = fmaxf(0.0f, fmaxf(lo.x - x, x - hi.x));
-    const float dy = fmaxf(0.0f, fmaxf(lo.y - y, y - hi.y));
-    const float dz = fmaxf(0.0f, fmaxf(lo.z - z, z - hi.z));
+__device__ __forceinline__ float box_d2(float x, float y, float z, float lx, float ly, float lz, float hx, float hy,
+                                        float hz) {
+    const float dx = fmaxf(0.0f, fmaxf(lx - x, x - hx));
+    const float dy = fmaxf(0.0f, fmaxf(ly - y, y - hy));
+    const float dz = fmaxf(0.0f, fmaxf(lz - z, z - hz));
     return dx * dx + dy * dy + dz * dz;
 }
 
 constexpr unsigned long long kNone = ~0ull;
-__device__ __forceinline__ unsigned long long pack_best(float d, int j) {
-    return j < 0 ? kNone : ((unsigned long long)__float_as_uint(d) << 32) | (unsigned)j;
-}
+constexpr unsigned kKeyMask = 0xFFFFFFC0u;  // d^2 bits kept in a scan key (low 6 = tile-local index)
 
 // --------------------------------------------------------------------------
 // Culled exact nearest search for the 2 queries of every lane of one wave,
-// restricted to tiles t with t % S == s.  bd[] enters as the per-query bound
-// (d^2 must be < bd to be taken), bj[] = -1.  Returns tiles scanned.
+// restricted to tiles t with t % S == s.  bound[] enters as the per-query
+// bound on d^2 (<= 0: invalid query).  Returns tiles scanned; bj[] = Morton
+// index of the chosen target or -1, bd[] its fp32 d^2 (key-truncated).
 // --------------------------------------------------------------------------
 __device__ __forceinline__ int culled_search(float4* stage, const float4* __restrict__ p4,
                                              const float4* __restrict__ tlo, const float4* __restrict__ thi,
                                              int ntiles, int S, int s, const float qx[2], const float qy[2],
-                                             const float qz[2], const bool valid[2], float bd[2], int bj[2]) {
+                                             const float qz[2], const float bound[2], float bd[2], int bj[2]) {
     const int lane = threadIdx.x & 63;
-    float b0 = valid[0] ? bd[0] : -1.0f, b1 = valid[1] ? bd[1] : -1.0f;
-    float W = wave_max_f(fmaxf(b0, b1));
-    if (!(W > 0.0f)) return 0;  // no query of this wave can take anything
+    const bool v0 = bound[0] > 0.0f, v1 = bound[1] > 0.0f;
+    unsigned k0 = v0 ? __float_as_uint(bound[0]) : 0u;  // best key (0: never improves)
+    unsigned k1 = v1 ? __float_as_uint(bound[1]) : 0u;
+    int t0 = -1, t1 = -1;                               // tile of the best key
+    bj[0] = bj[1] = -1;
+    bd[0] = bd[1] = 0.0f;
+    unsigned Wk = wave_umax((k0 > k1 ? k0 : k1) & kKeyMask);
+    if (Wk == 0u) return 0;  // no query of this wave can take anything
+    float W = __uint_as_float(Wk);
     const float inf = 3.0e38f;
-    const float lox = wave_min_f(fminf(valid[0] ? qx[0] : inf, valid[1] ? qx[1] : inf));
-    const float loy = wave_min_f(fminf(valid[0] ? qy[0] : inf, valid[1] ? qy[1] : inf));
-    const float loz = wave_min_f(fminf(valid[0] ? qz[0] : inf, valid[1] ? qz[1] : inf));
-    const float hix = wave_max_f(fmaxf(valid[0] ? qx[0] : -inf, valid[1] ? qx[1] : -inf));
-    const float hiy = wave_max_f(fmaxf(valid[0] ? qy[0] : -inf, valid[1] ? qy[1] : -inf));
-    const float hiz = wave_max_f(fmaxf(valid[0] ? qz[0] : -inf, valid[1] ? qz[1] : -inf));
-    const f2 QX = {qx[0], qx[1]}, QY = {qy[0], qy[1]}, QZ = {qz[0], qz[1]};
-    int j0 = -1, j1 = -1;
+    const float lox = wave_fmin(fminf(v0 ? qx[0] : inf, v1 ? qx[1] : inf));
+    const float loy = wave_fmin(fminf(v0 ? qy[0] : inf, v1 ? qy[1] : inf));
+    const float loz = wave_fmin(fminf(v0 ? qz[0] : inf, v1 ? qz[1] : inf));
+    const float hix = wave_fmax(fmaxf(v0 ? qx[0] : -inf, v1 ? qx[1] : -inf));
+    const float hiy = wave_fmax(fmaxf(v0 ? qy[0] : -inf, v1 ? qy[1] : -inf));
+    const float hiz = wave_fmax(fmaxf(v0 ? qz[0] : -inf, v1 ? qz[1] : -inf));
     int visited = 0;
-    for (int tb = 0; tb < ntiles; tb += 64) {
-        const int t = tb + lane;
-        float4 a = make_float4(0.f, 0.f, 0.f, 0.f), b = a;
-        float lb = inf;
-        if (t < ntiles && (S == 1 || t % S == s)) {
-            a = tlo[t];
-            b = thi[t];
-            const float dx = fmaxf(0.0f, fmaxf(a.x - hix, lox - b.x));
-            const float dy = fmaxf(0.0f, fmaxf(a.y - hiy, loy - b.y));
-            const float dz = fmaxf(0.0f, fmaxf(a.z - hiz, loz - b.z));
-            lb = dx * dx + dy * dy + dz * dz;
-        }
-        unsigned long long mask = __ballot(lb < W);
-        while (mask) {
+
+    // candidate cursor: rounds of 64 tiles, one tile per lane; wave-box test by
+    // ballot, then the per-query test for each set bit.
+    int tb = -64;
+    unsigned long long mask = 0;
+    float lb = inf;
+    float4 a = make_float4(0.f, 0.f, 0.f, 0.f), b = a;
+    auto next_candidate = [&](float& lbk) -> int {
+        for (;;) {
+            while (mask == 0) {
+                tb += 64;
+                if (tb >= ntiles) return -1;
+                const int t = tb + lane;
+                lb = inf;
+                if (t < ntiles && (S == 1 || t % S == s)) {
+                    a = tlo[t];
+                    b = thi[t];
+                    const float dx = fmaxf(0.0f, fmaxf(a.x - hix, lox - b.x));
+                    const float dy = fmaxf(0.0f, fmaxf(a.y - hiy, loy - b.y));
+                    const float dz = fmaxf(0.0f, fmaxf(a.z - hiz, loz - b.z));
+                    lb = dx * dx + dy * dy + dz * dz;
+                }
+                mask = __ballot(lb < W);
+            }
             const int k = __builtin_ctzll(mask);
             mask &= mask - 1;
-            if (!(__shfl(lb, k, 64) < W)) continue;  // the bound shrank since the ballot
-            // per-query test against this tile's AABB
-            const float4 ta = make_float4(__shfl(a.x, k, 64), __shfl(a.y, k, 64), __shfl(a.z, k, 64), 0.f);
-            const float4 tbx = make_float4(__shfl(b.x, k, 64), __shfl(b.y, k, 64), __shfl(b.z, k, 64), 0.f);
-            const bool need = box_d2(qx[0], qy[0], qz[0], ta, tbx) < b0 || box_d2(qx[1], qy[1], qz[1], ta, tbx) < b1;
-            if (!__any(need)) continue;
-            const int base = (tb + k) * kTile;
-            stage[lane] = p4[base + lane];
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-#pragma unroll 8
-            for (int kk = 0; kk < kTile; ++kk) {
-                const float4 tp = stage[kk];
-                const f2 tx = {tp.x, tp.x}, ty = {tp.y, tp.y}, tz = {tp.z, tp.z};
-                const f2 dx = QX - tx, dy = QY - ty, dz = QZ - tz;
-                f2 d = dx * dx;
-                d = pk_fma(dy, dy, d);
-                d = pk_fma(dz, dz, d);
-                const int j = base + kk;
-                if (d.x < b0) {
-                    b0 = d.x;
-                    j0 = j;
-                }
-                if (d.y < b1) {
-                    b1 = d.y;
-                    j1 = j;
-                }
-            }
-            asm volatile("" ::: "memory");  // all reads of this tile precede the next stage write
-            ++visited;
-            W = wave_max_f(fmaxf(b0, b1));
+            lbk = __uint_as_float(__builtin_amdgcn_readlane(__float_as_uint(lb), k));
+            if (!(lbk < W)) continue;  // the bound shrank since the ballot
+            const float lx = __uint_as_float(__builtin_amdgcn_readlane(__float_as_uint(a.x), k));
+            const float ly = __uint_as_float(__builtin_amdgcn_readlane(__float_as_uint(a.y), k));
+            const float lz = __uint_as_float(__builtin_amdgcn_readlane(__float_as_uint(a.z), k));
+            const float hx = __uint_as_float(__builtin_amdgcn_readlane(__float_as_uint(b.x), k));
+            const float hy = __uint_as_float(__builtin_amdgcn_readlane(__float_as_uint(b.y), k));
+            const float hz = __uint_as_float(__builtin_amdgcn_readlane(__float_as_uint(b.z), k));
+            const bool need = box_d2(qx[0], qy[0], qz[0], lx, ly, lz, hx, hy, hz) < __uint_as_float(k0 & kKeyMask) ||
+                              box_d2(qx[1], qy[1], qz[1], lx, ly, lz, hx, hy, hz) < __uint_as_float(k1 & kKeyMask);
+            if (__any(need)) return tb + k;
+        }
+    };
+
+    // software pipeline: the next candidate's 1 KiB tile load is in flight
+    // while the current tile is scanned out of LDS
+    float lbn = inf;
+    int nxt = next_candidate(lbn);
+    float4 pre = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (nxt >= 0) pre = p4[nxt * kTile + lane];
+    while (nxt >= 0) {
+        const int tile = __builtin_amdgcn_readfirstlane(nxt);
+        // SoA stage: x[64] | y[64] | z[64]; a ds_read_b64 yields two targets'
+        // coordinate, already an aligned register pair for v_pk_* math
+        float* sx = reinterpret_cast<float*>(stage);
+        sx[lane] = pre.x;
+        sx[64 + lane] = pre.y;
+        sx[128 + lane] = pre.z;
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        nxt = next_candidate(lbn);
+        if (nxt >= 0) pre = p4[nxt * kTile + lane];
+        unsigned m0 = 0xFFFFFFFFu, m1 = 0xFFFFFFFFu;
+        const f2 qx0 = {qx[0], qx[0]}, qy0 = {qy[0], qy[0]}, qz0 = {qz[0], qz[0]};
+        const f2 qx1 = {qx[1], qx[1]}, qy1 = {qy[1], qy[1]}, qz1 = {qz[1], qz[1]};
+#pragma unroll
+        for (int kk = 0; kk < kTile; kk += 2) {
+            const f2 tx = *reinterpret_cast<const f2*>(sx + kk);
+            const f2 ty = *reinterpret_cast<const f2*>(sx + 64 + kk);
+            const f2 tz = *reinterpret_cast<const f2*>(sx + 128 + kk);
+            f2 dx = qx0 - tx, dy = qy0 - ty, dz = qz0 - tz;  // query 0 vs targets kk, kk+1
+            f2 d0 = dx * dx;
+            d0 = pk_fma(dy, dy, d0);
+            d0 = pk_fma(dz, dz, d0);
+            dx = qx1 - tx;
+            dy = qy1 - ty;
+            dz = qz1 - tz;  // query 1
+            f2 d1 = dx * dx;
+            d1 = pk_fma(dy, dy, d1);
+            d1 = pk_fma(dz, dz, d1);
+            const unsigned a0 = (__float_as_uint(d0.x) & kKeyMask) | (unsigned)kk;
+            const unsigned c0 = (__float_as_uint(d0.y) & kKeyMask) | (unsigned)(kk + 1);
+            const unsigned a1 = (__float_as_uint(d1.x) & kKeyMask) | (unsigned)kk;
+            const unsigned c1 = (__float_as_uint(d1.y) & kKeyMask) | (unsigned)(kk + 1);
+            m0 = min(m0, min(a0, c0));
+            m1 = min(m1, min(a1, c1));
+        }
+        asm volatile("" ::: "memory");  // all reads of this tile precede the next stage write
+        // a tile improves a query only if its masked d^2 is strictly smaller
+        if ((m0 & kKeyMask) < (k0 & kKeyMask)) {
+            k0 = m0;
+            t0 = tile;
+        }
+        if ((m1 & kKeyMask) < (k1 & kKeyMask)) {
+            k1 = m1;
+            t1 = tile;
+        }
+        ++visited;
+        Wk = wave_umax((k0 > k1 ? k0 : k1) & kKeyMask);
+        W = __uint_as_float(Wk);
+        // the prefetched candidate was chosen under the previous bound: re-test
+        while (nxt >= 0 && !(lbn < W)) {
+            nxt = next_candidate(lbn);
+            if (nxt >= 0) pre = p4[nxt * kTile + lane];
         }
     }
-    bd[0] = b0;
-    bd[1] = b1;
-    bj[0] = j0;
-    bj[1] = j1;
+    if (t0 >= 0) {
+        bj[0] = t0 * kTile + (int)(k0 & 63u);
+        bd[0] = __uint_as_float(k0 & kKeyMask);
+    }
+    if (t1 >= 0) {
+        bj[1] = t1 * kTile + (int)(k1 & 63u);
+        bd[1] = __uint_as_float(k1 & kKeyMask);
+    }
     return visited;
 }
 
@@ -154,82 +241,94 @@ __device__ __forceinline__ void xform(const double Q[12], const double p[3], dou
 __device__ __forceinline__ constexpr int ut(int a, int b) { return a * 6 - a * (a - 1) / 2 + (b - a); }
 
 // fp32 search radius: enlarged so no pair with exact d^2 < r^2 is rejected by
-// fp32 rounding; the exact strict test is applied in fp64 afterwards.
+// fp32 rounding or key truncation; the strict test is applied in fp64 later.
 static inline float search_r2(double r2) { return (float)(r2 * (1.0 + 1e-5)) * 1.0001f; }
 
 // seed slack: bound = d^2(seed) * (1 + 1e-4) so the seed target itself (and
-// any closer one) is re-found by the strict-< scan
+// any closer one) is re-found by the scan (1e-4 >> the 2^-17 key truncation)
 constexpr float kSeedSlack = 1.0001f;
+
+// fp32 queries of every running start for the next pass: q = fp32(Q * p).
+__global__ __launch_bounds__(256) void xform_queries_kernel(const double* __restrict__ src, int N,
+                                                            const int32_t* __restrict__ active,
+                                                            const double* __restrict__ Qm,
+                                                            const int32_t* __restrict__ done,
+                                                            float4* __restrict__ q32) {
+    const int slot = active[blockIdx.y];
+    if (done[slot]) return;
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= N) return;
+    double Q[12];
+#pragma unroll
+    for (int t = 0; t < 12; ++t) Q[t] = Qm[12 * slot + t];
+    const double p[3] = {src[3 * i], src[3 * i + 1], src[3 * i + 2]};
+    double q[3];
+    xform(Q, p, q);
+    q32[(size_t)slot * N + i] = make_float4((float)q[0], (float)q[1], (float)q[2], 0.0f);
+}
 
 // --------------------------------------------------------------------------
 // Search kernel: grid = (blocks per start * S, running starts), 4 waves/block.
 // --------------------------------------------------------------------------
 __global__ __launch_bounds__(kCBlock) void nn_search_kernel(
-    const double* __restrict__ src, int N, const float4* __restrict__ p4, const float4* __restrict__ tlo,
-    const float4* __restrict__ thi, int ntiles, const int32_t* __restrict__ active, const double* __restrict__ Qm,
-    const int32_t* __restrict__ done, float r2s, int S, int seed_stride, const int32_t* __restrict__ prevnn,
-    unsigned long long* __restrict__ best, unsigned long long* __restrict__ counters) {
+    const float4* __restrict__ q32, int N, const float4* __restrict__ p4, const float4* __restrict__ tlo,
+    const float4* __restrict__ thi, int ntiles, const int32_t* __restrict__ active, const int32_t* __restrict__ done,
+    float r2s, int S, int seed_stride, const int32_t* __restrict__ prevnn, unsigned long long* __restrict__ best,
+    unsigned long long* __restrict__ counters) {
     const int slot = active[blockIdx.y];
     if (done[slot]) return;
     __shared__ float4 stage[kCWaves][kTile];
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     const int grp = blockIdx.x / S, split = blockIdx.x - grp * S;
-
-    double Q[12];
-#pragma unroll
-    for (int t = 0; t < 12; ++t) Q[t] = Qm[12 * slot + t];
-
     const int i0 = grp * kCBlockQ + wid * (64 * kCQPT) + lane;
-    bool valid[kCQPT];
-    float qx[kCQPT], qy[kCQPT], qz[kCQPT], bd[kCQPT];
+    float qx[kCQPT], qy[kCQPT], qz[kCQPT], bound[kCQPT], bd[kCQPT];
     int bj[kCQPT];
     const int32_t* pn = prevnn + (size_t)slot * N;
+    const float4* qs = q32 + (size_t)slot * N;
     bool need_seed = false;
 #pragma unroll
     for (int k = 0; k < kCQPT; ++k) {
         const int i = i0 + 64 * k;
-        valid[k] = i < N;
-        bj[k] = -1;
-        bd[k] = -1.0f;
+        bound[k] = 0.0f;
         qx[k] = qy[k] = qz[k] = 0.0f;
-        if (valid[k]) {
-            const double p[3] = {src[3 * i], src[3 * i + 1], src[3 * i + 2]};
-            double q[3];
-            xform(Q, p, q);
-            qx[k] = (float)q[0];
-            qy[k] = (float)q[1];
-            qz[k] = (float)q[2];
-            float b = r2s;
+        if (i < N) {
+            const float4 q = qs[i];
+            qx[k] = q.x;
+            qy[k] = q.y;
+            qz[k] = q.z;
+            float bb = r2s;
             const int jp = pn[i];
             if (jp >= 0)
-                b = fminf(b, d2f(qx[k], qy[k], qz[k], p4[jp]) * kSeedSlack);
+                bb = fminf(bb, d2f(q.x, q.y, q.z, p4[jp]) * kSeedSlack + 1e-30f);
             else
                 need_seed = true;
-            bd[k] = b;
+            bound[k] = bb;
         }
     }
     // pass-0 seed: strided tile representatives (real targets -> valid bounds)
     if (seed_stride > 0 && __any(need_seed)) {
-        float s0 = bd[0], s1 = bd[1];
+        float s0 = bound[0], s1 = bound[1];
         for (int t = 0; t < ntiles; t += seed_stride) {
             const float4 rep = p4[t * kTile];
-            s0 = fminf(s0, d2f(qx[0], qy[0], qz[0], rep) * kSeedSlack);
-            s1 = fminf(s1, d2f(qx[1], qy[1], qz[1], rep) * kSeedSlack);
+            s0 = fminf(s0, d2f(qx[0], qy[0], qz[0], rep) * kSeedSlack + 1e-30f);
+            s1 = fminf(s1, d2f(qx[1], qy[1], qz[1], rep) * kSeedSlack + 1e-30f);
         }
-        if (valid[0]) bd[0] = s0;
-        if (valid[1]) bd[1] = s1;
+        if (bound[0] > 0.0f) bound[0] = s0;
+        if (bound[1] > 0.0f) bound[1] = s1;
     }
-    const int visited = culled_search(stage[wid], p4, tlo, thi, ntiles, S, split, qx, qy, qz, valid, bd, bj);
+    const int visited = culled_search(stage[wid], p4, tlo, thi, ntiles, S, split, qx, qy, qz, bound, bd, bj);
     if (lane == 0 && counters) atomicAdd(counters, (unsigned long long)visited);
     unsigned long long* out = best + (size_t)slot * N;
 #pragma unroll
     for (int k = 0; k < kCQPT; ++k) {
-        if (!valid[k]) continue;
-        const unsigned long long v = pack_best(bd[k], bj[k]);
+        const int i = i0 + 64 * k;
+        if (i >= N) continue;
+        const unsigned long long v =
+            bj[k] < 0 ? kNone : ((unsigned long long)__float_as_uint(bd[k]) << 32) | (unsigned)bj[k];
         if (S == 1)
-            out[i0 + 64 * k] = v;
+            out[i] = v;
         else if (v != kNone)
-            atomicMin(out + i0 + 64 * k, v);
+            atomicMin(out + i, v);
     }
 }
 
@@ -410,9 +509,9 @@ __global__ __launch_bounds__(64) void gicp_solve_kernel(const int32_t* __restric
     }
 }
 
-// Kernel-level 1-NN (orpcd_nn1_radius): same culled search on Morton-ordered
-// targets (representative seed, S = 1), fp64 re-check, no accumulation.
-// Queries in input order.
+// Kernel-level 1-NN (orpcd_nn1_radius): the same culled search on Morton-
+// ordered targets (representative seed, S = 1), fp64 re-check, no
+// accumulation.  Queries in input order.
 __global__ __launch_bounds__(kCBlock) void nn1_kernel(const double* __restrict__ q64, int nq,
                                                       const float4* __restrict__ p4, const float4* __restrict__ tlo,
                                                       const float4* __restrict__ thi, int ntiles, int seed_stride,
@@ -422,28 +521,26 @@ __global__ __launch_bounds__(kCBlock) void nn1_kernel(const double* __restrict__
     __shared__ float4 stage[kCWaves][kTile];
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     const int i0 = blockIdx.x * kCBlockQ + wid * (64 * kCQPT) + lane;
-    bool valid[kCQPT];
-    float qx[kCQPT], qy[kCQPT], qz[kCQPT], bd[kCQPT];
+    float qx[kCQPT], qy[kCQPT], qz[kCQPT], bound[kCQPT], bd[kCQPT];
     int bj[kCQPT];
 #pragma unroll
     for (int k = 0; k < kCQPT; ++k) {
         const int i = i0 + 64 * k;
-        valid[k] = i < nq;
-        bj[k] = -1;
-        qx[k] = valid[k] ? (float)q64[3 * i] : 0.f;
-        qy[k] = valid[k] ? (float)q64[3 * i + 1] : 0.f;
-        qz[k] = valid[k] ? (float)q64[3 * i + 2] : 0.f;
-        float b = valid[k] ? r2s : -1.0f;
-        if (valid[k])
+        const bool valid = i < nq;
+        qx[k] = valid ? (float)q64[3 * i] : 0.f;
+        qy[k] = valid ? (float)q64[3 * i + 1] : 0.f;
+        qz[k] = valid ? (float)q64[3 * i + 2] : 0.f;
+        float b = valid ? r2s : 0.0f;
+        if (valid)
             for (int t = 0; t < ntiles; t += seed_stride)
-                b = fminf(b, d2f(qx[k], qy[k], qz[k], p4[t * kTile]) * kSeedSlack);
-        bd[k] = b;
+                b = fminf(b, d2f(qx[k], qy[k], qz[k], p4[t * kTile]) * kSeedSlack + 1e-30f);
+        bound[k] = b;
     }
-    culled_search(stage[wid], p4, tlo, thi, ntiles, 1, 0, qx, qy, qz, valid, bd, bj);
+    culled_search(stage[wid], p4, tlo, thi, ntiles, 1, 0, qx, qy, qz, bound, bd, bj);
 #pragma unroll
     for (int k = 0; k < kCQPT; ++k) {
         const int i = i0 + 64 * k;
-        if (!valid[k]) continue;
+        if (i >= nq) continue;
         int j = bj[k];
         double dd = 0.0;
         if (j >= 0) {
@@ -470,31 +567,35 @@ int search_splits(int nact, int blocks_per_start) {
     return (int)std::min<int64_t>(16, std::max<int64_t>(1, (want + waves - 1) / waves));
 }
 
+int accum_blocks(int64_t N) { return (int)((N + 255) / 256); }
+
+hipError_t launch_xform(const orpcd_ctx* c, int nact, hipStream_t s) {
+    const int N = (int)c->src.n;
+    xform_queries_kernel<<<dim3((unsigned)((N + 255) / 256), (unsigned)nact), 256, 0, s>>>(
+        c->src.xyz64.p, N, c->active.p, c->Q.p, c->done.p, c->q32.p);
+    return hipGetLastError();
+}
+
 hipError_t launch_gicp_pass(const orpcd_ctx* c, int nact, int pass, double r2, hipStream_t s, hipEvent_t mid) {
     const int N = (int)c->src.n;
     const int sblk = (N + kCBlockQ - 1) / kCBlockQ;
     const int S = search_splits(nact, sblk);
-    if (S > 1) {
-        // merged by atomicMin: reset every running start's slots
-        // (one memset over all B slots keeps this launch-free of host state)
-        hipError_t e = hipMemsetAsync(c->best.p, 0xff, c->best.n * sizeof(unsigned long long), s);
+    hipError_t e;
+    if (S > 1) {  // splits merge by atomicMin: reset every slot's result
+        e = hipMemsetAsync(c->best.p, 0xff, c->best.n * sizeof(unsigned long long), s);
         if (e != hipSuccess) return e;
     }
     nn_search_kernel<<<dim3((unsigned)(sblk * S), (unsigned)nact), kCBlock, 0, s>>>(
-        c->src.xyz64.p, N, c->tgt.p4.p, c->tgt.tlo.p, c->tgt.thi.p, (int)c->tgt.ntiles, c->active.p, c->Q.p,
-        c->done.p, search_r2(r2), S, pass == 0 ? seed_stride_for(c->tgt.ntiles) : 0, c->prevnn.p, c->best.p,
-        c->counters.p);
-    hipError_t e = hipGetLastError();
-    if (e != hipSuccess) return e;
+        c->q32.p, N, c->tgt.p4.p, c->tgt.tlo.p, c->tgt.thi.p, (int)c->tgt.ntiles, c->active.p, c->done.p,
+        search_r2(r2), S, pass == 0 ? seed_stride_for(c->tgt.ntiles) : 0, c->prevnn.p, c->best.p, c->counters.p);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
     if (mid && (e = hipEventRecord(mid, s)) != hipSuccess) return e;
-    const int ablk = (N + 255) / 256;
+    const int ablk = accum_blocks(N);
     gicp_accum_kernel<<<dim3((unsigned)ablk, (unsigned)nact), 256, 0, s>>>(
         c->src.xyz64.p, c->scov.p, N, c->tgt.xyz64.p, c->tcov.p, c->active.p, c->Q.p, c->R.p, c->done.p, r2,
         c->best.p, c->prevnn.p, c->partial.p, ablk);
     return hipGetLastError();
 }
-
-int accum_blocks(int64_t N) { return (int)((N + 255) / 256); }
 
 hipError_t launch_gicp_solve(const orpcd_ctx* c, int nact, int pass, const orpcd_gicp_params& p, hipStream_t s) {
     SolveArgs a{c->T.p,    c->Q.p,       c->R.p,        c->G.p,         c->prev.p,
@@ -502,7 +603,9 @@ hipError_t launch_gicp_solve(const orpcd_ctx* c, int nact, int pass, const orpcd
     gicp_solve_kernel<<<(unsigned)nact, 64, 0, s>>>(c->active.p, c->partial.p, accum_blocks(c->src.n),
                                                     (int)c->src.n, pass, p.max_iteration, p.relative_fitness,
                                                     p.relative_rmse, a);
-    return hipGetLastError();
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    return launch_xform(c, nact, s);  // queries of the next pass (done starts skip)
 }
 
 hipError_t launch_nn1(const double* q, int64_t nq, const CloudLayout& t, double r2, int32_t* idx, double* d2,

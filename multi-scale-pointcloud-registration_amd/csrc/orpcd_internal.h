@@ -109,6 +109,7 @@ struct orpcd_ctx {
     orpcd::DevBuf<double> scov;     // B*N*6 posed-frame source covariance
     orpcd::DevBuf<int32_t> prevnn;  // B*N previous correspondence (Morton target index)
     orpcd::DevBuf<unsigned long long> best;  // B*N packed (d^2 bits, target) of the current pass
+    orpcd::DevBuf<float4> q32;      // B*N fp32 queries of the current pass (x,y,z,0)
     orpcd::DevBuf<double> G;        // B*12 base pose (3x4, column convention)
     orpcd::DevBuf<double> T;        // B*16 accumulated ICP transform
     orpcd::DevBuf<double> Q;        // B*12 T*G (3x4)
@@ -151,6 +152,7 @@ hipError_t launch_normals_cov(const double* rawcov6, int64_t n, const double* Rc
 
 // gicp_kernels.hip
 int accum_blocks(int64_t N);
+hipError_t launch_xform(const orpcd_ctx* c, int nact, hipStream_t s);
 hipError_t launch_gicp_pass(const orpcd_ctx* c, int nact, int pass, double r2, hipStream_t s, hipEvent_t mid);
 hipError_t launch_gicp_solve(const orpcd_ctx* c, int nact, int pass, const orpcd_gicp_params& p, hipStream_t s);
 hipError_t launch_nn1(const double* q, int64_t nq, const CloudLayout& t, double r2, int32_t* idx, double* d2,

@@ -12,6 +12,8 @@
 
 using namespace orpcd;
 
+static constexpr int kSyncEvery = 4;  // passes between host checks of the done flags
+
 #define CTX_CHECK(ctx, call)                                                                          \
     do {                                                                                              \
         hipError_t e_ = (call);                                                                       \
@@ -121,6 +123,7 @@ int orpcd_ctx_destroy(orpcd_ctx* c) {
         b->release();
     c->prevnn.release();
     c->best.release();
+    c->q32.release();
     c->done.release();
     c->active.release();
     c->out_iters.release();
@@ -184,6 +187,7 @@ int orpcd_gicp_batch(orpcd_ctx* c, const double* R0, const double* t0, int32_t B
     CTX_CHECK(c, c->scov.ensure((size_t)B * N * 6));
     CTX_CHECK(c, c->prevnn.ensure((size_t)B * N));
     CTX_CHECK(c, c->best.ensure((size_t)B * N));
+    CTX_CHECK(c, c->q32.ensure((size_t)B * N));
     CTX_CHECK(c, c->G.ensure((size_t)B * 12));
     CTX_CHECK(c, c->T.ensure((size_t)B * 16));
     CTX_CHECK(c, c->Q.ensure((size_t)B * 12));
@@ -243,6 +247,7 @@ int orpcd_gicp_batch(orpcd_ctx* c, const double* R0, const double* t0, int32_t B
 
     // posed-frame source covariances for every start (rigid equivariance)
     CTX_CHECK(c, launch_normals_cov(c->sraw.p, N, c->scratch64c.p, B, p->epsilon, nullptr, c->scov.p, s));
+    CTX_CHECK(c, launch_xform(c, B, s));
 
     const double r2 = p->max_correspondence_distance * p->max_correspondence_distance;
     unsigned long long tiles_before = 0;
@@ -266,6 +271,11 @@ int orpcd_gicp_batch(orpcd_ctx* c, const double* R0, const double* t0, int32_t B
         CTX_CHECK(c, launch_gicp_pass(c, nact, pass, r2, s, e1));
         if (timed) CTX_CHECK(c, hipEventRecord(e2, s));
         CTX_CHECK(c, launch_gicp_solve(c, nact, pass, *p, s));
+        // the host learns which starts finished only every few passes; a
+        // finished start's blocks exit at once in the passes in between
+        const bool sync = timed || (pass % kSyncEvery) == kSyncEvery - 1 || pass == p->max_iteration;
+        c->stats.passes += nact;
+        if (!sync) continue;
         CTX_CHECK(c, hipMemcpyAsync(hDone, c->done.p, (size_t)B * 4, hipMemcpyDeviceToHost, s));
         unsigned long long tiles_now = 0;
         if (trace) CTX_CHECK(c, hipMemcpyAsync(&tiles_now, c->counters.p, 8, hipMemcpyDeviceToHost, s));
@@ -286,7 +296,6 @@ int orpcd_gicp_batch(orpcd_ctx* c, const double* R0, const double* t0, int32_t B
                 last = tiles_now;
             }
         }
-        c->stats.passes += nact;
         int k = 0;
         for (int b = 0; b < nact; ++b)
             if (!hDone[hAct[b]]) hAct[k++] = hAct[b];

@@ -2,8 +2,10 @@
 
 Tolerances (north_star "stated float tolerance"):
   * nearest-neighbour indices: identical, except certified near-ties where the
-    two candidates' exact distances differ by < 1e-6 relative (the fp32 search
-    cannot order them); d^2 of the chosen pair is fp64 (rtol 1e-12);
+    two candidates' exact squared distances differ by < 2e-5 relative: the
+    search orders candidates by fp32 d^2 truncated to 26 bits (2^-17 = 7.6e-6
+    relative) after fp32 rounding of the coordinates; d^2 of the chosen pair is
+    then fp64 (rtol 1e-12);
   * normals / covariances: fp64 on both sides, same operation order: 1e-10;
   * per-optimize GICP: T elementwise <= 1e-6, inlier RMSE |delta| <= 1e-7,
     fitness |delta| <= 1e-4, iteration count within 1;
@@ -26,7 +28,7 @@ def _certified_nn(oracle_idx, gpu_idx, q, t):
         assert a >= 0 and b >= 0, f"query {i}: one side found no neighbour ({a} vs {b})"
         da = ((q[i] - t[a]) ** 2).sum()
         db = ((q[i] - t[b]) ** 2).sum()
-        assert abs(da - db) <= 1e-6 * max(da, 1e-30), f"query {i}: not a near-tie ({da} vs {db})"
+        assert abs(da - db) <= 2e-5 * max(da, db, 1e-30), f"query {i}: not a near-tie ({da} vs {db})"
     return len(bad)
 
 
