@@ -317,7 +317,11 @@ __global__ __launch_bounds__(kCBlock) void nn_search_kernel(
         if (bound[1] > 0.0f) bound[1] = s1;
     }
     const int visited = culled_search(stage[wid], p4, tlo, thi, ntiles, S, split, qx, qy, qz, bound, bd, bj);
-    if (lane == 0 && counters) atomicAdd(counters, (unsigned long long)visited);
+    if (lane == 0 && counters) {  // spread over kCounterSlots cache lines (one address serialises)
+        unsigned long long* cs = counters + kCounterStride * ((blockIdx.x * kCWaves + wid + blockIdx.y) % kCounterSlots);
+        atomicAdd(cs, (unsigned long long)visited);
+        atomicMax(cs + 1, (unsigned long long)visited);
+    }
     unsigned long long* out = best + (size_t)slot * N;
 #pragma unroll
     for (int k = 0; k < kCQPT; ++k) {
@@ -587,7 +591,8 @@ hipError_t launch_gicp_pass(const orpcd_ctx* c, int nact, int pass, double r2, h
     }
     nn_search_kernel<<<dim3((unsigned)(sblk * S), (unsigned)nact), kCBlock, 0, s>>>(
         c->q32.p, N, c->tgt.p4.p, c->tgt.tlo.p, c->tgt.thi.p, (int)c->tgt.ntiles, c->active.p, c->done.p,
-        search_r2(r2), S, pass == 0 ? seed_stride_for(c->tgt.ntiles) : 0, c->prevnn.p, c->best.p, c->counters.p);
+        search_r2(r2), S, pass == 0 ? seed_stride_for(c->tgt.ntiles) : 0, c->prevnn.p, c->best.p,
+        c->count_tiles ? c->counters.p : nullptr);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     if (mid && (e = hipEventRecord(mid, s)) != hipSuccess) return e;
     const int ablk = accum_blocks(N);

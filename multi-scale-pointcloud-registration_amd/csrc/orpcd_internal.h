@@ -20,6 +20,8 @@ constexpr int kCBlockQ = kCBlock * kCQPT;      // queries per block (one start)
 constexpr int kNacc = 29;                      // JTJ(21) + JTr(6) + sum d2 + count
 constexpr int kPartialStride = 32;             // doubles per block partial
 constexpr float kFarCoord = 1.0e18f;           // padding coordinate
+constexpr int kCounterSlots = 256;             // profiling counters: {tiles, max tiles/wave} per slot
+constexpr int kCounterStride = 16;             // u64 per slot (128 B: one cache line each)
 
 // Device buffer that only grows (no hipMalloc inside steady-state loops).
 template <typename T>
@@ -121,7 +123,7 @@ struct orpcd_ctx {
     orpcd::DevBuf<double> out_fit, out_rmse;
     orpcd::DevBuf<int32_t> out_iters;
     orpcd::DevBuf<int64_t> out_ncorr;
-    orpcd::DevBuf<unsigned long long> counters;  // [0] tiles visited
+    orpcd::DevBuf<unsigned long long> counters;  // kCounterSlots x {tiles visited, max per wave}
 
     // kernel-level entry points
     orpcd::CloudLayout aux;
@@ -133,6 +135,7 @@ struct orpcd_ctx {
 
     // profiling
     bool profiling = false;
+    bool count_tiles = false;  // tile counters live only while timing (profiling / ORPCD_TRACE)
     std::vector<hipEvent_t> ev_pool;
     orpcd::KernelStats stats;
 };

@@ -78,6 +78,23 @@ int upload_target(orpcd_ctx* c, const double* xyz, int64_t m, double eps) {
     return ORPCD_OK;
 }
 
+// sum / max of the spread profiling counters (device -> host, synchronous on s)
+hipError_t read_counters(orpcd_ctx* c, unsigned long long& tiles, unsigned long long& maxw, bool reset_max) {
+    std::vector<unsigned long long> h((size_t)kCounterSlots * kCounterStride);
+    hipError_t e = hipMemcpyAsync(h.data(), c->counters.p, h.size() * 8, hipMemcpyDeviceToHost, c->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+    if (e != hipSuccess) return e;
+    tiles = 0;
+    maxw = 0;
+    for (int i = 0; i < kCounterSlots; ++i) {
+        tiles += h[(size_t)i * kCounterStride];
+        maxw = std::max(maxw, h[(size_t)i * kCounterStride + 1]);
+        if (reset_max) h[(size_t)i * kCounterStride + 1] = 0;
+    }
+    if (reset_max) e = hipMemcpyAsync(c->counters.p, h.data(), h.size() * 8, hipMemcpyHostToDevice, c->stream);
+    return e;
+}
+
 }  // namespace
 
 extern "C" {
@@ -103,7 +120,8 @@ int orpcd_ctx_create(int device, orpcd_ctx** out) {
     c->device = device;
     if (hipSetDevice(device) != hipSuccess ||
         hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
-        c->counters.ensure(4) != hipSuccess) {
+        c->counters.ensure(kCounterSlots * kCounterStride) != hipSuccess ||
+        hipMemset(c->counters.p, 0, kCounterSlots * kCounterStride * 8) != hipSuccess) {
         delete c;
         return ORPCD_EDEVICE;
     }
@@ -250,52 +268,56 @@ int orpcd_gicp_batch(orpcd_ctx* c, const double* R0, const double* t0, int32_t B
     CTX_CHECK(c, launch_xform(c, B, s));
 
     const double r2 = p->max_correspondence_distance * p->max_correspondence_distance;
-    unsigned long long tiles_before = 0;
-    if (c->profiling) CTX_CHECK(c, hipMemcpy(&tiles_before, c->counters.p, 8, hipMemcpyDeviceToHost));
+    unsigned long long tiles_before = 0, unused = 0;
+    if (c->profiling) CTX_CHECK(c, read_counters(c, tiles_before, unused, false));
     int nact = B;
     static const bool trace = getenv("ORPCD_TRACE") != nullptr;
     const bool timed = c->profiling || trace;
-    for (int pass = 0; pass <= p->max_iteration && nact > 0; ++pass) {
-        hipEvent_t e0 = nullptr, e1 = nullptr, e2 = nullptr;
-        if (timed) {
-            while (c->ev_pool.size() < 3) {
-                hipEvent_t e;
-                CTX_CHECK(c, hipEventCreate(&e));
-                c->ev_pool.push_back(e);
-            }
-            e0 = c->ev_pool[0];
-            e1 = c->ev_pool[1];
-            e2 = c->ev_pool[2];
-            CTX_CHECK(c, hipEventRecord(e0, s));
+    const int every = trace ? 1 : kSyncEvery;
+    c->count_tiles = timed;
+    if (timed) {
+        while ((int)c->ev_pool.size() < 3 * kSyncEvery) {
+            hipEvent_t e;
+            CTX_CHECK(c, hipEventCreate(&e));
+            c->ev_pool.push_back(e);
         }
-        CTX_CHECK(c, launch_gicp_pass(c, nact, pass, r2, s, e1));
-        if (timed) CTX_CHECK(c, hipEventRecord(e2, s));
+    }
+    int pending = 0;  // timed passes since the last host sync
+    for (int pass = 0; pass <= p->max_iteration && nact > 0; ++pass) {
+        hipEvent_t* ev = timed ? &c->ev_pool[3 * pending] : nullptr;
+        if (timed) CTX_CHECK(c, hipEventRecord(ev[0], s));
+        CTX_CHECK(c, launch_gicp_pass(c, nact, pass, r2, s, timed ? ev[1] : nullptr));
+        if (timed) CTX_CHECK(c, hipEventRecord(ev[2], s));
         CTX_CHECK(c, launch_gicp_solve(c, nact, pass, *p, s));
+        ++pending;
+        c->stats.passes += nact;
         // the host learns which starts finished only every few passes; a
         // finished start's blocks exit at once in the passes in between
-        const bool sync = timed || (pass % kSyncEvery) == kSyncEvery - 1 || pass == p->max_iteration;
-        c->stats.passes += nact;
+        const bool sync = (pass % every) == every - 1 || pass == p->max_iteration;
         if (!sync) continue;
         CTX_CHECK(c, hipMemcpyAsync(hDone, c->done.p, (size_t)B * 4, hipMemcpyDeviceToHost, s));
-        unsigned long long tiles_now = 0;
-        if (trace) CTX_CHECK(c, hipMemcpyAsync(&tiles_now, c->counters.p, 8, hipMemcpyDeviceToHost, s));
+        unsigned long long tiles_now[2] = {0, 0};
+        if (trace) CTX_CHECK(c, read_counters(c, tiles_now[0], tiles_now[1], true));
         CTX_CHECK(c, hipStreamSynchronize(s));
         if (timed) {
-            float ms = 0.f, ms2 = 0.f;
-            CTX_CHECK(c, hipEventElapsedTime(&ms, e0, e1));
-            CTX_CHECK(c, hipEventElapsedTime(&ms2, e1, e2));
-            if (c->profiling) {
-                c->stats.launches += 1;
-                c->stats.ms += ms;
-                c->stats.accum_ms += ms2;
-            }
-            if (trace) {
-                static unsigned long long last = 0;
-                fprintf(stderr, "[orpcd] pass %3d nact %3d search %.3f ms accum %.3f ms tiles %llu\n", pass, nact,
-                        ms, ms2, tiles_now - last);
-                last = tiles_now;
+            for (int q = 0; q < pending; ++q) {
+                float ms = 0.f, ms2 = 0.f;
+                CTX_CHECK(c, hipEventElapsedTime(&ms, c->ev_pool[3 * q], c->ev_pool[3 * q + 1]));
+                CTX_CHECK(c, hipEventElapsedTime(&ms2, c->ev_pool[3 * q + 1], c->ev_pool[3 * q + 2]));
+                if (c->profiling) {
+                    c->stats.launches += 1;
+                    c->stats.ms += ms;
+                    c->stats.accum_ms += ms2;
+                }
+                if (trace) {
+                    static unsigned long long last = 0;
+                    fprintf(stderr, "[orpcd] pass %3d nact %3d search %.3f ms accum %.3f ms tiles %llu max/wave %llu\n",
+                            pass, nact, ms, ms2, tiles_now[0] - last, tiles_now[1]);
+                    last = tiles_now[0];
+                }
             }
         }
+        pending = 0;
         int k = 0;
         for (int b = 0; b < nact; ++b)
             if (!hDone[hAct[b]]) hAct[k++] = hAct[b];
@@ -309,9 +331,9 @@ int orpcd_gicp_batch(orpcd_ctx* c, const double* R0, const double* t0, int32_t B
     CTX_CHECK(c, hipMemcpyAsync(hIters, c->out_iters.p, (size_t)B * 4, hipMemcpyDeviceToHost, s));
     std::vector<int64_t> nc((size_t)B);
     CTX_CHECK(c, hipMemcpyAsync(nc.data(), c->out_ncorr.p, (size_t)B * 8, hipMemcpyDeviceToHost, s));
-    unsigned long long tiles_after = 0;
-    if (c->profiling) CTX_CHECK(c, hipMemcpyAsync(&tiles_after, c->counters.p, 8, hipMemcpyDeviceToHost, s));
     CTX_CHECK(c, hipStreamSynchronize(s));
+    unsigned long long tiles_after = 0;
+    if (c->profiling) CTX_CHECK(c, read_counters(c, tiles_after, unused, false));
     if (c->profiling) {
         const double t = (double)(tiles_after - tiles_before);
         c->stats.tiles += t;
