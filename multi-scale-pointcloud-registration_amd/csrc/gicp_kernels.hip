@@ -99,7 +99,8 @@ constexpr unsigned kKeyMask = 0xFFFFFFC0u;  // d^2 bits kept in a scan key (low 
 // --------------------------------------------------------------------------
 __device__ __forceinline__ int culled_search(float4* stage, const float4* __restrict__ p4,
                                              const float4* __restrict__ tlo, const float4* __restrict__ thi,
-                                             int ntiles, int S, int s, const float qx[2], const float qy[2],
+                                             int ntiles, const float4* __restrict__ slo,
+                                             const float4* __restrict__ shi, int nsuper, int S, int s, const float qx[2], const float qy[2],
                                              const float qz[2], const float bound[2], float bd[2], int bj[2]) {
     const int lane = threadIdx.x & 63;
     const bool v0 = bound[0] > 0.0f, v1 = bound[1] > 0.0f;
@@ -122,15 +123,33 @@ __device__ __forceinline__ int culled_search(float4* stage, const float4* __rest
 
     // candidate cursor: rounds of 64 tiles, one tile per lane; wave-box test by
     // ballot, then the per-query test for each set bit.
-    int tb = -64;
+    // Two levels: super-tiles (64 tiles each) are tested 64 at a time against
+    // the wave box; the 64 tiles of each surviving super-tile form one round.
+    int sb = -64;                  // super-tile round base
+    unsigned long long smask = 0;  // surviving super-tiles of that round
+    int tb = 0;                    // tile round base (= super-tile * 64)
     unsigned long long mask = 0;
     float lb = inf;
     float4 a = make_float4(0.f, 0.f, 0.f, 0.f), b = a;
     auto next_candidate = [&](float& lbk) -> int {
         for (;;) {
             while (mask == 0) {
-                tb += 64;
-                if (tb >= ntiles) return -1;
+                while (smask == 0) {
+                    sb += 64;
+                    if (sb >= nsuper) return -1;
+                    const int u = sb + lane;
+                    float sl = inf;
+                    if (u < nsuper) {
+                        const float4 c = slo[u], d = shi[u];
+                        const float dx = fmaxf(0.0f, fmaxf(c.x - hix, lox - d.x));
+                        const float dy = fmaxf(0.0f, fmaxf(c.y - hiy, loy - d.y));
+                        const float dz = fmaxf(0.0f, fmaxf(c.z - hiz, loz - d.z));
+                        sl = dx * dx + dy * dy + dz * dz;
+                    }
+                    smask = __ballot(sl < W);
+                }
+                tb = (sb + __builtin_ctzll(smask)) * kSuper;
+                smask &= smask - 1;
                 const int t = tb + lane;
                 lb = inf;
                 if (t < ntiles && (S == 1 || t % S == s)) {
@@ -248,12 +267,17 @@ static inline float search_r2(double r2) { return (float)(r2 * (1.0 + 1e-5)) * 1
 // any closer one) is re-found by the scan (1e-4 >> the 2^-17 key truncation)
 constexpr float kSeedSlack = 1.0001f;
 
-// fp32 queries of every running start for the next pass: q = fp32(Q * p).
+// fp32 queries of every running start for the next pass: q = fp32(Q * p),
+// and in q.w the query's search bound: d^2 to its previous correspondence
+// (x 1 + 1e-4), or, without one, to the nearest of a strided set of tile
+// representatives (real targets, so either bound is valid), capped at r2s.
 __global__ __launch_bounds__(256) void xform_queries_kernel(const double* __restrict__ src, int N,
                                                             const int32_t* __restrict__ active,
                                                             const double* __restrict__ Qm,
                                                             const int32_t* __restrict__ done,
-                                                            float4* __restrict__ q32) {
+                                                            const float4* __restrict__ p4, int ntiles,
+                                                            int seed_stride, const int32_t* __restrict__ prevnn,
+                                                            float r2s, float4* __restrict__ q32) {
     const int slot = active[blockIdx.y];
     if (done[slot]) return;
     const int i = blockIdx.x * 256 + threadIdx.x;
@@ -264,7 +288,16 @@ __global__ __launch_bounds__(256) void xform_queries_kernel(const double* __rest
     const double p[3] = {src[3 * i], src[3 * i + 1], src[3 * i + 2]};
     double q[3];
     xform(Q, p, q);
-    q32[(size_t)slot * N + i] = make_float4((float)q[0], (float)q[1], (float)q[2], 0.0f);
+    const float x = (float)q[0], y = (float)q[1], z = (float)q[2];
+    float bound = r2s;
+    const int jp = prevnn[(size_t)slot * N + i];
+    if (jp >= 0) {
+        bound = fminf(bound, d2f(x, y, z, p4[jp]) * kSeedSlack + 1e-30f);
+    } else {
+        for (int t = 0; t < ntiles; t += seed_stride)
+            bound = fminf(bound, d2f(x, y, z, p4[t * kTile]) * kSeedSlack + 1e-30f);
+    }
+    q32[(size_t)slot * N + i] = make_float4(x, y, z, bound);
 }
 
 // --------------------------------------------------------------------------
@@ -272,9 +305,9 @@ __global__ __launch_bounds__(256) void xform_queries_kernel(const double* __rest
 // --------------------------------------------------------------------------
 __global__ __launch_bounds__(kCBlock) void nn_search_kernel(
     const float4* __restrict__ q32, int N, const float4* __restrict__ p4, const float4* __restrict__ tlo,
-    const float4* __restrict__ thi, int ntiles, const int32_t* __restrict__ active, const int32_t* __restrict__ done,
-    float r2s, int S, int seed_stride, const int32_t* __restrict__ prevnn, unsigned long long* __restrict__ best,
-    unsigned long long* __restrict__ counters) {
+    const float4* __restrict__ thi, int ntiles, const float4* __restrict__ slo, const float4* __restrict__ shi,
+    int nsuper, const int32_t* __restrict__ active, const int32_t* __restrict__ done, int S,
+    unsigned long long* __restrict__ best, unsigned long long* __restrict__ counters) {
     const int slot = active[blockIdx.y];
     if (done[slot]) return;
     __shared__ float4 stage[kCWaves][kTile];
@@ -283,40 +316,18 @@ __global__ __launch_bounds__(kCBlock) void nn_search_kernel(
     const int i0 = grp * kCBlockQ + wid * (64 * kCQPT) + lane;
     float qx[kCQPT], qy[kCQPT], qz[kCQPT], bound[kCQPT], bd[kCQPT];
     int bj[kCQPT];
-    const int32_t* pn = prevnn + (size_t)slot * N;
     const float4* qs = q32 + (size_t)slot * N;
-    bool need_seed = false;
 #pragma unroll
     for (int k = 0; k < kCQPT; ++k) {
         const int i = i0 + 64 * k;
-        bound[k] = 0.0f;
-        qx[k] = qy[k] = qz[k] = 0.0f;
-        if (i < N) {
-            const float4 q = qs[i];
-            qx[k] = q.x;
-            qy[k] = q.y;
-            qz[k] = q.z;
-            float bb = r2s;
-            const int jp = pn[i];
-            if (jp >= 0)
-                bb = fminf(bb, d2f(q.x, q.y, q.z, p4[jp]) * kSeedSlack + 1e-30f);
-            else
-                need_seed = true;
-            bound[k] = bb;
-        }
+        const float4 q = i < N ? qs[i] : make_float4(0.f, 0.f, 0.f, 0.f);
+        qx[k] = q.x;
+        qy[k] = q.y;
+        qz[k] = q.z;
+        bound[k] = q.w;  // 0 for padding lanes: never takes anything
     }
-    // pass-0 seed: strided tile representatives (real targets -> valid bounds)
-    if (seed_stride > 0 && __any(need_seed)) {
-        float s0 = bound[0], s1 = bound[1];
-        for (int t = 0; t < ntiles; t += seed_stride) {
-            const float4 rep = p4[t * kTile];
-            s0 = fminf(s0, d2f(qx[0], qy[0], qz[0], rep) * kSeedSlack + 1e-30f);
-            s1 = fminf(s1, d2f(qx[1], qy[1], qz[1], rep) * kSeedSlack + 1e-30f);
-        }
-        if (bound[0] > 0.0f) bound[0] = s0;
-        if (bound[1] > 0.0f) bound[1] = s1;
-    }
-    const int visited = culled_search(stage[wid], p4, tlo, thi, ntiles, S, split, qx, qy, qz, bound, bd, bj);
+    const int visited =
+        culled_search(stage[wid], p4, tlo, thi, ntiles, slo, shi, nsuper, S, split, qx, qy, qz, bound, bd, bj);
     if (lane == 0 && counters) {  // spread over kCounterSlots cache lines (one address serialises)
         unsigned long long* cs = counters + kCounterStride * ((blockIdx.x * kCWaves + wid + blockIdx.y) % kCounterSlots);
         atomicAdd(cs, (unsigned long long)visited);
@@ -518,8 +529,9 @@ __global__ __launch_bounds__(64) void gicp_solve_kernel(const int32_t* __restric
 // accumulation.  Queries in input order.
 __global__ __launch_bounds__(kCBlock) void nn1_kernel(const double* __restrict__ q64, int nq,
                                                       const float4* __restrict__ p4, const float4* __restrict__ tlo,
-                                                      const float4* __restrict__ thi, int ntiles, int seed_stride,
-                                                      const double* __restrict__ tgt64,
+                                                      const float4* __restrict__ thi, int ntiles,
+                                                      const float4* __restrict__ slo, const float4* __restrict__ shi,
+                                                      int nsuper, int seed_stride, const double* __restrict__ tgt64,
                                                       const int32_t* __restrict__ tperm, double r2, float r2s,
                                                       int32_t* __restrict__ idx, double* __restrict__ d2o) {
     __shared__ float4 stage[kCWaves][kTile];
@@ -540,7 +552,7 @@ __global__ __launch_bounds__(kCBlock) void nn1_kernel(const double* __restrict__
                 b = fminf(b, d2f(qx[k], qy[k], qz[k], p4[t * kTile]) * kSeedSlack + 1e-30f);
         bound[k] = b;
     }
-    culled_search(stage[wid], p4, tlo, thi, ntiles, 1, 0, qx, qy, qz, bound, bd, bj);
+    culled_search(stage[wid], p4, tlo, thi, ntiles, slo, shi, nsuper, 1, 0, qx, qy, qz, bound, bd, bj);
 #pragma unroll
     for (int k = 0; k < kCQPT; ++k) {
         const int i = i0 + 64 * k;
@@ -567,16 +579,17 @@ int seed_stride_for(int64_t ntiles) {  // at most ~512 representatives per query
 
 int search_splits(int nact, int blocks_per_start) {
     const int64_t waves = (int64_t)nact * blocks_per_start * kCWaves;
-    const int64_t want = 8192;  // ~8 waves per SIMD on 256 CUs x 4 SIMDs
+    const int64_t want = 4096;  // ~4 waves per SIMD on 256 CUs x 4 SIMDs
     return (int)std::min<int64_t>(16, std::max<int64_t>(1, (want + waves - 1) / waves));
 }
 
 int accum_blocks(int64_t N) { return (int)((N + 255) / 256); }
 
-hipError_t launch_xform(const orpcd_ctx* c, int nact, hipStream_t s) {
+hipError_t launch_xform(const orpcd_ctx* c, int nact, double r2, hipStream_t s) {
     const int N = (int)c->src.n;
     xform_queries_kernel<<<dim3((unsigned)((N + 255) / 256), (unsigned)nact), 256, 0, s>>>(
-        c->src.xyz64.p, N, c->active.p, c->Q.p, c->done.p, c->q32.p);
+        c->src.xyz64.p, N, c->active.p, c->Q.p, c->done.p, c->tgt.p4.p, (int)c->tgt.ntiles,
+        seed_stride_for(c->tgt.ntiles), c->prevnn.p, search_r2(r2), c->q32.p);
     return hipGetLastError();
 }
 
@@ -590,9 +603,8 @@ hipError_t launch_gicp_pass(const orpcd_ctx* c, int nact, int pass, double r2, h
         if (e != hipSuccess) return e;
     }
     nn_search_kernel<<<dim3((unsigned)(sblk * S), (unsigned)nact), kCBlock, 0, s>>>(
-        c->q32.p, N, c->tgt.p4.p, c->tgt.tlo.p, c->tgt.thi.p, (int)c->tgt.ntiles, c->active.p, c->done.p,
-        search_r2(r2), S, pass == 0 ? seed_stride_for(c->tgt.ntiles) : 0, c->prevnn.p, c->best.p,
-        c->count_tiles ? c->counters.p : nullptr);
+        c->q32.p, N, c->tgt.p4.p, c->tgt.tlo.p, c->tgt.thi.p, (int)c->tgt.ntiles, c->tgt.slo.p, c->tgt.shi.p,
+        (int)c->tgt.nsuper, c->active.p, c->done.p, S, c->best.p, c->count_tiles ? c->counters.p : nullptr);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     if (mid && (e = hipEventRecord(mid, s)) != hipSuccess) return e;
     const int ablk = accum_blocks(N);
@@ -610,15 +622,17 @@ hipError_t launch_gicp_solve(const orpcd_ctx* c, int nact, int pass, const orpcd
                                                     p.relative_rmse, a);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
-    return launch_xform(c, nact, s);  // queries of the next pass (done starts skip)
+    const double r2 = p.max_correspondence_distance * p.max_correspondence_distance;
+    return launch_xform(c, nact, r2, s);  // queries of the next pass (done starts skip)
 }
 
 hipError_t launch_nn1(const double* q, int64_t nq, const CloudLayout& t, double r2, int32_t* idx, double* d2,
                       hipStream_t s) {
     if (nq <= 0) return hipSuccess;
     const unsigned grid = (unsigned)((nq + kCBlockQ - 1) / kCBlockQ);
-    nn1_kernel<<<grid, kCBlock, 0, s>>>(q, (int)nq, t.p4.p, t.tlo.p, t.thi.p, (int)t.ntiles, seed_stride_for(t.ntiles),
-                                        t.xyz64.p, t.perm.p, r2, search_r2(r2), idx, d2);
+    nn1_kernel<<<grid, kCBlock, 0, s>>>(q, (int)nq, t.p4.p, t.tlo.p, t.thi.p, (int)t.ntiles, t.slo.p, t.shi.p,
+                                        (int)t.nsuper, seed_stride_for(t.ntiles), t.xyz64.p, t.perm.p, r2,
+                                        search_r2(r2), idx, d2);
     return hipGetLastError();
 }
 

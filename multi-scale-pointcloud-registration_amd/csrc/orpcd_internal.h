@@ -13,6 +13,7 @@ namespace orpcd {
 
 // ------------------------------------------------------------- geometry
 constexpr int kTile = 64;                      // targets per culling tile (one wave-wide load)
+constexpr int kSuper = 64;                     // tiles per super-tile (first culling level)
 constexpr int kCQPT = 2;                       // queries per lane in the culled search
 constexpr int kCWaves = 4;                     // waves per block
 constexpr int kCBlock = 64 * kCWaves;          // threads per block
@@ -66,11 +67,12 @@ struct HostBuf {  // pinned
 
 // A cloud in device memory, in Morton order (sort_kernels.hip).
 struct CloudLayout {
-    int64_t n = 0, npad = 0, ntiles = 0;
+    int64_t n = 0, npad = 0, ntiles = 0, nsuper = 0;
     DevBuf<double> xyz64;     // n*3, Morton order
     DevBuf<int32_t> perm;     // Morton position -> input index
     DevBuf<float4> p4;        // npad fp32 (x,y,z, input index bits), padded far
     DevBuf<float4> tlo, thi;  // per 64-point tile AABB
+    DevBuf<float4> slo, shi;  // per super-tile (64 tiles) AABB
     DevBuf<uint32_t> codes;   // scratch (2n)
     DevBuf<int32_t> ids;      // scratch
     DevBuf<unsigned char> sort_tmp;
@@ -80,6 +82,8 @@ struct CloudLayout {
         p4.release();
         tlo.release();
         thi.release();
+        slo.release();
+        shi.release();
         codes.release();
         ids.release();
         sort_tmp.release();
@@ -155,7 +159,7 @@ hipError_t launch_normals_cov(const double* rawcov6, int64_t n, const double* Rc
 
 // gicp_kernels.hip
 int accum_blocks(int64_t N);
-hipError_t launch_xform(const orpcd_ctx* c, int nact, hipStream_t s);
+hipError_t launch_xform(const orpcd_ctx* c, int nact, double r2, hipStream_t s);
 hipError_t launch_gicp_pass(const orpcd_ctx* c, int nact, int pass, double r2, hipStream_t s, hipEvent_t mid);
 hipError_t launch_gicp_solve(const orpcd_ctx* c, int nact, int pass, const orpcd_gicp_params& p, hipStream_t s);
 hipError_t launch_nn1(const double* q, int64_t nq, const CloudLayout& t, double r2, int32_t* idx, double* d2,

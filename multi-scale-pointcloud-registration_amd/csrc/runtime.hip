@@ -265,7 +265,7 @@ int orpcd_gicp_batch(orpcd_ctx* c, const double* R0, const double* t0, int32_t B
 
     // posed-frame source covariances for every start (rigid equivariance)
     CTX_CHECK(c, launch_normals_cov(c->sraw.p, N, c->scratch64c.p, B, p->epsilon, nullptr, c->scov.p, s));
-    CTX_CHECK(c, launch_xform(c, B, s));
+    CTX_CHECK(c, launch_xform(c, B, p->max_correspondence_distance * p->max_correspondence_distance, s));
 
     const double r2 = p->max_correspondence_distance * p->max_correspondence_distance;
     unsigned long long tiles_before = 0, unused = 0;

@@ -73,6 +73,26 @@ __global__ void tile_aabb_kernel(const float4* __restrict__ p4, int n, int ntile
     hi[t] = make_float4(mxx, mxy, mxz, 0.f);
 }
 
+// One thread per super-tile (64 tiles): AABB of the tile AABBs.
+__global__ void super_aabb_kernel(const float4* __restrict__ tlo, const float4* __restrict__ thi, int ntiles,
+                                  int nsuper, float4* __restrict__ slo, float4* __restrict__ shi) {
+    const int u = blockIdx.x * blockDim.x + threadIdx.x;
+    if (u >= nsuper) return;
+    float4 lo = make_float4(3.0e38f, 3.0e38f, 3.0e38f, 0.f), hi = make_float4(-3.0e38f, -3.0e38f, -3.0e38f, 0.f);
+    const int end = min(ntiles, (u + 1) * kSuper);
+    for (int t = u * kSuper; t < end; ++t) {
+        const float4 a = tlo[t], b = thi[t];
+        lo.x = fminf(lo.x, a.x);
+        lo.y = fminf(lo.y, a.y);
+        lo.z = fminf(lo.z, a.z);
+        hi.x = fmaxf(hi.x, b.x);
+        hi.y = fmaxf(hi.y, b.y);
+        hi.z = fmaxf(hi.z, b.z);
+    }
+    slo[u] = lo;
+    shi[u] = hi;
+}
+
 // Scatter per-point rows from Morton order back to input order.
 __global__ void unpermute_kernel(const double* __restrict__ in, const int32_t* __restrict__ perm, int n, int w,
                                  double* __restrict__ out) {
@@ -96,6 +116,9 @@ hipError_t build_layout(const double* dev_in64, int64_t n, const double bbox_lo[
         if ((e = L.p4.ensure((size_t)L.npad)) != hipSuccess) return e;
         if ((e = L.tlo.ensure((size_t)L.ntiles)) != hipSuccess) return e;
         if ((e = L.thi.ensure((size_t)L.ntiles)) != hipSuccess) return e;
+        L.nsuper = (L.ntiles + kSuper - 1) / kSuper;
+        if ((e = L.slo.ensure((size_t)L.nsuper)) != hipSuccess) return e;
+        if ((e = L.shi.ensure((size_t)L.nsuper)) != hipSuccess) return e;
     }
     const double scale = bbox_ext > 0 ? 1023.0 / bbox_ext : 0.0;
     const unsigned g = (unsigned)((n + 255) / 256);
@@ -116,6 +139,9 @@ hipError_t build_layout(const double* dev_in64, int64_t n, const double bbox_lo[
     if (with_tiles) {
         tile_aabb_kernel<<<(unsigned)((L.ntiles + 255) / 256), 256, 0, s>>>(L.p4.p, (int)n, (int)L.ntiles, L.tlo.p,
                                                                            L.thi.p);
+        if ((e = hipGetLastError()) != hipSuccess) return e;
+        super_aabb_kernel<<<(unsigned)((L.nsuper + 255) / 256), 256, 0, s>>>(L.tlo.p, L.thi.p, (int)L.ntiles,
+                                                                            (int)L.nsuper, L.slo.p, L.shi.p);
         if ((e = hipGetLastError()) != hipSuccess) return e;
     }
     return hipSuccess;
