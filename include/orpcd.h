@@ -117,6 +117,14 @@ int orpcd_fgr(orpcd_ctx* ctx, const double* src, int64_t n, const double* tgt, i
               double* T_out, double* fitness_out, double* rmse_out, int64_t* ncorr_out,
               int64_t* n_mutual_out);
 
+/* Tuning knobs (defaults are the measured best on MI355X):
+ *   "search_waves"  split a start's tiles over waves until ~this many run
+ *   "sync_every"    passes between host checks of the per-start done flags
+ *   "super_cull"    0/1: first culling level over 64-tile super-tiles
+ *   "reseed"        0/1: representative seeding for queries that found no
+ *                   target within radius in the previous pass             */
+int orpcd_set_option(orpcd_ctx* ctx, const char* key, double value);
+
 /* ------------------------------------------------------------ measurement
  * Live kernel timing (hipEvents on the context's stream).  When enabled,
  * every launch of the dominant correspondence kernel is bracketed.

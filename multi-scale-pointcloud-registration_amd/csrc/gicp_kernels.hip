@@ -89,6 +89,8 @@ __device__ __forceinline__ float box_d2(float x, float y, float z, float lx, flo
 }
 
 constexpr unsigned long long kNone = ~0ull;
+constexpr int kNoSeed = -1;   // prevnn before the first pass (representative seed)
+constexpr int kNoMatch = -2;  // no target within the search radius last pass
 constexpr unsigned kKeyMask = 0xFFFFFFC0u;  // d^2 bits kept in a scan key (low 6 = tile-local index)
 
 // --------------------------------------------------------------------------
@@ -100,7 +102,8 @@ constexpr unsigned kKeyMask = 0xFFFFFFC0u;  // d^2 bits kept in a scan key (low 
 __device__ __forceinline__ int culled_search(float4* stage, const float4* __restrict__ p4,
                                              const float4* __restrict__ tlo, const float4* __restrict__ thi,
                                              int ntiles, const float4* __restrict__ slo,
-                                             const float4* __restrict__ shi, int nsuper, int S, int s, const float qx[2], const float qy[2],
+                                             const float4* __restrict__ shi, int nsuper, int super_cull, int S, int s,
+                                             const float qx[2], const float qy[2],
                                              const float qz[2], const float bound[2], float bd[2], int bj[2]) {
     const int lane = threadIdx.x & 63;
     const bool v0 = bound[0] > 0.0f, v1 = bound[1] > 0.0f;
@@ -139,7 +142,9 @@ __device__ __forceinline__ int culled_search(float4* stage, const float4* __rest
                     if (sb >= nsuper) return -1;
                     const int u = sb + lane;
                     float sl = inf;
-                    if (u < nsuper) {
+                    if (u < nsuper && !super_cull) {
+                        sl = 0.0f;
+                    } else if (u < nsuper) {
                         const float4 c = slo[u], d = shi[u];
                         const float dx = fmaxf(0.0f, fmaxf(c.x - hix, lox - d.x));
                         const float dy = fmaxf(0.0f, fmaxf(c.y - hiy, loy - d.y));
@@ -277,7 +282,7 @@ __global__ __launch_bounds__(256) void xform_queries_kernel(const double* __rest
                                                             const int32_t* __restrict__ done,
                                                             const float4* __restrict__ p4, int ntiles,
                                                             int seed_stride, const int32_t* __restrict__ prevnn,
-                                                            float r2s, float4* __restrict__ q32) {
+                                                            float r2s, int reseed, float4* __restrict__ q32) {
     const int slot = active[blockIdx.y];
     if (done[slot]) return;
     const int i = blockIdx.x * 256 + threadIdx.x;
@@ -293,7 +298,7 @@ __global__ __launch_bounds__(256) void xform_queries_kernel(const double* __rest
     const int jp = prevnn[(size_t)slot * N + i];
     if (jp >= 0) {
         bound = fminf(bound, d2f(x, y, z, p4[jp]) * kSeedSlack + 1e-30f);
-    } else {
+    } else if (jp == kNoSeed || reseed) {
         for (int t = 0; t < ntiles; t += seed_stride)
             bound = fminf(bound, d2f(x, y, z, p4[t * kTile]) * kSeedSlack + 1e-30f);
     }
@@ -306,7 +311,7 @@ __global__ __launch_bounds__(256) void xform_queries_kernel(const double* __rest
 __global__ __launch_bounds__(kCBlock) void nn_search_kernel(
     const float4* __restrict__ q32, int N, const float4* __restrict__ p4, const float4* __restrict__ tlo,
     const float4* __restrict__ thi, int ntiles, const float4* __restrict__ slo, const float4* __restrict__ shi,
-    int nsuper, const int32_t* __restrict__ active, const int32_t* __restrict__ done, int S,
+    int nsuper, int super_cull, const int32_t* __restrict__ active, const int32_t* __restrict__ done, int S,
     unsigned long long* __restrict__ best, unsigned long long* __restrict__ counters) {
     const int slot = active[blockIdx.y];
     if (done[slot]) return;
@@ -327,7 +332,8 @@ __global__ __launch_bounds__(kCBlock) void nn_search_kernel(
         bound[k] = q.w;  // 0 for padding lanes: never takes anything
     }
     const int visited =
-        culled_search(stage[wid], p4, tlo, thi, ntiles, slo, shi, nsuper, S, split, qx, qy, qz, bound, bd, bj);
+        culled_search(stage[wid], p4, tlo, thi, ntiles, slo, shi, nsuper, super_cull, S, split, qx, qy, qz, bound,
+                      bd, bj);
     if (lane == 0 && counters) {  // spread over kCounterSlots cache lines (one address serialises)
         unsigned long long* cs = counters + kCounterStride * ((blockIdx.x * kCWaves + wid + blockIdx.y) % kCounterSlots);
         atomicAdd(cs, (unsigned long long)visited);
@@ -368,7 +374,7 @@ __global__ __launch_bounds__(256) void gicp_accum_kernel(
     if (i < N) {
         const unsigned long long v = best[(size_t)slot * N + i];
         const int j = v == kNone ? -1 : (int)(unsigned)(v & 0xffffffffu);
-        prevnn[(size_t)slot * N + i] = j;
+        prevnn[(size_t)slot * N + i] = j >= 0 ? j : kNoMatch;
         if (j >= 0) {
             double Q[12], R[9];
 #pragma unroll
@@ -552,7 +558,7 @@ __global__ __launch_bounds__(kCBlock) void nn1_kernel(const double* __restrict__
                 b = fminf(b, d2f(qx[k], qy[k], qz[k], p4[t * kTile]) * kSeedSlack + 1e-30f);
         bound[k] = b;
     }
-    culled_search(stage[wid], p4, tlo, thi, ntiles, slo, shi, nsuper, 1, 0, qx, qy, qz, bound, bd, bj);
+    culled_search(stage[wid], p4, tlo, thi, ntiles, slo, shi, nsuper, 1, 1, 0, qx, qy, qz, bound, bd, bj);
 #pragma unroll
     for (int k = 0; k < kCQPT; ++k) {
         const int i = i0 + 64 * k;
@@ -577,9 +583,8 @@ int seed_stride_for(int64_t ntiles) {  // at most ~512 representatives per query
     return (int)std::max<int64_t>(1, (ntiles + 511) / 512);
 }
 
-int search_splits(int nact, int blocks_per_start) {
+int search_splits(int nact, int blocks_per_start, int want) {
     const int64_t waves = (int64_t)nact * blocks_per_start * kCWaves;
-    const int64_t want = 4096;  // ~4 waves per SIMD on 256 CUs x 4 SIMDs
     return (int)std::min<int64_t>(16, std::max<int64_t>(1, (want + waves - 1) / waves));
 }
 
@@ -589,14 +594,14 @@ hipError_t launch_xform(const orpcd_ctx* c, int nact, double r2, hipStream_t s) 
     const int N = (int)c->src.n;
     xform_queries_kernel<<<dim3((unsigned)((N + 255) / 256), (unsigned)nact), 256, 0, s>>>(
         c->src.xyz64.p, N, c->active.p, c->Q.p, c->done.p, c->tgt.p4.p, (int)c->tgt.ntiles,
-        seed_stride_for(c->tgt.ntiles), c->prevnn.p, search_r2(r2), c->q32.p);
+        seed_stride_for(c->tgt.ntiles), c->prevnn.p, search_r2(r2), c->opt.reseed, c->q32.p);
     return hipGetLastError();
 }
 
 hipError_t launch_gicp_pass(const orpcd_ctx* c, int nact, int pass, double r2, hipStream_t s, hipEvent_t mid) {
     const int N = (int)c->src.n;
     const int sblk = (N + kCBlockQ - 1) / kCBlockQ;
-    const int S = search_splits(nact, sblk);
+    const int S = search_splits(nact, sblk, c->opt.search_waves);
     hipError_t e;
     if (S > 1) {  // splits merge by atomicMin: reset every slot's result
         e = hipMemsetAsync(c->best.p, 0xff, c->best.n * sizeof(unsigned long long), s);
@@ -604,7 +609,8 @@ hipError_t launch_gicp_pass(const orpcd_ctx* c, int nact, int pass, double r2, h
     }
     nn_search_kernel<<<dim3((unsigned)(sblk * S), (unsigned)nact), kCBlock, 0, s>>>(
         c->q32.p, N, c->tgt.p4.p, c->tgt.tlo.p, c->tgt.thi.p, (int)c->tgt.ntiles, c->tgt.slo.p, c->tgt.shi.p,
-        (int)c->tgt.nsuper, c->active.p, c->done.p, S, c->best.p, c->count_tiles ? c->counters.p : nullptr);
+        (int)c->tgt.nsuper, c->opt.super_cull, c->active.p, c->done.p, S, c->best.p,
+        c->count_tiles ? c->counters.p : nullptr);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     if (mid && (e = hipEventRecord(mid, s)) != hipSuccess) return e;
     const int ablk = accum_blocks(N);

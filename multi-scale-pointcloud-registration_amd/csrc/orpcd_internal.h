@@ -140,6 +140,14 @@ struct orpcd_ctx {
     // profiling
     bool profiling = false;
     bool count_tiles = false;  // tile counters live only while timing (profiling / ORPCD_TRACE)
+
+    // tunables (orpcd_set_option): defaults are the measured best on MI355X
+    struct Options {
+        int search_waves = 8192;  // split a start's tiles until ~this many waves run
+        int sync_every = 4;       // passes between host checks of the done flags
+        int super_cull = 1;       // first culling level over 64-tile super-tiles
+        int reseed = 0;           // representative seeding also after pass 0
+    } opt;
     std::vector<hipEvent_t> ev_pool;
     orpcd::KernelStats stats;
 };

@@ -12,7 +12,6 @@
 
 using namespace orpcd;
 
-static constexpr int kSyncEvery = 4;  // passes between host checks of the done flags
 
 #define CTX_CHECK(ctx, call)                                                                          \
     do {                                                                                              \
@@ -273,10 +272,10 @@ int orpcd_gicp_batch(orpcd_ctx* c, const double* R0, const double* t0, int32_t B
     int nact = B;
     static const bool trace = getenv("ORPCD_TRACE") != nullptr;
     const bool timed = c->profiling || trace;
-    const int every = trace ? 1 : kSyncEvery;
+    const int every = trace ? 1 : std::max(1, c->opt.sync_every);
     c->count_tiles = timed;
     if (timed) {
-        while ((int)c->ev_pool.size() < 3 * kSyncEvery) {
+        while ((int)c->ev_pool.size() < 3 * every) {
             hipEvent_t e;
             CTX_CHECK(c, hipEventCreate(&e));
             c->ev_pool.push_back(e);
@@ -433,6 +432,21 @@ int orpcd_fgr(orpcd_ctx* c, const double*, int64_t, const double*, int64_t, cons
     if (!c) return ORPCD_EINVAL;
     c->err = "fgr: not built in this revision";
     return ORPCD_EINVAL;
+}
+
+int orpcd_set_option(orpcd_ctx* c, const char* key, double value) {
+    if (!c || !key) return ORPCD_EINVAL;
+    const std::string k(key);
+    const int v = (int)value;
+    if (k == "search_waves" && v >= 1) c->opt.search_waves = v;
+    else if (k == "sync_every" && v >= 1 && v <= 64) c->opt.sync_every = v;
+    else if (k == "super_cull" && (v == 0 || v == 1)) c->opt.super_cull = v;
+    else if (k == "reseed" && (v == 0 || v == 1)) c->opt.reseed = v;
+    else {
+        c->err = "set_option: unknown key or bad value: " + k;
+        return ORPCD_EINVAL;
+    }
+    return ORPCD_OK;
 }
 
 int orpcd_profiling(orpcd_ctx* c, int32_t enable) {

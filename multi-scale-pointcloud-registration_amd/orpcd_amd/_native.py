@@ -46,8 +46,8 @@ _lib_lock = threading.Lock()
 # every symbol include/orpcd.h declares (checked by tests/test_abi.py)
 EXPORTED = ("orpcd_abi_version", "orpcd_device_count", "orpcd_ctx_create", "orpcd_ctx_destroy",
             "orpcd_last_error", "orpcd_set_target", "orpcd_set_source", "orpcd_gicp_batch",
-            "orpcd_nn1_radius", "orpcd_estimate_normals", "orpcd_fpfh", "orpcd_fgr", "orpcd_profiling",
-            "orpcd_stats", "orpcd_reset_stats")
+            "orpcd_nn1_radius", "orpcd_estimate_normals", "orpcd_fpfh", "orpcd_fgr", "orpcd_set_option",
+            "orpcd_profiling", "orpcd_stats", "orpcd_reset_stats")
 
 
 def load_library():
@@ -77,6 +77,7 @@ def load_library():
         L.orpcd_fpfh.argtypes = [vp, _f64p, c_i64, c_dbl, ctypes.c_int32, c_dbl, ctypes.c_int32, _f64p, _f64p]
         L.orpcd_fgr.argtypes = [vp, _f64p, c_i64, _f64p, c_i64, _f64p, _f64p, ctypes.POINTER(FgrParams), _f64p,
                                 _f64p, _f64p, _i64p, _i64p]
+        L.orpcd_set_option.argtypes = [vp, ctypes.c_char_p, c_dbl]
         L.orpcd_profiling.argtypes = [vp, ctypes.c_int32]
         L.orpcd_stats.argtypes = [vp, _f64p, ctypes.c_int32]
         L.orpcd_reset_stats.argtypes = [vp]
@@ -219,6 +220,9 @@ class Context:
                                       ctypes.byref(p), T, fit, rmse, nc, nm), "orpcd_fgr")
         return dict(T=T.reshape(4, 4), fitness=float(fit[0]), rmse=float(rmse[0]), ncorr=int(nc[0]),
                     n_mutual=int(nm[0]), n_tuple_corr=int(nm[1]))
+
+    def set_option(self, key: str, value: float):
+        self._check(self._L.orpcd_set_option(self._h, key.encode(), float(value)), "orpcd_set_option")
 
     # ---------------------------------------------------------- measuring
     def profiling(self, enable: bool = True):
