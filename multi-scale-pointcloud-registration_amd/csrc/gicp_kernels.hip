@@ -585,7 +585,7 @@ int seed_stride_for(int64_t ntiles) {  // at most ~512 representatives per query
 
 int search_splits(int nact, int blocks_per_start, int want) {
     const int64_t waves = (int64_t)nact * blocks_per_start * kCWaves;
-    return (int)std::min<int64_t>(16, std::max<int64_t>(1, (want + waves - 1) / waves));
+    return (int)std::min<int64_t>(64, std::max<int64_t>(1, (want + waves - 1) / waves));
 }
 
 int accum_blocks(int64_t N) { return (int)((N + 255) / 256); }

@@ -143,7 +143,7 @@ struct orpcd_ctx {
 
     // tunables (orpcd_set_option): defaults are the measured best on MI355X
     struct Options {
-        int search_waves = 8192;  // split a start's tiles until ~this many waves run
+        int search_waves = 32768;  // split a start's tiles until ~this many waves run (A/B: tools/ab_search.py)
         int sync_every = 4;       // passes between host checks of the done flags
         int super_cull = 1;       // first culling level over 64-tile super-tiles
         int reseed = 0;           // representative seeding also after pass 0

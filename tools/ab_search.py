@@ -20,7 +20,7 @@ from workloads import c2_pair, rot_xyz  # noqa: E402
 
 
 def main():
-    args = [a for a in sys.argv[1:] if not a.startswith("--")]
+    args = [a for a in sys.argv[1:] if a.startswith("{")]
     rounds = int(sys.argv[sys.argv.index("--rounds") + 1]) if "--rounds" in sys.argv else 5
     points = int(sys.argv[sys.argv.index("--points") + 1]) if "--points" in sys.argv else 50000
     B = int(sys.argv[sys.argv.index("--starts") + 1]) if "--starts" in sys.argv else 30
@@ -39,7 +39,7 @@ def main():
     iters = {}
     for _ in range(rounds):
         for i, cfg in enumerate(configs):
-            for k, v in {"search_waves": 8192, "sync_every": 4, "super_cull": 1, "reseed": 0, **cfg}.items():
+            for k, v in {"search_waves": 32768, "sync_every": 4, "super_cull": 1, "reseed": 0, **cfg}.items():
                 ctx.set_option(k, v)
             t1 = time.perf_counter()
             r = ctx.gicp_batch(R0, t0)
