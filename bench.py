@@ -106,6 +106,7 @@ def main():
         st["ms"], st["launches"], st["pairs"] = (float(x) for x in s.tolist())
 
     value = iters / elapsed
+    traffic, traffic_src = pmc_traffic()
     avg_ms = st["ms"] / max(st["launches"], 1)
     flops_per_launch = st["pairs"] / max(st["launches"], 1) * FLOP_PER_PAIR
     achieved = flops_per_launch / (avg_ms * 1e-3) / 1e12 if avg_ms > 0 else 0.0
@@ -142,7 +143,8 @@ def main():
                        "points": args.points, "attempts_per_step": args.attempts,
                        "parallelism": f"attempts sharded over {world} GPU(s)"},
             "roofline": {"bound": "mfma", "achieved": round(achieved, 3), "peak": FP32_PEAK_TFLOPS,
-                         "unit": "TFLOP/s", "frac": round(achieved / FP32_PEAK_TFLOPS, 4), "traffic": None,
+                         "unit": "TFLOP/s", "frac": round(achieved / FP32_PEAK_TFLOPS, 4), "traffic": traffic,
+                         "traffic_source": traffic_src,
                          "kernel": "nn_search_kernel", "avg_launch_ms": round(avg_ms, 4),
                          "accum_kernel_ms_total": round(st["accum_ms"], 3), "search_kernel_ms_total": round(st["ms"], 3),
                          "launches": int(st["launches"]), "flop_per_pair": FLOP_PER_PAIR,
@@ -156,6 +158,20 @@ def main():
         print(json.dumps(line))
     if dist is not None:
         dist.destroy_process_group()
+
+
+def pmc_traffic(kernel="orpcd::nn_search_kernel"):
+    """HBM bytes per launch of `kernel` from the newest committed PMC summary
+    (profiles/rNN_hbm.json: FETCH_SIZE x2 + WRITE_SIZE, MI355X_MICROARCH.md
+    §HBM), collected by rocprofv3 --pmc on this same bench command."""
+    import glob
+    files = sorted(glob.glob(os.path.join(REPO, "profiles", "r*_hbm.json")))
+    if not files:
+        return None, None
+    d = json.load(open(files[-1]))
+    if kernel not in d:
+        return None, None
+    return d[kernel]["hbm_bytes_per_launch_corrected"], os.path.basename(files[-1])
 
 
 def cpu_baseline(source, target, args):
