@@ -1,0 +1,65 @@
+"""N>1 path on CPU: the multistart sharded over a world_size-2 gloo group must
+reproduce the single-process result (and the reference's golden trace G3)."""
+import os
+import socket
+import sys
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN, PKG, REPO
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, out_dir):
+    sys.path[:0] = [PKG, os.path.join(REPO, "tests", "golden"), os.path.join(REPO, "tests")]
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch.distributed as dist
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from orpcd_amd import Aligner, Preprocessor
+    from scripted import ScriptedOptimizer
+    from test_host import BatchedScripted
+    g = np.load(f"{GOLDEN}/g3_aligner_trace.npz")
+    np.random.seed(7)
+    inner = ScriptedOptimizer(g["goal"], mode="scripted")
+    opt = BatchedScripted(inner)
+    al = Aligner(Preprocessor([]), Preprocessor([]), opt, attempts=4)
+    T, m, sf, err = al.align(g["src"].copy(), g["tgt"].copy(), refine_registration=False)
+    np.savez(os.path.join(out_dir, f"rank{rank}.npz"), T=T, m=m, sf=sf, err=np.asarray(err),
+             batches=np.asarray(opt.batches), rng=np.random.uniform(size=4))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_sharded_multistart_matches_reference_trace(tmp_path, world):
+    import torch.multiprocessing as mp
+    mp.start_processes(_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True,
+                       start_method="spawn")
+    g = np.load(f"{GOLDEN}/g3_aligner_trace.npz")
+    shards = []
+    for r in range(world):
+        z = np.load(tmp_path / f"rank{r}.npz")
+        assert np.array_equal(z["T"], g["scripted_T"]) and z["m"] == g["scripted_metric"]
+        assert np.array_equal(z["sf"], g["scripted_sf"]) and np.array_equal(z["err"], g["scripted_errors"])
+        assert np.array_equal(z["rng"], g["scripted_rng_after"])  # every rank replays the full RNG stream
+        shards.append(z["batches"])
+    # attempts (4 per multistart) were split over the ranks, each multistart
+    per_ms = np.sum(np.stack(shards), axis=0)
+    assert np.all(per_ms == 4) and all(np.all(s < 4) for s in shards)
+
+
+def test_record_pack_roundtrip():
+    from orpcd_amd import parallel
+    rng = np.random.default_rng(0)
+    r = dict(rmse=rng.random(5), fitness=rng.random(5), iters=np.arange(5), ncorr=np.arange(5) * 7,
+             T=rng.random((5, 4, 4)))
+    u = parallel.unpack(parallel.pack(r))
+    for k in r:
+        assert np.array_equal(np.asarray(u[k]), np.asarray(r[k]))
