@@ -23,9 +23,15 @@
  *       the correspondence step of every ICP iteration (generalizedICP.py:60)
  *   orpcd_fpfh
  *       o3d compute_fpfh_feature           Optimizer/fastGlobalOptimizer.py:130-142
+ *   orpcd_fpfh_from_normals
+ *       o3d compute_fpfh_feature on a cloud with normals (o3d Feature.cpp)
  *   orpcd_fgr
  *       o3d registration_fgr_based_on_feature_matching
  *                                          Optimizer/fastGlobalOptimizer.py:158-174
+ *   orpcd_feature_nn
+ *       the feature matching inside registration_fgr_based_on_feature_matching
+ *   orpcd_fgr_optimize
+ *       FastGlobalOptimizer.optimize       Optimizer/fastGlobalOptimizer.py:146-190
  */
 #ifndef ORPCD_H
 #define ORPCD_H
@@ -99,6 +105,10 @@ int orpcd_estimate_normals(orpcd_ctx* ctx, const double* xyz, int64_t n, int32_t
 int orpcd_fpfh(orpcd_ctx* ctx, const double* xyz, int64_t n, double normal_radius, int32_t normal_knn,
                double fpfh_radius, int32_t fpfh_knn, double* normals_out, double* feat_out);
 
+/* compute_fpfh_feature on a cloud that already carries normals (n x 3). */
+int orpcd_fpfh_from_normals(orpcd_ctx* ctx, const double* xyz, const double* normals, int64_t n,
+                            double fpfh_radius, int32_t fpfh_knn, double* feat_out);
+
 typedef struct {
     double division_factor;                 /* 1.4  fastGlobalOptimizer.py:25 */
     double tuple_scale;                     /* 0.9                            */
@@ -116,6 +126,24 @@ int orpcd_fgr(orpcd_ctx* ctx, const double* src, int64_t n, const double* tgt, i
               const double* src_feat, const double* tgt_feat, const orpcd_fgr_params* params,
               double* T_out, double* fitness_out, double* rmse_out, int64_t* ncorr_out,
               int64_t* n_mutual_out);
+
+/* Nearest feature row (squared Euclidean, ties -> lowest index) of every
+ * query row: the KDTreeFlann SearchKNN(feature, 1) calls of Open3D's
+ * AdvancedMatching (FastGlobalRegistration.cpp), on the fp64 matrix cores.
+ * q: nq x dim, t: nt x dim (row-major), dim <= 36.                          */
+int orpcd_feature_nn(orpcd_ctx* ctx, const double* q, int64_t nq, const double* t, int64_t nt, int32_t dim,
+                     int32_t* idx_out);
+
+/* FastGlobalOptimizer.optimize in one call (fastGlobalOptimizer.py:146-190):
+ * FPFH of both clouds on device (Hybrid normal / FPFH neighbourhoods), then
+ * FGR as orpcd_fgr.  target_features_from_source = 1 reproduces the
+ * reference's use of the SOURCE features for the target (:137-142); it
+ * requires m <= n (the reference would read past the features otherwise). */
+int orpcd_fgr_optimize(orpcd_ctx* ctx, const double* src, int64_t n, const double* tgt, int64_t m,
+                       double normal_radius, int32_t normal_knn, double fpfh_radius, int32_t fpfh_knn,
+                       int32_t target_features_from_source, const orpcd_fgr_params* params,
+                       double* T_out, double* fitness_out, double* rmse_out, int64_t* ncorr_out,
+                       int64_t* n_mutual_out);
 
 /* Tuning knobs (defaults are the measured best on MI355X):
  *   "search_waves"  split a start's tiles over waves until ~this many run

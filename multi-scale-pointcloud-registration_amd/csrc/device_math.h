@@ -16,6 +16,7 @@ struct Sym3 {  // symmetric 3x3: xx xy xz yy yz zz
 };
 
 __device__ __forceinline__ void cross3(const double a[3], const double b[3], double r[3]) {
+#pragma clang fp contract(off)
     r[0] = a[1] * b[2] - a[2] * b[1];
     r[1] = a[2] * b[0] - a[0] * b[2];
     r[2] = a[0] * b[1] - a[1] * b[0];

@@ -1,0 +1,474 @@
+// fgr_kernels.hip — FastGlobalOptimizer path on gfx950.
+//
+// Restates, for the reference's FastGlobalOptimizer (fastGlobalOptimizer.py:109-190):
+//   * compute_fpfh_feature (O3D Feature.cpp ComputeSPFHFeature / ComputeFPFHFeature)
+//     over Hybrid(r, k) neighbourhoods from knn_cov_kernel;
+//   * InitialMatching of O3D FastGlobalRegistration.cpp: nearest neighbour in
+//     the 33-D feature space in both directions.  This is the genuine dense
+//     contraction of the path: d(q, t) = |q|^2 + |t|^2 - 2 q.t with q.t on the
+//     fp64 matrix cores (v_mfma_f64_16x16x4_f64, K = 33 padded to 36, 9 MFMAs
+//     per 16x16 tile).  fp64 keeps the mutual-match set identical to the
+//     oracle's: FGR's tuple sampling indexes into that list, so one different
+//     match would change every later tuple;
+//   * OptimizePairwiseRegistration (GNC / Geman-McClure IRLS, 100 iterations)
+//     in one workgroup, fixed-order reductions, fp64;
+//   * the normalisation means / radius and EvaluateRegistration's reduction.
+// The tuple test (100 x ncorr draws of Open3D's global mt19937, stopping at
+// maximum_tuple_count) is RNG-sequential by construction and runs on the host
+// in runtime.hip.
+#include "device_math.h"
+#include "orpcd_internal.h"
+
+namespace orpcd {
+
+typedef double d4 __attribute__((ext_vector_type(4)));
+
+// ------------------------------------------------------------- FPFH
+// Contraction off: the swap test below compares acos(|a1|) with acos(|a2|),
+// which for nearly parallel normals is decided by the last bits of a1 and a2;
+// unfused arithmetic keeps those bits equal to the CPU restatement's.
+__device__ inline void pair_features(const double p1[3], const double n1[3], const double p2[3], const double n2[3],
+                                     double out[4]) {
+#pragma clang fp contract(off)
+    double d[3] = {p2[0] - p1[0], p2[1] - p1[1], p2[2] - p1[2]};
+    out[3] = sqrt(d[0] * d[0] + d[1] * d[1] + d[2] * d[2]);
+    if (out[3] == 0.0) {
+        out[0] = out[1] = out[2] = out[3] = 0.0;
+        return;
+    }
+    double a[3] = {n1[0], n1[1], n1[2]}, b[3] = {n2[0], n2[1], n2[2]};
+    const double angle1 = (a[0] * d[0] + a[1] * d[1] + a[2] * d[2]) / out[3];
+    const double angle2 = (b[0] * d[0] + b[1] * d[1] + b[2] * d[2]) / out[3];
+    if (acos(fabs(angle1)) > acos(fabs(angle2))) {
+        for (int t = 0; t < 3; ++t) {
+            const double tmp = a[t];
+            a[t] = b[t];
+            b[t] = tmp;
+            d[t] = -d[t];
+        }
+        out[2] = -angle2;
+    } else {
+        out[2] = angle1;
+    }
+    double v[3];
+    cross3(d, a, v);
+    const double vn = sqrt(v[0] * v[0] + v[1] * v[1] + v[2] * v[2]);
+    if (vn == 0.0) {
+        out[0] = out[1] = out[2] = out[3] = 0.0;
+        return;
+    }
+    v[0] /= vn;
+    v[1] /= vn;
+    v[2] /= vn;
+    double w[3];
+    cross3(a, v, w);
+    out[1] = v[0] * b[0] + v[1] * b[1] + v[2] * b[2];
+    out[0] = atan2(w[0] * b[0] + w[1] * b[1] + w[2] * b[2], a[0] * b[0] + a[1] * b[1] + a[2] * b[2]);
+}
+
+__device__ __forceinline__ int fpfh_bin(double x) {
+    int h = (int)floor(x);
+    return h < 0 ? 0 : (h >= 11 ? 10 : h);
+}
+
+// SPFH: one thread per point, histogram in LDS (64 threads x 33 doubles).
+__global__ __launch_bounds__(64) void spfh_kernel(const double* __restrict__ pts, const double* __restrict__ nrm,
+                                                  int n, const int32_t* __restrict__ nbr,
+                                                  const int32_t* __restrict__ cnt, int k, double* __restrict__ spfh) {
+    __shared__ double h[64][33];
+    const int i = blockIdx.x * 64 + threadIdx.x;
+    for (int j = 0; j < 33; ++j) h[threadIdx.x][j] = 0.0;
+    if (i < n) {
+        const int c = cnt[i];
+        if (c > 1) {
+            const double incr = 100.0 / (double)(c - 1);
+            const double p1[3] = {pts[3 * i], pts[3 * i + 1], pts[3 * i + 2]};
+            const double n1[3] = {nrm[3 * i], nrm[3 * i + 1], nrm[3 * i + 2]};
+            for (int s = 1; s < c; ++s) {
+                const int j = nbr[(size_t)i * k + s];
+                const double p2[3] = {pts[3 * j], pts[3 * j + 1], pts[3 * j + 2]};
+                const double n2[3] = {nrm[3 * j], nrm[3 * j + 1], nrm[3 * j + 2]};
+                double pf[4];
+                pair_features(p1, n1, p2, n2, pf);
+                h[threadIdx.x][fpfh_bin(11 * (pf[0] + M_PI) / (2.0 * M_PI))] += incr;
+                h[threadIdx.x][fpfh_bin(11 * (pf[1] + 1.0) * 0.5) + 11] += incr;
+                h[threadIdx.x][fpfh_bin(11 * (pf[2] + 1.0) * 0.5) + 22] += incr;
+            }
+        }
+        for (int j = 0; j < 33; ++j) spfh[(size_t)i * 33 + j] = h[threadIdx.x][j];
+    }
+}
+
+// FPFH: weighted sum of the neighbours' SPFH (1/d^2), per-block renormalised
+// to 100, plus the point's own SPFH.  Output padded to kFD columns (zeros).
+constexpr int kFD = 36;
+__global__ __launch_bounds__(256) void fpfh_kernel(const double* __restrict__ spfh, int n,
+                                                   const int32_t* __restrict__ nbr, const double* __restrict__ d2,
+                                                   const int32_t* __restrict__ cnt, int k, double* __restrict__ feat) {
+#pragma clang fp contract(off)
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    double f[33];
+#pragma unroll
+    for (int j = 0; j < 33; ++j) f[j] = 0.0;
+    const int c = cnt[i];
+    if (c > 1) {
+        double sum[3] = {0.0, 0.0, 0.0};
+        for (int s = 1; s < c; ++s) {
+            const double dist = d2[(size_t)i * k + s];
+            if (dist == 0.0) continue;
+            const double* sp = spfh + (size_t)nbr[(size_t)i * k + s] * 33;
+#pragma unroll
+            for (int j = 0; j < 33; ++j) {
+                const double val = sp[j] / dist;
+                sum[j / 11] += val;
+                f[j] += val;
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < 3; ++j)
+            if (sum[j] != 0.0) sum[j] = 100.0 / sum[j];
+#pragma unroll
+        for (int j = 0; j < 33; ++j) f[j] = f[j] * sum[j / 11] + spfh[(size_t)i * 33 + j];
+    }
+#pragma unroll
+    for (int j = 0; j < 33; ++j) feat[(size_t)i * kFD + j] = f[j];
+#pragma unroll
+    for (int j = 33; j < kFD; ++j) feat[(size_t)i * kFD + j] = 0.0;
+}
+
+// Pad caller-supplied n x 33 features to n x kFD.
+__global__ void pad_features_kernel(const double* __restrict__ in, int n, double* __restrict__ out) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    for (int j = 0; j < 33; ++j) out[(size_t)i * kFD + j] = in[(size_t)i * 33 + j];
+    for (int j = 33; j < kFD; ++j) out[(size_t)i * kFD + j] = 0.0;
+}
+
+__global__ void feat_norm_kernel(const double* __restrict__ F, int n, double* __restrict__ nrm2) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    double s = 0.0;
+    for (int j = 0; j < kFD; ++j) s += F[(size_t)i * kFD + j] * F[(size_t)i * kFD + j];
+    nrm2[i] = s;
+}
+
+// ------------------------------------------------ feature nearest neighbour
+// For every query row q of Fq: the target row t of Ft minimising
+// |q|^2 + |t|^2 - 2 q.t (ties -> lowest t), over the target range of
+// blockIdx.y (nparts ranges; merged by merge_parts_kernel).  One wave owns 64
+// queries as 4 column tiles of 16; the block stages 64 targets x 36 in LDS.
+// D[i][j] = sum_k A[i][k] B[k][j] with A = 16 targets (lane l supplies
+// A[l&15][l>>4]) and B = 16 queries (lane l supplies B[l>>4][l&15]); the f64
+// accumulator holds D[(l>>4) + 4r][l&15], r = 0..3.
+constexpr int kFT = 64;
+__global__ __launch_bounds__(256) void feat_nn_kernel(const double* __restrict__ Fq, const double* __restrict__ nq2,
+                                                      int nq, const double* __restrict__ Ft,
+                                                      const double* __restrict__ nt2, int nt, int part_len,
+                                                      double* __restrict__ out_d, int32_t* __restrict__ out_i) {
+    __shared__ double sT[kFT][kFD + 1];
+    __shared__ double sN[kFT];
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const int q0 = (blockIdx.x * 4 + wid) * 64;
+    const int t_begin = blockIdx.y * part_len, t_end = min(nt, t_begin + part_len);
+    double b[4][9], qn[4];
+#pragma unroll
+    for (int qt = 0; qt < 4; ++qt) {
+        const int q = q0 + 16 * qt + (lane & 15);
+        qn[qt] = q < nq ? nq2[q] : 0.0;
+#pragma unroll
+        for (int kb = 0; kb < 9; ++kb) b[qt][kb] = q < nq ? Fq[(size_t)q * kFD + 4 * kb + (lane >> 4)] : 0.0;
+    }
+    double bd[4] = {__builtin_huge_val(), __builtin_huge_val(), __builtin_huge_val(), __builtin_huge_val()};
+    int bi[4] = {-1, -1, -1, -1};
+    for (int t0 = t_begin; t0 < t_end; t0 += kFT) {
+        __syncthreads();
+        for (int e = threadIdx.x; e < kFT * kFD; e += 256) {
+            const int r = e / kFD, col = e - r * kFD;
+            sT[r][col] = (t0 + r < t_end) ? Ft[(size_t)(t0 + r) * kFD + col] : 0.0;
+        }
+        if (threadIdx.x < kFT) sN[threadIdx.x] = (t0 + threadIdx.x < t_end) ? nt2[t0 + threadIdx.x] : __builtin_huge_val();
+        __syncthreads();
+#pragma unroll
+        for (int sub = 0; sub < kFT / 16; ++sub) {
+            d4 acc[4];
+#pragma unroll
+            for (int qt = 0; qt < 4; ++qt) acc[qt] = d4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+            for (int kb = 0; kb < 9; ++kb) {
+                const double a = sT[sub * 16 + (lane & 15)][4 * kb + (lane >> 4)];
+#pragma unroll
+                for (int qt = 0; qt < 4; ++qt) acc[qt] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b[qt][kb], acc[qt], 0, 0, 0);
+            }
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int row = sub * 16 + (lane >> 4) + 4 * r;
+                const double tn = sN[row];
+#pragma unroll
+                for (int qt = 0; qt < 4; ++qt) {
+                    const double d = tn + qn[qt] - 2.0 * acc[qt][r];
+                    if (d < bd[qt]) {
+                        bd[qt] = d;
+                        bi[qt] = t0 + row;
+                    }
+                }
+            }
+        }
+    }
+    // merge the 4 lane groups (l>>4) holding the same query column
+#pragma unroll
+    for (int qt = 0; qt < 4; ++qt) {
+#pragma unroll
+        for (int off = 16; off < 64; off <<= 1) {
+            const double od = __shfl_xor(bd[qt], off, 64);
+            const int oi = __shfl_xor(bi[qt], off, 64);
+            if (oi >= 0 && (bi[qt] < 0 || od < bd[qt] || (od == bd[qt] && oi < bi[qt]))) {
+                bd[qt] = od;
+                bi[qt] = oi;
+            }
+        }
+        const int q = q0 + 16 * qt + lane;
+        if (lane < 16 && q < nq) {
+            out_d[(size_t)blockIdx.y * nq + q] = bd[qt];
+            out_i[(size_t)blockIdx.y * nq + q] = bi[qt];
+        }
+    }
+}
+
+__global__ void merge_parts_kernel(const double* __restrict__ pd, const int32_t* __restrict__ pi, int nq, int nparts,
+                                   int32_t* __restrict__ out) {
+    const int q = blockIdx.x * blockDim.x + threadIdx.x;
+    if (q >= nq) return;
+    double bd = pd[q];
+    int bi = pi[q];
+    for (int p = 1; p < nparts; ++p) {  // parts cover increasing target ranges: strict < keeps the lowest index
+        const double d = pd[(size_t)p * nq + q];
+        const int i = pi[(size_t)p * nq + q];
+        if (i >= 0 && (bi < 0 || d < bd)) {
+            bd = d;
+            bi = i;
+        }
+    }
+    out[q] = bi;
+}
+
+// ------------------------------------------------------ IRLS (one block)
+// O3D FastGlobalRegistration.cpp OptimizePairwiseRegistration over the tuple
+// correspondences: p (normalised source) and q (normalised target, moved by
+// every update in place).
+__global__ __launch_bounds__(256) void fgr_irls_kernel(const double* __restrict__ p, double* __restrict__ q, int K,
+                                                       double par0, int iters, double division_factor,
+                                                       double max_corr, int decrease_mu, double* __restrict__ T_out) {
+    __shared__ double red[4][27];
+    __shared__ double delta[16];
+    __shared__ double trans[16];
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    if (threadIdx.x < 16) trans[threadIdx.x] = (threadIdx.x % 5 == 0) ? 1.0 : 0.0;
+    double par = par0;
+    __syncthreads();
+    if (K < 10) {  // O3D: fewer than 10 correspondences -> identity
+        if (threadIdx.x < 16) T_out[threadIdx.x] = trans[threadIdx.x];
+        return;
+    }
+    for (int itr = 0; itr < iters; ++itr) {
+        double acc[27];
+#pragma unroll
+        for (int v = 0; v < 27; ++v) acc[v] = 0.0;
+        for (int c = threadIdx.x; c < K; c += 256) {
+            const double qx = q[3 * c], qy = q[3 * c + 1], qz = q[3 * c + 2];
+            const double r[3] = {p[3 * c] - qx, p[3 * c + 1] - qy, p[3 * c + 2] - qz};
+            const double temp = par / (r[0] * r[0] + r[1] * r[1] + r[2] * r[2] + par);
+            const double s = temp * temp;
+            const double J[3][6] = {{0, -qz, qy, -1, 0, 0}, {qz, 0, -qx, 0, -1, 0}, {-qy, qx, 0, 0, 0, -1}};
+#pragma unroll
+            for (int a = 0; a < 3; ++a) {
+                int e = 0;
+#pragma unroll
+                for (int u = 0; u < 6; ++u) {
+#pragma unroll
+                    for (int v = u; v < 6; ++v) acc[e++] += J[a][u] * J[a][v] * s;
+                    acc[21 + u] += J[a][u] * r[a] * s;
+                }
+            }
+        }
+#pragma unroll
+        for (int v = 0; v < 27; ++v) {
+            const double sv = wave_sum(acc[v]);
+            if (lane == 0) red[wid][v] = sv;
+        }
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            double s[27];
+            for (int v = 0; v < 27; ++v) s[v] = ((red[0][v] + red[1][v]) + red[2][v]) + red[3][v];
+            double A[36], bvec[6], x[6] = {0, 0, 0, 0, 0, 0};
+            int e = 0;
+            for (int u = 0; u < 6; ++u)
+                for (int v = u; v < 6; ++v) {
+                    A[6 * u + v] = -s[e];
+                    A[6 * v + u] = -s[e];
+                    ++e;
+                }
+            for (int u = 0; u < 6; ++u) bvec[u] = s[21 + u];
+            const double det = det6(A);  // SolveLinearSystemPSD(-JTJ, JTr): check_det
+            if (!(fabs(det) < 1e-6 || isnan(det) || isinf(det))) ldlt_solve6(A, bvec, x);
+            vec6_to_m4(x, delta);
+            double tn[16];
+            m4_mul(delta, trans, tn);
+            for (int t = 0; t < 16; ++t) trans[t] = tn[t];
+        }
+        __syncthreads();
+        for (int c = threadIdx.x; c < K; c += 256) {
+            const double x = q[3 * c], y = q[3 * c + 1], z = q[3 * c + 2];
+            q[3 * c] = delta[0] * x + delta[1] * y + delta[2] * z + delta[3];
+            q[3 * c + 1] = delta[4] * x + delta[5] * y + delta[6] * z + delta[7];
+            q[3 * c + 2] = delta[8] * x + delta[9] * y + delta[10] * z + delta[11];
+        }
+        if (decrease_mu && itr % 4 == 0 && par > max_corr) par /= division_factor;
+        __syncthreads();
+    }
+    if (threadIdx.x < 16) T_out[threadIdx.x] = trans[threadIdx.x];
+}
+
+// ---------------------------------------------------------- small helpers
+// Per-block fixed-order partial sums of x, y, z (normalisation means).
+__global__ __launch_bounds__(256) void sum3_kernel(const double* __restrict__ xyz, int n, double* __restrict__ part) {
+    __shared__ double red[4][3];
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    double v[3] = {0.0, 0.0, 0.0};
+    if (i < n) {
+        v[0] = xyz[3 * i];
+        v[1] = xyz[3 * i + 1];
+        v[2] = xyz[3 * i + 2];
+    }
+    for (int a = 0; a < 3; ++a) {
+        const double s = wave_sum(v[a]);
+        if (lane == 0) red[wid][a] = s;
+    }
+    __syncthreads();
+    if (threadIdx.x < 3)
+        part[3 * blockIdx.x + threadIdx.x] =
+            ((red[0][threadIdx.x] + red[1][threadIdx.x]) + red[2][threadIdx.x]) + red[3][threadIdx.x];
+}
+
+// Per-block max of |p - mean|.
+__global__ __launch_bounds__(256) void maxnorm_kernel(const double* __restrict__ xyz, int n, double mx, double my,
+                                                      double mz, double* __restrict__ part) {
+    __shared__ double red[4];
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    double v = 0.0;
+    if (i < n) {
+        const double x = xyz[3 * i] - mx, y = xyz[3 * i + 1] - my, z = xyz[3 * i + 2] - mz;
+        v = sqrt(x * x + y * y + z * z);
+    }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) v = fmax(v, __shfl_xor(v, off, 64));
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
+    __syncthreads();
+    if (threadIdx.x == 0) part[blockIdx.x] = fmax(fmax(red[0], red[1]), fmax(red[2], red[3]));
+}
+
+// q = T p (homogeneous, fp64) for EvaluateRegistration.
+__global__ void transform_points_kernel(const double* __restrict__ in, int n, const double* __restrict__ T,
+                                        double* __restrict__ out) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const double x = in[3 * i], y = in[3 * i + 1], z = in[3 * i + 2];
+    out[3 * i] = T[0] * x + T[1] * y + T[2] * z + T[3];
+    out[3 * i + 1] = T[4] * x + T[5] * y + T[6] * z + T[7];
+    out[3 * i + 2] = T[8] * x + T[9] * y + T[10] * z + T[11];
+}
+
+// Per-block (count, sum d^2) of nn1 results (EvaluateRegistration).
+__global__ __launch_bounds__(256) void corr_stats_kernel(const int32_t* __restrict__ idx,
+                                                         const double* __restrict__ d2, int n,
+                                                         double* __restrict__ part) {
+    __shared__ double red[4][2];
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    double c = 0.0, s = 0.0;
+    if (i < n && idx[i] >= 0) {
+        c = 1.0;
+        s = d2[i];
+    }
+    c = wave_sum(c);
+    s = wave_sum(s);
+    if (lane == 0) {
+        red[wid][0] = c;
+        red[wid][1] = s;
+    }
+    __syncthreads();
+    if (threadIdx.x < 2)
+        part[2 * blockIdx.x + threadIdx.x] =
+            ((red[0][threadIdx.x] + red[1][threadIdx.x]) + red[2][threadIdx.x]) + red[3][threadIdx.x];
+}
+
+// ---------------------------------------------------------------- launchers
+hipError_t launch_fpfh(const double* pts, const double* nrm, int64_t n, const int32_t* nbr, const double* d2,
+                       const int32_t* cnt, int k, double* spfh, double* feat36, hipStream_t s) {
+    if (n <= 0) return hipSuccess;
+    spfh_kernel<<<(unsigned)((n + 63) / 64), 64, 0, s>>>(pts, nrm, (int)n, nbr, cnt, k, spfh);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    fpfh_kernel<<<(unsigned)((n + 255) / 256), 256, 0, s>>>(spfh, (int)n, nbr, d2, cnt, k, feat36);
+    return hipGetLastError();
+}
+
+hipError_t launch_pad_features(const double* in33, int64_t n, double* out36, hipStream_t s) {
+    if (n <= 0) return hipSuccess;
+    pad_features_kernel<<<(unsigned)((n + 255) / 256), 256, 0, s>>>(in33, (int)n, out36);
+    return hipGetLastError();
+}
+
+hipError_t launch_feat_norm(const double* F36, int64_t n, double* nrm2, hipStream_t s) {
+    if (n <= 0) return hipSuccess;
+    feat_norm_kernel<<<(unsigned)((n + 255) / 256), 256, 0, s>>>(F36, (int)n, nrm2);
+    return hipGetLastError();
+}
+
+int feat_nn_parts(int64_t nq) {  // split targets so that ~8k waves run
+    const int64_t waves = (nq + 63) / 64;
+    return (int)std::min<int64_t>(16, std::max<int64_t>(1, 8192 / std::max<int64_t>(waves, 1)));
+}
+
+hipError_t launch_feat_nn(const double* Fq, const double* nq2, int64_t nq, const double* Ft, const double* nt2,
+                          int64_t nt, double* part_d, int32_t* part_i, int32_t* out, hipStream_t s) {
+    if (nq <= 0) return hipSuccess;
+    const int parts = feat_nn_parts(nq);
+    const int part_len = (int)(((nt + parts - 1) / parts + kFT - 1) / kFT * kFT);
+    const dim3 grid((unsigned)((nq + 255) / 256), (unsigned)parts);
+    feat_nn_kernel<<<grid, 256, 0, s>>>(Fq, nq2, (int)nq, Ft, nt2, (int)nt, part_len, part_d, part_i);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    merge_parts_kernel<<<(unsigned)((nq + 255) / 256), 256, 0, s>>>(part_d, part_i, (int)nq, parts, out);
+    return hipGetLastError();
+}
+
+hipError_t launch_fgr_irls(const double* p, double* q, int K, double par0, int iters, double division_factor,
+                           double max_corr, int decrease_mu, double* T_out, hipStream_t s) {
+    fgr_irls_kernel<<<1, 256, 0, s>>>(p, q, K, par0, iters, division_factor, max_corr, decrease_mu, T_out);
+    return hipGetLastError();
+}
+
+hipError_t launch_sum3(const double* xyz, int64_t n, double* part, hipStream_t s) {
+    sum3_kernel<<<(unsigned)((n + 255) / 256), 256, 0, s>>>(xyz, (int)n, part);
+    return hipGetLastError();
+}
+
+hipError_t launch_maxnorm(const double* xyz, int64_t n, const double mean[3], double* part, hipStream_t s) {
+    maxnorm_kernel<<<(unsigned)((n + 255) / 256), 256, 0, s>>>(xyz, (int)n, mean[0], mean[1], mean[2], part);
+    return hipGetLastError();
+}
+
+hipError_t launch_transform_points(const double* in, int64_t n, const double* T, double* out, hipStream_t s) {
+    if (n <= 0) return hipSuccess;
+    transform_points_kernel<<<(unsigned)((n + 255) / 256), 256, 0, s>>>(in, (int)n, T, out);
+    return hipGetLastError();
+}
+
+hipError_t launch_corr_stats(const int32_t* idx, const double* d2, int64_t n, double* part, hipStream_t s) {
+    corr_stats_kernel<<<(unsigned)((n + 255) / 256), 256, 0, s>>>(idx, d2, (int)n, part);
+    return hipGetLastError();
+}
+
+}  // namespace orpcd

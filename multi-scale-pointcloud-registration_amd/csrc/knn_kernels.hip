@@ -22,7 +22,7 @@ constexpr int kKnnTile = 1024;
 template <int K>
 __global__ __launch_bounds__(kKnnBlock) void knn_cov_kernel(const double* __restrict__ pts, int n, double r2,
                                                             double* __restrict__ rawcov6,
-                                                            int32_t* __restrict__ nbr_idx,
+                                                            int32_t* __restrict__ nbr_idx, double* __restrict__ nbr_d2,
                                                             int32_t* __restrict__ nbr_cnt, int kout) {
     __shared__ double sx[kKnnTile], sy[kKnnTile], sz[kKnnTile];
     const int i = blockIdx.x * kKnnBlock + threadIdx.x;
@@ -80,6 +80,11 @@ __global__ __launch_bounds__(kKnnBlock) void knn_cov_kernel(const double* __rest
 #pragma unroll
         for (int s = 0; s < K; ++s)
             if (s < kout) nbr_idx[(size_t)i * kout + s] = s < c ? bi[s] : -1;
+    }
+    if (nbr_d2) {
+#pragma unroll
+        for (int s = 0; s < K; ++s)
+            if (s < kout) nbr_d2[(size_t)i * kout + s] = s < c ? bd[s] : 0.0;
     }
     if (nbr_cnt) nbr_cnt[i] = c;
     if (!rawcov6) return;
@@ -168,18 +173,18 @@ __global__ __launch_bounds__(256) void normals_cov_kernel(const double* __restri
 }
 
 hipError_t launch_knn_cov(const double* pts, int64_t n, int k, double radius, double* rawcov6, int32_t* nbr_idx,
-                          int32_t* nbr_cnt, hipStream_t s) {
+                          double* nbr_d2, int32_t* nbr_cnt, hipStream_t s) {
     if (n <= 0) return hipSuccess;
     const double r2 = radius > 0 ? radius * radius : __builtin_huge_val();
     const dim3 grid((unsigned)((n + kKnnBlock - 1) / kKnnBlock));
     if (k <= 8)
-        knn_cov_kernel<8><<<grid, kKnnBlock, 0, s>>>(pts, (int)n, r2, rawcov6, nbr_idx, nbr_cnt, k);
+        knn_cov_kernel<8><<<grid, kKnnBlock, 0, s>>>(pts, (int)n, r2, rawcov6, nbr_idx, nbr_d2, nbr_cnt, k);
     else if (k <= 20)
-        knn_cov_kernel<20><<<grid, kKnnBlock, 0, s>>>(pts, (int)n, r2, rawcov6, nbr_idx, nbr_cnt, k);
+        knn_cov_kernel<20><<<grid, kKnnBlock, 0, s>>>(pts, (int)n, r2, rawcov6, nbr_idx, nbr_d2, nbr_cnt, k);
     else if (k <= 32)
-        knn_cov_kernel<32><<<grid, kKnnBlock, 0, s>>>(pts, (int)n, r2, rawcov6, nbr_idx, nbr_cnt, k);
+        knn_cov_kernel<32><<<grid, kKnnBlock, 0, s>>>(pts, (int)n, r2, rawcov6, nbr_idx, nbr_d2, nbr_cnt, k);
     else if (k <= 64)
-        knn_cov_kernel<64><<<grid, kKnnBlock, 0, s>>>(pts, (int)n, r2, rawcov6, nbr_idx, nbr_cnt, k);
+        knn_cov_kernel<64><<<grid, kKnnBlock, 0, s>>>(pts, (int)n, r2, rawcov6, nbr_idx, nbr_d2, nbr_cnt, k);
     else
         return hipErrorInvalidValue;
     return hipGetLastError();

@@ -137,6 +137,25 @@ struct orpcd_ctx {
     orpcd::HostBuf<double> h64;
     orpcd::HostBuf<int32_t> h32;
 
+    // FastGlobal path (fgr_kernels.hip); index 0 = source, 1 = target
+    struct FgrBufs {
+        orpcd::DevBuf<double> xyz[2];     // input-order points
+        orpcd::DevBuf<double> feat[2];    // n x 36 padded features
+        orpcd::DevBuf<double> fn2[2];     // |f|^2
+        orpcd::DevBuf<double> nrm, raw, nd2, spfh, part_d, red, pq, Tn;
+        orpcd::DevBuf<int32_t> nbr, cnt, part_i, nn[2];
+        void release() {
+            for (int k = 0; k < 2; ++k) {
+                xyz[k].release();
+                feat[k].release();
+                fn2[k].release();
+                nn[k].release();
+            }
+            for (auto* b : {&nrm, &raw, &nd2, &spfh, &part_d, &red, &pq, &Tn}) b->release();
+            for (auto* b : {&nbr, &cnt, &part_i}) b->release();
+        }
+    } fgr;
+
     // profiling
     bool profiling = false;
     bool count_tiles = false;  // tile counters live only while timing (profiling / ORPCD_TRACE)
@@ -161,7 +180,7 @@ hipError_t launch_unpermute(const double* in, const int32_t* perm, int64_t n, in
 
 // knn_kernels.hip
 hipError_t launch_knn_cov(const double* pts, int64_t n, int k, double radius, double* rawcov6, int32_t* nbr_idx,
-                          int32_t* nbr_cnt, hipStream_t s);
+                          double* nbr_d2, int32_t* nbr_cnt, hipStream_t s);
 hipError_t launch_normals_cov(const double* rawcov6, int64_t n, const double* Rc9, int nslots, double eps,
                               double* normals3, double* cov6, hipStream_t s);
 
@@ -172,5 +191,21 @@ hipError_t launch_gicp_pass(const orpcd_ctx* c, int nact, int pass, double r2, h
 hipError_t launch_gicp_solve(const orpcd_ctx* c, int nact, int pass, const orpcd_gicp_params& p, hipStream_t s);
 hipError_t launch_nn1(const double* q, int64_t nq, const CloudLayout& t, double r2, int32_t* idx, double* d2,
                       hipStream_t s);
+
+// fgr_kernels.hip
+constexpr int kFeatDim = 36;  // 33 FPFH bins padded for the 16x16x4 f64 MFMA
+hipError_t launch_fpfh(const double* pts, const double* nrm, int64_t n, const int32_t* nbr, const double* d2,
+                       const int32_t* cnt, int k, double* spfh, double* feat36, hipStream_t s);
+hipError_t launch_pad_features(const double* in33, int64_t n, double* out36, hipStream_t s);
+hipError_t launch_feat_norm(const double* F36, int64_t n, double* nrm2, hipStream_t s);
+int feat_nn_parts(int64_t nq);
+hipError_t launch_feat_nn(const double* Fq, const double* nq2, int64_t nq, const double* Ft, const double* nt2,
+                          int64_t nt, double* part_d, int32_t* part_i, int32_t* out, hipStream_t s);
+hipError_t launch_fgr_irls(const double* p, double* q, int K, double par0, int iters, double division_factor,
+                           double max_corr, int decrease_mu, double* T_out, hipStream_t s);
+hipError_t launch_sum3(const double* xyz, int64_t n, double* part, hipStream_t s);
+hipError_t launch_maxnorm(const double* xyz, int64_t n, const double mean[3], double* part, hipStream_t s);
+hipError_t launch_transform_points(const double* in, int64_t n, const double* T, double* out, hipStream_t s);
+hipError_t launch_corr_stats(const int32_t* idx, const double* d2, int64_t n, double* part, hipStream_t s);
 
 }  // namespace orpcd

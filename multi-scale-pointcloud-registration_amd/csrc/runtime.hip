@@ -7,6 +7,8 @@
 #include <cstdlib>
 #include <cstring>
 #include <new>
+#include <random>
+#include <utility>
 
 #include "orpcd_internal.h"
 
@@ -69,7 +71,7 @@ int upload_target(orpcd_ctx* c, const double* xyz, int64_t m, double eps) {
     CTX_CHECK(c, c->tcov.ensure((size_t)m * 6));
     CTX_CHECK(c, c->scratch64b.ensure((size_t)m * 6));
     if (eps >= 0.0) {
-        CTX_CHECK(c, launch_knn_cov(c->tgt.xyz64.p, m, 20, -1.0, c->scratch64b.p, nullptr, nullptr, c->stream));
+        CTX_CHECK(c, launch_knn_cov(c->tgt.xyz64.p, m, 20, -1.0, c->scratch64b.p, nullptr, nullptr, nullptr, c->stream));
         CTX_CHECK(c, launch_normals_cov(c->scratch64b.p, m, nullptr, 1, eps, nullptr, c->tcov.p, c->stream));
     }
     c->tgt_eps = eps;
@@ -92,6 +94,217 @@ hipError_t read_counters(orpcd_ctx* c, unsigned long long& tiles, unsigned long 
     }
     if (reset_max) e = hipMemcpyAsync(c->counters.p, h.data(), h.size() * 8, hipMemcpyHostToDevice, c->stream);
     return e;
+}
+
+int check_fgr_params(orpcd_ctx* c, const orpcd_fgr_params* p) {
+    CTX_REQUIRE(c, p->division_factor > 0 && p->tuple_scale > 0 && p->maximum_correspondence_distance > 0,
+                "fgr: division_factor, tuple_scale and maximum_correspondence_distance must be > 0");
+    CTX_REQUIRE(c, p->iteration_number > 0 && p->maximum_tuple_count > 0,
+                "fgr: iteration_number and maximum_tuple_count must be > 0");
+    return ORPCD_OK;
+}
+
+// estimate_normals(Hybrid(normal_radius, normal_knn)) + compute_fpfh_feature(
+// Hybrid(fpfh_radius, fpfh_knn)) of the input-order cloud in fgr.xyz[k]
+// (fastGlobalOptimizer.py:114-142).  Normals -> fgr.nrm, features (n x 36,
+// padded) -> fgr.feat[k].  Neighbour sets are exact (ties -> lower index) in
+// input order, as the KD-tree of the oracle returns them.
+int features_device(orpcd_ctx* c, int k, int64_t n, double fpfh_radius, int fpfh_knn);
+
+int fpfh_buffers(orpcd_ctx* c, int k, int64_t n, int fpfh_knn) {
+    auto& F = c->fgr;
+    CTX_CHECK(c, F.raw.ensure((size_t)n * 6));
+    CTX_CHECK(c, F.nrm.ensure((size_t)n * 3));
+    CTX_CHECK(c, F.nbr.ensure((size_t)n * fpfh_knn));
+    CTX_CHECK(c, F.nd2.ensure((size_t)n * fpfh_knn));
+    CTX_CHECK(c, F.cnt.ensure((size_t)n));
+    CTX_CHECK(c, F.spfh.ensure((size_t)n * 33));
+    CTX_CHECK(c, F.feat[k].ensure((size_t)n * kFeatDim));
+    return ORPCD_OK;
+}
+
+int fpfh_device(orpcd_ctx* c, int k, int64_t n, double normal_radius, int normal_knn, double fpfh_radius,
+                int fpfh_knn) {
+    CTX_REQUIRE(c, normal_knn > 0 && normal_knn <= 64 && fpfh_knn > 0 && fpfh_knn <= 64,
+                "fpfh: knn must be in [1, 64]");
+    CTX_REQUIRE(c, normal_radius > 0 && fpfh_radius > 0, "fpfh: radii must be > 0");
+    int rc = fpfh_buffers(c, k, n, fpfh_knn);
+    if (rc) return rc;
+    auto& F = c->fgr;
+    const double* pts = F.xyz[k].p;
+    CTX_CHECK(c, launch_knn_cov(pts, n, normal_knn, normal_radius, F.raw.p, nullptr, nullptr, nullptr, c->stream));
+    CTX_CHECK(c, launch_normals_cov(F.raw.p, n, nullptr, 1, -1.0, F.nrm.p, nullptr, c->stream));
+    return features_device(c, k, n, fpfh_radius, fpfh_knn);
+}
+
+// compute_fpfh_feature of fgr.xyz[k] with the normals in fgr.nrm.
+int features_device(orpcd_ctx* c, int k, int64_t n, double fpfh_radius, int fpfh_knn) {
+    auto& F = c->fgr;
+    const double* pts = F.xyz[k].p;
+    CTX_CHECK(c, launch_knn_cov(pts, n, fpfh_knn, fpfh_radius, nullptr, F.nbr.p, F.nd2.p, F.cnt.p, c->stream));
+    CTX_CHECK(c, launch_fpfh(pts, F.nrm.p, n, F.nbr.p, F.nd2.p, F.cnt.p, fpfh_knn, F.spfh.p, F.feat[k].p, c->stream));
+    return ORPCD_OK;
+}
+
+double norm3(const double* a) { return std::sqrt(a[0] * a[0] + a[1] * a[1] + a[2] * a[2]); }
+
+// O3D FastGlobalRegistration.cpp: NormalizePointCloud, AdvancedMatching,
+// OptimizePairwiseRegistration, GetInvTransformationOriginalScale and
+// EvaluateRegistration, with points and padded features already on device
+// (fgr.xyz[0..1], fgr.feat[0..1]).  src / tgt are the host copies used by the
+// sequential tuple test.
+int fgr_device(orpcd_ctx* c, const double* src, int64_t n, const double* tgt, int64_t m, const orpcd_fgr_params& p,
+               double* T_out, double* fitness_out, double* rmse_out, int64_t* ncorr_out, int64_t* n_mutual_out) {
+    auto& F = c->fgr;
+    hipStream_t s = c->stream;
+    const int64_t np[2] = {n, m};
+    const double* host[2] = {src, tgt};
+    // --- normalisation: means and the global radius (fixed-order partials)
+    const int64_t nb_max = (std::max(n, m) + 255) / 256;
+    CTX_CHECK(c, F.red.ensure((size_t)nb_max * 3));
+    double mean[2][3];
+    double scale = 0.0;
+    for (int k = 0; k < 2; ++k) {
+        const int64_t nb = (np[k] + 255) / 256;
+        std::vector<double> part((size_t)nb * 3);
+        CTX_CHECK(c, launch_sum3(F.xyz[k].p, np[k], F.red.p, s));
+        CTX_CHECK(c, hipMemcpyAsync(part.data(), F.red.p, part.size() * 8, hipMemcpyDeviceToHost, s));
+        CTX_CHECK(c, hipStreamSynchronize(s));
+        double sum[3] = {0.0, 0.0, 0.0};
+        for (int64_t b = 0; b < nb; ++b)
+            for (int a = 0; a < 3; ++a) sum[a] += part[(size_t)3 * b + a];
+        for (int a = 0; a < 3; ++a) mean[k][a] = sum[a] / (double)np[k];
+        CTX_CHECK(c, launch_maxnorm(F.xyz[k].p, np[k], mean[k], F.red.p, s));
+        CTX_CHECK(c, hipMemcpyAsync(part.data(), F.red.p, (size_t)nb * 8, hipMemcpyDeviceToHost, s));
+        CTX_CHECK(c, hipStreamSynchronize(s));
+        double mx = 0.0;
+        for (int64_t b = 0; b < nb; ++b) mx = std::max(mx, part[(size_t)b]);
+        scale = std::max(scale, mx);
+    }
+    CTX_REQUIRE(c, scale > 0.0, "fgr: degenerate clouds (all points at their mean)");
+    auto normalised = [&](int k, int64_t i, double out[3]) {
+        for (int a = 0; a < 3; ++a) out[a] = (host[k][3 * i + a] - mean[k][a]) / scale;
+    };
+    // --- initial matching on the matrix cores, both directions
+    int fi = 0, fj = 1;
+    if (np[1] > np[0]) std::swap(fi, fj);
+    const int64_t nPti = np[fi], nPtj = np[fj];
+    for (int k = 0; k < 2; ++k) {
+        CTX_CHECK(c, F.fn2[k].ensure((size_t)np[k]));
+        CTX_CHECK(c, launch_feat_norm(F.feat[k].p, np[k], F.fn2[k].p, s));
+    }
+    const int64_t parts_max = std::max(feat_nn_parts(nPti), feat_nn_parts(nPtj));
+    CTX_CHECK(c, F.part_d.ensure((size_t)parts_max * std::max(nPti, nPtj)));
+    CTX_CHECK(c, F.part_i.ensure((size_t)parts_max * std::max(nPti, nPtj)));
+    CTX_CHECK(c, F.nn[0].ensure((size_t)nPtj));
+    CTX_CHECK(c, F.nn[1].ensure((size_t)nPti));
+    CTX_CHECK(c, launch_feat_nn(F.feat[fj].p, F.fn2[fj].p, nPtj, F.feat[fi].p, F.fn2[fi].p, nPti, F.part_d.p,
+                                F.part_i.p, F.nn[0].p, s));
+    CTX_CHECK(c, launch_feat_nn(F.feat[fi].p, F.fn2[fi].p, nPti, F.feat[fj].p, F.fn2[fj].p, nPtj, F.part_d.p,
+                                F.part_i.p, F.nn[1].p, s));
+    std::vector<int32_t> j_to_i((size_t)nPtj), i_to_j((size_t)nPti);
+    CTX_CHECK(c, hipMemcpyAsync(j_to_i.data(), F.nn[0].p, (size_t)nPtj * 4, hipMemcpyDeviceToHost, s));
+    CTX_CHECK(c, hipMemcpyAsync(i_to_j.data(), F.nn[1].p, (size_t)nPti * 4, hipMemcpyDeviceToHost, s));
+    CTX_CHECK(c, hipStreamSynchronize(s));
+    // --- cross check, in i order: (i, i_to_j[i]) with j_to_i[i_to_j[i]] == i
+    std::vector<std::pair<int, int>> corres;
+    for (int64_t i = 0; i < nPti; ++i) {
+        const int j = i_to_j[i];
+        if (j >= 0 && j < nPtj && j_to_i[j] == i) corres.push_back({(int)i, j});
+    }
+    // --- tuple test: Open3D's sequential mt19937 draws (RNG-bound, host)
+    const int ncorr = (int)corres.size();
+    std::vector<std::pair<int, int>> tup;
+    if (ncorr > 0) {
+        std::mt19937 gen((std::mt19937::result_type)p.seed);
+        std::uniform_int_distribution<int> dis(0, ncorr - 1);
+        const int64_t trials = (int64_t)ncorr * 100;
+        const double sc = p.tuple_scale;
+        int cnt = 0;
+        for (int64_t t = 0; t < trials; ++t) {
+            const int r[3] = {dis(gen), dis(gen), dis(gen)};
+            double pi[3][3], pj[3][3];
+            for (int e = 0; e < 3; ++e) {
+                normalised(fi, corres[r[e]].first, pi[e]);
+                normalised(fj, corres[r[e]].second, pj[e]);
+            }
+            double li[3], lj[3];
+            for (int e = 0; e < 3; ++e) {
+                const int f = (e + 1) % 3;
+                const double di[3] = {pi[e][0] - pi[f][0], pi[e][1] - pi[f][1], pi[e][2] - pi[f][2]};
+                const double dj[3] = {pj[e][0] - pj[f][0], pj[e][1] - pj[f][1], pj[e][2] - pj[f][2]};
+                li[e] = norm3(di);
+                lj[e] = norm3(dj);
+            }
+            if ((li[0] * sc < lj[0]) && (lj[0] < li[0] / sc) && (li[1] * sc < lj[1]) && (lj[1] < li[1] / sc) &&
+                (li[2] * sc < lj[2]) && (lj[2] < li[2] / sc)) {
+                for (int e = 0; e < 3; ++e) tup.push_back(corres[r[e]]);
+                ++cnt;
+            }
+            if (cnt >= p.maximum_tuple_count) break;
+        }
+    }
+    // pairs back to (source, target)
+    const int K = (int)tup.size();
+    std::vector<double> pq((size_t)std::max(K, 1) * 6);
+    for (int e = 0; e < K; ++e) {
+        const int si = fi == 0 ? tup[e].first : tup[e].second;
+        const int ti = fi == 0 ? tup[e].second : tup[e].first;
+        normalised(0, si, &pq[(size_t)3 * e]);
+        normalised(1, ti, &pq[(size_t)3 * K + 3 * e]);
+    }
+    // --- GNC / Geman-McClure IRLS in one workgroup (fp64)
+    CTX_CHECK(c, F.pq.ensure(pq.size()));
+    CTX_CHECK(c, F.Tn.ensure(16));
+    if (K > 0) CTX_CHECK(c, hipMemcpyAsync(F.pq.p, pq.data(), (size_t)K * 48, hipMemcpyHostToDevice, s));
+    CTX_CHECK(c, launch_fgr_irls(F.pq.p, F.pq.p + (size_t)3 * K, K, 1.0, p.iteration_number, p.division_factor,
+                                 p.maximum_correspondence_distance, p.decrease_mu ? 1 : 0, F.Tn.p, s));
+    double Tn[16];
+    CTX_CHECK(c, hipMemcpyAsync(Tn, F.Tn.p, sizeof(Tn), hipMemcpyDeviceToHost, s));
+    CTX_CHECK(c, hipStreamSynchronize(s));
+    // --- GetInvTransformationOriginalScale (4x4 algebra)
+    double T[16] = {0};
+    double inner[3];
+    for (int a = 0; a < 3; ++a) {
+        const double mr = Tn[4 * a] * mean[1][0] + Tn[4 * a + 1] * mean[1][1] + Tn[4 * a + 2] * mean[1][2];
+        inner[a] = -mr + Tn[4 * a + 3] * scale + mean[0][a];
+    }
+    for (int a = 0; a < 3; ++a) {
+        for (int b = 0; b < 3; ++b) T[4 * a + b] = Tn[4 * b + a];
+        T[4 * a + 3] = -(Tn[a] * inner[0] + Tn[4 + a] * inner[1] + Tn[8 + a] * inner[2]);
+    }
+    T[15] = 1.0;
+    // --- EvaluateRegistration(source, target, max_corr, T)
+    int rc = upload_layout(c, tgt, m, c->aux, true);
+    if (rc) return rc;
+    CTX_CHECK(c, F.raw.ensure((size_t)n * 3 + 16));
+    CTX_CHECK(c, c->scratch32.ensure((size_t)n));
+    CTX_CHECK(c, c->scratch64c.ensure((size_t)n));
+    double* dT = F.raw.p + (size_t)n * 3;
+    CTX_CHECK(c, hipMemcpyAsync(dT, T, sizeof(T), hipMemcpyHostToDevice, s));
+    CTX_CHECK(c, launch_transform_points(F.xyz[0].p, n, dT, F.raw.p, s));
+    const double r = p.maximum_correspondence_distance;
+    CTX_CHECK(c, launch_nn1(F.raw.p, n, c->aux, r * r, c->scratch32.p, c->scratch64c.p, s));
+    const int64_t nb = (n + 255) / 256;
+    CTX_CHECK(c, F.red.ensure((size_t)nb * 2));
+    CTX_CHECK(c, launch_corr_stats(c->scratch32.p, c->scratch64c.p, n, F.red.p, s));
+    std::vector<double> part((size_t)nb * 2);
+    CTX_CHECK(c, hipMemcpyAsync(part.data(), F.red.p, part.size() * 8, hipMemcpyDeviceToHost, s));
+    CTX_CHECK(c, hipStreamSynchronize(s));
+    double cnt = 0.0, err2 = 0.0;
+    for (int64_t b = 0; b < nb; ++b) {
+        cnt += part[(size_t)2 * b];
+        err2 += part[(size_t)2 * b + 1];
+    }
+    std::memcpy(T_out, T, sizeof(T));
+    if (fitness_out) *fitness_out = cnt > 0 ? cnt / (double)n : 0.0;
+    if (rmse_out) *rmse_out = cnt > 0 ? std::sqrt(err2 / cnt) : 0.0;
+    if (ncorr_out) *ncorr_out = (int64_t)cnt;
+    if (n_mutual_out) {
+        n_mutual_out[0] = ncorr;
+        n_mutual_out[1] = K;
+    }
+    return ORPCD_OK;
 }
 
 }  // namespace
@@ -149,6 +362,7 @@ int orpcd_ctx_destroy(orpcd_ctx* c) {
     c->counters.release();
     c->h64.release();
     c->h32.release();
+    c->fgr.release();
     for (hipEvent_t e : c->ev_pool) (void)hipEventDestroy(e);
     (void)hipStreamDestroy(c->stream);
     delete c;
@@ -178,7 +392,7 @@ int orpcd_set_source(orpcd_ctx* c, const double* xyz, int64_t n) {
     int rc = upload_layout(c, xyz, n, c->src, false);
     if (rc) return rc;
     CTX_CHECK(c, c->sraw.ensure((size_t)n * 6));
-    CTX_CHECK(c, launch_knn_cov(c->src.xyz64.p, n, 20, -1.0, c->sraw.p, nullptr, nullptr, c->stream));
+    CTX_CHECK(c, launch_knn_cov(c->src.xyz64.p, n, 20, -1.0, c->sraw.p, nullptr, nullptr, nullptr, c->stream));
     CTX_CHECK(c, hipStreamSynchronize(c->stream));
     return ORPCD_OK;
 }
@@ -385,7 +599,7 @@ int orpcd_estimate_normals(orpcd_ctx* c, const double* xyz, int64_t n, int32_t k
     double* raw = c->scratch64b.p;
     double* nrm = raw + 6 * n;
     double* cov = nrm + 3 * n;
-    CTX_CHECK(c, launch_knn_cov(c->aux.xyz64.p, n, knn, radius, raw, nullptr, nullptr, c->stream));
+    CTX_CHECK(c, launch_knn_cov(c->aux.xyz64.p, n, knn, radius, raw, nullptr, nullptr, nullptr, c->stream));
     CTX_CHECK(c, launch_normals_cov(raw, n, nullptr, 1, epsilon, nrm, epsilon >= 0 ? cov : nullptr, c->stream));
     double* uraw = c->scratch64c.p;
     double* unrm = uraw + 6 * n;
@@ -421,17 +635,131 @@ int orpcd_estimate_normals(orpcd_ctx* c, const double* xyz, int64_t n, int32_t k
     return ORPCD_OK;
 }
 
-int orpcd_fpfh(orpcd_ctx* c, const double*, int64_t, double, int32_t, double, int32_t, double*, double*) {
+int orpcd_fpfh(orpcd_ctx* c, const double* xyz, int64_t n, double normal_radius, int32_t normal_knn,
+               double fpfh_radius, int32_t fpfh_knn, double* normals_out, double* feat_out) {
     if (!c) return ORPCD_EINVAL;
-    c->err = "fpfh: not built in this revision";
-    return ORPCD_EINVAL;
+    CTX_REQUIRE(c, xyz && n > 0 && feat_out, "fpfh: bad arguments");
+    CTX_REQUIRE(c, finite_cloud(xyz, n), "fpfh: non-finite coordinates");
+    CTX_CHECK(c, hipSetDevice(c->device));
+    CTX_CHECK(c, c->fgr.xyz[0].ensure((size_t)n * 3));
+    CTX_CHECK(c, hipMemcpyAsync(c->fgr.xyz[0].p, xyz, (size_t)n * 24, hipMemcpyHostToDevice, c->stream));
+    int rc = fpfh_device(c, 0, n, normal_radius, normal_knn, fpfh_radius, fpfh_knn);
+    if (rc) return rc;
+    if (normals_out)
+        CTX_CHECK(c, hipMemcpyAsync(normals_out, c->fgr.nrm.p, (size_t)n * 24, hipMemcpyDeviceToHost, c->stream));
+    CTX_CHECK(c, hipMemcpy2DAsync(feat_out, 33 * sizeof(double), c->fgr.feat[0].p, kFeatDim * sizeof(double),
+                                  33 * sizeof(double), (size_t)n, hipMemcpyDeviceToHost, c->stream));
+    CTX_CHECK(c, hipStreamSynchronize(c->stream));
+    return ORPCD_OK;
 }
 
-int orpcd_fgr(orpcd_ctx* c, const double*, int64_t, const double*, int64_t, const double*, const double*,
-              const orpcd_fgr_params*, double*, double*, double*, int64_t*, int64_t*) {
+int orpcd_fpfh_from_normals(orpcd_ctx* c, const double* xyz, const double* normals, int64_t n,
+                            double fpfh_radius, int32_t fpfh_knn, double* feat_out) {
     if (!c) return ORPCD_EINVAL;
-    c->err = "fgr: not built in this revision";
-    return ORPCD_EINVAL;
+    CTX_REQUIRE(c, xyz && normals && n > 0 && feat_out, "fpfh_from_normals: bad arguments");
+    CTX_REQUIRE(c, fpfh_knn > 0 && fpfh_knn <= 64, "fpfh: knn must be in [1, 64]");
+    CTX_REQUIRE(c, fpfh_radius > 0, "fpfh: radii must be > 0");
+    CTX_REQUIRE(c, finite_cloud(xyz, n) && finite_cloud(normals, n), "fpfh_from_normals: non-finite values");
+    CTX_CHECK(c, hipSetDevice(c->device));
+    int rc = fpfh_buffers(c, 0, n, fpfh_knn);
+    if (rc) return rc;
+    CTX_CHECK(c, c->fgr.xyz[0].ensure((size_t)n * 3));
+    CTX_CHECK(c, hipMemcpyAsync(c->fgr.xyz[0].p, xyz, (size_t)n * 24, hipMemcpyHostToDevice, c->stream));
+    CTX_CHECK(c, hipMemcpyAsync(c->fgr.nrm.p, normals, (size_t)n * 24, hipMemcpyHostToDevice, c->stream));
+    rc = features_device(c, 0, n, fpfh_radius, fpfh_knn);
+    if (rc) return rc;
+    CTX_CHECK(c, hipMemcpy2DAsync(feat_out, 33 * sizeof(double), c->fgr.feat[0].p, kFeatDim * sizeof(double),
+                                  33 * sizeof(double), (size_t)n, hipMemcpyDeviceToHost, c->stream));
+    CTX_CHECK(c, hipStreamSynchronize(c->stream));
+    return ORPCD_OK;
+}
+
+int orpcd_fgr(orpcd_ctx* c, const double* src, int64_t n, const double* tgt, int64_t m, const double* src_feat,
+              const double* tgt_feat, const orpcd_fgr_params* p, double* T_out, double* fitness_out,
+              double* rmse_out, int64_t* ncorr_out, int64_t* n_mutual_out) {
+    if (!c) return ORPCD_EINVAL;
+    CTX_REQUIRE(c, src && tgt && src_feat && tgt_feat && p && T_out && n > 0 && m > 0, "fgr: bad arguments");
+    int rc = check_fgr_params(c, p);
+    if (rc) return rc;
+    CTX_REQUIRE(c, finite_cloud(src, n) && finite_cloud(tgt, m), "fgr: non-finite coordinates");
+    for (int64_t i = 0; i < 33 * n; ++i) CTX_REQUIRE(c, std::isfinite(src_feat[i]), "fgr: non-finite feature");
+    for (int64_t i = 0; i < 33 * m; ++i) CTX_REQUIRE(c, std::isfinite(tgt_feat[i]), "fgr: non-finite feature");
+    CTX_CHECK(c, hipSetDevice(c->device));
+    const double* xyz[2] = {src, tgt};
+    const double* feat[2] = {src_feat, tgt_feat};
+    const int64_t np[2] = {n, m};
+    CTX_CHECK(c, c->fgr.raw.ensure((size_t)std::max(n, m) * 33));
+    for (int k = 0; k < 2; ++k) {
+        CTX_CHECK(c, c->fgr.xyz[k].ensure((size_t)np[k] * 3));
+        CTX_CHECK(c, c->fgr.feat[k].ensure((size_t)np[k] * kFeatDim));
+        CTX_CHECK(c, hipMemcpyAsync(c->fgr.xyz[k].p, xyz[k], (size_t)np[k] * 24, hipMemcpyHostToDevice, c->stream));
+        CTX_CHECK(c, hipMemcpyAsync(c->fgr.raw.p, feat[k], (size_t)np[k] * 33 * 8, hipMemcpyHostToDevice, c->stream));
+        CTX_CHECK(c, launch_pad_features(c->fgr.raw.p, np[k], c->fgr.feat[k].p, c->stream));
+    }
+    return fgr_device(c, src, n, tgt, m, *p, T_out, fitness_out, rmse_out, ncorr_out, n_mutual_out);
+}
+
+int orpcd_feature_nn(orpcd_ctx* c, const double* q, int64_t nq, const double* t, int64_t nt, int32_t dim,
+                     int32_t* idx_out) {
+    if (!c) return ORPCD_EINVAL;
+    CTX_REQUIRE(c, q && t && idx_out && nq >= 0 && nt > 0, "feature_nn: bad arguments");
+    CTX_REQUIRE(c, dim > 0 && dim <= kFeatDim, "feature_nn: dim must be in [1, 36]");
+    for (int64_t i = 0; i < nq * dim; ++i) CTX_REQUIRE(c, std::isfinite(q[i]), "feature_nn: non-finite value");
+    for (int64_t i = 0; i < nt * dim; ++i) CTX_REQUIRE(c, std::isfinite(t[i]), "feature_nn: non-finite value");
+    if (nq == 0) return ORPCD_OK;
+    CTX_CHECK(c, hipSetDevice(c->device));
+    auto& F = c->fgr;
+    const double* in[2] = {q, t};
+    const int64_t np[2] = {nq, nt};
+    for (int k = 0; k < 2; ++k) {
+        CTX_CHECK(c, F.feat[k].ensure((size_t)np[k] * kFeatDim));
+        CTX_CHECK(c, F.fn2[k].ensure((size_t)np[k]));
+        CTX_CHECK(c, hipMemsetAsync(F.feat[k].p, 0, (size_t)np[k] * kFeatDim * 8, c->stream));
+        CTX_CHECK(c, hipMemcpy2DAsync(F.feat[k].p, kFeatDim * 8, in[k], (size_t)dim * 8, (size_t)dim * 8,
+                                      (size_t)np[k], hipMemcpyHostToDevice, c->stream));
+        CTX_CHECK(c, launch_feat_norm(F.feat[k].p, np[k], F.fn2[k].p, c->stream));
+    }
+    const int parts = feat_nn_parts(nq);
+    CTX_CHECK(c, F.part_d.ensure((size_t)parts * nq));
+    CTX_CHECK(c, F.part_i.ensure((size_t)parts * nq));
+    CTX_CHECK(c, F.nn[0].ensure((size_t)nq));
+    CTX_CHECK(c, launch_feat_nn(F.feat[0].p, F.fn2[0].p, nq, F.feat[1].p, F.fn2[1].p, nt, F.part_d.p, F.part_i.p,
+                                F.nn[0].p, c->stream));
+    CTX_CHECK(c, hipMemcpyAsync(idx_out, F.nn[0].p, (size_t)nq * 4, hipMemcpyDeviceToHost, c->stream));
+    CTX_CHECK(c, hipStreamSynchronize(c->stream));
+    return ORPCD_OK;
+}
+
+int orpcd_fgr_optimize(orpcd_ctx* c, const double* src, int64_t n, const double* tgt, int64_t m,
+                       double normal_radius, int32_t normal_knn, double fpfh_radius, int32_t fpfh_knn,
+                       int32_t target_features_from_source, const orpcd_fgr_params* p, double* T_out,
+                       double* fitness_out, double* rmse_out, int64_t* ncorr_out, int64_t* n_mutual_out) {
+    if (!c) return ORPCD_EINVAL;
+    CTX_REQUIRE(c, src && tgt && p && T_out && n > 0 && m > 0, "fgr_optimize: bad arguments");
+    int rc = check_fgr_params(c, p);
+    if (rc) return rc;
+    CTX_REQUIRE(c, !target_features_from_source || m <= n,
+                "fgr_optimize: target features taken from the source need m <= n "
+                "(fastGlobalOptimizer.py:137-142 would index past the source's features)");
+    CTX_REQUIRE(c, finite_cloud(src, n) && finite_cloud(tgt, m), "fgr_optimize: non-finite coordinates");
+    CTX_CHECK(c, hipSetDevice(c->device));
+    const double* xyz[2] = {src, tgt};
+    const int64_t np[2] = {n, m};
+    for (int k = 0; k < 2; ++k) {
+        CTX_CHECK(c, c->fgr.xyz[k].ensure((size_t)np[k] * 3));
+        CTX_CHECK(c, hipMemcpyAsync(c->fgr.xyz[k].p, xyz[k], (size_t)np[k] * 24, hipMemcpyHostToDevice, c->stream));
+    }
+    rc = fpfh_device(c, 0, n, normal_radius, normal_knn, fpfh_radius, fpfh_knn);
+    if (rc) return rc;
+    CTX_CHECK(c, c->fgr.feat[1].ensure((size_t)m * kFeatDim));
+    if (target_features_from_source) {
+        CTX_CHECK(c, hipMemcpyAsync(c->fgr.feat[1].p, c->fgr.feat[0].p, (size_t)m * kFeatDim * 8,
+                                    hipMemcpyDeviceToDevice, c->stream));
+    } else {
+        rc = fpfh_device(c, 1, m, normal_radius, normal_knn, fpfh_radius, fpfh_knn);
+        if (rc) return rc;
+    }
+    return fgr_device(c, src, n, tgt, m, *p, T_out, fitness_out, rmse_out, ncorr_out, n_mutual_out);
 }
 
 int orpcd_set_option(orpcd_ctx* c, const char* key, double value) {

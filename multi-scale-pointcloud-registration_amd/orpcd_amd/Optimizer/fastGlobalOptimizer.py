@@ -1,0 +1,145 @@
+"""FastGlobalOptimizer plugin on the MI355X kernels.
+
+Reference: or_pcd/Optimizer/fastGlobalOptimizer.py:22-203 (wraps Open3D 0.18's
+``estimate_normals`` + ``compute_fpfh_feature`` + ``registration_fgr_based_on_
+feature_matching``).  Same constructor, defaults, validation (log + fall back
+to the default), R-transposed return (:176-178) and ``Warning`` raised when
+the evaluation finds no correspondence (:181-188).
+
+One call = one ``orpcd_fgr_optimize``: FPFH of both clouds, the fp64-MFMA
+mutual feature matching, the tuple test, the GNC IRLS and the evaluation all
+run against device-resident clouds; only the tuple test's sequential
+mt19937 draws run on the host.
+
+Quirk Q4 (fastGlobalOptimizer.py:137-142): the reference computes the TARGET
+features from the SOURCE cloud.  ``target_features_from_source=True`` (the
+default) reproduces that; it needs ``len(target) <= len(source)`` — the
+reference would index past the source's features otherwise, so this build
+raises ``ValueError`` there.  Set it to False for the evidently intended
+behaviour (features of each cloud).
+
+``seed`` seeds the tuple test's mt19937.  Open3D draws it from its global
+engine, which is not seeded by the reference, so the reference's FGR result
+varies run to run; here it is reproducible.
+"""
+from typing import Optional, Tuple
+
+import numpy as np
+
+from .. import _native
+from ..utils.constants import (
+    __DECREASE_MU__,
+    __DIVISION_FACTOR__,
+    __FGR_MAXIMUM_TUPLE_COUNT__,
+    __FPFH_KNN__,
+    __FPFH_RADIUS__,
+    __ITERATION_NUMBER__,
+    __MAXIMUM_CORRESPONDENCE_DISTANCE__,
+    __NORMAL_ESTIMATE_KNN__,
+    __NORMAL_ESTIMATE_RADIUS__,
+    __TUPLE_SCALE__,
+)
+from ..utils.logger_factory import LoggerFactory
+from .iOptimizer import IOptimizer
+
+_NO_CORR_MSG = """No correspondences detected from the optimizer. Parameters are not well set.
+        Probably due to:
+        -   maximum_correspondence_distance set too low
+        -   tuple_scale set too high
+        """
+
+
+class FastGlobalOptimizer(IOptimizer):
+    def __init__(
+        self,
+        division_factor: float = __DIVISION_FACTOR__,
+        tuple_scale: float = __TUPLE_SCALE__,
+        maximum_correspondence_distance: float = __MAXIMUM_CORRESPONDENCE_DISTANCE__,
+        iteration_number: int = __ITERATION_NUMBER__,
+        decrease_mu: bool = __DECREASE_MU__,
+        normal_estimate_radius: float = __NORMAL_ESTIMATE_RADIUS__,
+        normal_estimate_knn: int = __NORMAL_ESTIMATE_KNN__,
+        fpfh_radius: float = __FPFH_RADIUS__,
+        fpfh_knn: int = __FPFH_KNN__,
+        *,
+        target_features_from_source: bool = True,
+        maximum_tuple_count: int = __FGR_MAXIMUM_TUPLE_COUNT__,
+        seed: int = 0,
+        device: Optional[int] = None,
+    ):
+        self._LOG = LoggerFactory.get_logger(log_name=self.__class__.__name__)
+
+        def positive(value, default, what):
+            if value <= 0:
+                self._LOG.error(f"{what} cannot be 0 or less. Provided: {value}")
+                return default
+            return value
+
+        self._division_factor = positive(division_factor, __DIVISION_FACTOR__,
+                                         "division factor")
+        self._tuple_scale = positive(tuple_scale, __TUPLE_SCALE__, "tuple scale")
+        self._maximum_correspondence_distance = positive(maximum_correspondence_distance,
+            __MAXIMUM_CORRESPONDENCE_DISTANCE__, "maximum correspondence distance")
+        self._iteration_number = positive(iteration_number, __ITERATION_NUMBER__,
+                                          "iteration number")
+        self._decrease_mu = decrease_mu
+        self._fpfh_radius = positive(fpfh_radius, __FPFH_RADIUS__, "fpfh radius")
+        self._fpfh_knn = positive(fpfh_knn, __FPFH_KNN__, "fpfh knn")
+        self._normal_estimate_radius = positive(normal_estimate_radius,
+                                                __NORMAL_ESTIMATE_RADIUS__, "normal estimate radius")
+        self._normal_estimate_knn = positive(normal_estimate_knn, __NORMAL_ESTIMATE_KNN__,
+                                             "normal estimate knn")
+        if not (1 <= int(self._fpfh_knn) <= 64 and 1 <= int(self._normal_estimate_knn) <= 64):
+            raise ValueError("this build supports neighbourhoods of at most 64 points (knn <= 64)")
+        self._target_features_from_source = bool(target_features_from_source)
+        self._maximum_tuple_count = int(maximum_tuple_count)
+        self._seed = int(seed)
+        self._device = device
+        self._ctx = None
+        self.last_result = None
+        self._LOG.debug(msg=f"initialized optimizer: {self}")
+
+    @property
+    def context(self) -> _native.Context:
+        if self._ctx is None:
+            self._ctx = _native.default_context(self._device)
+        return self._ctx
+
+    def get_fpfh_features(self, source_point_cloud: np.ndarray, target_point_cloud: np.ndarray):
+        """(source features, target features), each (N, 33) — fastGlobalOptimizer.py:109-144,
+        including Q4 when ``target_features_from_source``."""
+        ctx = self.context
+        args = (self._normal_estimate_radius, self._normal_estimate_knn, self._fpfh_radius, self._fpfh_knn)
+        _, fs = ctx.fpfh(source_point_cloud, *args)
+        ft = fs.copy() if self._target_features_from_source else ctx.fpfh(target_point_cloud, *args)[1]
+        return fs, ft
+
+    def optimize(self, source: np.ndarray, target: np.ndarray, **kwargs) -> Tuple[np.ndarray, float]:
+        r = self.context.fgr_optimize(
+            source, target, normal_radius=self._normal_estimate_radius, normal_knn=self._normal_estimate_knn,
+            fpfh_radius=self._fpfh_radius, fpfh_knn=self._fpfh_knn,
+            target_features_from_source=self._target_features_from_source,
+            division_factor=self._division_factor, tuple_scale=self._tuple_scale,
+            maximum_correspondence_distance=self._maximum_correspondence_distance,
+            iteration_number=self._iteration_number, decrease_mu=self._decrease_mu,
+            maximum_tuple_count=self._maximum_tuple_count, seed=self._seed)
+        self.last_result = r
+        roto_translation = np.copy(r["T"])
+        roto_translation[:3, :3] = roto_translation[:3, :3].T
+        if r["ncorr"] == 0:
+            self._LOG.error(_NO_CORR_MSG)
+            raise Warning(_NO_CORR_MSG)
+        return roto_translation, r["rmse"]
+
+    def __repr__(self):
+        return f"""{self.__class__.__name__}
+            (division_factor={self._division_factor},
+            tuple_scale={self._tuple_scale},
+            maximum_correspondence_distance={self._maximum_correspondence_distance},
+            iteration_number={self._iteration_number},
+            decrease_mu={self._decrease_mu},
+            normal_estimate_radius={self._normal_estimate_radius},
+            normal_estimate_knn={self._normal_estimate_knn},
+            fpfh_radius={self._fpfh_radius},
+            fpfh_knn={self._fpfh_knn})"
+        """

@@ -12,5 +12,5 @@ ctypes C-ABI (include/orpcd.h).  There is no CPU fallback.
 __version__ = "0.1.0"
 
 from .Aligner import Aligner  # noqa: F401,E402
-from .Optimizer import GeneralizedICP, IOptimizer  # noqa: F401,E402
+from .Optimizer import FastGlobalOptimizer, GeneralizedICP, IOptimizer  # noqa: F401,E402
 from .Preprocessor import Preprocessor  # noqa: F401,E402

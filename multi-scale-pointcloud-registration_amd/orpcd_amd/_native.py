@@ -46,7 +46,9 @@ _lib_lock = threading.Lock()
 # every symbol include/orpcd.h declares (checked by tests/test_abi.py)
 EXPORTED = ("orpcd_abi_version", "orpcd_device_count", "orpcd_ctx_create", "orpcd_ctx_destroy",
             "orpcd_last_error", "orpcd_set_target", "orpcd_set_source", "orpcd_gicp_batch",
-            "orpcd_nn1_radius", "orpcd_estimate_normals", "orpcd_fpfh", "orpcd_fgr", "orpcd_set_option",
+            "orpcd_nn1_radius", "orpcd_estimate_normals", "orpcd_fpfh", "orpcd_fpfh_from_normals", "orpcd_fgr", "orpcd_feature_nn",
+            "orpcd_fgr_optimize",
+            "orpcd_set_option",
             "orpcd_profiling", "orpcd_stats", "orpcd_reset_stats")
 
 
@@ -75,8 +77,13 @@ def load_library():
         L.orpcd_nn1_radius.argtypes = [vp, _f64p, c_i64, _f64p, c_i64, c_dbl, _i32p, _f64p]
         L.orpcd_estimate_normals.argtypes = [vp, _f64p, c_i64, ctypes.c_int32, c_dbl, c_dbl, vp, vp, vp]
         L.orpcd_fpfh.argtypes = [vp, _f64p, c_i64, c_dbl, ctypes.c_int32, c_dbl, ctypes.c_int32, _f64p, _f64p]
+        L.orpcd_fpfh_from_normals.argtypes = [vp, _f64p, _f64p, c_i64, c_dbl, ctypes.c_int32, _f64p]
         L.orpcd_fgr.argtypes = [vp, _f64p, c_i64, _f64p, c_i64, _f64p, _f64p, ctypes.POINTER(FgrParams), _f64p,
                                 _f64p, _f64p, _i64p, _i64p]
+        L.orpcd_feature_nn.argtypes = [vp, _f64p, c_i64, _f64p, c_i64, ctypes.c_int32, _i32p]
+        L.orpcd_fgr_optimize.argtypes = [vp, _f64p, c_i64, _f64p, c_i64, c_dbl, ctypes.c_int32, c_dbl,
+                                         ctypes.c_int32, ctypes.c_int32, ctypes.POINTER(FgrParams), _f64p, _f64p,
+                                         _f64p, _i64p, _i64p]
         L.orpcd_set_option.argtypes = [vp, ctypes.c_char_p, c_dbl]
         L.orpcd_profiling.argtypes = [vp, ctypes.c_int32]
         L.orpcd_stats.argtypes = [vp, _f64p, ctypes.c_int32]
@@ -204,20 +211,66 @@ class Context:
                                        float(fpfh_radius), int(fpfh_knn), normals, feat.reshape(-1)), "orpcd_fpfh")
         return normals, feat
 
+    def fpfh_from_normals(self, xyz: np.ndarray, normals: np.ndarray, fpfh_radius=0.1, fpfh_knn=20):
+        xyz, normals = _c3(xyz), _c3(normals)
+        if len(normals) != len(xyz):
+            raise ValueError("fpfh_from_normals: one normal per point")
+        feat = np.empty((len(xyz), 33))
+        self._check(self._L.orpcd_fpfh_from_normals(self._h, xyz, normals, len(xyz), float(fpfh_radius),
+                                                    int(fpfh_knn), feat.reshape(-1)), "orpcd_fpfh_from_normals")
+        return feat
+
+    def feature_nn(self, q: np.ndarray, t: np.ndarray) -> np.ndarray:
+        """Nearest row of ``t`` for every row of ``q`` (squared L2, ties -> lowest index)."""
+        q = np.ascontiguousarray(q, dtype=np.float64)
+        t = np.ascontiguousarray(t, dtype=np.float64)
+        if q.ndim != 2 or t.ndim != 2 or q.shape[1] != t.shape[1]:
+            raise ValueError(f"feature_nn: expected (Nq, D) and (Nt, D), got {q.shape} and {t.shape}")
+        idx = np.empty(len(q), np.int32)
+        self._check(self._L.orpcd_feature_nn(self._h, q.reshape(-1), len(q), t.reshape(-1), len(t), q.shape[1],
+                                             idx), "orpcd_feature_nn")
+        return idx
+
     def fgr(self, src, tgt, src_feat, tgt_feat, division_factor=1.4, tuple_scale=0.9,
             maximum_correspondence_distance=0.5, iteration_number=100, decrease_mu=True,
             maximum_tuple_count=1000, seed=0) -> dict:
         src, tgt = _c3(src), _c3(tgt)
         fs = np.ascontiguousarray(src_feat, dtype=np.float64)
         ft = np.ascontiguousarray(tgt_feat, dtype=np.float64)
-        p = FgrParams(float(division_factor), float(tuple_scale), float(maximum_correspondence_distance),
-                      int(iteration_number), int(bool(decrease_mu)), int(maximum_tuple_count),
-                      int(seed) & 0xFFFFFFFFFFFFFFFF)
+        if fs.shape != (len(src), 33) or ft.shape != (len(tgt), 33):
+            raise ValueError(f"features must be (N, 33) per cloud, got {fs.shape} and {ft.shape}")
+        p = self._fgr_params(division_factor, tuple_scale, maximum_correspondence_distance, iteration_number,
+                             decrease_mu, maximum_tuple_count, seed)
         T = np.zeros(16)
         fit, rmse = np.zeros(1), np.zeros(1)
         nc, nm = np.zeros(1, np.int64), np.zeros(2, np.int64)
         self._check(self._L.orpcd_fgr(self._h, src, len(src), tgt, len(tgt), fs.reshape(-1), ft.reshape(-1),
                                       ctypes.byref(p), T, fit, rmse, nc, nm), "orpcd_fgr")
+        return dict(T=T.reshape(4, 4), fitness=float(fit[0]), rmse=float(rmse[0]), ncorr=int(nc[0]),
+                    n_mutual=int(nm[0]), n_tuple_corr=int(nm[1]))
+
+    @staticmethod
+    def _fgr_params(division_factor, tuple_scale, maximum_correspondence_distance, iteration_number, decrease_mu,
+                    maximum_tuple_count, seed):
+        return FgrParams(float(division_factor), float(tuple_scale), float(maximum_correspondence_distance),
+                         int(iteration_number), int(bool(decrease_mu)), int(maximum_tuple_count),
+                         int(seed) & 0xFFFFFFFFFFFFFFFF)
+
+    def fgr_optimize(self, src, tgt, normal_radius=0.1, normal_knn=20, fpfh_radius=0.1, fpfh_knn=20,
+                     target_features_from_source=True, division_factor=1.4, tuple_scale=0.9,
+                     maximum_correspondence_distance=0.5, iteration_number=100, decrease_mu=True,
+                     maximum_tuple_count=1000, seed=0) -> dict:
+        """FPFH of both clouds + FGR in one device pass (orpcd_fgr_optimize)."""
+        src, tgt = _c3(src), _c3(tgt)
+        p = self._fgr_params(division_factor, tuple_scale, maximum_correspondence_distance, iteration_number,
+                             decrease_mu, maximum_tuple_count, seed)
+        T = np.zeros(16)
+        fit, rmse = np.zeros(1), np.zeros(1)
+        nc, nm = np.zeros(1, np.int64), np.zeros(2, np.int64)
+        self._check(self._L.orpcd_fgr_optimize(self._h, src, len(src), tgt, len(tgt), float(normal_radius),
+                                               int(normal_knn), float(fpfh_radius), int(fpfh_knn),
+                                               int(bool(target_features_from_source)), ctypes.byref(p), T, fit,
+                                               rmse, nc, nm), "orpcd_fgr_optimize")
         return dict(T=T.reshape(4, 4), fitness=float(fit[0]), rmse=float(rmse[0]), ncorr=int(nc[0]),
                     n_mutual=int(nm[0]), n_tuple_corr=int(nm[1]))
 

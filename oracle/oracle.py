@@ -65,9 +65,9 @@ def lib():
     L.oracle_gicp.argtypes = [_f64p, c_i64, _f64p, c_i64, c_dbl, c_int, c_dbl, c_dbl, c_dbl,
                               _f64p, _f64p, _f64p, _i32p, _i64p, vp, vp, vp]
     L.oracle_gicp_step.argtypes = [_f64p, _f64p, c_i64, _f64p, _f64p, c_i64, _i32p, _f64p, _f64p, _f64p]
-    if hasattr(L, "oracle_fpfh"):
-        L.oracle_fpfh.argtypes = [_f64p, c_i64, c_dbl, c_int, c_dbl, c_int, _f64p, _f64p]
-        L.oracle_fgr.argtypes = [_f64p, c_i64, _f64p, c_i64, _f64p, _f64p, c_dbl, c_dbl, c_dbl, c_int, c_int,
+    L.oracle_fpfh.argtypes = [_f64p, c_i64, c_dbl, c_int, c_dbl, c_int, _f64p, _f64p]
+    L.oracle_fpfh_from_normals.argtypes = [_f64p, _f64p, c_i64, c_dbl, c_int, _f64p]
+    L.oracle_fgr.argtypes = [_f64p, c_i64, _f64p, c_i64, _f64p, _f64p, c_dbl, c_dbl, c_dbl, c_int, c_int,
                                  c_int, ctypes.c_uint64, _f64p, _f64p, _f64p, _i64p, _i64p]
     _lib = L
     return L
@@ -194,6 +194,14 @@ def fpfh(points: np.ndarray, normal_radius: float = 0.1, normal_knn: int = 20, f
     return normals, feat
 
 
+def fpfh_from_normals(points: np.ndarray, normals: np.ndarray, fpfh_radius: float = 0.1, fpfh_knn: int = 20):
+    """compute_fpfh_feature(Hybrid) on a cloud that carries normals → (N, 33)."""
+    p, nr = _c3(points), _c3(normals)
+    feat = np.empty((len(p), 33))
+    lib().oracle_fpfh_from_normals(p, nr, len(p), float(fpfh_radius), int(fpfh_knn), feat.reshape(-1))
+    return feat
+
+
 def fgr(source, target, source_feat, target_feat, division_factor=1.4, tuple_scale=0.9,
         maximum_correspondence_distance=0.5, iteration_number=100, decrease_mu=True,
         maximum_tuple_count=1000, seed=0) -> dict:
@@ -247,7 +255,13 @@ class OracleFastGlobalOptimizer:
 
     def optimize(self, source, target, **kwargs):
         _, fs = fpfh(source, self.nr, self.nk, self.fr, self.fk)
-        ft = fs if self.compat_q4 else fpfh(target, self.nr, self.nk, self.fr, self.fk)[1]
+        if self.compat_q4:
+            # Q4: Open3D indexes the (source) feature columns by target point index
+            if len(target) > len(source):
+                raise ValueError("Q4 with more target than source points reads past the features")
+            ft = fs[:len(target)]
+        else:
+            ft = fpfh(target, self.nr, self.nk, self.fr, self.fk)[1]
         r = fgr(source, target, fs, ft, seed=self.seed, **self.opt)
         T = np.copy(r["T"])
         T[:3, :3] = T[:3, :3].T

@@ -1,0 +1,168 @@
+"""GPU parity for the FastGlobal path (orpcd_fpfh / orpcd_feature_nn /
+orpcd_fgr / orpcd_fgr_optimize) against the CPU oracle.
+
+Tolerances:
+  * normals: fp64, same operation order: 1e-10; FPFH features: 1e-9 absolute
+    (values 0..200; a histogram bin can only change if a pair feature lands
+    within rounding of a bin edge, which the test counts and bounds);
+  * feature nearest neighbour: identical indices, except certified near-ties
+    whose exact squared distances differ by <= 1e-9 relative (the GPU forms
+    |q|^2 + |t|^2 - 2 q.t on the fp64 matrix cores);
+  * FGR with the same features and seed: the same mutual-match and tuple
+    counts (so the same tuples), T elementwise <= 1e-9, fitness identical,
+    RMSE <= 1e-9 relative.
+"""
+import numpy as np
+import pytest
+
+from workloads import bumpy_sphere, rot_xyz
+
+pytestmark = pytest.mark.gpu
+
+
+def _pair(n=3000, m=None, seed=4, deg=(25, -10, 40), t=(0.1, -0.05, 0.2), noise=0.0):
+    rng = np.random.default_rng(seed)
+    src = bumpy_sphere(n, rng) * np.array([1.0, 0.8, 0.6])
+    m = n if m is None else m
+    base = src[:m] if m <= n else bumpy_sphere(m, rng) * np.array([1.0, 0.8, 0.6])
+    tgt = base @ rot_xyz(*deg).T + np.array(t) + rng.normal(0, noise, size=(m, 3))
+    return src, tgt
+
+
+ARGS = ((0.1, 20, 0.25, 40), (0.3, 8, 0.2, 64), (0.05, 30, 0.1, 20))
+
+
+def test_fpfh_from_normals_matches_oracle(ctx, oracle):
+    src, _ = _pair(5003)                              # ragged size
+    for nr, nk, fr, fk in ARGS:
+        normals, _ = oracle.fpfh(src, nr, nk, fr, fk)
+        of = oracle.fpfh_from_normals(src, normals, fr, fk)
+        gf = ctx.fpfh_from_normals(src, normals, fr, fk)
+        assert np.allclose(gf, of, atol=1e-9, rtol=0), np.abs(gf - of).max()
+
+
+def test_fpfh_matches_oracle(ctx, oracle):
+    """Normals to 1e-10.  Open3D's pair feature swaps the two points when
+    acos(|n1.d|) > acos(|n2.d|): for two points whose neighbourhoods coincide
+    the normals agree to rounding and that test is decided by the last bits
+    of the normals (libm acos/cos inside FastEigen3x3 on either side).  Such a
+    flip moves one SPFH count (100/(k-1)) between two mirrored bins and
+    spreads to the neighbours' FPFH; the test bounds how often that happens
+    and that nothing else differs (test_fpfh_from_normals_matches_oracle
+    shows the features are otherwise identical)."""
+    src, _ = _pair(5003)
+    for nr, nk, fr, fk in ARGS:
+        on, of = oracle.fpfh(src, nr, nk, fr, fk)
+        gn, gf = ctx.fpfh(src, nr, nk, fr, fk)
+        assert np.allclose(gn, on, atol=1e-10, rtol=0)
+        bad = np.nonzero(~np.all(np.abs(gf - of) <= 1e-9, axis=1))[0]
+        assert len(bad) <= 0.02 * len(src), f"{len(bad)} feature rows differ for {(nr, nk, fr, fk)}"
+        assert np.abs(gf - of).max() <= 2 * 100.0 / (fk - 1)
+
+
+def test_fpfh_edge_cases(ctx, oracle):
+    pts = np.array([[0.0, 0, 0], [5.0, 0, 0], [0, 5.0, 0]])     # isolated points
+    gn, gf = ctx.fpfh(pts, 0.1, 20, 0.1, 20)
+    on, of = oracle.fpfh(pts, 0.1, 20, 0.1, 20)
+    assert np.array_equal(gf, of) and np.all(gf == 0) and np.allclose(gn, on)
+    dup = np.repeat(np.random.default_rng(1).normal(size=(50, 3)) * 0.05, 3, axis=0)   # duplicates
+    gn, gf = ctx.fpfh(dup, 0.1, 10, 0.1, 10)
+    on, of = oracle.fpfh(dup, 0.1, 10, 0.1, 10)
+    assert np.allclose(gn, on, atol=1e-10) and np.allclose(gf, of, atol=1e-9)
+    with pytest.raises(ValueError):
+        ctx.fpfh(dup, 0.1, 65, 0.1, 10)
+
+
+def _certify_feature_nn(q, t, got):
+    d = ((q[:, None, :] - t[None, :, :]) ** 2).sum(-1)
+    want = np.argmin(d, axis=1)                       # first minimum = lowest index
+    bad = np.nonzero(want != got)[0]
+    for i in bad:
+        a, b = d[i, want[i]], d[i, got[i]]
+        assert abs(a - b) <= 1e-9 * max(a, b, 1e-300), f"row {i}: {a} vs {b}"
+    return len(bad)
+
+
+def test_feature_nn_matches_brute_force(ctx):
+    rng = np.random.default_rng(2)
+    for nq, nt, dim in ((1000, 3001, 33), (257, 70, 33), (64, 1, 5), (5, 200, 36)):
+        q = rng.random((nq, dim)) * 100
+        t = rng.random((nt, dim)) * 100
+        got = ctx.feature_nn(q, t)
+        assert _certify_feature_nn(q, t, got) == 0
+    # exact duplicates and all-zero rows: lowest index
+    t = np.zeros((300, 33))
+    t[100:] = rng.random((200, 33))
+    t[250] = t[120]
+    q = np.vstack([np.zeros((1, 33)), t[120:121], t[200:201] + 1e-3])
+    got = ctx.feature_nn(q, t)
+    assert got[0] == 0 and got[1] == 120 and got[2] == 200
+    assert len(ctx.feature_nn(np.zeros((0, 33)), t)) == 0
+
+
+def test_feature_nn_large_splits(ctx):
+    rng = np.random.default_rng(3)
+    q = rng.random((600, 33)) * 50
+    t = rng.random((20000, 33)) * 50                  # several target parts
+    assert _certify_feature_nn(q, t, ctx.feature_nn(q, t)) == 0
+
+
+@pytest.mark.parametrize("case", ["q4", "own", "swap", "noisy"])
+def test_fgr_matches_oracle_same_features(ctx, oracle, case):
+    if case == "swap":   # more target than source points: Open3D swaps the roles
+        src, tgt = _pair(2000, 2600, noise=1e-3)
+    elif case == "noisy":
+        src, tgt = _pair(3000, 3000, seed=8, noise=5e-3)
+    else:
+        src, tgt = _pair(3000)
+    _, fs = oracle.fpfh(src, 0.1, 20, 0.25, 40)
+    ft = fs[:len(tgt)] if case == "q4" else oracle.fpfh(tgt, 0.1, 20, 0.25, 40)[1]
+    kw = dict(maximum_correspondence_distance=0.05, seed=7)
+    o = oracle.fgr(src, tgt, fs, ft, **kw)
+    g = ctx.fgr(src, tgt, fs, ft, **kw)
+    assert g["n_mutual"] == o["n_mutual"] and g["n_tuple_corr"] == o["n_tuple_corr"]
+    assert np.allclose(g["T"], o["T"], atol=1e-9, rtol=0)
+    assert g["ncorr"] == o["ncorr"] and g["fitness"] == o["fitness"]
+    assert abs(g["rmse"] - o["rmse"]) <= 1e-12 + 1e-9 * o["rmse"]
+
+
+def test_fgr_optimize_plugin_matches_oracle_plugin(ctx, oracle):
+    from orpcd_amd.Optimizer import FastGlobalOptimizer
+    src, tgt = _pair(4000, noise=1e-3)
+    for q4 in (True, False):
+        kw = dict(maximum_correspondence_distance=0.05, fpfh_radius=0.25, fpfh_knn=40)
+        gopt = FastGlobalOptimizer(**kw, target_features_from_source=q4, seed=5)
+        oopt = oracle.OracleFastGlobalOptimizer(**kw, seed=5, compat_q4=q4)
+        gT, grmse = gopt.optimize(src, tgt)
+        oT, ormse = oopt.optimize(src, tgt)
+        assert np.allclose(gT, oT, atol=1e-9, rtol=0)
+        assert abs(grmse - ormse) <= 1e-12 + 1e-9 * ormse
+        fs, ft = gopt.get_fpfh_features(src, tgt)
+        assert fs.shape == (4000, 33) and (np.array_equal(fs, ft) if q4 else not np.array_equal(fs, ft))
+
+
+def test_fgr_plugin_errors(ctx):
+    from orpcd_amd.Optimizer import FastGlobalOptimizer
+    src, tgt = _pair(500, 700)
+    with pytest.raises(ValueError):        # Q4 with m > n would read past the features
+        FastGlobalOptimizer().optimize(src, tgt)
+    src, tgt = _pair(800)
+    with pytest.raises(Warning):           # no correspondence within the distance
+        FastGlobalOptimizer(maximum_correspondence_distance=1e-9).optimize(
+            src, np.random.default_rng(0).normal(size=tgt.shape))
+    opt = FastGlobalOptimizer(division_factor=-1, tuple_scale=0, iteration_number=-3)
+    assert opt._division_factor == 1.4 and opt._tuple_scale == 0.9 and opt._iteration_number == 100
+
+
+def test_aligner_with_fgr_matches_oracle_aligner(ctx, oracle):
+    from orpcd_amd import Aligner, FastGlobalOptimizer, Preprocessor
+    src, tgt = _pair(1500, noise=1e-3)
+    kw = dict(maximum_correspondence_distance=0.05, fpfh_radius=0.25, fpfh_knn=40)
+    np.random.seed(3)
+    al = Aligner(Preprocessor([]), Preprocessor([]), FastGlobalOptimizer(**kw, seed=1), attempts=3, max_iter=2)
+    gT, gm, gsf, gerr = al.align(src.copy(), tgt.copy(), refine_registration=False)
+    np.random.seed(3)
+    oal = oracle.OracleAligner(oracle.OracleFastGlobalOptimizer(**kw, seed=1), attempts=3, max_iter=2)
+    oT, om, osf, oerr = oal.align(src.copy(), tgt.copy())
+    assert np.array_equal(gsf, osf)
+    assert np.allclose(gT, oT, atol=1e-8) and abs(gm - om) <= 1e-9
