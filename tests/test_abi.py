@@ -34,10 +34,12 @@ def test_library_exports_every_declared_symbol():
     assert L.orpcd_abi_version() == 1
 
 
-def test_library_is_gfx950_code_object():
+def test_library_is_gfx950_code_object(tmp_path):
+    import shutil
     from orpcd_amd import _native
-    out = subprocess.run(["/opt/rocm/lib/llvm/bin/llvm-objdump", "--offloading", _native.LIB_PATH],
-                         capture_output=True, text=True)
+    lib = shutil.copy(_native.LIB_PATH, tmp_path)     # --offloading extracts the bundles next to its input
+    out = subprocess.run(["/opt/rocm/lib/llvm/bin/llvm-objdump", "--offloading", lib],
+                         capture_output=True, text=True, cwd=tmp_path)
     text = out.stdout + out.stderr
     if "gfx" not in text:  # older objdump: fall back to scanning the bundle
         text = open(_native.LIB_PATH, "rb").read().decode("latin1")
