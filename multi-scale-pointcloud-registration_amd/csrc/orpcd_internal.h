@@ -176,11 +176,11 @@ namespace orpcd {
 // sort_kernels.hip
 hipError_t build_layout(const double* dev_in64, int64_t n, const double bbox_lo[3], double bbox_ext, CloudLayout& L,
                         bool with_tiles, hipStream_t s);
-hipError_t launch_unpermute(const double* in, const int32_t* perm, int64_t n, int w, double* out, hipStream_t s);
 
 // knn_kernels.hip
-hipError_t launch_knn_cov(const double* pts, int64_t n, int k, double radius, double* rawcov6, int32_t* nbr_idx,
-                          double* nbr_d2, int32_t* nbr_cnt, hipStream_t s);
+hipError_t launch_knn_tiles(const CloudLayout& L, const double* in64, int k, double radius, double margin,
+                            bool out_input_order, double* rawcov6, int32_t* nbr_idx, double* nbr_d2,
+                            int32_t* nbr_cnt, hipStream_t s);
 hipError_t launch_normals_cov(const double* rawcov6, int64_t n, const double* Rc9, int nslots, double eps,
                               double* normals3, double* cov6, hipStream_t s);
 

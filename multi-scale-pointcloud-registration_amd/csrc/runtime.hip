@@ -54,24 +54,42 @@ void host_bbox(const double* xyz, int64_t n, double lo[3], double* ext) {
     *ext = std::max(hi[0] - lo[0], std::max(hi[1] - lo[1], hi[2] - lo[2]));
 }
 
-// Upload a cloud (input order) and lay it out in Morton order on device.
-int upload_layout(orpcd_ctx* c, const double* xyz, int64_t n, CloudLayout& L, bool tiles) {
+// Absolute bound (with 4x safety) on the fp32 rounding of any coordinate of
+// the cloud: the culled KNN widens its fp32 box tests by it.
+double coord_margin(const double lo[3], double ext) {
+    double m = 0.0;
+    for (int a = 0; a < 3; ++a) m = std::max(m, std::max(std::fabs(lo[a]), std::fabs(lo[a] + ext)));
+    return m * 0x1p-21;
+}
+
+// Lay out a device-resident (input-order) cloud in Morton order with tiles.
+int layout_from_device(orpcd_ctx* c, const double* host_xyz, const double* dev_xyz, int64_t n, CloudLayout& L,
+                       bool tiles, double* margin = nullptr) {
     double lo[3], ext;
-    host_bbox(xyz, n, lo, &ext);
+    host_bbox(host_xyz, n, lo, &ext);
+    if (margin) *margin = coord_margin(lo, ext);
+    CTX_CHECK(c, build_layout(dev_xyz, n, lo, ext, L, tiles, c->stream));
+    return ORPCD_OK;
+}
+
+// Upload a cloud (input order, kept in scratch64a) and lay it out in Morton
+// order on device.
+int upload_layout(orpcd_ctx* c, const double* xyz, int64_t n, CloudLayout& L, bool tiles, double* margin = nullptr) {
     CTX_CHECK(c, c->scratch64a.ensure((size_t)n * 3));
     CTX_CHECK(c, hipMemcpyAsync(c->scratch64a.p, xyz, (size_t)n * 24, hipMemcpyHostToDevice, c->stream));
-    CTX_CHECK(c, build_layout(c->scratch64a.p, n, lo, ext, L, tiles, c->stream));
-    return ORPCD_OK;
+    return layout_from_device(c, xyz, c->scratch64a.p, n, L, tiles, margin);
 }
 
 // Target: Morton layout + tiles + GICP covariances (KNN-20 normals).
 int upload_target(orpcd_ctx* c, const double* xyz, int64_t m, double eps) {
-    int rc = upload_layout(c, xyz, m, c->tgt, true);
+    double margin = 0.0;
+    int rc = upload_layout(c, xyz, m, c->tgt, true, &margin);
     if (rc) return rc;
     CTX_CHECK(c, c->tcov.ensure((size_t)m * 6));
     CTX_CHECK(c, c->scratch64b.ensure((size_t)m * 6));
     if (eps >= 0.0) {
-        CTX_CHECK(c, launch_knn_cov(c->tgt.xyz64.p, m, 20, -1.0, c->scratch64b.p, nullptr, nullptr, nullptr, c->stream));
+        CTX_CHECK(c, launch_knn_tiles(c->tgt, c->scratch64a.p, 20, -1.0, margin, false, c->scratch64b.p, nullptr,
+                                      nullptr, nullptr, c->stream));
         CTX_CHECK(c, launch_normals_cov(c->scratch64b.p, m, nullptr, 1, eps, nullptr, c->tcov.p, c->stream));
     }
     c->tgt_eps = eps;
@@ -109,7 +127,8 @@ int check_fgr_params(orpcd_ctx* c, const orpcd_fgr_params* p) {
 // (fastGlobalOptimizer.py:114-142).  Normals -> fgr.nrm, features (n x 36,
 // padded) -> fgr.feat[k].  Neighbour sets are exact (ties -> lower index) in
 // input order, as the KD-tree of the oracle returns them.
-int features_device(orpcd_ctx* c, int k, int64_t n, double fpfh_radius, int fpfh_knn);
+int features_device(orpcd_ctx* c, const double* host_xyz, int k, int64_t n, double fpfh_radius, int fpfh_knn,
+                    double margin);
 
 int fpfh_buffers(orpcd_ctx* c, int k, int64_t n, int fpfh_knn) {
     auto& F = c->fgr;
@@ -123,25 +142,36 @@ int fpfh_buffers(orpcd_ctx* c, int k, int64_t n, int fpfh_knn) {
     return ORPCD_OK;
 }
 
-int fpfh_device(orpcd_ctx* c, int k, int64_t n, double normal_radius, int normal_knn, double fpfh_radius,
-                int fpfh_knn) {
+int fpfh_device(orpcd_ctx* c, const double* host_xyz, int k, int64_t n, double normal_radius, int normal_knn,
+                double fpfh_radius, int fpfh_knn) {
     CTX_REQUIRE(c, normal_knn > 0 && normal_knn <= 64 && fpfh_knn > 0 && fpfh_knn <= 64,
                 "fpfh: knn must be in [1, 64]");
     CTX_REQUIRE(c, normal_radius > 0 && fpfh_radius > 0, "fpfh: radii must be > 0");
     int rc = fpfh_buffers(c, k, n, fpfh_knn);
     if (rc) return rc;
     auto& F = c->fgr;
-    const double* pts = F.xyz[k].p;
-    CTX_CHECK(c, launch_knn_cov(pts, n, normal_knn, normal_radius, F.raw.p, nullptr, nullptr, nullptr, c->stream));
+    double margin = 0.0;
+    rc = layout_from_device(c, host_xyz, F.xyz[k].p, n, c->aux, true, &margin);
+    if (rc) return rc;
+    CTX_CHECK(c, launch_knn_tiles(c->aux, F.xyz[k].p, normal_knn, normal_radius, margin, true, F.raw.p, nullptr,
+                                  nullptr, nullptr, c->stream));
     CTX_CHECK(c, launch_normals_cov(F.raw.p, n, nullptr, 1, -1.0, F.nrm.p, nullptr, c->stream));
-    return features_device(c, k, n, fpfh_radius, fpfh_knn);
+    return features_device(c, nullptr, k, n, fpfh_radius, fpfh_knn, margin);
 }
 
-// compute_fpfh_feature of fgr.xyz[k] with the normals in fgr.nrm.
-int features_device(orpcd_ctx* c, int k, int64_t n, double fpfh_radius, int fpfh_knn) {
+// compute_fpfh_feature of fgr.xyz[k] with the normals in fgr.nrm.  host_xyz
+// (the same cloud on the host) == nullptr: c->aux already holds its layout
+// and `margin` its box margin.
+int features_device(orpcd_ctx* c, const double* host_xyz, int k, int64_t n, double fpfh_radius, int fpfh_knn,
+                    double margin) {
     auto& F = c->fgr;
     const double* pts = F.xyz[k].p;
-    CTX_CHECK(c, launch_knn_cov(pts, n, fpfh_knn, fpfh_radius, nullptr, F.nbr.p, F.nd2.p, F.cnt.p, c->stream));
+    if (host_xyz) {
+        int rc = layout_from_device(c, host_xyz, pts, n, c->aux, true, &margin);
+        if (rc) return rc;
+    }
+    CTX_CHECK(c, launch_knn_tiles(c->aux, pts, fpfh_knn, fpfh_radius, margin, true, nullptr, F.nbr.p, F.nd2.p,
+                                  F.cnt.p, c->stream));
     CTX_CHECK(c, launch_fpfh(pts, F.nrm.p, n, F.nbr.p, F.nd2.p, F.cnt.p, fpfh_knn, F.spfh.p, F.feat[k].p, c->stream));
     return ORPCD_OK;
 }
@@ -389,10 +419,12 @@ int orpcd_set_source(orpcd_ctx* c, const double* xyz, int64_t n) {
     CTX_REQUIRE(c, n < (int64_t)1 << 30, "set_source: too many points");
     CTX_REQUIRE(c, finite_cloud(xyz, n), "set_source: non-finite coordinates");
     CTX_CHECK(c, hipSetDevice(c->device));
-    int rc = upload_layout(c, xyz, n, c->src, false);
+    double margin = 0.0;
+    int rc = upload_layout(c, xyz, n, c->src, true, &margin);
     if (rc) return rc;
     CTX_CHECK(c, c->sraw.ensure((size_t)n * 6));
-    CTX_CHECK(c, launch_knn_cov(c->src.xyz64.p, n, 20, -1.0, c->sraw.p, nullptr, nullptr, nullptr, c->stream));
+    CTX_CHECK(c, launch_knn_tiles(c->src, c->scratch64a.p, 20, -1.0, margin, false, c->sraw.p, nullptr, nullptr,
+                                  nullptr, c->stream));
     CTX_CHECK(c, hipStreamSynchronize(c->stream));
     return ORPCD_OK;
 }
@@ -591,22 +623,17 @@ int orpcd_estimate_normals(orpcd_ctx* c, const double* xyz, int64_t n, int32_t k
     CTX_REQUIRE(c, knn > 0 && knn <= 64, "estimate_normals: knn must be in [1, 64]");
     CTX_REQUIRE(c, finite_cloud(xyz, n), "estimate_normals: non-finite coordinates");
     CTX_CHECK(c, hipSetDevice(c->device));
-    int rc = upload_layout(c, xyz, n, c->aux, false);
+    double margin = 0.0;
+    int rc = upload_layout(c, xyz, n, c->aux, true, &margin);
     if (rc) return rc;
-    // Morton-order results in scratch64b: raw(6n) | normals(3n) | cov(6n)
-    CTX_CHECK(c, c->scratch64b.ensure((size_t)n * 15));
+    // input-order results in scratch64c: raw(6n) | normals(3n) | cov(6n)
     CTX_CHECK(c, c->scratch64c.ensure((size_t)n * 15));
-    double* raw = c->scratch64b.p;
-    double* nrm = raw + 6 * n;
-    double* cov = nrm + 3 * n;
-    CTX_CHECK(c, launch_knn_cov(c->aux.xyz64.p, n, knn, radius, raw, nullptr, nullptr, nullptr, c->stream));
-    CTX_CHECK(c, launch_normals_cov(raw, n, nullptr, 1, epsilon, nrm, epsilon >= 0 ? cov : nullptr, c->stream));
     double* uraw = c->scratch64c.p;
     double* unrm = uraw + 6 * n;
     double* ucov = unrm + 3 * n;
-    CTX_CHECK(c, launch_unpermute(raw, c->aux.perm.p, n, 6, uraw, c->stream));
-    CTX_CHECK(c, launch_unpermute(nrm, c->aux.perm.p, n, 3, unrm, c->stream));
-    if (epsilon >= 0) CTX_CHECK(c, launch_unpermute(cov, c->aux.perm.p, n, 6, ucov, c->stream));
+    CTX_CHECK(c, launch_knn_tiles(c->aux, c->scratch64a.p, knn, radius, margin, true, uraw, nullptr, nullptr, nullptr,
+                                  c->stream));
+    CTX_CHECK(c, launch_normals_cov(uraw, n, nullptr, 1, epsilon, unrm, epsilon >= 0 ? ucov : nullptr, c->stream));
     std::vector<double> raw6((size_t)n * 6), cov6;
     CTX_CHECK(c, hipMemcpyAsync(raw6.data(), uraw, (size_t)n * 48, hipMemcpyDeviceToHost, c->stream));
     if (normals_out) CTX_CHECK(c, hipMemcpyAsync(normals_out, unrm, (size_t)n * 24, hipMemcpyDeviceToHost, c->stream));
@@ -643,7 +670,7 @@ int orpcd_fpfh(orpcd_ctx* c, const double* xyz, int64_t n, double normal_radius,
     CTX_CHECK(c, hipSetDevice(c->device));
     CTX_CHECK(c, c->fgr.xyz[0].ensure((size_t)n * 3));
     CTX_CHECK(c, hipMemcpyAsync(c->fgr.xyz[0].p, xyz, (size_t)n * 24, hipMemcpyHostToDevice, c->stream));
-    int rc = fpfh_device(c, 0, n, normal_radius, normal_knn, fpfh_radius, fpfh_knn);
+    int rc = fpfh_device(c, xyz, 0, n, normal_radius, normal_knn, fpfh_radius, fpfh_knn);
     if (rc) return rc;
     if (normals_out)
         CTX_CHECK(c, hipMemcpyAsync(normals_out, c->fgr.nrm.p, (size_t)n * 24, hipMemcpyDeviceToHost, c->stream));
@@ -666,7 +693,7 @@ int orpcd_fpfh_from_normals(orpcd_ctx* c, const double* xyz, const double* norma
     CTX_CHECK(c, c->fgr.xyz[0].ensure((size_t)n * 3));
     CTX_CHECK(c, hipMemcpyAsync(c->fgr.xyz[0].p, xyz, (size_t)n * 24, hipMemcpyHostToDevice, c->stream));
     CTX_CHECK(c, hipMemcpyAsync(c->fgr.nrm.p, normals, (size_t)n * 24, hipMemcpyHostToDevice, c->stream));
-    rc = features_device(c, 0, n, fpfh_radius, fpfh_knn);
+    rc = features_device(c, xyz, 0, n, fpfh_radius, fpfh_knn, 0.0);
     if (rc) return rc;
     CTX_CHECK(c, hipMemcpy2DAsync(feat_out, 33 * sizeof(double), c->fgr.feat[0].p, kFeatDim * sizeof(double),
                                   33 * sizeof(double), (size_t)n, hipMemcpyDeviceToHost, c->stream));
@@ -749,14 +776,14 @@ int orpcd_fgr_optimize(orpcd_ctx* c, const double* src, int64_t n, const double*
         CTX_CHECK(c, c->fgr.xyz[k].ensure((size_t)np[k] * 3));
         CTX_CHECK(c, hipMemcpyAsync(c->fgr.xyz[k].p, xyz[k], (size_t)np[k] * 24, hipMemcpyHostToDevice, c->stream));
     }
-    rc = fpfh_device(c, 0, n, normal_radius, normal_knn, fpfh_radius, fpfh_knn);
+    rc = fpfh_device(c, src, 0, n, normal_radius, normal_knn, fpfh_radius, fpfh_knn);
     if (rc) return rc;
     CTX_CHECK(c, c->fgr.feat[1].ensure((size_t)m * kFeatDim));
     if (target_features_from_source) {
         CTX_CHECK(c, hipMemcpyAsync(c->fgr.feat[1].p, c->fgr.feat[0].p, (size_t)m * kFeatDim * 8,
                                     hipMemcpyDeviceToDevice, c->stream));
     } else {
-        rc = fpfh_device(c, 1, m, normal_radius, normal_knn, fpfh_radius, fpfh_knn);
+        rc = fpfh_device(c, tgt, 1, m, normal_radius, normal_knn, fpfh_radius, fpfh_knn);
         if (rc) return rc;
     }
     return fgr_device(c, src, n, tgt, m, *p, T_out, fitness_out, rmse_out, ncorr_out, n_mutual_out);

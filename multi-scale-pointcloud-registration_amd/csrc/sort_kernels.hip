@@ -93,15 +93,6 @@ __global__ void super_aabb_kernel(const float4* __restrict__ tlo, const float4* 
     shi[u] = hi;
 }
 
-// Scatter per-point rows from Morton order back to input order.
-__global__ void unpermute_kernel(const double* __restrict__ in, const int32_t* __restrict__ perm, int n, int w,
-                                 double* __restrict__ out) {
-    const int k = blockIdx.x * blockDim.x + threadIdx.x;
-    if (k >= n) return;
-    const int j = perm[k];
-    for (int c = 0; c < w; ++c) out[(size_t)j * w + c] = in[(size_t)k * w + c];
-}
-
 hipError_t build_layout(const double* dev_in64, int64_t n, const double bbox_lo[3], double bbox_ext,
                         CloudLayout& L, bool with_tiles, hipStream_t s) {
     L.n = n;
@@ -145,12 +136,6 @@ hipError_t build_layout(const double* dev_in64, int64_t n, const double bbox_lo[
         if ((e = hipGetLastError()) != hipSuccess) return e;
     }
     return hipSuccess;
-}
-
-hipError_t launch_unpermute(const double* in, const int32_t* perm, int64_t n, int w, double* out, hipStream_t s) {
-    if (n <= 0) return hipSuccess;
-    unpermute_kernel<<<(unsigned)((n + 255) / 256), 256, 0, s>>>(in, perm, (int)n, w, out);
-    return hipGetLastError();
 }
 
 }  // namespace orpcd
