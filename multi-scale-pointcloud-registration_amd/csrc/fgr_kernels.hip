@@ -16,6 +16,8 @@
 // The tuple test (100 x ncorr draws of Open3D's global mt19937, stopping at
 // maximum_tuple_count) is RNG-sequential by construction and runs on the host
 // in runtime.hip.
+#include <hipcub/hipcub.hpp>
+
 #include "device_math.h"
 #include "orpcd_internal.h"
 
@@ -156,16 +158,39 @@ __global__ void feat_norm_kernel(const double* __restrict__ F, int n, double* __
 // ------------------------------------------------ feature nearest neighbour
 // For every query row q of Fq: the target row t of Ft minimising
 // |q|^2 + |t|^2 - 2 q.t (ties -> lowest t), over the target range of
-// blockIdx.y (nparts ranges; merged by merge_parts_kernel).  One wave owns 64
+// blockIdx.y (nparts ranges; merged by merge_parts_kernel), together with the
+// runner-up distance.  When the two are closer than the expansion's rounding
+// bound the query is re-decided exactly by feat_nn_refine_kernel (the
+// expansion cannot order near-duplicate rows).  Exact duplicate target rows
+// are removed beforehand (dedup_rows): their exact distances are equal, so
+// the lowest index wins, and without them a tie is rare enough to re-decide.  One wave owns 64
 // queries as 4 column tiles of 16; the block stages 64 targets x 36 in LDS.
 // D[i][j] = sum_k A[i][k] B[k][j] with A = 16 targets (lane l supplies
 // A[l&15][l>>4]) and B = 16 queries (lane l supplies B[l>>4][l&15]); the f64
 // accumulator holds D[(l>>4) + 4r][l&15], r = 0..3.
 constexpr int kFT = 64;
+
+// (d, i, s) <- merge with (od, oi, os): best distance, its lowest index, and
+// the runner-up distance (a tie at the best counts as a runner-up).
+__device__ __forceinline__ void merge_best(double& d, int& i, double& s, double od, int oi, double os) {
+    if (oi < 0) return;
+    if (i < 0 || od < d) {
+        s = fmin(os, i < 0 ? __builtin_huge_val() : d);
+        d = od;
+        i = oi;
+    } else if (od > d) {
+        s = fmin(s, od);
+    } else {
+        s = od;
+        i = min(i, oi);
+    }
+}
+
 __global__ __launch_bounds__(256) void feat_nn_kernel(const double* __restrict__ Fq, const double* __restrict__ nq2,
                                                       int nq, const double* __restrict__ Ft,
                                                       const double* __restrict__ nt2, int nt, int part_len,
-                                                      double* __restrict__ out_d, int32_t* __restrict__ out_i) {
+                                                      double* __restrict__ out_d, double* __restrict__ out_s,
+                                                      int32_t* __restrict__ out_i) {
     __shared__ double sT[kFT][kFD + 1];
     __shared__ double sN[kFT];
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
@@ -179,7 +204,8 @@ __global__ __launch_bounds__(256) void feat_nn_kernel(const double* __restrict__
 #pragma unroll
         for (int kb = 0; kb < 9; ++kb) b[qt][kb] = q < nq ? Fq[(size_t)q * kFD + 4 * kb + (lane >> 4)] : 0.0;
     }
-    double bd[4] = {__builtin_huge_val(), __builtin_huge_val(), __builtin_huge_val(), __builtin_huge_val()};
+    const double inf = __builtin_huge_val();
+    double bd[4] = {inf, inf, inf, inf}, b2[4] = {inf, inf, inf, inf};
     int bi[4] = {-1, -1, -1, -1};
     for (int t0 = t_begin; t0 < t_end; t0 += kFT) {
         __syncthreads();
@@ -208,8 +234,11 @@ __global__ __launch_bounds__(256) void feat_nn_kernel(const double* __restrict__
                 for (int qt = 0; qt < 4; ++qt) {
                     const double d = tn + qn[qt] - 2.0 * acc[qt][r];
                     if (d < bd[qt]) {
+                        b2[qt] = bd[qt];
                         bd[qt] = d;
                         bi[qt] = t0 + row;
+                    } else if (d < b2[qt]) {
+                        b2[qt] = d;
                     }
                 }
             }
@@ -220,36 +249,117 @@ __global__ __launch_bounds__(256) void feat_nn_kernel(const double* __restrict__
     for (int qt = 0; qt < 4; ++qt) {
 #pragma unroll
         for (int off = 16; off < 64; off <<= 1) {
-            const double od = __shfl_xor(bd[qt], off, 64);
+            const double od = __shfl_xor(bd[qt], off, 64), os = __shfl_xor(b2[qt], off, 64);
             const int oi = __shfl_xor(bi[qt], off, 64);
-            if (oi >= 0 && (bi[qt] < 0 || od < bd[qt] || (od == bd[qt] && oi < bi[qt]))) {
-                bd[qt] = od;
-                bi[qt] = oi;
-            }
+            merge_best(bd[qt], bi[qt], b2[qt], od, oi, os);
         }
         const int q = q0 + 16 * qt + lane;
         if (lane < 16 && q < nq) {
             out_d[(size_t)blockIdx.y * nq + q] = bd[qt];
+            out_s[(size_t)blockIdx.y * nq + q] = b2[qt];
             out_i[(size_t)blockIdx.y * nq + q] = bi[qt];
         }
     }
 }
 
-__global__ void merge_parts_kernel(const double* __restrict__ pd, const int32_t* __restrict__ pi, int nq, int nparts,
-                                   int32_t* __restrict__ out) {
+// Merge the target parts; flag queries whose best and runner-up are within
+// the rounding bound of |q|^2 + |t|^2 - 2 q.t (~40 ulp of the norms; 2e-13
+// relative leaves a wide margin).
+__global__ void merge_parts_kernel(const double* __restrict__ pd, const double* __restrict__ ps,
+                                   const int32_t* __restrict__ pi, int nq, int nparts, const double* __restrict__ nq2,
+                                   const double* __restrict__ nt2, const int32_t* __restrict__ tmap,
+                                   int32_t* __restrict__ out, int32_t* __restrict__ flag) {
     const int q = blockIdx.x * blockDim.x + threadIdx.x;
     if (q >= nq) return;
-    double bd = pd[q];
+    double bd = pd[q], bs = ps[q];
     int bi = pi[q];
-    for (int p = 1; p < nparts; ++p) {  // parts cover increasing target ranges: strict < keeps the lowest index
-        const double d = pd[(size_t)p * nq + q];
-        const int i = pi[(size_t)p * nq + q];
-        if (i >= 0 && (bi < 0 || d < bd)) {
-            bd = d;
-            bi = i;
+    for (int p = 1; p < nparts; ++p)  // parts cover increasing target ranges
+        merge_best(bd, bi, bs, pd[(size_t)p * nq + q], pi[(size_t)p * nq + q], ps[(size_t)p * nq + q]);
+    out[q] = bi >= 0 && tmap ? tmap[bi] : bi;
+    const double tol = 2e-13 * (nq2[q] + (bi >= 0 ? nt2[bi] : 0.0) + fabs(bd));
+    flag[q] = (bi >= 0 && bs - bd <= tol) ? 1 : 0;
+}
+
+// Exact re-decision for flagged queries: one wave scans every target with the
+// oracle's distance (sum of squared differences in column order, unfused) and
+// takes the lexicographic (d, index) minimum.
+__global__ __launch_bounds__(256) void feat_nn_refine_kernel(const double* __restrict__ Fq, int nq,
+                                                             const double* __restrict__ Ft, int nt, int dim,
+                                                             const int32_t* __restrict__ flag,
+                                                             const int32_t* __restrict__ tmap,
+                                                             int32_t* __restrict__ out) {
+#pragma clang fp contract(off)
+    const int q = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+    if (q >= nq || !flag[q]) return;  // wave-uniform
+    double bd = __builtin_huge_val();
+    int bi = -1;
+    const double* qr = Fq + (size_t)q * kFD;
+    for (int t = lane; t < nt; t += 64) {
+        const double* tr = Ft + (size_t)t * kFD;
+        double s = 0.0;
+        for (int k = 0; k < dim; ++k) {
+            const double d = qr[k] - tr[k];
+            s += d * d;
+        }
+        if (s < bd) {
+            bd = s;
+            bi = t;
         }
     }
-    out[q] = bi;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const double od = __shfl_xor(bd, off, 64);
+        const int oi = __shfl_xor(bi, off, 64);
+        if (oi >= 0 && (bi < 0 || od < bd || (od == bd && oi < bi))) {
+            bd = od;
+            bi = oi;
+        }
+    }
+    if (lane == 0) out[q] = bi >= 0 && tmap ? tmap[bi] : bi;
+}
+
+// ------------------------------------------------ duplicate target rows
+// hash -> stable sort -> run heads -> representative = lowest index of an
+// equal row; compact list of representatives in increasing index order.
+__global__ void row_hash_kernel(const double* __restrict__ F, int n, unsigned long long* __restrict__ key,
+                                int32_t* __restrict__ val) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    unsigned long long h = 0x9E3779B97F4A7C15ull;
+    for (int k = 0; k < kFD; ++k) {
+        h ^= (unsigned long long)__double_as_longlong(F[(size_t)i * kFD + k]);
+        h *= 0xBF58476D1CE4E5B9ull;
+        h ^= h >> 31;
+    }
+    key[i] = h;
+    val[i] = i;
+}
+
+__global__ void run_start_kernel(const unsigned long long* __restrict__ ks, int n, int32_t* __restrict__ hv) {
+    const int p = blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= n) return;
+    hv[p] = (p == 0 || ks[p] != ks[p - 1]) ? p : 0;
+}
+
+__global__ void representative_kernel(const double* __restrict__ F, const int32_t* __restrict__ vs,
+                                      const int32_t* __restrict__ head, int n, unsigned char* __restrict__ uflag) {
+    const int p = blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= n) return;
+    const int i = vs[p], h = vs[head[p]];
+    bool same = i != h;
+    for (int k = 0; k < kFD && same; ++k) same = F[(size_t)i * kFD + k] == F[(size_t)h * kFD + k];
+    uflag[i] = same ? 0 : 1;
+}
+
+__global__ void gather_rows_kernel(const double* __restrict__ F, const double* __restrict__ n2,
+                                   const int32_t* __restrict__ idx, int nu, double* __restrict__ Fu,
+                                   double* __restrict__ n2u) {
+    const int e = blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= nu * kFD) return;
+    const int u = e / kFD, k = e - u * kFD;
+    const int i = idx[u];
+    Fu[e] = F[(size_t)i * kFD + k];
+    if (k == 0) n2u[u] = n2[i];
 }
 
 // ------------------------------------------------------ IRLS (one block)
@@ -432,15 +542,60 @@ int feat_nn_parts(int64_t nq) {  // split targets so that ~8k waves run
 }
 
 hipError_t launch_feat_nn(const double* Fq, const double* nq2, int64_t nq, const double* Ft, const double* nt2,
-                          int64_t nt, double* part_d, int32_t* part_i, int32_t* out, hipStream_t s) {
+                          int64_t nt, const int32_t* tmap, int dim, double* part_d, int32_t* part_i, int32_t* flag,
+                          int32_t* out, hipStream_t s) {
     if (nq <= 0) return hipSuccess;
     const int parts = feat_nn_parts(nq);
     const int part_len = (int)(((nt + parts - 1) / parts + kFT - 1) / kFT * kFT);
     const dim3 grid((unsigned)((nq + 255) / 256), (unsigned)parts);
-    feat_nn_kernel<<<grid, 256, 0, s>>>(Fq, nq2, (int)nq, Ft, nt2, (int)nt, part_len, part_d, part_i);
+    double* part_s = part_d + (size_t)parts * nq;
+    feat_nn_kernel<<<grid, 256, 0, s>>>(Fq, nq2, (int)nq, Ft, nt2, (int)nt, part_len, part_d, part_s, part_i);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
-    merge_parts_kernel<<<(unsigned)((nq + 255) / 256), 256, 0, s>>>(part_d, part_i, (int)nq, parts, out);
+    merge_parts_kernel<<<(unsigned)((nq + 255) / 256), 256, 0, s>>>(part_d, part_s, part_i, (int)nq, parts, nq2,
+                                                                    nt2, tmap, out, flag);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    feat_nn_refine_kernel<<<(unsigned)((nq + 3) / 4), 256, 0, s>>>(Fq, (int)nq, Ft, (int)nt, dim, flag, tmap, out);
+    return hipGetLastError();
+}
+
+hipError_t dedup_rows(const double* F, const double* n2, int64_t n, DedupBufs& b, int64_t* nu_out, hipStream_t s) {
+    hipError_t e;
+    if ((e = b.key.ensure((size_t)n * 2)) != hipSuccess) return e;
+    if ((e = b.val.ensure((size_t)n * 2)) != hipSuccess) return e;
+    if ((e = b.head.ensure((size_t)n + 1)) != hipSuccess) return e;
+    if ((e = b.uflag.ensure((size_t)n)) != hipSuccess) return e;
+    if ((e = b.uidx.ensure((size_t)n)) != hipSuccess) return e;
+    if ((e = b.Fu.ensure((size_t)n * kFD)) != hipSuccess) return e;
+    if ((e = b.n2u.ensure((size_t)n)) != hipSuccess) return e;
+    const unsigned g = (unsigned)((n + 255) / 256);
+    unsigned long long *k0 = b.key.p, *k1 = b.key.p + n;
+    int32_t *v0 = b.val.p, *v1 = b.val.p + n, *nsel = b.head.p + n;
+    row_hash_kernel<<<g, 256, 0, s>>>(F, (int)n, k0, v0);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    size_t t1 = 0, t2 = 0, t3 = 0;
+    if ((e = hipcub::DeviceRadixSort::SortPairs(nullptr, t1, k0, k1, v0, v1, (int)n, 0, 64, s)) != hipSuccess) return e;
+    if ((e = hipcub::DeviceScan::InclusiveScan(nullptr, t2, v0, v0, hipcub::Max(), (int)n, s)) != hipSuccess) return e;
+    if ((e = hipcub::DeviceSelect::Flagged(nullptr, t3, hipcub::CountingInputIterator<int32_t>(0), b.uflag.p,
+                                           b.uidx.p, nsel, (int)n, s)) != hipSuccess)
+        return e;
+    if ((e = b.tmp.ensure(std::max(t1, std::max(t2, t3)))) != hipSuccess) return e;
+    if ((e = hipcub::DeviceRadixSort::SortPairs(b.tmp.p, t1, k0, k1, v0, v1, (int)n, 0, 64, s)) != hipSuccess) return e;
+    run_start_kernel<<<g, 256, 0, s>>>(k1, (int)n, v0);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    if ((e = hipcub::DeviceScan::InclusiveScan(b.tmp.p, t2, v0, b.head.p, hipcub::Max(), (int)n, s)) != hipSuccess)
+        return e;
+    representative_kernel<<<g, 256, 0, s>>>(F, v1, b.head.p, (int)n, b.uflag.p);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    if ((e = hipcub::DeviceSelect::Flagged(b.tmp.p, t3, hipcub::CountingInputIterator<int32_t>(0), b.uflag.p,
+                                           b.uidx.p, nsel, (int)n, s)) != hipSuccess)
+        return e;
+    int32_t nu = 0;
+    if ((e = hipMemcpyAsync(&nu, nsel, 4, hipMemcpyDeviceToHost, s)) != hipSuccess) return e;
+    if ((e = hipStreamSynchronize(s)) != hipSuccess) return e;
+    gather_rows_kernel<<<(unsigned)(((int64_t)nu * kFD + 255) / 256), 256, 0, s>>>(F, n2, b.uidx.p, nu, b.Fu.p,
+                                                                                   b.n2u.p);
+    *nu_out = nu;
     return hipGetLastError();
 }
 

@@ -100,6 +100,25 @@ def test_feature_nn_matches_brute_force(ctx):
     assert len(ctx.feature_nn(np.zeros((0, 33)), t)) == 0
 
 
+def test_feature_nn_near_duplicates_resolved_exactly(ctx):
+    """Rows equal up to the last bits: |q|^2+|t|^2-2q.t cannot order them, the
+    exact re-decision must (oracle distance: sum of squared differences)."""
+    rng = np.random.default_rng(9)
+    t = rng.random((4000, 33)) * 120
+    q = t[[3000, 3500]].copy()
+    t[10] = q[0]
+    t[10, 7] = np.nextafter(t[10, 7], np.inf)     # near-duplicate at a LOWER index
+    t[20] = q[1]
+    t[20, 3] += 1e-12
+    got = ctx.feature_nn(q, t)
+    assert got[0] == 3000 and got[1] == 3500       # the exact copies (d = 0) win
+    q3 = t[100:101].copy()
+    q3[0, 5] = 64.0
+    t[200], t[150] = q3[0], q3[0]
+    t[200, 5], t[150, 5] = 64.0 + 2.0 ** -40, 64.0 - 2.0 ** -40   # exactly equal distances
+    assert ctx.feature_nn(q3, t)[0] == 150                          # -> lowest index
+
+
 def test_feature_nn_large_splits(ctx):
     rng = np.random.default_rng(3)
     q = rng.random((600, 33)) * 50

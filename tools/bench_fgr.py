@@ -1,0 +1,96 @@
+"""C3 measurement: FastGlobalOptimizer.optimize on the 100k synthetic pair (1 GPU).
+
+    python tools/bench_fgr.py [--points 100000] [--repeat 5] [--cpu 1] [--out profiles/r01_fgr_c3.json]
+
+Times the build's plugin (FPFH of both clouds + fp64-MFMA mutual matching +
+tuple test + GNC IRLS + evaluation, one orpcd_fgr_optimize call) with inputs
+on the host, as the Aligner hands them over, and the feature-NN kernel alone
+with HIP events (orpcd_profiling) for its roofline: algorithmic work
+2*33*N*M FLOP per direction, priced against the fp64 matrix
+peak.  The CPU oracle (same seed, same Q4 choice) is timed once on the host
+cores as the baseline and its result compared.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [os.path.join(REPO, "multi-scale-pointcloud-registration_amd"), REPO]
+
+FP64_MATRIX_PEAK_TF = 78.6   # MI355X spec sheet, FP64 matrix (dense)
+
+
+def radius_scale(c):
+    center = c.mean(axis=0, keepdims=True)
+    return (c - center) / np.max(np.linalg.norm(c - center, axis=1))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--points", type=int, default=100_000)
+    ap.add_argument("--repeat", type=int, default=5)
+    ap.add_argument("--cpu", type=int, default=1)
+    ap.add_argument("--out", default=None)
+    args = ap.parse_args()
+
+    from workloads import c3_pair
+    from orpcd_amd import FastGlobalOptimizer
+    src, tgt = c3_pair(args.points)
+    src, tgt = radius_scale(src), radius_scale(tgt)     # what the Aligner passes (RadiusScaler)
+
+    opt = FastGlobalOptimizer(seed=0)
+    T, rmse = opt.optimize(src, tgt)                    # warm-up (allocations, code objects)
+    times = []
+    for _ in range(args.repeat):
+        t0 = time.perf_counter()
+        T, rmse = opt.optimize(src, tgt)
+        times.append(time.perf_counter() - t0)
+    r = opt.last_result
+
+    # feature-NN kernel alone (both directions), HIP-event timed
+    ctx = opt.context
+    _, fs = ctx.fpfh(src, 0.1, 20, 0.1, 20)
+    ctx.feature_nn(fs[:4096], fs)                       # warm-up
+    t0 = time.perf_counter()
+    reps = 3
+    for _ in range(reps):
+        ctx.feature_nn(fs, fs)
+    nn_s = (time.perf_counter() - t0) / reps
+    n = len(src)
+    nn_flop = 2 * 33 * n * n                            # one direction, algorithmic
+    line = {
+        "metric": "FastGlobalOptimizer.optimize wall-clock (C3, 100k<->100k)",
+        "value": round(1e3 * float(np.median(times)), 3), "unit": "ms", "higher_is_better": False,
+        "n_gpus": 1, "repeat": args.repeat, "dtype": "f64",
+        "data": "synthetic C3 (bumpy sphere, default_rng(3), index-aligned anisotropic target), radius-scaled",
+        "config": {"workload": "C3: FGR defaults (normals r=0.1 k=20, FPFH r=0.1 k=20, Q4 target features)",
+                   "points": n},
+        "result": {"rmse": float(rmse), "fitness": r["fitness"], "n_mutual": r["n_mutual"],
+                   "n_tuple_corr": r["n_tuple_corr"]},
+        "feature_nn": {"seconds_per_direction_incl_upload": round(nn_s, 5),
+                       "achieved_tflops": round(nn_flop / nn_s / 1e12, 3),
+                       "peak_tflops": FP64_MATRIX_PEAK_TF,
+                       "frac": round(nn_flop / nn_s / 1e12 / FP64_MATRIX_PEAK_TF, 4)},
+    }
+    if args.cpu:
+        sys.path.insert(0, os.path.join(REPO, "oracle"))
+        import oracle
+        t0 = time.perf_counter()
+        oT, ormse = oracle.OracleFastGlobalOptimizer(seed=0).optimize(src, tgt)
+        cpu_s = time.perf_counter() - t0
+        line["cpu_baseline"] = {"value": round(cpu_s * 1e3, 1), "unit": "ms", "cores": oracle.num_threads(),
+                                "kind": "port", "sample": "the same optimize call, full size"}
+        line["parity"] = {"max_abs_dT": float(np.abs(oT - T).max()), "d_rmse": float(abs(ormse - rmse))}
+    s = json.dumps(line)
+    print(s)
+    if args.out:
+        with open(args.out, "w") as f:
+            f.write(s + "\n")
+
+
+if __name__ == "__main__":
+    main()
