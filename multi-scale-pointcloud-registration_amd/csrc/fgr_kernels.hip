@@ -156,19 +156,30 @@ __global__ void feat_norm_kernel(const double* __restrict__ F, int n, double* __
 }
 
 // ------------------------------------------------ feature nearest neighbour
-// For every query row q of Fq: the target row t of Ft minimising
-// |q|^2 + |t|^2 - 2 q.t (ties -> lowest t), over the target range of
-// blockIdx.y (nparts ranges; merged by merge_parts_kernel), together with the
-// runner-up distance.  When the two are closer than the expansion's rounding
-// bound the query is re-decided exactly by feat_nn_refine_kernel (the
-// expansion cannot order near-duplicate rows).  Exact duplicate target rows
-// are removed beforehand (dedup_rows): their exact distances are equal, so
-// the lowest index wins, and without them a tie is rare enough to re-decide.  One wave owns 64
-// queries as 4 column tiles of 16; the block stages 64 targets x 36 in LDS.
-// D[i][j] = sum_k A[i][k] B[k][j] with A = 16 targets (lane l supplies
-// A[l&15][l>>4]) and B = 16 queries (lane l supplies B[l>>4][l&15]); the f64
-// accumulator holds D[(l>>4) + 4r][l&15], r = 0..3.
+// Two passes over the targets on the fp64 matrix cores.
+//
+// Pass 1 (EXACT = false), every query: the target minimising the expansion
+// |q|^2 + |t|^2 - 2 q.t (ties -> lowest index) and the runner-up distance.
+// The expansion carries a rounding error of ~40 ulp of the norms, so it
+// cannot order rows that are equal up to their last bits — FPFH produces many
+// of those (neighbourhoods whose pair features all fall in the same bins).
+// Queries whose best and runner-up lie within that bound are flagged.
+//
+// Pass 2 (EXACT = true), flagged queries only (compacted): the same products,
+// and every target within the bound of the pass-1 best is re-measured with
+// the oracle's distance (sum of squared differences in column order,
+// unfused); the lexicographic (d, index) minimum of those wins.  Exact
+// duplicate target rows are collapsed to their lowest index beforehand
+// (dedup_rows): their exact distances are equal, so that is the answer the
+// oracle gives, and the near-tie sets stay small.
+//
+// Tiling: one wave owns 64 queries as 4 column tiles of 16; the block stages
+// 64 targets x 36 in LDS.  D[i][j] = sum_k A[i][k] B[k][j] with A = 16 targets
+// (lane l supplies A[l&15][l>>4]) and B = 16 queries (lane l supplies
+// B[l>>4][l&15]); the f64 accumulator holds D[(l>>4) + 4r][l&15], r = 0..3.
+// blockIdx.y splits the targets into parts (merged by the merge kernels).
 constexpr int kFT = 64;
+constexpr int kExactParts = 16;
 
 // (d, i, s) <- merge with (od, oi, os): best distance, its lowest index, and
 // the runner-up distance (a tie at the best counts as a runner-up).
@@ -186,23 +197,41 @@ __device__ __forceinline__ void merge_best(double& d, int& i, double& s, double 
     }
 }
 
+__device__ __forceinline__ void merge_lex(double& d, int& i, double od, int oi) {
+    if (oi >= 0 && (i < 0 || od < d || (od == d && oi < i))) {
+        d = od;
+        i = oi;
+    }
+}
+
+// EXACT: qidx / nsel / thr give the compacted flagged queries and their
+// pass-1 thresholds; out_s is unused.
+template <bool EXACT>
 __global__ __launch_bounds__(256) void feat_nn_kernel(const double* __restrict__ Fq, const double* __restrict__ nq2,
-                                                      int nq, const double* __restrict__ Ft,
-                                                      const double* __restrict__ nt2, int nt, int part_len,
+                                                      int nq, const int32_t* __restrict__ qidx,
+                                                      const int32_t* __restrict__ nsel,
+                                                      const double* __restrict__ thr, const double* __restrict__ Ft,
+                                                      const double* __restrict__ nt2, int nt, int part_len, int dim,
                                                       double* __restrict__ out_d, double* __restrict__ out_s,
                                                       int32_t* __restrict__ out_i) {
     __shared__ double sT[kFT][kFD + 1];
     __shared__ double sN[kFT];
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const int nrow = EXACT ? *nsel : nq;  // queries (rows of the compact list in EXACT mode)
+    if ((int)blockIdx.x * 256 >= nrow) return;  // block-uniform
     const int q0 = (blockIdx.x * 4 + wid) * 64;
     const int t_begin = blockIdx.y * part_len, t_end = min(nt, t_begin + part_len);
-    double b[4][9], qn[4];
+    double b[4][9], qn[4], th[4];
+    const double* qrow[4];
 #pragma unroll
     for (int qt = 0; qt < 4; ++qt) {
-        const int q = q0 + 16 * qt + (lane & 15);
-        qn[qt] = q < nq ? nq2[q] : 0.0;
+        const int j = q0 + 16 * qt + (lane & 15);
+        const int q = j < nrow ? (EXACT ? qidx[j] : j) : -1;
+        qn[qt] = q >= 0 ? nq2[q] : 0.0;
+        th[qt] = (EXACT && q >= 0) ? thr[q] : -1.0;
+        qrow[qt] = Fq + (size_t)(q >= 0 ? q : 0) * kFD;
 #pragma unroll
-        for (int kb = 0; kb < 9; ++kb) b[qt][kb] = q < nq ? Fq[(size_t)q * kFD + 4 * kb + (lane >> 4)] : 0.0;
+        for (int kb = 0; kb < 9; ++kb) b[qt][kb] = q >= 0 ? qrow[qt][4 * kb + (lane >> 4)] : 0.0;
     }
     const double inf = __builtin_huge_val();
     double bd[4] = {inf, inf, inf, inf}, b2[4] = {inf, inf, inf, inf};
@@ -213,7 +242,7 @@ __global__ __launch_bounds__(256) void feat_nn_kernel(const double* __restrict__
             const int r = e / kFD, col = e - r * kFD;
             sT[r][col] = (t0 + r < t_end) ? Ft[(size_t)(t0 + r) * kFD + col] : 0.0;
         }
-        if (threadIdx.x < kFT) sN[threadIdx.x] = (t0 + threadIdx.x < t_end) ? nt2[t0 + threadIdx.x] : __builtin_huge_val();
+        if (threadIdx.x < kFT) sN[threadIdx.x] = (t0 + threadIdx.x < t_end) ? nt2[t0 + threadIdx.x] : inf;
         __syncthreads();
 #pragma unroll
         for (int sub = 0; sub < kFT / 16; ++sub) {
@@ -233,12 +262,27 @@ __global__ __launch_bounds__(256) void feat_nn_kernel(const double* __restrict__
 #pragma unroll
                 for (int qt = 0; qt < 4; ++qt) {
                     const double d = tn + qn[qt] - 2.0 * acc[qt][r];
-                    if (d < bd[qt]) {
-                        b2[qt] = bd[qt];
-                        bd[qt] = d;
-                        bi[qt] = t0 + row;
-                    } else if (d < b2[qt]) {
-                        b2[qt] = d;
+                    if (!EXACT) {
+                        if (d < bd[qt]) {
+                            b2[qt] = bd[qt];
+                            bd[qt] = d;
+                            bi[qt] = t0 + row;
+                        } else if (d < b2[qt]) {
+                            b2[qt] = d;
+                        }
+                    } else if (d <= th[qt]) {
+                        double ex = 0.0;
+                        {
+#pragma clang fp contract(off)
+                            for (int k = 0; k < dim; ++k) {
+                                const double df = qrow[qt][k] - sT[row][k];
+                                ex += df * df;
+                            }
+                        }
+                        if (ex < bd[qt]) {  // increasing rows per lane: strict keeps the lowest index
+                            bd[qt] = ex;
+                            bi[qt] = t0 + row;
+                        }
                     }
                 }
             }
@@ -251,24 +295,27 @@ __global__ __launch_bounds__(256) void feat_nn_kernel(const double* __restrict__
         for (int off = 16; off < 64; off <<= 1) {
             const double od = __shfl_xor(bd[qt], off, 64), os = __shfl_xor(b2[qt], off, 64);
             const int oi = __shfl_xor(bi[qt], off, 64);
-            merge_best(bd[qt], bi[qt], b2[qt], od, oi, os);
+            if (EXACT)
+                merge_lex(bd[qt], bi[qt], od, oi);
+            else
+                merge_best(bd[qt], bi[qt], b2[qt], od, oi, os);
         }
-        const int q = q0 + 16 * qt + lane;
-        if (lane < 16 && q < nq) {
-            out_d[(size_t)blockIdx.y * nq + q] = bd[qt];
-            out_s[(size_t)blockIdx.y * nq + q] = b2[qt];
-            out_i[(size_t)blockIdx.y * nq + q] = bi[qt];
+        const int j = q0 + 16 * qt + lane;
+        if (lane < 16 && j < nrow) {
+            out_d[(size_t)blockIdx.y * nq + j] = bd[qt];
+            if (!EXACT) out_s[(size_t)blockIdx.y * nq + j] = b2[qt];
+            out_i[(size_t)blockIdx.y * nq + j] = bi[qt];
         }
     }
 }
 
-// Merge the target parts; flag queries whose best and runner-up are within
-// the rounding bound of |q|^2 + |t|^2 - 2 q.t (~40 ulp of the norms; 2e-13
-// relative leaves a wide margin).
+// Pass-1 merge over the target parts: answer, flag and pass-2 threshold.
+// The expansion's error is ~40 ulp of the norms; 2e-13 relative leaves a
+// wide margin (twice: the best's and the competitor's error).
 __global__ void merge_parts_kernel(const double* __restrict__ pd, const double* __restrict__ ps,
                                    const int32_t* __restrict__ pi, int nq, int nparts, const double* __restrict__ nq2,
                                    const double* __restrict__ nt2, const int32_t* __restrict__ tmap,
-                                   int32_t* __restrict__ out, int32_t* __restrict__ flag) {
+                                   int32_t* __restrict__ out, int32_t* __restrict__ flag, double* __restrict__ thr) {
     const int q = blockIdx.x * blockDim.x + threadIdx.x;
     if (q >= nq) return;
     double bd = pd[q], bs = ps[q];
@@ -278,44 +325,19 @@ __global__ void merge_parts_kernel(const double* __restrict__ pd, const double* 
     out[q] = bi >= 0 && tmap ? tmap[bi] : bi;
     const double tol = 2e-13 * (nq2[q] + (bi >= 0 ? nt2[bi] : 0.0) + fabs(bd));
     flag[q] = (bi >= 0 && bs - bd <= tol) ? 1 : 0;
+    thr[q] = bd + 2.0 * tol;
 }
 
-// Exact re-decision for flagged queries: one wave scans every target with the
-// oracle's distance (sum of squared differences in column order, unfused) and
-// takes the lexicographic (d, index) minimum.
-__global__ __launch_bounds__(256) void feat_nn_refine_kernel(const double* __restrict__ Fq, int nq,
-                                                             const double* __restrict__ Ft, int nt, int dim,
-                                                             const int32_t* __restrict__ flag,
-                                                             const int32_t* __restrict__ tmap,
-                                                             int32_t* __restrict__ out) {
-#pragma clang fp contract(off)
-    const int q = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
-    if (q >= nq || !flag[q]) return;  // wave-uniform
-    double bd = __builtin_huge_val();
-    int bi = -1;
-    const double* qr = Fq + (size_t)q * kFD;
-    for (int t = lane; t < nt; t += 64) {
-        const double* tr = Ft + (size_t)t * kFD;
-        double s = 0.0;
-        for (int k = 0; k < dim; ++k) {
-            const double d = qr[k] - tr[k];
-            s += d * d;
-        }
-        if (s < bd) {
-            bd = s;
-            bi = t;
-        }
-    }
-#pragma unroll
-    for (int off = 1; off < 64; off <<= 1) {
-        const double od = __shfl_xor(bd, off, 64);
-        const int oi = __shfl_xor(bi, off, 64);
-        if (oi >= 0 && (bi < 0 || od < bd || (od == bd && oi < bi))) {
-            bd = od;
-            bi = oi;
-        }
-    }
-    if (lane == 0) out[q] = bi >= 0 && tmap ? tmap[bi] : bi;
+// Pass-2 merge (lexicographic on the exact distance) into the answers.
+__global__ void merge_exact_kernel(const double* __restrict__ pd, const int32_t* __restrict__ pi, int nq,
+                                   int nparts, const int32_t* __restrict__ qidx, const int32_t* __restrict__ nsel,
+                                   const int32_t* __restrict__ tmap, int32_t* __restrict__ out) {
+    const int j = blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= *nsel) return;
+    double bd = pd[j];
+    int bi = pi[j];
+    for (int p = 1; p < nparts; ++p) merge_lex(bd, bi, pd[(size_t)p * nq + j], pi[(size_t)p * nq + j]);
+    if (bi >= 0) out[qidx[j]] = tmap ? tmap[bi] : bi;
 }
 
 // ------------------------------------------------ duplicate target rows
@@ -542,20 +564,40 @@ int feat_nn_parts(int64_t nq) {  // split targets so that ~8k waves run
 }
 
 hipError_t launch_feat_nn(const double* Fq, const double* nq2, int64_t nq, const double* Ft, const double* nt2,
-                          int64_t nt, const int32_t* tmap, int dim, double* part_d, int32_t* part_i, int32_t* flag,
-                          int32_t* out, hipStream_t s) {
+                          int64_t nt, const int32_t* tmap, int dim, FeatNNBufs& b, int32_t* out, hipStream_t s) {
     if (nq <= 0) return hipSuccess;
+    hipError_t e;
     const int parts = feat_nn_parts(nq);
-    const int part_len = (int)(((nt + parts - 1) / parts + kFT - 1) / kFT * kFT);
-    const dim3 grid((unsigned)((nq + 255) / 256), (unsigned)parts);
-    double* part_s = part_d + (size_t)parts * nq;
-    feat_nn_kernel<<<grid, 256, 0, s>>>(Fq, nq2, (int)nq, Ft, nt2, (int)nt, part_len, part_d, part_s, part_i);
-    hipError_t e = hipGetLastError();
-    if (e != hipSuccess) return e;
-    merge_parts_kernel<<<(unsigned)((nq + 255) / 256), 256, 0, s>>>(part_d, part_s, part_i, (int)nq, parts, nq2,
-                                                                    nt2, tmap, out, flag);
+    if ((e = b.part_d.ensure((size_t)2 * std::max(parts, kExactParts) * nq)) != hipSuccess) return e;
+    if ((e = b.part_i.ensure((size_t)std::max(parts, kExactParts) * nq)) != hipSuccess) return e;
+    if ((e = b.flag.ensure((size_t)nq)) != hipSuccess) return e;
+    if ((e = b.qidx.ensure((size_t)nq + 1)) != hipSuccess) return e;
+    if ((e = b.thr.ensure((size_t)nq)) != hipSuccess) return e;
+    double* part_s = b.part_d.p + (size_t)std::max(parts, kExactParts) * nq;
+    int32_t* nsel = b.qidx.p + nq;
+    const unsigned gq = (unsigned)((nq + 255) / 256);
+    const int len1 = (int)(((nt + parts - 1) / parts + kFT - 1) / kFT * kFT);
+    feat_nn_kernel<false><<<dim3(gq, (unsigned)parts), 256, 0, s>>>(Fq, nq2, (int)nq, nullptr, nullptr, nullptr, Ft,
+                                                                   nt2, (int)nt, len1, dim, b.part_d.p, part_s,
+                                                                   b.part_i.p);
     if ((e = hipGetLastError()) != hipSuccess) return e;
-    feat_nn_refine_kernel<<<(unsigned)((nq + 3) / 4), 256, 0, s>>>(Fq, (int)nq, Ft, (int)nt, dim, flag, tmap, out);
+    merge_parts_kernel<<<gq, 256, 0, s>>>(b.part_d.p, part_s, b.part_i.p, (int)nq, parts, nq2, nt2, tmap, out,
+                                          b.flag.p, b.thr.p);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    size_t tmp = 0;
+    if ((e = hipcub::DeviceSelect::Flagged(nullptr, tmp, hipcub::CountingInputIterator<int32_t>(0), b.flag.p,
+                                           b.qidx.p, nsel, (int)nq, s)) != hipSuccess)
+        return e;
+    if ((e = b.tmp.ensure(tmp)) != hipSuccess) return e;
+    if ((e = hipcub::DeviceSelect::Flagged(b.tmp.p, tmp, hipcub::CountingInputIterator<int32_t>(0), b.flag.p,
+                                           b.qidx.p, nsel, (int)nq, s)) != hipSuccess)
+        return e;
+    const int len2 = (int)(((nt + kExactParts - 1) / kExactParts + kFT - 1) / kFT * kFT);
+    feat_nn_kernel<true><<<dim3(gq, (unsigned)kExactParts), 256, 0, s>>>(Fq, nq2, (int)nq, b.qidx.p, nsel, b.thr.p,
+                                                                        Ft, nt2, (int)nt, len2, dim, b.part_d.p,
+                                                                        nullptr, b.part_i.p);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    merge_exact_kernel<<<gq, 256, 0, s>>>(b.part_d.p, b.part_i.p, (int)nq, kExactParts, b.qidx.p, nsel, tmap, out);
     return hipGetLastError();
 }
 

@@ -107,6 +107,20 @@ struct DedupBufs {
     }
 };
 
+struct FeatNNBufs {
+    DevBuf<double> part_d, thr;
+    DevBuf<int32_t> part_i, flag, qidx;
+    DevBuf<unsigned char> tmp;
+    void release() {
+        part_d.release();
+        thr.release();
+        part_i.release();
+        flag.release();
+        qidx.release();
+        tmp.release();
+    }
+};
+
 struct KernelStats {
     double launches = 0, ms = 0, pairs = 0, iterations = 0, passes = 0, tiles = 0, accum_ms = 0;
 };
@@ -159,9 +173,10 @@ struct orpcd_ctx {
         orpcd::DevBuf<double> xyz[2];     // input-order points
         orpcd::DevBuf<double> feat[2];    // n x 36 padded features
         orpcd::DevBuf<double> fn2[2];     // |f|^2
-        orpcd::DevBuf<double> nrm, raw, nd2, spfh, part_d, red, pq, Tn;
-        orpcd::DevBuf<int32_t> nbr, cnt, part_i, flag, nn[2];
+        orpcd::DevBuf<double> nrm, raw, nd2, spfh, red, pq, Tn;
+        orpcd::DevBuf<int32_t> nbr, cnt, nn[2];
         orpcd::DedupBufs dedup;
+        orpcd::FeatNNBufs fnn;
         void release() {
             for (int k = 0; k < 2; ++k) {
                 xyz[k].release();
@@ -169,9 +184,10 @@ struct orpcd_ctx {
                 fn2[k].release();
                 nn[k].release();
             }
-            for (auto* b : {&nrm, &raw, &nd2, &spfh, &part_d, &red, &pq, &Tn}) b->release();
-            for (auto* b : {&nbr, &cnt, &part_i, &flag}) b->release();
+            for (auto* b : {&nrm, &raw, &nd2, &spfh, &red, &pq, &Tn}) b->release();
+            for (auto* b : {&nbr, &cnt}) b->release();
             dedup.release();
+            fnn.release();
         }
     } fgr;
 
@@ -218,11 +234,9 @@ hipError_t launch_fpfh(const double* pts, const double* nrm, int64_t n, const in
 hipError_t launch_pad_features(const double* in33, int64_t n, double* out36, hipStream_t s);
 hipError_t launch_feat_norm(const double* F36, int64_t n, double* nrm2, hipStream_t s);
 int feat_nn_parts(int64_t nq);
-// part_d: 2 * parts * nq doubles, part_i: parts * nq, flag: nq; tmap (or
-// null): target row -> reported index
+// tmap (or null): target row -> reported index
 hipError_t launch_feat_nn(const double* Fq, const double* nq2, int64_t nq, const double* Ft, const double* nt2,
-                          int64_t nt, const int32_t* tmap, int dim, double* part_d, int32_t* part_i, int32_t* flag,
-                          int32_t* out, hipStream_t s);
+                          int64_t nt, const int32_t* tmap, int dim, FeatNNBufs& b, int32_t* out, hipStream_t s);
 // Representatives (lowest index) of the distinct rows of F (n x 36): b.uidx
 // (increasing), b.Fu / b.n2u their rows and norms; *nu_out their count.
 hipError_t dedup_rows(const double* F, const double* n2, int64_t n, DedupBufs& b, int64_t* nu_out, hipStream_t s);

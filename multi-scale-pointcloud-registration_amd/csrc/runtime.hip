@@ -223,19 +223,15 @@ int fgr_device(orpcd_ctx* c, const double* src, int64_t n, const double* tgt, in
         CTX_CHECK(c, F.fn2[k].ensure((size_t)np[k]));
         CTX_CHECK(c, launch_feat_norm(F.feat[k].p, np[k], F.fn2[k].p, s));
     }
-    const int64_t parts_max = std::max(feat_nn_parts(nPti), feat_nn_parts(nPtj));
-    CTX_CHECK(c, F.part_d.ensure((size_t)2 * parts_max * std::max(nPti, nPtj)));
-    CTX_CHECK(c, F.part_i.ensure((size_t)parts_max * std::max(nPti, nPtj)));
-    CTX_CHECK(c, F.flag.ensure((size_t)std::max(nPti, nPtj)));
     CTX_CHECK(c, F.nn[0].ensure((size_t)nPtj));
     CTX_CHECK(c, F.nn[1].ensure((size_t)nPti));
     int64_t nu = 0;
     CTX_CHECK(c, dedup_rows(F.feat[fi].p, F.fn2[fi].p, nPti, F.dedup, &nu, s));
     CTX_CHECK(c, launch_feat_nn(F.feat[fj].p, F.fn2[fj].p, nPtj, F.dedup.Fu.p, F.dedup.n2u.p, nu, F.dedup.uidx.p, 33,
-                                F.part_d.p, F.part_i.p, F.flag.p, F.nn[0].p, s));
+                                F.fnn, F.nn[0].p, s));
     CTX_CHECK(c, dedup_rows(F.feat[fj].p, F.fn2[fj].p, nPtj, F.dedup, &nu, s));
     CTX_CHECK(c, launch_feat_nn(F.feat[fi].p, F.fn2[fi].p, nPti, F.dedup.Fu.p, F.dedup.n2u.p, nu, F.dedup.uidx.p, 33,
-                                F.part_d.p, F.part_i.p, F.flag.p, F.nn[1].p, s));
+                                F.fnn, F.nn[1].p, s));
     std::vector<int32_t> j_to_i((size_t)nPtj), i_to_j((size_t)nPti);
     CTX_CHECK(c, hipMemcpyAsync(j_to_i.data(), F.nn[0].p, (size_t)nPtj * 4, hipMemcpyDeviceToHost, s));
     CTX_CHECK(c, hipMemcpyAsync(i_to_j.data(), F.nn[1].p, (size_t)nPti * 4, hipMemcpyDeviceToHost, s));
@@ -750,15 +746,11 @@ int orpcd_feature_nn(orpcd_ctx* c, const double* q, int64_t nq, const double* t,
                                       (size_t)np[k], hipMemcpyHostToDevice, c->stream));
         CTX_CHECK(c, launch_feat_norm(F.feat[k].p, np[k], F.fn2[k].p, c->stream));
     }
-    const int parts = feat_nn_parts(nq);
-    CTX_CHECK(c, F.part_d.ensure((size_t)2 * parts * nq));
-    CTX_CHECK(c, F.part_i.ensure((size_t)parts * nq));
-    CTX_CHECK(c, F.flag.ensure((size_t)nq));
     CTX_CHECK(c, F.nn[0].ensure((size_t)nq));
     int64_t nu = 0;
     CTX_CHECK(c, dedup_rows(F.feat[1].p, F.fn2[1].p, nt, F.dedup, &nu, c->stream));
     CTX_CHECK(c, launch_feat_nn(F.feat[0].p, F.fn2[0].p, nq, F.dedup.Fu.p, F.dedup.n2u.p, nu, F.dedup.uidx.p, dim,
-                                F.part_d.p, F.part_i.p, F.flag.p, F.nn[0].p, c->stream));
+                                F.fnn, F.nn[0].p, c->stream));
     CTX_CHECK(c, hipMemcpyAsync(idx_out, F.nn[0].p, (size_t)nq * 4, hipMemcpyDeviceToHost, c->stream));
     CTX_CHECK(c, hipStreamSynchronize(c->stream));
     return ORPCD_OK;
