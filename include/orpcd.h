@@ -15,6 +15,9 @@
  *       GeneralizedICP.optimize            Optimizer/generalizedICP.py:47-83
  *       -> o3d registration_generalized_icp Optimizer/generalizedICP.py:59-70
  *       batched over the multistart loop   Aligner/Aligner.py:178-202
+ *   orpcd_set_source_rows / orpcd_gicp_shard_*
+ *       one GeneralizedICP.optimize with the source rows split over GPUs
+ *                                          Optimizer/generalizedICP.py:59-70
  *   orpcd_estimate_normals
  *       o3d EstimateNormals(KNN 20) inside registration_generalized_icp, and
  *       source_copy.estimate_normals(Hybrid) Optimizer/fastGlobalOptimizer.py:118-127
@@ -126,6 +129,25 @@ int orpcd_fgr(orpcd_ctx* ctx, const double* src, int64_t n, const double* tgt, i
               const double* src_feat, const double* tgt_feat, const orpcd_fgr_params* params,
               double* T_out, double* fitness_out, double* rmse_out, int64_t* ncorr_out,
               int64_t* n_mutual_out);
+
+/* ------------------------------------------- one start, rows over ranks (C5)
+ * A single GICP whose SOURCE rows are split over ranks; the target is
+ * replicated.  Per pass every rank computes its local normal-equation sums
+ * (29 doubles: JTJ upper 21, JTr 6, sum d^2, count), the caller all-reduces
+ * them (RCCL), and every rank applies the same update.  The reference runs
+ * this as one registration_generalized_icp call (generalizedICP.py:59-70).
+ *
+ * orpcd_set_source_rows: covariances from the FULL cloud's neighbourhoods,
+ * device rows [row_begin, row_end) only.                                    */
+int orpcd_set_source_rows(orpcd_ctx* ctx, const double* xyz, int64_t n, int64_t row_begin, int64_t row_end);
+int orpcd_gicp_shard_begin(orpcd_ctx* ctx, const double* R0, const double* t0, const orpcd_gicp_params* params,
+                           int64_t n_total);
+/* local sums of the current pass; *active = 0 once the start has finished */
+int orpcd_gicp_shard_pass(orpcd_ctx* ctx, double* sums_out, int32_t* active);
+/* global (all-reduced) sums -> convergence test, solve, next queries */
+int orpcd_gicp_shard_update(orpcd_ctx* ctx, const double* sums_in, int32_t* done_out);
+int orpcd_gicp_shard_result(orpcd_ctx* ctx, double* T_out, double* rmse_out, double* fitness_out,
+                            int32_t* iters_out, int64_t* ncorr_out);
 
 /* Nearest feature row (squared Euclidean, ties -> lowest index) of every
  * query row: the KDTreeFlann SearchKNN(feature, 1) calls of Open3D's

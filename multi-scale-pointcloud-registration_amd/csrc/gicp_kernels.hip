@@ -439,14 +439,12 @@ struct SolveArgs {
 // Per-start reduction of the block partials, convergence test
 // (RegistrationICP), and the 6x6 solve + pose update.  One wave per start.
 // --------------------------------------------------------------------------
-__global__ __launch_bounds__(64) void gicp_solve_kernel(const int32_t* __restrict__ active,
-                                                        const double* __restrict__ partial, int nblk, int N,
-                                                        int pass, int max_iter, double rel_fit, double rel_rmse,
-                                                        SolveArgs a) {
-    const int slot = active[blockIdx.x];
-    if (a.done[slot]) return;
-    const int lane = threadIdx.x;
-    double s[kNacc];
+// Fixed-order reduction of one start's block partials (lane-strided, then
+// the wave).  sums_in != null: the sums are given (row-sharded mode, already
+// all-reduced over ranks) and the partials are not read.
+__device__ __forceinline__ void reduce_partials(const double* __restrict__ partial, int slot, int nblk,
+                                                double s[kNacc]) {
+    const int lane = threadIdx.x & 63;
 #pragma unroll
     for (int v = 0; v < kNacc; ++v) s[v] = 0.0;
     for (int b = lane; b < nblk; b += 64) {
@@ -456,6 +454,30 @@ __global__ __launch_bounds__(64) void gicp_solve_kernel(const int32_t* __restric
     }
 #pragma unroll
     for (int v = 0; v < kNacc; ++v) s[v] = wave_sum(s[v]);
+}
+
+__global__ __launch_bounds__(64) void reduce_partials_kernel(const double* __restrict__ partial, int slot, int nblk,
+                                                             double* __restrict__ sums) {
+    double s[kNacc];
+    reduce_partials(partial, slot, nblk, s);
+    if (threadIdx.x == 0)
+        for (int v = 0; v < kNacc; ++v) sums[v] = s[v];
+}
+
+__global__ __launch_bounds__(64) void gicp_solve_kernel(const int32_t* __restrict__ active,
+                                                        const double* __restrict__ partial, int nblk,
+                                                        const double* __restrict__ sums_in, int64_t N, int pass,
+                                                        int max_iter, double rel_fit, double rel_rmse, SolveArgs a) {
+    const int slot = active[blockIdx.x];
+    if (a.done[slot]) return;
+    const int lane = threadIdx.x;
+    double s[kNacc];
+    if (sums_in) {
+#pragma unroll
+        for (int v = 0; v < kNacc; ++v) s[v] = sums_in[v];
+    } else {
+        reduce_partials(partial, slot, nblk, s);
+    }
     if (lane != 0) return;
 
     const double cnt = s[28];
@@ -596,13 +618,30 @@ hipError_t launch_gicp_pass(const orpcd_ctx* c, int nact, int pass, double r2, h
 hipError_t launch_gicp_solve(const orpcd_ctx* c, int nact, int pass, const orpcd_gicp_params& p, hipStream_t s) {
     SolveArgs a{c->T.p,    c->Q.p,       c->R.p,        c->G.p,         c->prev.p,
                 c->done.p, c->out_fit.p, c->out_rmse.p, c->out_iters.p, c->out_ncorr.p};
-    gicp_solve_kernel<<<(unsigned)nact, 64, 0, s>>>(c->active.p, c->partial.p, accum_blocks(c->src.n),
-                                                    (int)c->src.n, pass, p.max_iteration, p.relative_fitness,
+    gicp_solve_kernel<<<(unsigned)nact, 64, 0, s>>>(c->active.p, c->partial.p, accum_blocks(c->src.n), nullptr,
+                                                    c->src.n, pass, p.max_iteration, p.relative_fitness,
                                                     p.relative_rmse, a);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     const double r2 = p.max_correspondence_distance * p.max_correspondence_distance;
     return launch_xform(c, nact, r2, s);  // queries of the next pass (done starts skip)
+}
+
+hipError_t launch_reduce_partials(const orpcd_ctx* c, int slot, double* sums29, hipStream_t s) {
+    reduce_partials_kernel<<<1, 64, 0, s>>>(c->partial.p, slot, accum_blocks(c->src.n), sums29);
+    return hipGetLastError();
+}
+
+hipError_t launch_gicp_solve_sums(const orpcd_ctx* c, const double* sums29, int64_t n_total, int pass,
+                                  const orpcd_gicp_params& p, hipStream_t s) {
+    SolveArgs a{c->T.p,    c->Q.p,       c->R.p,        c->G.p,         c->prev.p,
+                c->done.p, c->out_fit.p, c->out_rmse.p, c->out_iters.p, c->out_ncorr.p};
+    gicp_solve_kernel<<<1, 64, 0, s>>>(c->active.p, nullptr, 0, sums29, n_total, pass, p.max_iteration,
+                                       p.relative_fitness, p.relative_rmse, a);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    const double r2 = p.max_correspondence_distance * p.max_correspondence_distance;
+    return launch_xform(c, 1, r2, s);
 }
 
 hipError_t launch_nn1(const double* q, int64_t nq, const CloudLayout& t, double r2, int32_t* idx, double* d2,

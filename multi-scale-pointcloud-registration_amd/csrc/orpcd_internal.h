@@ -204,11 +204,21 @@ struct orpcd_ctx {
     } opt;
     std::vector<hipEvent_t> ev_pool;
     orpcd::KernelStats stats;
+
+    // row-sharded single start (orpcd_gicp_shard_*)
+    struct Shard {
+        bool begun = false;
+        int pass = 0;
+        int64_t n_total = 0;
+        orpcd_gicp_params p{};
+    } shard;
 };
 
 namespace orpcd {
 
 // sort_kernels.hip
+hipError_t launch_gather_rows(const double* in, const int32_t* idx, int64_t offset, int64_t n, int w, double* out,
+                              hipStream_t s);
 hipError_t build_layout(const double* dev_in64, int64_t n, const double bbox_lo[3], double bbox_ext, CloudLayout& L,
                         bool with_tiles, hipStream_t s);
 
@@ -224,6 +234,9 @@ int accum_blocks(int64_t N);
 hipError_t launch_xform(const orpcd_ctx* c, int nact, double r2, hipStream_t s);
 hipError_t launch_gicp_pass(const orpcd_ctx* c, int nact, int pass, double r2, hipStream_t s, hipEvent_t mid);
 hipError_t launch_gicp_solve(const orpcd_ctx* c, int nact, int pass, const orpcd_gicp_params& p, hipStream_t s);
+hipError_t launch_reduce_partials(const orpcd_ctx* c, int slot, double* sums29, hipStream_t s);
+hipError_t launch_gicp_solve_sums(const orpcd_ctx* c, const double* sums29, int64_t n_total, int pass,
+                                  const orpcd_gicp_params& p, hipStream_t s);
 hipError_t launch_nn1(const double* q, int64_t nq, const CloudLayout& t, double r2, int32_t* idx, double* d2,
                       hipStream_t s);
 

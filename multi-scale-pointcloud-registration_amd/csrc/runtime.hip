@@ -337,6 +337,80 @@ int fgr_device(orpcd_ctx* c, const double* src, int64_t n, const double* tgt, in
     return ORPCD_OK;
 }
 
+// Device state of a batch of B starts (pose = source @ R0_b + t0_b) before
+// pass 0: base poses, identity T, posed-frame source covariances, first
+// queries.  Host staging in c->h64 / c->h32 (layout used by gicp_batch).
+int batch_setup(orpcd_ctx* c, const double* R0, const double* t0, int B, const orpcd_gicp_params* p) {
+    const int64_t N = c->src.n;
+    const int nblk = accum_blocks(N);
+    CTX_CHECK(c, c->scov.ensure((size_t)B * N * 6));
+    CTX_CHECK(c, c->prevnn.ensure((size_t)B * N));
+    CTX_CHECK(c, c->best.ensure((size_t)B * N));
+    CTX_CHECK(c, c->q32.ensure((size_t)B * N));
+    CTX_CHECK(c, c->G.ensure((size_t)B * 12));
+    CTX_CHECK(c, c->T.ensure((size_t)B * 16));
+    CTX_CHECK(c, c->Q.ensure((size_t)B * 12));
+    CTX_CHECK(c, c->R.ensure((size_t)B * 9));
+    CTX_CHECK(c, c->prev.ensure((size_t)B * 2));
+    CTX_CHECK(c, c->partial.ensure((size_t)B * nblk * kPartialStride));
+    CTX_CHECK(c, c->done.ensure((size_t)B));
+    CTX_CHECK(c, c->active.ensure((size_t)B));
+    CTX_CHECK(c, c->out_fit.ensure((size_t)B));
+    CTX_CHECK(c, c->out_rmse.ensure((size_t)B));
+    CTX_CHECK(c, c->out_iters.ensure((size_t)B));
+    CTX_CHECK(c, c->out_ncorr.ensure((size_t)B));
+    CTX_CHECK(c, c->scratch64c.ensure((size_t)B * 9));
+    CTX_CHECK(c, c->h64.ensure((size_t)B * 80));
+    CTX_CHECK(c, c->h32.ensure((size_t)B * 4));
+
+    // host: base pose G_b = [R0_b^T | t0_b] (source @ R0 + t0 in column form)
+    double* hG = c->h64.p;
+    double* hT = hG + (size_t)B * 12;
+    double* hQ = hT + (size_t)B * 16;
+    double* hR = hQ + (size_t)B * 12;
+    double* hRc = hR + (size_t)B * 9;
+    double* hPrev = hRc + (size_t)B * 9;
+    double* hFit = hPrev + (size_t)B * 2;
+    double* hRmse = hFit + B;
+    for (int b = 0; b < B; ++b) {
+        const double* r = R0 + 9 * b;
+        for (int i = 0; i < 3; ++i) {
+            for (int j = 0; j < 3; ++j) {
+                hG[12 * b + 4 * i + j] = r[3 * j + i];
+                hRc[9 * b + 3 * i + j] = r[3 * j + i];
+            }
+            hG[12 * b + 4 * i + 3] = t0[3 * b + i];
+        }
+        for (int t = 0; t < 16; ++t) hT[16 * b + t] = (t % 5 == 0) ? 1.0 : 0.0;
+        for (int t = 0; t < 12; ++t) hQ[12 * b + t] = hG[12 * b + t];
+        for (int t = 0; t < 9; ++t) hR[9 * b + t] = (t % 4 == 0) ? 1.0 : 0.0;
+        hPrev[2 * b] = hPrev[2 * b + 1] = 0.0;
+    }
+    int32_t* hAct = c->h32.p;
+    int32_t* hDone = hAct + B;
+    int32_t* hIters = hDone + B;
+    for (int b = 0; b < B; ++b) {
+        hAct[b] = b;
+        hDone[b] = 0;
+    }
+    hipStream_t s = c->stream;
+    CTX_CHECK(c, hipMemcpyAsync(c->G.p, hG, (size_t)B * 12 * 8, hipMemcpyHostToDevice, s));
+    CTX_CHECK(c, hipMemcpyAsync(c->T.p, hT, (size_t)B * 16 * 8, hipMemcpyHostToDevice, s));
+    CTX_CHECK(c, hipMemcpyAsync(c->Q.p, hQ, (size_t)B * 12 * 8, hipMemcpyHostToDevice, s));
+    CTX_CHECK(c, hipMemcpyAsync(c->R.p, hR, (size_t)B * 9 * 8, hipMemcpyHostToDevice, s));
+    CTX_CHECK(c, hipMemcpyAsync(c->scratch64c.p, hRc, (size_t)B * 9 * 8, hipMemcpyHostToDevice, s));
+    CTX_CHECK(c, hipMemcpyAsync(c->prev.p, hPrev, (size_t)B * 2 * 8, hipMemcpyHostToDevice, s));
+    CTX_CHECK(c, hipMemcpyAsync(c->active.p, hAct, (size_t)B * 4, hipMemcpyHostToDevice, s));
+    CTX_CHECK(c, hipMemcpyAsync(c->done.p, hDone, (size_t)B * 4, hipMemcpyHostToDevice, s));
+    CTX_CHECK(c, hipMemsetAsync(c->prevnn.p, 0xff, (size_t)B * N * 4, s));
+
+    // posed-frame source covariances for every start (rigid equivariance)
+    CTX_CHECK(c, launch_normals_cov(c->sraw.p, N, c->scratch64c.p, B, p->epsilon, nullptr, c->scov.p, s));
+    CTX_CHECK(c, launch_xform(c, B, p->max_correspondence_distance * p->max_correspondence_distance, s));
+
+    return ORPCD_OK;
+}
+
 }  // namespace
 
 extern "C" {
@@ -445,73 +519,17 @@ int orpcd_gicp_batch(orpcd_ctx* c, const double* R0, const double* t0, int32_t B
         int rc = upload_target(c, host.data(), c->tgt.n, p->epsilon);
         if (rc) return rc;
     }
+    int rc = batch_setup(c, R0, t0, B, p);
+    if (rc) return rc;
     const int64_t N = c->src.n;
-    const int nblk = accum_blocks(N);
-    CTX_CHECK(c, c->scov.ensure((size_t)B * N * 6));
-    CTX_CHECK(c, c->prevnn.ensure((size_t)B * N));
-    CTX_CHECK(c, c->best.ensure((size_t)B * N));
-    CTX_CHECK(c, c->q32.ensure((size_t)B * N));
-    CTX_CHECK(c, c->G.ensure((size_t)B * 12));
-    CTX_CHECK(c, c->T.ensure((size_t)B * 16));
-    CTX_CHECK(c, c->Q.ensure((size_t)B * 12));
-    CTX_CHECK(c, c->R.ensure((size_t)B * 9));
-    CTX_CHECK(c, c->prev.ensure((size_t)B * 2));
-    CTX_CHECK(c, c->partial.ensure((size_t)B * nblk * kPartialStride));
-    CTX_CHECK(c, c->done.ensure((size_t)B));
-    CTX_CHECK(c, c->active.ensure((size_t)B));
-    CTX_CHECK(c, c->out_fit.ensure((size_t)B));
-    CTX_CHECK(c, c->out_rmse.ensure((size_t)B));
-    CTX_CHECK(c, c->out_iters.ensure((size_t)B));
-    CTX_CHECK(c, c->out_ncorr.ensure((size_t)B));
-    CTX_CHECK(c, c->scratch64c.ensure((size_t)B * 9));
-    CTX_CHECK(c, c->h64.ensure((size_t)B * 80));
-    CTX_CHECK(c, c->h32.ensure((size_t)B * 4));
-
-    // host: base pose G_b = [R0_b^T | t0_b] (source @ R0 + t0 in column form)
-    double* hG = c->h64.p;
-    double* hT = hG + (size_t)B * 12;
-    double* hQ = hT + (size_t)B * 16;
-    double* hR = hQ + (size_t)B * 12;
-    double* hRc = hR + (size_t)B * 9;
-    double* hPrev = hRc + (size_t)B * 9;
-    double* hFit = hPrev + (size_t)B * 2;
+    (void)N;
+    double* hT = c->h64.p + (size_t)B * 12;
+    double* hFit = hT + (size_t)B * (16 + 12 + 9 + 9 + 2);
     double* hRmse = hFit + B;
-    for (int b = 0; b < B; ++b) {
-        const double* r = R0 + 9 * b;
-        for (int i = 0; i < 3; ++i) {
-            for (int j = 0; j < 3; ++j) {
-                hG[12 * b + 4 * i + j] = r[3 * j + i];
-                hRc[9 * b + 3 * i + j] = r[3 * j + i];
-            }
-            hG[12 * b + 4 * i + 3] = t0[3 * b + i];
-        }
-        for (int t = 0; t < 16; ++t) hT[16 * b + t] = (t % 5 == 0) ? 1.0 : 0.0;
-        for (int t = 0; t < 12; ++t) hQ[12 * b + t] = hG[12 * b + t];
-        for (int t = 0; t < 9; ++t) hR[9 * b + t] = (t % 4 == 0) ? 1.0 : 0.0;
-        hPrev[2 * b] = hPrev[2 * b + 1] = 0.0;
-    }
     int32_t* hAct = c->h32.p;
     int32_t* hDone = hAct + B;
     int32_t* hIters = hDone + B;
-    for (int b = 0; b < B; ++b) {
-        hAct[b] = b;
-        hDone[b] = 0;
-    }
     hipStream_t s = c->stream;
-    CTX_CHECK(c, hipMemcpyAsync(c->G.p, hG, (size_t)B * 12 * 8, hipMemcpyHostToDevice, s));
-    CTX_CHECK(c, hipMemcpyAsync(c->T.p, hT, (size_t)B * 16 * 8, hipMemcpyHostToDevice, s));
-    CTX_CHECK(c, hipMemcpyAsync(c->Q.p, hQ, (size_t)B * 12 * 8, hipMemcpyHostToDevice, s));
-    CTX_CHECK(c, hipMemcpyAsync(c->R.p, hR, (size_t)B * 9 * 8, hipMemcpyHostToDevice, s));
-    CTX_CHECK(c, hipMemcpyAsync(c->scratch64c.p, hRc, (size_t)B * 9 * 8, hipMemcpyHostToDevice, s));
-    CTX_CHECK(c, hipMemcpyAsync(c->prev.p, hPrev, (size_t)B * 2 * 8, hipMemcpyHostToDevice, s));
-    CTX_CHECK(c, hipMemcpyAsync(c->active.p, hAct, (size_t)B * 4, hipMemcpyHostToDevice, s));
-    CTX_CHECK(c, hipMemcpyAsync(c->done.p, hDone, (size_t)B * 4, hipMemcpyHostToDevice, s));
-    CTX_CHECK(c, hipMemsetAsync(c->prevnn.p, 0xff, (size_t)B * N * 4, s));
-
-    // posed-frame source covariances for every start (rigid equivariance)
-    CTX_CHECK(c, launch_normals_cov(c->sraw.p, N, c->scratch64c.p, B, p->epsilon, nullptr, c->scov.p, s));
-    CTX_CHECK(c, launch_xform(c, B, p->max_correspondence_distance * p->max_correspondence_distance, s));
-
     const double r2 = p->max_correspondence_distance * p->max_correspondence_distance;
     unsigned long long tiles_before = 0, unused = 0;
     if (c->profiling) CTX_CHECK(c, read_counters(c, tiles_before, unused, false));
@@ -592,6 +610,111 @@ int orpcd_gicp_batch(orpcd_ctx* c, const double* R0, const double* t0, int32_t B
         if (ncorr_out) ncorr_out[b] = nc[b];
         c->stats.iterations += hIters[b];
     }
+    return ORPCD_OK;
+}
+
+int orpcd_set_source_rows(orpcd_ctx* c, const double* xyz, int64_t n, int64_t row_begin, int64_t row_end) {
+    if (!c) return ORPCD_EINVAL;
+    CTX_REQUIRE(c, xyz && n > 0, "set_source_rows: empty source cloud");
+    CTX_REQUIRE(c, n < (int64_t)1 << 30, "set_source_rows: too many points");
+    CTX_REQUIRE(c, row_begin >= 0 && row_begin < row_end && row_end <= n, "set_source_rows: bad row range");
+    CTX_REQUIRE(c, finite_cloud(xyz, n), "set_source_rows: non-finite coordinates");
+    CTX_CHECK(c, hipSetDevice(c->device));
+    // KNN-20 covariances of every point against the full cloud (input order)
+    double margin = 0.0;
+    int rc = upload_layout(c, xyz, n, c->aux, true, &margin);
+    if (rc) return rc;
+    CTX_CHECK(c, c->scratch64b.ensure((size_t)n * 6));
+    CTX_CHECK(c, launch_knn_tiles(c->aux, c->scratch64a.p, 20, -1.0, margin, true, c->scratch64b.p, nullptr, nullptr,
+                                  nullptr, c->stream));
+    // the shard's rows in their own Morton layout, covariances gathered to it
+    const int64_t ns = row_end - row_begin;
+    rc = upload_layout(c, xyz + 3 * row_begin, ns, c->src, true);
+    if (rc) return rc;
+    CTX_CHECK(c, c->sraw.ensure((size_t)ns * 6));
+    CTX_CHECK(c, launch_gather_rows(c->scratch64b.p, c->src.perm.p, row_begin, ns, 6, c->sraw.p, c->stream));
+    CTX_CHECK(c, hipStreamSynchronize(c->stream));
+    return ORPCD_OK;
+}
+
+int orpcd_gicp_shard_begin(orpcd_ctx* c, const double* R0, const double* t0, const orpcd_gicp_params* p,
+                           int64_t n_total) {
+    if (!c) return ORPCD_EINVAL;
+    CTX_REQUIRE(c, R0 && t0 && p, "gicp_shard_begin: null argument");
+    CTX_REQUIRE(c, c->src.n > 0 && c->tgt.n > 0, "gicp_shard_begin: set the target and the source rows first");
+    CTX_REQUIRE(c, n_total >= c->src.n, "gicp_shard_begin: n_total smaller than this rank's rows");
+    CTX_REQUIRE(c, p->max_correspondence_distance > 0 && p->max_iteration >= 0 && p->epsilon >= 0,
+                "gicp_shard_begin: bad parameters");
+    CTX_CHECK(c, hipSetDevice(c->device));
+    if (c->tgt_eps != p->epsilon) {
+        std::vector<double> host = c->tgt_host;
+        int rc = upload_target(c, host.data(), c->tgt.n, p->epsilon);
+        if (rc) return rc;
+    }
+    int rc = batch_setup(c, R0, t0, 1, p);
+    if (rc) return rc;
+    CTX_CHECK(c, c->scratch64c.ensure(kNacc));
+    c->shard.begun = true;
+    c->shard.pass = 0;
+    c->shard.n_total = n_total;
+    c->shard.p = *p;
+    return ORPCD_OK;
+}
+
+int orpcd_gicp_shard_pass(orpcd_ctx* c, double* sums_out, int32_t* active) {
+    if (!c) return ORPCD_EINVAL;
+    CTX_REQUIRE(c, sums_out && active, "gicp_shard_pass: null argument");
+    CTX_REQUIRE(c, c->shard.begun, "gicp_shard_pass: call orpcd_gicp_shard_begin first");
+    int32_t done = 0;
+    CTX_CHECK(c, hipMemcpyAsync(&done, c->done.p, 4, hipMemcpyDeviceToHost, c->stream));
+    CTX_CHECK(c, hipStreamSynchronize(c->stream));
+    *active = done ? 0 : 1;
+    for (int v = 0; v < kNacc; ++v) sums_out[v] = 0.0;
+    if (done) return ORPCD_OK;
+    const double r2 = c->shard.p.max_correspondence_distance * c->shard.p.max_correspondence_distance;
+    CTX_CHECK(c, launch_gicp_pass(c, 1, c->shard.pass, r2, c->stream, nullptr));
+    CTX_CHECK(c, launch_reduce_partials(c, 0, c->scratch64c.p, c->stream));
+    CTX_CHECK(c, hipMemcpyAsync(sums_out, c->scratch64c.p, kNacc * 8, hipMemcpyDeviceToHost, c->stream));
+    CTX_CHECK(c, hipStreamSynchronize(c->stream));
+    c->stats.passes += 1;
+    return ORPCD_OK;
+}
+
+int orpcd_gicp_shard_update(orpcd_ctx* c, const double* sums_in, int32_t* done_out) {
+    if (!c) return ORPCD_EINVAL;
+    CTX_REQUIRE(c, sums_in && done_out, "gicp_shard_update: null argument");
+    CTX_REQUIRE(c, c->shard.begun, "gicp_shard_update: call orpcd_gicp_shard_begin first");
+    CTX_CHECK(c, hipMemcpyAsync(c->scratch64c.p, sums_in, kNacc * 8, hipMemcpyHostToDevice, c->stream));
+    CTX_CHECK(c, launch_gicp_solve_sums(c, c->scratch64c.p, c->shard.n_total, c->shard.pass, c->shard.p, c->stream));
+    int32_t done = 0;
+    CTX_CHECK(c, hipMemcpyAsync(&done, c->done.p, 4, hipMemcpyDeviceToHost, c->stream));
+    CTX_CHECK(c, hipStreamSynchronize(c->stream));
+    c->shard.pass += 1;
+    *done_out = done;
+    return ORPCD_OK;
+}
+
+int orpcd_gicp_shard_result(orpcd_ctx* c, double* T_out, double* rmse_out, double* fitness_out, int32_t* iters_out,
+                            int64_t* ncorr_out) {
+    if (!c) return ORPCD_EINVAL;
+    CTX_REQUIRE(c, T_out && rmse_out, "gicp_shard_result: null argument");
+    CTX_REQUIRE(c, c->shard.begun, "gicp_shard_result: call orpcd_gicp_shard_begin first");
+    int32_t done = 0, iters = 0;
+    double fit = 0.0;
+    int64_t nc = 0;
+    hipStream_t s = c->stream;
+    CTX_CHECK(c, hipMemcpyAsync(&done, c->done.p, 4, hipMemcpyDeviceToHost, s));
+    CTX_CHECK(c, hipMemcpyAsync(T_out, c->T.p, 16 * 8, hipMemcpyDeviceToHost, s));
+    CTX_CHECK(c, hipMemcpyAsync(rmse_out, c->out_rmse.p, 8, hipMemcpyDeviceToHost, s));
+    CTX_CHECK(c, hipMemcpyAsync(&fit, c->out_fit.p, 8, hipMemcpyDeviceToHost, s));
+    CTX_CHECK(c, hipMemcpyAsync(&iters, c->out_iters.p, 4, hipMemcpyDeviceToHost, s));
+    CTX_CHECK(c, hipMemcpyAsync(&nc, c->out_ncorr.p, 8, hipMemcpyDeviceToHost, s));
+    CTX_CHECK(c, hipStreamSynchronize(s));
+    CTX_REQUIRE(c, done, "gicp_shard_result: the start has not finished");
+    if (fitness_out) *fitness_out = fit;
+    if (iters_out) *iters_out = iters;
+    if (ncorr_out) *ncorr_out = nc;
+    c->stats.iterations += iters;
     return ORPCD_OK;
 }
 

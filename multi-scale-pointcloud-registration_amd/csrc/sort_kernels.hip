@@ -93,6 +93,22 @@ __global__ void super_aabb_kernel(const float4* __restrict__ tlo, const float4* 
     shi[u] = hi;
 }
 
+// out[k] = in[offset + idx[k]] (rows of w doubles)
+__global__ void gather_rows_kernel(const double* __restrict__ in, const int32_t* __restrict__ idx, int64_t offset,
+                                   int n, int w, double* __restrict__ out) {
+    const int k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= n) return;
+    const double* r = in + (size_t)(offset + idx[k]) * w;
+    for (int c = 0; c < w; ++c) out[(size_t)k * w + c] = r[c];
+}
+
+hipError_t launch_gather_rows(const double* in, const int32_t* idx, int64_t offset, int64_t n, int w, double* out,
+                              hipStream_t s) {
+    if (n <= 0) return hipSuccess;
+    gather_rows_kernel<<<(unsigned)((n + 255) / 256), 256, 0, s>>>(in, idx, offset, (int)n, w, out);
+    return hipGetLastError();
+}
+
 hipError_t build_layout(const double* dev_in64, int64_t n, const double bbox_lo[3], double bbox_ext,
                         CloudLayout& L, bool with_tiles, hipStream_t s) {
     L.n = n;

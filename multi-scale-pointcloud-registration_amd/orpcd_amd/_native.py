@@ -46,6 +46,8 @@ _lib_lock = threading.Lock()
 # every symbol include/orpcd.h declares (checked by tests/test_abi.py)
 EXPORTED = ("orpcd_abi_version", "orpcd_device_count", "orpcd_ctx_create", "orpcd_ctx_destroy",
             "orpcd_last_error", "orpcd_set_target", "orpcd_set_source", "orpcd_gicp_batch",
+            "orpcd_set_source_rows", "orpcd_gicp_shard_begin", "orpcd_gicp_shard_pass", "orpcd_gicp_shard_update",
+            "orpcd_gicp_shard_result",
             "orpcd_nn1_radius", "orpcd_estimate_normals", "orpcd_fpfh", "orpcd_fpfh_from_normals", "orpcd_fgr", "orpcd_feature_nn",
             "orpcd_fgr_optimize",
             "orpcd_set_option",
@@ -74,6 +76,11 @@ def load_library():
         L.orpcd_set_source.argtypes = [vp, _f64p, c_i64]
         L.orpcd_gicp_batch.argtypes = [vp, _f64p, _f64p, ctypes.c_int32, ctypes.POINTER(GicpParams), _f64p, _f64p,
                                        _f64p, _i32p, _i64p]
+        L.orpcd_set_source_rows.argtypes = [vp, _f64p, c_i64, c_i64, c_i64]
+        L.orpcd_gicp_shard_begin.argtypes = [vp, _f64p, _f64p, ctypes.POINTER(GicpParams), c_i64]
+        L.orpcd_gicp_shard_pass.argtypes = [vp, _f64p, _i32p]
+        L.orpcd_gicp_shard_update.argtypes = [vp, _f64p, _i32p]
+        L.orpcd_gicp_shard_result.argtypes = [vp, _f64p, _f64p, _f64p, _i32p, _i64p]
         L.orpcd_nn1_radius.argtypes = [vp, _f64p, c_i64, _f64p, c_i64, c_dbl, _i32p, _f64p]
         L.orpcd_estimate_normals.argtypes = [vp, _f64p, c_i64, ctypes.c_int32, c_dbl, c_dbl, vp, vp, vp]
         L.orpcd_fpfh.argtypes = [vp, _f64p, c_i64, c_dbl, ctypes.c_int32, c_dbl, ctypes.c_int32, _f64p, _f64p]
@@ -181,6 +188,42 @@ class Context:
         self._check(self._L.orpcd_gicp_batch(self._h, R0.reshape(-1), t0.reshape(-1), B, ctypes.byref(p),
                                              T.reshape(-1), rmse, fit, iters, ncorr), "orpcd_gicp_batch")
         return dict(T=T, rmse=rmse, fitness=fit, iters=iters, ncorr=ncorr)
+
+    # ------------------------------------------ one start, rows over ranks
+    def set_source_rows(self, xyz: np.ndarray, row_begin: int, row_end: int):
+        xyz = _c3(xyz)
+        self._check(self._L.orpcd_set_source_rows(self._h, xyz, len(xyz), int(row_begin), int(row_end)),
+                    "orpcd_set_source_rows")
+        self._source_key = None
+
+    def shard_begin(self, R0, t0, n_total: int, max_correspondence_distance=0.5, max_iteration=100,
+                    relative_fitness=1e-6, relative_rmse=1e-6, epsilon=1e-3):
+        p = GicpParams(float(max_correspondence_distance), int(max_iteration), float(relative_fitness),
+                       float(relative_rmse), float(epsilon))
+        R0 = np.ascontiguousarray(R0, dtype=np.float64).reshape(9)
+        t0 = np.ascontiguousarray(t0, dtype=np.float64).reshape(3)
+        self._check(self._L.orpcd_gicp_shard_begin(self._h, R0, t0, ctypes.byref(p), int(n_total)),
+                    "orpcd_gicp_shard_begin")
+
+    def shard_pass(self):
+        """(local sums (29,), active)"""
+        sums = np.zeros(29)
+        act = np.zeros(1, np.int32)
+        self._check(self._L.orpcd_gicp_shard_pass(self._h, sums, act), "orpcd_gicp_shard_pass")
+        return sums, bool(act[0])
+
+    def shard_update(self, sums: np.ndarray) -> bool:
+        sums = np.ascontiguousarray(sums, dtype=np.float64).reshape(29)
+        done = np.zeros(1, np.int32)
+        self._check(self._L.orpcd_gicp_shard_update(self._h, sums, done), "orpcd_gicp_shard_update")
+        return bool(done[0])
+
+    def shard_result(self) -> dict:
+        T, rmse, fit = np.zeros(16), np.zeros(1), np.zeros(1)
+        it, nc = np.zeros(1, np.int32), np.zeros(1, np.int64)
+        self._check(self._L.orpcd_gicp_shard_result(self._h, T, rmse, fit, it, nc), "orpcd_gicp_shard_result")
+        return dict(T=T.reshape(4, 4), rmse=float(rmse[0]), fitness=float(fit[0]), iters=int(it[0]),
+                    ncorr=int(nc[0]))
 
     # -------------------------------------------------------- kernel level
     def nn1_radius(self, q: np.ndarray, t: np.ndarray, radius: float):

@@ -1,11 +1,19 @@
-"""Multistart sharding across ranks (one process per GPU).
+"""Sharding across ranks (one process per GPU).
 
-The attempts of one ``multistart_registration`` (Aligner.py:178-202) are
-independent: every rank replays the identical host RNG stream, runs a
+1. Multistart sharding.  The attempts of one ``multistart_registration``
+(Aligner.py:178-202) are independent: every rank replays the identical host RNG stream, runs a
 contiguous block of attempts on its own GPU, and one all-gather of a fixed
 160-byte record per attempt gives every rank the full table, on which each
 applies the reference's strict-< argmin in attempt order.  No other data-path
-collective exists.  Backend: ``torch.distributed`` — "nccl" (= RCCL over
+collective exists.
+
+2. Row sharding of one start (C5: one GICP over 1M points).  Each rank owns
+a contiguous block of source rows (covariances still from the full cloud's
+neighbourhoods) and the whole target; per ICP pass it computes the 29 local
+normal-equation sums, one all-reduce(sum) of 232 bytes combines them, and
+every rank solves the same 6x6 system (gicp_rows_sharded).
+
+Backend: ``torch.distributed`` — "nccl" (= RCCL over
 xGMI on ROCm) on GPUs, "gloo" for CPU tests.
 """
 from __future__ import annotations
@@ -73,3 +81,40 @@ def allgather_records(local: np.ndarray, B: int) -> np.ndarray:
         lo, hi = shard(B, r, ws)
         table[lo:hi] = outs[r][: hi - lo].cpu().numpy()
     return table
+
+
+def allreduce_sum(v: np.ndarray) -> np.ndarray:
+    """Sum a small float64 vector over ranks (identity on one rank)."""
+    rank, ws = world()
+    if ws == 1:
+        return v
+    import torch
+    import torch.distributed as dist
+
+    dev = torch.device("cuda", torch.cuda.current_device()) if dist.get_backend() == "nccl" else torch.device("cpu")
+    t = torch.from_numpy(np.ascontiguousarray(v, dtype=np.float64)).to(dev)
+    dist.all_reduce(t, op=dist.ReduceOp.SUM)
+    return t.cpu().numpy()
+
+
+def gicp_rows_sharded(ctx, source: np.ndarray, target: np.ndarray, R0=None, t0=None, epsilon: float = 1e-3,
+                      **params) -> dict:
+    """One GICP (pose ``source @ R0 + t0``) with the source rows split over the
+    ranks of the default process group.  ``ctx`` is this rank's device
+    context (``_native.Context`` or any object with the same shard_* calls).
+    Returns the Open3D-convention result (T column convention)."""
+    rank, ws = world()
+    n = len(source)
+    lo, hi = shard(n, rank, ws)
+    R0 = np.eye(3) if R0 is None else R0
+    t0 = np.zeros(3) if t0 is None else t0
+    ctx.set_target(target, epsilon)
+    ctx.set_source_rows(source, lo, hi)
+    ctx.shard_begin(R0, t0, n_total=n, epsilon=epsilon, **params)
+    while True:
+        sums, active = ctx.shard_pass()
+        if not active:
+            break
+        if ctx.shard_update(allreduce_sum(sums)):
+            break
+    return ctx.shard_result()

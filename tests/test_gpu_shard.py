@@ -1,0 +1,68 @@
+"""GPU: one GICP with the source rows split over ranks (C5's multi-GPU path),
+through the C-ABI (orpcd_set_source_rows / orpcd_gicp_shard_*).
+
+* one rank: bit-identical to orpcd_gicp_batch with B = 1 (same reduction);
+* two ranks emulated by two contexts in one process, the 29 sums added on the
+  host as the all-reduce would: T within 1e-9 of the un-sharded run (only the
+  summation order of the sums differs), same iteration count;
+* against the CPU oracle: the usual GICP tolerances (T <= 1e-6, rmse <= 1e-7).
+"""
+import numpy as np
+import pytest
+
+from workloads import small_pair
+
+pytestmark = pytest.mark.gpu
+
+
+def _pair():
+    return small_pair(6007, 5003, seed=11)
+
+
+def test_shard_single_rank_is_bitwise_gicp_batch(ctx):
+    from orpcd_amd import parallel
+    src, tgt = _pair()
+    r = parallel.gicp_rows_sharded(ctx, src, tgt, max_correspondence_distance=0.3)
+    ctx.set_target(tgt, 1e-3, cache=False)
+    ctx.set_source(src, cache=False)
+    b = ctx.gicp_batch(np.eye(3)[None], np.zeros((1, 3)), max_correspondence_distance=0.3)
+    assert np.array_equal(r["T"], b["T"][0]) and r["rmse"] == b["rmse"][0]
+    assert r["iters"] == b["iters"][0] and r["ncorr"] == b["ncorr"][0] and r["fitness"] == b["fitness"][0]
+
+
+@pytest.mark.parametrize("splits", [2, 3])
+def test_shard_emulated_ranks_match_unsharded(ctx, oracle, splits):
+    from orpcd_amd import _native, parallel
+    src, tgt = _pair()
+    ctxs = [_native.Context(0) for _ in range(splits)]
+    for k, c in enumerate(ctxs):
+        lo, hi = parallel.shard(len(src), k, splits)
+        c.set_target(tgt, 1e-3)
+        c.set_source_rows(src, lo, hi)
+        c.shard_begin(np.eye(3), np.zeros(3), n_total=len(src), max_correspondence_distance=0.3)
+    while True:
+        parts = [c.shard_pass() for c in ctxs]
+        assert len({a for _, a in parts}) == 1
+        if not parts[0][1]:
+            break
+        total = np.sum([s for s, _ in parts], axis=0)
+        done = {c.shard_update(total) for c in ctxs}
+        assert len(done) == 1
+        if done.pop():
+            break
+    res = [c.shard_result() for c in ctxs]
+    for r in res[1:]:
+        assert np.array_equal(r["T"], res[0]["T"]) and r["rmse"] == res[0]["rmse"]
+    ref = parallel.gicp_rows_sharded(ctx, src, tgt, max_correspondence_distance=0.3)
+    assert res[0]["iters"] == ref["iters"] and res[0]["ncorr"] == ref["ncorr"]
+    assert np.allclose(res[0]["T"], ref["T"], atol=1e-9, rtol=0)
+    o = oracle.gicp(src, tgt, 0.3)
+    assert np.allclose(res[0]["T"], o["T"], atol=1e-6, rtol=0) and abs(res[0]["rmse"] - o["rmse"]) <= 1e-7
+
+
+def test_shard_errors(ctx):
+    src, tgt = _pair()
+    with pytest.raises(ValueError):
+        ctx.set_source_rows(src, 10, 5)
+    with pytest.raises(ValueError):
+        ctx.set_source_rows(src, 0, len(src) + 1)
