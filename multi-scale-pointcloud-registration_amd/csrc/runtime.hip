@@ -672,10 +672,34 @@ int orpcd_gicp_shard_pass(orpcd_ctx* c, double* sums_out, int32_t* active) {
     for (int v = 0; v < kNacc; ++v) sums_out[v] = 0.0;
     if (done) return ORPCD_OK;
     const double r2 = c->shard.p.max_correspondence_distance * c->shard.p.max_correspondence_distance;
-    CTX_CHECK(c, launch_gicp_pass(c, 1, c->shard.pass, r2, c->stream, nullptr));
+    const bool timed = c->profiling;
+    c->count_tiles = timed;
+    unsigned long long tiles0 = 0, tiles1 = 0, unused = 0;
+    if (timed) {
+        while (c->ev_pool.size() < 3) {
+            hipEvent_t e;
+            CTX_CHECK(c, hipEventCreate(&e));
+            c->ev_pool.push_back(e);
+        }
+        CTX_CHECK(c, read_counters(c, tiles0, unused, false));
+        CTX_CHECK(c, hipEventRecord(c->ev_pool[0], c->stream));
+    }
+    CTX_CHECK(c, launch_gicp_pass(c, 1, c->shard.pass, r2, c->stream, timed ? c->ev_pool[1] : nullptr));
+    if (timed) CTX_CHECK(c, hipEventRecord(c->ev_pool[2], c->stream));
     CTX_CHECK(c, launch_reduce_partials(c, 0, c->scratch64c.p, c->stream));
     CTX_CHECK(c, hipMemcpyAsync(sums_out, c->scratch64c.p, kNacc * 8, hipMemcpyDeviceToHost, c->stream));
     CTX_CHECK(c, hipStreamSynchronize(c->stream));
+    if (timed) {
+        float ms = 0.f, ms2 = 0.f;
+        CTX_CHECK(c, hipEventElapsedTime(&ms, c->ev_pool[0], c->ev_pool[1]));
+        CTX_CHECK(c, hipEventElapsedTime(&ms2, c->ev_pool[1], c->ev_pool[2]));
+        CTX_CHECK(c, read_counters(c, tiles1, unused, false));
+        c->stats.launches += 1;
+        c->stats.ms += ms;
+        c->stats.accum_ms += ms2;
+        c->stats.tiles += (double)(tiles1 - tiles0);
+        c->stats.pairs += (double)(tiles1 - tiles0) * kTile * (64.0 * kCQPT);
+    }
     c->stats.passes += 1;
     return ORPCD_OK;
 }
