@@ -171,6 +171,7 @@ int orpcd_fgr_optimize(orpcd_ctx* ctx, const double* src, int64_t n, const doubl
  *   "search_waves"  split a start's tiles over waves until ~this many run
  *   "sync_every"    passes between host checks of the per-start done flags
  *   "super_cull"    0/1: first culling level over 64-tile super-tiles
+ *   "search_occupancy" 0 or 6: register budget of the search kernel
  *   "reseed"        0/1: representative seeding for queries that found no
  *                   target within radius in the previous pass             */
 int orpcd_set_option(orpcd_ctx* ctx, const char* key, double value);

@@ -283,44 +283,80 @@ __device__ __forceinline__ Sym3 rotate_sym(const double R[9], const Sym3& S) {
 // ---------------------------------------------------------------- 6x6 solve
 // O3D utility/Eigen.cpp SolveLinearSystemPSD with check_det=true:
 // det by partial-pivot LU; |det| < 1e-6 -> failure; else Eigen LDLT.
+// Row / column exchanges below are written as fully unrolled selects on a
+// compile-time index (never A[piv][j] with a runtime piv), so the 6x6 stays in
+// registers; the arithmetic and its order are those of the CPU restatement.
+__device__ __forceinline__ void swap_rows6(double A[6][6], int k, int p) {
+#pragma unroll
+    for (int i = 0; i < 6; ++i) {
+        if (i <= k) continue;
+        const bool sw = i == p;
+#pragma unroll
+        for (int j = 0; j < 6; ++j) {
+            const double a = A[k][j], b = A[i][j];
+            A[k][j] = sw ? b : a;
+            A[i][j] = sw ? a : b;
+        }
+    }
+}
+__device__ __forceinline__ void swap_cols6(double A[6][6], int k, int p) {
+#pragma unroll
+    for (int i = 0; i < 6; ++i) {
+        if (i <= k) continue;
+        const bool sw = i == p;
+#pragma unroll
+        for (int j = 0; j < 6; ++j) {
+            const double a = A[j][k], b = A[j][i];
+            A[j][k] = sw ? b : a;
+            A[j][i] = sw ? a : b;
+        }
+    }
+}
+
+// Eigen PartialPivLU determinant (SolveLinearSystemPSD's check_det).
 __device__ inline double det6(const double Ain[36]) {
     double A[6][6];
 #pragma unroll
     for (int i = 0; i < 36; ++i) A[i / 6][i % 6] = Ain[i];
     double det = 1.0;
+    bool zero = false;
+#pragma unroll
     for (int k = 0; k < 6; ++k) {
         int piv = k;
         double best = fabs(A[k][k]);
+#pragma unroll
         for (int i = k + 1; i < 6; ++i)
             if (fabs(A[i][k]) > best) {
                 best = fabs(A[i][k]);
                 piv = i;
             }
         if (piv != k) {
-            for (int j = 0; j < 6; ++j) {
-                double t = A[k][j];
-                A[k][j] = A[piv][j];
-                A[piv][j] = t;
-            }
+            swap_rows6(A, k, piv);
             det = -det;
         }
-        if (A[k][k] == 0.0) return 0.0;
+        zero = zero || A[k][k] == 0.0;
+#pragma unroll
         for (int i = k + 1; i < 6; ++i) {
-            double f = A[i][k] / A[k][k];
+            const double f = A[i][k] / A[k][k];
+#pragma unroll
             for (int j = k + 1; j < 6; ++j) A[i][j] -= f * A[k][j];
         }
         det *= A[k][k];
     }
-    return det;
+    return zero ? 0.0 : det;
 }
 
+// Eigen LDLT (diagonal pivoting) solve of A x = b.
 __device__ inline void ldlt_solve6(const double Ain[36], const double b[6], double x[6]) {
     double A[6][6];
+#pragma unroll
     for (int i = 0; i < 36; ++i) A[i / 6][i % 6] = Ain[i];
     int tr[6];
+#pragma unroll
     for (int k = 0; k < 6; ++k) {
         int idx = k;
         double big = fabs(A[k][k]);
+#pragma unroll
         for (int i = k + 1; i < 6; ++i)
             if (fabs(A[i][i]) > big) {
                 big = fabs(A[i][i]);
@@ -328,51 +364,60 @@ __device__ inline void ldlt_solve6(const double Ain[36], const double b[6], doub
             }
         tr[k] = idx;
         if (idx != k) {
-            for (int j = 0; j < 6; ++j) {
-                double t = A[k][j];
-                A[k][j] = A[idx][j];
-                A[idx][j] = t;
-            }
-            for (int j = 0; j < 6; ++j) {
-                double t = A[j][k];
-                A[j][k] = A[j][idx];
-                A[j][idx] = t;
-            }
+            swap_rows6(A, k, idx);
+            swap_cols6(A, k, idx);
         }
         double tmp[6];
+#pragma unroll
         for (int j = 0; j < k; ++j) tmp[j] = A[j][j] * A[k][j];
         double s = 0.0;
+#pragma unroll
         for (int j = 0; j < k; ++j) s += A[k][j] * tmp[j];
         A[k][k] -= s;
+#pragma unroll
         for (int i = k + 1; i < 6; ++i) {
             double t = 0.0;
+#pragma unroll
             for (int j = 0; j < k; ++j) t += A[i][j] * tmp[j];
             A[i][k] -= t;
         }
-        double akk = A[k][k];
-        if (fabs(akk) > 0.0)
+        const double akk = A[k][k];
+        if (fabs(akk) > 0.0) {
+#pragma unroll
             for (int i = k + 1; i < 6; ++i) A[i][k] /= akk;
+        }
     }
     double y[6];
+#pragma unroll
     for (int i = 0; i < 6; ++i) y[i] = b[i];
-    for (int k = 0; k < 6; ++k)
-        if (tr[k] != k) {
-            double t = y[k];
-            y[k] = y[tr[k]];
-            y[tr[k]] = t;
+    auto swap_y = [&](int k, int p) {
+#pragma unroll
+        for (int m = 0; m < 6; ++m) {
+            if (m <= k) continue;
+            const bool sw = m == p;
+            const double a = y[k], c = y[m];
+            y[k] = sw ? c : a;
+            y[m] = sw ? a : c;
         }
+    };
+#pragma unroll
+    for (int k = 0; k < 6; ++k)
+        if (tr[k] != k) swap_y(k, tr[k]);
+#pragma unroll
     for (int i = 0; i < 6; ++i)
+#pragma unroll
         for (int j = 0; j < i; ++j) y[i] -= A[i][j] * y[j];
     const double tol = 2.2250738585072014e-308;
+#pragma unroll
     for (int i = 0; i < 6; ++i) y[i] = fabs(A[i][i]) > tol ? y[i] / A[i][i] : 0.0;
+#pragma unroll
     for (int i = 5; i >= 0; --i)
+#pragma unroll
         for (int j = i + 1; j < 6; ++j) y[i] -= A[j][i] * y[j];
+#pragma unroll
     for (int k = 5; k >= 0; --k)
-        if (tr[k] != k) {
-            double t = y[k];
-            y[k] = y[tr[k]];
-            y[tr[k]] = t;
-        }
+        if (tr[k] != k) swap_y(k, tr[k]);
+#pragma unroll
     for (int i = 0; i < 6; ++i) x[i] = y[i];
 }
 

@@ -255,11 +255,13 @@ __global__ __launch_bounds__(256) void xform_queries_kernel(const double* __rest
                                                             const int32_t* __restrict__ done,
                                                             const float4* __restrict__ p4, int ntiles,
                                                             int seed_stride, const int32_t* __restrict__ prevnn,
-                                                            float r2s, int reseed, float4* __restrict__ q32) {
+                                                            float r2s, int reseed, float4* __restrict__ q32,
+                                                            unsigned long long* __restrict__ best) {
     const int slot = active[blockIdx.y];
     if (done[slot]) return;
     const int i = blockIdx.x * 256 + threadIdx.x;
     if (i >= N) return;
+    best[(size_t)slot * N + i] = kNone;  // split searches merge into it by atomicMin
     double Q[12];
 #pragma unroll
     for (int t = 0; t < 12; ++t) Q[t] = Qm[12 * slot + t];
@@ -281,7 +283,7 @@ __global__ __launch_bounds__(256) void xform_queries_kernel(const double* __rest
 // --------------------------------------------------------------------------
 // Search kernel: grid = (blocks per start * S, running starts), 4 waves/block.
 // --------------------------------------------------------------------------
-__global__ __launch_bounds__(kCBlock) void nn_search_kernel(
+__device__ __forceinline__ void nn_search_body(
     const float4* __restrict__ q32, int N, const float4* __restrict__ p4, const float4* __restrict__ tlo,
     const float4* __restrict__ thi, int ntiles, const float4* __restrict__ slo, const float4* __restrict__ shi,
     int nsuper, int super_cull, const int32_t* __restrict__ active, const int32_t* __restrict__ done, int S,
@@ -325,6 +327,24 @@ __global__ __launch_bounds__(kCBlock) void nn_search_kernel(
             atomicMin(out + i, v);
     }
 }
+
+// Two register budgets of the same search (orpcd_set_option "search_occupancy"):
+// the compiler's choice (88 VGPRs, 5 waves/SIMD) and a cap at 6 waves/SIMD
+// (74 VGPRs, no spills).
+#define ORPCD_NN_SEARCH_ARGS                                                                                   \
+    const float4 *__restrict__ q32, int N, const float4 *__restrict__ p4, const float4 *__restrict__ tlo,    \
+        const float4 *__restrict__ thi, int ntiles, const float4 *__restrict__ slo,                          \
+        const float4 *__restrict__ shi, int nsuper, int super_cull, const int32_t *__restrict__ active,      \
+        const int32_t *__restrict__ done, int S, unsigned long long *__restrict__ best,                      \
+        unsigned long long *__restrict__ counters
+__global__ __launch_bounds__(kCBlock) void nn_search_kernel(ORPCD_NN_SEARCH_ARGS) {
+    nn_search_body(q32, N, p4, tlo, thi, ntiles, slo, shi, nsuper, super_cull, active, done, S, best, counters);
+}
+__global__ __launch_bounds__(kCBlock) __attribute__((amdgpu_waves_per_eu(6, 8))) void nn_search_kernel_o6(
+    ORPCD_NN_SEARCH_ARGS) {
+    nn_search_body(q32, N, p4, tlo, thi, ntiles, slo, shi, nsuper, super_cull, active, done, S, best, counters);
+}
+#undef ORPCD_NN_SEARCH_ARGS
 
 // --------------------------------------------------------------------------
 // Accumulation kernel: one query per thread, grid = (blocks per start, running
@@ -589,7 +609,7 @@ hipError_t launch_xform(const orpcd_ctx* c, int nact, double r2, hipStream_t s) 
     const int N = (int)c->src.n;
     xform_queries_kernel<<<dim3((unsigned)((N + 255) / 256), (unsigned)nact), 256, 0, s>>>(
         c->src.xyz64.p, N, c->active.p, c->Q.p, c->done.p, c->tgt.p4.p, (int)c->tgt.ntiles,
-        seed_stride_for(c->tgt.ntiles), c->prevnn.p, search_r2(r2), c->opt.reseed, c->q32.p);
+        seed_stride_for(c->tgt.ntiles), c->prevnn.p, search_r2(r2), c->opt.reseed, c->q32.p, c->best.p);
     return hipGetLastError();
 }
 
@@ -597,12 +617,9 @@ hipError_t launch_gicp_pass(const orpcd_ctx* c, int nact, int pass, double r2, h
     const int N = (int)c->src.n;
     const int sblk = (N + kCBlockQ - 1) / kCBlockQ;
     const int S = search_splits(nact, sblk, c->opt.search_waves);
-    hipError_t e;
-    if (S > 1) {  // splits merge by atomicMin: reset every slot's result
-        e = hipMemsetAsync(c->best.p, 0xff, c->best.n * sizeof(unsigned long long), s);
-        if (e != hipSuccess) return e;
-    }
-    nn_search_kernel<<<dim3((unsigned)(sblk * S), (unsigned)nact), kCBlock, 0, s>>>(
+    hipError_t e;  // best[] was reset to kNone by xform_queries_kernel
+    auto kern = c->opt.search_occupancy == 6 ? nn_search_kernel_o6 : nn_search_kernel;
+    kern<<<dim3((unsigned)(sblk * S), (unsigned)nact), kCBlock, 0, s>>>(
         c->q32.p, N, c->tgt.p4.p, c->tgt.tlo.p, c->tgt.thi.p, (int)c->tgt.ntiles, c->tgt.slo.p, c->tgt.shi.p,
         (int)c->tgt.nsuper, c->opt.super_cull, c->active.p, c->done.p, S, c->best.p,
         c->count_tiles ? c->counters.p : nullptr);

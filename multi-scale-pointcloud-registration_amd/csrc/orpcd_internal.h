@@ -201,6 +201,7 @@ struct orpcd_ctx {
         int sync_every = 4;       // passes between host checks of the done flags
         int super_cull = 1;       // first culling level over 64-tile super-tiles
         int reseed = 0;           // representative seeding also after pass 0
+        int search_occupancy = 0; // 0: compiler's register budget; 6: capped at 6 waves/SIMD
     } opt;
     std::vector<hipEvent_t> ev_pool;
     orpcd::KernelStats stats;

@@ -943,6 +943,7 @@ int orpcd_set_option(orpcd_ctx* c, const char* key, double value) {
     else if (k == "sync_every" && v >= 1 && v <= 64) c->opt.sync_every = v;
     else if (k == "super_cull" && (v == 0 || v == 1)) c->opt.super_cull = v;
     else if (k == "reseed" && (v == 0 || v == 1)) c->opt.reseed = v;
+    else if (k == "search_occupancy" && (v == 0 || v == 6)) c->opt.search_occupancy = v;
     else {
         c->err = "set_option: unknown key or bad value: " + k;
         return ORPCD_EINVAL;
