@@ -18,6 +18,9 @@
  *   orpcd_set_source_rows / orpcd_gicp_shard_*
  *       one GeneralizedICP.optimize with the source rows split over GPUs
  *                                          Optimizer/generalizedICP.py:59-70
+ *   orpcd_set_source_points / orpcd_icp_p2p_batch
+ *       Aligner.refine_registration(PointToPoint) Aligner/Aligner.py:319-364
+ *       -> o3d registration_icp             Aligner/Aligner.py:352-359
  *   orpcd_estimate_normals
  *       o3d EstimateNormals(KNN 20) inside registration_generalized_icp, and
  *       source_copy.estimate_normals(Hybrid) Optimizer/fastGlobalOptimizer.py:118-127
@@ -92,6 +95,22 @@ typedef struct {
 int orpcd_gicp_batch(orpcd_ctx* ctx, const double* R0, const double* t0, int32_t B,
                      const orpcd_gicp_params* params, double* T_out, double* rmse_out,
                      double* fitness_out, int32_t* iters_out, int64_t* ncorr_out);
+
+/* --------------------------------------- PointToPoint ICP refinement (§8f)
+ * Aligner.refine_registration (Aligner.py:319-364, icp_type="PointToPoint")
+ * -> o3d registration_icp(source, target, distance_threshold, init,
+ *    TransformationEstimationPointToPoint(), ICPConvergenceCriteria(max_iter)).
+ * orpcd_set_source_points: the source's search layout only (no covariances;
+ * a later orpcd_gicp_batch needs orpcd_set_source again).  The target comes
+ * from orpcd_set_target (epsilon < 0 skips its covariances).
+ * orpcd_icp_p2p_batch: B independent refinements, init[16*b] a 4x4 applied
+ * as Open3D applies `init` (column convention: p' = R p + t, row-major
+ * storage); T_out[16*b] = Open3D's result.transformation (init included).
+ * params->epsilon is ignored.                                               */
+int orpcd_set_source_points(orpcd_ctx* ctx, const double* xyz, int64_t n);
+int orpcd_icp_p2p_batch(orpcd_ctx* ctx, const double* init, int32_t B, const orpcd_gicp_params* params,
+                        double* T_out, double* rmse_out, double* fitness_out, int32_t* iters_out,
+                        int64_t* ncorr_out);
 
 /* ------------------------------------------------------- kernel-level entry
  * Radius-bounded exact 1-NN (d^2 < r^2 strictly, fp64 re-checked);

@@ -467,6 +467,104 @@ __device__ __forceinline__ void m4_mul(const double A[16], const double B[16], d
         }
 }
 
+// ------------------------------------------------ PointToPoint (Umeyama)
+// 3x3 SVD A = U diag(s) V^T by one-sided (Hestenes) Jacobi in fp64, singular
+// values descending; a vanished singular value's U column is completed
+// orthonormally.  Single-lane code (the solve runs one lane per start).
+__device__ inline void svd3_jacobi(const double A[3][3], double U[3][3], double s[3], double V[3][3]) {
+    double a[3][3], v[3][3] = {{1, 0, 0}, {0, 1, 0}, {0, 0, 1}};
+    for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j) a[i][j] = A[i][j];
+    for (int sweep = 0; sweep < 60; ++sweep) {
+        bool rotated = false;
+        for (int p = 0; p < 2; ++p)
+            for (int q = p + 1; q < 3; ++q) {
+                double al = 0, be = 0, ga = 0;
+                for (int i = 0; i < 3; ++i) {
+                    al += a[i][p] * a[i][p];
+                    be += a[i][q] * a[i][q];
+                    ga += a[i][p] * a[i][q];
+                }
+                if (ga == 0.0 || fabs(ga) <= 1e-15 * sqrt(al * be)) continue;
+                rotated = true;
+                const double zeta = (be - al) / (2.0 * ga);
+                const double t = (zeta >= 0 ? 1.0 : -1.0) / (fabs(zeta) + sqrt(1.0 + zeta * zeta));
+                const double c = 1.0 / sqrt(1.0 + t * t), sn = c * t;
+                for (int i = 0; i < 3; ++i) {
+                    const double x = a[i][p], y = a[i][q];
+                    a[i][p] = c * x - sn * y;
+                    a[i][q] = sn * x + c * y;
+                    const double vx = v[i][p], vy = v[i][q];
+                    v[i][p] = c * vx - sn * vy;
+                    v[i][q] = sn * vx + c * vy;
+                }
+            }
+        if (!rotated) break;
+    }
+    double nrm[3];
+    for (int j = 0; j < 3; ++j) nrm[j] = sqrt(a[0][j] * a[0][j] + a[1][j] * a[1][j] + a[2][j] * a[2][j]);
+    int ord[3] = {0, 1, 2};
+    for (int x = 0; x < 2; ++x)  // stable descending sort of 3
+        for (int y = 0; y < 2 - x; ++y)
+            if (nrm[ord[y + 1]] > nrm[ord[y]]) {
+                const int t = ord[y];
+                ord[y] = ord[y + 1];
+                ord[y + 1] = t;
+            }
+    for (int k = 0; k < 3; ++k) {
+        const int j = ord[k];
+        s[k] = nrm[j];
+        for (int i = 0; i < 3; ++i) {
+            V[i][k] = v[i][j];
+            U[i][k] = nrm[j] > 1e-300 ? a[i][j] / nrm[j] : 0.0;
+        }
+    }
+    if (!(s[0] > 1e-300)) {  // sigma == 0 (e.g. one pair): U = V = I as JacobiSVD leaves them
+        for (int i = 0; i < 3; ++i)
+            for (int k = 0; k < 3; ++k) U[i][k] = V[i][k] = i == k ? 1.0 : 0.0;
+    }
+    else if (!(s[1] > 1e-300)) {
+        const double c0[3] = {U[0][0], U[1][0], U[2][0]};
+        const double e[3] = {fabs(c0[0]) < 0.9 ? 1.0 : 0.0, fabs(c0[0]) < 0.9 ? 0.0 : 1.0, 0.0};
+        double c1[3];
+        cross3(c0, e, c1);
+        const double l = sqrt(c1[0] * c1[0] + c1[1] * c1[1] + c1[2] * c1[2]);
+        for (int i = 0; i < 3; ++i) U[i][1] = c1[i] / l;
+    }
+    if (s[0] > 1e-300 && !(s[2] > 1e-300)) {
+        const double c0[3] = {U[0][0], U[1][0], U[2][0]}, c1[3] = {U[0][1], U[1][1], U[2][1]};
+        double c2[3];
+        cross3(c0, c1, c2);
+        for (int i = 0; i < 3; ++i) U[i][2] = c2[i];
+    }
+}
+
+__device__ __forceinline__ double det3(const double a[3][3]) {
+    return a[0][0] * (a[1][1] * a[2][2] - a[1][2] * a[2][1]) - a[0][1] * (a[1][0] * a[2][2] - a[1][2] * a[2][0]) +
+           a[0][2] * (a[1][0] * a[2][1] - a[1][1] * a[2][0]);
+}
+
+// Eigen::umeyama(src, dst, with_scaling = false) from first moments:
+// s = [sum src (3), sum dst (3), sum dst_a src_b (9, row-major)], n pairs.
+// sigma = sum(dst src^T)/n - mean_dst mean_src^T; R = U diag(1,1,+-1) V^T;
+// t = mean_dst - R mean_src.  T: 4x4 row-major, column convention.
+__device__ inline void umeyama_from_moments(const double* s, double n, double T[16]) {
+    const double inv = 1.0 / n;
+    const double ms[3] = {s[0] * inv, s[1] * inv, s[2] * inv};
+    const double md[3] = {s[3] * inv, s[4] * inv, s[5] * inv};
+    double sig[3][3], U[3][3], V[3][3], sv[3];
+    for (int a = 0; a < 3; ++a)
+        for (int b = 0; b < 3; ++b) sig[a][b] = s[6 + 3 * a + b] * inv - md[a] * ms[b];
+    svd3_jacobi(sig, U, sv, V);
+    const double sgn = det3(U) * det3(V) < 0 ? -1.0 : 1.0;
+    for (int a = 0; a < 3; ++a) {
+        for (int b = 0; b < 3; ++b) T[4 * a + b] = U[a][0] * V[b][0] + U[a][1] * V[b][1] + sgn * U[a][2] * V[b][2];
+        T[4 * a + 3] = md[a] - (T[4 * a] * ms[0] + T[4 * a + 1] * ms[1] + T[4 * a + 2] * ms[2]);
+    }
+    T[12] = T[13] = T[14] = 0.0;
+    T[15] = 1.0;
+}
+
 // ------------------------------------------------------- wave reductions
 __device__ __forceinline__ double wave_sum(double v) {
 #pragma unroll

@@ -34,7 +34,7 @@
 //    block in a fixed order.  Because W is symmetric, J^T J = A^T (Cs+Ct)^-1 A
 //    and J^T r = A^T (Cs+Ct)^-1 d with A = [-[q]x | I]: no matrix square root
 //    is needed.
-//  * gicp_solve_kernel: per start, fixed-order reduction, convergence test,
+//  * icp_solve_kernel: per start, fixed-order reduction, convergence test,
 //    6x6 LDLT solve and pose update; then xform_queries_kernel writes the fp32
 //    queries of the next pass (fp64 transform, one rounding).
 #include "device_math.h"
@@ -442,6 +442,70 @@ __global__ __launch_bounds__(256) void gicp_accum_kernel(
     }
 }
 
+// PointToPoint accumulation (TransformationEstimationPointToPoint, Eigen::
+// umeyama): per correspondence the fp64 re-check as above, then the first
+// moments  sum src (0..2), sum dst (3..5), sum dst_a src_b (6..14), sum d^2
+// (27), count (28) in the partial layout of the GICP terms.
+constexpr int kP2PTerms = 17;
+__device__ __forceinline__ int p2p_slot(int v) { return v < 15 ? v : 12 + v; }  // 15 -> 27, 16 -> 28
+
+__global__ __launch_bounds__(256) void p2p_accum_kernel(const double* __restrict__ src, int N,
+                                                        const double* __restrict__ tgt64,
+                                                        const int32_t* __restrict__ active,
+                                                        const double* __restrict__ Qm,
+                                                        const int32_t* __restrict__ done, double r2,
+                                                        const unsigned long long* __restrict__ best,
+                                                        int32_t* __restrict__ prevnn, double* __restrict__ partial,
+                                                        int nblk) {
+    const int slot = active[blockIdx.y];
+    if (done[slot]) return;
+    __shared__ double red[4][kP2PTerms];
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    double acc[kP2PTerms];
+#pragma unroll
+    for (int v = 0; v < kP2PTerms; ++v) acc[v] = 0.0;
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i < N) {
+        const unsigned long long v = best[(size_t)slot * N + i];
+        const int j = v == kNone ? -1 : (int)(unsigned)(v & 0xffffffffu);
+        prevnn[(size_t)slot * N + i] = j >= 0 ? j : kNoMatch;
+        if (j >= 0) {
+            double Q[12];
+#pragma unroll
+            for (int t = 0; t < 12; ++t) Q[t] = Qm[12 * slot + t];
+            const double p[3] = {src[3 * i], src[3 * i + 1], src[3 * i + 2]};
+            double q[3];
+            xform(Q, p, q);
+            const double t3[3] = {tgt64[3 * j], tgt64[3 * j + 1], tgt64[3 * j + 2]};
+            const double d[3] = {q[0] - t3[0], q[1] - t3[1], q[2] - t3[2]};
+            const double d2 = d[0] * d[0] + d[1] * d[1] + d[2] * d[2];
+            if (d2 < r2) {
+#pragma unroll
+                for (int a = 0; a < 3; ++a) {
+                    acc[a] = q[a];
+                    acc[3 + a] = t3[a];
+#pragma unroll
+                    for (int b = 0; b < 3; ++b) acc[6 + 3 * a + b] = t3[a] * q[b];
+                }
+                acc[15] = d2;
+                acc[16] = 1.0;
+            }
+        }
+    }
+#pragma unroll
+    for (int v = 0; v < kP2PTerms; ++v) {
+        const double s = wave_sum(acc[v]);
+        if (lane == 0) red[wid][v] = s;
+    }
+    __syncthreads();
+    if (threadIdx.x < kNacc) {
+        double s = 0.0;
+        for (int v = 0; v < kP2PTerms; ++v)
+            if (p2p_slot(v) == (int)threadIdx.x) s = ((red[0][v] + red[1][v]) + red[2][v]) + red[3][v];
+        partial[((size_t)slot * nblk + blockIdx.x) * kPartialStride + threadIdx.x] = s;
+    }
+}
+
 struct SolveArgs {
     double* T;
     double* Q;
@@ -484,7 +548,8 @@ __global__ __launch_bounds__(64) void reduce_partials_kernel(const double* __res
         for (int v = 0; v < kNacc; ++v) sums[v] = s[v];
 }
 
-__global__ __launch_bounds__(64) void gicp_solve_kernel(const int32_t* __restrict__ active,
+template <int kEst>  // 0: GeneralizedICP, 1: PointToPoint
+__global__ __launch_bounds__(64) void icp_solve_kernel(const int32_t* __restrict__ active,
                                                         const double* __restrict__ partial, int nblk,
                                                         const double* __restrict__ sums_in, int64_t N, int pass,
                                                         int max_iter, double rel_fit, double rel_rmse, SolveArgs a) {
@@ -517,7 +582,9 @@ __global__ __launch_bounds__(64) void gicp_solve_kernel(const int32_t* __restric
     a.prev[2 * slot + 1] = rmse;
 
     double upd[16] = {1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1};
-    if (cnt > 0) {
+    if (cnt > 0 && kEst == 1) {
+        umeyama_from_moments(s, cnt, upd);
+    } else if (cnt > 0) {
         double JTJ[36], b[6];
         for (int r = 0; r < 6; ++r)
             for (int c = 0; c < 6; ++c) JTJ[6 * r + c] = r <= c ? s[ut(r, c)] : s[ut(c, r)];
@@ -626,6 +693,12 @@ hipError_t launch_gicp_pass(const orpcd_ctx* c, int nact, int pass, double r2, h
     if ((e = hipGetLastError()) != hipSuccess) return e;
     if (mid && (e = hipEventRecord(mid, s)) != hipSuccess) return e;
     const int ablk = accum_blocks(N);
+    if (c->est == kEstP2P) {
+        p2p_accum_kernel<<<dim3((unsigned)ablk, (unsigned)nact), 256, 0, s>>>(
+            c->src.xyz64.p, N, c->tgt.xyz64.p, c->active.p, c->Q.p, c->done.p, r2, c->best.p, c->prevnn.p,
+            c->partial.p, ablk);
+        return hipGetLastError();
+    }
     gicp_accum_kernel<<<dim3((unsigned)ablk, (unsigned)nact), 256, 0, s>>>(
         c->src.xyz64.p, c->scov.p, N, c->tgt.xyz64.p, c->tcov.p, c->active.p, c->Q.p, c->R.p, c->done.p, r2,
         c->best.p, c->prevnn.p, c->partial.p, ablk);
@@ -635,7 +708,8 @@ hipError_t launch_gicp_pass(const orpcd_ctx* c, int nact, int pass, double r2, h
 hipError_t launch_gicp_solve(const orpcd_ctx* c, int nact, int pass, const orpcd_gicp_params& p, hipStream_t s) {
     SolveArgs a{c->T.p,    c->Q.p,       c->R.p,        c->G.p,         c->prev.p,
                 c->done.p, c->out_fit.p, c->out_rmse.p, c->out_iters.p, c->out_ncorr.p};
-    gicp_solve_kernel<<<(unsigned)nact, 64, 0, s>>>(c->active.p, c->partial.p, accum_blocks(c->src.n), nullptr,
+    auto solve = c->est == kEstP2P ? icp_solve_kernel<1> : icp_solve_kernel<0>;
+    solve<<<(unsigned)nact, 64, 0, s>>>(c->active.p, c->partial.p, accum_blocks(c->src.n), nullptr,
                                                     c->src.n, pass, p.max_iteration, p.relative_fitness,
                                                     p.relative_rmse, a);
     hipError_t e = hipGetLastError();
@@ -653,7 +727,7 @@ hipError_t launch_gicp_solve_sums(const orpcd_ctx* c, const double* sums29, int6
                                   const orpcd_gicp_params& p, hipStream_t s) {
     SolveArgs a{c->T.p,    c->Q.p,       c->R.p,        c->G.p,         c->prev.p,
                 c->done.p, c->out_fit.p, c->out_rmse.p, c->out_iters.p, c->out_ncorr.p};
-    gicp_solve_kernel<<<1, 64, 0, s>>>(c->active.p, nullptr, 0, sums29, n_total, pass, p.max_iteration,
+    icp_solve_kernel<0><<<1, 64, 0, s>>>(c->active.p, nullptr, 0, sums29, n_total, pass, p.max_iteration,
                                        p.relative_fitness, p.relative_rmse, a);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;

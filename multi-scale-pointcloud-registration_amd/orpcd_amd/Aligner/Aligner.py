@@ -21,7 +21,7 @@ from typing import List, Tuple
 
 import numpy as np
 
-from .. import parallel
+from .. import _native, parallel
 from ..Optimizer.iOptimizer import IOptimizer
 from ..Preprocessor.Scalers.BaseScaler import BaseScaler
 from ..utils.constants import (
@@ -73,6 +73,8 @@ class Aligner:
         self._optimizer = optimizer
         # instrumentation (not in the reference): per-multistart records
         self.history: List[dict] = []
+        self.last_refine = None
+        self._refine_ctx = None  # device context for refine_registration when the optimizer has none
 
     # ----------------------------------------------------------------- RNG
     def initialize_rotation(self) -> Tuple[np.ndarray, np.ndarray]:
@@ -202,15 +204,31 @@ class Aligner:
 
     def refine_registration(self, source, target, initial_transform, max_iteration: int = __REFINER_MAX_ITER__,
                             distance_threshold: float = __REFINER_DISTANCE_THRESHOLD__, icp_type: str = "PointToPoint"):
-        """Aligner.py:319-364 — out of scope for this revision.
+        """Aligner.py:319-364 on the MI355X kernels (orpcd_icp_p2p_batch).
 
-        With the reference default ``PointToPlane`` Open3D 0.18 raises because the
-        target cloud carries no normals (Q5); this raises the same error type."""
+        As in the reference, ``initial_transform`` (the row-convention T that
+        align() composes) is handed to registration_icp, which applies it in
+        its own column convention, and Open3D's column-convention result is
+        returned (Q5).  ``PointToPlane`` raises as Open3D 0.18 does: the
+        target cloud built by create_cloud carries no normals."""
         if icp_type == "PointToPlane":
             raise RuntimeError("TransformationEstimationPointToPlane and TransformationEstimationColoredICP "
                                "require pre-computed normal vectors for target PointCloud.")
-        raise NotImplementedError("refine_registration(PointToPoint) is not built yet; "
-                                  "call align(..., refine_registration=False)")
+        if icp_type != "PointToPoint":
+            raise TypeError(f"registration_icp(): incompatible estimation_method {icp_type!r}")
+        if distance_threshold <= 0:
+            raise RuntimeError("Invalid max_correspondence_distance.")
+        ctx = getattr(self._optimizer, "context", None)
+        if ctx is None or not hasattr(ctx, "icp_p2p_batch"):
+            if self._refine_ctx is None:
+                self._refine_ctx = _native.default_context(None)
+            ctx = self._refine_ctx
+        ctx.set_target_points(np.asarray(target, dtype=np.float64))
+        ctx.set_source_points(np.asarray(source, dtype=np.float64))
+        r = ctx.icp_p2p_batch(np.asarray(initial_transform, dtype=np.float64)[None],
+                              max_correspondence_distance=distance_threshold, max_iteration=max_iteration)
+        self.last_refine = dict(fitness=float(r["fitness"][0]), iters=int(r["iters"][0]), ncorr=int(r["ncorr"][0]))
+        return r["T"][0].copy(), float(r["rmse"][0])
 
     def transfrom(self, source: np.ndarray) -> np.ndarray:
         """Aligner.py:367-394."""

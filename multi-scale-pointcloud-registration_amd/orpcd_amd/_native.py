@@ -49,7 +49,7 @@ EXPORTED = ("orpcd_abi_version", "orpcd_device_count", "orpcd_ctx_create", "orpc
             "orpcd_set_source_rows", "orpcd_gicp_shard_begin", "orpcd_gicp_shard_pass", "orpcd_gicp_shard_update",
             "orpcd_gicp_shard_result",
             "orpcd_nn1_radius", "orpcd_estimate_normals", "orpcd_fpfh", "orpcd_fpfh_from_normals", "orpcd_fgr", "orpcd_feature_nn",
-            "orpcd_fgr_optimize",
+            "orpcd_fgr_optimize", "orpcd_set_source_points", "orpcd_icp_p2p_batch",
             "orpcd_set_option",
             "orpcd_profiling", "orpcd_stats", "orpcd_reset_stats")
 
@@ -91,6 +91,9 @@ def load_library():
         L.orpcd_fgr_optimize.argtypes = [vp, _f64p, c_i64, _f64p, c_i64, c_dbl, ctypes.c_int32, c_dbl,
                                          ctypes.c_int32, ctypes.c_int32, ctypes.POINTER(FgrParams), _f64p, _f64p,
                                          _f64p, _i64p, _i64p]
+        L.orpcd_set_source_points.argtypes = [vp, _f64p, c_i64]
+        L.orpcd_icp_p2p_batch.argtypes = [vp, _f64p, ctypes.c_int32, ctypes.POINTER(GicpParams), _f64p, _f64p,
+                                          _f64p, _i32p, _i64p]
         L.orpcd_set_option.argtypes = [vp, ctypes.c_char_p, c_dbl]
         L.orpcd_profiling.argtypes = [vp, ctypes.c_int32]
         L.orpcd_stats.argtypes = [vp, _f64p, ctypes.c_int32]
@@ -162,15 +165,35 @@ class Context:
         key = (self._key(xyz), float(epsilon))
         if cache and key == self._target_key:
             return
+        self._target_key = None
         self._check(self._L.orpcd_set_target(self._h, xyz, len(xyz), float(epsilon)), "orpcd_set_target")
         self._target_key = key
 
+    def set_target_points(self, xyz: np.ndarray, cache: bool = True):
+        """The target's search layout (covariances skipped) for PointToPoint ICP."""
+        xyz = _c3(xyz)
+        k = self._key(xyz)
+        if cache and self._target_key is not None and self._target_key[0] == k:
+            return  # any current layout of the same points serves
+        self.set_target(xyz, -1.0, cache=False)
+
     def set_source(self, xyz: np.ndarray, cache: bool = True):
         xyz = _c3(xyz)
-        key = self._key(xyz)
+        key = (self._key(xyz), "cov")
         if cache and key == self._source_key:
             return
+        self._source_key = None
         self._check(self._L.orpcd_set_source(self._h, xyz, len(xyz)), "orpcd_set_source")
+        self._source_key = key
+
+    def set_source_points(self, xyz: np.ndarray, cache: bool = True):
+        """The source's search layout only (PointToPoint ICP needs no covariances)."""
+        xyz = _c3(xyz)
+        key = (self._key(xyz), "points")
+        if cache and self._source_key is not None and self._source_key[0] == key[0]:
+            return  # a source with covariances serves PointToPoint as well
+        self._source_key = None
+        self._check(self._L.orpcd_set_source_points(self._h, xyz, len(xyz)), "orpcd_set_source_points")
         self._source_key = key
 
     # --------------------------------------------------------------- GICP
@@ -187,6 +210,23 @@ class Context:
         ncorr = np.zeros(B, np.int64)
         self._check(self._L.orpcd_gicp_batch(self._h, R0.reshape(-1), t0.reshape(-1), B, ctypes.byref(p),
                                              T.reshape(-1), rmse, fit, iters, ncorr), "orpcd_gicp_batch")
+        return dict(T=T, rmse=rmse, fitness=fit, iters=iters, ncorr=ncorr)
+
+    def icp_p2p_batch(self, init: np.ndarray, max_correspondence_distance=0.5, max_iteration=200,
+                      relative_fitness=1e-6, relative_rmse=1e-6) -> dict:
+        """registration_icp(PointToPoint) of the current source / target from
+        each init[b] (column convention, applied as Open3D applies `init`).
+        Returns Open3D's result.transformation per init (init included)."""
+        init = np.ascontiguousarray(init, dtype=np.float64).reshape(-1, 4, 4)
+        B = init.shape[0]
+        p = GicpParams(float(max_correspondence_distance), int(max_iteration), float(relative_fitness),
+                       float(relative_rmse), -1.0)
+        T = np.zeros((B, 4, 4))
+        rmse, fit = np.zeros(B), np.zeros(B)
+        iters = np.zeros(B, np.int32)
+        ncorr = np.zeros(B, np.int64)
+        self._check(self._L.orpcd_icp_p2p_batch(self._h, init.reshape(-1), B, ctypes.byref(p), T.reshape(-1), rmse,
+                                                fit, iters, ncorr), "orpcd_icp_p2p_batch")
         return dict(T=T, rmse=rmse, fitness=fit, iters=iters, ncorr=ncorr)
 
     # ------------------------------------------ one start, rows over ranks

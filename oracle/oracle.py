@@ -69,6 +69,11 @@ def lib():
     L.oracle_fpfh_from_normals.argtypes = [_f64p, _f64p, c_i64, c_dbl, c_int, _f64p]
     L.oracle_fgr.argtypes = [_f64p, c_i64, _f64p, c_i64, _f64p, _f64p, c_dbl, c_dbl, c_dbl, c_int, c_int,
                                  c_int, ctypes.c_uint64, _f64p, _f64p, _f64p, _i64p, _i64p]
+    L.oracle_umeyama.argtypes = [_f64p, _f64p, c_i64, _f64p]
+    L.oracle_icp_p2p.argtypes = [_f64p, c_i64, _f64p, c_i64, c_dbl, _f64p, c_int, c_dbl, c_dbl, _f64p, _f64p,
+                                 _f64p, _i32p, _i64p]
+    L.oracle_sor.argtypes = [_f64p, c_i64, c_int, c_dbl, _i64p, _i64p, _f64p]
+    L.oracle_voxel_down_sample.argtypes = [_f64p, c_i64, c_dbl, vp, _i64p]
     _lib = L
     return L
 
@@ -181,6 +186,74 @@ def gicp_step(src, scov, tgt, tcov, corr_tgt):
                            np.ascontiguousarray(tcov, dtype=np.float64).reshape(-1), len(tgt),
                            np.ascontiguousarray(corr_tgt, dtype=np.int32), JTJ, JTr, upd)
     return JTJ.reshape(6, 6), JTr, upd.reshape(4, 4)
+
+
+def umeyama(src: np.ndarray, dst: np.ndarray) -> np.ndarray:
+    """Eigen::umeyama(src^T, dst^T, with_scaling=false) → 4x4 (column convention)."""
+    s, d = _c3(src), _c3(dst)
+    T = np.zeros(16)
+    lib().oracle_umeyama(s, d, len(s), T)
+    return T.reshape(4, 4)
+
+
+def icp_p2p(source: np.ndarray, target: np.ndarray, max_correspondence_distance: float = 0.5,
+            init: Optional[np.ndarray] = None, max_iteration: int = 200, relative_fitness: float = 1e-6,
+            relative_rmse: float = 1e-6) -> dict:
+    """registration_icp(..., TransformationEstimationPointToPoint()) restated
+    (O3D Registration.cpp RegistrationICP).  ``init`` is used as Open3D uses it
+    (column convention); returns Open3D's column-convention transformation."""
+    s, t = _c3(source), _c3(target)
+    init = np.eye(4) if init is None else np.ascontiguousarray(init, dtype=np.float64).reshape(4, 4)
+    T = np.zeros(16)
+    fit, rmse = np.zeros(1), np.zeros(1)
+    it = np.zeros(1, np.int32)
+    nc = np.zeros(1, np.int64)
+    rc = lib().oracle_icp_p2p(s, len(s), t, len(t), float(max_correspondence_distance), init.reshape(16).copy(),
+                              int(max_iteration), float(relative_fitness), float(relative_rmse), T, fit, rmse, it,
+                              nc)
+    if rc != 0:
+        raise ValueError("oracle_icp_p2p: invalid arguments")
+    return dict(T=T.reshape(4, 4), fitness=float(fit[0]), rmse=float(rmse[0]), iters=int(it[0]),
+                ncorr=int(nc[0]))
+
+
+def sor(cloud: np.ndarray, nb_neighbors: int = 64, std_ratio: float = 2.0):
+    """RemoveStatisticalOutliers restated → (kept indices (increasing), per-point mean distances)."""
+    p = _c3(cloud)
+    idx = np.empty(len(p), np.int64)
+    k = np.zeros(1, np.int64)
+    avg = np.empty(len(p))
+    if lib().oracle_sor(p, len(p), int(nb_neighbors), float(std_ratio), idx, k, avg) != 0:
+        raise ValueError("oracle_sor: illegal parameters")
+    return idx[:int(k[0])].copy(), avg
+
+
+def voxel_down_sample(cloud: np.ndarray, voxel_size: float, count_only: bool = False):
+    """VoxelDownSample restated; voxels in lexicographic (ix, iy, iz) order."""
+    p = _c3(cloud)
+    k = np.zeros(1, np.int64)
+    out = None if count_only else np.empty((len(p), 3))
+    ptr = out.ctypes.data_as(ctypes.c_void_p) if out is not None else None
+    if lib().oracle_voxel_down_sample(p, len(p), float(voxel_size), ptr, k) != 0:
+        raise ValueError("oracle_voxel_down_sample: voxel_size is too small")
+    return int(k[0]) if count_only else out[:int(k[0])].copy()
+
+
+def farthest_downsample(cloud: np.ndarray, sample_size: int, first: int) -> np.ndarray:
+    """farthestDownsampler.py:26-54 restated in numpy (``first`` = the
+    np.random.randint draw of :35): distances start at 1e6, per step the
+    Euclidean distance to the last chosen point (difference, squares summed
+    x,y,z in order, sqrt — scipy cdist), elementwise min, first argmax."""
+    c = np.ascontiguousarray(cloud, dtype=np.float64)
+    idx = np.zeros(sample_size, np.int64)
+    idx[0] = first
+    dist = np.full(len(c), 1e6)
+    for i in range(sample_size - 1):
+        d = c - c[idx[i]]
+        e = np.sqrt((d[:, 0] * d[:, 0] + d[:, 1] * d[:, 1]) + d[:, 2] * d[:, 2])
+        dist = np.minimum(e, dist)
+        idx[i + 1] = int(np.argmax(dist))
+    return idx
 
 
 def fpfh(points: np.ndarray, normal_radius: float = 0.1, normal_knn: int = 20, fpfh_radius: float = 0.1,
