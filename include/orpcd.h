@@ -21,6 +21,10 @@
  *   orpcd_set_source_points / orpcd_icp_p2p_batch
  *       Aligner.refine_registration(PointToPoint) Aligner/Aligner.py:319-364
  *       -> o3d registration_icp             Aligner/Aligner.py:352-359
+ *   orpcd_sor / orpcd_voxel_down_sample / orpcd_farthest_downsample
+ *       SOR.process                        Preprocessor/Outliers/sor.py:51-79
+ *       VoxelDownsampler.process           Preprocessor/Downsamplers/voxelDownsampler.py:77-126
+ *       FarthestDownsampler.process        Preprocessor/Downsamplers/farthestDownsampler.py:26-54
  *   orpcd_estimate_normals
  *       o3d EstimateNormals(KNN 20) inside registration_generalized_icp, and
  *       source_copy.estimate_normals(Hybrid) Optimizer/fastGlobalOptimizer.py:118-127
@@ -111,6 +115,25 @@ int orpcd_set_source_points(orpcd_ctx* ctx, const double* xyz, int64_t n);
 int orpcd_icp_p2p_batch(orpcd_ctx* ctx, const double* init, int32_t B, const orpcd_gicp_params* params,
                         double* T_out, double* rmse_out, double* fitness_out, int32_t* iters_out,
                         int64_t* ncorr_out);
+
+/* ------------------------------------------------ preprocessing (§8f)
+ * orpcd_sor: SOR.process (Preprocessor/Outliers/sor.py:51-79) -> o3d
+ *   remove_statistical_outlier(nb_neighbors, std_ratio): kept input indices
+ *   (increasing) in idx_out (n capacity), their count in *n_out; avg_out (n,
+ *   nullable) the per-point mean KNN distance.  nb_neighbors <= 64.
+ * orpcd_voxel_down_sample: VoxelDownsampler (Downsamplers/voxelDownsampler.py:
+ *   77-126) -> o3d voxel_down_sample(voxel_size): averaged points (n*3
+ *   capacity, nullable = count only), voxels in lexicographic (ix, iy, iz)
+ *   order (Open3D: unordered_map order); at most 2^21 voxels per axis.
+ * orpcd_farthest_downsample: FarthestDownsampler.process (Downsamplers/
+ *   farthestDownsampler.py:26-54): sample_size indices starting at `first`
+ *   (the caller's np.random.randint draw).                                  */
+int orpcd_sor(orpcd_ctx* ctx, const double* xyz, int64_t n, int32_t nb_neighbors, double std_ratio,
+              int64_t* idx_out, int64_t* n_out, double* avg_out);
+int orpcd_voxel_down_sample(orpcd_ctx* ctx, const double* xyz, int64_t n, double voxel_size, double* out_xyz,
+                            int64_t* n_out);
+int orpcd_farthest_downsample(orpcd_ctx* ctx, const double* xyz, int64_t n, int32_t sample_size, int64_t first,
+                              int64_t* idx_out);
 
 /* ------------------------------------------------------- kernel-level entry
  * Radius-bounded exact 1-NN (d^2 < r^2 strictly, fp64 re-checked);

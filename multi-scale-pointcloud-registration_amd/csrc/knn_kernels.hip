@@ -84,7 +84,7 @@ __global__ __launch_bounds__(256) void knn_tiles_kernel(
     const float4* __restrict__ thi, int ntiles, const float4* __restrict__ slo, const float4* __restrict__ shi,
     int nsuper, const double* __restrict__ in64, double r2, float margin, int kout, int out_input_order,
     double* __restrict__ rawcov6, int32_t* __restrict__ nbr_idx, double* __restrict__ nbr_d2,
-    int32_t* __restrict__ nbr_cnt) {
+    int32_t* __restrict__ nbr_cnt, double* __restrict__ mean_dist) {
     __shared__ double sx[4][kTile], sy[4][kTile], sz[4][kTile];
     __shared__ int32_t sid[4][kTile];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -222,6 +222,17 @@ __global__ __launch_bounds__(256) void knn_tiles_kernel(
             if (s < kout) nbr_d2[(size_t)o * kout + s] = s < c ? bd[s] : 0.0;
     }
     if (nbr_cnt) nbr_cnt[o] = c;
+    if (mean_dist) {  // SOR: mean of sqrt(d^2) over the neighbours, ascending (-1: empty search)
+        double m = -1.0;
+        if (c > 0) {
+            double sd = 0.0;
+#pragma unroll
+            for (int s = 0; s < K; ++s)
+                if (s < c) sd += sqrt(bd[s]);
+            m = sd / (double)c;
+        }
+        mean_dist[o] = m;
+    }
     if (!rawcov6) return;
     Sym3 C;
     if (c >= 3) {
@@ -266,14 +277,14 @@ __global__ __launch_bounds__(256) void knn_tiles_kernel(
 
 hipError_t launch_knn_tiles(const CloudLayout& L, const double* in64, int k, double radius, double margin,
                             bool out_input_order, double* rawcov6, int32_t* nbr_idx, double* nbr_d2,
-                            int32_t* nbr_cnt, hipStream_t s) {
+                            int32_t* nbr_cnt, hipStream_t s, double* mean_dist) {
     if (L.n <= 0) return hipSuccess;
     const double r2 = radius > 0 ? radius * radius : __builtin_huge_val();
     const dim3 grid((unsigned)((L.ntiles + 3) / 4));
 #define ORPCD_KNN_TILES(KK)                                                                                      \
     knn_tiles_kernel<KK><<<grid, 256, 0, s>>>(L.xyz64.p, L.perm.p, (int)L.n, L.tlo.p, L.thi.p, (int)L.ntiles,   \
                                               L.slo.p, L.shi.p, (int)L.nsuper, in64, r2, (float)margin, k,      \
-                                              out_input_order ? 1 : 0, rawcov6, nbr_idx, nbr_d2, nbr_cnt)
+                                              out_input_order ? 1 : 0, rawcov6, nbr_idx, nbr_d2, nbr_cnt, mean_dist)
     if (k <= 8)
         ORPCD_KNN_TILES(8);
     else if (k <= 20)

@@ -19,6 +19,7 @@ constexpr int kCWaves = 4;                     // waves per block
 constexpr int kCBlock = 64 * kCWaves;          // threads per block
 constexpr int kCBlockQ = kCBlock * kCQPT;      // queries per block (one start)
 constexpr int kNacc = 29;                      // JTJ(21) + JTr(6) + sum d2 + count
+constexpr int kEstGICP = 0, kEstP2P = 1;       // transformation estimation of a batch
 constexpr int kPartialStride = 32;             // doubles per block partial
 constexpr float kFarCoord = 1.0e18f;           // padding coordinate
 constexpr int kCounterSlots = 256;             // profiling counters: {tiles, max tiles/wave} per slot
@@ -121,6 +122,25 @@ struct FeatNNBufs {
     }
 };
 
+struct VoxelBufs {  // preprocessing scratch (voxel, SOR, FPS)
+    DevBuf<unsigned long long> key, ukey;
+    DevBuf<int32_t> idx, run;
+    DevBuf<unsigned char> tmp, flag;
+    DevBuf<double> xyz, out;
+    DevBuf<int64_t> idx64;
+    void release() {
+        flag.release();
+        idx64.release();
+        key.release();
+        ukey.release();
+        idx.release();
+        run.release();
+        tmp.release();
+        xyz.release();
+        out.release();
+    }
+};
+
 struct KernelStats {
     double launches = 0, ms = 0, pairs = 0, iterations = 0, passes = 0, tiles = 0, accum_ms = 0;
 };
@@ -141,6 +161,8 @@ struct orpcd_ctx {
     // source (set per align), Morton order
     orpcd::CloudLayout src;
     orpcd::DevBuf<double> sraw;     // N*6 raw KNN-20 neighbourhood covariance
+    bool src_cov = false;           // sraw holds the source's covariances (orpcd_set_source)
+    int est = orpcd::kEstGICP;      // estimation of the running batch (GICP / PointToPoint)
 
     // batch state (per start slot)
     orpcd::DevBuf<double> scov;     // B*N*6 posed-frame source covariance
@@ -191,6 +213,10 @@ struct orpcd_ctx {
         }
     } fgr;
 
+    // preprocessing (SOR, voxel, FPS)
+    orpcd::VoxelBufs vox;
+    int fps_blocks = 0;  // co-resident blocks of the cooperative FPS launch (one per CU)
+
     // profiling
     bool profiling = false;
     bool count_tiles = false;  // tile counters live only while timing (profiling / ORPCD_TRACE)
@@ -226,9 +252,19 @@ hipError_t build_layout(const double* dev_in64, int64_t n, const double bbox_lo[
 // knn_kernels.hip
 hipError_t launch_knn_tiles(const CloudLayout& L, const double* in64, int k, double radius, double margin,
                             bool out_input_order, double* rawcov6, int32_t* nbr_idx, double* nbr_d2,
-                            int32_t* nbr_cnt, hipStream_t s);
+                            int32_t* nbr_cnt, hipStream_t s, double* mean_dist = nullptr);
 hipError_t launch_normals_cov(const double* rawcov6, int64_t n, const double* Rc9, int nslots, double eps,
                               double* normals3, double* cov6, hipStream_t s);
+
+// prep_kernels.hip
+hipError_t launch_sor_select(const double* avg, int64_t n, double std_ratio, double* stats, unsigned char* flag,
+                             int32_t* kept, int32_t* nkept, DevBuf<unsigned char>& tmp, hipStream_t s);
+hipError_t launch_voxel_down_sample(const double* xyz, int64_t n, const double vmin[3], double vs, VoxelBufs& b,
+                                    double* out, int64_t* nvox_out, hipStream_t s);
+int fps_max_blocks(int device);
+int fps_points_per_thread(int64_t n, int max_blocks);
+hipError_t launch_fps(const double* xyz, int64_t n, int first, int k, int max_blocks, int64_t* out, double* bval,
+                      int32_t* bidx, unsigned* bar, hipStream_t s);
 
 // gicp_kernels.hip
 int accum_blocks(int64_t N);

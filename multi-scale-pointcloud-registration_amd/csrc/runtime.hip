@@ -340,10 +340,13 @@ int fgr_device(orpcd_ctx* c, const double* src, int64_t n, const double* tgt, in
 // Device state of a batch of B starts (pose = source @ R0_b + t0_b) before
 // pass 0: base poses, identity T, posed-frame source covariances, first
 // queries.  Host staging in c->h64 / c->h32 (layout used by gicp_batch).
-int batch_setup(orpcd_ctx* c, const double* R0, const double* t0, int B, const orpcd_gicp_params* p) {
+// init16 != null (PointToPoint refinement): base pose G_b = init16[b] (column
+// convention, as registration_icp applies `init`), no covariances.
+int batch_setup(orpcd_ctx* c, const double* R0, const double* t0, int B, const orpcd_gicp_params* p,
+                const double* init16 = nullptr) {
     const int64_t N = c->src.n;
     const int nblk = accum_blocks(N);
-    CTX_CHECK(c, c->scov.ensure((size_t)B * N * 6));
+    if (!init16) CTX_CHECK(c, c->scov.ensure((size_t)B * N * 6));
     CTX_CHECK(c, c->prevnn.ensure((size_t)B * N));
     CTX_CHECK(c, c->best.ensure((size_t)B * N));
     CTX_CHECK(c, c->q32.ensure((size_t)B * N));
@@ -373,13 +376,19 @@ int batch_setup(orpcd_ctx* c, const double* R0, const double* t0, int B, const o
     double* hFit = hPrev + (size_t)B * 2;
     double* hRmse = hFit + B;
     for (int b = 0; b < B; ++b) {
-        const double* r = R0 + 9 * b;
-        for (int i = 0; i < 3; ++i) {
-            for (int j = 0; j < 3; ++j) {
-                hG[12 * b + 4 * i + j] = r[3 * j + i];
-                hRc[9 * b + 3 * i + j] = r[3 * j + i];
+        if (init16) {
+            for (int t = 0; t < 12; ++t) hG[12 * b + t] = init16[16 * b + t];
+            for (int i = 0; i < 3; ++i)
+                for (int j = 0; j < 3; ++j) hRc[9 * b + 3 * i + j] = init16[16 * b + 4 * i + j];
+        } else {
+            const double* r = R0 + 9 * b;
+            for (int i = 0; i < 3; ++i) {
+                for (int j = 0; j < 3; ++j) {
+                    hG[12 * b + 4 * i + j] = r[3 * j + i];
+                    hRc[9 * b + 3 * i + j] = r[3 * j + i];
+                }
+                hG[12 * b + 4 * i + 3] = t0[3 * b + i];
             }
-            hG[12 * b + 4 * i + 3] = t0[3 * b + i];
         }
         for (int t = 0; t < 16; ++t) hT[16 * b + t] = (t % 5 == 0) ? 1.0 : 0.0;
         for (int t = 0; t < 12; ++t) hQ[12 * b + t] = hG[12 * b + t];
@@ -405,11 +414,15 @@ int batch_setup(orpcd_ctx* c, const double* R0, const double* t0, int B, const o
     CTX_CHECK(c, hipMemsetAsync(c->prevnn.p, 0xff, (size_t)B * N * 4, s));
 
     // posed-frame source covariances for every start (rigid equivariance)
-    CTX_CHECK(c, launch_normals_cov(c->sraw.p, N, c->scratch64c.p, B, p->epsilon, nullptr, c->scov.p, s));
+    c->est = init16 ? kEstP2P : kEstGICP;
+    if (!init16) CTX_CHECK(c, launch_normals_cov(c->sraw.p, N, c->scratch64c.p, B, p->epsilon, nullptr, c->scov.p, s));
     CTX_CHECK(c, launch_xform(c, B, p->max_correspondence_distance * p->max_correspondence_distance, s));
 
     return ORPCD_OK;
 }
+
+int run_passes(orpcd_ctx* c, int B, const orpcd_gicp_params* p, double* T_out, double* rmse_out,
+               double* fitness_out, int32_t* iters_out, int64_t* ncorr_out);
 
 }  // namespace
 
@@ -467,6 +480,7 @@ int orpcd_ctx_destroy(orpcd_ctx* c) {
     c->h64.release();
     c->h32.release();
     c->fgr.release();
+    c->vox.release();
     for (hipEvent_t e : c->ev_pool) (void)hipEventDestroy(e);
     (void)hipStreamDestroy(c->stream);
     delete c;
@@ -493,6 +507,7 @@ int orpcd_set_source(orpcd_ctx* c, const double* xyz, int64_t n) {
     CTX_REQUIRE(c, n < (int64_t)1 << 30, "set_source: too many points");
     CTX_REQUIRE(c, finite_cloud(xyz, n), "set_source: non-finite coordinates");
     CTX_CHECK(c, hipSetDevice(c->device));
+    c->src_cov = false;
     double margin = 0.0;
     int rc = upload_layout(c, xyz, n, c->src, true, &margin);
     if (rc) return rc;
@@ -500,6 +515,7 @@ int orpcd_set_source(orpcd_ctx* c, const double* xyz, int64_t n) {
     CTX_CHECK(c, launch_knn_tiles(c->src, c->scratch64a.p, 20, -1.0, margin, false, c->sraw.p, nullptr, nullptr,
                                   nullptr, c->stream));
     CTX_CHECK(c, hipStreamSynchronize(c->stream));
+    c->src_cov = true;
     return ORPCD_OK;
 }
 
@@ -519,8 +535,51 @@ int orpcd_gicp_batch(orpcd_ctx* c, const double* R0, const double* t0, int32_t B
         int rc = upload_target(c, host.data(), c->tgt.n, p->epsilon);
         if (rc) return rc;
     }
+    CTX_REQUIRE(c, c->src_cov, "gicp_batch: the source has no covariances (set it with orpcd_set_source)");
     int rc = batch_setup(c, R0, t0, B, p);
     if (rc) return rc;
+    return run_passes(c, B, p, T_out, rmse_out, fitness_out, iters_out, ncorr_out);
+}
+
+int orpcd_set_source_points(orpcd_ctx* c, const double* xyz, int64_t n) {
+    if (!c) return ORPCD_EINVAL;
+    CTX_REQUIRE(c, xyz && n > 0, "set_source_points: empty source cloud");
+    CTX_REQUIRE(c, n < (int64_t)1 << 30, "set_source_points: too many points");
+    CTX_REQUIRE(c, finite_cloud(xyz, n), "set_source_points: non-finite coordinates");
+    CTX_CHECK(c, hipSetDevice(c->device));
+    c->src_cov = false;
+    int rc = upload_layout(c, xyz, n, c->src, true);
+    if (rc) return rc;
+    CTX_CHECK(c, hipStreamSynchronize(c->stream));
+    return ORPCD_OK;
+}
+
+int orpcd_icp_p2p_batch(orpcd_ctx* c, const double* init, int32_t B, const orpcd_gicp_params* p, double* T_out,
+                        double* rmse_out, double* fitness_out, int32_t* iters_out, int64_t* ncorr_out) {
+    if (!c) return ORPCD_EINVAL;
+    CTX_REQUIRE(c, init && p && T_out && rmse_out, "icp_p2p_batch: null argument");
+    CTX_REQUIRE(c, B > 0, "icp_p2p_batch: B must be > 0");
+    CTX_REQUIRE(c, c->src.n > 0, "icp_p2p_batch: no source (call orpcd_set_source_points)");
+    CTX_REQUIRE(c, c->tgt.n > 0, "icp_p2p_batch: no target (call orpcd_set_target)");
+    CTX_REQUIRE(c, p->max_correspondence_distance > 0, "icp_p2p_batch: max_correspondence_distance must be > 0");
+    CTX_REQUIRE(c, p->max_iteration >= 0, "icp_p2p_batch: max_iteration must be >= 0");
+    for (int64_t t = 0; t < 16 * (int64_t)B; ++t) CTX_REQUIRE(c, std::isfinite(init[t]), "icp_p2p_batch: non-finite init");
+    CTX_CHECK(c, hipSetDevice(c->device));
+    int rc = batch_setup(c, nullptr, nullptr, B, p, init);
+    if (rc) return rc;
+    return run_passes(c, B, p, T_out, rmse_out, fitness_out, iters_out, ncorr_out);
+}
+
+}  // extern "C"
+
+namespace {
+
+// The ICP loop of every start of the batch set up by batch_setup (GICP or
+// PointToPoint by c->est).  GICP outputs T (the ICP transform relative to the
+// posed source); PointToPoint outputs T * G (registration_icp's result, init
+// included).
+int run_passes(orpcd_ctx* c, int B, const orpcd_gicp_params* p, double* T_out, double* rmse_out,
+               double* fitness_out, int32_t* iters_out, int64_t* ncorr_out) {
     const int64_t N = c->src.n;
     (void)N;
     double* hT = c->h64.p + (size_t)B * 12;
@@ -588,7 +647,18 @@ int orpcd_gicp_batch(orpcd_ctx* c, const double* R0, const double* t0, int32_t B
         nact = k;
     }
     // outputs
-    CTX_CHECK(c, hipMemcpyAsync(hT, c->T.p, (size_t)B * 16 * 8, hipMemcpyDeviceToHost, s));
+    if (c->est == kEstP2P) {
+        double* hQ = hT + (size_t)B * 16;
+        CTX_CHECK(c, hipMemcpyAsync(hQ, c->Q.p, (size_t)B * 12 * 8, hipMemcpyDeviceToHost, s));
+        CTX_CHECK(c, hipStreamSynchronize(s));
+        for (int b = 0; b < B; ++b) {
+            for (int t = 0; t < 12; ++t) hT[16 * b + t] = hQ[12 * b + t];
+            hT[16 * b + 12] = hT[16 * b + 13] = hT[16 * b + 14] = 0.0;
+            hT[16 * b + 15] = 1.0;
+        }
+    } else {
+        CTX_CHECK(c, hipMemcpyAsync(hT, c->T.p, (size_t)B * 16 * 8, hipMemcpyDeviceToHost, s));
+    }
     CTX_CHECK(c, hipMemcpyAsync(hFit, c->out_fit.p, (size_t)B * 8, hipMemcpyDeviceToHost, s));
     CTX_CHECK(c, hipMemcpyAsync(hRmse, c->out_rmse.p, (size_t)B * 8, hipMemcpyDeviceToHost, s));
     CTX_CHECK(c, hipMemcpyAsync(hIters, c->out_iters.p, (size_t)B * 4, hipMemcpyDeviceToHost, s));
@@ -613,6 +683,112 @@ int orpcd_gicp_batch(orpcd_ctx* c, const double* R0, const double* t0, int32_t B
     return ORPCD_OK;
 }
 
+}  // namespace
+
+extern "C" {
+
+int orpcd_sor(orpcd_ctx* c, const double* xyz, int64_t n, int32_t nb_neighbors, double std_ratio, int64_t* idx_out,
+              int64_t* n_out, double* avg_out) {
+    if (!c) return ORPCD_EINVAL;
+    CTX_REQUIRE(c, n_out && (idx_out || n == 0), "sor: null argument");
+    *n_out = 0;
+    CTX_REQUIRE(c, nb_neighbors >= 1 && std_ratio > 0,
+                "Illegal input parameters, the number of neighbors and standard deviation ratio must be positive.");
+    CTX_REQUIRE(c, nb_neighbors <= 64, "sor: nb_neighbors > 64 is not supported by the device KNN");
+    if (n == 0) return ORPCD_OK;
+    CTX_REQUIRE(c, xyz && n > 0 && n < (int64_t)1 << 30, "sor: bad cloud size");
+    CTX_REQUIRE(c, finite_cloud(xyz, n), "sor: non-finite coordinates");
+    CTX_CHECK(c, hipSetDevice(c->device));
+    hipStream_t s = c->stream;
+    double margin = 0.0;
+    int rc = upload_layout(c, xyz, n, c->aux, true, &margin);
+    if (rc) return rc;
+    CTX_CHECK(c, c->scratch64b.ensure((size_t)n));
+    CTX_CHECK(c, c->scratch64c.ensure(4));
+    CTX_CHECK(c, c->scratch32.ensure((size_t)n + 1));
+    CTX_CHECK(c, c->vox.flag.ensure((size_t)n));
+    double* avg = c->scratch64b.p;
+    CTX_CHECK(c, launch_knn_tiles(c->aux, c->scratch64a.p, nb_neighbors, -1.0, margin, true, nullptr, nullptr,
+                                  nullptr, nullptr, s, avg));
+    CTX_CHECK(c, launch_sor_select(avg, n, std_ratio, c->scratch64c.p, c->vox.flag.p, c->scratch32.p,
+                                   c->scratch32.p + n, c->vox.tmp, s));
+    int32_t k = 0;
+    CTX_CHECK(c, hipMemcpyAsync(&k, c->scratch32.p + n, 4, hipMemcpyDeviceToHost, s));
+    CTX_CHECK(c, hipStreamSynchronize(s));
+    std::vector<int32_t> kept((size_t)k);
+    if (k > 0) CTX_CHECK(c, hipMemcpyAsync(kept.data(), c->scratch32.p, (size_t)k * 4, hipMemcpyDeviceToHost, s));
+    if (avg_out) CTX_CHECK(c, hipMemcpyAsync(avg_out, avg, (size_t)n * 8, hipMemcpyDeviceToHost, s));
+    CTX_CHECK(c, hipStreamSynchronize(s));
+    for (int32_t i = 0; i < k; ++i) idx_out[i] = kept[i];
+    *n_out = k;
+    return ORPCD_OK;
+}
+
+int orpcd_voxel_down_sample(orpcd_ctx* c, const double* xyz, int64_t n, double voxel_size, double* out_xyz,
+                            int64_t* n_out) {
+    if (!c) return ORPCD_EINVAL;
+    CTX_REQUIRE(c, n_out, "voxel_down_sample: null argument");
+    *n_out = 0;
+    CTX_REQUIRE(c, voxel_size > 0.0, "voxel_size <= 0.");
+    if (n == 0) return ORPCD_OK;
+    CTX_REQUIRE(c, xyz && n > 0 && n < (int64_t)1 << 30, "voxel_down_sample: bad cloud size");
+    CTX_REQUIRE(c, finite_cloud(xyz, n), "voxel_down_sample: non-finite coordinates");
+    double lo[3], hi[3], vmin[3];
+    for (int a = 0; a < 3; ++a) lo[a] = hi[a] = xyz[a];
+    for (int64_t i = 1; i < n; ++i)
+        for (int a = 0; a < 3; ++a) {
+            lo[a] = std::min(lo[a], xyz[3 * i + a]);
+            hi[a] = std::max(hi[a], xyz[3 * i + a]);
+        }
+    double ext = 0.0, cells = 0.0;
+    for (int a = 0; a < 3; ++a) {
+        vmin[a] = lo[a] - voxel_size * 0.5;
+        ext = std::max(ext, (hi[a] + voxel_size * 0.5) - vmin[a]);
+        cells = std::max(cells, std::floor((hi[a] - vmin[a]) / voxel_size) + 1.0);
+    }
+    CTX_REQUIRE(c, !(voxel_size * 2147483647.0 < ext), "voxel_size is too small.");
+    CTX_REQUIRE(c, cells <= (double)(1 << 21), "voxel_down_sample: more than 2^21 voxels along an axis");
+    CTX_CHECK(c, hipSetDevice(c->device));
+    hipStream_t s = c->stream;
+    CTX_CHECK(c, c->vox.xyz.ensure((size_t)n * 3));
+    if (out_xyz) CTX_CHECK(c, c->vox.out.ensure((size_t)n * 3));
+    CTX_CHECK(c, hipMemcpyAsync(c->vox.xyz.p, xyz, (size_t)n * 24, hipMemcpyHostToDevice, s));
+    int64_t nv = 0;
+    CTX_CHECK(c, launch_voxel_down_sample(c->vox.xyz.p, n, vmin, voxel_size, c->vox, out_xyz ? c->vox.out.p : nullptr,
+                                          &nv, s));
+    if (out_xyz && nv > 0)
+        CTX_CHECK(c, hipMemcpyAsync(out_xyz, c->vox.out.p, (size_t)nv * 24, hipMemcpyDeviceToHost, s));
+    CTX_CHECK(c, hipStreamSynchronize(s));
+    *n_out = nv;
+    return ORPCD_OK;
+}
+
+int orpcd_farthest_downsample(orpcd_ctx* c, const double* xyz, int64_t n, int32_t sample_size, int64_t first,
+                              int64_t* idx_out) {
+    if (!c) return ORPCD_EINVAL;
+    CTX_REQUIRE(c, xyz && idx_out, "farthest_downsample: null argument");
+    CTX_REQUIRE(c, n > 0 && n < (int64_t)1 << 30, "farthest_downsample: empty cloud");
+    CTX_REQUIRE(c, sample_size > 0, "farthest_downsample: sample_size must be > 0");
+    CTX_REQUIRE(c, first >= 0 && first < n, "farthest_downsample: first index out of range");
+    CTX_REQUIRE(c, finite_cloud(xyz, n), "farthest_downsample: non-finite coordinates");
+    CTX_CHECK(c, hipSetDevice(c->device));
+    if (c->fps_blocks == 0) c->fps_blocks = fps_max_blocks(c->device);
+    CTX_REQUIRE(c, c->fps_blocks > 0 && fps_points_per_thread(n, c->fps_blocks) > 0,
+                "farthest_downsample: cloud too large for one cooperative launch");
+    hipStream_t s = c->stream;
+    CTX_CHECK(c, c->vox.xyz.ensure((size_t)n * 3));
+    CTX_CHECK(c, c->vox.idx64.ensure((size_t)sample_size));
+    CTX_CHECK(c, c->scratch64c.ensure((size_t)2 * c->fps_blocks));
+    CTX_CHECK(c, c->scratch32.ensure((size_t)2 * c->fps_blocks + 2));
+    CTX_CHECK(c, hipMemcpyAsync(c->vox.xyz.p, xyz, (size_t)n * 24, hipMemcpyHostToDevice, s));
+    CTX_CHECK(c, launch_fps(c->vox.xyz.p, n, (int)first, sample_size, c->fps_blocks, c->vox.idx64.p,
+                            c->scratch64c.p, c->scratch32.p, reinterpret_cast<unsigned*>(c->scratch32.p +
+                                                                                         2 * c->fps_blocks), s));
+    CTX_CHECK(c, hipMemcpyAsync(idx_out, c->vox.idx64.p, (size_t)sample_size * 8, hipMemcpyDeviceToHost, s));
+    CTX_CHECK(c, hipStreamSynchronize(s));
+    return ORPCD_OK;
+}
+
 int orpcd_set_source_rows(orpcd_ctx* c, const double* xyz, int64_t n, int64_t row_begin, int64_t row_end) {
     if (!c) return ORPCD_EINVAL;
     CTX_REQUIRE(c, xyz && n > 0, "set_source_rows: empty source cloud");
@@ -634,6 +810,7 @@ int orpcd_set_source_rows(orpcd_ctx* c, const double* xyz, int64_t n, int64_t ro
     CTX_CHECK(c, c->sraw.ensure((size_t)ns * 6));
     CTX_CHECK(c, launch_gather_rows(c->scratch64b.p, c->src.perm.p, row_begin, ns, 6, c->sraw.p, c->stream));
     CTX_CHECK(c, hipStreamSynchronize(c->stream));
+    c->src_cov = true;
     return ORPCD_OK;
 }
 
@@ -642,6 +819,7 @@ int orpcd_gicp_shard_begin(orpcd_ctx* c, const double* R0, const double* t0, con
     if (!c) return ORPCD_EINVAL;
     CTX_REQUIRE(c, R0 && t0 && p, "gicp_shard_begin: null argument");
     CTX_REQUIRE(c, c->src.n > 0 && c->tgt.n > 0, "gicp_shard_begin: set the target and the source rows first");
+    CTX_REQUIRE(c, c->src_cov, "gicp_shard_begin: the source rows have no covariances (orpcd_set_source_rows)");
     CTX_REQUIRE(c, n_total >= c->src.n, "gicp_shard_begin: n_total smaller than this rank's rows");
     CTX_REQUIRE(c, p->max_correspondence_distance > 0 && p->max_iteration >= 0 && p->epsilon >= 0,
                 "gicp_shard_begin: bad parameters");

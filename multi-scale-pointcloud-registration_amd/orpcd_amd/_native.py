@@ -50,6 +50,7 @@ EXPORTED = ("orpcd_abi_version", "orpcd_device_count", "orpcd_ctx_create", "orpc
             "orpcd_gicp_shard_result",
             "orpcd_nn1_radius", "orpcd_estimate_normals", "orpcd_fpfh", "orpcd_fpfh_from_normals", "orpcd_fgr", "orpcd_feature_nn",
             "orpcd_fgr_optimize", "orpcd_set_source_points", "orpcd_icp_p2p_batch",
+            "orpcd_sor", "orpcd_voxel_down_sample", "orpcd_farthest_downsample",
             "orpcd_set_option",
             "orpcd_profiling", "orpcd_stats", "orpcd_reset_stats")
 
@@ -94,6 +95,9 @@ def load_library():
         L.orpcd_set_source_points.argtypes = [vp, _f64p, c_i64]
         L.orpcd_icp_p2p_batch.argtypes = [vp, _f64p, ctypes.c_int32, ctypes.POINTER(GicpParams), _f64p, _f64p,
                                           _f64p, _i32p, _i64p]
+        L.orpcd_sor.argtypes = [vp, _f64p, c_i64, ctypes.c_int32, c_dbl, _i64p, _i64p, vp]
+        L.orpcd_voxel_down_sample.argtypes = [vp, _f64p, c_i64, c_dbl, vp, _i64p]
+        L.orpcd_farthest_downsample.argtypes = [vp, _f64p, c_i64, ctypes.c_int32, c_i64, _i64p]
         L.orpcd_set_option.argtypes = [vp, ctypes.c_char_p, c_dbl]
         L.orpcd_profiling.argtypes = [vp, ctypes.c_int32]
         L.orpcd_stats.argtypes = [vp, _f64p, ctypes.c_int32]
@@ -228,6 +232,39 @@ class Context:
         self._check(self._L.orpcd_icp_p2p_batch(self._h, init.reshape(-1), B, ctypes.byref(p), T.reshape(-1), rmse,
                                                 fit, iters, ncorr), "orpcd_icp_p2p_batch")
         return dict(T=T, rmse=rmse, fitness=fit, iters=iters, ncorr=ncorr)
+
+    # ------------------------------------------------------ preprocessing
+    def sor(self, xyz: np.ndarray, nb_neighbors: int = 64, std_ratio: float = 2.0, return_avg: bool = False):
+        """remove_statistical_outlier: kept indices (increasing) [, per-point mean distances]."""
+        xyz = _c3(xyz)
+        n = len(xyz)
+        idx = np.empty(max(n, 1), np.int64)
+        k = np.zeros(1, np.int64)
+        avg = np.empty(n) if return_avg else None
+        self._check(self._L.orpcd_sor(self._h, xyz if n else np.zeros((1, 3)), n, int(nb_neighbors),
+                                      float(std_ratio), idx, k, avg.ctypes.data_as(ctypes.c_void_p)
+                                      if avg is not None else None), "orpcd_sor")
+        kept = idx[:int(k[0])].copy()
+        return (kept, avg) if return_avg else kept
+
+    def voxel_down_sample(self, xyz: np.ndarray, voxel_size: float, count_only: bool = False):
+        """voxel_down_sample: averaged points, voxels in (ix, iy, iz) order (or their count)."""
+        xyz = _c3(xyz)
+        n = len(xyz)
+        k = np.zeros(1, np.int64)
+        out = None if count_only else np.empty((max(n, 1), 3))
+        self._check(self._L.orpcd_voxel_down_sample(self._h, xyz if n else np.zeros((1, 3)), n, float(voxel_size),
+                                                    out.ctypes.data_as(ctypes.c_void_p) if out is not None else None,
+                                                    k), "orpcd_voxel_down_sample")
+        return int(k[0]) if count_only else out[:int(k[0])].copy()
+
+    def farthest_downsample(self, xyz: np.ndarray, sample_size: int, first: int) -> np.ndarray:
+        """Farthest-point sampling from index ``first``: the chosen indices."""
+        xyz = _c3(xyz)
+        idx = np.empty(max(int(sample_size), 1), np.int64)
+        self._check(self._L.orpcd_farthest_downsample(self._h, xyz, len(xyz), int(sample_size), int(first), idx),
+                    "orpcd_farthest_downsample")
+        return idx[:int(sample_size)]
 
     # ------------------------------------------ one start, rows over ranks
     def set_source_rows(self, xyz: np.ndarray, row_begin: int, row_end: int):

@@ -5,6 +5,13 @@ import math
 __NB_NEIGHBOURS__ = 64
 __STD_RATIO__ = 2
 # downsamplers (constants.py:41-56)
+__RANDOM_SAMPLE_SIZE__ = 15000
+__FARTHEST_SAMPLE_SIZE__ = 10000
+__VOXEL_SAMPLE_SIZE__ = 2000
+__BASE_VOXEL_SIZE__ = 0.01
+__MIN_VOXEL_SIZE__ = 0.0001
+__DELTA__ = 0.01
+__EPS__ = 0.0005
 __SAMPLE_SIZE__ = 4096
 # fast global optimizer (constants.py:58-66)
 __DIVISION_FACTOR__ = 1.4
