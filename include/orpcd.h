@@ -215,7 +215,11 @@ int orpcd_fgr_optimize(orpcd_ctx* ctx, const double* src, int64_t n, const doubl
  *   "super_cull"    0/1: first culling level over 64-tile super-tiles
  *   "search_occupancy" 0 or 6: register budget of the search kernel
  *   "reseed"        0/1: representative seeding for queries that found no
- *                   target within radius in the previous pass             */
+ *                   target within radius in the previous pass
+ *   "search_kernel" 0: split search (default); 1: one workgroup per query
+ *                   group; 2: cull once per group + persistent scan.  All
+ *                   three return identical correspondences.
+ *   "scan_blocks"   persistent grid of search_kernel 2                    */
 int orpcd_set_option(orpcd_ctx* ctx, const char* key, double value);
 
 /* ------------------------------------------------------------ measurement

@@ -347,9 +347,581 @@ __global__ __launch_bounds__(kCBlock) __attribute__((amdgpu_waves_per_eu(6, 8)))
 #undef ORPCD_NN_SEARCH_ARGS
 
 // --------------------------------------------------------------------------
-// Accumulation kernel: one query per thread, grid = (blocks per start, running
-// starts).  Writes the chosen correspondence back as next pass's seed.
+// Cooperative search (default): one workgroup of W waves per group of 128
+// Morton-consecutive queries of one start.  The queries are transformed here
+// (fp64 pose -> fp32, bound from the previous correspondence; no separate
+// query kernel), the group's candidate tiles are culled ONCE (the waves split
+// the super-tiles; tiles whose box is within the group's worst bound are
+// appended to an LDS list), then the waves pull tiles from the list (LDS
+// cursor) and scan them; per query the waves' results merge by an LDS 64-bit
+// min on (masked d^2, Morton index) and one plain store writes best[].  The
+// answer is the same as nn_search_kernel's: among candidates whose d^2 agree
+// in the top 26 bits the lowest Morton index wins.
 // --------------------------------------------------------------------------
+constexpr int kGroupQ = 64 * kCQPT;  // queries per group (2 per lane)
+constexpr int kCoopMaxW = 16;        // waves per workgroup at most
+
+struct CoopShared {
+    float4 q[kGroupQ];                 // x, y, z, bound
+    unsigned long long mb[kGroupQ];    // merged (masked d^2 << 32 | Morton index)
+    int ncand, cursor;
+};
+
+__global__ __launch_bounds__(1024) void nn_search_coop_kernel(
+    const double* __restrict__ src, int N, const double* __restrict__ Qm, const int32_t* __restrict__ prevnn,
+    float r2s, int reseed, int seed_stride, const float4* __restrict__ p4, const float4* __restrict__ tlo,
+    const float4* __restrict__ thi, int ntiles, const float4* __restrict__ slo, const float4* __restrict__ shi,
+    int nsuper, const int32_t* __restrict__ active, const int32_t* __restrict__ done,
+    unsigned long long* __restrict__ best, unsigned long long* __restrict__ counters) {
+    const int slot = active[blockIdx.y];
+    if (done[slot]) return;
+    extern __shared__ uint16_t cand[];  // candidate tiles of the group (dynamic: ntiles entries)
+    __shared__ CoopShared sh;
+    __shared__ float stage_all[kCoopMaxW * 3 * kTile];  // per wave: x[64] | y[64] | z[64]
+    const int W = blockDim.x >> 6;
+    const int lane = threadIdx.x & 63, wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    float* stage = stage_all + wid * (3 * kTile);
+    const int g0 = blockIdx.x * kGroupQ;
+
+    // ---- 1. the group's queries (wave 0): q = fp32(Q p), bound from the seed
+    if (wid == 0) {
+        double Q[12];
+#pragma unroll
+        for (int t = 0; t < 12; ++t) Q[t] = Qm[12 * slot + t];
+#pragma unroll
+        for (int k = 0; k < kCQPT; ++k) {
+            const int i = g0 + lane + 64 * k;
+            float4 qv = make_float4(0.f, 0.f, 0.f, 0.f);  // bound 0: padding never takes anything
+            if (i < N) {
+                const double pp[3] = {src[3 * i], src[3 * i + 1], src[3 * i + 2]};
+                double q[3];
+                xform(Q, pp, q);
+                const float x = (float)q[0], y = (float)q[1], z = (float)q[2];
+                float bound = r2s;
+                const int jp = prevnn[(size_t)slot * N + i];
+                if (jp >= 0) {
+                    bound = fminf(bound, d2f(x, y, z, p4[jp]) * kSeedSlack + 1e-30f);
+                } else if (jp == kNoSeed || reseed) {
+                    for (int t = 0; t < ntiles; t += seed_stride)
+                        bound = fminf(bound, d2f(x, y, z, p4[t * kTile]) * kSeedSlack + 1e-30f);
+                }
+                qv = make_float4(x, y, z, bound);
+            }
+            sh.q[lane + 64 * k] = qv;
+            sh.mb[lane + 64 * k] = kNone;
+        }
+        if (lane == 0) {
+            sh.ncand = 0;
+            sh.cursor = 0;
+        }
+    }
+    __syncthreads();
+    float qx[kCQPT], qy[kCQPT], qz[kCQPT];
+    unsigned kk[kCQPT];  // running best key per query: masked d^2 | tile-local index
+    int jj[kCQPT];       // its Morton index (-1: the seed bound only)
+#pragma unroll
+    for (int k = 0; k < kCQPT; ++k) {
+        const float4 qv = sh.q[lane + 64 * k];
+        qx[k] = qv.x;
+        qy[k] = qv.y;
+        qz[k] = qv.z;
+        kk[k] = qv.w > 0.0f ? __float_as_uint(qv.w) : 0u;
+        jj[k] = -1;
+    }
+    const bool v0 = kk[0] != 0u, v1 = kk[1] != 0u;
+    const unsigned Wk = wave_umax((kk[0] > kk[1] ? kk[0] : kk[1]) & kKeyMask);
+    int visited = 0;
+    if (Wk != 0u) {  // block-uniform: every wave read the same queries
+        const float Wb = __uint_as_float(Wk);
+        const float inf = 3.0e38f;
+        const float lox = wave_fmin(fminf(v0 ? qx[0] : inf, v1 ? qx[1] : inf));
+        const float loy = wave_fmin(fminf(v0 ? qy[0] : inf, v1 ? qy[1] : inf));
+        const float loz = wave_fmin(fminf(v0 ? qz[0] : inf, v1 ? qz[1] : inf));
+        const float hix = wave_fmax(fmaxf(v0 ? qx[0] : -inf, v1 ? qx[1] : -inf));
+        const float hiy = wave_fmax(fmaxf(v0 ? qy[0] : -inf, v1 ? qy[1] : -inf));
+        const float hiz = wave_fmax(fmaxf(v0 ? qz[0] : -inf, v1 ? qz[1] : -inf));
+        auto box_gap = [&](float4 a, float4 b) {
+            const float dx = fmaxf(0.0f, fmaxf(a.x - hix, lox - b.x));
+            const float dy = fmaxf(0.0f, fmaxf(a.y - hiy, loy - b.y));
+            const float dz = fmaxf(0.0f, fmaxf(a.z - hiz, loz - b.z));
+            return dx * dx + dy * dy + dz * dz;
+        };
+        // ---- 2. culling, once per group: the waves split the surviving super-tiles
+        int surv = 0;  // survivors seen so far (block-uniform order)
+        for (int sb = 0; sb < nsuper; sb += 64) {
+            const int u = sb + lane;
+            const float sl = u < nsuper ? box_gap(slo[u], shi[u]) : inf;
+            unsigned long long smask = __ballot(sl < Wb);
+            while (smask) {
+                const int su = sb + __builtin_ctzll(smask);
+                smask &= smask - 1;
+                if ((surv++ % W) != wid) continue;
+                const int t = su * kSuper + lane;
+                const float lb = t < ntiles ? box_gap(tlo[t], thi[t]) : inf;
+                const unsigned long long tm = __ballot(lb < Wb);
+                if (tm == 0ull) continue;
+                int base = 0;
+                if (lane == 0) base = atomicAdd(&sh.ncand, __popcll(tm));
+                base = __shfl(base, 0, 64);
+                if (lb < Wb) cand[base + __builtin_amdgcn_mbcnt_hi((unsigned)(tm >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)tm, 0u))] = (uint16_t)t;
+            }
+        }
+    }
+    __syncthreads();
+    const int ncand = sh.ncand;
+    // ---- 3. scan: the waves pull candidate tiles from the list
+    auto take = [&]() -> int {
+        int k = 0;
+        if (lane == 0) k = atomicAdd(&sh.cursor, 1);
+        k = __builtin_amdgcn_readfirstlane(k);
+        return k < ncand ? __builtin_amdgcn_readfirstlane((int)cand[k]) : -1;
+    };
+    int tile = ncand > 0 ? take() : -1;
+    float4 pre = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (tile >= 0) pre = p4[tile * kTile + lane];
+    while (tile >= 0) {
+        const int nxt = take();
+        const float4 cur = pre;
+        if (nxt >= 0) pre = p4[nxt * kTile + lane];  // in flight while this tile is tested / scanned
+        const float4 a = tlo[tile], b = thi[tile];     // uniform address: scalar loads
+        const bool need = box_d2(qx[0], qy[0], qz[0], a.x, a.y, a.z, b.x, b.y, b.z) < __uint_as_float(kk[0] & kKeyMask) ||
+                          box_d2(qx[1], qy[1], qz[1], a.x, a.y, a.z, b.x, b.y, b.z) < __uint_as_float(kk[1] & kKeyMask);
+        if (__any(need)) {
+            stage[lane] = cur.x;
+            stage[64 + lane] = cur.y;
+            stage[128 + lane] = cur.z;
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            unsigned m0 = 0xFFFFFFFFu, m1 = 0xFFFFFFFFu;
+            const f2 qx0 = {qx[0], qx[0]}, qy0 = {qy[0], qy[0]}, qz0 = {qz[0], qz[0]};
+            const f2 qx1 = {qx[1], qx[1]}, qy1 = {qy[1], qy[1]}, qz1 = {qz[1], qz[1]};
+#pragma unroll 8
+            for (int c = 0; c < kTile; c += 2) {
+                const f2 tx = *reinterpret_cast<const f2*>(stage + c);
+                const f2 ty = *reinterpret_cast<const f2*>(stage + 64 + c);
+                const f2 tz = *reinterpret_cast<const f2*>(stage + 128 + c);
+                f2 dx = qx0 - tx, dy = qy0 - ty, dz = qz0 - tz;
+                f2 d0 = dx * dx;
+                d0 = pk_fma(dy, dy, d0);
+                d0 = pk_fma(dz, dz, d0);
+                dx = qx1 - tx;
+                dy = qy1 - ty;
+                dz = qz1 - tz;
+                f2 d1 = dx * dx;
+                d1 = pk_fma(dy, dy, d1);
+                d1 = pk_fma(dz, dz, d1);
+                const unsigned a0 = (__float_as_uint(d0.x) & kKeyMask) | (unsigned)c;
+                const unsigned c0 = (__float_as_uint(d0.y) & kKeyMask) | (unsigned)(c + 1);
+                const unsigned a1 = (__float_as_uint(d1.x) & kKeyMask) | (unsigned)c;
+                const unsigned c1 = (__float_as_uint(d1.y) & kKeyMask) | (unsigned)(c + 1);
+                m0 = min(m0, min(a0, c0));
+                m1 = min(m1, min(a1, c1));
+            }
+            asm volatile("" ::: "memory");  // all reads of this tile precede the next stage write
+            const int gi0 = tile * kTile + (int)(m0 & 63u), gi1 = tile * kTile + (int)(m1 & 63u);
+            if ((m0 & kKeyMask) < (kk[0] & kKeyMask) ||
+                ((m0 & kKeyMask) == (kk[0] & kKeyMask) && jj[0] >= 0 && gi0 < jj[0])) {
+                kk[0] = m0;
+                jj[0] = gi0;
+            }
+            if ((m1 & kKeyMask) < (kk[1] & kKeyMask) ||
+                ((m1 & kKeyMask) == (kk[1] & kKeyMask) && jj[1] >= 0 && gi1 < jj[1])) {
+                kk[1] = m1;
+                jj[1] = gi1;
+            }
+            ++visited;
+        }
+        tile = nxt;
+    }
+    // ---- 4. merge over the waves, one store per query
+#pragma unroll
+    for (int k = 0; k < kCQPT; ++k)
+        if (jj[k] >= 0)
+            atomicMin(&sh.mb[lane + 64 * k], ((unsigned long long)(kk[k] & kKeyMask) << 32) | (unsigned)jj[k]);
+    if (lane == 0 && counters) {
+        unsigned long long* cs = counters + kCounterStride * ((blockIdx.x * W + wid + blockIdx.y) % kCounterSlots);
+        atomicAdd(cs, (unsigned long long)visited);
+        atomicMax(cs + 1, (unsigned long long)visited);
+    }
+    __syncthreads();
+    if (wid == 0) {
+        unsigned long long* out = best + (size_t)slot * N;
+#pragma unroll
+        for (int k = 0; k < kCQPT; ++k) {
+            const int i = g0 + lane + 64 * k;
+            if (i < N) out[i] = sh.mb[lane + 64 * k];
+        }
+    }
+}
+
+// --------------------------------------------------------------------------
+// Two-phase search (default, search_kernel = 2).
+//
+// cull_groups_kernel: one wave per group of 128 Morton-consecutive queries of
+// one start.  It transforms the group's queries (fp64 pose -> fp32, bound
+// from the previous correspondence or the tile representatives), writes them
+// to q32, resets best[] for them, and culls the target ONCE for the group:
+// super-tiles and tiles against the group box and its worst bound, then each
+// surviving tile against every query's own bound.  The tiles that may hold a
+// query's nearest target become work items (start, group, tile), appended
+// contiguously per group to a global list.
+//
+// scan_items_kernel: a persistent grid of waves pulls chunks of items from
+// the list (one atomic per chunk).  Consecutive items of a group reuse the
+// queries already in registers; the next item's tile is loaded while the
+// current one is scanned (the same packed fp32 scan and 32-bit keys as
+// nn_search_kernel).  When a wave leaves a group it merges its answers into
+// best[] by a 64-bit atomicMin on (masked d^2, Morton index), so the result
+// is the same as the one-kernel searches': among candidates whose d^2 agree
+// in the top 26 bits the lowest Morton index wins.
+//
+// Work is thus culled once per group (not once per split wave) and spread
+// evenly over the waves, whatever the number of running starts.
+// --------------------------------------------------------------------------
+constexpr int kCullBuf = 128;  // per-wave LDS staging of a group's items
+
+// grid: (ceil(groups per start / 4), running starts); one wave per group.
+// Group gidx = blockIdx.y * gblk + group writes its candidate tiles to
+// items[gidx * ntiles ...] and their number to gcount[gidx] (0 when the
+// start is done or nothing can improve).
+__global__ __launch_bounds__(256) void cull_groups_kernel(
+    const double* __restrict__ src, int N, const double* __restrict__ Qm, const int32_t* __restrict__ prevnn,
+    float r2s, int reseed, int seed_stride, const float4* __restrict__ p4, const float4* __restrict__ tlo,
+    const float4* __restrict__ thi, int ntiles, const float4* __restrict__ slo, const float4* __restrict__ shi,
+    int nsuper, const int32_t* __restrict__ active, const int32_t* __restrict__ done, int gblk,
+    float4* __restrict__ q32, unsigned long long* __restrict__ best, unsigned* __restrict__ items,
+    unsigned* __restrict__ gcount) {
+    __shared__ unsigned buf[4][kCullBuf];
+    const int lane = threadIdx.x & 63, wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int group = blockIdx.x * 4 + wid;
+    if (group >= gblk) return;  // wave-uniform
+    const size_t gidx = (size_t)blockIdx.y * gblk + group;
+    const int slot = active[blockIdx.y];
+    const int g0 = group * kGroupQ;
+    if (done[slot]) {
+        if (lane == 0) gcount[gidx] = 0u;
+        return;
+    }
+    double Q[12];
+#pragma unroll
+    for (int t = 0; t < 12; ++t) Q[t] = Qm[12 * slot + t];
+    float qx[kCQPT], qy[kCQPT], qz[kCQPT], bound[kCQPT];
+#pragma unroll
+    for (int k = 0; k < kCQPT; ++k) {
+        const int i = g0 + lane + 64 * k;
+        float4 qv = make_float4(0.f, 0.f, 0.f, 0.f);  // bound 0: padding never takes anything
+        if (i < N) {
+            const double pp[3] = {src[3 * i], src[3 * i + 1], src[3 * i + 2]};
+            double q[3];
+            xform(Q, pp, q);
+            const float x = (float)q[0], y = (float)q[1], z = (float)q[2];
+            float b = r2s;
+            const int jp = prevnn[(size_t)slot * N + i];
+            if (jp >= 0) {
+                b = fminf(b, d2f(x, y, z, p4[jp]) * kSeedSlack + 1e-30f);
+            } else if (jp == kNoSeed || reseed) {
+                for (int t = 0; t < ntiles; t += seed_stride)
+                    b = fminf(b, d2f(x, y, z, p4[t * kTile]) * kSeedSlack + 1e-30f);
+            }
+            qv = make_float4(x, y, z, b);
+            q32[(size_t)slot * N + i] = qv;
+            best[(size_t)slot * N + i] = kNone;
+        }
+        qx[k] = qv.x;
+        qy[k] = qv.y;
+        qz[k] = qv.z;
+        bound[k] = qv.w;
+    }
+    const bool v0 = bound[0] > 0.0f, v1 = bound[1] > 0.0f;
+    const unsigned b0 = v0 ? __float_as_uint(bound[0]) : 0u, b1 = v1 ? __float_as_uint(bound[1]) : 0u;
+    const unsigned Wk = wave_umax(b0 > b1 ? b0 : b1);
+    unsigned* out = items + gidx * (size_t)ntiles;
+    unsigned* wb = buf[wid];
+    int nb = 0, nout = 0;  // staged in wb / written to out (wave-uniform)
+    auto flush = [&]() {
+        for (int k = lane; k < nb; k += 64) out[nout + k] = wb[k];
+        nout += nb;
+        nb = 0;
+    };
+    if (Wk != 0u) {
+        const float Wb = __uint_as_float(Wk);
+        const float inf = 3.0e38f;
+        const float lox = wave_fmin(fminf(v0 ? qx[0] : inf, v1 ? qx[1] : inf));
+        const float loy = wave_fmin(fminf(v0 ? qy[0] : inf, v1 ? qy[1] : inf));
+        const float loz = wave_fmin(fminf(v0 ? qz[0] : inf, v1 ? qz[1] : inf));
+        const float hix = wave_fmax(fmaxf(v0 ? qx[0] : -inf, v1 ? qx[1] : -inf));
+        const float hiy = wave_fmax(fmaxf(v0 ? qy[0] : -inf, v1 ? qy[1] : -inf));
+        const float hiz = wave_fmax(fmaxf(v0 ? qz[0] : -inf, v1 ? qz[1] : -inf));
+        auto box_gap = [&](float4 a, float4 b) {
+            const float dx = fmaxf(0.0f, fmaxf(a.x - hix, lox - b.x));
+            const float dy = fmaxf(0.0f, fmaxf(a.y - hiy, loy - b.y));
+            const float dz = fmaxf(0.0f, fmaxf(a.z - hiz, loz - b.z));
+            return dx * dx + dy * dy + dz * dz;
+        };
+        for (int sb = 0; sb < nsuper; sb += 64) {
+            const int u = sb + lane;
+            const float sl = u < nsuper ? box_gap(slo[u], shi[u]) : inf;
+            unsigned long long smask = __ballot(sl < Wb);
+            while (smask) {
+                const int su = sb + __builtin_ctzll(smask);
+                smask &= smask - 1;
+                const int t = su * kSuper + lane;
+                float4 a = make_float4(0.f, 0.f, 0.f, 0.f), b = a;
+                float lb = inf;
+                if (t < ntiles) {
+                    a = tlo[t];
+                    b = thi[t];
+                    lb = box_gap(a, b);
+                }
+                unsigned long long tm = __ballot(lb < Wb);
+                unsigned long long keep = 0ull;
+                while (tm) {  // per-query test of each surviving tile
+                    const int k = __builtin_ctzll(tm);
+                    tm &= tm - 1;
+                    const float lx = __uint_as_float(__builtin_amdgcn_readlane(__float_as_uint(a.x), k));
+                    const float ly = __uint_as_float(__builtin_amdgcn_readlane(__float_as_uint(a.y), k));
+                    const float lz = __uint_as_float(__builtin_amdgcn_readlane(__float_as_uint(a.z), k));
+                    const float hx = __uint_as_float(__builtin_amdgcn_readlane(__float_as_uint(b.x), k));
+                    const float hy = __uint_as_float(__builtin_amdgcn_readlane(__float_as_uint(b.y), k));
+                    const float hz = __uint_as_float(__builtin_amdgcn_readlane(__float_as_uint(b.z), k));
+                    const bool need = box_d2(qx[0], qy[0], qz[0], lx, ly, lz, hx, hy, hz) < bound[0] ||
+                                      box_d2(qx[1], qy[1], qz[1], lx, ly, lz, hx, hy, hz) < bound[1];
+                    if (__any(need)) keep |= 1ull << k;
+                }
+                if (keep == 0ull) continue;
+                const int nk = __popcll(keep);
+                if (nb + nk > kCullBuf) flush();
+                if ((keep >> lane) & 1ull)
+                    wb[nb + __builtin_amdgcn_mbcnt_hi((unsigned)(keep >> 32),
+                                                      __builtin_amdgcn_mbcnt_lo((unsigned)keep, 0u))] = (unsigned)t;
+                nb += nk;
+            }
+        }
+        flush();
+    }
+    if (lane == 0) gcount[gidx] = (unsigned)nout;
+}
+
+// Exclusive prefix of the G group counts -> offs[0..G] (offs[G] = total), one
+// workgroup of 1024 threads, each owning a contiguous run of counts.
+__global__ __launch_bounds__(1024) void items_prefix_kernel(const unsigned* __restrict__ gcount, int G,
+                                                            unsigned* __restrict__ offs) {
+    __shared__ unsigned part[1024];
+    const int t = threadIdx.x;
+    const int per = (G + 1023) / 1024;
+    const int lo = min(G, t * per), hi = min(G, lo + per);
+    unsigned sum = 0;
+    for (int g = lo; g < hi; ++g) sum += gcount[g];
+    part[t] = sum;
+    __syncthreads();
+    for (int off = 1; off < 1024; off <<= 1) {  // inclusive Hillis-Steele scan of the run sums
+        const unsigned v = t >= off ? part[t - off] : 0u;
+        __syncthreads();
+        part[t] += v;
+        __syncthreads();
+    }
+    unsigned run = t > 0 ? part[t - 1] : 0u;
+    for (int g = lo; g < hi; ++g) {
+        offs[g] = run;
+        run += gcount[g];
+    }
+    if (t == 1023) offs[G] = part[1023];
+}
+
+// Persistent scan: wave w owns items [w*total/W, (w+1)*total/W) of the
+// concatenated per-group lists; consecutive items of a group share the
+// queries in registers; answers merge into best[] by 64-bit atomicMin.
+__global__ __launch_bounds__(256) void scan_items_kernel(const float4* __restrict__ q32, int N, int gblk,
+                                                         const int32_t* __restrict__ active,
+                                                         const float4* __restrict__ p4,
+                                                         const float4* __restrict__ tlo,
+                                                         const float4* __restrict__ thi, int ntiles,
+                                                         const unsigned* __restrict__ items,
+                                                         const unsigned* __restrict__ offs, int G,
+                                                         unsigned long long* __restrict__ best,
+                                                         unsigned long long* __restrict__ counters) {
+    __shared__ float stage_all[4 * 3 * kTile];
+    const int lane = threadIdx.x & 63, wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    float* stage = stage_all + wid * (3 * kTile);
+    const unsigned total = offs[G];
+    const unsigned nw = gridDim.x * 4, w = blockIdx.x * 4 + wid;
+    const unsigned e0 = (unsigned)(((unsigned long long)total * w) / nw);
+    const unsigned e1 = (unsigned)(((unsigned long long)total * (w + 1)) / nw);
+    if (e0 >= e1) return;
+    // the group holding e0: last g with offs[g] <= e0 (binary search, uniform)
+    int lo = 0, hi = G - 1;
+    while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (offs[mid] <= e0) lo = mid;
+        else hi = mid - 1;
+    }
+    int g = lo;
+    unsigned gend = offs[g + 1];
+    int cur_g = -1, slot = 0, gbase = 0;
+    float qx[kCQPT], qy[kCQPT], qz[kCQPT];
+    unsigned kk[kCQPT];
+    int jj[kCQPT];
+#pragma unroll
+    for (int k = 0; k < kCQPT; ++k) {
+        qx[k] = qy[k] = qz[k] = 0.f;
+        kk[k] = 0u;
+        jj[k] = -1;
+    }
+    auto merge = [&]() {
+        if (cur_g < 0) return;
+#pragma unroll
+        for (int k = 0; k < kCQPT; ++k) {
+            const int i = gbase + lane + 64 * k;
+            if (jj[k] >= 0 && i < N)
+                atomicMin(best + (size_t)slot * N + i, ((unsigned long long)(kk[k] & kKeyMask) << 32) | (unsigned)jj[k]);
+        }
+    };
+    // item e -> (group, tile); advances g past empty groups
+    auto tile_of = [&](unsigned e) -> int {
+        while (e >= gend) {
+            ++g;
+            gend = offs[g + 1];
+        }
+        return (int)items[(size_t)g * ntiles + (e - offs[g])];
+    };
+    int visited = 0;
+    int tile = tile_of(e0), tg = g;
+    float4 pre = p4[tile * kTile + lane];
+    for (unsigned e = e0; e < e1; ++e) {
+        const int ctile = tile, cg = tg;
+        const float4 cur = pre;
+        if (e + 1 < e1) {
+            tile = tile_of(e + 1);
+            tg = g;
+            pre = p4[tile * kTile + lane];  // in flight during this tile
+        }
+        if (cg != cur_g) {
+            merge();
+            cur_g = cg;
+            slot = active[cg / gblk];
+            gbase = (cg % gblk) * kGroupQ;
+#pragma unroll
+            for (int q = 0; q < kCQPT; ++q) {
+                const int i = gbase + lane + 64 * q;
+                const float4 qv = i < N ? q32[(size_t)slot * N + i] : make_float4(0.f, 0.f, 0.f, 0.f);
+                qx[q] = qv.x;
+                qy[q] = qv.y;
+                qz[q] = qv.z;
+                kk[q] = qv.w > 0.0f ? __float_as_uint(qv.w) : 0u;
+                jj[q] = -1;
+            }
+        }
+        const float4 a = tlo[ctile], b = thi[ctile];
+        const bool need =
+            box_d2(qx[0], qy[0], qz[0], a.x, a.y, a.z, b.x, b.y, b.z) < __uint_as_float(kk[0] & kKeyMask) ||
+            box_d2(qx[1], qy[1], qz[1], a.x, a.y, a.z, b.x, b.y, b.z) < __uint_as_float(kk[1] & kKeyMask);
+        if (!__any(need)) continue;
+        stage[lane] = cur.x;
+        stage[64 + lane] = cur.y;
+        stage[128 + lane] = cur.z;
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        unsigned m0 = 0xFFFFFFFFu, m1 = 0xFFFFFFFFu;
+        const f2 qx0 = {qx[0], qx[0]}, qy0 = {qy[0], qy[0]}, qz0 = {qz[0], qz[0]};
+        const f2 qx1 = {qx[1], qx[1]}, qy1 = {qy[1], qy[1]}, qz1 = {qz[1], qz[1]};
+#pragma unroll 8
+        for (int c = 0; c < kTile; c += 2) {
+            const f2 tx = *reinterpret_cast<const f2*>(stage + c);
+            const f2 ty = *reinterpret_cast<const f2*>(stage + 64 + c);
+            const f2 tz = *reinterpret_cast<const f2*>(stage + 128 + c);
+            f2 dx = qx0 - tx, dy = qy0 - ty, dz = qz0 - tz;
+            f2 d0 = dx * dx;
+            d0 = pk_fma(dy, dy, d0);
+            d0 = pk_fma(dz, dz, d0);
+            dx = qx1 - tx;
+            dy = qy1 - ty;
+            dz = qz1 - tz;
+            f2 d1 = dx * dx;
+            d1 = pk_fma(dy, dy, d1);
+            d1 = pk_fma(dz, dz, d1);
+            const unsigned a0 = (__float_as_uint(d0.x) & kKeyMask) | (unsigned)c;
+            const unsigned c0k = (__float_as_uint(d0.y) & kKeyMask) | (unsigned)(c + 1);
+            const unsigned a1 = (__float_as_uint(d1.x) & kKeyMask) | (unsigned)c;
+            const unsigned c1k = (__float_as_uint(d1.y) & kKeyMask) | (unsigned)(c + 1);
+            m0 = min(m0, min(a0, c0k));
+            m1 = min(m1, min(a1, c1k));
+        }
+        asm volatile("" ::: "memory");  // all reads of this tile precede the next stage write
+        const int gi0 = ctile * kTile + (int)(m0 & 63u), gi1 = ctile * kTile + (int)(m1 & 63u);
+        if ((m0 & kKeyMask) < (kk[0] & kKeyMask) ||
+            ((m0 & kKeyMask) == (kk[0] & kKeyMask) && jj[0] >= 0 && gi0 < jj[0])) {
+            kk[0] = m0;
+            jj[0] = gi0;
+        }
+        if ((m1 & kKeyMask) < (kk[1] & kKeyMask) ||
+            ((m1 & kKeyMask) == (kk[1] & kKeyMask) && jj[1] >= 0 && gi1 < jj[1])) {
+            kk[1] = m1;
+            jj[1] = gi1;
+        }
+        ++visited;
+    }
+    merge();
+    if (lane == 0 && counters) {
+        unsigned long long* cs = counters + kCounterStride * ((blockIdx.x * 4 + wid) % kCounterSlots);
+        atomicAdd(cs, (unsigned long long)visited);
+        atomicMax(cs + 1, (unsigned long long)visited);
+    }
+}
+
+size_t coop_smem_bytes(int W, int64_t ntiles) { return (size_t)ntiles * 2 + 16; }
+
+// --------------------------------------------------------------------------
+// Accumulation kernels: kAccQ queries per thread (grid = (blocks per start,
+// running starts), 256 threads), each thread summing its queries' terms in
+// registers; then a fixed-order block reduction (DPP within rows of 16 lanes,
+// the four row sums, then the four waves) into one partial per block.  The
+// chosen correspondence is written back as the next pass's seed.
+// --------------------------------------------------------------------------
+constexpr int kAccQ = 4;
+constexpr int kAccBlockQ = 256 * kAccQ;
+
+template <int Ctrl>
+__device__ __forceinline__ double dpp_f64(double v) {
+    const long long b = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_update_dpp(0, (int)b, Ctrl, 0xf, 0xf, false);
+    const int hi = __builtin_amdgcn_update_dpp(0, (int)(b >> 32), Ctrl, 0xf, 0xf, false);
+    return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+}
+
+// wave sum in a fixed order (identical in every lane): rows of 16 by DPP, then
+// (row0 + row1) + (row2 + row3)
+__device__ __forceinline__ double wave_sum_fixed(double v) {
+    v += dpp_f64<0xb1>(v);   // quad_perm [1,0,3,2]
+    v += dpp_f64<0x4e>(v);   // quad_perm [2,3,0,1]
+    v += dpp_f64<0x141>(v);  // row_half_mirror
+    v += dpp_f64<0x140>(v);  // row_mirror
+    auto rl = [&](int k) {
+        const long long b = __double_as_longlong(v);
+        const unsigned lo = __builtin_amdgcn_readlane((unsigned)b, k);
+        const unsigned hi = __builtin_amdgcn_readlane((unsigned)(b >> 32), k);
+        return __longlong_as_double(((long long)hi << 32) | lo);
+    };
+    return (rl(0) + rl(16)) + (rl(32) + rl(48));
+}
+
+// Block reduction of NV per-thread values into partial[slot, block][slot_of(v)].
+template <int NV, typename SlotOf>
+__device__ __forceinline__ void block_partial(const double* acc, double (*red)[NV], SlotOf slot_of,
+                                              double* __restrict__ out) {
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+#pragma unroll
+    for (int v = 0; v < NV; ++v) {
+        const double s = wave_sum_fixed(acc[v]);
+        if (lane == 0) red[wid][v] = s;
+    }
+    __syncthreads();
+    if (threadIdx.x < kNacc) {
+        double s = 0.0;
+#pragma unroll
+        for (int v = 0; v < NV; ++v)
+            if (slot_of(v) == (int)threadIdx.x) s = ((red[0][v] + red[1][v]) + red[2][v]) + red[3][v];
+        out[threadIdx.x] = s;
+    }
+}
+
 __global__ __launch_bounds__(256) void gicp_accum_kernel(
     const double* __restrict__ src, const double* __restrict__ scov, int N, const double* __restrict__ tgt64,
     const double* __restrict__ tcov, const int32_t* __restrict__ active, const double* __restrict__ Qm,
@@ -359,87 +931,75 @@ __global__ __launch_bounds__(256) void gicp_accum_kernel(
     const int slot = active[blockIdx.y];
     if (done[slot]) return;
     __shared__ double red[4][kNacc];
-    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     double acc[kNacc];
 #pragma unroll
     for (int v = 0; v < kNacc; ++v) acc[v] = 0.0;
-    const int i = blockIdx.x * 256 + threadIdx.x;
-    if (i < N) {
+    double Q[12], R[9];
+#pragma unroll
+    for (int t = 0; t < 12; ++t) Q[t] = Qm[12 * slot + t];
+#pragma unroll
+    for (int t = 0; t < 9; ++t) R[t] = Rm[9 * slot + t];
+    for (int k = 0; k < kAccQ; ++k) {
+        const int i = blockIdx.x * kAccBlockQ + k * 256 + threadIdx.x;
+        if (i >= N) break;
         const unsigned long long v = best[(size_t)slot * N + i];
         const int j = v == kNone ? -1 : (int)(unsigned)(v & 0xffffffffu);
         prevnn[(size_t)slot * N + i] = j >= 0 ? j : kNoMatch;
-        if (j >= 0) {
-            double Q[12], R[9];
+        if (j < 0) continue;
+        const double p[3] = {src[3 * i], src[3 * i + 1], src[3 * i + 2]};
+        double q[3];
+        xform(Q, p, q);
+        const double d[3] = {q[0] - tgt64[3 * j], q[1] - tgt64[3 * j + 1], q[2] - tgt64[3 * j + 2]};
+        const double d2 = d[0] * d[0] + d[1] * d[1] + d[2] * d[2];
+        if (!(d2 < r2)) continue;
+        const double* cs6 = scov + ((size_t)slot * N + i) * 6;
+        const double* ct6 = tcov + (size_t)j * 6;
+        Sym3 Cs{cs6[0], cs6[1], cs6[2], cs6[3], cs6[4], cs6[5]};
+        Cs = rotate_sym(R, Cs);
+        const Sym3 Mm{Cs.xx + ct6[0], Cs.xy + ct6[1], Cs.xz + ct6[2], Cs.yy + ct6[3], Cs.yz + ct6[4],
+                      Cs.zz + ct6[5]};
+        const Sym3 P = sym3_inverse(Mm);
+        const double Pm[3][3] = {{P.xx, P.xy, P.xz}, {P.xy, P.yy, P.yz}, {P.xz, P.yz, P.zz}};
+        // g = P d ; JTr = [q x g ; g]
+        const double g[3] = {P.xx * d[0] + P.xy * d[1] + P.xz * d[2], P.xy * d[0] + P.yy * d[1] + P.yz * d[2],
+                             P.xz * d[0] + P.yz * d[1] + P.zz * d[2]};
+        double qg[3];
+        cross3(q, g, qg);
+        acc[21] += qg[0];
+        acc[22] += qg[1];
+        acc[23] += qg[2];
+        acc[24] += g[0];
+        acc[25] += g[1];
+        acc[26] += g[2];
+        // SP = [q]x P (column b = q x P[:,b]);  TL row a = q x SP[a,:]
+        double SP[3][3];
 #pragma unroll
-            for (int t = 0; t < 12; ++t) Q[t] = Qm[12 * slot + t];
-#pragma unroll
-            for (int t = 0; t < 9; ++t) R[t] = Rm[9 * slot + t];
-            const double p[3] = {src[3 * i], src[3 * i + 1], src[3 * i + 2]};
-            double q[3];
-            xform(Q, p, q);
-            const double d[3] = {q[0] - tgt64[3 * j], q[1] - tgt64[3 * j + 1], q[2] - tgt64[3 * j + 2]};
-            const double d2 = d[0] * d[0] + d[1] * d[1] + d[2] * d[2];
-            if (d2 < r2) {
-                const double* cs6 = scov + ((size_t)slot * N + i) * 6;
-                const double* ct6 = tcov + (size_t)j * 6;
-                Sym3 Cs{cs6[0], cs6[1], cs6[2], cs6[3], cs6[4], cs6[5]};
-                Cs = rotate_sym(R, Cs);
-                const Sym3 Mm{Cs.xx + ct6[0], Cs.xy + ct6[1], Cs.xz + ct6[2], Cs.yy + ct6[3], Cs.yz + ct6[4],
-                              Cs.zz + ct6[5]};
-                const Sym3 P = sym3_inverse(Mm);
-                const double Pm[3][3] = {{P.xx, P.xy, P.xz}, {P.xy, P.yy, P.yz}, {P.xz, P.yz, P.zz}};
-                // g = P d ; JTr = [q x g ; g]
-                const double g[3] = {P.xx * d[0] + P.xy * d[1] + P.xz * d[2],
-                                     P.xy * d[0] + P.yy * d[1] + P.yz * d[2],
-                                     P.xz * d[0] + P.yz * d[1] + P.zz * d[2]};
-                double qg[3];
-                cross3(q, g, qg);
-                acc[21] = qg[0];
-                acc[22] = qg[1];
-                acc[23] = qg[2];
-                acc[24] = g[0];
-                acc[25] = g[1];
-                acc[26] = g[2];
-                // SP = [q]x P (column b = q x P[:,b]);  TL row a = q x SP[a,:]
-                double SP[3][3];
-#pragma unroll
-                for (int b = 0; b < 3; ++b) {
-                    const double col[3] = {Pm[0][b], Pm[1][b], Pm[2][b]};
-                    double c3[3];
-                    cross3(q, col, c3);
-                    SP[0][b] = c3[0];
-                    SP[1][b] = c3[1];
-                    SP[2][b] = c3[2];
-                }
-#pragma unroll
-                for (int a = 0; a < 3; ++a) {
-                    double tl[3];
-                    cross3(q, SP[a], tl);
-#pragma unroll
-                    for (int b = a; b < 3; ++b) acc[ut(a, b)] = tl[b];
-#pragma unroll
-                    for (int b = 0; b < 3; ++b) acc[ut(a, 3 + b)] = SP[a][b];
-                }
-#pragma unroll
-                for (int a = 0; a < 3; ++a)
-#pragma unroll
-                    for (int b = a; b < 3; ++b) acc[ut(3 + a, 3 + b)] = Pm[a][b];
-                acc[27] = d2;
-                acc[28] = 1.0;
-            }
+        for (int b = 0; b < 3; ++b) {
+            const double col[3] = {Pm[0][b], Pm[1][b], Pm[2][b]};
+            double c3[3];
+            cross3(q, col, c3);
+            SP[0][b] = c3[0];
+            SP[1][b] = c3[1];
+            SP[2][b] = c3[2];
         }
-    }
-    // fixed-order block reduction -> one partial per block
 #pragma unroll
-    for (int v = 0; v < kNacc; ++v) {
-        const double s = wave_sum(acc[v]);
-        if (lane == 0) red[wid][v] = s;
+        for (int a = 0; a < 3; ++a) {
+            double tl[3];
+            cross3(q, SP[a], tl);
+#pragma unroll
+            for (int b = a; b < 3; ++b) acc[ut(a, b)] += tl[b];
+#pragma unroll
+            for (int b = 0; b < 3; ++b) acc[ut(a, 3 + b)] += SP[a][b];
+        }
+#pragma unroll
+        for (int a = 0; a < 3; ++a)
+#pragma unroll
+            for (int b = a; b < 3; ++b) acc[ut(3 + a, 3 + b)] += Pm[a][b];
+        acc[27] += d2;
+        acc[28] += 1.0;
     }
-    __syncthreads();
-    if (threadIdx.x < kNacc) {
-        const double s = ((red[0][threadIdx.x] + red[1][threadIdx.x]) + red[2][threadIdx.x]) + red[3][threadIdx.x];
-        partial[((size_t)slot * nblk + blockIdx.x) * kPartialStride + threadIdx.x] = s;
-    }
+    block_partial<kNacc>(acc, red, [](int v) { return v; },
+                         partial + ((size_t)slot * nblk + blockIdx.x) * kPartialStride);
 }
 
 // PointToPoint accumulation (TransformationEstimationPointToPoint, Eigen::
@@ -460,50 +1020,37 @@ __global__ __launch_bounds__(256) void p2p_accum_kernel(const double* __restrict
     const int slot = active[blockIdx.y];
     if (done[slot]) return;
     __shared__ double red[4][kP2PTerms];
-    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     double acc[kP2PTerms];
 #pragma unroll
     for (int v = 0; v < kP2PTerms; ++v) acc[v] = 0.0;
-    const int i = blockIdx.x * 256 + threadIdx.x;
-    if (i < N) {
+    double Q[12];
+#pragma unroll
+    for (int t = 0; t < 12; ++t) Q[t] = Qm[12 * slot + t];
+    for (int k = 0; k < kAccQ; ++k) {
+        const int i = blockIdx.x * kAccBlockQ + k * 256 + threadIdx.x;
+        if (i >= N) break;
         const unsigned long long v = best[(size_t)slot * N + i];
         const int j = v == kNone ? -1 : (int)(unsigned)(v & 0xffffffffu);
         prevnn[(size_t)slot * N + i] = j >= 0 ? j : kNoMatch;
-        if (j >= 0) {
-            double Q[12];
+        if (j < 0) continue;
+        const double p[3] = {src[3 * i], src[3 * i + 1], src[3 * i + 2]};
+        double q[3];
+        xform(Q, p, q);
+        const double t3[3] = {tgt64[3 * j], tgt64[3 * j + 1], tgt64[3 * j + 2]};
+        const double d[3] = {q[0] - t3[0], q[1] - t3[1], q[2] - t3[2]};
+        const double d2 = d[0] * d[0] + d[1] * d[1] + d[2] * d[2];
+        if (!(d2 < r2)) continue;
 #pragma unroll
-            for (int t = 0; t < 12; ++t) Q[t] = Qm[12 * slot + t];
-            const double p[3] = {src[3 * i], src[3 * i + 1], src[3 * i + 2]};
-            double q[3];
-            xform(Q, p, q);
-            const double t3[3] = {tgt64[3 * j], tgt64[3 * j + 1], tgt64[3 * j + 2]};
-            const double d[3] = {q[0] - t3[0], q[1] - t3[1], q[2] - t3[2]};
-            const double d2 = d[0] * d[0] + d[1] * d[1] + d[2] * d[2];
-            if (d2 < r2) {
+        for (int a = 0; a < 3; ++a) {
+            acc[a] += q[a];
+            acc[3 + a] += t3[a];
 #pragma unroll
-                for (int a = 0; a < 3; ++a) {
-                    acc[a] = q[a];
-                    acc[3 + a] = t3[a];
-#pragma unroll
-                    for (int b = 0; b < 3; ++b) acc[6 + 3 * a + b] = t3[a] * q[b];
-                }
-                acc[15] = d2;
-                acc[16] = 1.0;
-            }
+            for (int b = 0; b < 3; ++b) acc[6 + 3 * a + b] += t3[a] * q[b];
         }
+        acc[15] += d2;
+        acc[16] += 1.0;
     }
-#pragma unroll
-    for (int v = 0; v < kP2PTerms; ++v) {
-        const double s = wave_sum(acc[v]);
-        if (lane == 0) red[wid][v] = s;
-    }
-    __syncthreads();
-    if (threadIdx.x < kNacc) {
-        double s = 0.0;
-        for (int v = 0; v < kP2PTerms; ++v)
-            if (p2p_slot(v) == (int)threadIdx.x) s = ((red[0][v] + red[1][v]) + red[2][v]) + red[3][v];
-        partial[((size_t)slot * nblk + blockIdx.x) * kPartialStride + threadIdx.x] = s;
-    }
+    block_partial<kP2PTerms>(acc, red, p2p_slot, partial + ((size_t)slot * nblk + blockIdx.x) * kPartialStride);
 }
 
 struct SolveArgs {
@@ -670,9 +1217,15 @@ int search_splits(int nact, int blocks_per_start, int want) {
     return (int)std::min<int64_t>(64, std::max<int64_t>(1, (want + waves - 1) / waves));
 }
 
-int accum_blocks(int64_t N) { return (int)((N + 255) / 256); }
+int accum_blocks(int64_t N) { return (int)((N + kAccBlockQ - 1) / kAccBlockQ); }
+
+// the cooperative search needs 16-bit tile ids in its LDS candidate list
+static bool use_coop(const orpcd_ctx* c) { return c->opt.search_kernel == 1 && c->tgt.ntiles <= 65535; }
+// the two-phase search keeps a candidate list of every query group
+static bool use_two_phase(const orpcd_ctx* c) { return c->opt.search_kernel == 2 && c->two_phase_ok; }
 
 hipError_t launch_xform(const orpcd_ctx* c, int nact, double r2, hipStream_t s) {
+    if (use_coop(c) || use_two_phase(c)) return hipSuccess;  // these searches transform their own queries
     const int N = (int)c->src.n;
     xform_queries_kernel<<<dim3((unsigned)((N + 255) / 256), (unsigned)nact), 256, 0, s>>>(
         c->src.xyz64.p, N, c->active.p, c->Q.p, c->done.p, c->tgt.p4.p, (int)c->tgt.ntiles,
@@ -683,13 +1236,45 @@ hipError_t launch_xform(const orpcd_ctx* c, int nact, double r2, hipStream_t s) 
 hipError_t launch_gicp_pass(const orpcd_ctx* c, int nact, int pass, double r2, hipStream_t s, hipEvent_t mid) {
     const int N = (int)c->src.n;
     const int sblk = (N + kCBlockQ - 1) / kCBlockQ;
+    hipError_t e;
+    if (use_two_phase(c)) {
+        const int gblk = (N + kGroupQ - 1) / kGroupQ;
+        const int G = nact * gblk;
+        unsigned* gcount = c->item_counts.p;
+        unsigned* offs = gcount + G;
+        cull_groups_kernel<<<dim3((unsigned)((gblk + 3) / 4), (unsigned)nact), 256, 0, s>>>(
+            c->src.xyz64.p, N, c->Q.p, c->prevnn.p, search_r2(r2), c->opt.reseed, seed_stride_for(c->tgt.ntiles),
+            c->tgt.p4.p, c->tgt.tlo.p, c->tgt.thi.p, (int)c->tgt.ntiles, c->tgt.slo.p, c->tgt.shi.p,
+            (int)c->tgt.nsuper, c->active.p, c->done.p, gblk, c->q32.p, c->best.p, c->items.p, gcount);
+        if ((e = hipGetLastError()) != hipSuccess) return e;
+        items_prefix_kernel<<<1, 1024, 0, s>>>(gcount, G, offs);
+        if ((e = hipGetLastError()) != hipSuccess) return e;
+        scan_items_kernel<<<(unsigned)c->opt.scan_blocks, 256, 0, s>>>(
+            c->q32.p, N, gblk, c->active.p, c->tgt.p4.p, c->tgt.tlo.p, c->tgt.thi.p, (int)c->tgt.ntiles,
+            c->items.p, offs, G, c->best.p, c->count_tiles ? c->counters.p : nullptr);
+    } else if (use_coop(c)) {
+        const int gblk = (N + kGroupQ - 1) / kGroupQ;  // 128-query groups per start
+        const int64_t groups = (int64_t)nact * gblk;
+        const int W = (int)std::min<int64_t>(kCoopMaxW, std::max<int64_t>(1, (c->opt.search_waves + groups - 1) / groups));
+        const size_t smem = coop_smem_bytes(W, c->tgt.ntiles);
+        if (smem > 32 * 1024) {  // large targets: raise the dynamic LDS limit of the launch
+            if ((e = hipFuncSetAttribute((const void*)nn_search_coop_kernel,
+                                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem)) != hipSuccess)
+                return e;
+        }
+        nn_search_coop_kernel<<<dim3((unsigned)gblk, (unsigned)nact), 64 * W, smem, s>>>(
+            c->src.xyz64.p, N, c->Q.p, c->prevnn.p, search_r2(r2), c->opt.reseed, seed_stride_for(c->tgt.ntiles),
+            c->tgt.p4.p, c->tgt.tlo.p, c->tgt.thi.p, (int)c->tgt.ntiles, c->tgt.slo.p, c->tgt.shi.p,
+            (int)c->tgt.nsuper, c->active.p, c->done.p, c->best.p, c->count_tiles ? c->counters.p : nullptr);
+    } else {
     const int S = search_splits(nact, sblk, c->opt.search_waves);
-    hipError_t e;  // best[] was reset to kNone by xform_queries_kernel
+    // best[] was reset to kNone by xform_queries_kernel
     auto kern = c->opt.search_occupancy == 6 ? nn_search_kernel_o6 : nn_search_kernel;
     kern<<<dim3((unsigned)(sblk * S), (unsigned)nact), kCBlock, 0, s>>>(
         c->q32.p, N, c->tgt.p4.p, c->tgt.tlo.p, c->tgt.thi.p, (int)c->tgt.ntiles, c->tgt.slo.p, c->tgt.shi.p,
         (int)c->tgt.nsuper, c->opt.super_cull, c->active.p, c->done.p, S, c->best.p,
         c->count_tiles ? c->counters.p : nullptr);
+    }
     if ((e = hipGetLastError()) != hipSuccess) return e;
     if (mid && (e = hipEventRecord(mid, s)) != hipSuccess) return e;
     const int ablk = accum_blocks(N);

@@ -168,6 +168,9 @@ struct orpcd_ctx {
     orpcd::DevBuf<double> scov;     // B*N*6 posed-frame source covariance
     orpcd::DevBuf<int32_t> prevnn;  // B*N previous correspondence (Morton target index)
     orpcd::DevBuf<unsigned long long> best;  // B*N packed (d^2 bits, target) of the current pass
+    orpcd::DevBuf<unsigned> items;           // two-phase search: candidate tiles per query group
+    orpcd::DevBuf<unsigned> item_counts;     // per group: candidate count, then the exclusive offsets
+    bool two_phase_ok = false;               // the batch's worst-case item list fits
     orpcd::DevBuf<float4> q32;      // B*N fp32 queries of the current pass (x,y,z,0)
     orpcd::DevBuf<double> G;        // B*12 base pose (3x4, column convention)
     orpcd::DevBuf<double> T;        // B*16 accumulated ICP transform
@@ -228,6 +231,10 @@ struct orpcd_ctx {
         int super_cull = 1;       // first culling level over 64-tile super-tiles
         int reseed = 0;           // representative seeding also after pass 0
         int search_occupancy = 0; // 0: compiler's register budget; 6: capped at 6 waves/SIMD
+        int search_kernel = 0;    // 0: split search (measured best, tools/ab_search.py);
+                                  // 1: cooperative (one workgroup per query group, queries fused);
+                                  // 2: two-phase (cull once per group, persistent scan of the items)
+        int scan_blocks = 1280;   // persistent grid of the two-phase scan (256-thread blocks)
     } opt;
     std::vector<hipEvent_t> ev_pool;
     orpcd::KernelStats stats;

@@ -31,21 +31,29 @@ namespace orpcd {
 
 // ---------------------------------------------------------------- SOR
 // stats[0] = cloud_mean, [1] = std_dev, [2] = threshold, [3] = valid count.
+// The folds are sequential in index order (as std::accumulate and
+// std::inner_product run them): the wave loads 64 values per step and the
+// unrolled readlanes feed them, in lane order, to one dependent add chain.
 __global__ __launch_bounds__(64) void sor_stats_kernel(const double* __restrict__ avg, int n, double std_ratio,
                                                        double* __restrict__ stats) {
 #pragma clang fp contract(off)
     const int lane = threadIdx.x;
+    auto rl = [](double v, int k) {
+        const unsigned long long b = __double_as_longlong(v);
+        const unsigned lo = __builtin_amdgcn_readlane((unsigned)b, k), hi = __builtin_amdgcn_readlane((unsigned)(b >> 32), k);
+        return __longlong_as_double(((unsigned long long)hi << 32) | lo);
+    };
     double cloud_mean = 0.0, sq_sum = 0.0;
     int valid = 0;
     // pass 1: accumulate(avg, 0.0, [](x, y) { return y > 0 ? x + y : x; }) and the
-    // count of non-empty searches; the wave loads 64 values, lane order folds them
+    // count of non-empty searches (mean != -1)
     for (int b = 0; b < n; b += 64) {
         const double v = b + lane < n ? avg[b + lane] : -1.0;
-        const int m = min(64, n - b);
-        for (int k = 0; k < m; ++k) {
-            const double y = __shfl(v, k, 64);
-            if (y > 0) cloud_mean = cloud_mean + y;
-            if (y != -1.0) ++valid;
+        valid += __popcll(__ballot(v != -1.0));
+#pragma unroll
+        for (int k = 0; k < 64; ++k) {
+            const double y = rl(v, k);
+            cloud_mean = y > 0 ? cloud_mean + y : cloud_mean;
         }
     }
     if (valid == 0) {
@@ -56,11 +64,9 @@ __global__ __launch_bounds__(64) void sor_stats_kernel(const double* __restrict_
     // pass 2: inner_product(..., plus, [](x, y) { return x > 0 ? (x-m)*(y-m) : 0; })
     for (int b = 0; b < n; b += 64) {
         const double v = b + lane < n ? avg[b + lane] : -1.0;
-        const int m = min(64, n - b);
-        for (int k = 0; k < m; ++k) {
-            const double x = __shfl(v, k, 64);
-            sq_sum = sq_sum + (x > 0 ? (x - cloud_mean) * (x - cloud_mean) : 0.0);
-        }
+        const double t = v > 0 ? (v - cloud_mean) * (v - cloud_mean) : 0.0;  // per element, then folded in order
+#pragma unroll
+        for (int k = 0; k < 64; ++k) sq_sum = sq_sum + rl(t, k);
     }
     const double std_dev = sqrt(sq_sum / (double)(valid - 1));
     const double thr = cloud_mean + std_ratio * std_dev;

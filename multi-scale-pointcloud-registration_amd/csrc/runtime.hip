@@ -356,6 +356,11 @@ int batch_setup(orpcd_ctx* c, const double* R0, const double* t0, int B, const o
     CTX_CHECK(c, c->R.ensure((size_t)B * 9));
     CTX_CHECK(c, c->prev.ensure((size_t)B * 2));
     CTX_CHECK(c, c->partial.ensure((size_t)B * nblk * kPartialStride));
+    // two-phase search: worst case every tile a candidate of every group (else the split search)
+    const size_t worst_items = (size_t)B * ((N + 127) / 128) * (size_t)c->tgt.ntiles;
+    c->two_phase_ok = worst_items <= ((size_t)1 << 29);  // <= 2 GiB of items
+    if (c->two_phase_ok) CTX_CHECK(c, c->items.ensure(worst_items));
+    CTX_CHECK(c, c->item_counts.ensure((size_t)2 * B * ((N + 127) / 128) + 2));
     CTX_CHECK(c, c->done.ensure((size_t)B));
     CTX_CHECK(c, c->active.ensure((size_t)B));
     CTX_CHECK(c, c->out_fit.ensure((size_t)B));
@@ -470,6 +475,8 @@ int orpcd_ctx_destroy(orpcd_ctx* c) {
         b->release();
     c->prevnn.release();
     c->best.release();
+    c->items.release();
+    c->item_counts.release();
     c->q32.release();
     c->done.release();
     c->active.release();
@@ -600,7 +607,7 @@ int run_passes(orpcd_ctx* c, int B, const orpcd_gicp_params* p, double* T_out, d
     if (timed) {
         while ((int)c->ev_pool.size() < 3 * every) {
             hipEvent_t e;
-            CTX_CHECK(c, hipEventCreate(&e));
+            CTX_CHECK(c, hipEventCreateWithFlags(&e, hipEventDisableSystemFence));  // timing only: no cache writeback per record
             c->ev_pool.push_back(e);
         }
     }
@@ -856,7 +863,7 @@ int orpcd_gicp_shard_pass(orpcd_ctx* c, double* sums_out, int32_t* active) {
     if (timed) {
         while (c->ev_pool.size() < 3) {
             hipEvent_t e;
-            CTX_CHECK(c, hipEventCreate(&e));
+            CTX_CHECK(c, hipEventCreateWithFlags(&e, hipEventDisableSystemFence));  // timing only: no cache writeback per record
             c->ev_pool.push_back(e);
         }
         CTX_CHECK(c, read_counters(c, tiles0, unused, false));
@@ -1122,6 +1129,8 @@ int orpcd_set_option(orpcd_ctx* c, const char* key, double value) {
     else if (k == "super_cull" && (v == 0 || v == 1)) c->opt.super_cull = v;
     else if (k == "reseed" && (v == 0 || v == 1)) c->opt.reseed = v;
     else if (k == "search_occupancy" && (v == 0 || v == 6)) c->opt.search_occupancy = v;
+    else if (k == "search_kernel" && v >= 0 && v <= 2) c->opt.search_kernel = v;
+    else if (k == "scan_blocks" && v >= 1 && v <= 65536) c->opt.scan_blocks = v;
     else {
         c->err = "set_option: unknown key or bad value: " + k;
         return ORPCD_EINVAL;

@@ -40,6 +40,14 @@ class FgrParams(ctypes.Structure):
                 ("seed", ctypes.c_uint64)]
 
 
+try:
+    from xxhash import xxh3_64_intdigest as _xxh3
+except ImportError:  # pragma: no cover - xxhash is in the image; hashlib is the slower stand-in
+    import hashlib
+
+    def _xxh3(buf):
+        return hashlib.blake2b(buf, digest_size=8).digest()
+
 _lib = None
 _lib_lock = threading.Lock()
 
@@ -162,7 +170,9 @@ class Context:
     # ------------------------------------------------------------- clouds
     @staticmethod
     def _key(a: np.ndarray):
-        return (a.shape, hash(a.tobytes()))
+        # content fingerprint of the cloud (xxh3 over the buffer, no copy): a
+        # cloud re-sent unchanged is not re-uploaded, a changed one always is
+        return (a.shape, _xxh3(memoryview(a).cast("B")))
 
     def set_target(self, xyz: np.ndarray, epsilon: float = 1e-3, cache: bool = True):
         xyz = _c3(xyz)

@@ -161,3 +161,22 @@ def test_align_matches_oracle_aligner(oracle):
     assert len(e) == len(eo)
     assert abs(m - mo) <= 1e-5
     assert np.abs(T - To).max() <= 1e-4
+
+
+@pytest.mark.parametrize("kernel", [1, 2])
+def test_search_variants_identical(ctx, kernel):
+    """The alternative search kernels (orpcd_set_option "search_kernel") return
+    the same correspondences, hence bit-identical GICP results."""
+    src, tgt = small_pair(6000, 5500, seed=11)
+    R0 = np.array([np.eye(3), rot_xyz(30, -20, 10), rot_xyz(-60, 45, 80)])
+    t0 = np.array([[0.0, 0.0, 0.0], [0.05, -0.02, 0.01], [0.1, 0.0, -0.1]])
+    ctx.set_target(tgt)
+    ctx.set_source(src)
+    ref = ctx.gicp_batch(R0, t0)
+    try:
+        ctx.set_option("search_kernel", kernel)
+        got = ctx.gicp_batch(R0, t0)
+    finally:
+        ctx.set_option("search_kernel", 0)
+    assert np.array_equal(got["T"], ref["T"]) and np.array_equal(got["iters"], ref["iters"])
+    assert np.array_equal(got["rmse"], ref["rmse"])

@@ -37,6 +37,7 @@ def main():
     ctx.gicp_batch(R0, t0)  # warm-up (code objects, allocations)
     times = {i: [] for i in range(len(configs))}
     iters = {}
+    Ts = {}
     for _ in range(rounds):
         for i, cfg in enumerate(configs):
             for k, v in {"search_waves": 32768, "sync_every": 4, "super_cull": 1, "reseed": 0, **cfg}.items():
@@ -45,9 +46,12 @@ def main():
             r = ctx.gicp_batch(R0, t0)
             times[i].append((time.perf_counter() - t1) * 1e3)
             iters[i] = int(r["iters"].sum())
+            Ts[i] = r["T"]
     for i, cfg in enumerate(configs):
         a = np.array(times[i])
-        print(f"{json.dumps(cfg):50s} median {np.median(a):8.2f} ms  min {a.min():8.2f} ms  iters {iters[i]}")
+        dT = float(np.abs(Ts[i] - Ts[0]).max())
+        print(f"{json.dumps(cfg):50s} median {np.median(a):8.2f} ms  min {a.min():8.2f} ms  iters {iters[i]}  "
+              f"max|dT| vs first {dT:.1e}")
 
 
 if __name__ == "__main__":

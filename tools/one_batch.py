@@ -1,0 +1,36 @@
+"""One C2 multistart (30 starts, GICP) with the given runtime options, for
+profiling a single configuration:  python tools/one_batch.py '{"search_kernel":1}' [--reps 2]"""
+import json
+import os
+import sys
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [os.path.join(REPO, "multi-scale-pointcloud-registration_amd"), REPO]
+from orpcd_amd import Preprocessor, _native  # noqa: E402
+from workloads import c2_pair, rot_xyz  # noqa: E402
+
+
+def main():
+    cfg = json.loads(sys.argv[1]) if len(sys.argv) > 1 and sys.argv[1].startswith("{") else {}
+    reps = int(sys.argv[sys.argv.index("--reps") + 1]) if "--reps" in sys.argv else 2
+    s, t = c2_pair(50000)
+    s = Preprocessor([]).preprocess(s)
+    t = Preprocessor([]).preprocess(t)
+    rng = np.random.default_rng(1000)
+    R0 = np.array([rot_xyz(*rng.uniform(-90, 90, 3)) for _ in range(30)])
+    t0 = rng.normal(size=(30, 3)) * 0.1
+    ctx = _native.Context(0)
+    for k, v in cfg.items():
+        ctx.set_option(k, v)
+    ctx.set_target(t)
+    ctx.set_source(s)
+    for _ in range(reps):
+        r = ctx.gicp_batch(R0, t0)
+    print("iters", int(r["iters"].sum()))
+    ctx.close()
+
+
+if __name__ == "__main__":
+    main()
