@@ -19,10 +19,11 @@ REPO = os.path.dirname(HERE)
 CSRC = os.path.join(HERE, "csrc")
 OBJ = os.path.join(HERE, "build", "obj")
 LIBDIR = os.path.join(HERE, "orpcd_amd", "_lib")
-LIB = os.path.join(LIBDIR, "liborpcd_hip.so")
+LIB = os.environ.get("ORPCD_BUILD_LIB", os.path.join(LIBDIR, "liborpcd_hip.so"))
+EXTRA = os.environ.get("ORPCD_EXTRA_FLAGS", "").split()  # e.g. -DORPCD_PHASES (instrumented variant)
 ARCH = os.environ.get("ORPCD_OFFLOAD_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
-CXXFLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-Wall", "-Wno-unused-function",
+CXXFLAGS = EXTRA + ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-Wall", "-Wno-unused-function",
             "-munsafe-fp-atomics", f"-I{os.path.join(REPO, 'include')}", f"-I{CSRC}"]
 
 
@@ -38,7 +39,7 @@ def _stale(target, deps):
 
 
 def _compile(src, force):
-    obj = os.path.join(OBJ, os.path.basename(src) + ".o")
+    obj = os.path.join(OBJ + ("_x" if EXTRA else ""), os.path.basename(src) + ".o")
     if force or _stale(obj, [src] + _headers()):
         cmd = [HIPCC] + CXXFLAGS + ["-c", src, "-o", obj]
         r = subprocess.run(cmd, capture_output=True, text=True)
@@ -48,7 +49,7 @@ def _compile(src, force):
 
 
 def build(force: bool = False, verbose: bool = False) -> str:
-    os.makedirs(OBJ, exist_ok=True)
+    os.makedirs(OBJ + ("_x" if EXTRA else ""), exist_ok=True)
     os.makedirs(LIBDIR, exist_ok=True)
     srcs = sorted(glob.glob(os.path.join(CSRC, "*.hip")))
     with ThreadPoolExecutor(max_workers=min(8, len(srcs))) as ex:

@@ -77,7 +77,8 @@ __device__ __forceinline__ int culled_search(float4* stage, const float4* __rest
                                              int ntiles, const float4* __restrict__ slo,
                                              const float4* __restrict__ shi, int nsuper, int super_cull, int S, int s,
                                              const float qx[2], const float qy[2],
-                                             const float qz[2], const float bound[2], float bd[2], int bj[2]) {
+                                             const float qz[2], const float bound[2], float bd[2], int bj[2],
+                                             unsigned long long* phase_cull_out = nullptr) {
     const int lane = threadIdx.x & 63;
     const bool v0 = bound[0] > 0.0f, v1 = bound[1] > 0.0f;
     unsigned k0 = v0 ? __float_as_uint(bound[0]) : 0u;  // best key (0: never improves)
@@ -107,32 +108,59 @@ __device__ __forceinline__ int culled_search(float4* stage, const float4* __rest
     unsigned long long mask = 0;
     float lb = inf;
     float4 a = make_float4(0.f, 0.f, 0.f, 0.f), b = a;
-    auto next_candidate = [&](float& lbk) -> int {
+#ifdef ORPCD_PHASES
+    unsigned long long ph_cull = 0, ph_rounds = 0, ph_tests = 0;
+#endif
+    // the tile AABBs of the NEXT surviving super-tile are loaded while the
+    // current round is tested and scanned (one round of load latency hidden)
+    int tbn = -1;  // base of the prefetched round (-1: none)
+    float4 an = a, bn = b;
+    auto prefetch_round = [&]() {
+        while (smask == 0) {
+            sb += 64;
+            if (sb >= nsuper) {
+                tbn = -1;
+                return;
+            }
+            const int u = sb + lane;
+            float sl = inf;
+            if (u < nsuper && !super_cull) {
+                sl = 0.0f;
+            } else if (u < nsuper) {
+                const float4 c = slo[u], d = shi[u];
+                const float dx = fmaxf(0.0f, fmaxf(c.x - hix, lox - d.x));
+                const float dy = fmaxf(0.0f, fmaxf(c.y - hiy, loy - d.y));
+                const float dz = fmaxf(0.0f, fmaxf(c.z - hiz, loz - d.z));
+                sl = dx * dx + dy * dy + dz * dz;
+            }
+            smask = __ballot(sl < W);
+        }
+        tbn = (sb + __builtin_ctzll(smask)) * kSuper;
+        smask &= smask - 1;
+        const int t = tbn + lane;
+        if (t < ntiles && (S == 1 || t % S == s)) {
+            an = tlo[t];
+            bn = thi[t];
+        } else {
+            an = make_float4(inf, inf, inf, 0.f);  // empty box: never within the bound
+            bn = make_float4(-inf, -inf, -inf, 0.f);
+        }
+    };
+    prefetch_round();
+    auto next_candidate_impl = [&](float& lbk) -> int {
         for (;;) {
             while (mask == 0) {
-                while (smask == 0) {
-                    sb += 64;
-                    if (sb >= nsuper) return -1;
-                    const int u = sb + lane;
-                    float sl = inf;
-                    if (u < nsuper && !super_cull) {
-                        sl = 0.0f;
-                    } else if (u < nsuper) {
-                        const float4 c = slo[u], d = shi[u];
-                        const float dx = fmaxf(0.0f, fmaxf(c.x - hix, lox - d.x));
-                        const float dy = fmaxf(0.0f, fmaxf(c.y - hiy, loy - d.y));
-                        const float dz = fmaxf(0.0f, fmaxf(c.z - hiz, loz - d.z));
-                        sl = dx * dx + dy * dy + dz * dz;
-                    }
-                    smask = __ballot(sl < W);
-                }
-                tb = (sb + __builtin_ctzll(smask)) * kSuper;
-                smask &= smask - 1;
+                if (tbn < 0) return -1;
+                tb = tbn;
+                a = an;
+                b = bn;
+#ifdef ORPCD_PHASES
+                ++ph_rounds;
+#endif
+                prefetch_round();
                 const int t = tb + lane;
                 lb = inf;
                 if (t < ntiles && (S == 1 || t % S == s)) {
-                    a = tlo[t];
-                    b = thi[t];
                     const float dx = fmaxf(0.0f, fmaxf(a.x - hix, lox - b.x));
                     const float dy = fmaxf(0.0f, fmaxf(a.y - hiy, loy - b.y));
                     const float dz = fmaxf(0.0f, fmaxf(a.z - hiz, loz - b.z));
@@ -144,6 +172,9 @@ __device__ __forceinline__ int culled_search(float4* stage, const float4* __rest
             mask &= mask - 1;
             lbk = __uint_as_float(__builtin_amdgcn_readlane(__float_as_uint(lb), k));
             if (!(lbk < W)) continue;  // the bound shrank since the ballot
+#ifdef ORPCD_PHASES
+            ++ph_tests;
+#endif
             const float lx = __uint_as_float(__builtin_amdgcn_readlane(__float_as_uint(a.x), k));
             const float ly = __uint_as_float(__builtin_amdgcn_readlane(__float_as_uint(a.y), k));
             const float lz = __uint_as_float(__builtin_amdgcn_readlane(__float_as_uint(a.z), k));
@@ -156,6 +187,16 @@ __device__ __forceinline__ int culled_search(float4* stage, const float4* __rest
         }
     };
 
+    auto next_candidate = [&](float& lbk) -> int {
+#ifdef ORPCD_PHASES
+        const unsigned long long t0 = __builtin_readcyclecounter();
+        const int r = next_candidate_impl(lbk);
+        ph_cull += __builtin_readcyclecounter() - t0;
+        return r;
+#else
+        return next_candidate_impl(lbk);
+#endif
+    };
     // software pipeline: the next candidate's 1 KiB tile load is in flight
     // while the current tile is scanned out of LDS
     float lbn = inf;
@@ -225,6 +266,13 @@ __device__ __forceinline__ int culled_search(float4* stage, const float4* __rest
         bj[1] = t1 * kTile + (int)(k1 & 63u);
         bd[1] = __uint_as_float(k1 & kKeyMask);
     }
+#ifdef ORPCD_PHASES
+    if (phase_cull_out) {
+        phase_cull_out[0] = ph_cull;
+        phase_cull_out[1] = ph_rounds;
+        phase_cull_out[2] = ph_tests;
+    }
+#endif
     return visited;
 }
 
@@ -287,12 +335,15 @@ __device__ __forceinline__ void nn_search_body(
     const float4* __restrict__ q32, int N, const float4* __restrict__ p4, const float4* __restrict__ tlo,
     const float4* __restrict__ thi, int ntiles, const float4* __restrict__ slo, const float4* __restrict__ shi,
     int nsuper, int super_cull, const int32_t* __restrict__ active, const int32_t* __restrict__ done, int S,
-    unsigned long long* __restrict__ best, unsigned long long* __restrict__ counters) {
-    const int slot = active[blockIdx.y];
+    unsigned long long* __restrict__ best, unsigned long long* __restrict__ counters, int by, int bx, int wid,
+    float4* stage_w) {
+    const int slot = active[by];
     if (done[slot]) return;
-    __shared__ float4 stage[kCWaves][kTile];
-    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    const int grp = blockIdx.x / S, split = blockIdx.x - grp * S;
+#ifdef ORPCD_PHASES
+    const unsigned long long ph_t0 = __builtin_readcyclecounter();
+#endif
+    const int lane = threadIdx.x & 63;
+    const int grp = bx / S, split = bx - grp * S;
     const int i0 = grp * kCBlockQ + wid * (64 * kCQPT) + lane;
     float qx[kCQPT], qy[kCQPT], qz[kCQPT], bound[kCQPT], bd[kCQPT];
     int bj[kCQPT];
@@ -306,13 +357,30 @@ __device__ __forceinline__ void nn_search_body(
         qz[k] = q.z;
         bound[k] = q.w;  // 0 for padding lanes: never takes anything
     }
+#ifdef ORPCD_PHASES
+    const float wq = __uint_as_float(wave_umax(__float_as_uint(qx[0] + qy[1])));  // the query loads have landed
+    const unsigned long long ph_t1 = __builtin_readcyclecounter() + (wq == 1.2345f ? 1 : 0);
+    unsigned long long ph_cull[3] = {0, 0, 0};
+    const int visited = culled_search(stage_w, p4, tlo, thi, ntiles, slo, shi, nsuper, super_cull, S, split, qx,
+                                      qy, qz, bound, bd, bj, ph_cull);
+#else
     const int visited =
-        culled_search(stage[wid], p4, tlo, thi, ntiles, slo, shi, nsuper, super_cull, S, split, qx, qy, qz, bound,
+        culled_search(stage_w, p4, tlo, thi, ntiles, slo, shi, nsuper, super_cull, S, split, qx, qy, qz, bound,
                       bd, bj);
+#endif
     if (lane == 0 && counters) {  // spread over kCounterSlots cache lines (one address serialises)
-        unsigned long long* cs = counters + kCounterStride * ((blockIdx.x * kCWaves + wid + blockIdx.y) % kCounterSlots);
+        unsigned long long* cs = counters + kCounterStride * ((bx * kCWaves + wid + by) % kCounterSlots);
         atomicAdd(cs, (unsigned long long)visited);
         atomicMax(cs + 1, (unsigned long long)visited);
+#ifdef ORPCD_PHASES
+        const unsigned long long ph_t2 = __builtin_readcyclecounter();
+        atomicAdd(cs + 2, ph_t1 - ph_t0);   // query loads
+        atomicAdd(cs + 3, ph_cull[0]);      // culling (next_candidate)
+        atomicAdd(cs + 6, ph_cull[1]);      // tile-AABB rounds loaded
+        atomicAdd(cs + 7, ph_cull[2]);      // per-query candidate tests
+        atomicAdd(cs + 4, ph_t2 - ph_t1);   // search incl. culling
+        atomicAdd(cs + 5, 1ull);            // waves
+#endif
     }
     unsigned long long* out = best + (size_t)slot * N;
 #pragma unroll
@@ -338,11 +406,17 @@ __device__ __forceinline__ void nn_search_body(
         const int32_t *__restrict__ done, int S, unsigned long long *__restrict__ best,                      \
         unsigned long long *__restrict__ counters
 __global__ __launch_bounds__(kCBlock) void nn_search_kernel(ORPCD_NN_SEARCH_ARGS) {
-    nn_search_body(q32, N, p4, tlo, thi, ntiles, slo, shi, nsuper, super_cull, active, done, S, best, counters);
+    __shared__ float4 stage[kCWaves][kTile];
+    const int wid = threadIdx.x >> 6;
+    nn_search_body(q32, N, p4, tlo, thi, ntiles, slo, shi, nsuper, super_cull, active, done, S, best, counters,
+                   blockIdx.y, blockIdx.x, wid, stage[wid]);
 }
 __global__ __launch_bounds__(kCBlock) __attribute__((amdgpu_waves_per_eu(6, 8))) void nn_search_kernel_o6(
     ORPCD_NN_SEARCH_ARGS) {
-    nn_search_body(q32, N, p4, tlo, thi, ntiles, slo, shi, nsuper, super_cull, active, done, S, best, counters);
+    __shared__ float4 stage[kCWaves][kTile];
+    const int wid = threadIdx.x >> 6;
+    nn_search_body(q32, N, p4, tlo, thi, ntiles, slo, shi, nsuper, super_cull, active, done, S, best, counters,
+                   blockIdx.y, blockIdx.x, wid, stage[wid]);
 }
 #undef ORPCD_NN_SEARCH_ARGS
 
