@@ -1,0 +1,10 @@
+set -e
+mkdir -p gpurun_out
+cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
+B="python3 bench.py --steps 3 --warmup 1 --cpu-seconds 0 --align 0"
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/kt -- $B > gpurun_out/kt.log 2>&1
+timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/fetch -- $B > gpurun_out/fetch.log 2>&1
+timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/write -- $B > gpurun_out/write.log 2>&1
+timeout -k 10 300 python3 tools/bench_fgr.py --out gpurun_out/fgr_c3.json > gpurun_out/fgr.log 2>&1
+timeout -k 10 400 python3 tools/bench_c5.py --out gpurun_out/c5.json > gpurun_out/c5.log 2>&1
+timeout -k 10 300 python3 tools/bench_prep.py --out gpurun_out/prep.json > gpurun_out/prep.log 2>&1
