@@ -132,6 +132,10 @@ def main():
             align_s = dict(seconds=round(time.perf_counter() - t1, 3), rmse=float(metric),
                            scale_factors=[round(float(x), 6) for x in sf.ravel()],
                            multistarts=len(al.history), gicp_iters=int(sum(h["iters"] for h in al.history)))
+            if cpu:  # the CPU oracle at its measured GICP rate over the same iterations (an estimate: a full
+                # CPU align() of ~25k GICP iterations takes minutes; labelled as such)
+                align_s["cpu_estimated_seconds"] = round(align_s["gicp_iters"] / cpu["value"], 1)
+                align_s["speedup_vs_cpu_estimate"] = round(align_s["cpu_estimated_seconds"] / align_s["seconds"], 1)
 
     if rank == 0:
         line = {

@@ -1158,7 +1158,7 @@ __device__ __forceinline__ void reduce_partials(const double* __restrict__ parti
         for (int v = 0; v < kNacc; ++v) s[v] += pp[v];
     }
 #pragma unroll
-    for (int v = 0; v < kNacc; ++v) s[v] = wave_sum(s[v]);
+    for (int v = 0; v < kNacc; ++v) s[v] = wave_sum_fixed(s[v]);
 }
 
 __global__ __launch_bounds__(64) void reduce_partials_kernel(const double* __restrict__ partial, int slot, int nblk,

@@ -11,6 +11,8 @@
 // cumulants are summed in that order with contraction off, so the covariance
 // and FastEigen3x3 normal match the CPU restatement operation for operation.
 // This pass runs once per cloud (not per ICP iteration).
+#include <cstdlib>
+
 #include "device_math.h"
 #include "orpcd_internal.h"
 #include "wave_ops.h"
@@ -275,11 +277,196 @@ __global__ __launch_bounds__(256) void knn_tiles_kernel(
     out[5] = C.zz;
 }
 
+// ---------------------------------------------------------------------------
+// One wave per query (default KNN): the wave holds the query's K <= 64 best
+// (d^2, input index) so far SORTED across its lanes (lane s = s-th nearest).
+// Each candidate tile puts one point per lane: exact fp64 d^2 (contraction
+// off, the oracle's expression), a bitonic sort of the 64 candidates across
+// lanes, then the merge with the kept list (reverse, lane-wise min -> bitonic
+// -> 6 merge steps).  A tile is skipped when no candidate beats the K-th kept
+// pair, and whole tiles / super-tiles when their (conservative fp32) box is
+// farther than the K-th distance.  The list -- and every sum made from it in
+// list order (covariance cumulants, SOR's mean distance) -- is the oracle's
+// KD-tree answer exactly.  Tiles: own, then +-1, +-2 (Morton neighbours), then
+// the culled walk over super-tiles and tiles.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ bool pair_less(double d, int i, double e, int j) { return d < e || (d == e && i < j); }
+
+__device__ __forceinline__ void xchg(double& d, int& i, int j_xor, bool keep_min) {
+    const double pd = __shfl_xor(d, j_xor, 64);
+    const int pi = __shfl_xor(i, j_xor, 64);
+    const bool pl = pair_less(pd, pi, d, i);  // partner < self
+    if (keep_min ? pl : pair_less(d, i, pd, pi)) {
+        d = pd;
+        i = pi;
+    }
+}
+
+__device__ __forceinline__ void bitonic_sort64(double& d, int& i, int lane) {
+#pragma unroll
+    for (int k = 2; k <= 64; k <<= 1)
+#pragma unroll
+        for (int j = k >> 1; j > 0; j >>= 1) {
+            const bool up = (lane & k) == 0 || k == 64;
+            const bool lower = (lane & j) == 0;
+            xchg(d, i, j, lower == up);
+        }
+}
+
+__global__ __launch_bounds__(256) void knn_wave_kernel(
+    const double* __restrict__ xyz64, const int32_t* __restrict__ perm, int n, const float4* __restrict__ tlo,
+    const float4* __restrict__ thi, int ntiles, const float4* __restrict__ slo, const float4* __restrict__ shi,
+    int nsuper, const double* __restrict__ in64, double r2, float margin, int K, int out_input_order,
+    double* __restrict__ rawcov6, int32_t* __restrict__ nbr_idx, double* __restrict__ nbr_d2,
+    int32_t* __restrict__ nbr_cnt, double* __restrict__ mean_dist) {
+#pragma clang fp contract(off)
+    const int lane = threadIdx.x & 63;
+    const int q = blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    if (q >= n) return;  // wave-uniform
+    const double qx = xyz64[3 * q], qy = xyz64[3 * q + 1], qz = xyz64[3 * q + 2];
+    const float fx = (float)qx, fy = (float)qy, fz = (float)qz;
+    const double INF = __builtin_huge_val();
+    double Ld = INF;  // sorted kept list: lane s holds the s-th nearest so far
+    int Li = 0x7fffffff;
+    auto kth = [&]() {  // the K-th kept pair (uniform)
+        const long long b = __double_as_longlong(Ld);
+        const unsigned lo = __builtin_amdgcn_readlane((unsigned)b, K - 1);
+        const unsigned hi = __builtin_amdgcn_readlane((unsigned)(b >> 32), K - 1);
+        return __longlong_as_double(((long long)hi << 32) | lo);
+    };
+    auto bound_f = [&]() -> float {  // fp32 upper bound of the K-th d^2 (and of the radius)
+        const double b = fmin(kth(), r2);
+        return b >= 3.0e38 ? 3.0e38f : (float)b * 1.0000003f + 1e-37f;
+    };
+    const int own = q / kTile;
+    auto scan_tile = [&](int t) {
+        const int k = t * kTile + lane;
+        double d = INF;
+        int id = 0x7fffffff;
+        if (k < n) {
+            const double dx = qx - xyz64[3 * k], dy = qy - xyz64[3 * k + 1], dz = qz - xyz64[3 * k + 2];
+            const double dd = dx * dx + dy * dy + dz * dz;
+            if (dd < r2) {
+                d = dd;
+                id = perm[k];
+            }
+        }
+        const double kd = kth();
+        const int ki = __builtin_amdgcn_readlane(Li, K - 1);
+        if (!__any(pair_less(d, id, kd, ki))) return;
+        bitonic_sort64(d, id, lane);
+        // merge: the 64 smallest of (kept, new) are the lane-wise minima of the
+        // kept list and the reversed new list (a bitonic sequence) ...
+        const double rd = __shfl(d, 63 - lane, 64);
+        const int ri = __shfl(id, 63 - lane, 64);
+        if (pair_less(rd, ri, Ld, Li)) {
+            Ld = rd;
+            Li = ri;
+        }
+        // ... sorted ascending by the bitonic merge
+#pragma unroll
+        for (int j = 32; j > 0; j >>= 1) xchg(Ld, Li, j, (lane & j) == 0);
+    };
+    constexpr int kWin = 2;
+    scan_tile(own);
+    for (int dt = 1; dt <= kWin; ++dt) {
+        if (own - dt >= 0) scan_tile(own - dt);
+        if (own + dt < ntiles) scan_tile(own + dt);
+    }
+    auto gap = [&](float4 a, float4 b) {
+        const float gx = fmaxf(0.0f, fmaxf(a.x - fx, fx - b.x) - margin);
+        const float gy = fmaxf(0.0f, fmaxf(a.y - fy, fy - b.y) - margin);
+        const float gz = fmaxf(0.0f, fmaxf(a.z - fz, fz - b.z) - margin);
+        return gx * gx + gy * gy + gz * gz;
+    };
+    for (int sb = 0; sb < nsuper; sb += 64) {
+        const int u = sb + lane;
+        const float sl = u < nsuper ? gap(slo[u], shi[u]) : 3.0e38f;
+        unsigned long long smask = __ballot(sl < bound_f());
+        while (smask) {
+            const int su = sb + __builtin_ctzll(smask);
+            smask &= smask - 1;
+            const int t = su * kSuper + lane;
+            const float lb = (t < ntiles && (t < own - kWin || t > own + kWin)) ? gap(tlo[t], thi[t]) : 3.0e38f;
+            unsigned long long tm = __ballot(lb < bound_f());
+            while (tm) {
+                const int k = __builtin_ctzll(tm);
+                tm &= tm - 1;
+                const float lbk = __uint_as_float(__builtin_amdgcn_readlane(__float_as_uint(lb), k));
+                if (!(lbk < bound_f())) continue;  // the K-th distance shrank meanwhile
+                scan_tile(su * kSuper + k);
+            }
+        }
+    }
+    // outputs (kept pairs beyond the count are (INF, max) and written as -1 / 0)
+    const int c = __popcll(__ballot(lane < K && Ld < INF));
+    const int o = out_input_order ? perm[q] : q;
+    if (nbr_idx && lane < K) nbr_idx[(size_t)o * K + lane] = lane < c ? Li : -1;
+    if (nbr_d2 && lane < K) nbr_d2[(size_t)o * K + lane] = lane < c ? Ld : 0.0;
+    if (nbr_cnt && lane == 0) nbr_cnt[o] = c;
+    if (mean_dist) {  // SOR: mean of sqrt(d^2) over the neighbours in list order (-1: empty search)
+        const double sq = lane < c ? sqrt(Ld) : 0.0;
+        double sd = 0.0;
+        for (int s2 = 0; s2 < c; ++s2) {
+            const long long b = __double_as_longlong(sq);
+            const unsigned lo = __builtin_amdgcn_readlane((unsigned)b, s2);
+            const unsigned hi = __builtin_amdgcn_readlane((unsigned)(b >> 32), s2);
+            sd += __longlong_as_double(((long long)hi << 32) | lo);
+        }
+        if (lane == 0) mean_dist[o] = c > 0 ? sd / (double)c : -1.0;
+    }
+    if (!rawcov6) return;
+    Sym3 C;
+    if (c >= 3) {  // O3D ComputeCovariance: one-pass cumulants in list order, 1/n
+        double cu[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+        for (int s2 = 0; s2 < c; ++s2) {
+            const int j = __builtin_amdgcn_readlane(Li, s2);
+            const double px = in64[3 * j], py = in64[3 * j + 1], pz = in64[3 * j + 2];
+            cu[0] += px;
+            cu[1] += py;
+            cu[2] += pz;
+            cu[3] += px * px;
+            cu[4] += px * py;
+            cu[5] += px * pz;
+            cu[6] += py * py;
+            cu[7] += py * pz;
+            cu[8] += pz * pz;
+        }
+        const double cn = (double)c;
+#pragma unroll
+        for (int t = 0; t < 9; ++t) cu[t] /= cn;
+        C.xx = cu[3] - cu[0] * cu[0];
+        C.yy = cu[6] - cu[1] * cu[1];
+        C.zz = cu[8] - cu[2] * cu[2];
+        C.xy = cu[4] - cu[0] * cu[1];
+        C.xz = cu[5] - cu[0] * cu[2];
+        C.yz = cu[7] - cu[1] * cu[2];
+    } else {
+        C = Sym3{1.0, 0.0, 0.0, 1.0, 0.0, 1.0};
+    }
+    if (lane == 0) {
+        double* out = rawcov6 + (size_t)o * 6;
+        out[0] = C.xx;
+        out[1] = C.xy;
+        out[2] = C.xz;
+        out[3] = C.yy;
+        out[4] = C.yz;
+        out[5] = C.zz;
+    }
+}
+
 hipError_t launch_knn_tiles(const CloudLayout& L, const double* in64, int k, double radius, double margin,
                             bool out_input_order, double* rawcov6, int32_t* nbr_idx, double* nbr_d2,
                             int32_t* nbr_cnt, hipStream_t s, double* mean_dist) {
     if (L.n <= 0) return hipSuccess;
     const double r2 = radius > 0 ? radius * radius : __builtin_huge_val();
+    static const bool lane_per_query = getenv("ORPCD_KNN_TILES") != nullptr;  // A/B: the lane-per-query kernel
+    if (!lane_per_query && k >= 1 && k <= 64) {
+        knn_wave_kernel<<<(unsigned)((L.n + 3) / 4), 256, 0, s>>>(
+            L.xyz64.p, L.perm.p, (int)L.n, L.tlo.p, L.thi.p, (int)L.ntiles, L.slo.p, L.shi.p, (int)L.nsuper, in64, r2,
+            (float)margin, k, out_input_order ? 1 : 0, rawcov6, nbr_idx, nbr_d2, nbr_cnt, mean_dist);
+        return hipGetLastError();
+    }
     const dim3 grid((unsigned)((L.ntiles + 3) / 4));
 #define ORPCD_KNN_TILES(KK)                                                                                      \
     knn_tiles_kernel<KK><<<grid, 256, 0, s>>>(L.xyz64.p, L.perm.p, (int)L.n, L.tlo.p, L.thi.p, (int)L.ntiles,   \

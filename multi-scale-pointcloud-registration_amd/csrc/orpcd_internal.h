@@ -128,7 +128,9 @@ struct VoxelBufs {  // preprocessing scratch (voxel, SOR, FPS)
     DevBuf<unsigned char> tmp, flag;
     DevBuf<double> xyz, out;
     DevBuf<int64_t> idx64;
+    DevBuf<unsigned long long> tag;
     void release() {
+        tag.release();
         flag.release();
         idx64.release();
         key.release();
@@ -271,7 +273,7 @@ hipError_t launch_voxel_down_sample(const double* xyz, int64_t n, const double v
 int fps_max_blocks(int device);
 int fps_points_per_thread(int64_t n, int max_blocks);
 hipError_t launch_fps(const double* xyz, int64_t n, int first, int k, int max_blocks, int64_t* out, double* bval,
-                      int32_t* bidx, unsigned* bar, hipStream_t s);
+                      unsigned long long* btag, unsigned* err, hipStream_t s);
 
 // gicp_kernels.hip
 int accum_blocks(int64_t N);

@@ -20,8 +20,8 @@
 //    cooperative launch runs all sample_size-1 steps: every thread keeps its
 //    points and their running minimum distance in registers; per step each
 //    block reduces (max distance, lowest index), publishes it, one grid
-//    barrier, then every block reduces the published values itself (no second
-//    barrier).  Distances are the reference's cdist Euclidean: differences,
+//    barrier (a step counter), then every block reduces the published values
+//    itself (no second barrier).  Distances are the reference's cdist Euclidean: differences,
 //    squares summed x, y, z in order, correctly rounded sqrt, contraction off.
 #include <hipcub/hipcub.hpp>
 
@@ -173,15 +173,15 @@ hipError_t launch_voxel_down_sample(const double* xyz, int64_t n, const double v
 }
 
 // ---------------------------------------------------------------- FPS
-constexpr int kFpsThreads = 256;
+constexpr int kFpsThreads = 1024;
 
 struct FpsArgs {
     const double* xyz;                  // n x 3, input order
     int n, first, k, per_block;         // per_block = P * kFpsThreads
     int64_t* out;                       // k chosen indices
-    double* bval;                       // 2 x gridDim.x published block maxima
-    int32_t* bidx;                      // 2 x gridDim.x their indices
-    unsigned* bar;                      // grid barrier counter (starts at 0)
+    double* bval;                       // 2 x gridDim.x published block maxima (by step parity)
+    unsigned long long* btag;           // 2 x gridDim.x: index of the maximum
+    unsigned* err;                      // [0] set when a wait exceeded its bound, [1] step counter
 };
 
 // (value, index) order of np.argmax: larger value, then lower index
@@ -219,10 +219,18 @@ __device__ __forceinline__ void fps_block_best(double& v, int& i, double* sv, in
     __syncthreads();
 }
 
+// Per step, block b publishes its maximum in slot (step & 1, b), then one
+// agent-scope add on the step counter (release); thread 0 of every block
+// waits for the counter to reach (step + 1) * G (acquire), and every block
+// reduces the G published values itself.  Double buffering by step parity is
+// safe: a block writes step s+2 only after every block has added for step
+// s+1, i.e. finished reading step s.  Large blocks (1024 threads) keep G, the
+// number of adders and of published values, small.  Waits are bounded.
 template <int P>
 __global__ __launch_bounds__(kFpsThreads) void fps_kernel(FpsArgs a) {
     __shared__ double sv[kFpsThreads / 64];
     __shared__ int si[kFpsThreads / 64];
+    __shared__ int timed_out;
     const int G = gridDim.x;
     const int base = blockIdx.x * a.per_block + threadIdx.x;
     double px[P], py[P], pz[P], d[P];
@@ -235,6 +243,7 @@ __global__ __launch_bounds__(kFpsThreads) void fps_kernel(FpsArgs a) {
         pz[s] = ok ? a.xyz[3 * i + 2] : 0.0;
         d[s] = ok ? 1e6 : -1.0;  // distances = np.ones((1, N)) * 1e6; padding never wins
     }
+    if (threadIdx.x == 0) timed_out = 0;
     int cur = a.first;
     if (blockIdx.x == 0 && threadIdx.x == 0) a.out[0] = cur;
     for (int step = 0; step + 1 < a.k; ++step) {
@@ -257,19 +266,30 @@ __global__ __launch_bounds__(kFpsThreads) void fps_kernel(FpsArgs a) {
         const int par = step & 1;
         if (threadIdx.x == 0) {
             __hip_atomic_store(&a.bval[par * G + blockIdx.x], bv, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_store(&a.bidx[par * G + blockIdx.x], bi, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_fetch_add(a.bar, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(&a.btag[par * G + blockIdx.x], (unsigned long long)(unsigned)bi, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_fetch_add(a.err + 1, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
             const unsigned target = (unsigned)(step + 1) * (unsigned)G;
-            while (__hip_atomic_load(a.bar, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) < target)
+            int spins = 0;
+            while (__hip_atomic_load(a.err + 1, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) < target) {
+                if (++spins > (1 << 22)) {  // a co-residency failure: give up loudly, never hang
+                    timed_out = 1;
+                    break;
+                }
                 __builtin_amdgcn_s_sleep(1);
+            }
         }
         __syncthreads();
-        // every block reduces the published maxima itself
+        if (timed_out) {  // block-uniform (shared, after the barrier)
+            if (threadIdx.x == 0) atomicExch(a.err, 1u);
+            return;
+        }
         bv = -2.0;
         bi = 0x7fffffff;
         for (int b = threadIdx.x; b < G; b += kFpsThreads) {
             const double w = __hip_atomic_load(&a.bval[par * G + b], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            const int j = __hip_atomic_load(&a.bidx[par * G + b], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const int j = (int)(unsigned)__hip_atomic_load(&a.btag[par * G + b], __ATOMIC_RELAXED,
+                                                            __HIP_MEMORY_SCOPE_AGENT);
             if (fps_better(w, j, bv, bi)) {
                 bv = w;
                 bi = j;
@@ -282,29 +302,27 @@ __global__ __launch_bounds__(kFpsThreads) void fps_kernel(FpsArgs a) {
 }
 
 int fps_points_per_thread(int64_t n, int max_blocks) {
-    for (int P : {1, 2, 4, 8, 16, 32})
+    for (int P : {1, 2, 4, 8})
         if ((int64_t)P * kFpsThreads * max_blocks >= n) return P;
     return 0;
 }
 
 hipError_t launch_fps(const double* xyz, int64_t n, int first, int k, int max_blocks, int64_t* out, double* bval,
-                      int32_t* bidx, unsigned* bar, hipStream_t s) {
+                      unsigned long long* btag, unsigned* err, hipStream_t s) {
     const int P = fps_points_per_thread(n, max_blocks);
     if (P == 0) return hipErrorInvalidValue;
     const int per_block = P * kFpsThreads;
     const int G = (int)((n + per_block - 1) / per_block);
-    hipError_t e = hipMemsetAsync(bar, 0, sizeof(unsigned), s);
+    hipError_t e = hipMemsetAsync(err, 0, 2 * sizeof(unsigned), s);
     if (e != hipSuccess) return e;
-    FpsArgs a{xyz, (int)n, first, k, per_block, out, bval, bidx, bar};
+    FpsArgs a{xyz, (int)n, first, k, per_block, out, bval, btag, err};
     void* args[] = {&a};
     const void* fn = nullptr;
     switch (P) {
         case 1: fn = (const void*)fps_kernel<1>; break;
         case 2: fn = (const void*)fps_kernel<2>; break;
         case 4: fn = (const void*)fps_kernel<4>; break;
-        case 8: fn = (const void*)fps_kernel<8>; break;
-        case 16: fn = (const void*)fps_kernel<16>; break;
-        default: fn = (const void*)fps_kernel<32>; break;
+        default: fn = (const void*)fps_kernel<8>; break;
     }
     return hipLaunchCooperativeKernel(fn, dim3((unsigned)G), dim3(kFpsThreads), args, 0, s);
 }
@@ -312,7 +330,7 @@ hipError_t launch_fps(const double* xyz, int64_t n, int first, int k, int max_bl
 int fps_max_blocks(int device) {
     int cus = 0, per_cu = 0;
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess) return 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)fps_kernel<32>, kFpsThreads, 0) !=
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)fps_kernel<8>, kFpsThreads, 0) !=
         hipSuccess)
         return 0;
     return per_cu >= 1 ? cus : 0;  // one block per CU: every block co-resident

@@ -801,13 +801,20 @@ int orpcd_farthest_downsample(orpcd_ctx* c, const double* xyz, int64_t n, int32_
     CTX_CHECK(c, c->vox.xyz.ensure((size_t)n * 3));
     CTX_CHECK(c, c->vox.idx64.ensure((size_t)sample_size));
     CTX_CHECK(c, c->scratch64c.ensure((size_t)2 * c->fps_blocks));
-    CTX_CHECK(c, c->scratch32.ensure((size_t)2 * c->fps_blocks + 2));
+    CTX_CHECK(c, c->vox.tag.ensure((size_t)2 * c->fps_blocks));
+    CTX_CHECK(c, c->scratch32.ensure(2));
     CTX_CHECK(c, hipMemcpyAsync(c->vox.xyz.p, xyz, (size_t)n * 24, hipMemcpyHostToDevice, s));
+    unsigned* err = reinterpret_cast<unsigned*>(c->scratch32.p);
     CTX_CHECK(c, launch_fps(c->vox.xyz.p, n, (int)first, sample_size, c->fps_blocks, c->vox.idx64.p,
-                            c->scratch64c.p, c->scratch32.p, reinterpret_cast<unsigned*>(c->scratch32.p +
-                                                                                         2 * c->fps_blocks), s));
+                            c->scratch64c.p, c->vox.tag.p, err, s));
+    unsigned herr = 0;
     CTX_CHECK(c, hipMemcpyAsync(idx_out, c->vox.idx64.p, (size_t)sample_size * 8, hipMemcpyDeviceToHost, s));
+    CTX_CHECK(c, hipMemcpyAsync(&herr, err, 4, hipMemcpyDeviceToHost, s));
     CTX_CHECK(c, hipStreamSynchronize(s));
+    if (herr) {
+        c->err = "farthest_downsample: blocks of the cooperative launch were not co-resident";
+        return ORPCD_EDEVICE;
+    }
     return ORPCD_OK;
 }
 
