@@ -180,3 +180,63 @@ def test_search_variants_identical(ctx, kernel):
         ctx.set_option("search_kernel", 0)
     assert np.array_equal(got["T"], ref["T"]) and np.array_equal(got["iters"], ref["iters"])
     assert np.array_equal(got["rmse"], ref["rmse"])
+
+
+def test_gicp_matches_g4_fixtures(ctx):
+    """The GPU GICP against the committed oracle traces G4 (300-pair and C1
+    with RandomDownsampler(5000) + SOR preprocessing)."""
+    import os
+    from conftest import GOLDEN
+    from make_golden_oracle import c1_pair
+    z = np.load(os.path.join(GOLDEN, "g45_oracle.npz"))
+    for name, (s, t) in {"p300": small_pair(300, seed=0), "c1": c1_pair()}.items():
+        ctx.set_target(t)
+        ctx.set_source(s)
+        r = ctx.gicp_batch(np.eye(3)[None], np.zeros((1, 3)))
+        assert np.abs(r["T"][0] - z[f"g4_{name}_T"]).max() <= T_TOL
+        assert abs(r["rmse"][0] - float(z[f"g4_{name}_rmse"])) <= RMSE_TOL
+        assert abs(int(r["iters"][0]) - int(z[f"g4_{name}_iters"])) <= 1
+
+
+def test_c1_preprocessing_on_gpu_matches_fixture_input():
+    """C1's preprocessing through the product blocks (RadiusScaler auto-inserted,
+    RandomDownsampler(5000), SOR on the GPU) gives the fixture's clouds exactly."""
+    from make_golden_oracle import c1_pair
+    from orpcd_amd.Preprocessor import Preprocessor
+    from orpcd_amd.Preprocessor.Downsamplers import RandomDownsampler
+    from orpcd_amd.Preprocessor.Outliers import SOR
+    from workloads import armadillo
+    src, tgt = armadillo()
+    np.random.seed(0)
+    s = Preprocessor([RandomDownsampler(5000), SOR()]).preprocess(src)
+    t = Preprocessor([RandomDownsampler(5000), SOR()]).preprocess(tgt)
+    es, et = c1_pair()
+    assert np.array_equal(s, es) and np.array_equal(t, et)
+
+
+def test_align_known_answer_anisotropic_scale(oracle):
+    """KAT (the reference's notes): target = source * diag(d0) rotated + t.
+    align() must find scale factors near 1/d0 and a small RMSE, and agree with
+    the oracle's Aligner."""
+    from orpcd_amd import Aligner, GeneralizedICP, Preprocessor
+    rng = np.random.default_rng(31)
+    src = workloads_bumpy(3000, rng) * np.array([1.0, 0.7, 0.5])
+    d0 = np.array([1.0, 1.25, 1.0])
+    tgt = (src * d0) @ rot_xyz(10, -5, 8).T + np.array([0.3, -0.2, 0.1])
+    np.random.seed(7)
+    al = Aligner(Preprocessor([]), Preprocessor([]), GeneralizedICP(), attempts=12)
+    T, metric, sf, errors = al.align(src, tgt, refine_registration=False)
+    np.random.seed(7)
+    oal = oracle.OracleAligner(oracle.OracleGeneralizedICP(), attempts=12)
+    To, mo, sfo, _ = oal.align(src, tgt)
+    assert np.array_equal(sf, sfo) and abs(metric - mo) <= 1e-5
+    assert metric < 0.05, (metric, sf)  # the compass stops at delta < eps = 0.05: scale error ~0.025
+    # RadiusScaler normalises each cloud by its own radius, so the recovered
+    # factors are 1/d0 up to one common factor
+    ratio = sf.ravel() * d0
+    assert np.abs(ratio / ratio[0] - 1.0).max() < 0.1
+
+
+def workloads_bumpy(n, rng):
+    from workloads import bumpy_sphere
+    return bumpy_sphere(n, rng)

@@ -138,3 +138,25 @@ def test_oracle_aligner_matches_reference_G3(oracle, mode, attempts, seed):
     assert np.array_equal(sf, g[f"{mode}_sf"]) and np.array_equal(err, g[f"{mode}_errors"])
     assert len(opt.calls) == len(g[f"{mode}_call_rmse"])
     assert np.array_equal(np.random.uniform(size=4), g[f"{mode}_rng_after"])
+
+
+def test_oracle_reproduces_g4_g5_regression_fixtures(oracle):
+    """G4/G5 (tests/golden/make_golden_oracle.py): the oracle's GICP traces and
+    FPFH/FGR outputs are stable across rounds (regression anchors, not Open3D)."""
+    import os
+    from conftest import GOLDEN
+    from make_golden_oracle import c1_pair, g5_pair
+    from workloads import small_pair
+    z = np.load(os.path.join(GOLDEN, "g45_oracle.npz"))
+    for name, (s, t) in {"p300": small_pair(300, seed=0), "c1": c1_pair()}.items():
+        r = oracle.gicp(s, t, 0.5, 100, trace=True)
+        assert np.allclose(r["T"], z[f"g4_{name}_T"], rtol=0, atol=1e-12)
+        assert r["iters"] == int(z[f"g4_{name}_iters"])
+        assert np.array_equal(r["trace_ncorr"], z[f"g4_{name}_trace_ncorr"])
+        assert np.allclose(r["trace_rmse"], z[f"g4_{name}_trace_rmse"], rtol=1e-12, atol=0)
+    s, t = g5_pair()
+    _, fs = oracle.fpfh(s)
+    assert np.allclose(fs, z["g5_src_feat"], rtol=0, atol=1e-9)
+    r = oracle.fgr(s, t, fs, z["g5_tgt_feat"], seed=0)
+    assert r["n_mutual"] == int(z["g5_n_mutual"]) and r["n_tuple_corr"] == int(z["g5_n_tuple"])
+    assert np.allclose(r["T"], z["g5_T"], rtol=0, atol=1e-12)
