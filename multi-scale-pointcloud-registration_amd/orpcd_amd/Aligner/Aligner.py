@@ -14,6 +14,13 @@ as one device batch, sharded over the ranks of an initialised
 records are replayed through the reference's selection loop in attempt order.
 Any other IOptimizer (including the reference's own) is called per attempt,
 exactly as the reference does.
+
+With a batched optimizer the compass search is also speculative
+(``speculative_compass=True``, keyword-only): each compass iteration draws the
+six candidates' RNG blocks up front, runs the six multistarts concurrently
+(one device context and stream each) and replays the reference's candidate
+order, so the results and the RNG stream are identical to the sequential
+search while the device runs the candidates side by side.
 """
 import copy
 import time
@@ -45,7 +52,8 @@ class Aligner:
     def __init__(self, source_preprocessor, target_preprocessor, optimizer: IOptimizer,
                  attempts: int = __MULTISTART_ATTEMPTS__, deg: float = __ALIGNER_DEG__, mu: float = __ALIGNER_MU__,
                  std: float = __ALIGNER_STD__, delta: float = __ALIGNER_DELTA__, max_iter: int = __ALIGNER_MAX_ITER__,
-                 eps: float = __ALIGNER_EPS__, visualize_intermediate_steps: bool = False):
+                 eps: float = __ALIGNER_EPS__, visualize_intermediate_steps: bool = False, *,
+                 speculative_compass: bool = True):
         self._LOG = LoggerFactory.get_logger(log_name=self.__class__.__name__)
         checks = [("attempts", attempts, lambda v: v <= 0, __MULTISTART_ATTEMPTS__),
                   ("deg", deg, lambda v: v <= 0, __ALIGNER_DEG__),
@@ -75,6 +83,8 @@ class Aligner:
         self.history: List[dict] = []
         self.last_refine = None
         self._refine_ctx = None  # device context for refine_registration when the optimizer has none
+        self._speculative_compass = speculative_compass
+        self.speculative_history: List[dict] = []  # candidates run ahead but not reached by the reference's order
 
     # ----------------------------------------------------------------- RNG
     def initialize_rotation(self) -> Tuple[np.ndarray, np.ndarray]:
@@ -117,28 +127,42 @@ class Aligner:
         T[:3, 3] = np.dot(t0, Tc[:3, :3]).ravel() + Tc[:3, 3]
         return T
 
-    def _multistart_batched(self, source, target):
-        B = self._attempts
+    def _draw_starts(self):
+        """The attempts' (R0, t0) in the reference's order, and the RNG state after each."""
         R0s, t0s, states = [], [], []
-        for _ in range(B):  # same draws, same order as the sequential loop
+        for _ in range(self._attempts):  # same draws, same order as the sequential loop
             R, t = self.initialize_rotation()
             R0s.append(R)
             t0s.append(t)
             states.append(np.random.get_state())
+        return R0s, t0s, states
+
+    def _run_tables(self, source, targets, draws):
+        """Per target k, the gathered per-attempt table of the starts draws[k]:
+        this rank runs its shard of every target's starts (concurrently when
+        the optimizer offers optimize_batch_multi), then one all-gather per
+        target."""
+        B = self._attempts
         rank, ws = parallel.world()
         lo, hi = parallel.shard(B, rank, ws)
-        t_start = time.perf_counter()
+        locals_ = [np.zeros((0, parallel.REC)) for _ in targets]
         if hi > lo:
-            local = parallel.pack(self._optimizer.optimize_batch(source, target, np.array(R0s[lo:hi]),
-                                                                 np.array(t0s[lo:hi])))
-        else:
-            local = np.zeros((0, parallel.REC))
-        table = parallel.unpack(parallel.allgather_records(local, B))
-        self.history.append(dict(B=B, seconds=time.perf_counter() - t_start, iters=int(table["iters"].sum()),
-                                 rmse=table["rmse"].copy()))
+            R0 = [np.array(d[0][lo:hi]) for d in draws]
+            t0 = [np.array(d[1][lo:hi]) for d in draws]
+            if len(targets) > 1 and hasattr(self._optimizer, "optimize_batch_multi"):
+                res = self._optimizer.optimize_batch_multi(source, targets, R0, t0)
+            else:
+                res = [self._optimizer.optimize_batch(source, tg, r, t) for tg, r, t in zip(targets, R0, t0)]
+            locals_ = [parallel.pack(r) for r in res]
+        return [parallel.unpack(parallel.allgather_records(loc, B)) for loc in locals_]
+
+    def _select(self, table, draw):
+        """Aligner.py:178-202 over a finished table, in attempt order: strict <,
+        ValueError (RNG left after the failing attempt's draw) on rmse == 0."""
+        R0s, t0s, states = draw
         metric = np.inf
         best_transformation = np.eye(4)
-        for n in range(B):
+        for n in range(self._attempts):
             current_metric = float(table["rmse"][n])
             if current_metric == 0 and hasattr(self._optimizer, "zero_rmse_message"):
                 # the reference raises inside optimize() of attempt n, before
@@ -149,6 +173,45 @@ class Aligner:
                 metric = current_metric
                 best_transformation = self._compose(R0s[n], t0s[n], table["T"][n])
         return best_transformation, metric
+
+    def _multistart_batched(self, source, target):
+        draw = self._draw_starts()
+        t_start = time.perf_counter()
+        table = self._run_tables(source, [target], [draw])[0]
+        self.history.append(dict(B=self._attempts, seconds=time.perf_counter() - t_start,
+                                 iters=int(table["iters"].sum()), rmse=table["rmse"].copy()))
+        return self._select(table, draw)
+
+    def _compass_iteration_speculative(self, source, target, scale_factors, optimal_metric):
+        """One compass iteration (Aligner.py:270-297) with all six candidates'
+        multistarts drawn up front (the RNG blocks the reference would draw if
+        it evaluated them all, in its candidate order +x, -x, +y, -y, +z, -z)
+        and run concurrently; the reference's decisions are then replayed in
+        order: the first candidate with metric <= optimal is accepted and
+        np.random is left exactly where the reference leaves it (after that
+        candidate's block, or at a failing attempt).  Results are identical to
+        the sequential compass; candidates after the accepted one are extra
+        device work (recorded in speculative_history)."""
+        directions = np.eye(3)
+        steps = [sign * self._delta * directions[:, axis] for axis in range(3) for sign in (1.0, -1.0)]
+        state0 = np.random.get_state()
+        draws = [self._draw_starts() for _ in steps]
+        t_start = time.perf_counter()
+        tables = self._run_tables(source, [target * (scale_factors + d) for d in steps], draws)
+        seconds = time.perf_counter() - t_start
+        np.random.set_state(state0)
+        new_metric = None
+        for k, (d, table, draw) in enumerate(zip(steps, tables, draws)):
+            np.random.set_state(draw[2][-1])  # as if the blocks up to k had been drawn in sequence
+            rec = dict(B=self._attempts, seconds=seconds / len(steps), iters=int(table["iters"].sum()),
+                       rmse=table["rmse"].copy())
+            self.history.append(rec)
+            T, new_metric = self._select(table, draw)
+            if new_metric <= optimal_metric:
+                self.speculative_history.extend(
+                    dict(B=self._attempts, iters=int(t["iters"].sum())) for t in tables[k + 1:])
+                return d, T, new_metric
+        return None, None, new_metric
 
     # -------------------------------------------------------------- compass
     def compass_step(self, source, target, scale_factors, delta):
@@ -170,8 +233,22 @@ class Aligner:
         self._LOG.info(f"Multi-start registration time: {time.time() - start}")
         errors = [optimal_metric]
         directions = np.eye(3)
+        # speculation needs an optimizer whose result is a pure function of its
+        # inputs and that can run several targets at once (optimize_batch_multi)
+        speculate = self._speculative_compass and hasattr(self._optimizer, "optimize_batch_multi")
         while self._delta >= self._eps and iteration <= self._max_iter:
             iteration += 1
+            if speculate:
+                step, new_rotation, new_metric = self._compass_iteration_speculative(
+                    source, target, optimal_scale_factors, optimal_metric)
+                if step is not None:
+                    optimal_metric = new_metric
+                    optimal_transformation = new_rotation
+                    optimal_scale_factors += step
+                    errors.append(new_metric)
+                if new_metric > optimal_metric:
+                    self._delta = self._delta / 2
+                continue
             for axis in range(3):
                 scale_plus = self._delta * directions[:, axis]
                 new_scale_factors, new_rotation, new_metric = self.compass_step(

@@ -143,3 +143,32 @@ def test_transfrom_matches_reference_formula():
     sc_s, sc_t = ps.preprocessor_blocks[0], pt.preprocessor_blocks[0]
     expect = (((src - sc_s.mean) / sc_s.scale) + [0.1, 0, 0]) / al.scale_factors * sc_t.scale + sc_t.mean
     assert np.allclose(al.transfrom(src), expect)
+
+
+class SpeculativeScripted(BatchedScripted):
+    """Adds optimize_batch_multi, which turns on the Aligner's speculative compass."""
+
+    def optimize_batch_multi(self, source, targets, R0s, t0s):
+        return [self.optimize_batch(source, tg, r, t) for tg, r, t in zip(targets, R0s, t0s)]
+
+
+@pytest.mark.parametrize("mode,attempts,seed", [("scripted", 4, 7), ("constant", 2, 3)])
+def test_speculative_compass_matches_reference_G3(mode, attempts, seed):
+    """The speculative compass (all six candidates drawn and run up front, the
+    reference's order replayed) reproduces the reference's align() exactly:
+    T, metric, scale factors, errors, the RNG position and delta (G3).  The
+    scripted optimizer is a pure function of its inputs in these modes."""
+    from orpcd_amd import Aligner, Preprocessor
+    from scripted import ScriptedOptimizer
+    g = np.load(f"{GOLDEN}/g3_aligner_trace.npz")
+    np.random.seed(seed)
+    opt = SpeculativeScripted(ScriptedOptimizer(g["goal"], mode=mode))
+    al = Aligner(Preprocessor([]), Preprocessor([]), opt, attempts=attempts)
+    T, m, sf, err = al.align(g["src"].copy(), g["tgt"].copy(), refine_registration=False)
+    assert np.array_equal(T, g[f"{mode}_T"]) and m == g[f"{mode}_metric"]
+    assert np.array_equal(sf, g[f"{mode}_sf"]) and np.array_equal(err, g[f"{mode}_errors"])
+    assert np.array_equal(np.random.uniform(size=4), g[f"{mode}_rng_after"])
+    assert al._delta == g[f"{mode}_delta_after"]
+    # the replayed multistarts are exactly the reference's calls, in order
+    assert len(al.history) * attempts == len(g[f"{mode}_call_rmse"])
+    assert np.array_equal(np.concatenate([h["rmse"] for h in al.history]), g[f"{mode}_call_rmse"])
