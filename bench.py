@@ -169,7 +169,12 @@ def main():
                          "launches": int(st["launches"]), "flop_per_pair": FLOP_PER_PAIR,
                          "pairs_per_launch": round(st["pairs"] / max(st["launches"], 1)),
                          "pairs_vs_bruteforce": round(st["pairs"] / max(st["passes"] * len(source) * len(target), 1),
-                                                      5)},
+                                                      5),
+                         # SURVEY §8d's brute-force count (8*N*M per start per pass) over the same kernel
+                         # time: what a brute-force search would have to sustain to match (not a roofline)
+                         "bruteforce_equivalent_tflops": round(
+                             8.0 * st["passes"] * len(source) * len(target) / max(st["launches"], 1)
+                             / (avg_ms * 1e-3) / 1e12, 1) if avg_ms > 0 else None},
             "cpu_baseline": cpu,
             "gicp_iterations": int(iters),
             "align": align_s,
