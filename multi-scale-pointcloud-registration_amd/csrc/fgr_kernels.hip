@@ -16,6 +16,9 @@
 // The tuple test (100 x ncorr draws of Open3D's global mt19937, stopping at
 // maximum_tuple_count) is RNG-sequential by construction and runs on the host
 // in runtime.hip.
+#include <cstdio>
+#include <cstdlib>
+
 #include <hipcub/hipcub.hpp>
 
 #include "device_math.h"
@@ -592,6 +595,13 @@ hipError_t launch_feat_nn(const double* Fq, const double* nq2, int64_t nq, const
     if ((e = hipcub::DeviceSelect::Flagged(b.tmp.p, tmp, hipcub::CountingInputIterator<int32_t>(0), b.flag.p,
                                            b.qidx.p, nsel, (int)nq, s)) != hipSuccess)
         return e;
+    if (getenv("ORPCD_TRACE")) {
+        int32_t h = 0;
+        if ((e = hipMemcpyAsync(&h, nsel, 4, hipMemcpyDeviceToHost, s)) != hipSuccess) return e;
+        if ((e = hipStreamSynchronize(s)) != hipSuccess) return e;
+        fprintf(stderr, "[orpcd] feat_nn: %lld queries, %lld targets, %d parts, %d flagged for the exact pass\n",
+                (long long)nq, (long long)nt, parts, h);
+    }
     const int len2 = (int)(((nt + kExactParts - 1) / kExactParts + kFT - 1) / kFT * kFT);
     feat_nn_kernel<true><<<dim3(gq, (unsigned)kExactParts), 256, 0, s>>>(Fq, nq2, (int)nq, b.qidx.p, nsel, b.thr.p,
                                                                         Ft, nt2, (int)nt, len2, dim, b.part_d.p,

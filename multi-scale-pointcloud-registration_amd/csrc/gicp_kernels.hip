@@ -109,7 +109,7 @@ __device__ __forceinline__ int culled_search(float4* stage, const float4* __rest
     float lb = inf;
     float4 a = make_float4(0.f, 0.f, 0.f, 0.f), b = a;
 #ifdef ORPCD_PHASES
-    unsigned long long ph_cull = 0, ph_rounds = 0, ph_tests = 0;
+    unsigned long long ph_cull = 0, ph_rounds = 0, ph_tests = 0, ph_impr = 0;
 #endif
     // the tile AABBs of the NEXT surviving super-tile are loaded while the
     // current round is tested and scanned (one round of load latency hidden)
@@ -241,6 +241,9 @@ __device__ __forceinline__ int culled_search(float4* stage, const float4* __rest
         }
         asm volatile("" ::: "memory");  // all reads of this tile precede the next stage write
         // a tile improves a query only if its masked d^2 is strictly smaller
+#ifdef ORPCD_PHASES
+        ph_impr += __any((m0 & kKeyMask) < (k0 & kKeyMask) || (m1 & kKeyMask) < (k1 & kKeyMask)) ? 1 : 0;
+#endif
         if ((m0 & kKeyMask) < (k0 & kKeyMask)) {
             k0 = m0;
             t0 = tile;
@@ -271,6 +274,7 @@ __device__ __forceinline__ int culled_search(float4* stage, const float4* __rest
         phase_cull_out[0] = ph_cull;
         phase_cull_out[1] = ph_rounds;
         phase_cull_out[2] = ph_tests;
+        phase_cull_out[3] = ph_impr;
     }
 #endif
     return visited;
@@ -360,7 +364,7 @@ __device__ __forceinline__ void nn_search_body(
 #ifdef ORPCD_PHASES
     const float wq = __uint_as_float(wave_umax(__float_as_uint(qx[0] + qy[1])));  // the query loads have landed
     const unsigned long long ph_t1 = __builtin_readcyclecounter() + (wq == 1.2345f ? 1 : 0);
-    unsigned long long ph_cull[3] = {0, 0, 0};
+    unsigned long long ph_cull[4] = {0, 0, 0, 0};
     const int visited = culled_search(stage_w, p4, tlo, thi, ntiles, slo, shi, nsuper, super_cull, S, split, qx,
                                       qy, qz, bound, bd, bj, ph_cull);
 #else
@@ -380,6 +384,7 @@ __device__ __forceinline__ void nn_search_body(
         atomicAdd(cs + 7, ph_cull[2]);      // per-query candidate tests
         atomicAdd(cs + 4, ph_t2 - ph_t1);   // search incl. culling
         atomicAdd(cs + 5, 1ull);            // waves
+        atomicAdd(cs + 8, ph_cull[3]);      // scanned tiles that improved some query of the wave
 #endif
     }
     unsigned long long* out = best + (size_t)slot * N;
