@@ -109,7 +109,7 @@ __device__ __forceinline__ int culled_search(float4* stage, const float4* __rest
     float lb = inf;
     float4 a = make_float4(0.f, 0.f, 0.f, 0.f), b = a;
 #ifdef ORPCD_PHASES
-    unsigned long long ph_cull = 0, ph_rounds = 0, ph_tests = 0, ph_impr = 0;
+    unsigned long long ph_cull = 0, ph_rounds = 0, ph_tests = 0, ph_impr = 0, ph_need = 0;
 #endif
     // the tile AABBs of the NEXT surviving super-tile are loaded while the
     // current round is tested and scanned (one round of load latency hidden)
@@ -181,9 +181,15 @@ __device__ __forceinline__ int culled_search(float4* stage, const float4* __rest
             const float hx = __uint_as_float(__builtin_amdgcn_readlane(__float_as_uint(b.x), k));
             const float hy = __uint_as_float(__builtin_amdgcn_readlane(__float_as_uint(b.y), k));
             const float hz = __uint_as_float(__builtin_amdgcn_readlane(__float_as_uint(b.z), k));
-            const bool need = box_d2(qx[0], qy[0], qz[0], lx, ly, lz, hx, hy, hz) < __uint_as_float(k0 & kKeyMask) ||
-                              box_d2(qx[1], qy[1], qz[1], lx, ly, lz, hx, hy, hz) < __uint_as_float(k1 & kKeyMask);
-            if (__any(need)) return tb + k;
+            const bool need0 = box_d2(qx[0], qy[0], qz[0], lx, ly, lz, hx, hy, hz) < __uint_as_float(k0 & kKeyMask);
+            const bool need1 = box_d2(qx[1], qy[1], qz[1], lx, ly, lz, hx, hy, hz) < __uint_as_float(k1 & kKeyMask);
+#ifdef ORPCD_PHASES
+            {
+                const unsigned long long b0 = __ballot(need0), b1 = __ballot(need1);
+                if (b0 | b1) ph_need += __builtin_popcountll(b0) + __builtin_popcountll(b1);
+            }
+#endif
+            if (__any(need0 || need1)) return tb + k;
         }
     };
 
@@ -275,6 +281,7 @@ __device__ __forceinline__ int culled_search(float4* stage, const float4* __rest
         phase_cull_out[1] = ph_rounds;
         phase_cull_out[2] = ph_tests;
         phase_cull_out[3] = ph_impr;
+        phase_cull_out[4] = ph_need;
     }
 #endif
     return visited;
@@ -364,7 +371,7 @@ __device__ __forceinline__ void nn_search_body(
 #ifdef ORPCD_PHASES
     const float wq = __uint_as_float(wave_umax(__float_as_uint(qx[0] + qy[1])));  // the query loads have landed
     const unsigned long long ph_t1 = __builtin_readcyclecounter() + (wq == 1.2345f ? 1 : 0);
-    unsigned long long ph_cull[4] = {0, 0, 0, 0};
+    unsigned long long ph_cull[5] = {0, 0, 0, 0, 0};
     const int visited = culled_search(stage_w, p4, tlo, thi, ntiles, slo, shi, nsuper, super_cull, S, split, qx,
                                       qy, qz, bound, bd, bj, ph_cull);
 #else
@@ -385,6 +392,7 @@ __device__ __forceinline__ void nn_search_body(
         atomicAdd(cs + 4, ph_t2 - ph_t1);   // search incl. culling
         atomicAdd(cs + 5, 1ull);            // waves
         atomicAdd(cs + 8, ph_cull[3]);      // scanned tiles that improved some query of the wave
+        atomicAdd(cs + 9, ph_cull[4]);      // queries whose own box test wanted the candidate tile
 #endif
     }
     unsigned long long* out = best + (size_t)slot * N;
