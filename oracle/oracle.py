@@ -1,8 +1,9 @@
 """TEST INFRASTRUCTURE ONLY — numpy/ctypes front-end of the CPU oracle.
 
 This module is the *checker* and the CPU baseline.  Only ``tests/``,
-``__graft_entry__.smoke()`` and ``bench.py``'s ``cpu_baseline`` leg may import
-it; the product package (``orpcd_amd``) never does.
+``__graft_entry__.smoke()``, ``bench.py``'s ``cpu_baseline`` leg and the
+measurement scripts under ``tools/`` (their CPU-baseline and parity legs) may
+import it; the product package (``orpcd_amd``) never does.
 
 It wraps ``oracle/build/liborpcd_oracle.so`` (a C++ restatement of the
 Open3D 0.18.0 algorithms the reference delegates to — see the header of

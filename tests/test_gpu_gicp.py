@@ -240,3 +240,50 @@ def test_align_known_answer_anisotropic_scale(oracle):
 def workloads_bumpy(n, rng):
     from workloads import bumpy_sphere
     return bumpy_sphere(n, rng)
+
+
+def test_gicp_full_c2_size_posed_starts_match_oracle(ctx, oracle):
+    """BASELINE configs[1] size (50k <-> 50k densified Armadillo, radius-scaled),
+    three of the bench's posed starts, run to convergence.
+
+    At this size the fp32 search meets near-ties: ~12 of 50k queries per pass
+    pick a different target than the fp64 oracle, every one a certified tie
+    (exact d^2 within 2e-5 relative).  Each such flip moves a far-off pose by
+    ~1e-5, so trajectories drift apart inside the basin, and the stopping test
+    (relative change < 1e-6) ends them at slightly different points of a flat
+    minimum.  Stated tolerance at full size: converged inlier RMSE within 1e-5
+    (north_star) and T within 2e-4 elementwise; per pass-0 query the chosen
+    neighbour is the oracle's or a certified tie."""
+    from workloads import c2_pair
+    from orpcd_amd import Preprocessor
+    s, t = c2_pair(50_000)
+    s = Preprocessor([]).preprocess(s)
+    t = Preprocessor([]).preprocess(t)
+    rng = np.random.default_rng(1000)
+    R0 = np.array([rot_xyz(*rng.uniform(-90, 90, 3)) for _ in range(3)])
+    t0 = rng.normal(size=(3, 3)) * 0.1
+    q = np.dot(s, R0[0]) + t0[0]
+    gi, _ = ctx.nn1_radius(q, t, 0.5)
+    oi, _ = oracle.nn1_radius(q, t, 0.5)
+    assert np.count_nonzero(gi != oi) <= 1e-3 * len(q)
+    _certified_nn(oi, gi, q, t)
+    ctx.set_target(t)
+    ctx.set_source(s)
+    r = ctx.gicp_batch(R0, t0)
+    for b in range(3):
+        o = oracle.gicp(np.dot(s, R0[b]) + t0[b], t, 0.5, 100)
+        assert abs(r["rmse"][b] - o["rmse"]) <= 1e-5, (b, r["rmse"][b], o["rmse"])
+        assert np.abs(r["T"][b] - o["T"]).max() <= 2e-4, (b, np.abs(r["T"][b] - o["T"]).max())
+        assert abs(r["fitness"][b] - o["fitness"]) <= 1e-3
+
+
+def test_gicp_full_c5_size_two_passes_match_oracle(ctx, oracle):
+    """SURVEY §8d C5 size (1M <-> 1M, near-aligned pair): two GICP passes
+    against the oracle at the per-optimize tolerance."""
+    from workloads import c5_pair
+    s, t = c5_pair()
+    ctx.set_target(t)
+    ctx.set_source(s)
+    r = ctx.gicp_batch(np.eye(3)[None], np.zeros((1, 3)), max_iteration=2)
+    o = oracle.gicp(s, t, 0.5, 2)
+    _cmp_gicp(dict(T=r["T"][0], rmse=r["rmse"][0], fitness=r["fitness"][0], iters=r["iters"][0]), o, 0)
