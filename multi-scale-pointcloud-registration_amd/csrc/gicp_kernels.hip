@@ -65,16 +65,17 @@ constexpr unsigned long long kNone = ~0ull;
 constexpr int kNoSeed = -1;   // prevnn before the first pass (representative seed)
 constexpr int kNoMatch = -2;  // no target within the search radius last pass
 constexpr unsigned kKeyMask = 0xFFFFFFC0u;  // d^2 bits kept in a scan key (low 6 = tile-local index)
+constexpr float kQuarterSlack = 1.0f - 1.0f / 1048576.0f;  // quarter test: box d^2 x (1 - 2^-20) vs the bound
 
 // --------------------------------------------------------------------------
 // Culled exact nearest search for the 2 queries of every lane of one wave,
 // restricted to tiles t with t % S == s.  bound[] enters as the per-query
-// bound on d^2 (<= 0: invalid query).  Returns tiles scanned; bj[] = Morton
+// bound on d^2 (<= 0: invalid query).  Returns quarters scanned; bj[] = Morton
 // index of the chosen target or -1, bd[] its fp32 d^2 (key-truncated).
 // --------------------------------------------------------------------------
 __device__ __forceinline__ int culled_search(float4* stage, const float4* __restrict__ p4,
                                              const float4* __restrict__ tlo, const float4* __restrict__ thi,
-                                             int ntiles, const float4* __restrict__ slo,
+                                             const float4* __restrict__ qbox, int ntiles, const float4* __restrict__ slo,
                                              const float4* __restrict__ shi, int nsuper, int super_cull, int S, int s,
                                              const float qx[2], const float qy[2],
                                              const float qz[2], const float bound[2], float bd[2], int bj[2],
@@ -207,43 +208,66 @@ __device__ __forceinline__ int culled_search(float4* stage, const float4* __rest
     // while the current tile is scanned out of LDS
     float lbn = inf;
     int nxt = next_candidate(lbn);
-    float4 pre = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (nxt >= 0) pre = p4[nxt * kTile + lane];
+    float4 pre = make_float4(0.f, 0.f, 0.f, 0.f), preq = pre;
+    if (nxt >= 0) {
+        pre = p4[nxt * kTile + lane];
+        if (lane < 8) preq = qbox[nxt * 8 + lane];
+    }
     while (nxt >= 0) {
         const int tile = __builtin_amdgcn_readfirstlane(nxt);
-        // SoA stage: x[64] | y[64] | z[64]; a ds_read_b64 yields two targets'
-        // coordinate, already an aligned register pair for v_pk_* math
+        // SoA stage: x[64] | y[64] | z[64] | quarter boxes (lo x4, hi x4); a
+        // ds_read_b64 yields two targets' coordinate, already an aligned
+        // register pair for v_pk_* math
         float* sx = reinterpret_cast<float*>(stage);
         sx[lane] = pre.x;
         sx[64 + lane] = pre.y;
         sx[128 + lane] = pre.z;
+        if (lane < 8) reinterpret_cast<float4*>(sx + 192)[lane] = preq;
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         nxt = next_candidate(lbn);
-        if (nxt >= 0) pre = p4[nxt * kTile + lane];
+        if (nxt >= 0) {
+            pre = p4[nxt * kTile + lane];
+            if (lane < 8) preq = qbox[nxt * 8 + lane];
+        }
         unsigned m0 = 0xFFFFFFFFu, m1 = 0xFFFFFFFFu;
         const f2 qx0 = {qx[0], qx[0]}, qy0 = {qy[0], qy[0]}, qz0 = {qz[0], qz[0]};
         const f2 qx1 = {qx[1], qx[1]}, qy1 = {qy[1], qy[1]}, qz1 = {qz[1], qz[1]};
+        const float4* qb = reinterpret_cast<const float4*>(sx + 192);
 #pragma unroll
-        for (int kk = 0; kk < kTile; kk += 2) {
-            const f2 tx = *reinterpret_cast<const f2*>(sx + kk);
-            const f2 ty = *reinterpret_cast<const f2*>(sx + 64 + kk);
-            const f2 tz = *reinterpret_cast<const f2*>(sx + 128 + kk);
-            f2 dx = qx0 - tx, dy = qy0 - ty, dz = qz0 - tz;  // query 0 vs targets kk, kk+1
-            f2 d0 = dx * dx;
-            d0 = pk_fma(dy, dy, d0);
-            d0 = pk_fma(dz, dz, d0);
-            dx = qx1 - tx;
-            dy = qy1 - ty;
-            dz = qz1 - tz;  // query 1
-            f2 d1 = dx * dx;
-            d1 = pk_fma(dy, dy, d1);
-            d1 = pk_fma(dz, dz, d1);
-            const unsigned a0 = (__float_as_uint(d0.x) & kKeyMask) | (unsigned)kk;
-            const unsigned c0 = (__float_as_uint(d0.y) & kKeyMask) | (unsigned)(kk + 1);
-            const unsigned a1 = (__float_as_uint(d1.x) & kKeyMask) | (unsigned)kk;
-            const unsigned c1 = (__float_as_uint(d1.y) & kKeyMask) | (unsigned)(kk + 1);
-            m0 = min(m0, min(a0, c0));
-            m1 = min(m1, min(a1, c1));
+        for (int qd = 0; qd < kTile / kQuarter; ++qd) {
+            // a quarter is scanned only if some query's box distance to it is
+            // below that query's bound (including this tile's earlier
+            // quarters); the 2^-20 slack keeps the test conservative against
+            // the scan's own fp32 rounding
+            const float4 lo = qb[qd], hi = qb[4 + qd];
+            const float b0 = __uint_as_float((k0 < m0 ? k0 : m0) & kKeyMask);
+            const float b1 = __uint_as_float((k1 < m1 ? k1 : m1) & kKeyMask);
+            const bool need = box_d2(qx[0], qy[0], qz[0], lo.x, lo.y, lo.z, hi.x, hi.y, hi.z) * kQuarterSlack < b0 ||
+                              box_d2(qx[1], qy[1], qz[1], lo.x, lo.y, lo.z, hi.x, hi.y, hi.z) * kQuarterSlack < b1;
+            if (!__any(need)) continue;
+            ++visited;
+#pragma unroll
+            for (int kk = qd * kQuarter; kk < (qd + 1) * kQuarter; kk += 2) {
+                const f2 tx = *reinterpret_cast<const f2*>(sx + kk);
+                const f2 ty = *reinterpret_cast<const f2*>(sx + 64 + kk);
+                const f2 tz = *reinterpret_cast<const f2*>(sx + 128 + kk);
+                f2 dx = qx0 - tx, dy = qy0 - ty, dz = qz0 - tz;  // query 0 vs targets kk, kk+1
+                f2 d0 = dx * dx;
+                d0 = pk_fma(dy, dy, d0);
+                d0 = pk_fma(dz, dz, d0);
+                dx = qx1 - tx;
+                dy = qy1 - ty;
+                dz = qz1 - tz;  // query 1
+                f2 d1 = dx * dx;
+                d1 = pk_fma(dy, dy, d1);
+                d1 = pk_fma(dz, dz, d1);
+                const unsigned a0 = (__float_as_uint(d0.x) & kKeyMask) | (unsigned)kk;
+                const unsigned c0 = (__float_as_uint(d0.y) & kKeyMask) | (unsigned)(kk + 1);
+                const unsigned a1 = (__float_as_uint(d1.x) & kKeyMask) | (unsigned)kk;
+                const unsigned c1 = (__float_as_uint(d1.y) & kKeyMask) | (unsigned)(kk + 1);
+                m0 = min(m0, min(a0, c0));
+                m1 = min(m1, min(a1, c1));
+            }
         }
         asm volatile("" ::: "memory");  // all reads of this tile precede the next stage write
         // a tile improves a query only if its masked d^2 is strictly smaller
@@ -258,13 +282,15 @@ __device__ __forceinline__ int culled_search(float4* stage, const float4* __rest
             k1 = m1;
             t1 = tile;
         }
-        ++visited;
         Wk = wave_umax((k0 > k1 ? k0 : k1) & kKeyMask);
         W = __uint_as_float(Wk);
         // the prefetched candidate was chosen under the previous bound: re-test
         while (nxt >= 0 && !(lbn < W)) {
             nxt = next_candidate(lbn);
-            if (nxt >= 0) pre = p4[nxt * kTile + lane];
+            if (nxt >= 0) {
+                pre = p4[nxt * kTile + lane];
+                if (lane < 8) preq = qbox[nxt * 8 + lane];
+            }
         }
     }
     if (t0 >= 0) {
@@ -315,7 +341,9 @@ __global__ __launch_bounds__(256) void xform_queries_kernel(const double* __rest
                                                             const float4* __restrict__ p4, int ntiles,
                                                             int seed_stride, const int32_t* __restrict__ prevnn,
                                                             float r2s, int reseed, float4* __restrict__ q32,
-                                                            unsigned long long* __restrict__ best) {
+                                                            unsigned long long* __restrict__ best,
+                                                            const int32_t* __restrict__ nact_dev) {
+    if (nact_dev && (int)blockIdx.y >= *nact_dev) return;  // pipelined: grid sized for an upper bound
     const int slot = active[blockIdx.y];
     if (done[slot]) return;
     const int i = blockIdx.x * 256 + threadIdx.x;
@@ -344,7 +372,7 @@ __global__ __launch_bounds__(256) void xform_queries_kernel(const double* __rest
 // --------------------------------------------------------------------------
 __device__ __forceinline__ void nn_search_body(
     const float4* __restrict__ q32, int N, const float4* __restrict__ p4, const float4* __restrict__ tlo,
-    const float4* __restrict__ thi, int ntiles, const float4* __restrict__ slo, const float4* __restrict__ shi,
+    const float4* __restrict__ thi, const float4* __restrict__ qbox, int ntiles, const float4* __restrict__ slo, const float4* __restrict__ shi,
     int nsuper, int super_cull, const int32_t* __restrict__ active, const int32_t* __restrict__ done, int S,
     unsigned long long* __restrict__ best, unsigned long long* __restrict__ counters, int by, int bx, int wid,
     float4* stage_w) {
@@ -372,11 +400,11 @@ __device__ __forceinline__ void nn_search_body(
     const float wq = __uint_as_float(wave_umax(__float_as_uint(qx[0] + qy[1])));  // the query loads have landed
     const unsigned long long ph_t1 = __builtin_readcyclecounter() + (wq == 1.2345f ? 1 : 0);
     unsigned long long ph_cull[5] = {0, 0, 0, 0, 0};
-    const int visited = culled_search(stage_w, p4, tlo, thi, ntiles, slo, shi, nsuper, super_cull, S, split, qx,
+    const int visited = culled_search(stage_w, p4, tlo, thi, qbox, ntiles, slo, shi, nsuper, super_cull, S, split, qx,
                                       qy, qz, bound, bd, bj, ph_cull);
 #else
     const int visited =
-        culled_search(stage_w, p4, tlo, thi, ntiles, slo, shi, nsuper, super_cull, S, split, qx, qy, qz, bound,
+        culled_search(stage_w, p4, tlo, thi, qbox, ntiles, slo, shi, nsuper, super_cull, S, split, qx, qy, qz, bound,
                       bd, bj);
 #endif
     if (lane == 0 && counters) {  // spread over kCounterSlots cache lines (one address serialises)
@@ -414,22 +442,51 @@ __device__ __forceinline__ void nn_search_body(
 // (74 VGPRs, no spills).
 #define ORPCD_NN_SEARCH_ARGS                                                                                   \
     const float4 *__restrict__ q32, int N, const float4 *__restrict__ p4, const float4 *__restrict__ tlo,    \
-        const float4 *__restrict__ thi, int ntiles, const float4 *__restrict__ slo,                          \
+        const float4 *__restrict__ thi, const float4 *__restrict__ qbox, int ntiles, const float4 *__restrict__ slo,                          \
         const float4 *__restrict__ shi, int nsuper, int super_cull, const int32_t *__restrict__ active,      \
         const int32_t *__restrict__ done, int S, unsigned long long *__restrict__ best,                      \
-        unsigned long long *__restrict__ counters
+        unsigned long long *__restrict__ counters, const int32_t *__restrict__ nact_dev, int sblk, int want
+
+// Block -> (start, query group x split).  Unpipelined: the grid is
+// (sblk * S, running starts) as the host counted them.  Pipelined (nact_dev):
+// a 1-D grid sized for an upper bound of the running starts; the device's
+// count sets the splits, S = ceil(want / (nact * sblk * waves)) capped at 64
+// and at what the grid holds, and the surplus blocks exit.
+__device__ __forceinline__ bool map_search_block(const int32_t* __restrict__ nact_dev, int sblk, int want, int& by,
+                                                 int& bx, int& S) {
+    if (!nact_dev) {
+        by = blockIdx.y;
+        bx = blockIdx.x;
+        return true;
+    }
+    const int nact = *nact_dev;
+    if (nact <= 0) return false;
+    const int per = nact * sblk;
+    const int waves = per * kCWaves;
+    S = min(min(64, max(1, (int)gridDim.x / per)), max(1, (want + waves - 1) / waves));
+    const int b = blockIdx.x;
+    if (b >= per * S) return false;
+    by = b / (sblk * S);
+    bx = b - by * (sblk * S);
+    return true;
+}
+
 __global__ __launch_bounds__(kCBlock) void nn_search_kernel(ORPCD_NN_SEARCH_ARGS) {
     __shared__ float4 stage[kCWaves][kTile];
     const int wid = threadIdx.x >> 6;
-    nn_search_body(q32, N, p4, tlo, thi, ntiles, slo, shi, nsuper, super_cull, active, done, S, best, counters,
-                   blockIdx.y, blockIdx.x, wid, stage[wid]);
+    int by, bx;
+    if (!map_search_block(nact_dev, sblk, want, by, bx, S)) return;
+    nn_search_body(q32, N, p4, tlo, thi, qbox, ntiles, slo, shi, nsuper, super_cull, active, done, S, best, counters,
+                   by, bx, wid, stage[wid]);
 }
 __global__ __launch_bounds__(kCBlock) __attribute__((amdgpu_waves_per_eu(6, 8))) void nn_search_kernel_o6(
     ORPCD_NN_SEARCH_ARGS) {
     __shared__ float4 stage[kCWaves][kTile];
     const int wid = threadIdx.x >> 6;
-    nn_search_body(q32, N, p4, tlo, thi, ntiles, slo, shi, nsuper, super_cull, active, done, S, best, counters,
-                   blockIdx.y, blockIdx.x, wid, stage[wid]);
+    int by, bx;
+    if (!map_search_block(nact_dev, sblk, want, by, bx, S)) return;
+    nn_search_body(q32, N, p4, tlo, thi, qbox, ntiles, slo, shi, nsuper, super_cull, active, done, S, best, counters,
+                   by, bx, wid, stage[wid]);
 }
 #undef ORPCD_NN_SEARCH_ARGS
 
@@ -626,8 +683,8 @@ __global__ __launch_bounds__(1024) void nn_search_coop_kernel(
             atomicMin(&sh.mb[lane + 64 * k], ((unsigned long long)(kk[k] & kKeyMask) << 32) | (unsigned)jj[k]);
     if (lane == 0 && counters) {
         unsigned long long* cs = counters + kCounterStride * ((blockIdx.x * W + wid + blockIdx.y) % kCounterSlots);
-        atomicAdd(cs, (unsigned long long)visited);
-        atomicMax(cs + 1, (unsigned long long)visited);
+        atomicAdd(cs, 4ull * visited);  // full tiles: 4 quarters each
+        atomicMax(cs + 1, 4ull * visited);
     }
     __syncthreads();
     if (wid == 0) {
@@ -948,8 +1005,8 @@ __global__ __launch_bounds__(256) void scan_items_kernel(const float4* __restric
     merge();
     if (lane == 0 && counters) {
         unsigned long long* cs = counters + kCounterStride * ((blockIdx.x * 4 + wid) % kCounterSlots);
-        atomicAdd(cs, (unsigned long long)visited);
-        atomicMax(cs + 1, (unsigned long long)visited);
+        atomicAdd(cs, 4ull * visited);  // full tiles: 4 quarters each
+        atomicMax(cs + 1, 4ull * visited);
     }
 }
 
@@ -990,7 +1047,9 @@ __device__ __forceinline__ double wave_sum_fixed(double v) {
 }
 
 // Block reduction of NV per-thread values into partial[slot, block][slot_of(v)].
-template <int NV, typename SlotOf>
+// kSc1: the partial is stored write-through (sc1), to be read in the same
+// launch by the start's last-arriving block (pipelined passes).
+template <int NV, bool kSc1 = false, typename SlotOf>
 __device__ __forceinline__ void block_partial(const double* acc, double (*red)[NV], SlotOf slot_of,
                                               double* __restrict__ out) {
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
@@ -1005,16 +1064,188 @@ __device__ __forceinline__ void block_partial(const double* acc, double (*red)[N
 #pragma unroll
         for (int v = 0; v < NV; ++v)
             if (slot_of(v) == (int)threadIdx.x) s = ((red[0][v] + red[1][v]) + red[2][v]) + red[3][v];
-        out[threadIdx.x] = s;
+        if (kSc1)
+            __hip_atomic_store(reinterpret_cast<unsigned long long*>(out) + threadIdx.x,
+                               (unsigned long long)__double_as_longlong(s), __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+        else
+            out[threadIdx.x] = s;
     }
 }
 
+// Fixed-order reduction of one start's block partials (lane-strided, then
+// the wave).  kSc1: the partials were stored sc1 in this launch and are read
+// with sc1 loads (L1 bypassed) behind the caller's agent acquire.
+template <bool kSc1 = false>
+__device__ __forceinline__ void reduce_partials(const double* __restrict__ partial, int slot, int nblk,
+                                                double s[kNacc]) {
+    const int lane = threadIdx.x & 63;
+#pragma unroll
+    for (int v = 0; v < kNacc; ++v) s[v] = 0.0;
+    for (int b = lane; b < nblk; b += 64) {
+        const double* pp = partial + ((size_t)slot * nblk + b) * kPartialStride;
+#pragma unroll
+        for (int v = 0; v < kNacc; ++v) {
+            if (kSc1)
+                s[v] += __longlong_as_double((long long)__hip_atomic_load(
+                    reinterpret_cast<const unsigned long long*>(pp) + v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+            else
+                s[v] += pp[v];
+        }
+    }
+#pragma unroll
+    for (int v = 0; v < kNacc; ++v) s[v] = wave_sum_fixed(s[v]);
+}
+
+struct SolveArgs {
+    double* T;
+    double* Q;
+    double* R;
+    const double* G;
+    double* prev;
+    int32_t* done;
+    double* out_fit;
+    double* out_rmse;
+    int32_t* out_iters;
+    int64_t* out_ncorr;
+};
+
+// --------------------------------------------------------------------------
+// One start's convergence test (RegistrationICP), 6x6 solve (or Umeyama) and
+// pose update from its 29 reduced sums.  Lane 0 only.  done[] is stored sc1:
+// the pipelined pass compacts the running starts in the same launch.
+// --------------------------------------------------------------------------
+template <int kEst>  // 0: GeneralizedICP, 1: PointToPoint
+__device__ void solve_start(int slot, const double s[kNacc], int64_t N, int pass, int max_iter, double rel_fit,
+                            double rel_rmse, const SolveArgs& a) {
+    const double cnt = s[28];
+    const double fit = cnt > 0 ? cnt / (double)N : 0.0;
+    const double rmse = cnt > 0 ? sqrt(s[27] / cnt) : 0.0;
+    const double pf = a.prev[2 * slot], pr = a.prev[2 * slot + 1];
+    const bool converged = pass >= 1 && fabs(pf - fit) < rel_fit && fabs(pr - rmse) < rel_rmse;
+    if (converged || pass >= max_iter) {
+        a.out_fit[slot] = fit;
+        a.out_rmse[slot] = rmse;
+        a.out_iters[slot] = pass;
+        a.out_ncorr[slot] = (int64_t)cnt;
+        __hip_atomic_store(a.done + slot, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        return;
+    }
+    a.prev[2 * slot] = fit;
+    a.prev[2 * slot + 1] = rmse;
+
+    double upd[16] = {1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1};
+    if (cnt > 0 && kEst == 1) {
+        umeyama_from_moments(s, cnt, upd);
+    } else if (cnt > 0) {
+        double JTJ[36], b[6];
+        for (int r = 0; r < 6; ++r)
+            for (int c = 0; c < 6; ++c) JTJ[6 * r + c] = r <= c ? s[ut(r, c)] : s[ut(c, r)];
+        for (int r = 0; r < 6; ++r) b[r] = -s[21 + r];
+        const double det = det6(JTJ);
+        if (!(fabs(det) < 1e-6 || isnan(det) || isinf(det))) {
+            double x[6];
+            ldlt_solve6(JTJ, b, x);
+            vec6_to_m4(x, upd);
+        }
+    }
+    double Tcur[16], Tn[16];
+    for (int t = 0; t < 16; ++t) Tcur[t] = a.T[16 * slot + t];
+    m4_mul(upd, Tcur, Tn);
+    for (int t = 0; t < 16; ++t) a.T[16 * slot + t] = Tn[t];
+    // Q = Tn * [G; 0 0 0 1]  (3x4), R = Tn[:3,:3]
+    const double* G = a.G + 12 * slot;
+    for (int r = 0; r < 3; ++r) {
+        for (int c = 0; c < 4; ++c) {
+            double v = Tn[4 * r + 0] * G[c] + Tn[4 * r + 1] * G[4 + c] + Tn[4 * r + 2] * G[8 + c];
+            if (c == 3) v += Tn[4 * r + 3];
+            a.Q[12 * slot + 4 * r + c] = v;
+        }
+        for (int c = 0; c < 3; ++c) a.R[9 * slot + 3 * r + c] = Tn[4 * r + c];
+    }
+}
+
+// --------------------------------------------------------------------------
+// Pipelined passes: the host enqueues passes without waiting; the device
+// keeps the list of running starts.
+//   ctl[0]       running starts (active[0 .. ctl[0]) ), read by every kernel
+//                of the next pass to map its blocks
+//   ctl[1]       starts solved in the current pass
+//   ctl[2+slot]  accumulation blocks of the start that have arrived
+//   progress     host-mapped word: (passes completed << 32) | running starts
+// The last-arriving accumulation block of a start reduces the partials and
+// solves (in the order of icp_solve_kernel: identical results); the block
+// that solves the pass's last start compacts active[] and publishes.
+// Hand-offs (MI355X_MICROARCH.md, inter-workgroup visibility): sc1 partial and
+// done[] stores, every storing wave drained, then one relaxed agent atomic;
+// the last arriver takes an agent acquire before its sc1 loads.
+// --------------------------------------------------------------------------
+struct PassCtl {
+    int32_t* ctl;
+    unsigned long long* progress;
+    int32_t* active;
+    int pass, max_iter;
+    double rel_fit, rel_rmse;
+    int64_t N;
+    SolveArgs a;
+};
+
+template <int kEst>
+__device__ __forceinline__ void finish_pass(int slot, int nact, const double* __restrict__ partial, int nblk,
+                                            const PassCtl& pc) {
+    __shared__ int last;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's sc1 partial stores have landed
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const int t = __hip_atomic_fetch_add(pc.ctl + 2 + slot, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        last = t == nblk - 1;
+    }
+    __syncthreads();
+    if (!last || threadIdx.x >= 64) return;
+    // wave 0 of the start's last block
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const int lane = threadIdx.x;
+    double s[kNacc];
+    reduce_partials<true>(partial, slot, nblk, s);
+    int last_solve = 0;
+    if (lane == 0) {
+        pc.ctl[2 + slot] = 0;  // for the next pass (read after the launch boundary)
+        solve_start<kEst>(slot, s, pc.N, pc.pass, pc.max_iter, pc.rel_fit, pc.rel_rmse, pc.a);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // done[slot] (sc1) has landed
+        last_solve = __hip_atomic_fetch_add(pc.ctl + 1, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == nact - 1;
+    }
+    if (!__builtin_amdgcn_readfirstlane(last_solve)) return;
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    // compact the running starts in place, order kept
+    int k = 0;
+    for (int b0 = 0; b0 < nact; b0 += 64) {
+        const int b = b0 + lane;
+        const int sl = b < nact ? pc.active[b] : -1;
+        const bool run = sl >= 0 && __hip_atomic_load(pc.a.done + sl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0;
+        const unsigned long long m = __ballot(run);
+        const int pos = k + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m, 0));
+        if (run) pc.active[pos] = sl;  // pos <= b: every lane read its entry before any write of this round
+        k += __builtin_popcountll(m);
+    }
+    if (lane == 0) {
+        pc.ctl[0] = k;
+        pc.ctl[1] = 0;
+        __hip_atomic_store(pc.progress, ((unsigned long long)(pc.pass + 1) << 32) | (unsigned)k, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+}
+
+template <bool kFused>
 __global__ __launch_bounds__(256) void gicp_accum_kernel(
     const double* __restrict__ src, const double* __restrict__ scov, int N, const double* __restrict__ tgt64,
     const double* __restrict__ tcov, const int32_t* __restrict__ active, const double* __restrict__ Qm,
     const double* __restrict__ Rm, const int32_t* __restrict__ done, double r2,
     const unsigned long long* __restrict__ best, int32_t* __restrict__ prevnn, double* __restrict__ partial,
-    int nblk) {
+    int nblk, PassCtl pc) {
+    const int nact = kFused ? pc.ctl[0] : 0;
+    if (kFused && (int)blockIdx.y >= nact) return;
     const int slot = active[blockIdx.y];
     if (done[slot]) return;
     __shared__ double red[4][kNacc];
@@ -1085,8 +1316,9 @@ __global__ __launch_bounds__(256) void gicp_accum_kernel(
         acc[27] += d2;
         acc[28] += 1.0;
     }
-    block_partial<kNacc>(acc, red, [](int v) { return v; },
-                         partial + ((size_t)slot * nblk + blockIdx.x) * kPartialStride);
+    block_partial<kNacc, kFused>(acc, red, [](int v) { return v; },
+                                 partial + ((size_t)slot * nblk + blockIdx.x) * kPartialStride);
+    if constexpr (kFused) finish_pass<kEstGICP>(slot, nact, partial, nblk, pc);
 }
 
 // PointToPoint accumulation (TransformationEstimationPointToPoint, Eigen::
@@ -1096,6 +1328,7 @@ __global__ __launch_bounds__(256) void gicp_accum_kernel(
 constexpr int kP2PTerms = 17;
 __device__ __forceinline__ int p2p_slot(int v) { return v < 15 ? v : 12 + v; }  // 15 -> 27, 16 -> 28
 
+template <bool kFused>
 __global__ __launch_bounds__(256) void p2p_accum_kernel(const double* __restrict__ src, int N,
                                                         const double* __restrict__ tgt64,
                                                         const int32_t* __restrict__ active,
@@ -1103,7 +1336,9 @@ __global__ __launch_bounds__(256) void p2p_accum_kernel(const double* __restrict
                                                         const int32_t* __restrict__ done, double r2,
                                                         const unsigned long long* __restrict__ best,
                                                         int32_t* __restrict__ prevnn, double* __restrict__ partial,
-                                                        int nblk) {
+                                                        int nblk, PassCtl pc) {
+    const int nact = kFused ? pc.ctl[0] : 0;
+    if (kFused && (int)blockIdx.y >= nact) return;
     const int slot = active[blockIdx.y];
     if (done[slot]) return;
     __shared__ double red[4][kP2PTerms];
@@ -1137,43 +1372,19 @@ __global__ __launch_bounds__(256) void p2p_accum_kernel(const double* __restrict
         acc[15] += d2;
         acc[16] += 1.0;
     }
-    block_partial<kP2PTerms>(acc, red, p2p_slot, partial + ((size_t)slot * nblk + blockIdx.x) * kPartialStride);
+    block_partial<kP2PTerms, kFused>(acc, red, p2p_slot,
+                                     partial + ((size_t)slot * nblk + blockIdx.x) * kPartialStride);
+    if constexpr (kFused) finish_pass<kEstP2P>(slot, nact, partial, nblk, pc);
 }
-
-struct SolveArgs {
-    double* T;
-    double* Q;
-    double* R;
-    const double* G;
-    double* prev;
-    int32_t* done;
-    double* out_fit;
-    double* out_rmse;
-    int32_t* out_iters;
-    int64_t* out_ncorr;
-};
 
 // --------------------------------------------------------------------------
 // Per-start reduction of the block partials, convergence test
-// (RegistrationICP), and the 6x6 solve + pose update.  One wave per start.
+// (RegistrationICP), and the 6x6 solve + pose update.  One wave per start
+// (the unpipelined loop; the pipelined pass runs the same code in the
+// accumulation kernel's last block).  sums_in != null: the sums are given
+// (row-sharded mode, already all-reduced over ranks) and the partials are
+// not read.
 // --------------------------------------------------------------------------
-// Fixed-order reduction of one start's block partials (lane-strided, then
-// the wave).  sums_in != null: the sums are given (row-sharded mode, already
-// all-reduced over ranks) and the partials are not read.
-__device__ __forceinline__ void reduce_partials(const double* __restrict__ partial, int slot, int nblk,
-                                                double s[kNacc]) {
-    const int lane = threadIdx.x & 63;
-#pragma unroll
-    for (int v = 0; v < kNacc; ++v) s[v] = 0.0;
-    for (int b = lane; b < nblk; b += 64) {
-        const double* pp = partial + ((size_t)slot * nblk + b) * kPartialStride;
-#pragma unroll
-        for (int v = 0; v < kNacc; ++v) s[v] += pp[v];
-    }
-#pragma unroll
-    for (int v = 0; v < kNacc; ++v) s[v] = wave_sum_fixed(s[v]);
-}
-
 __global__ __launch_bounds__(64) void reduce_partials_kernel(const double* __restrict__ partial, int slot, int nblk,
                                                              double* __restrict__ sums) {
     double s[kNacc];
@@ -1189,7 +1400,6 @@ __global__ __launch_bounds__(64) void icp_solve_kernel(const int32_t* __restrict
                                                         int max_iter, double rel_fit, double rel_rmse, SolveArgs a) {
     const int slot = active[blockIdx.x];
     if (a.done[slot]) return;
-    const int lane = threadIdx.x;
     double s[kNacc];
     if (sums_in) {
 #pragma unroll
@@ -1197,53 +1407,7 @@ __global__ __launch_bounds__(64) void icp_solve_kernel(const int32_t* __restrict
     } else {
         reduce_partials(partial, slot, nblk, s);
     }
-    if (lane != 0) return;
-
-    const double cnt = s[28];
-    const double fit = cnt > 0 ? cnt / (double)N : 0.0;
-    const double rmse = cnt > 0 ? sqrt(s[27] / cnt) : 0.0;
-    const double pf = a.prev[2 * slot], pr = a.prev[2 * slot + 1];
-    const bool converged = pass >= 1 && fabs(pf - fit) < rel_fit && fabs(pr - rmse) < rel_rmse;
-    if (converged || pass >= max_iter) {
-        a.done[slot] = 1;
-        a.out_fit[slot] = fit;
-        a.out_rmse[slot] = rmse;
-        a.out_iters[slot] = pass;
-        a.out_ncorr[slot] = (int64_t)cnt;
-        return;
-    }
-    a.prev[2 * slot] = fit;
-    a.prev[2 * slot + 1] = rmse;
-
-    double upd[16] = {1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1};
-    if (cnt > 0 && kEst == 1) {
-        umeyama_from_moments(s, cnt, upd);
-    } else if (cnt > 0) {
-        double JTJ[36], b[6];
-        for (int r = 0; r < 6; ++r)
-            for (int c = 0; c < 6; ++c) JTJ[6 * r + c] = r <= c ? s[ut(r, c)] : s[ut(c, r)];
-        for (int r = 0; r < 6; ++r) b[r] = -s[21 + r];
-        const double det = det6(JTJ);
-        if (!(fabs(det) < 1e-6 || isnan(det) || isinf(det))) {
-            double x[6];
-            ldlt_solve6(JTJ, b, x);
-            vec6_to_m4(x, upd);
-        }
-    }
-    double Tcur[16], Tn[16];
-    for (int t = 0; t < 16; ++t) Tcur[t] = a.T[16 * slot + t];
-    m4_mul(upd, Tcur, Tn);
-    for (int t = 0; t < 16; ++t) a.T[16 * slot + t] = Tn[t];
-    // Q = Tn * [G; 0 0 0 1]  (3x4), R = Tn[:3,:3]
-    const double* G = a.G + 12 * slot;
-    for (int r = 0; r < 3; ++r) {
-        for (int c = 0; c < 4; ++c) {
-            double v = Tn[4 * r + 0] * G[c] + Tn[4 * r + 1] * G[4 + c] + Tn[4 * r + 2] * G[8 + c];
-            if (c == 3) v += Tn[4 * r + 3];
-            a.Q[12 * slot + 4 * r + c] = v;
-        }
-        for (int c = 0; c < 3; ++c) a.R[9 * slot + 3 * r + c] = Tn[4 * r + c];
-    }
+    if (threadIdx.x == 0) solve_start<kEst>(slot, s, N, pass, max_iter, rel_fit, rel_rmse, a);
 }
 
 // Kernel-level 1-NN (orpcd_nn1_radius): the same culled search on Morton-
@@ -1251,7 +1415,7 @@ __global__ __launch_bounds__(64) void icp_solve_kernel(const int32_t* __restrict
 // accumulation.  Queries in input order.
 __global__ __launch_bounds__(kCBlock) void nn1_kernel(const double* __restrict__ q64, int nq,
                                                       const float4* __restrict__ p4, const float4* __restrict__ tlo,
-                                                      const float4* __restrict__ thi, int ntiles,
+                                                      const float4* __restrict__ thi, const float4* __restrict__ qbox, int ntiles,
                                                       const float4* __restrict__ slo, const float4* __restrict__ shi,
                                                       int nsuper, int seed_stride, const double* __restrict__ tgt64,
                                                       const int32_t* __restrict__ tperm, double r2, float r2s,
@@ -1274,7 +1438,7 @@ __global__ __launch_bounds__(kCBlock) void nn1_kernel(const double* __restrict__
                 b = fminf(b, d2f(qx[k], qy[k], qz[k], p4[t * kTile]) * kSeedSlack + 1e-30f);
         bound[k] = b;
     }
-    culled_search(stage[wid], p4, tlo, thi, ntiles, slo, shi, nsuper, 1, 1, 0, qx, qy, qz, bound, bd, bj);
+    culled_search(stage[wid], p4, tlo, thi, qbox, ntiles, slo, shi, nsuper, 1, 1, 0, qx, qy, qz, bound, bd, bj);
 #pragma unroll
     for (int k = 0; k < kCQPT; ++k) {
         const int i = i0 + 64 * k;
@@ -1311,13 +1475,57 @@ static bool use_coop(const orpcd_ctx* c) { return c->opt.search_kernel == 1 && c
 // the two-phase search keeps a candidate list of every query group
 static bool use_two_phase(const orpcd_ctx* c) { return c->opt.search_kernel == 2 && c->two_phase_ok; }
 
-hipError_t launch_xform(const orpcd_ctx* c, int nact, double r2, hipStream_t s) {
+hipError_t launch_xform(const orpcd_ctx* c, int nact, double r2, hipStream_t s, bool dev_nact) {
     if (use_coop(c) || use_two_phase(c)) return hipSuccess;  // these searches transform their own queries
     const int N = (int)c->src.n;
     xform_queries_kernel<<<dim3((unsigned)((N + 255) / 256), (unsigned)nact), 256, 0, s>>>(
         c->src.xyz64.p, N, c->active.p, c->Q.p, c->done.p, c->tgt.p4.p, (int)c->tgt.ntiles,
-        seed_stride_for(c->tgt.ntiles), c->prevnn.p, search_r2(r2), c->opt.reseed, c->q32.p, c->best.p);
+        seed_stride_for(c->tgt.ntiles), c->prevnn.p, search_r2(r2), c->opt.reseed, c->q32.p, c->best.p,
+        dev_nact ? c->ctl.p : nullptr);
     return hipGetLastError();
+}
+
+static SolveArgs solve_args(const orpcd_ctx* c) {
+    return SolveArgs{c->T.p,    c->Q.p,       c->R.p,        c->G.p,         c->prev.p,
+                     c->done.p, c->out_fit.p, c->out_rmse.p, c->out_iters.p, c->out_ncorr.p};
+}
+
+bool pipelined_ok(const orpcd_ctx* c) { return !use_coop(c) && !use_two_phase(c) && c->opt.pipeline; }
+
+// One pipelined pass (see PassCtl): search over the device's running starts,
+// accumulation with the fused solve + compaction, the next pass's queries.
+// nact_host is an upper bound of the running starts (grid sizes only).
+hipError_t launch_gicp_pass_pipelined(const orpcd_ctx* c, int nact_host, int pass, const orpcd_gicp_params& p,
+                                      hipStream_t s, hipEvent_t mid, hipEvent_t after_accum) {
+    const int N = (int)c->src.n;
+    const double r2 = p.max_correspondence_distance * p.max_correspondence_distance;
+    const int sblk = (N + kCBlockQ - 1) / kCBlockQ;
+    const int want = c->opt.search_waves;
+    const int S = search_splits(nact_host, sblk, want);
+    const int64_t grid = std::max<int64_t>((int64_t)nact_host * sblk * S, (want + kCWaves - 1) / kCWaves);
+    hipError_t e;
+    auto kern = c->opt.search_occupancy == 6 ? nn_search_kernel_o6 : nn_search_kernel;
+    kern<<<dim3((unsigned)grid), kCBlock, 0, s>>>(c->q32.p, N, c->tgt.p4.p, c->tgt.tlo.p, c->tgt.thi.p, c->tgt.qbox.p,
+                                                  (int)c->tgt.ntiles, c->tgt.slo.p, c->tgt.shi.p, (int)c->tgt.nsuper,
+                                                  c->opt.super_cull, c->active.p, c->done.p, 1, c->best.p,
+                                                  c->count_tiles ? c->counters.p : nullptr, c->ctl.p, sblk, want);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    if (mid && (e = hipEventRecord(mid, s)) != hipSuccess) return e;
+    const int ablk = accum_blocks(N);
+    const PassCtl pc{c->ctl.p,          c->prog_d,          c->active.p, pass, p.max_iteration, p.relative_fitness,
+                     p.relative_rmse, (int64_t)N, solve_args(c)};
+    if (c->est == kEstP2P)
+        p2p_accum_kernel<true><<<dim3((unsigned)ablk, (unsigned)nact_host), 256, 0, s>>>(
+            c->src.xyz64.p, N, c->tgt.xyz64.p, c->active.p, c->Q.p, c->done.p, r2, c->best.p, c->prevnn.p,
+            c->partial.p, ablk, pc);
+    else
+        gicp_accum_kernel<true><<<dim3((unsigned)ablk, (unsigned)nact_host), 256, 0, s>>>(
+            c->src.xyz64.p, c->scov.p, N, c->tgt.xyz64.p, c->tcov.p, c->active.p, c->Q.p, c->R.p, c->done.p, r2,
+            c->best.p, c->prevnn.p, c->partial.p, ablk, pc);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    if (after_accum && (e = hipEventRecord(after_accum, s)) != hipSuccess) return e;
+    if (pass >= p.max_iteration) return hipSuccess;  // every start is done after this pass
+    return launch_xform(c, nact_host, r2, s, true);
 }
 
 hipError_t launch_gicp_pass(const orpcd_ctx* c, int nact, int pass, double r2, hipStream_t s, hipEvent_t mid) {
@@ -1358,28 +1566,27 @@ hipError_t launch_gicp_pass(const orpcd_ctx* c, int nact, int pass, double r2, h
     // best[] was reset to kNone by xform_queries_kernel
     auto kern = c->opt.search_occupancy == 6 ? nn_search_kernel_o6 : nn_search_kernel;
     kern<<<dim3((unsigned)(sblk * S), (unsigned)nact), kCBlock, 0, s>>>(
-        c->q32.p, N, c->tgt.p4.p, c->tgt.tlo.p, c->tgt.thi.p, (int)c->tgt.ntiles, c->tgt.slo.p, c->tgt.shi.p,
+        c->q32.p, N, c->tgt.p4.p, c->tgt.tlo.p, c->tgt.thi.p, c->tgt.qbox.p, (int)c->tgt.ntiles, c->tgt.slo.p, c->tgt.shi.p,
         (int)c->tgt.nsuper, c->opt.super_cull, c->active.p, c->done.p, S, c->best.p,
-        c->count_tiles ? c->counters.p : nullptr);
+        c->count_tiles ? c->counters.p : nullptr, nullptr, sblk, c->opt.search_waves);
     }
     if ((e = hipGetLastError()) != hipSuccess) return e;
     if (mid && (e = hipEventRecord(mid, s)) != hipSuccess) return e;
     const int ablk = accum_blocks(N);
     if (c->est == kEstP2P) {
-        p2p_accum_kernel<<<dim3((unsigned)ablk, (unsigned)nact), 256, 0, s>>>(
+        p2p_accum_kernel<false><<<dim3((unsigned)ablk, (unsigned)nact), 256, 0, s>>>(
             c->src.xyz64.p, N, c->tgt.xyz64.p, c->active.p, c->Q.p, c->done.p, r2, c->best.p, c->prevnn.p,
-            c->partial.p, ablk);
+            c->partial.p, ablk, PassCtl{});
         return hipGetLastError();
     }
-    gicp_accum_kernel<<<dim3((unsigned)ablk, (unsigned)nact), 256, 0, s>>>(
+    gicp_accum_kernel<false><<<dim3((unsigned)ablk, (unsigned)nact), 256, 0, s>>>(
         c->src.xyz64.p, c->scov.p, N, c->tgt.xyz64.p, c->tcov.p, c->active.p, c->Q.p, c->R.p, c->done.p, r2,
-        c->best.p, c->prevnn.p, c->partial.p, ablk);
+        c->best.p, c->prevnn.p, c->partial.p, ablk, PassCtl{});
     return hipGetLastError();
 }
 
 hipError_t launch_gicp_solve(const orpcd_ctx* c, int nact, int pass, const orpcd_gicp_params& p, hipStream_t s) {
-    SolveArgs a{c->T.p,    c->Q.p,       c->R.p,        c->G.p,         c->prev.p,
-                c->done.p, c->out_fit.p, c->out_rmse.p, c->out_iters.p, c->out_ncorr.p};
+    const SolveArgs a = solve_args(c);
     auto solve = c->est == kEstP2P ? icp_solve_kernel<1> : icp_solve_kernel<0>;
     solve<<<(unsigned)nact, 64, 0, s>>>(c->active.p, c->partial.p, accum_blocks(c->src.n), nullptr,
                                                     c->src.n, pass, p.max_iteration, p.relative_fitness,
@@ -1387,7 +1594,7 @@ hipError_t launch_gicp_solve(const orpcd_ctx* c, int nact, int pass, const orpcd
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     const double r2 = p.max_correspondence_distance * p.max_correspondence_distance;
-    return launch_xform(c, nact, r2, s);  // queries of the next pass (done starts skip)
+    return launch_xform(c, nact, r2, s, false);  // queries of the next pass (done starts skip)
 }
 
 hipError_t launch_reduce_partials(const orpcd_ctx* c, int slot, double* sums29, hipStream_t s) {
@@ -1397,21 +1604,20 @@ hipError_t launch_reduce_partials(const orpcd_ctx* c, int slot, double* sums29, 
 
 hipError_t launch_gicp_solve_sums(const orpcd_ctx* c, const double* sums29, int64_t n_total, int pass,
                                   const orpcd_gicp_params& p, hipStream_t s) {
-    SolveArgs a{c->T.p,    c->Q.p,       c->R.p,        c->G.p,         c->prev.p,
-                c->done.p, c->out_fit.p, c->out_rmse.p, c->out_iters.p, c->out_ncorr.p};
+    const SolveArgs a = solve_args(c);
     icp_solve_kernel<0><<<1, 64, 0, s>>>(c->active.p, nullptr, 0, sums29, n_total, pass, p.max_iteration,
                                        p.relative_fitness, p.relative_rmse, a);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     const double r2 = p.max_correspondence_distance * p.max_correspondence_distance;
-    return launch_xform(c, 1, r2, s);
+    return launch_xform(c, 1, r2, s, false);
 }
 
 hipError_t launch_nn1(const double* q, int64_t nq, const CloudLayout& t, double r2, int32_t* idx, double* d2,
                       hipStream_t s) {
     if (nq <= 0) return hipSuccess;
     const unsigned grid = (unsigned)((nq + kCBlockQ - 1) / kCBlockQ);
-    nn1_kernel<<<grid, kCBlock, 0, s>>>(q, (int)nq, t.p4.p, t.tlo.p, t.thi.p, (int)t.ntiles, t.slo.p, t.shi.p,
+    nn1_kernel<<<grid, kCBlock, 0, s>>>(q, (int)nq, t.p4.p, t.tlo.p, t.thi.p, t.qbox.p, (int)t.ntiles, t.slo.p, t.shi.p,
                                         (int)t.nsuper, seed_stride_for(t.ntiles), t.xyz64.p, t.perm.p, r2,
                                         search_r2(r2), idx, d2);
     return hipGetLastError();

@@ -14,6 +14,7 @@ namespace orpcd {
 // ------------------------------------------------------------- geometry
 constexpr int kTile = 64;                      // targets per culling tile (one wave-wide load)
 constexpr int kSuper = 64;                     // tiles per super-tile (first culling level)
+constexpr int kQuarter = 16;                   // targets per tile quarter (per-query test inside a staged tile)
 constexpr int kCQPT = 2;                       // queries per lane in the culled search
 constexpr int kCWaves = 4;                     // waves per block
 constexpr int kCBlock = 64 * kCWaves;          // threads per block
@@ -73,6 +74,7 @@ struct CloudLayout {
     DevBuf<int32_t> perm;     // Morton position -> input index
     DevBuf<float4> p4;        // npad fp32 (x,y,z, input index bits), padded far
     DevBuf<float4> tlo, thi;  // per 64-point tile AABB
+    DevBuf<float4> qbox;      // per tile: its four 16-point quarters' AABBs (lo x4, hi x4)
     DevBuf<float4> slo, shi;  // per super-tile (64 tiles) AABB
     DevBuf<uint32_t> codes;   // scratch (2n)
     DevBuf<int32_t> ids;      // scratch
@@ -83,6 +85,7 @@ struct CloudLayout {
         p4.release();
         tlo.release();
         thi.release();
+        qbox.release();
         slo.release();
         shi.release();
         codes.release();
@@ -182,6 +185,9 @@ struct orpcd_ctx {
     orpcd::DevBuf<double> partial;  // B*nblk*32
     orpcd::DevBuf<int32_t> done;    // B
     orpcd::DevBuf<int32_t> active;  // B
+    orpcd::DevBuf<int32_t> ctl;     // 2 + B: pipelined pass control (gicp_kernels.hip, PassCtl)
+    unsigned long long* prog_h = nullptr;  // host-mapped progress word of the pipelined passes
+    unsigned long long* prog_d = nullptr;  // its device address
     orpcd::DevBuf<double> out_fit, out_rmse;
     orpcd::DevBuf<int32_t> out_iters;
     orpcd::DevBuf<int64_t> out_ncorr;
@@ -237,6 +243,9 @@ struct orpcd_ctx {
                                   // 1: cooperative (one workgroup per query group, queries fused);
                                   // 2: two-phase (cull once per group, persistent scan of the items)
         int scan_blocks = 1280;   // persistent grid of the two-phase scan (256-thread blocks)
+        int pipeline = 0;         // 1: passes enqueued ahead, running starts kept on the device;
+                                  // 0: host sync every sync_every passes (also under ORPCD_TRACE)
+        int lookahead = 4;        // pipelined: passes enqueued beyond the last one known complete
     } opt;
     std::vector<hipEvent_t> ev_pool;
     orpcd::KernelStats stats;
@@ -277,7 +286,10 @@ hipError_t launch_fps(const double* xyz, int64_t n, int first, int k, int max_bl
 
 // gicp_kernels.hip
 int accum_blocks(int64_t N);
-hipError_t launch_xform(const orpcd_ctx* c, int nact, double r2, hipStream_t s);
+hipError_t launch_xform(const orpcd_ctx* c, int nact, double r2, hipStream_t s, bool dev_nact = false);
+bool pipelined_ok(const orpcd_ctx* c);
+hipError_t launch_gicp_pass_pipelined(const orpcd_ctx* c, int nact_host, int pass, const orpcd_gicp_params& p,
+                                      hipStream_t s, hipEvent_t mid, hipEvent_t after_accum);
 hipError_t launch_gicp_pass(const orpcd_ctx* c, int nact, int pass, double r2, hipStream_t s, hipEvent_t mid);
 hipError_t launch_gicp_solve(const orpcd_ctx* c, int nact, int pass, const orpcd_gicp_params& p, hipStream_t s);
 hipError_t launch_reduce_partials(const orpcd_ctx* c, int slot, double* sums29, hipStream_t s);

@@ -8,6 +8,7 @@
 #include <cstring>
 #include <new>
 #include <random>
+#include <thread>
 #include <utility>
 
 #include "orpcd_internal.h"
@@ -363,6 +364,7 @@ int batch_setup(orpcd_ctx* c, const double* R0, const double* t0, int B, const o
     CTX_CHECK(c, c->item_counts.ensure((size_t)2 * B * ((N + 127) / 128) + 2));
     CTX_CHECK(c, c->done.ensure((size_t)B));
     CTX_CHECK(c, c->active.ensure((size_t)B));
+    CTX_CHECK(c, c->ctl.ensure((size_t)B + 2));
     CTX_CHECK(c, c->out_fit.ensure((size_t)B));
     CTX_CHECK(c, c->out_rmse.ensure((size_t)B));
     CTX_CHECK(c, c->out_iters.ensure((size_t)B));
@@ -417,6 +419,9 @@ int batch_setup(orpcd_ctx* c, const double* R0, const double* t0, int B, const o
     CTX_CHECK(c, hipMemcpyAsync(c->active.p, hAct, (size_t)B * 4, hipMemcpyHostToDevice, s));
     CTX_CHECK(c, hipMemcpyAsync(c->done.p, hDone, (size_t)B * 4, hipMemcpyHostToDevice, s));
     CTX_CHECK(c, hipMemsetAsync(c->prevnn.p, 0xff, (size_t)B * N * 4, s));
+    // pipelined pass control: B running starts, no arrivals
+    CTX_CHECK(c, hipMemsetAsync(c->ctl.p, 0, ((size_t)B + 2) * 4, s));
+    CTX_CHECK(c, hipMemsetD32Async((hipDeviceptr_t)c->ctl.p, B, 1, s));
 
     // posed-frame source covariances for every start (rigid equivariance)
     c->est = init16 ? kEstP2P : kEstGICP;
@@ -428,6 +433,10 @@ int batch_setup(orpcd_ctx* c, const double* R0, const double* t0, int B, const o
 
 int run_passes(orpcd_ctx* c, int B, const orpcd_gicp_params* p, double* T_out, double* rmse_out,
                double* fitness_out, int32_t* iters_out, int64_t* ncorr_out);
+int run_passes_pipelined(orpcd_ctx* c, int B, const orpcd_gicp_params* p, double* T_out, double* rmse_out,
+                         double* fitness_out, int32_t* iters_out, int64_t* ncorr_out);
+int read_outputs(orpcd_ctx* c, int B, unsigned long long tiles_before, double* T_out, double* rmse_out,
+                 double* fitness_out, int32_t* iters_out, int64_t* ncorr_out);
 
 }  // namespace
 
@@ -455,7 +464,13 @@ int orpcd_ctx_create(int device, orpcd_ctx** out) {
     if (hipSetDevice(device) != hipSuccess ||
         hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
         c->counters.ensure(kCounterSlots * kCounterStride) != hipSuccess ||
-        hipMemset(c->counters.p, 0, kCounterSlots * kCounterStride * 8) != hipSuccess) {
+        hipMemset(c->counters.p, 0, kCounterSlots * kCounterStride * 8) != hipSuccess ||
+        hipHostMalloc(reinterpret_cast<void**>(&c->prog_h), 64, hipHostMallocMapped | hipHostMallocCoherent) !=
+            hipSuccess ||
+        hipHostGetDevicePointer(reinterpret_cast<void**>(&c->prog_d), c->prog_h, 0) != hipSuccess) {
+        if (c->prog_h) (void)hipHostFree(c->prog_h);
+        if (c->stream) (void)hipStreamDestroy(c->stream);
+        c->counters.release();
         delete c;
         return ORPCD_EDEVICE;
     }
@@ -480,6 +495,8 @@ int orpcd_ctx_destroy(orpcd_ctx* c) {
     c->q32.release();
     c->done.release();
     c->active.release();
+    c->ctl.release();
+    if (c->prog_h) (void)hipHostFree(c->prog_h);
     c->out_iters.release();
     c->out_ncorr.release();
     c->scratch32.release();
@@ -581,6 +598,120 @@ int orpcd_icp_p2p_batch(orpcd_ctx* c, const double* init, int32_t B, const orpcd
 
 namespace {
 
+// Outputs of the batch (after the last pass): T (GICP: ICP transform of the
+// posed source; PointToPoint: T * G), rmse, fitness, iterations, inliers.
+int read_outputs(orpcd_ctx* c, int B, unsigned long long tiles_before, double* T_out, double* rmse_out,
+                 double* fitness_out, int32_t* iters_out, int64_t* ncorr_out) {
+    double* hT = c->h64.p + (size_t)B * 12;
+    double* hFit = hT + (size_t)B * (16 + 12 + 9 + 9 + 2);
+    double* hRmse = hFit + B;
+    int32_t* hIters = c->h32.p + 2 * B;
+    hipStream_t s = c->stream;
+    unsigned long long unused = 0;
+    if (c->est == kEstP2P) {
+        double* hQ = hT + (size_t)B * 16;
+        CTX_CHECK(c, hipMemcpyAsync(hQ, c->Q.p, (size_t)B * 12 * 8, hipMemcpyDeviceToHost, s));
+        CTX_CHECK(c, hipStreamSynchronize(s));
+        for (int b = 0; b < B; ++b) {
+            for (int t = 0; t < 12; ++t) hT[16 * b + t] = hQ[12 * b + t];
+            hT[16 * b + 12] = hT[16 * b + 13] = hT[16 * b + 14] = 0.0;
+            hT[16 * b + 15] = 1.0;
+        }
+    } else {
+        CTX_CHECK(c, hipMemcpyAsync(hT, c->T.p, (size_t)B * 16 * 8, hipMemcpyDeviceToHost, s));
+    }
+    CTX_CHECK(c, hipMemcpyAsync(hFit, c->out_fit.p, (size_t)B * 8, hipMemcpyDeviceToHost, s));
+    CTX_CHECK(c, hipMemcpyAsync(hRmse, c->out_rmse.p, (size_t)B * 8, hipMemcpyDeviceToHost, s));
+    CTX_CHECK(c, hipMemcpyAsync(hIters, c->out_iters.p, (size_t)B * 4, hipMemcpyDeviceToHost, s));
+    std::vector<int64_t> nc((size_t)B);
+    CTX_CHECK(c, hipMemcpyAsync(nc.data(), c->out_ncorr.p, (size_t)B * 8, hipMemcpyDeviceToHost, s));
+    CTX_CHECK(c, hipStreamSynchronize(s));
+    unsigned long long tiles_after = 0;
+    if (c->profiling) CTX_CHECK(c, read_counters(c, tiles_after, unused, false));
+    if (c->profiling) {
+        const double t = (double)(tiles_after - tiles_before);
+        c->stats.tiles += t;
+        c->stats.pairs += t * kQuarter * (64.0 * kCQPT);  // pairs evaluated by the scan (t in quarters)
+    }
+    for (int b = 0; b < B; ++b) {
+        std::memcpy(T_out + 16 * b, hT + 16 * b, 16 * sizeof(double));
+        rmse_out[b] = hRmse[b];
+        if (fitness_out) fitness_out[b] = hFit[b];
+        if (iters_out) iters_out[b] = hIters[b];
+        if (ncorr_out) ncorr_out[b] = nc[b];
+        c->stats.iterations += hIters[b];
+    }
+    return ORPCD_OK;
+}
+
+// The pipelined ICP loop (opt.pipeline, default): every pass is enqueued
+// without a host round trip.  The device keeps the running starts (PassCtl:
+// solve fused into the accumulation's last block, compaction of active[],
+// splits re-derived by the search from the device count) and publishes
+// (passes completed, running starts) in a host-mapped word.  The host reads
+// that word only to shrink the grids, to stop enqueueing once no start runs,
+// and to stay at most opt.lookahead passes ahead; passes enqueued after the
+// last start finished exit at once.
+int run_passes_pipelined(orpcd_ctx* c, int B, const orpcd_gicp_params* p, double* T_out, double* rmse_out,
+                         double* fitness_out, int32_t* iters_out, int64_t* ncorr_out) {
+    hipStream_t s = c->stream;
+    unsigned long long tiles_before = 0, unused = 0;
+    if (c->profiling) CTX_CHECK(c, read_counters(c, tiles_before, unused, false));
+    const bool timed = c->profiling;
+    c->count_tiles = timed;
+    const int npass = p->max_iteration + 1;
+    if (timed) {
+        while ((int)c->ev_pool.size() < 3 * npass) {
+            hipEvent_t e;
+            CTX_CHECK(c, hipEventCreateWithFlags(&e, hipEventDisableSystemFence));  // timing only
+            c->ev_pool.push_back(e);
+        }
+    }
+    volatile unsigned long long* prog = c->prog_h;
+    *prog = 0;  // no pipelined kernel of this batch has run yet (the stream is idle after batch_setup's copies)
+    int nact_host = B, launched = 0;
+    for (int pass = 0; pass < npass; ++pass) {
+        unsigned long long v = *prog;
+        int pdone = (int)(v >> 32), nrun = (int)(v & 0xffffffffu);
+        while (pdone > 0 && nrun > 0 && pass - pdone >= c->opt.lookahead) {  // far enough ahead: wait
+            std::this_thread::yield();
+            v = *prog;
+            pdone = (int)(v >> 32);
+            nrun = (int)(v & 0xffffffffu);
+        }
+        if (pdone == 0 && pass >= c->opt.lookahead) {  // nothing complete yet: bound the queue anyway
+            while ((v = *prog) >> 32 == 0) std::this_thread::yield();
+            pdone = (int)(v >> 32);
+            nrun = (int)(v & 0xffffffffu);
+        }
+        if (pdone > 0) {
+            if (nrun == 0) break;
+            nact_host = std::min(nact_host, nrun);
+        }
+        hipEvent_t* ev = timed ? &c->ev_pool[3 * pass] : nullptr;
+        if (timed) CTX_CHECK(c, hipEventRecord(ev[0], s));
+        CTX_CHECK(c, launch_gicp_pass_pipelined(c, nact_host, pass, *p, s, timed ? ev[1] : nullptr,
+                                                timed ? ev[2] : nullptr));
+        ++launched;
+    }
+    CTX_CHECK(c, hipStreamSynchronize(s));
+    const int passes_run = (int)(*prog >> 32);  // passes with a running start
+    if (timed) {
+        for (int q = 0; q < std::min(launched, passes_run); ++q) {
+            float ms = 0.f, ms2 = 0.f;
+            CTX_CHECK(c, hipEventElapsedTime(&ms, c->ev_pool[3 * q], c->ev_pool[3 * q + 1]));
+            CTX_CHECK(c, hipEventElapsedTime(&ms2, c->ev_pool[3 * q + 1], c->ev_pool[3 * q + 2]));
+            c->stats.launches += 1;
+            c->stats.ms += ms;
+            c->stats.accum_ms += ms2;
+        }
+    }
+    int rc = read_outputs(c, B, tiles_before, T_out, rmse_out, fitness_out, iters_out, ncorr_out);
+    if (rc) return rc;
+    for (int b = 0; b < B; ++b) c->stats.passes += (iters_out ? iters_out[b] : 0) + 1;
+    return ORPCD_OK;
+}
+
 // The ICP loop of every start of the batch set up by batch_setup (GICP or
 // PointToPoint by c->est).  GICP outputs T (the ICP transform relative to the
 // posed source); PointToPoint outputs T * G (registration_icp's result, init
@@ -601,6 +732,8 @@ int run_passes(orpcd_ctx* c, int B, const orpcd_gicp_params* p, double* T_out, d
     if (c->profiling) CTX_CHECK(c, read_counters(c, tiles_before, unused, false));
     int nact = B;
     static const bool trace = getenv("ORPCD_TRACE") != nullptr;
+    if (!trace && pipelined_ok(c)) return run_passes_pipelined(c, B, p, T_out, rmse_out, fitness_out, iters_out,
+                                                                ncorr_out);
     const bool timed = c->profiling || trace;
     const int every = trace ? 1 : std::max(1, c->opt.sync_every);
     c->count_tiles = timed;
@@ -640,7 +773,7 @@ int run_passes(orpcd_ctx* c, int B, const orpcd_gicp_params* p, double* T_out, d
                 }
                 if (trace) {
                     static unsigned long long last = 0;
-                    fprintf(stderr, "[orpcd] pass %3d nact %3d search %.3f ms accum %.3f ms tiles %llu max/wave %llu\n",
+                    fprintf(stderr, "[orpcd] pass %3d nact %3d search %.3f ms accum %.3f ms quarters %llu max/wave %llu\n",
                             pass, nact, ms, ms2, tiles_now[0] - last, tiles_now[1]);
                     last = tiles_now[0];
                     if (getenv("ORPCD_PHASES")) {  // libraries built with -DORPCD_PHASES
@@ -669,41 +802,7 @@ int run_passes(orpcd_ctx* c, int B, const orpcd_gicp_params* p, double* T_out, d
         if (k != nact && k > 0) CTX_CHECK(c, hipMemcpyAsync(c->active.p, hAct, (size_t)k * 4, hipMemcpyHostToDevice, s));
         nact = k;
     }
-    // outputs
-    if (c->est == kEstP2P) {
-        double* hQ = hT + (size_t)B * 16;
-        CTX_CHECK(c, hipMemcpyAsync(hQ, c->Q.p, (size_t)B * 12 * 8, hipMemcpyDeviceToHost, s));
-        CTX_CHECK(c, hipStreamSynchronize(s));
-        for (int b = 0; b < B; ++b) {
-            for (int t = 0; t < 12; ++t) hT[16 * b + t] = hQ[12 * b + t];
-            hT[16 * b + 12] = hT[16 * b + 13] = hT[16 * b + 14] = 0.0;
-            hT[16 * b + 15] = 1.0;
-        }
-    } else {
-        CTX_CHECK(c, hipMemcpyAsync(hT, c->T.p, (size_t)B * 16 * 8, hipMemcpyDeviceToHost, s));
-    }
-    CTX_CHECK(c, hipMemcpyAsync(hFit, c->out_fit.p, (size_t)B * 8, hipMemcpyDeviceToHost, s));
-    CTX_CHECK(c, hipMemcpyAsync(hRmse, c->out_rmse.p, (size_t)B * 8, hipMemcpyDeviceToHost, s));
-    CTX_CHECK(c, hipMemcpyAsync(hIters, c->out_iters.p, (size_t)B * 4, hipMemcpyDeviceToHost, s));
-    std::vector<int64_t> nc((size_t)B);
-    CTX_CHECK(c, hipMemcpyAsync(nc.data(), c->out_ncorr.p, (size_t)B * 8, hipMemcpyDeviceToHost, s));
-    CTX_CHECK(c, hipStreamSynchronize(s));
-    unsigned long long tiles_after = 0;
-    if (c->profiling) CTX_CHECK(c, read_counters(c, tiles_after, unused, false));
-    if (c->profiling) {
-        const double t = (double)(tiles_after - tiles_before);
-        c->stats.tiles += t;
-        c->stats.pairs += t * kTile * (64.0 * kCQPT);  // pairs evaluated by the scan
-    }
-    for (int b = 0; b < B; ++b) {
-        std::memcpy(T_out + 16 * b, hT + 16 * b, 16 * sizeof(double));
-        rmse_out[b] = hRmse[b];
-        if (fitness_out) fitness_out[b] = hFit[b];
-        if (iters_out) iters_out[b] = hIters[b];
-        if (ncorr_out) ncorr_out[b] = nc[b];
-        c->stats.iterations += hIters[b];
-    }
-    return ORPCD_OK;
+    return read_outputs(c, B, tiles_before, T_out, rmse_out, fitness_out, iters_out, ncorr_out);
 }
 
 }  // namespace
@@ -906,7 +1005,7 @@ int orpcd_gicp_shard_pass(orpcd_ctx* c, double* sums_out, int32_t* active) {
         c->stats.ms += ms;
         c->stats.accum_ms += ms2;
         c->stats.tiles += (double)(tiles1 - tiles0);
-        c->stats.pairs += (double)(tiles1 - tiles0) * kTile * (64.0 * kCQPT);
+        c->stats.pairs += (double)(tiles1 - tiles0) * kQuarter * (64.0 * kCQPT);
     }
     c->stats.passes += 1;
     return ORPCD_OK;
@@ -1154,6 +1253,8 @@ int orpcd_set_option(orpcd_ctx* c, const char* key, double value) {
     else if (k == "search_occupancy" && (v == 0 || v == 6)) c->opt.search_occupancy = v;
     else if (k == "search_kernel" && v >= 0 && v <= 2) c->opt.search_kernel = v;
     else if (k == "scan_blocks" && v >= 1 && v <= 65536) c->opt.scan_blocks = v;
+    else if (k == "pipeline" && (v == 0 || v == 1)) c->opt.pipeline = v;
+    else if (k == "lookahead" && v >= 1 && v <= 64) c->opt.lookahead = v;
     else {
         c->err = "set_option: unknown key or bad value: " + k;
         return ORPCD_EINVAL;

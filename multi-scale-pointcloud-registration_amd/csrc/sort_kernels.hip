@@ -53,21 +53,34 @@ __global__ void gather_points_kernel(const double* __restrict__ in64, const int3
     }
 }
 
-// One thread per 64-point tile: fp32 AABB over the tile's real points.
+// One thread per 64-point tile: fp32 AABB over the tile's real points, and
+// the AABBs of its four 16-point quarters (qbox[8t + k] = lo of quarter k,
+// qbox[8t + 4 + k] = hi; a quarter without real points gets an empty box).
 __global__ void tile_aabb_kernel(const float4* __restrict__ p4, int n, int ntiles, float4* __restrict__ lo,
-                                 float4* __restrict__ hi) {
+                                 float4* __restrict__ hi, float4* __restrict__ qbox) {
     const int t = blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= ntiles) return;
     float mnx = 3.0e38f, mny = 3.0e38f, mnz = 3.0e38f, mxx = -3.0e38f, mxy = -3.0e38f, mxz = -3.0e38f;
-    const int end = min(n, (t + 1) * kTile);
-    for (int k = t * kTile; k < end; ++k) {
-        const float4 p = p4[k];
-        mnx = fminf(mnx, p.x);
-        mny = fminf(mny, p.y);
-        mnz = fminf(mnz, p.z);
-        mxx = fmaxf(mxx, p.x);
-        mxy = fmaxf(mxy, p.y);
-        mxz = fmaxf(mxz, p.z);
+    for (int q = 0; q < 4; ++q) {
+        float ax = 3.0e38f, ay = 3.0e38f, az = 3.0e38f, bx = -3.0e38f, by = -3.0e38f, bz = -3.0e38f;
+        const int beg = t * kTile + q * kQuarter, end = min(n, beg + kQuarter);
+        for (int k = beg; k < end; ++k) {
+            const float4 p = p4[k];
+            ax = fminf(ax, p.x);
+            ay = fminf(ay, p.y);
+            az = fminf(az, p.z);
+            bx = fmaxf(bx, p.x);
+            by = fmaxf(by, p.y);
+            bz = fmaxf(bz, p.z);
+        }
+        qbox[8 * (size_t)t + q] = make_float4(ax, ay, az, 0.f);
+        qbox[8 * (size_t)t + 4 + q] = make_float4(bx, by, bz, 0.f);
+        mnx = fminf(mnx, ax);
+        mny = fminf(mny, ay);
+        mnz = fminf(mnz, az);
+        mxx = fmaxf(mxx, bx);
+        mxy = fmaxf(mxy, by);
+        mxz = fmaxf(mxz, bz);
     }
     lo[t] = make_float4(mnx, mny, mnz, 0.f);
     hi[t] = make_float4(mxx, mxy, mxz, 0.f);
@@ -123,6 +136,7 @@ hipError_t build_layout(const double* dev_in64, int64_t n, const double bbox_lo[
         if ((e = L.p4.ensure((size_t)L.npad)) != hipSuccess) return e;
         if ((e = L.tlo.ensure((size_t)L.ntiles)) != hipSuccess) return e;
         if ((e = L.thi.ensure((size_t)L.ntiles)) != hipSuccess) return e;
+        if ((e = L.qbox.ensure((size_t)L.ntiles * 8)) != hipSuccess) return e;
         L.nsuper = (L.ntiles + kSuper - 1) / kSuper;
         if ((e = L.slo.ensure((size_t)L.nsuper)) != hipSuccess) return e;
         if ((e = L.shi.ensure((size_t)L.nsuper)) != hipSuccess) return e;
@@ -145,7 +159,7 @@ hipError_t build_layout(const double* dev_in64, int64_t n, const double bbox_lo[
     if ((e = hipGetLastError()) != hipSuccess) return e;
     if (with_tiles) {
         tile_aabb_kernel<<<(unsigned)((L.ntiles + 255) / 256), 256, 0, s>>>(L.p4.p, (int)n, (int)L.ntiles, L.tlo.p,
-                                                                           L.thi.p);
+                                                                           L.thi.p, L.qbox.p);
         if ((e = hipGetLastError()) != hipSuccess) return e;
         super_aabb_kernel<<<(unsigned)((L.nsuper + 255) / 256), 256, 0, s>>>(L.tlo.p, L.thi.p, (int)L.ntiles,
                                                                             (int)L.nsuper, L.slo.p, L.shi.p);

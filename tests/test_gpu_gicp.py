@@ -182,6 +182,45 @@ def test_search_variants_identical(ctx, kernel):
     assert np.array_equal(got["rmse"], ref["rmse"])
 
 
+@pytest.mark.parametrize("lookahead", [1, 4, 64])
+def test_pipelined_passes_identical(ctx, lookahead):
+    """Pipelined passes (solve fused into the accumulation, running starts
+    compacted on the device, no host round trip per pass) against the
+    host-synchronised loop: bit-identical T, rmse, fitness, iterations, for a
+    batch of 70 starts (two compaction rounds) that finish at different passes,
+    with max_iteration both reached and not; and PointToPoint refinement."""
+    src, tgt = small_pair(3000, 2800, seed=21)
+    rng = np.random.default_rng(5)
+    R0 = np.array([rot_xyz(*rng.uniform(-90, 90, 3)) for _ in range(70)])
+    t0 = rng.normal(size=(70, 3)) * 0.1
+    ctx.set_target(tgt)
+    ctx.set_source(src)
+    inits = np.repeat(np.eye(4)[None], 5, axis=0)
+    inits[:, :3, 3] = rng.normal(size=(5, 3)) * 0.02
+    try:
+        ctx.set_option("pipeline", 1)
+        ctx.set_option("lookahead", lookahead)
+        got = [ctx.gicp_batch(R0, t0), ctx.gicp_batch(R0[:9], t0[:9], max_iteration=7)]
+        ctx.set_target_points(tgt)
+        ctx.set_source_points(src)
+        got.append(ctx.icp_p2p_batch(inits, max_iteration=30))
+        ctx.set_option("pipeline", 0)
+        ctx.set_target(tgt)
+        ctx.set_source(src)
+        ref = [ctx.gicp_batch(R0, t0), ctx.gicp_batch(R0[:9], t0[:9], max_iteration=7)]
+        ctx.set_target_points(tgt)
+        ctx.set_source_points(src)
+        ref.append(ctx.icp_p2p_batch(inits, max_iteration=30))
+    finally:
+        ctx.set_option("pipeline", 0)
+        ctx.set_option("lookahead", 4)
+    assert len(set(got[0]["iters"].tolist())) > 5  # the starts finish at many different passes
+    assert (got[1]["iters"] == 7).any()
+    for g, r in zip(got, ref):
+        for k in ("T", "rmse", "fitness", "iters"):
+            assert np.array_equal(g[k], r[k]), k
+
+
 def test_gicp_matches_g4_fixtures(ctx):
     """The GPU GICP against the committed oracle traces G4 (300-pair and C1
     with RandomDownsampler(5000) + SOR preprocessing)."""

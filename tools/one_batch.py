@@ -1,6 +1,7 @@
 """One C2 multistart (30 starts, GICP) with the given runtime options, for
 profiling a single configuration:  python tools/one_batch.py '{"search_kernel":1}' [--reps 2]"""
 import json
+import time
 import os
 import sys
 
@@ -27,7 +28,9 @@ def main():
     ctx.set_target(t)
     ctx.set_source(s)
     for _ in range(reps):
+        t_0 = time.perf_counter()
         r = ctx.gicp_batch(R0, t0)
+        print(f"gicp_batch {1e3 * (time.perf_counter() - t_0):.2f} ms")
     print("iters", int(r["iters"].sum()))
     ctx.close()
 
