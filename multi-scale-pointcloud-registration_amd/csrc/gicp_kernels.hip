@@ -69,7 +69,8 @@ constexpr float kQuarterSlack = 1.0f - 1.0f / 1048576.0f;  // quarter test: box 
 
 // --------------------------------------------------------------------------
 // Culled exact nearest search for the 2 queries of every lane of one wave,
-// restricted to tiles t with t % S == s.  bound[] enters as the per-query
+// restricted to tiles t with t % S == s.  s0lo/s0hi: super-tile `lane`'s box
+// (loaded early by the caller; any value when lane >= nsuper).  bound[] enters as the per-query
 // bound on d^2 (<= 0: invalid query).  Returns quarters scanned; bj[] = Morton
 // index of the chosen target or -1, bd[] its fp32 d^2 (key-truncated).
 // --------------------------------------------------------------------------
@@ -79,6 +80,7 @@ __device__ __forceinline__ int culled_search(float4* stage, const float4* __rest
                                              const float4* __restrict__ shi, int nsuper, int super_cull, int S, int s,
                                              const float qx[2], const float qy[2],
                                              const float qz[2], const float bound[2], float bd[2], int bj[2],
+                                             float4 s0lo, float4 s0hi,
                                              unsigned long long* phase_cull_out = nullptr) {
     const int lane = threadIdx.x & 63;
     const bool v0 = bound[0] > 0.0f, v1 = bound[1] > 0.0f;
@@ -128,7 +130,9 @@ __device__ __forceinline__ int culled_search(float4* stage, const float4* __rest
             if (u < nsuper && !super_cull) {
                 sl = 0.0f;
             } else if (u < nsuper) {
-                const float4 c = slo[u], d = shi[u];
+                // the first round's super-tile boxes were loaded by the caller
+                // together with its queries (no query dependence)
+                const float4 c = sb == 0 ? s0lo : slo[u], d = sb == 0 ? s0hi : shi[u];
                 const float dx = fmaxf(0.0f, fmaxf(c.x - hix, lox - d.x));
                 const float dy = fmaxf(0.0f, fmaxf(c.y - hiy, loy - d.y));
                 const float dz = fmaxf(0.0f, fmaxf(c.z - hiz, loz - d.z));
@@ -376,12 +380,19 @@ __device__ __forceinline__ void nn_search_body(
     int nsuper, int super_cull, const int32_t* __restrict__ active, const int32_t* __restrict__ done, int S,
     unsigned long long* __restrict__ best, unsigned long long* __restrict__ counters, int by, int bx, int wid,
     float4* stage_w) {
+    const int lane = threadIdx.x & 63;
+    // first culling round's super-tile boxes: independent of the start and
+    // its queries, so their load overlaps the slot and query loads
+    float4 s0lo = make_float4(0.f, 0.f, 0.f, 0.f), s0hi = s0lo;
+    if (lane < nsuper) {
+        s0lo = slo[lane];
+        s0hi = shi[lane];
+    }
     const int slot = active[by];
     if (done[slot]) return;
 #ifdef ORPCD_PHASES
     const unsigned long long ph_t0 = __builtin_readcyclecounter();
 #endif
-    const int lane = threadIdx.x & 63;
     const int grp = bx / S, split = bx - grp * S;
     const int i0 = grp * kCBlockQ + wid * (64 * kCQPT) + lane;
     float qx[kCQPT], qy[kCQPT], qz[kCQPT], bound[kCQPT], bd[kCQPT];
@@ -401,11 +412,11 @@ __device__ __forceinline__ void nn_search_body(
     const unsigned long long ph_t1 = __builtin_readcyclecounter() + (wq == 1.2345f ? 1 : 0);
     unsigned long long ph_cull[5] = {0, 0, 0, 0, 0};
     const int visited = culled_search(stage_w, p4, tlo, thi, qbox, ntiles, slo, shi, nsuper, super_cull, S, split, qx,
-                                      qy, qz, bound, bd, bj, ph_cull);
+                                      qy, qz, bound, bd, bj, s0lo, s0hi, ph_cull);
 #else
     const int visited =
         culled_search(stage_w, p4, tlo, thi, qbox, ntiles, slo, shi, nsuper, super_cull, S, split, qx, qy, qz, bound,
-                      bd, bj);
+                      bd, bj, s0lo, s0hi);
 #endif
     if (lane == 0 && counters) {  // spread over kCounterSlots cache lines (one address serialises)
         unsigned long long* cs = counters + kCounterStride * ((bx * kCWaves + wid + by) % kCounterSlots);
@@ -1438,7 +1449,9 @@ __global__ __launch_bounds__(kCBlock) void nn1_kernel(const double* __restrict__
                 b = fminf(b, d2f(qx[k], qy[k], qz[k], p4[t * kTile]) * kSeedSlack + 1e-30f);
         bound[k] = b;
     }
-    culled_search(stage[wid], p4, tlo, thi, qbox, ntiles, slo, shi, nsuper, 1, 1, 0, qx, qy, qz, bound, bd, bj);
+    culled_search(stage[wid], p4, tlo, thi, qbox, ntiles, slo, shi, nsuper, 1, 1, 0, qx, qy, qz, bound, bd, bj,
+                  lane < nsuper ? slo[lane] : make_float4(0.f, 0.f, 0.f, 0.f),
+                  lane < nsuper ? shi[lane] : make_float4(0.f, 0.f, 0.f, 0.f));
 #pragma unroll
     for (int k = 0; k < kCQPT; ++k) {
         const int i = i0 + 64 * k;

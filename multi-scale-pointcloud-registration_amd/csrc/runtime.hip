@@ -690,8 +690,7 @@ int run_passes_pipelined(orpcd_ctx* c, int B, const orpcd_gicp_params* p, double
         }
         hipEvent_t* ev = timed ? &c->ev_pool[3 * pass] : nullptr;
         if (timed) CTX_CHECK(c, hipEventRecord(ev[0], s));
-        CTX_CHECK(c, launch_gicp_pass_pipelined(c, nact_host, pass, *p, s, timed ? ev[1] : nullptr,
-                                                timed ? ev[2] : nullptr));
+        CTX_CHECK(c, launch_gicp_pass_pipelined(c, nact_host, pass, *p, s, timed ? ev[1] : nullptr, nullptr));
         ++launched;
     }
     CTX_CHECK(c, hipStreamSynchronize(s));
@@ -700,7 +699,6 @@ int run_passes_pipelined(orpcd_ctx* c, int B, const orpcd_gicp_params* p, double
         for (int q = 0; q < std::min(launched, passes_run); ++q) {
             float ms = 0.f, ms2 = 0.f;
             CTX_CHECK(c, hipEventElapsedTime(&ms, c->ev_pool[3 * q], c->ev_pool[3 * q + 1]));
-            CTX_CHECK(c, hipEventElapsedTime(&ms2, c->ev_pool[3 * q + 1], c->ev_pool[3 * q + 2]));
             c->stats.launches += 1;
             c->stats.ms += ms;
             c->stats.accum_ms += ms2;
@@ -749,7 +747,7 @@ int run_passes(orpcd_ctx* c, int B, const orpcd_gicp_params* p, double* T_out, d
         hipEvent_t* ev = timed ? &c->ev_pool[3 * pending] : nullptr;
         if (timed) CTX_CHECK(c, hipEventRecord(ev[0], s));
         CTX_CHECK(c, launch_gicp_pass(c, nact, pass, r2, s, timed ? ev[1] : nullptr));
-        if (timed) CTX_CHECK(c, hipEventRecord(ev[2], s));
+        if (trace) CTX_CHECK(c, hipEventRecord(ev[2], s));  // accumulation time: traced runs only
         CTX_CHECK(c, launch_gicp_solve(c, nact, pass, *p, s));
         ++pending;
         c->stats.passes += nact;
@@ -765,7 +763,7 @@ int run_passes(orpcd_ctx* c, int B, const orpcd_gicp_params* p, double* T_out, d
             for (int q = 0; q < pending; ++q) {
                 float ms = 0.f, ms2 = 0.f;
                 CTX_CHECK(c, hipEventElapsedTime(&ms, c->ev_pool[3 * q], c->ev_pool[3 * q + 1]));
-                CTX_CHECK(c, hipEventElapsedTime(&ms2, c->ev_pool[3 * q + 1], c->ev_pool[3 * q + 2]));
+                if (trace) CTX_CHECK(c, hipEventElapsedTime(&ms2, c->ev_pool[3 * q + 1], c->ev_pool[3 * q + 2]));
                 if (c->profiling) {
                     c->stats.launches += 1;
                     c->stats.ms += ms;

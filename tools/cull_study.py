@@ -110,10 +110,24 @@ def main():
             tot["aabb_matched_only"] += int((a & mm[:, None]).any(0).sum())
             tot["obb_matched_only"] += int((o & mm[:, None]).any(0).sum())
             tot["groups"] += 1
+            # wave-level prefilter: tiles / 64-tile super-tiles within W of
+            # the box of K query subgroups (K = 1 as built)
+            for K in (1, 4, 8):
+                ok_t = np.zeros(len(lo), bool)
+                for sub in np.array_split(np.arange(len(qq)), K):
+                    slo_, shi_ = qq[sub].min(0), qq[sub].max(0)
+                    dd = np.maximum(0, np.maximum(lo - shi_, slo_ - hi))
+                    ok_t |= (dd * dd).sum(1) < bb[sub].max()
+                tot[f"cand_K{K}"] = tot.get(f"cand_K{K}", 0) + int(ok_t.sum())
+                sup = np.unique(np.nonzero(ok_t)[0] // 64)
+                tot[f"super_K{K}"] = tot.get(f"super_K{K}", 0) + len(sup)
     G = tot["groups"]
     print(f"starts {starts} converged={converged}: no-match queries {tot['nomatch'] / tot['q']:.3f}")
     for k in ("aabb", "obb", "slab", "aabb_matched_only", "obb_matched_only"):
         print(f"  {k:18s} tiles/group {tot[k] / G:7.2f}  targets/group {tot[k] / G * size:8.1f}")
+    for K in (1, 4, 8):
+        print(f"  K={K} subgroups: tiles passing the wave test {tot[f'cand_K{K}'] / G:7.2f}, "
+              f"super-tiles holding one {tot[f'super_K{K}'] / G:5.2f}")
 
 
 if __name__ == "__main__":

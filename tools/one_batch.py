@@ -24,7 +24,10 @@ def main():
     t0 = rng.normal(size=(30, 3)) * 0.1
     ctx = _native.Context(0)
     for k, v in cfg.items():
-        ctx.set_option(k, v)
+        if k == "profiling":
+            ctx.profiling(bool(v))
+        else:
+            ctx.set_option(k, v)
     ctx.set_target(t)
     ctx.set_source(s)
     for _ in range(reps):
