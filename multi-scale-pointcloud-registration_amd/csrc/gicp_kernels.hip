@@ -482,7 +482,8 @@ __device__ __forceinline__ bool map_search_block(const int32_t* __restrict__ nac
     return true;
 }
 
-__global__ __launch_bounds__(kCBlock) void nn_search_kernel(ORPCD_NN_SEARCH_ARGS) {
+__global__ __launch_bounds__(kCBlock) __attribute__((amdgpu_waves_per_eu(5, 8))) void nn_search_kernel(
+    ORPCD_NN_SEARCH_ARGS) {
     __shared__ float4 stage[kCWaves][kTile];
     const int wid = threadIdx.x >> 6;
     int by, bx;
