@@ -61,6 +61,22 @@ __device__ __forceinline__ float box_d2(float x, float y, float z, float lx, flo
     return dx * dx + dy * dy + dz * dz;
 }
 
+// box d^2 of a lane's two queries (packed: x = query 0, y = query 1) in the
+// scan's own operation order, fma(dz, dz, fma(dy, dy, dx * dx)): each axis
+// distance is <= |q - t| for every point t of the box and fp32 rounding and fma
+// are monotone, so the result never exceeds the scan's d^2 of a point inside.
+__device__ __forceinline__ f2 box_d2_2q(f2 qx, f2 qy, f2 qz, float lx, float ly, float lz, float hx, float hy,
+                                        float hz) {
+    const f2 lx2 = {lx, lx}, ly2 = {ly, ly}, lz2 = {lz, lz}, hx2 = {hx, hx}, hy2 = {hy, hy}, hz2 = {hz, hz};
+    const f2 ax = lx2 - qx, bx = qx - hx2, ay = ly2 - qy, by = qy - hy2, az = lz2 - qz, bz = qz - hz2;
+    const f2 dx = {fmaxf(fmaxf(ax.x, bx.x), 0.0f), fmaxf(fmaxf(ax.y, bx.y), 0.0f)};
+    const f2 dy = {fmaxf(fmaxf(ay.x, by.x), 0.0f), fmaxf(fmaxf(ay.y, by.y), 0.0f)};
+    const f2 dz = {fmaxf(fmaxf(az.x, bz.x), 0.0f), fmaxf(fmaxf(az.y, bz.y), 0.0f)};
+    f2 d = dx * dx;
+    d = pk_fma(dy, dy, d);
+    return pk_fma(dz, dz, d);
+}
+
 constexpr unsigned long long kNone = ~0ull;
 constexpr int kNoSeed = -1;   // prevnn before the first pass (representative seed)
 constexpr int kNoMatch = -2;  // no target within the search radius last pass
@@ -74,13 +90,14 @@ constexpr float kQuarterSlack = 1.0f - 1.0f / 1048576.0f;  // quarter test: box 
 // bound on d^2 (<= 0: invalid query).  Returns quarters scanned; bj[] = Morton
 // index of the chosen target or -1, bd[] its fp32 d^2 (key-truncated).
 // --------------------------------------------------------------------------
+template <bool kGBox>
 __device__ __forceinline__ int culled_search(float4* stage, const float4* __restrict__ p4,
                                              const float4* __restrict__ tlo, const float4* __restrict__ thi,
                                              const float4* __restrict__ qbox, int ntiles, const float4* __restrict__ slo,
                                              const float4* __restrict__ shi, int nsuper, int super_cull, int S, int s,
                                              const float qx[2], const float qy[2],
                                              const float qz[2], const float bound[2], float bd[2], int bj[2],
-                                             float4 s0lo, float4 s0hi,
+                                             float4 s0lo, float4 s0hi, const float4* gbox = nullptr,
                                              unsigned long long* phase_cull_out = nullptr) {
     const int lane = threadIdx.x & 63;
     const bool v0 = bound[0] > 0.0f, v1 = bound[1] > 0.0f;
@@ -89,16 +106,26 @@ __device__ __forceinline__ int culled_search(float4* stage, const float4* __rest
     int t0 = -1, t1 = -1;                               // tile of the best key
     bj[0] = bj[1] = -1;
     bd[0] = bd[1] = 0.0f;
-    unsigned Wk = wave_umax((k0 > k1 ? k0 : k1) & kKeyMask);
+    const float inf = 3.0e38f;
+    // the wave's query box and worst bound: given by the query transform
+    // (gbox: lo.xyz | max bound bits, hi.xyz), else reduced here
+    unsigned Wk;
+    float lox, loy, loz, hix, hiy, hiz;
+    if constexpr (kGBox) {
+        const float4 g0 = gbox[0], g1 = gbox[1];
+        Wk = __float_as_uint(g0.w) & kKeyMask;
+        lox = g0.x, loy = g0.y, loz = g0.z, hix = g1.x, hiy = g1.y, hiz = g1.z;
+    } else {
+        Wk = wave_umax((k0 > k1 ? k0 : k1) & kKeyMask);
+        lox = wave_fmin(fminf(v0 ? qx[0] : inf, v1 ? qx[1] : inf));
+        loy = wave_fmin(fminf(v0 ? qy[0] : inf, v1 ? qy[1] : inf));
+        loz = wave_fmin(fminf(v0 ? qz[0] : inf, v1 ? qz[1] : inf));
+        hix = wave_fmax(fmaxf(v0 ? qx[0] : -inf, v1 ? qx[1] : -inf));
+        hiy = wave_fmax(fmaxf(v0 ? qy[0] : -inf, v1 ? qy[1] : -inf));
+        hiz = wave_fmax(fmaxf(v0 ? qz[0] : -inf, v1 ? qz[1] : -inf));
+    }
     if (Wk == 0u) return 0;  // no query of this wave can take anything
     float W = __uint_as_float(Wk);
-    const float inf = 3.0e38f;
-    const float lox = wave_fmin(fminf(v0 ? qx[0] : inf, v1 ? qx[1] : inf));
-    const float loy = wave_fmin(fminf(v0 ? qy[0] : inf, v1 ? qy[1] : inf));
-    const float loz = wave_fmin(fminf(v0 ? qz[0] : inf, v1 ? qz[1] : inf));
-    const float hix = wave_fmax(fmaxf(v0 ? qx[0] : -inf, v1 ? qx[1] : -inf));
-    const float hiy = wave_fmax(fmaxf(v0 ? qy[0] : -inf, v1 ? qy[1] : -inf));
-    const float hiz = wave_fmax(fmaxf(v0 ? qz[0] : -inf, v1 ? qz[1] : -inf));
     int visited = 0;
 
     // candidate cursor: rounds of 64 tiles, one tile per lane; wave-box test by
@@ -186,8 +213,9 @@ __device__ __forceinline__ int culled_search(float4* stage, const float4* __rest
             const float hx = __uint_as_float(__builtin_amdgcn_readlane(__float_as_uint(b.x), k));
             const float hy = __uint_as_float(__builtin_amdgcn_readlane(__float_as_uint(b.y), k));
             const float hz = __uint_as_float(__builtin_amdgcn_readlane(__float_as_uint(b.z), k));
-            const bool need0 = box_d2(qx[0], qy[0], qz[0], lx, ly, lz, hx, hy, hz) < __uint_as_float(k0 & kKeyMask);
-            const bool need1 = box_d2(qx[1], qy[1], qz[1], lx, ly, lz, hx, hy, hz) < __uint_as_float(k1 & kKeyMask);
+            const f2 bd2 = box_d2_2q(f2{qx[0], qx[1]}, f2{qy[0], qy[1]}, f2{qz[0], qz[1]}, lx, ly, lz, hx, hy, hz);
+            const bool need0 = bd2.x < __uint_as_float(k0 & kKeyMask);
+            const bool need1 = bd2.y < __uint_as_float(k1 & kKeyMask);
 #ifdef ORPCD_PHASES
             {
                 const unsigned long long b0 = __ballot(need0), b1 = __ballot(need1);
@@ -246,8 +274,9 @@ __device__ __forceinline__ int culled_search(float4* stage, const float4* __rest
             const float4 lo = qb[qd], hi = qb[4 + qd];
             const float b0 = __uint_as_float((k0 < m0 ? k0 : m0) & kKeyMask);
             const float b1 = __uint_as_float((k1 < m1 ? k1 : m1) & kKeyMask);
-            const bool need = box_d2(qx[0], qy[0], qz[0], lo.x, lo.y, lo.z, hi.x, hi.y, hi.z) * kQuarterSlack < b0 ||
-                              box_d2(qx[1], qy[1], qz[1], lo.x, lo.y, lo.z, hi.x, hi.y, hi.z) * kQuarterSlack < b1;
+            const f2 qd2 = box_d2_2q(f2{qx[0], qx[1]}, f2{qy[0], qy[1]}, f2{qz[0], qz[1]}, lo.x, lo.y, lo.z, hi.x,
+                                     hi.y, hi.z);
+            const bool need = qd2.x * kQuarterSlack < b0 || qd2.y * kQuarterSlack < b1;
             if (!__any(need)) continue;
             ++visited;
 #pragma unroll
@@ -346,29 +375,52 @@ __global__ __launch_bounds__(256) void xform_queries_kernel(const double* __rest
                                                             int seed_stride, const int32_t* __restrict__ prevnn,
                                                             float r2s, int reseed, float4* __restrict__ q32,
                                                             unsigned long long* __restrict__ best,
-                                                            const int32_t* __restrict__ nact_dev) {
+                                                            const int32_t* __restrict__ nact_dev,
+                                                            float4* __restrict__ gbox) {
     if (nact_dev && (int)blockIdx.y >= *nact_dev) return;  // pipelined: grid sized for an upper bound
     const int slot = active[blockIdx.y];
     if (done[slot]) return;
     const int i = blockIdx.x * 256 + threadIdx.x;
-    if (i >= N) return;
-    best[(size_t)slot * N + i] = kNone;  // split searches merge into it by atomicMin
-    double Q[12];
+    const bool valid = i < N;
+    const float inf = 3.0e38f;
+    float x = inf, y = inf, z = inf, bound = 0.0f;
+    if (valid) {
+        best[(size_t)slot * N + i] = kNone;  // split searches merge into it by atomicMin
+        double Q[12];
 #pragma unroll
-    for (int t = 0; t < 12; ++t) Q[t] = Qm[12 * slot + t];
-    const double p[3] = {src[3 * i], src[3 * i + 1], src[3 * i + 2]};
-    double q[3];
-    xform(Q, p, q);
-    const float x = (float)q[0], y = (float)q[1], z = (float)q[2];
-    float bound = r2s;
-    const int jp = prevnn[(size_t)slot * N + i];
-    if (jp >= 0) {
-        bound = fminf(bound, d2f(x, y, z, p4[jp]) * kSeedSlack + 1e-30f);
-    } else if (jp == kNoSeed || reseed) {
-        for (int t = 0; t < ntiles; t += seed_stride)
-            bound = fminf(bound, d2f(x, y, z, p4[t * kTile]) * kSeedSlack + 1e-30f);
+        for (int t = 0; t < 12; ++t) Q[t] = Qm[12 * slot + t];
+        const double p[3] = {src[3 * i], src[3 * i + 1], src[3 * i + 2]};
+        double q[3];
+        xform(Q, p, q);
+        x = (float)q[0], y = (float)q[1], z = (float)q[2];
+        bound = r2s;
+        const int jp = prevnn[(size_t)slot * N + i];
+        if (jp >= 0) {
+            bound = fminf(bound, d2f(x, y, z, p4[jp]) * kSeedSlack + 1e-30f);
+        } else if (jp == kNoSeed || reseed) {
+            for (int t = 0; t < ntiles; t += seed_stride)
+                bound = fminf(bound, d2f(x, y, z, p4[t * kTile]) * kSeedSlack + 1e-30f);
+        }
+        q32[(size_t)slot * N + i] = make_float4(x, y, z, bound);
     }
-    q32[(size_t)slot * N + i] = make_float4(x, y, z, bound);
+    if (!gbox) return;
+    // box and worst bound of each search wave's 128 queries (waves 0-1 and
+    // 2-3 of this block): what the search would reduce, computed once here
+    __shared__ float part[4][7];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const float r[7] = {wave_fmin(x), wave_fmin(y), wave_fmin(z), wave_fmax(valid ? x : -inf),
+                        wave_fmax(valid ? y : -inf), wave_fmax(valid ? z : -inf),
+                        __uint_as_float(wave_umax(__float_as_uint(bound)))};
+    if (lane < 7) part[w][lane] = r[lane];
+    __syncthreads();
+    if (threadIdx.x < 2 && (blockIdx.x * 2 + threadIdx.x) * 128 < N) {
+        const float* a = part[2 * threadIdx.x];
+        const float* b = part[2 * threadIdx.x + 1];
+        float4* g = gbox + ((size_t)slot * ((N + 127) / 128) + blockIdx.x * 2 + threadIdx.x) * 2;
+        g[0] = make_float4(fminf(a[0], b[0]), fminf(a[1], b[1]), fminf(a[2], b[2]),
+                           __uint_as_float(max(__float_as_uint(a[6]), __float_as_uint(b[6]))));
+        g[1] = make_float4(fmaxf(a[3], b[3]), fmaxf(a[4], b[4]), fmaxf(a[5], b[5]), 0.0f);
+    }
 }
 
 // --------------------------------------------------------------------------
@@ -379,7 +431,7 @@ __device__ __forceinline__ void nn_search_body(
     const float4* __restrict__ thi, const float4* __restrict__ qbox, int ntiles, const float4* __restrict__ slo, const float4* __restrict__ shi,
     int nsuper, int super_cull, const int32_t* __restrict__ active, const int32_t* __restrict__ done, int S,
     unsigned long long* __restrict__ best, unsigned long long* __restrict__ counters, int by, int bx, int wid,
-    float4* stage_w) {
+    float4* stage_w, const float4* __restrict__ gbox) {
     const int lane = threadIdx.x & 63;
     // first culling round's super-tile boxes: independent of the start and
     // its queries, so their load overlaps the slot and query loads
@@ -398,6 +450,7 @@ __device__ __forceinline__ void nn_search_body(
     float qx[kCQPT], qy[kCQPT], qz[kCQPT], bound[kCQPT], bd[kCQPT];
     int bj[kCQPT];
     const float4* qs = q32 + (size_t)slot * N;
+    const float4* gb = gbox + ((size_t)slot * ((N + 127) / 128) + grp * kCWaves + __builtin_amdgcn_readfirstlane(wid)) * 2;
 #pragma unroll
     for (int k = 0; k < kCQPT; ++k) {
         const int i = i0 + 64 * k;
@@ -411,12 +464,12 @@ __device__ __forceinline__ void nn_search_body(
     const float wq = __uint_as_float(wave_umax(__float_as_uint(qx[0] + qy[1])));  // the query loads have landed
     const unsigned long long ph_t1 = __builtin_readcyclecounter() + (wq == 1.2345f ? 1 : 0);
     unsigned long long ph_cull[5] = {0, 0, 0, 0, 0};
-    const int visited = culled_search(stage_w, p4, tlo, thi, qbox, ntiles, slo, shi, nsuper, super_cull, S, split, qx,
-                                      qy, qz, bound, bd, bj, s0lo, s0hi, ph_cull);
+    const int visited = culled_search<true>(stage_w, p4, tlo, thi, qbox, ntiles, slo, shi, nsuper, super_cull, S, split, qx,
+                                      qy, qz, bound, bd, bj, s0lo, s0hi, gb, ph_cull);
 #else
     const int visited =
-        culled_search(stage_w, p4, tlo, thi, qbox, ntiles, slo, shi, nsuper, super_cull, S, split, qx, qy, qz, bound,
-                      bd, bj, s0lo, s0hi);
+        culled_search<true>(stage_w, p4, tlo, thi, qbox, ntiles, slo, shi, nsuper, super_cull, S, split, qx, qy, qz, bound,
+                      bd, bj, s0lo, s0hi, gb);
 #endif
     if (lane == 0 && counters) {  // spread over kCounterSlots cache lines (one address serialises)
         unsigned long long* cs = counters + kCounterStride * ((bx * kCWaves + wid + by) % kCounterSlots);
@@ -456,7 +509,8 @@ __device__ __forceinline__ void nn_search_body(
         const float4 *__restrict__ thi, const float4 *__restrict__ qbox, int ntiles, const float4 *__restrict__ slo,                          \
         const float4 *__restrict__ shi, int nsuper, int super_cull, const int32_t *__restrict__ active,      \
         const int32_t *__restrict__ done, int S, unsigned long long *__restrict__ best,                      \
-        unsigned long long *__restrict__ counters, const int32_t *__restrict__ nact_dev, int sblk, int want
+        unsigned long long *__restrict__ counters, const int32_t *__restrict__ nact_dev, int sblk, int want,   \
+        const float4 *__restrict__ gbox
 
 // Block -> (start, query group x split).  Unpipelined: the grid is
 // (sblk * S, running starts) as the host counted them.  Pipelined (nact_dev):
@@ -489,7 +543,7 @@ __global__ __launch_bounds__(kCBlock) __attribute__((amdgpu_waves_per_eu(5, 8)))
     int by, bx;
     if (!map_search_block(nact_dev, sblk, want, by, bx, S)) return;
     nn_search_body(q32, N, p4, tlo, thi, qbox, ntiles, slo, shi, nsuper, super_cull, active, done, S, best, counters,
-                   by, bx, wid, stage[wid]);
+                   by, bx, wid, stage[wid], gbox);
 }
 __global__ __launch_bounds__(kCBlock) __attribute__((amdgpu_waves_per_eu(6, 8))) void nn_search_kernel_o6(
     ORPCD_NN_SEARCH_ARGS) {
@@ -498,7 +552,7 @@ __global__ __launch_bounds__(kCBlock) __attribute__((amdgpu_waves_per_eu(6, 8)))
     int by, bx;
     if (!map_search_block(nact_dev, sblk, want, by, bx, S)) return;
     nn_search_body(q32, N, p4, tlo, thi, qbox, ntiles, slo, shi, nsuper, super_cull, active, done, S, best, counters,
-                   by, bx, wid, stage[wid]);
+                   by, bx, wid, stage[wid], gbox);
 }
 #undef ORPCD_NN_SEARCH_ARGS
 
@@ -1450,7 +1504,7 @@ __global__ __launch_bounds__(kCBlock) void nn1_kernel(const double* __restrict__
                 b = fminf(b, d2f(qx[k], qy[k], qz[k], p4[t * kTile]) * kSeedSlack + 1e-30f);
         bound[k] = b;
     }
-    culled_search(stage[wid], p4, tlo, thi, qbox, ntiles, slo, shi, nsuper, 1, 1, 0, qx, qy, qz, bound, bd, bj,
+    culled_search<false>(stage[wid], p4, tlo, thi, qbox, ntiles, slo, shi, nsuper, 1, 1, 0, qx, qy, qz, bound, bd, bj,
                   lane < nsuper ? slo[lane] : make_float4(0.f, 0.f, 0.f, 0.f),
                   lane < nsuper ? shi[lane] : make_float4(0.f, 0.f, 0.f, 0.f));
 #pragma unroll
@@ -1495,7 +1549,7 @@ hipError_t launch_xform(const orpcd_ctx* c, int nact, double r2, hipStream_t s, 
     xform_queries_kernel<<<dim3((unsigned)((N + 255) / 256), (unsigned)nact), 256, 0, s>>>(
         c->src.xyz64.p, N, c->active.p, c->Q.p, c->done.p, c->tgt.p4.p, (int)c->tgt.ntiles,
         seed_stride_for(c->tgt.ntiles), c->prevnn.p, search_r2(r2), c->opt.reseed, c->q32.p, c->best.p,
-        dev_nact ? c->ctl.p : nullptr);
+        dev_nact ? c->ctl.p : nullptr, c->gbox.p);
     return hipGetLastError();
 }
 
@@ -1522,7 +1576,8 @@ hipError_t launch_gicp_pass_pipelined(const orpcd_ctx* c, int nact_host, int pas
     kern<<<dim3((unsigned)grid), kCBlock, 0, s>>>(c->q32.p, N, c->tgt.p4.p, c->tgt.tlo.p, c->tgt.thi.p, c->tgt.qbox.p,
                                                   (int)c->tgt.ntiles, c->tgt.slo.p, c->tgt.shi.p, (int)c->tgt.nsuper,
                                                   c->opt.super_cull, c->active.p, c->done.p, 1, c->best.p,
-                                                  c->count_tiles ? c->counters.p : nullptr, c->ctl.p, sblk, want);
+                                                  c->count_tiles ? c->counters.p : nullptr, c->ctl.p, sblk, want,
+                                                  c->gbox.p);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     if (mid && (e = hipEventRecord(mid, s)) != hipSuccess) return e;
     const int ablk = accum_blocks(N);
@@ -1582,7 +1637,7 @@ hipError_t launch_gicp_pass(const orpcd_ctx* c, int nact, int pass, double r2, h
     kern<<<dim3((unsigned)(sblk * S), (unsigned)nact), kCBlock, 0, s>>>(
         c->q32.p, N, c->tgt.p4.p, c->tgt.tlo.p, c->tgt.thi.p, c->tgt.qbox.p, (int)c->tgt.ntiles, c->tgt.slo.p, c->tgt.shi.p,
         (int)c->tgt.nsuper, c->opt.super_cull, c->active.p, c->done.p, S, c->best.p,
-        c->count_tiles ? c->counters.p : nullptr, nullptr, sblk, c->opt.search_waves);
+        c->count_tiles ? c->counters.p : nullptr, nullptr, sblk, c->opt.search_waves, c->gbox.p);
     }
     if ((e = hipGetLastError()) != hipSuccess) return e;
     if (mid && (e = hipEventRecord(mid, s)) != hipSuccess) return e;

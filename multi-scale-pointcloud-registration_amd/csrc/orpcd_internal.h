@@ -177,6 +177,7 @@ struct orpcd_ctx {
     orpcd::DevBuf<unsigned> item_counts;     // per group: candidate count, then the exclusive offsets
     bool two_phase_ok = false;               // the batch's worst-case item list fits
     orpcd::DevBuf<float4> q32;      // B*N fp32 queries of the current pass (x,y,z,0)
+    orpcd::DevBuf<float4> gbox;     // B*ceil(N/128)*2: per search wave, its queries' box + worst bound
     orpcd::DevBuf<double> G;        // B*12 base pose (3x4, column convention)
     orpcd::DevBuf<double> T;        // B*16 accumulated ICP transform
     orpcd::DevBuf<double> Q;        // B*12 T*G (3x4)

@@ -351,6 +351,7 @@ int batch_setup(orpcd_ctx* c, const double* R0, const double* t0, int B, const o
     CTX_CHECK(c, c->prevnn.ensure((size_t)B * N));
     CTX_CHECK(c, c->best.ensure((size_t)B * N));
     CTX_CHECK(c, c->q32.ensure((size_t)B * N));
+    CTX_CHECK(c, c->gbox.ensure((size_t)B * ((N + 127) / 128) * 2));
     CTX_CHECK(c, c->G.ensure((size_t)B * 12));
     CTX_CHECK(c, c->T.ensure((size_t)B * 16));
     CTX_CHECK(c, c->Q.ensure((size_t)B * 12));
@@ -493,6 +494,7 @@ int orpcd_ctx_destroy(orpcd_ctx* c) {
     c->items.release();
     c->item_counts.release();
     c->q32.release();
+    c->gbox.release();
     c->done.release();
     c->active.release();
     c->ctl.release();
