@@ -283,32 +283,43 @@ __device__ __forceinline__ Sym3 rotate_sym(const double R[9], const Sym3& S) {
 // ---------------------------------------------------------------- 6x6 solve
 // O3D utility/Eigen.cpp SolveLinearSystemPSD with check_det=true:
 // det by partial-pivot LU; |det| < 1e-6 -> failure; else Eigen LDLT.
-// Row / column exchanges below are written as fully unrolled selects on a
-// compile-time index (never A[piv][j] with a runtime piv), so the 6x6 stays in
-// registers; the arithmetic and its order are those of the CPU restatement.
+// Row / column exchanges below index the 6x6 only at compile-time positions
+// (never A[piv][j] with a runtime piv), so it stays in registers; the
+// arithmetic and its order are those of the CPU restatement.  Every caller
+// runs the solve in ONE lane (icp_solve_kernel / finish_pass / fgr_irls lane
+// 0), so the pivot is made wave-uniform and each candidate exchange is a
+// scalar branch that moves registers only when taken (written as selects
+// over all candidates, the exchanges were ~half of the solve's 13k cycles,
+// tools/solve_bench.hip).
 __device__ __forceinline__ void swap_rows6(double A[6][6], int k, int p) {
+    p = __builtin_amdgcn_readfirstlane(p);
 #pragma unroll
     for (int i = 0; i < 6; ++i) {
         if (i <= k) continue;
-        const bool sw = i == p;
+        if (i == p) {
+            asm volatile("" ::: "memory");  // keep the branch: no speculation into selects
 #pragma unroll
-        for (int j = 0; j < 6; ++j) {
-            const double a = A[k][j], b = A[i][j];
-            A[k][j] = sw ? b : a;
-            A[i][j] = sw ? a : b;
+            for (int j = 0; j < 6; ++j) {
+                const double a = A[k][j];
+                A[k][j] = A[i][j];
+                A[i][j] = a;
+            }
         }
     }
 }
 __device__ __forceinline__ void swap_cols6(double A[6][6], int k, int p) {
+    p = __builtin_amdgcn_readfirstlane(p);
 #pragma unroll
     for (int i = 0; i < 6; ++i) {
         if (i <= k) continue;
-        const bool sw = i == p;
+        if (i == p) {
+            asm volatile("" ::: "memory");
 #pragma unroll
-        for (int j = 0; j < 6; ++j) {
-            const double a = A[j][k], b = A[j][i];
-            A[j][k] = sw ? b : a;
-            A[j][i] = sw ? a : b;
+            for (int j = 0; j < 6; ++j) {
+                const double a = A[j][k];
+                A[j][k] = A[j][i];
+                A[j][i] = a;
+            }
         }
     }
 }

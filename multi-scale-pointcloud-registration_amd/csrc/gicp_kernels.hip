@@ -1079,14 +1079,16 @@ __global__ __launch_bounds__(256) void scan_items_kernel(const float4* __restric
 size_t coop_smem_bytes(int W, int64_t ntiles) { return (size_t)ntiles * 2 + 16; }
 
 // --------------------------------------------------------------------------
-// Accumulation kernels: kAccQ queries per thread (grid = (blocks per start,
+// Accumulation kernels: accum_qpt(N) queries per thread (grid = (blocks per start,
 // running starts), 256 threads), each thread summing its queries' terms in
 // registers; then a fixed-order block reduction (DPP within rows of 16 lanes,
 // the four row sums, then the four waves) into one partial per block.  The
 // chosen correspondence is written back as the next pass's seed.
 // --------------------------------------------------------------------------
-constexpr int kAccQ = 4;
-constexpr int kAccBlockQ = 256 * kAccQ;
+// queries per thread.  A function of N only, so the fixed-order reduction is
+// the same for every batch composition.  Measured at C2: 1 (4x the blocks, 4x
+// the partials for the solve) 18.5 ms per multistart, 2: 17.9, 4: 17.8.
+__host__ __device__ __forceinline__ int accum_qpt(int64_t) { return 4; }
 
 template <int Ctrl>
 __device__ __forceinline__ double dpp_f64(double v) {
@@ -1323,8 +1325,9 @@ __global__ __launch_bounds__(256) void gicp_accum_kernel(
     for (int t = 0; t < 12; ++t) Q[t] = Qm[12 * slot + t];
 #pragma unroll
     for (int t = 0; t < 9; ++t) R[t] = Rm[9 * slot + t];
-    for (int k = 0; k < kAccQ; ++k) {
-        const int i = blockIdx.x * kAccBlockQ + k * 256 + threadIdx.x;
+    const int qpt = accum_qpt(N);
+    for (int k = 0; k < qpt; ++k) {
+        const int i = (blockIdx.x * qpt + k) * 256 + threadIdx.x;
         if (i >= N) break;
         const unsigned long long v = best[(size_t)slot * N + i];
         const int j = v == kNone ? -1 : (int)(unsigned)(v & 0xffffffffu);
@@ -1414,8 +1417,9 @@ __global__ __launch_bounds__(256) void p2p_accum_kernel(const double* __restrict
     double Q[12];
 #pragma unroll
     for (int t = 0; t < 12; ++t) Q[t] = Qm[12 * slot + t];
-    for (int k = 0; k < kAccQ; ++k) {
-        const int i = blockIdx.x * kAccBlockQ + k * 256 + threadIdx.x;
+    const int qpt = accum_qpt(N);
+    for (int k = 0; k < qpt; ++k) {
+        const int i = (blockIdx.x * qpt + k) * 256 + threadIdx.x;
         if (i >= N) break;
         const unsigned long long v = best[(size_t)slot * N + i];
         const int j = v == kNone ? -1 : (int)(unsigned)(v & 0xffffffffu);
@@ -1527,8 +1531,8 @@ __global__ __launch_bounds__(kCBlock) void nn1_kernel(const double* __restrict__
     }
 }
 
-int seed_stride_for(int64_t ntiles) {  // at most ~512 representatives per query
-    return (int)std::max<int64_t>(1, (ntiles + 511) / 512);
+int seed_stride_for(int64_t ntiles, int reps = 512) {  // at most ~reps representatives per query
+    return (int)std::max<int64_t>(1, (ntiles + reps - 1) / reps);
 }
 
 int search_splits(int nact, int blocks_per_start, int want) {
@@ -1536,7 +1540,7 @@ int search_splits(int nact, int blocks_per_start, int want) {
     return (int)std::min<int64_t>(64, std::max<int64_t>(1, (want + waves - 1) / waves));
 }
 
-int accum_blocks(int64_t N) { return (int)((N + kAccBlockQ - 1) / kAccBlockQ); }
+int accum_blocks(int64_t N) { return (int)((N + 256 * accum_qpt(N) - 1) / (256 * accum_qpt(N))); }
 
 // the cooperative search needs 16-bit tile ids in its LDS candidate list
 static bool use_coop(const orpcd_ctx* c) { return c->opt.search_kernel == 1 && c->tgt.ntiles <= 65535; }
@@ -1548,8 +1552,8 @@ hipError_t launch_xform(const orpcd_ctx* c, int nact, double r2, hipStream_t s, 
     const int N = (int)c->src.n;
     xform_queries_kernel<<<dim3((unsigned)((N + 255) / 256), (unsigned)nact), 256, 0, s>>>(
         c->src.xyz64.p, N, c->active.p, c->Q.p, c->done.p, c->tgt.p4.p, (int)c->tgt.ntiles,
-        seed_stride_for(c->tgt.ntiles), c->prevnn.p, search_r2(r2), c->opt.reseed, c->q32.p, c->best.p,
-        dev_nact ? c->ctl.p : nullptr, c->gbox.p);
+        seed_stride_for(c->tgt.ntiles, c->opt.seed_reps), c->prevnn.p, search_r2(r2), c->opt.reseed, c->q32.p,
+        c->best.p, dev_nact ? c->ctl.p : nullptr, c->gbox.p);
     return hipGetLastError();
 }
 

@@ -247,6 +247,8 @@ struct orpcd_ctx {
         int pipeline = 0;         // 1: passes enqueued ahead, running starts kept on the device;
                                   // 0: host sync every sync_every passes (also under ORPCD_TRACE)
         int lookahead = 4;        // pipelined: passes enqueued beyond the last one known complete
+        int seed_reps = 64;       // pass-0 seed: nearest of ~this many tile representatives per query
+                                  // (C2 sweep 8..512: equal within noise; 64 keeps the transform cheap)
     } opt;
     std::vector<hipEvent_t> ev_pool;
     orpcd::KernelStats stats;

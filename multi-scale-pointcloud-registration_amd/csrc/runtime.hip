@@ -1255,6 +1255,7 @@ int orpcd_set_option(orpcd_ctx* c, const char* key, double value) {
     else if (k == "scan_blocks" && v >= 1 && v <= 65536) c->opt.scan_blocks = v;
     else if (k == "pipeline" && (v == 0 || v == 1)) c->opt.pipeline = v;
     else if (k == "lookahead" && v >= 1 && v <= 64) c->opt.lookahead = v;
+    else if (k == "seed_reps" && v >= 1) c->opt.seed_reps = v;
     else {
         c->err = "set_option: unknown key or bad value: " + k;
         return ORPCD_EINVAL;
