@@ -446,6 +446,7 @@ __device__ __forceinline__ void nn_search_body(
     const unsigned long long ph_t0 = __builtin_readcyclecounter();
 #endif
     const int grp = bx / S, split = bx - grp * S;
+    if (grp * kCBlockQ + wid * (64 * kCQPT) >= N) return;  // a wave past the last query group (no gbox entry)
     const int i0 = grp * kCBlockQ + wid * (64 * kCQPT) + lane;
     float qx[kCQPT], qy[kCQPT], qz[kCQPT], bound[kCQPT], bd[kCQPT];
     int bj[kCQPT];

@@ -1,7 +1,7 @@
 set -e
 mkdir -p gpurun_out
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
-B="python3 bench.py --steps 3 --warmup 1 --cpu-seconds 0 --align 0"
+B="python3 bench.py --cpu-seconds 0 --align 0"  # default steps/warmup: the same kernel mix as the bench line
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/kt -- $B > gpurun_out/kt.log 2>&1
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/fetch -- $B > gpurun_out/fetch.log 2>&1
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/write -- $B > gpurun_out/write.log 2>&1
