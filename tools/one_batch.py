@@ -34,7 +34,9 @@ def main():
         t_0 = time.perf_counter()
         r = ctx.gicp_batch(R0, t0)
         print(f"gicp_batch {1e3 * (time.perf_counter() - t_0):.2f} ms")
-    print("iters", int(r["iters"].sum()))
+    import hashlib
+    h = hashlib.sha1(np.ascontiguousarray(r["T"]).tobytes() + r["rmse"].tobytes() + r["iters"].tobytes()).hexdigest()
+    print("iters", int(r["iters"].sum()), "result sha1", h[:16])
     ctx.close()
 
 
