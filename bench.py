@@ -92,6 +92,7 @@ def main():
 
     for k in range(args.warmup):
         step(k)
+    rmse_step0 = np.array(aligner.history[0]["rmse"]) if args.warmup > 0 else None  # seed 1000's starts
     ctx.reset_stats()
     ctx.profiling(True)
     barrier()
@@ -121,9 +122,19 @@ def main():
 
     cpu = None
     align_s = None
+    parity = None
     if rank == 0 and world == 1:
         if args.cpu_seconds > 0:
             cpu = cpu_baseline(source, target, args)
+            # "final RMSE vs ref": the GPU's per-start inlier RMSE of step 0 against the
+            # oracle's on the same starts (stated full-size tolerance 1e-5)
+            o = np.array(cpu.pop("oracle_rmse"))
+            if rmse_step0 is not None and len(o):
+                d = np.abs(rmse_step0[: len(o)] - o)
+                parity = {"starts": int(len(o)), "max_abs_d_rmse": float(d.max()),
+                          "within_1e-5": int((d <= 1e-5).sum()),
+                          "multistart_min_rmse_gpu": float(rmse_step0[: len(o)].min()),
+                          "multistart_min_rmse_oracle": float(o.min())}
         if args.align:
             # one cold align() (device contexts of the speculative compass created
             # inside it), then the same align() warm: the figure reported
@@ -176,6 +187,7 @@ def main():
                              8.0 * st["passes"] * len(source) * len(target) / max(st["launches"], 1)
                              / (avg_ms * 1e-3) / 1e12, 1) if avg_ms > 0 else None},
             "cpu_baseline": cpu,
+            "parity_vs_oracle": parity,
             "gicp_iterations": int(iters),
             "align": align_s,
         }
@@ -210,14 +222,17 @@ def cpu_baseline(source, target, args):
     t0 = time.perf_counter()
     iters = 0
     done = 0
+    oracle_rmse = []
     for R0, t0_ in starts:
         r = O.gicp(np.dot(source, R0) + t0_, target, 0.5, 100)
         iters += r["iters"]
+        oracle_rmse.append(float(r["rmse"]))
         done += 1
         if time.perf_counter() - t0 > args.cpu_seconds:
             break
     el = time.perf_counter() - t0
-    return {"value": round(iters / el, 3), "unit": "GICP iterations/s", "cores": O.num_threads(),
+    return {"oracle_rmse": oracle_rmse, "value": round(iters / el, 3), "unit": "GICP iterations/s",
+            "cores": O.num_threads(),
             "kind": "port",
             "sample": f"{done} of {args.attempts} starts of step 0 (same R0,t0), {iters} GICP iterations, "
                       f"{el:.1f} s, {os.cpu_count()} host cpus visible"}
