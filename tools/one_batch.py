@@ -16,12 +16,15 @@ from workloads import c2_pair, rot_xyz  # noqa: E402
 def main():
     cfg = json.loads(sys.argv[1]) if len(sys.argv) > 1 and sys.argv[1].startswith("{") else {}
     reps = int(sys.argv[sys.argv.index("--reps") + 1]) if "--reps" in sys.argv else 2
+    starts = int(sys.argv[sys.argv.index("--starts") + 1]) if "--starts" in sys.argv else 30
     s, t = c2_pair(50000)
     s = Preprocessor([]).preprocess(s)
     t = Preprocessor([]).preprocess(t)
     rng = np.random.default_rng(1000)
     R0 = np.array([rot_xyz(*rng.uniform(-90, 90, 3)) for _ in range(30)])
     t0 = rng.normal(size=(30, 3)) * 0.1
+    if starts != 30:  # the first starts of the same stream, or it repeated
+        R0, t0 = np.resize(R0, (starts, 3, 3)), np.resize(t0, (starts, 3))
     ctx = _native.Context(0)
     for k, v in cfg.items():
         if k == "profiling":
@@ -33,7 +36,7 @@ def main():
     for _ in range(reps):
         t_0 = time.perf_counter()
         r = ctx.gicp_batch(R0, t0)
-        print(f"gicp_batch {1e3 * (time.perf_counter() - t_0):.2f} ms")
+        print(f"gicp_batch {1e3 * (time.perf_counter() - t_0):.2f} ms", flush=True)
     import hashlib
     h = hashlib.sha1(np.ascontiguousarray(r["T"]).tobytes() + r["rmse"].tobytes() + r["iters"].tobytes()).hexdigest()
     print("iters", int(r["iters"].sum()), "result sha1", h[:16])
