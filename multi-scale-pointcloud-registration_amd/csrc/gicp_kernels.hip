@@ -134,22 +134,29 @@ __device__ __forceinline__ int culled_search(float4* stage, const float4* __rest
     // the wave box; the 64 tiles of each surviving super-tile form one round.
     int sb = -64;                  // super-tile round base
     unsigned long long smask = 0;  // surviving super-tiles of that round
-    int tb = 0;                    // tile round base (= super-tile * 64)
     unsigned long long mask = 0;
     float lb = inf;
     float4 a = make_float4(0.f, 0.f, 0.f, 0.f), b = a;
 #ifdef ORPCD_PHASES
     unsigned long long ph_cull = 0, ph_rounds = 0, ph_tests = 0, ph_impr = 0, ph_need = 0;
 #endif
-    // the tile AABBs of the NEXT surviving super-tile are loaded while the
-    // current round is tested and scanned (one round of load latency hidden)
-    int tbn = -1;  // base of the prefetched round (-1: none)
+    // the tile AABBs of the NEXT round are loaded while the current round is
+    // tested and scanned (one round of load latency hidden).  A round holds
+    // this split's tiles of up to P surviving super-tiles, packed over the
+    // lanes: split s owns tiles s, s+S, ... of each super-tile (per of them),
+    // so with S splits one round covers P = 64/per super-tiles instead of one
+    // (S = 1: one super-tile, one tile per lane).  Lanes follow increasing
+    // tile order, so candidates are visited in the same order as before.
+    const int per = S == 1 ? kSuper : (kSuper - s + S - 1) / S;
+    const int P = kSuper / per;
+    bool haven = false;  // a prefetched round exists
+    int tln = -1;        // this lane's tile in the prefetched round (-1: none)
     float4 an = a, bn = b;
     auto prefetch_round = [&]() {
         while (smask == 0) {
             sb += 64;
             if (sb >= nsuper) {
-                tbn = -1;
+                haven = false;
                 return;
             }
             const int u = sb + lane;
@@ -167,32 +174,41 @@ __device__ __forceinline__ int culled_search(float4* stage, const float4* __rest
             }
             smask = __ballot(sl < W);
         }
-        tbn = (sb + __builtin_ctzll(smask)) * kSuper;
-        smask &= smask - 1;
-        const int t = tbn + lane;
-        if (t < ntiles && (S == 1 || t % S == s)) {
+        haven = true;
+        const int lr = lane / per, lm = lane - lr * per;  // lane -> (super-tile of the round, tile of it)
+        int su = -1;
+        for (int r = 0; r < P && smask; ++r) {  // the next P surviving super-tiles (scalar)
+            const int st = sb + __builtin_ctzll(smask);
+            smask &= smask - 1;
+            if (lr == r) su = st;
+        }
+        const int tin = S == 1 ? lm : s + S * lm;  // tile within the super-tile
+        const int t = su * kSuper + tin;
+        if (su >= 0 && tin < kSuper && t < ntiles) {
+            tln = t;
             an = tlo[t];
             bn = thi[t];
         } else {
+            tln = -1;
             an = make_float4(inf, inf, inf, 0.f);  // empty box: never within the bound
             bn = make_float4(-inf, -inf, -inf, 0.f);
         }
     };
     prefetch_round();
+    int tl = -1;  // this lane's tile in the current round
     auto next_candidate_impl = [&](float& lbk) -> int {
         for (;;) {
             while (mask == 0) {
-                if (tbn < 0) return -1;
-                tb = tbn;
+                if (!haven) return -1;
+                tl = tln;
                 a = an;
                 b = bn;
 #ifdef ORPCD_PHASES
                 ++ph_rounds;
 #endif
                 prefetch_round();
-                const int t = tb + lane;
                 lb = inf;
-                if (t < ntiles && (S == 1 || t % S == s)) {
+                if (tl >= 0) {
                     const float dx = fmaxf(0.0f, fmaxf(a.x - hix, lox - b.x));
                     const float dy = fmaxf(0.0f, fmaxf(a.y - hiy, loy - b.y));
                     const float dz = fmaxf(0.0f, fmaxf(a.z - hiz, loz - b.z));
@@ -222,7 +238,7 @@ __device__ __forceinline__ int culled_search(float4* stage, const float4* __rest
                 if (b0 | b1) ph_need += __builtin_popcountll(b0) + __builtin_popcountll(b1);
             }
 #endif
-            if (__any(need0 || need1)) return tb + k;
+            if (__any(need0 || need1)) return __builtin_amdgcn_readlane(tl, k);
         }
     };
 
