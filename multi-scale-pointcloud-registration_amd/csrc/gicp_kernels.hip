@@ -150,7 +150,23 @@ __device__ __forceinline__ int culled_search(float4* stage, const float4* __rest
     const int per = S == 1 ? kSuper : (kSuper - s + S - 1) / S;
     const int P = kSuper / per;
     bool haven = false;  // a prefetched round exists
-    int tln = -1;        // this lane's tile in the prefetched round (-1: none)
+    // the prefetched round's super-tile base and surviving mask before it was
+    // consumed (scalar): lanes recompute their tile from them at the switch
+    // instead of holding it in a VGPR through the scan
+    int nsb = 0;
+    unsigned long long nmask = 0;
+    auto lane_tile = [&](int base, unsigned long long m) -> int {
+        const int lr = lane / per, lm = lane - lr * per;  // lane -> (super-tile of the round, tile of it)
+        int su = -1;
+        for (int r = 0; r < P && m; ++r) {  // the next P surviving super-tiles (scalar)
+            const int st = base + __builtin_ctzll(m);
+            m &= m - 1;
+            if (lr == r) su = st;
+        }
+        const int tin = S == 1 ? lm : s + S * lm;  // tile within the super-tile
+        const int t = su * kSuper + tin;
+        return su >= 0 && tin < kSuper && t < ntiles ? t : -1;
+    };
     float4 an = a, bn = b;
     auto prefetch_round = [&]() {
         while (smask == 0) {
@@ -175,40 +191,34 @@ __device__ __forceinline__ int culled_search(float4* stage, const float4* __rest
             smask = __ballot(sl < W);
         }
         haven = true;
-        const int lr = lane / per, lm = lane - lr * per;  // lane -> (super-tile of the round, tile of it)
-        int su = -1;
-        for (int r = 0; r < P && smask; ++r) {  // the next P surviving super-tiles (scalar)
-            const int st = sb + __builtin_ctzll(smask);
-            smask &= smask - 1;
-            if (lr == r) su = st;
-        }
-        const int tin = S == 1 ? lm : s + S * lm;  // tile within the super-tile
-        const int t = su * kSuper + tin;
-        if (su >= 0 && tin < kSuper && t < ntiles) {
-            tln = t;
+        nsb = sb;
+        nmask = smask;
+        const int t = lane_tile(sb, smask);
+        for (int r = 0; r < P && smask; ++r) smask &= smask - 1;  // those super-tiles are taken
+        if (t >= 0) {
             an = tlo[t];
             bn = thi[t];
         } else {
-            tln = -1;
             an = make_float4(inf, inf, inf, 0.f);  // empty box: never within the bound
             bn = make_float4(-inf, -inf, -inf, 0.f);
         }
     };
     prefetch_round();
-    int tl = -1;  // this lane's tile in the current round
+    int csb = 0;                  // the current round's super-tile base and mask (scalar)
+    unsigned long long cmask = 0;
     auto next_candidate_impl = [&](float& lbk) -> int {
         for (;;) {
             while (mask == 0) {
                 if (!haven) return -1;
-                tl = tln;
+                csb = nsb;
+                cmask = nmask;
                 a = an;
                 b = bn;
 #ifdef ORPCD_PHASES
                 ++ph_rounds;
 #endif
                 prefetch_round();
-                lb = inf;
-                if (tl >= 0) {
+                {  // lanes without a tile hold the empty box: lb = inf
                     const float dx = fmaxf(0.0f, fmaxf(a.x - hix, lox - b.x));
                     const float dy = fmaxf(0.0f, fmaxf(a.y - hiy, loy - b.y));
                     const float dz = fmaxf(0.0f, fmaxf(a.z - hiz, loz - b.z));
@@ -238,7 +248,12 @@ __device__ __forceinline__ int culled_search(float4* stage, const float4* __rest
                 if (b0 | b1) ph_need += __builtin_popcountll(b0) + __builtin_popcountll(b1);
             }
 #endif
-            if (__any(need0 || need1)) return __builtin_amdgcn_readlane(tl, k);
+            if (__any(need0 || need1)) {  // lane k's tile, from the round's scalar state
+                const int r = k / per, m = k - r * per;
+                unsigned long long cm = cmask;
+                for (int i = 0; i < r; ++i) cm &= cm - 1;
+                return (csb + __builtin_ctzll(cm)) * kSuper + (S == 1 ? m : s + S * m);
+            }
         }
     };
 
