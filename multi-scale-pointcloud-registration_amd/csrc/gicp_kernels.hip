@@ -466,10 +466,18 @@ __device__ __forceinline__ void nn_search_body(
     const int lane = threadIdx.x & 63;
     // first culling round's super-tile boxes: independent of the start and
     // its queries, so their load overlaps the slot and query loads
-    float4 s0lo = make_float4(0.f, 0.f, 0.f, 0.f), s0hi = s0lo;
-    if (lane < nsuper) {
-        s0lo = slo[lane];
-        s0hi = shi[lane];
+    // (xyz only, by raw buffer loads: lanes past nsuper read zeros, unguarded;
+    // a guarded 16 B load whose unused .w register was reused forced a wait
+    // for it before the query loads were issued)
+    float4 s0lo, s0hi;
+    {
+        const int nb = nsuper * (int)sizeof(float4);
+        const auto lo = __builtin_amdgcn_raw_buffer_load_b96(
+            __builtin_amdgcn_make_buffer_rsrc(const_cast<float4*>(slo), (short)0, nb, 0x00020000), lane * 16, 0, 0);
+        const auto hi = __builtin_amdgcn_raw_buffer_load_b96(
+            __builtin_amdgcn_make_buffer_rsrc(const_cast<float4*>(shi), (short)0, nb, 0x00020000), lane * 16, 0, 0);
+        s0lo = make_float4(__uint_as_float(lo[0]), __uint_as_float(lo[1]), __uint_as_float(lo[2]), 0.f);
+        s0hi = make_float4(__uint_as_float(hi[0]), __uint_as_float(hi[1]), __uint_as_float(hi[2]), 0.f);
     }
     const int slot = active[by];
     if (done[slot]) return;
@@ -483,14 +491,19 @@ __device__ __forceinline__ void nn_search_body(
     int bj[kCQPT];
     const float4* qs = q32 + (size_t)slot * N;
     const float4* gb = gbox + ((size_t)slot * ((N + 127) / 128) + grp * kCWaves + __builtin_amdgcn_readfirstlane(wid)) * 2;
+    // the queries by raw buffer loads: a lane past N reads zeros (bound 0: never
+    // takes anything) without a guard.  Guarded global loads were each put in
+    // a branch with its own wait, which serialised the two.
+    const __amdgpu_buffer_rsrc_t qrs =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<float4*>(qs), (short)0, N * (int)sizeof(float4), 0x00020000);
 #pragma unroll
     for (int k = 0; k < kCQPT; ++k) {
         const int i = i0 + 64 * k;
-        const float4 q = i < N ? qs[i] : make_float4(0.f, 0.f, 0.f, 0.f);
-        qx[k] = q.x;
-        qy[k] = q.y;
-        qz[k] = q.z;
-        bound[k] = q.w;  // 0 for padding lanes: never takes anything
+        const auto q = __builtin_amdgcn_raw_buffer_load_b128(qrs, i * (int)sizeof(float4), 0, 0);
+        qx[k] = __uint_as_float(q[0]);
+        qy[k] = __uint_as_float(q[1]);
+        qz[k] = __uint_as_float(q[2]);
+        bound[k] = __uint_as_float(q[3]);
     }
 #ifdef ORPCD_PHASES
     const float wq = __uint_as_float(wave_umax(__float_as_uint(qx[0] + qy[1])));  // the query loads have landed
