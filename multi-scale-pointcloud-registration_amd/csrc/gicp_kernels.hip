@@ -1680,13 +1680,16 @@ hipError_t launch_gicp_pass(const orpcd_ctx* c, int nact, int pass, double r2, h
             c->tgt.p4.p, c->tgt.tlo.p, c->tgt.thi.p, (int)c->tgt.ntiles, c->tgt.slo.p, c->tgt.shi.p,
             (int)c->tgt.nsuper, c->active.p, c->done.p, c->best.p, c->count_tiles ? c->counters.p : nullptr);
     } else {
-    const int S = search_splits(nact, sblk, c->opt.search_waves);
+    // few running starts: half the wave target (8 starts: 16k waves 8.16 ms vs
+    // 32k 8.40 ms per batch; 30 starts keep 32k).  Splits never change answers.
+    const int want = nact <= c->opt.small_batch ? c->opt.search_waves / 2 : c->opt.search_waves;
+    const int S = search_splits(nact, sblk, want);
     // best[] was reset to kNone by xform_queries_kernel
     auto kern = c->opt.search_occupancy == 6 ? nn_search_kernel_o6 : nn_search_kernel;
     kern<<<dim3((unsigned)(sblk * S), (unsigned)nact), kCBlock, 0, s>>>(
         c->q32.p, N, c->tgt.p4.p, c->tgt.tlo.p, c->tgt.thi.p, c->tgt.qbox.p, (int)c->tgt.ntiles, c->tgt.slo.p, c->tgt.shi.p,
         (int)c->tgt.nsuper, c->opt.super_cull, c->active.p, c->done.p, S, c->best.p,
-        c->count_tiles ? c->counters.p : nullptr, nullptr, sblk, c->opt.search_waves, c->gbox.p);
+        c->count_tiles ? c->counters.p : nullptr, nullptr, sblk, want, c->gbox.p);
     }
     if ((e = hipGetLastError()) != hipSuccess) return e;
     if (mid && (e = hipEventRecord(mid, s)) != hipSuccess) return e;

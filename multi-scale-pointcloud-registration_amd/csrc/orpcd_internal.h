@@ -236,6 +236,7 @@ struct orpcd_ctx {
     // tunables (orpcd_set_option): defaults are the measured best on MI355X
     struct Options {
         int search_waves = 32768;  // split a start's tiles until ~this many waves run (A/B: tools/ab_search.py)
+        int small_batch = 8;      // at most this many running starts: half the search_waves target
         int sync_every = 8;       // passes between host checks of the done flags (C2 sweep: 4 17.6 ms, 8-16 17.3)
         int super_cull = 1;       // first culling level over 64-tile super-tiles
         int reseed = 0;           // representative seeding also after pass 0

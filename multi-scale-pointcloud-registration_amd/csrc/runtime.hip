@@ -1249,6 +1249,7 @@ int orpcd_set_option(orpcd_ctx* c, const char* key, double value) {
     if (k == "search_waves" && v >= 1) c->opt.search_waves = v;
     else if (k == "sync_every" && v >= 1 && v <= 64) c->opt.sync_every = v;
     else if (k == "super_cull" && (v == 0 || v == 1)) c->opt.super_cull = v;
+    else if (k == "small_batch" && v >= 0) c->opt.small_batch = v;
     else if (k == "reseed" && (v == 0 || v == 1)) c->opt.reseed = v;
     else if (k == "search_occupancy" && (v == 0 || v == 6)) c->opt.search_occupancy = v;
     else if (k == "search_kernel" && v >= 0 && v <= 2) c->opt.search_kernel = v;
