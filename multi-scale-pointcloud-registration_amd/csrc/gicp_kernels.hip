@@ -383,6 +383,13 @@ __device__ __forceinline__ void xform(const double Q[12], const double p[3], dou
     q[2] = Q[8] * p[0] + Q[9] * p[1] + Q[10] * p[2] + Q[11];
 }
 
+// The target's fp32 frame origin (CloudLayout::org): an fp32 query is
+// (float)(q - org), subtracted in fp64 before the one rounding.
+struct Org3 {
+    double x, y, z;
+};
+static inline Org3 org_of(const CloudLayout& L) { return Org3{L.org[0], L.org[1], L.org[2]}; }
+
 // upper-triangle index of (a,b), a<=b, in a 6x6
 __device__ __forceinline__ constexpr int ut(int a, int b) { return a * 6 - a * (a - 1) / 2 + (b - a); }
 
@@ -407,7 +414,7 @@ __global__ __launch_bounds__(256) void xform_queries_kernel(const double* __rest
                                                             float r2s, int reseed, float4* __restrict__ q32,
                                                             unsigned long long* __restrict__ best,
                                                             const int32_t* __restrict__ nact_dev,
-                                                            float4* __restrict__ gbox) {
+                                                            float4* __restrict__ gbox, Org3 org) {
     if (nact_dev && (int)blockIdx.y >= *nact_dev) return;  // pipelined: grid sized for an upper bound
     const int slot = active[blockIdx.y];
     if (done[slot]) return;
@@ -423,7 +430,7 @@ __global__ __launch_bounds__(256) void xform_queries_kernel(const double* __rest
         const double p[3] = {src[3 * i], src[3 * i + 1], src[3 * i + 2]};
         double q[3];
         xform(Q, p, q);
-        x = (float)q[0], y = (float)q[1], z = (float)q[2];
+        x = (float)(q[0] - org.x), y = (float)(q[1] - org.y), z = (float)(q[2] - org.z);
         bound = r2s;
         const int jp = prevnn[(size_t)slot * N + i];
         if (jp >= 0) {
@@ -627,7 +634,7 @@ __global__ __launch_bounds__(1024) void nn_search_coop_kernel(
     float r2s, int reseed, int seed_stride, const float4* __restrict__ p4, const float4* __restrict__ tlo,
     const float4* __restrict__ thi, int ntiles, const float4* __restrict__ slo, const float4* __restrict__ shi,
     int nsuper, const int32_t* __restrict__ active, const int32_t* __restrict__ done,
-    unsigned long long* __restrict__ best, unsigned long long* __restrict__ counters) {
+    unsigned long long* __restrict__ best, unsigned long long* __restrict__ counters, Org3 org) {
     const int slot = active[blockIdx.y];
     if (done[slot]) return;
     extern __shared__ uint16_t cand[];  // candidate tiles of the group (dynamic: ntiles entries)
@@ -651,7 +658,7 @@ __global__ __launch_bounds__(1024) void nn_search_coop_kernel(
                 const double pp[3] = {src[3 * i], src[3 * i + 1], src[3 * i + 2]};
                 double q[3];
                 xform(Q, pp, q);
-                const float x = (float)q[0], y = (float)q[1], z = (float)q[2];
+                const float x = (float)(q[0] - org.x), y = (float)(q[1] - org.y), z = (float)(q[2] - org.z);
                 float bound = r2s;
                 const int jp = prevnn[(size_t)slot * N + i];
                 if (jp >= 0) {
@@ -844,7 +851,7 @@ __global__ __launch_bounds__(256) void cull_groups_kernel(
     const float4* __restrict__ thi, int ntiles, const float4* __restrict__ slo, const float4* __restrict__ shi,
     int nsuper, const int32_t* __restrict__ active, const int32_t* __restrict__ done, int gblk,
     float4* __restrict__ q32, unsigned long long* __restrict__ best, unsigned* __restrict__ items,
-    unsigned* __restrict__ gcount) {
+    unsigned* __restrict__ gcount, Org3 org) {
     __shared__ unsigned buf[4][kCullBuf];
     const int lane = threadIdx.x & 63, wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int group = blockIdx.x * 4 + wid;
@@ -868,7 +875,7 @@ __global__ __launch_bounds__(256) void cull_groups_kernel(
             const double pp[3] = {src[3 * i], src[3 * i + 1], src[3 * i + 2]};
             double q[3];
             xform(Q, pp, q);
-            const float x = (float)q[0], y = (float)q[1], z = (float)q[2];
+            const float x = (float)(q[0] - org.x), y = (float)(q[1] - org.y), z = (float)(q[2] - org.z);
             float b = r2s;
             const int jp = prevnn[(size_t)slot * N + i];
             if (jp >= 0) {
@@ -1534,7 +1541,7 @@ __global__ __launch_bounds__(kCBlock) void nn1_kernel(const double* __restrict__
                                                       const float4* __restrict__ slo, const float4* __restrict__ shi,
                                                       int nsuper, int seed_stride, const double* __restrict__ tgt64,
                                                       const int32_t* __restrict__ tperm, double r2, float r2s,
-                                                      int32_t* __restrict__ idx, double* __restrict__ d2o) {
+                                                      int32_t* __restrict__ idx, double* __restrict__ d2o, Org3 org) {
     __shared__ float4 stage[kCWaves][kTile];
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     const int i0 = blockIdx.x * kCBlockQ + wid * (64 * kCQPT) + lane;
@@ -1544,9 +1551,9 @@ __global__ __launch_bounds__(kCBlock) void nn1_kernel(const double* __restrict__
     for (int k = 0; k < kCQPT; ++k) {
         const int i = i0 + 64 * k;
         const bool valid = i < nq;
-        qx[k] = valid ? (float)q64[3 * i] : 0.f;
-        qy[k] = valid ? (float)q64[3 * i + 1] : 0.f;
-        qz[k] = valid ? (float)q64[3 * i + 2] : 0.f;
+        qx[k] = valid ? (float)(q64[3 * i] - org.x) : 0.f;
+        qy[k] = valid ? (float)(q64[3 * i + 1] - org.y) : 0.f;
+        qz[k] = valid ? (float)(q64[3 * i + 2] - org.z) : 0.f;
         float b = valid ? r2s : 0.0f;
         if (valid)
             for (int t = 0; t < ntiles; t += seed_stride)
@@ -1598,7 +1605,7 @@ hipError_t launch_xform(const orpcd_ctx* c, int nact, double r2, hipStream_t s, 
     xform_queries_kernel<<<dim3((unsigned)((N + 255) / 256), (unsigned)nact), 256, 0, s>>>(
         c->src.xyz64.p, N, c->active.p, c->Q.p, c->done.p, c->tgt.p4.p, (int)c->tgt.ntiles,
         seed_stride_for(c->tgt.ntiles, c->opt.seed_reps), c->prevnn.p, search_r2(r2), c->opt.reseed, c->q32.p,
-        c->best.p, dev_nact ? c->ctl.p : nullptr, c->gbox.p);
+        c->best.p, dev_nact ? c->ctl.p : nullptr, c->gbox.p, org_of(c->tgt));
     return hipGetLastError();
 }
 
@@ -1658,7 +1665,8 @@ hipError_t launch_gicp_pass(const orpcd_ctx* c, int nact, int pass, double r2, h
         cull_groups_kernel<<<dim3((unsigned)((gblk + 3) / 4), (unsigned)nact), 256, 0, s>>>(
             c->src.xyz64.p, N, c->Q.p, c->prevnn.p, search_r2(r2), c->opt.reseed, seed_stride_for(c->tgt.ntiles),
             c->tgt.p4.p, c->tgt.tlo.p, c->tgt.thi.p, (int)c->tgt.ntiles, c->tgt.slo.p, c->tgt.shi.p,
-            (int)c->tgt.nsuper, c->active.p, c->done.p, gblk, c->q32.p, c->best.p, c->items.p, gcount);
+            (int)c->tgt.nsuper, c->active.p, c->done.p, gblk, c->q32.p, c->best.p, c->items.p, gcount,
+            org_of(c->tgt));
         if ((e = hipGetLastError()) != hipSuccess) return e;
         items_prefix_kernel<<<1, 1024, 0, s>>>(gcount, G, offs);
         if ((e = hipGetLastError()) != hipSuccess) return e;
@@ -1678,7 +1686,8 @@ hipError_t launch_gicp_pass(const orpcd_ctx* c, int nact, int pass, double r2, h
         nn_search_coop_kernel<<<dim3((unsigned)gblk, (unsigned)nact), 64 * W, smem, s>>>(
             c->src.xyz64.p, N, c->Q.p, c->prevnn.p, search_r2(r2), c->opt.reseed, seed_stride_for(c->tgt.ntiles),
             c->tgt.p4.p, c->tgt.tlo.p, c->tgt.thi.p, (int)c->tgt.ntiles, c->tgt.slo.p, c->tgt.shi.p,
-            (int)c->tgt.nsuper, c->active.p, c->done.p, c->best.p, c->count_tiles ? c->counters.p : nullptr);
+            (int)c->tgt.nsuper, c->active.p, c->done.p, c->best.p, c->count_tiles ? c->counters.p : nullptr,
+            org_of(c->tgt));
     } else {
     // few running starts: half the wave target (8 starts: 16k waves 8.16 ms vs
     // 32k 8.40 ms per batch; 30 starts keep 32k).  Splits never change answers.
@@ -1740,7 +1749,7 @@ hipError_t launch_nn1(const double* q, int64_t nq, const CloudLayout& t, double 
     const unsigned grid = (unsigned)((nq + kCBlockQ - 1) / kCBlockQ);
     nn1_kernel<<<grid, kCBlock, 0, s>>>(q, (int)nq, t.p4.p, t.tlo.p, t.thi.p, t.qbox.p, (int)t.ntiles, t.slo.p, t.shi.p,
                                         (int)t.nsuper, seed_stride_for(t.ntiles), t.xyz64.p, t.perm.p, r2,
-                                        search_r2(r2), idx, d2);
+                                        search_r2(r2), idx, d2, org_of(t));
     return hipGetLastError();
 }
 

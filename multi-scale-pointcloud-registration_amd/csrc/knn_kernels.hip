@@ -84,8 +84,8 @@ template <int K>
 __global__ __launch_bounds__(256) void knn_tiles_kernel(
     const double* __restrict__ xyz64, const int32_t* __restrict__ perm, int n, const float4* __restrict__ tlo,
     const float4* __restrict__ thi, int ntiles, const float4* __restrict__ slo, const float4* __restrict__ shi,
-    int nsuper, const double* __restrict__ in64, double r2, float margin, int kout, int out_input_order,
-    double* __restrict__ rawcov6, int32_t* __restrict__ nbr_idx, double* __restrict__ nbr_d2,
+    int nsuper, const double* __restrict__ in64, double r2, float margin, double ox, double oy, double oz, int kout,
+    int out_input_order, double* __restrict__ rawcov6, int32_t* __restrict__ nbr_idx, double* __restrict__ nbr_d2,
     int32_t* __restrict__ nbr_cnt, double* __restrict__ mean_dist) {
     __shared__ double sx[4][kTile], sy[4][kTile], sz[4][kTile];
     __shared__ int32_t sid[4][kTile];
@@ -159,7 +159,7 @@ __global__ __launch_bounds__(256) void knn_tiles_kernel(
     }
 
     const float inf = 3.0e38f;
-    const float fx = (float)qx, fy = (float)qy, fz = (float)qz;
+    const float fx = (float)(qx - ox), fy = (float)(qy - oy), fz = (float)(qz - oz);  // the boxes' fp32 frame
     const float lox = wave_fmin(valid ? fx : inf), hix = wave_fmax(valid ? fx : -inf);
     const float loy = wave_fmin(valid ? fy : inf), hiy = wave_fmax(valid ? fy : -inf);
     const float loz = wave_fmin(valid ? fz : inf), hiz = wave_fmax(valid ? fz : -inf);
@@ -316,15 +316,15 @@ __device__ __forceinline__ void bitonic_sort64(double& d, int& i, int lane) {
 __global__ __launch_bounds__(256) void knn_wave_kernel(
     const double* __restrict__ xyz64, const int32_t* __restrict__ perm, int n, const float4* __restrict__ tlo,
     const float4* __restrict__ thi, int ntiles, const float4* __restrict__ slo, const float4* __restrict__ shi,
-    int nsuper, const double* __restrict__ in64, double r2, float margin, int K, int out_input_order,
-    double* __restrict__ rawcov6, int32_t* __restrict__ nbr_idx, double* __restrict__ nbr_d2,
+    int nsuper, const double* __restrict__ in64, double r2, float margin, double ox, double oy, double oz, int K,
+    int out_input_order, double* __restrict__ rawcov6, int32_t* __restrict__ nbr_idx, double* __restrict__ nbr_d2,
     int32_t* __restrict__ nbr_cnt, double* __restrict__ mean_dist) {
 #pragma clang fp contract(off)
     const int lane = threadIdx.x & 63;
     const int q = blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     if (q >= n) return;  // wave-uniform
     const double qx = xyz64[3 * q], qy = xyz64[3 * q + 1], qz = xyz64[3 * q + 2];
-    const float fx = (float)qx, fy = (float)qy, fz = (float)qz;
+    const float fx = (float)(qx - ox), fy = (float)(qy - oy), fz = (float)(qz - oz);  // the boxes' fp32 frame
     const double INF = __builtin_huge_val();
     double Ld = INF;  // sorted kept list: lane s holds the s-th nearest so far
     int Li = 0x7fffffff;
@@ -464,14 +464,16 @@ hipError_t launch_knn_tiles(const CloudLayout& L, const double* in64, int k, dou
     if (!lane_per_query && k >= 1 && k <= 64) {
         knn_wave_kernel<<<(unsigned)((L.n + 3) / 4), 256, 0, s>>>(
             L.xyz64.p, L.perm.p, (int)L.n, L.tlo.p, L.thi.p, (int)L.ntiles, L.slo.p, L.shi.p, (int)L.nsuper, in64, r2,
-            (float)margin, k, out_input_order ? 1 : 0, rawcov6, nbr_idx, nbr_d2, nbr_cnt, mean_dist);
+            (float)margin, L.org[0], L.org[1], L.org[2], k, out_input_order ? 1 : 0, rawcov6, nbr_idx, nbr_d2, nbr_cnt,
+            mean_dist);
         return hipGetLastError();
     }
     const dim3 grid((unsigned)((L.ntiles + 3) / 4));
 #define ORPCD_KNN_TILES(KK)                                                                                      \
     knn_tiles_kernel<KK><<<grid, 256, 0, s>>>(L.xyz64.p, L.perm.p, (int)L.n, L.tlo.p, L.thi.p, (int)L.ntiles,   \
-                                              L.slo.p, L.shi.p, (int)L.nsuper, in64, r2, (float)margin, k,      \
-                                              out_input_order ? 1 : 0, rawcov6, nbr_idx, nbr_d2, nbr_cnt, mean_dist)
+                                              L.slo.p, L.shi.p, (int)L.nsuper, in64, r2, (float)margin,         \
+                                              L.org[0], L.org[1], L.org[2], k, out_input_order ? 1 : 0, rawcov6, \
+                                              nbr_idx, nbr_d2, nbr_cnt, mean_dist)
     if (k <= 8)
         ORPCD_KNN_TILES(8);
     else if (k <= 20)

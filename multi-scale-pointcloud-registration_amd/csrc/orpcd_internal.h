@@ -25,6 +25,10 @@ constexpr int kPartialStride = 32;             // doubles per block partial
 constexpr float kFarCoord = 1.0e18f;           // padding coordinate
 constexpr int kCounterSlots = 256;             // profiling counters: {tiles, max tiles/wave} per slot
 constexpr int kCounterStride = 16;             // u64 per slot (128 B: one cache line each)
+// Largest cloud the ABI accepts: the raw buffer descriptors of the search
+// (num_records = n * sizeof(float4), 32-bit) and its 32-bit byte offsets
+// must not wrap.
+constexpr int64_t kMaxPoints = (int64_t)1 << 27;
 
 // Device buffer that only grows (no hipMalloc inside steady-state loops).
 template <typename T>
@@ -68,11 +72,17 @@ struct HostBuf {  // pinned
 };
 
 // A cloud in device memory, in Morton order (sort_kernels.hip).
+// Every fp32 copy (p4, tile / quarter / super-tile boxes) is relative to
+// `org`, the cloud's bounding-box centre, subtracted in fp64 before the cast:
+// fp32 resolution then follows the cloud's extent, not its distance from the
+// coordinate origin.  Every fp32 query is formed the same way (q - org in
+// fp64, then one rounding); xyz64 stays absolute.
 struct CloudLayout {
     int64_t n = 0, npad = 0, ntiles = 0, nsuper = 0;
-    DevBuf<double> xyz64;     // n*3, Morton order
+    double org[3] = {0.0, 0.0, 0.0};  // fp32 frame origin (bbox centre)
+    DevBuf<double> xyz64;     // n*3, Morton order (absolute)
     DevBuf<int32_t> perm;     // Morton position -> input index
-    DevBuf<float4> p4;        // npad fp32 (x,y,z, input index bits), padded far
+    DevBuf<float4> p4;        // npad fp32 (x,y,z relative to org, input index bits), padded far
     DevBuf<float4> tlo, thi;  // per 64-point tile AABB
     DevBuf<float4> qbox;      // per tile: its four 16-point quarters' AABBs (lo x4, hi x4)
     DevBuf<float4> slo, shi;  // per super-tile (64 tiles) AABB
@@ -268,8 +278,9 @@ namespace orpcd {
 // sort_kernels.hip
 hipError_t launch_gather_rows(const double* in, const int32_t* idx, int64_t offset, int64_t n, int w, double* out,
                               hipStream_t s);
-hipError_t build_layout(const double* dev_in64, int64_t n, const double bbox_lo[3], double bbox_ext, CloudLayout& L,
-                        bool with_tiles, hipStream_t s);
+// origin: the fp32 frame origin stored in L.org (the bbox centre)
+hipError_t build_layout(const double* dev_in64, int64_t n, const double bbox_lo[3], double bbox_ext,
+                        const double origin[3], CloudLayout& L, bool with_tiles, hipStream_t s);
 
 // knn_kernels.hip
 hipError_t launch_knn_tiles(const CloudLayout& L, const double* in64, int k, double radius, double margin,

@@ -2,6 +2,7 @@
 // and the batched GICP driver.  Host orchestration only; all arithmetic on
 // the hot path runs in the kernels of knn_kernels.hip / gicp_kernels.hip.
 #include <algorithm>
+#include <chrono>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -41,8 +42,7 @@ bool finite_cloud(const double* xyz, int64_t n) {
     return true;
 }
 
-void host_bbox(const double* xyz, int64_t n, double lo[3], double* ext) {
-    double hi[3];
+void host_bbox(const double* xyz, int64_t n, double lo[3], double hi[3], double* ext) {
     for (int a = 0; a < 3; ++a) {
         lo[a] = xyz[a];
         hi[a] = xyz[a];
@@ -56,20 +56,23 @@ void host_bbox(const double* xyz, int64_t n, double lo[3], double* ext) {
 }
 
 // Absolute bound (with 4x safety) on the fp32 rounding of any coordinate of
-// the cloud: the culled KNN widens its fp32 box tests by it.
-double coord_margin(const double lo[3], double ext) {
+// the cloud in its fp32 frame (relative to `org`): the culled KNN widens its
+// fp32 box tests by it.
+double coord_margin(const double lo[3], const double hi[3], const double org[3]) {
     double m = 0.0;
-    for (int a = 0; a < 3; ++a) m = std::max(m, std::max(std::fabs(lo[a]), std::fabs(lo[a] + ext)));
+    for (int a = 0; a < 3; ++a) m = std::max(m, std::max(std::fabs(lo[a] - org[a]), std::fabs(hi[a] - org[a])));
     return m * 0x1p-21;
 }
 
-// Lay out a device-resident (input-order) cloud in Morton order with tiles.
+// Lay out a device-resident (input-order) cloud in Morton order with tiles;
+// its fp32 frame is centred on the bounding box (CloudLayout::org).
 int layout_from_device(orpcd_ctx* c, const double* host_xyz, const double* dev_xyz, int64_t n, CloudLayout& L,
                        bool tiles, double* margin = nullptr) {
-    double lo[3], ext;
-    host_bbox(host_xyz, n, lo, &ext);
-    if (margin) *margin = coord_margin(lo, ext);
-    CTX_CHECK(c, build_layout(dev_xyz, n, lo, ext, L, tiles, c->stream));
+    double lo[3], hi[3], org[3], ext;
+    host_bbox(host_xyz, n, lo, hi, &ext);
+    for (int a = 0; a < 3; ++a) org[a] = 0.5 * (lo[a] + hi[a]);
+    if (margin) *margin = coord_margin(lo, hi, org);
+    CTX_CHECK(c, build_layout(dev_xyz, n, lo, ext, org, L, tiles, c->stream));
     return ORPCD_OK;
 }
 
@@ -358,9 +361,10 @@ int batch_setup(orpcd_ctx* c, const double* R0, const double* t0, int B, const o
     CTX_CHECK(c, c->R.ensure((size_t)B * 9));
     CTX_CHECK(c, c->prev.ensure((size_t)B * 2));
     CTX_CHECK(c, c->partial.ensure((size_t)B * nblk * kPartialStride));
-    // two-phase search: worst case every tile a candidate of every group (else the split search)
+    // two-phase search (only when selected): worst case every tile a candidate
+    // of every group; a batch whose list would not fit runs the split search
     const size_t worst_items = (size_t)B * ((N + 127) / 128) * (size_t)c->tgt.ntiles;
-    c->two_phase_ok = worst_items <= ((size_t)1 << 29);  // <= 2 GiB of items
+    c->two_phase_ok = c->opt.search_kernel == 2 && worst_items <= ((size_t)1 << 29);  // <= 2 GiB of items
     if (c->two_phase_ok) CTX_CHECK(c, c->items.ensure(worst_items));
     CTX_CHECK(c, c->item_counts.ensure((size_t)2 * B * ((N + 127) / 128) + 2));
     CTX_CHECK(c, c->done.ensure((size_t)B));
@@ -518,7 +522,7 @@ const char* orpcd_last_error(const orpcd_ctx* c) { return c ? c->err.c_str() : "
 int orpcd_set_target(orpcd_ctx* c, const double* xyz, int64_t m, double epsilon) {
     if (!c) return ORPCD_EINVAL;
     CTX_REQUIRE(c, xyz && m > 0, "set_target: empty target cloud");
-    CTX_REQUIRE(c, m < (int64_t)1 << 30, "set_target: too many points");
+    CTX_REQUIRE(c, m < kMaxPoints, "set_target: too many points");
     CTX_REQUIRE(c, finite_cloud(xyz, m), "set_target: non-finite coordinates");
     CTX_CHECK(c, hipSetDevice(c->device));
     int rc = upload_target(c, xyz, m, epsilon);
@@ -530,7 +534,7 @@ int orpcd_set_target(orpcd_ctx* c, const double* xyz, int64_t m, double epsilon)
 int orpcd_set_source(orpcd_ctx* c, const double* xyz, int64_t n) {
     if (!c) return ORPCD_EINVAL;
     CTX_REQUIRE(c, xyz && n > 0, "set_source: empty source cloud");
-    CTX_REQUIRE(c, n < (int64_t)1 << 30, "set_source: too many points");
+    CTX_REQUIRE(c, n < kMaxPoints, "set_source: too many points");
     CTX_REQUIRE(c, finite_cloud(xyz, n), "set_source: non-finite coordinates");
     CTX_CHECK(c, hipSetDevice(c->device));
     c->src_cov = false;
@@ -570,7 +574,7 @@ int orpcd_gicp_batch(orpcd_ctx* c, const double* R0, const double* t0, int32_t B
 int orpcd_set_source_points(orpcd_ctx* c, const double* xyz, int64_t n) {
     if (!c) return ORPCD_EINVAL;
     CTX_REQUIRE(c, xyz && n > 0, "set_source_points: empty source cloud");
-    CTX_REQUIRE(c, n < (int64_t)1 << 30, "set_source_points: too many points");
+    CTX_REQUIRE(c, n < kMaxPoints, "set_source_points: too many points");
     CTX_REQUIRE(c, finite_cloud(xyz, n), "set_source_points: non-finite coordinates");
     CTX_CHECK(c, hipSetDevice(c->device));
     c->src_cov = false;
@@ -672,17 +676,52 @@ int run_passes_pipelined(orpcd_ctx* c, int B, const orpcd_gicp_params* p, double
     volatile unsigned long long* prog = c->prog_h;
     *prog = 0;  // no pipelined kernel of this batch has run yet (the stream is idle after batch_setup's copies)
     int nact_host = B, launched = 0;
+    // Wait on the progress word until `ready(v)`.  Bounded: the stream is
+    // polled for an asynchronous fault (or for having drained without
+    // publishing what is awaited), and the wait gives up after 120 s.
+    auto wait_progress = [&](auto ready, unsigned long long& v) -> int {
+        const auto t0 = std::chrono::steady_clock::now();
+        for (unsigned spin = 0;; ++spin) {
+            v = *prog;
+            if (ready(v)) return ORPCD_OK;
+            if ((spin & 1023u) == 1023u) {
+                const hipError_t q = hipStreamQuery(s);
+                if (q != hipSuccess && q != hipErrorNotReady) {
+                    c->err = std::string("pipelined passes: device error: ") + hipGetErrorString(q);
+                    return ORPCD_EDEVICE;
+                }
+                if (q == hipSuccess) {  // drained: the word is final
+                    v = *prog;
+                    if (ready(v)) return ORPCD_OK;
+                    c->err = "pipelined passes: the stream drained without publishing the awaited pass";
+                    return ORPCD_EDEVICE;
+                }
+                if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(120)) {
+                    c->err = "pipelined passes: timed out waiting for the device";
+                    return ORPCD_EDEVICE;
+                }
+            }
+            std::this_thread::yield();
+        }
+    };
     for (int pass = 0; pass < npass; ++pass) {
         unsigned long long v = *prog;
         int pdone = (int)(v >> 32), nrun = (int)(v & 0xffffffffu);
-        while (pdone > 0 && nrun > 0 && pass - pdone >= c->opt.lookahead) {  // far enough ahead: wait
-            std::this_thread::yield();
-            v = *prog;
+        if (pdone > 0 && nrun > 0 && pass - pdone >= c->opt.lookahead) {  // far enough ahead: wait
+            const int la = c->opt.lookahead;
+            const int rc = wait_progress(
+                [pass, la](unsigned long long w) {
+                    const int pd = (int)(w >> 32), nr = (int)(w & 0xffffffffu);
+                    return !(pd > 0 && nr > 0 && pass - pd >= la);
+                },
+                v);
+            if (rc) return rc;
             pdone = (int)(v >> 32);
             nrun = (int)(v & 0xffffffffu);
         }
         if (pdone == 0 && pass >= c->opt.lookahead) {  // nothing complete yet: bound the queue anyway
-            while ((v = *prog) >> 32 == 0) std::this_thread::yield();
+            const int rc = wait_progress([](unsigned long long w) { return (w >> 32) != 0; }, v);
+            if (rc) return rc;
             pdone = (int)(v >> 32);
             nrun = (int)(v & 0xffffffffu);
         }
@@ -818,7 +857,7 @@ int orpcd_sor(orpcd_ctx* c, const double* xyz, int64_t n, int32_t nb_neighbors, 
                 "Illegal input parameters, the number of neighbors and standard deviation ratio must be positive.");
     CTX_REQUIRE(c, nb_neighbors <= 64, "sor: nb_neighbors > 64 is not supported by the device KNN");
     if (n == 0) return ORPCD_OK;
-    CTX_REQUIRE(c, xyz && n > 0 && n < (int64_t)1 << 30, "sor: bad cloud size");
+    CTX_REQUIRE(c, xyz && n > 0 && n < kMaxPoints, "sor: bad cloud size");
     CTX_REQUIRE(c, finite_cloud(xyz, n), "sor: non-finite coordinates");
     CTX_CHECK(c, hipSetDevice(c->device));
     hipStream_t s = c->stream;
@@ -853,7 +892,7 @@ int orpcd_voxel_down_sample(orpcd_ctx* c, const double* xyz, int64_t n, double v
     *n_out = 0;
     CTX_REQUIRE(c, voxel_size > 0.0, "voxel_size <= 0.");
     if (n == 0) return ORPCD_OK;
-    CTX_REQUIRE(c, xyz && n > 0 && n < (int64_t)1 << 30, "voxel_down_sample: bad cloud size");
+    CTX_REQUIRE(c, xyz && n > 0 && n < kMaxPoints, "voxel_down_sample: bad cloud size");
     CTX_REQUIRE(c, finite_cloud(xyz, n), "voxel_down_sample: non-finite coordinates");
     double lo[3], hi[3], vmin[3];
     for (int a = 0; a < 3; ++a) lo[a] = hi[a] = xyz[a];
@@ -889,7 +928,7 @@ int orpcd_farthest_downsample(orpcd_ctx* c, const double* xyz, int64_t n, int32_
                               int64_t* idx_out) {
     if (!c) return ORPCD_EINVAL;
     CTX_REQUIRE(c, xyz && idx_out, "farthest_downsample: null argument");
-    CTX_REQUIRE(c, n > 0 && n < (int64_t)1 << 30, "farthest_downsample: empty cloud");
+    CTX_REQUIRE(c, n > 0 && n < kMaxPoints, "farthest_downsample: empty cloud");
     CTX_REQUIRE(c, sample_size > 0, "farthest_downsample: sample_size must be > 0");
     CTX_REQUIRE(c, first >= 0 && first < n, "farthest_downsample: first index out of range");
     CTX_REQUIRE(c, finite_cloud(xyz, n), "farthest_downsample: non-finite coordinates");
@@ -921,7 +960,7 @@ int orpcd_farthest_downsample(orpcd_ctx* c, const double* xyz, int64_t n, int32_
 int orpcd_set_source_rows(orpcd_ctx* c, const double* xyz, int64_t n, int64_t row_begin, int64_t row_end) {
     if (!c) return ORPCD_EINVAL;
     CTX_REQUIRE(c, xyz && n > 0, "set_source_rows: empty source cloud");
-    CTX_REQUIRE(c, n < (int64_t)1 << 30, "set_source_rows: too many points");
+    CTX_REQUIRE(c, n < kMaxPoints, "set_source_rows: too many points");
     CTX_REQUIRE(c, row_begin >= 0 && row_begin < row_end && row_end <= n, "set_source_rows: bad row range");
     CTX_REQUIRE(c, finite_cloud(xyz, n), "set_source_rows: non-finite coordinates");
     CTX_CHECK(c, hipSetDevice(c->device));
@@ -1054,6 +1093,7 @@ int orpcd_nn1_radius(orpcd_ctx* c, const double* q, int64_t nq, const double* t,
     if (!c) return ORPCD_EINVAL;
     CTX_REQUIRE(c, q && t && idx_out && d2_out && nq >= 0 && m > 0, "nn1_radius: bad arguments");
     CTX_REQUIRE(c, radius > 0, "nn1_radius: radius must be > 0");
+    CTX_REQUIRE(c, nq < kMaxPoints && m < kMaxPoints, "nn1_radius: too many points");
     CTX_REQUIRE(c, finite_cloud(t, m) && finite_cloud(q, nq), "nn1_radius: non-finite coordinates");
     if (nq == 0) return ORPCD_OK;
     CTX_CHECK(c, hipSetDevice(c->device));
@@ -1074,6 +1114,7 @@ int orpcd_estimate_normals(orpcd_ctx* c, const double* xyz, int64_t n, int32_t k
                            double* normals_out, double* rawcov_out, double* gicpcov_out) {
     if (!c) return ORPCD_EINVAL;
     CTX_REQUIRE(c, xyz && n > 0, "estimate_normals: empty cloud");
+    CTX_REQUIRE(c, n < kMaxPoints, "estimate_normals: too many points");
     CTX_REQUIRE(c, knn > 0 && knn <= 64, "estimate_normals: knn must be in [1, 64]");
     CTX_REQUIRE(c, finite_cloud(xyz, n), "estimate_normals: non-finite coordinates");
     CTX_CHECK(c, hipSetDevice(c->device));
@@ -1119,7 +1160,7 @@ int orpcd_estimate_normals(orpcd_ctx* c, const double* xyz, int64_t n, int32_t k
 int orpcd_fpfh(orpcd_ctx* c, const double* xyz, int64_t n, double normal_radius, int32_t normal_knn,
                double fpfh_radius, int32_t fpfh_knn, double* normals_out, double* feat_out) {
     if (!c) return ORPCD_EINVAL;
-    CTX_REQUIRE(c, xyz && n > 0 && feat_out, "fpfh: bad arguments");
+    CTX_REQUIRE(c, xyz && n > 0 && feat_out && n < kMaxPoints, "fpfh: bad arguments");
     CTX_REQUIRE(c, finite_cloud(xyz, n), "fpfh: non-finite coordinates");
     CTX_CHECK(c, hipSetDevice(c->device));
     CTX_CHECK(c, c->fgr.xyz[0].ensure((size_t)n * 3));
@@ -1137,7 +1178,7 @@ int orpcd_fpfh(orpcd_ctx* c, const double* xyz, int64_t n, double normal_radius,
 int orpcd_fpfh_from_normals(orpcd_ctx* c, const double* xyz, const double* normals, int64_t n,
                             double fpfh_radius, int32_t fpfh_knn, double* feat_out) {
     if (!c) return ORPCD_EINVAL;
-    CTX_REQUIRE(c, xyz && normals && n > 0 && feat_out, "fpfh_from_normals: bad arguments");
+    CTX_REQUIRE(c, xyz && normals && n > 0 && feat_out && n < kMaxPoints, "fpfh_from_normals: bad arguments");
     CTX_REQUIRE(c, fpfh_knn > 0 && fpfh_knn <= 64, "fpfh: knn must be in [1, 64]");
     CTX_REQUIRE(c, fpfh_radius > 0, "fpfh: radii must be > 0");
     CTX_REQUIRE(c, finite_cloud(xyz, n) && finite_cloud(normals, n), "fpfh_from_normals: non-finite values");
@@ -1159,7 +1200,9 @@ int orpcd_fgr(orpcd_ctx* c, const double* src, int64_t n, const double* tgt, int
               const double* tgt_feat, const orpcd_fgr_params* p, double* T_out, double* fitness_out,
               double* rmse_out, int64_t* ncorr_out, int64_t* n_mutual_out) {
     if (!c) return ORPCD_EINVAL;
-    CTX_REQUIRE(c, src && tgt && src_feat && tgt_feat && p && T_out && n > 0 && m > 0, "fgr: bad arguments");
+    CTX_REQUIRE(c, src && tgt && src_feat && tgt_feat && p && T_out && n > 0 && m > 0 && n < kMaxPoints &&
+                       m < kMaxPoints,
+                "fgr: bad arguments");
     int rc = check_fgr_params(c, p);
     if (rc) return rc;
     CTX_REQUIRE(c, finite_cloud(src, n) && finite_cloud(tgt, m), "fgr: non-finite coordinates");
@@ -1215,7 +1258,8 @@ int orpcd_fgr_optimize(orpcd_ctx* c, const double* src, int64_t n, const double*
                        int32_t target_features_from_source, const orpcd_fgr_params* p, double* T_out,
                        double* fitness_out, double* rmse_out, int64_t* ncorr_out, int64_t* n_mutual_out) {
     if (!c) return ORPCD_EINVAL;
-    CTX_REQUIRE(c, src && tgt && p && T_out && n > 0 && m > 0, "fgr_optimize: bad arguments");
+    CTX_REQUIRE(c, src && tgt && p && T_out && n > 0 && m > 0 && n < kMaxPoints && m < kMaxPoints,
+                "fgr_optimize: bad arguments");
     int rc = check_fgr_params(c, p);
     if (rc) return rc;
     CTX_REQUIRE(c, !target_features_from_source || m <= n,

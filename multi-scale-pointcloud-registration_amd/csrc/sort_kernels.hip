@@ -36,9 +36,11 @@ __global__ void morton_kernel(const double* __restrict__ xyz, int n, double lox,
     idx[i] = i;
 }
 
-// out64[k] = in64[perm[k]], out4[k] = (float xyz, orig index bits); padding far.
+// out64[k] = in64[perm[k]], out4[k] = (float (xyz - origin), orig index bits);
+// padding far.
 __global__ void gather_points_kernel(const double* __restrict__ in64, const int32_t* __restrict__ perm, int n,
-                                     int npad, double* __restrict__ out64, float4* __restrict__ out4) {
+                                     int npad, double ox, double oy, double oz, double* __restrict__ out64,
+                                     float4* __restrict__ out4) {
     const int k = blockIdx.x * blockDim.x + threadIdx.x;
     if (k >= npad) return;
     if (k < n) {
@@ -47,7 +49,7 @@ __global__ void gather_points_kernel(const double* __restrict__ in64, const int3
         out64[3 * k] = x;
         out64[3 * k + 1] = y;
         out64[3 * k + 2] = z;
-        if (out4) out4[k] = make_float4((float)x, (float)y, (float)z, __int_as_float(j));
+        if (out4) out4[k] = make_float4((float)(x - ox), (float)(y - oy), (float)(z - oz), __int_as_float(j));
     } else if (out4) {
         out4[k] = make_float4(kFarCoord, kFarCoord, kFarCoord, __int_as_float(-1));
     }
@@ -123,8 +125,9 @@ hipError_t launch_gather_rows(const double* in, const int32_t* idx, int64_t offs
 }
 
 hipError_t build_layout(const double* dev_in64, int64_t n, const double bbox_lo[3], double bbox_ext,
-                        CloudLayout& L, bool with_tiles, hipStream_t s) {
+                        const double origin[3], CloudLayout& L, bool with_tiles, hipStream_t s) {
     L.n = n;
+    for (int a = 0; a < 3; ++a) L.org[a] = origin[a];
     L.npad = std::max<int64_t>(kTile, ((n + kTile - 1) / kTile) * kTile);
     L.ntiles = (n + kTile - 1) / kTile;
     hipError_t e;
@@ -154,8 +157,8 @@ hipError_t build_layout(const double* dev_in64, int64_t n, const double bbox_lo[
                                            30, s);
     if (e != hipSuccess) return e;
     const unsigned gp = (unsigned)((L.npad + 255) / 256);
-    gather_points_kernel<<<gp, 256, 0, s>>>(dev_in64, L.perm.p, (int)n, (int)L.npad, L.xyz64.p,
-                                            with_tiles ? L.p4.p : nullptr);
+    gather_points_kernel<<<gp, 256, 0, s>>>(dev_in64, L.perm.p, (int)n, (int)L.npad, origin[0], origin[1],
+                                            origin[2], L.xyz64.p, with_tiles ? L.p4.p : nullptr);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     if (with_tiles) {
         tile_aabb_kernel<<<(unsigned)((L.ntiles + 255) / 256), 256, 0, s>>>(L.p4.p, (int)n, (int)L.ntiles, L.tlo.p,

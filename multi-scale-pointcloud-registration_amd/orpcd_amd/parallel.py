@@ -108,6 +108,11 @@ def gicp_rows_sharded(ctx, source: np.ndarray, target: np.ndarray, R0=None, t0=N
     Returns the Open3D-convention result (T column convention)."""
     rank, ws = world()
     n = len(source)
+    if n < ws:
+        # every rank sees the same n and ws, so every rank raises here, before
+        # any collective (a rank with an empty shard would otherwise leave the
+        # others blocked in the per-pass all_reduce)
+        raise ValueError(f"gicp_rows_sharded: {n} source rows cannot be split over {ws} ranks")
     lo, hi = shard(n, rank, ws)
     R0 = np.eye(3) if R0 is None else R0
     t0 = np.zeros(3) if t0 is None else t0

@@ -80,6 +80,37 @@ def _rows_worker(rank, world, port, out_dir):
     dist.destroy_process_group()
 
 
+def _rows_too_few_worker(rank, world, port, out_dir):
+    sys.path[:0] = [PKG, os.path.join(REPO, "tests"), os.path.join(REPO, "oracle"), REPO]
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch.distributed as dist
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from orpcd_amd import parallel
+    from shard_fake import FakeShardContext
+    from workloads import small_pair
+    src, tgt = small_pair(300, 300, seed=4)
+    try:
+        parallel.gicp_rows_sharded(FakeShardContext(), src[: world - 1], tgt)
+        outcome = "returned"
+    except ValueError:
+        outcome = "ValueError"
+    dist.barrier()  # every rank got here: nobody is stuck in a collective
+    with open(os.path.join(out_dir, f"few{rank}.txt"), "w") as f:
+        f.write(outcome)
+    dist.destroy_process_group()
+
+
+def test_row_sharded_fewer_rows_than_ranks_raises_everywhere(tmp_path):
+    """n < world_size: every rank raises ValueError before any collective
+    (no rank is left waiting in the per-pass all_reduce)."""
+    import torch.multiprocessing as mp
+    world = 3
+    mp.start_processes(_rows_too_few_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True,
+                       start_method="spawn")
+    for r in range(world):
+        assert (tmp_path / f"few{r}.txt").read_text() == "ValueError"
+
+
 @pytest.mark.parametrize("world", [2, 3])
 def test_row_sharded_gicp_matches_single_process_oracle(tmp_path, world, oracle):
     """C5's multi-GPU path: source rows split over ranks, one all-reduce of

@@ -129,6 +129,49 @@ def test_gicp_plugin_drop_in(oracle):
         GeneralizedICP().optimize(src, tgt + 50.0)  # no correspondences within 0.5
 
 
+@pytest.mark.parametrize("offset", [1e4, -3e5, 2e6])
+def test_far_from_origin_nn_matches_oracle(ctx, oracle, offset):
+    """Clouds far from the coordinate origin (raw metre / UTM-like data, as a
+    GeneralizedICP used without the Aligner's RadiusScaler would see): the
+    fp32 search works relative to the target's bounding-box centre, so the
+    nearest targets match the fp64 oracle as they do near the origin.
+    (Without the shift the fp32 ulp at 1e4 is ~1e-3, the pair's
+    nearest-neighbour spacing; at 2e6 it is 0.25.)"""
+    src, tgt = small_pair(2000, 2200, seed=12)
+    shift = np.array([offset, -0.5 * offset, 0.25 * offset])
+    s, t = src + shift, tgt + shift
+    gi, gd = ctx.nn1_radius(s, t, 0.5)
+    oi, od = oracle.nn1_radius(s, t, 0.5)
+    assert _certified_nn(oi, gi, s, t) <= 2
+    same = oi == gi
+    # d^2 of the same pair: both fp64, from coordinates of magnitude |shift|
+    assert np.allclose(gd[same], od[same], rtol=0, atol=1e-16 * np.abs(shift).max() ** 2 + 1e-15)
+
+
+@pytest.mark.parametrize("offset", [1e4, -1.5e4])
+def test_far_from_origin_gicp_matches_oracle(ctx, oracle, offset):
+    """GICP on the same far-off pair.  Open3D's update rotates about the
+    coordinate origin, so its 6x6 normal equations carry |q|^2 ~ offset^2 in
+    the rotation block and their condition grows with offset^2: beyond ~1e5
+    the fp64 solve itself (oracle included) is no longer meaningful, hence the
+    GICP offsets stay at 1e4 scale (the search is checked further out above)."""
+    src, tgt = small_pair(2000, 2200, seed=12)
+    shift = np.array([offset, -0.5 * offset, 0.25 * offset])
+    s, t = src + shift, tgt + shift
+    o = oracle.gicp(s, t, 0.5, 100)
+    ctx.set_target(t)
+    ctx.set_source(s)
+    r = ctx.gicp_batch(np.eye(3)[None], np.zeros((1, 3)))
+    g = dict(T=r["T"][0], rmse=r["rmse"][0], fitness=r["fitness"][0], iters=r["iters"][0])
+    # rotation about the far origin couples into translation by |offset|:
+    # compare the rotation at 1e-6 and the translation at 1e-6 * |shift|
+    assert np.abs(g["T"][:3, :3] - o["T"][:3, :3]).max() <= T_TOL
+    assert np.abs(g["T"][:3, 3] - o["T"][:3, 3]).max() <= T_TOL * max(1.0, np.abs(shift).max())
+    assert abs(g["rmse"] - o["rmse"]) <= RMSE_TOL
+    assert abs(g["fitness"] - o["fitness"]) <= 1e-4
+    assert abs(g["iters"] - o["iters"]) <= 1
+
+
 def test_gicp_max_iteration_and_tiny_clouds(ctx, oracle):
     src, tgt = small_pair(400, seed=5)
     for it in (1, 3):
