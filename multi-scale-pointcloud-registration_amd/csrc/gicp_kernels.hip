@@ -83,6 +83,39 @@ constexpr int kNoMatch = -2;  // no target within the search radius last pass
 constexpr unsigned kKeyMask = 0xFFFFFFC0u;  // d^2 bits kept in a scan key (low 6 = tile-local index)
 constexpr float kQuarterSlack = 1.0f - 1.0f / 1048576.0f;  // quarter test: box d^2 x (1 - 2^-20) vs the bound
 
+// Accesses of state that another workgroup publishes inside the SAME launch
+// (the persistent pass loop): relaxed agent-scope atomics (global sc1
+// loads / stores), ordered by the release / acquire hand-offs around them.
+// kAt = false: plain accesses (the data was written before a kernel boundary).
+template <bool kAt>
+__device__ __forceinline__ unsigned long long ld_u64(const unsigned long long* p) {
+    if constexpr (kAt) return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    else return *p;
+}
+template <bool kAt>
+__device__ __forceinline__ void st_u64(unsigned long long* p, unsigned long long v) {
+    if constexpr (kAt) __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    else *p = v;
+}
+template <bool kAt>
+__device__ __forceinline__ double ld_f64(const double* p) {
+    return __longlong_as_double((long long)ld_u64<kAt>(reinterpret_cast<const unsigned long long*>(p)));
+}
+template <bool kAt>
+__device__ __forceinline__ void st_f64(double* p, double v) {
+    st_u64<kAt>(reinterpret_cast<unsigned long long*>(p), (unsigned long long)__double_as_longlong(v));
+}
+template <bool kAt>
+__device__ __forceinline__ int ld_i32(const int32_t* p) {
+    if constexpr (kAt) return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    else return *p;
+}
+template <bool kAt>
+__device__ __forceinline__ void st_i32(int32_t* p, int v) {
+    if constexpr (kAt) __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    else *p = v;
+}
+
 // --------------------------------------------------------------------------
 // Culled exact nearest search for the 2 queries of every lane of one wave,
 // restricted to tiles t with t % S == s.  s0lo/s0hi: super-tile `lane`'s box
@@ -1235,13 +1268,16 @@ struct SolveArgs {
 // pose update from its 29 reduced sums.  Lane 0 only.  done[] is stored sc1:
 // the pipelined pass compacts the running starts in the same launch.
 // --------------------------------------------------------------------------
-template <int kEst>  // 0: GeneralizedICP, 1: PointToPoint
-__device__ void solve_start(int slot, const double s[kNacc], int64_t N, int pass, int max_iter, double rel_fit,
+// kAt: the pose state (prev, T, Q, R) is read and written by a different
+// workgroup every pass of the same launch (persistent loop): atomic accesses.
+// Returns true when the start finished.
+template <int kEst, bool kAt = false>  // kEst 0: GeneralizedICP, 1: PointToPoint
+__device__ bool solve_start(int slot, const double s[kNacc], int64_t N, int pass, int max_iter, double rel_fit,
                             double rel_rmse, const SolveArgs& a) {
     const double cnt = s[28];
     const double fit = cnt > 0 ? cnt / (double)N : 0.0;
     const double rmse = cnt > 0 ? sqrt(s[27] / cnt) : 0.0;
-    const double pf = a.prev[2 * slot], pr = a.prev[2 * slot + 1];
+    const double pf = ld_f64<kAt>(a.prev + 2 * slot), pr = ld_f64<kAt>(a.prev + 2 * slot + 1);
     const bool converged = pass >= 1 && fabs(pf - fit) < rel_fit && fabs(pr - rmse) < rel_rmse;
     if (converged || pass >= max_iter) {
         a.out_fit[slot] = fit;
@@ -1249,10 +1285,10 @@ __device__ void solve_start(int slot, const double s[kNacc], int64_t N, int pass
         a.out_iters[slot] = pass;
         a.out_ncorr[slot] = (int64_t)cnt;
         __hip_atomic_store(a.done + slot, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        return;
+        return true;
     }
-    a.prev[2 * slot] = fit;
-    a.prev[2 * slot + 1] = rmse;
+    st_f64<kAt>(a.prev + 2 * slot, fit);
+    st_f64<kAt>(a.prev + 2 * slot + 1, rmse);
 
     double upd[16] = {1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1};
     if (cnt > 0 && kEst == 1) {
@@ -1270,19 +1306,20 @@ __device__ void solve_start(int slot, const double s[kNacc], int64_t N, int pass
         }
     }
     double Tcur[16], Tn[16];
-    for (int t = 0; t < 16; ++t) Tcur[t] = a.T[16 * slot + t];
+    for (int t = 0; t < 16; ++t) Tcur[t] = ld_f64<kAt>(a.T + 16 * slot + t);
     m4_mul(upd, Tcur, Tn);
-    for (int t = 0; t < 16; ++t) a.T[16 * slot + t] = Tn[t];
+    for (int t = 0; t < 16; ++t) st_f64<kAt>(a.T + 16 * slot + t, Tn[t]);
     // Q = Tn * [G; 0 0 0 1]  (3x4), R = Tn[:3,:3]
     const double* G = a.G + 12 * slot;
     for (int r = 0; r < 3; ++r) {
         for (int c = 0; c < 4; ++c) {
             double v = Tn[4 * r + 0] * G[c] + Tn[4 * r + 1] * G[4 + c] + Tn[4 * r + 2] * G[8 + c];
             if (c == 3) v += Tn[4 * r + 3];
-            a.Q[12 * slot + 4 * r + c] = v;
+            st_f64<kAt>(a.Q + 12 * slot + 4 * r + c, v);
         }
-        for (int c = 0; c < 3; ++c) a.R[9 * slot + 3 * r + c] = Tn[4 * r + c];
+        for (int c = 0; c < 3; ++c) st_f64<kAt>(a.R + 9 * slot + 3 * r + c, Tn[4 * r + c]);
     }
+    return false;
 }
 
 // --------------------------------------------------------------------------
@@ -1357,33 +1394,33 @@ __device__ __forceinline__ void finish_pass(int slot, int nact, const double* __
     }
 }
 
-template <bool kFused>
-__global__ __launch_bounds__(256) void gicp_accum_kernel(
-    const double* __restrict__ src, const double* __restrict__ scov, int N, const double* __restrict__ tgt64,
-    const double* __restrict__ tcov, const int32_t* __restrict__ active, const double* __restrict__ Qm,
-    const double* __restrict__ Rm, const int32_t* __restrict__ done, double r2,
-    const unsigned long long* __restrict__ best, int32_t* __restrict__ prevnn, double* __restrict__ partial,
-    int nblk, PassCtl pc) {
-    const int nact = kFused ? pc.ctl[0] : 0;
-    if (kFused && (int)blockIdx.y >= nact) return;
-    const int slot = active[blockIdx.y];
-    if (done[slot]) return;
-    __shared__ double red[4][kNacc];
-    double acc[kNacc];
+// The GICP normal-equation terms of accumulation block `ablk` of start
+// `slot` (queries (ablk * qpt + k) * 256 + threadIdx.x): this thread's sums,
+// in query order k.  Writes the next pass's seed (prevnn).  kPersist: the
+// correspondences and the pose were published inside the launch (atomic
+// accesses), and best[] is reset for the next pass's atomicMin merges.
+template <bool kPersist>
+__device__ __forceinline__ void gicp_block_terms(int slot, int ablk, const double* __restrict__ src,
+                                                 const double* __restrict__ scov, int N,
+                                                 const double* __restrict__ tgt64, const double* __restrict__ tcov,
+                                                 const double* __restrict__ Qm, const double* __restrict__ Rm,
+                                                 double r2, unsigned long long* __restrict__ best,
+                                                 int32_t* __restrict__ prevnn, double acc[kNacc]) {
 #pragma unroll
     for (int v = 0; v < kNacc; ++v) acc[v] = 0.0;
     double Q[12], R[9];
 #pragma unroll
-    for (int t = 0; t < 12; ++t) Q[t] = Qm[12 * slot + t];
+    for (int t = 0; t < 12; ++t) Q[t] = ld_f64<kPersist>(Qm + 12 * slot + t);
 #pragma unroll
-    for (int t = 0; t < 9; ++t) R[t] = Rm[9 * slot + t];
+    for (int t = 0; t < 9; ++t) R[t] = ld_f64<kPersist>(Rm + 9 * slot + t);
     const int qpt = accum_qpt(N);
     for (int k = 0; k < qpt; ++k) {
-        const int i = (blockIdx.x * qpt + k) * 256 + threadIdx.x;
+        const int i = (ablk * qpt + k) * 256 + threadIdx.x;
         if (i >= N) break;
-        const unsigned long long v = best[(size_t)slot * N + i];
+        const unsigned long long v = ld_u64<kPersist>(best + (size_t)slot * N + i);
         const int j = v == kNone ? -1 : (int)(unsigned)(v & 0xffffffffu);
-        prevnn[(size_t)slot * N + i] = j >= 0 ? j : kNoMatch;
+        st_i32<kPersist>(prevnn + (size_t)slot * N + i, j >= 0 ? j : kNoMatch);
+        if constexpr (kPersist) st_u64<true>(best + (size_t)slot * N + i, kNone);
         if (j < 0) continue;
         const double p[3] = {src[3 * i], src[3 * i + 1], src[3 * i + 2]};
         double q[3];
@@ -1437,6 +1474,22 @@ __global__ __launch_bounds__(256) void gicp_accum_kernel(
         acc[27] += d2;
         acc[28] += 1.0;
     }
+}
+
+template <bool kFused>
+__global__ __launch_bounds__(256) void gicp_accum_kernel(
+    const double* __restrict__ src, const double* __restrict__ scov, int N, const double* __restrict__ tgt64,
+    const double* __restrict__ tcov, const int32_t* __restrict__ active, const double* __restrict__ Qm,
+    const double* __restrict__ Rm, const int32_t* __restrict__ done, double r2,
+    unsigned long long* __restrict__ best, int32_t* __restrict__ prevnn, double* __restrict__ partial,
+    int nblk, PassCtl pc) {
+    const int nact = kFused ? pc.ctl[0] : 0;
+    if (kFused && (int)blockIdx.y >= nact) return;
+    const int slot = active[blockIdx.y];
+    if (done[slot]) return;
+    __shared__ double red[4][kNacc];
+    double acc[kNacc];
+    gicp_block_terms<false>(slot, blockIdx.x, src, scov, N, tgt64, tcov, Qm, Rm, r2, best, prevnn, acc);
     block_partial<kNacc, kFused>(acc, red, [](int v) { return v; },
                                  partial + ((size_t)slot * nblk + blockIdx.x) * kPartialStride);
     if constexpr (kFused) finish_pass<kEstGICP>(slot, nact, partial, nblk, pc);
@@ -1449,33 +1502,24 @@ __global__ __launch_bounds__(256) void gicp_accum_kernel(
 constexpr int kP2PTerms = 17;
 __device__ __forceinline__ int p2p_slot(int v) { return v < 15 ? v : 12 + v; }  // 15 -> 27, 16 -> 28
 
-template <bool kFused>
-__global__ __launch_bounds__(256) void p2p_accum_kernel(const double* __restrict__ src, int N,
-                                                        const double* __restrict__ tgt64,
-                                                        const int32_t* __restrict__ active,
-                                                        const double* __restrict__ Qm,
-                                                        const int32_t* __restrict__ done, double r2,
-                                                        const unsigned long long* __restrict__ best,
-                                                        int32_t* __restrict__ prevnn, double* __restrict__ partial,
-                                                        int nblk, PassCtl pc) {
-    const int nact = kFused ? pc.ctl[0] : 0;
-    if (kFused && (int)blockIdx.y >= nact) return;
-    const int slot = active[blockIdx.y];
-    if (done[slot]) return;
-    __shared__ double red[4][kP2PTerms];
-    double acc[kP2PTerms];
+template <bool kPersist>
+__device__ __forceinline__ void p2p_block_terms(int slot, int ablk, const double* __restrict__ src, int N,
+                                                const double* __restrict__ tgt64, const double* __restrict__ Qm,
+                                                double r2, unsigned long long* __restrict__ best,
+                                                int32_t* __restrict__ prevnn, double acc[kP2PTerms]) {
 #pragma unroll
     for (int v = 0; v < kP2PTerms; ++v) acc[v] = 0.0;
     double Q[12];
 #pragma unroll
-    for (int t = 0; t < 12; ++t) Q[t] = Qm[12 * slot + t];
+    for (int t = 0; t < 12; ++t) Q[t] = ld_f64<kPersist>(Qm + 12 * slot + t);
     const int qpt = accum_qpt(N);
     for (int k = 0; k < qpt; ++k) {
-        const int i = (blockIdx.x * qpt + k) * 256 + threadIdx.x;
+        const int i = (ablk * qpt + k) * 256 + threadIdx.x;
         if (i >= N) break;
-        const unsigned long long v = best[(size_t)slot * N + i];
+        const unsigned long long v = ld_u64<kPersist>(best + (size_t)slot * N + i);
         const int j = v == kNone ? -1 : (int)(unsigned)(v & 0xffffffffu);
-        prevnn[(size_t)slot * N + i] = j >= 0 ? j : kNoMatch;
+        st_i32<kPersist>(prevnn + (size_t)slot * N + i, j >= 0 ? j : kNoMatch);
+        if constexpr (kPersist) st_u64<true>(best + (size_t)slot * N + i, kNone);
         if (j < 0) continue;
         const double p[3] = {src[3 * i], src[3 * i + 1], src[3 * i + 2]};
         double q[3];
@@ -1494,6 +1538,24 @@ __global__ __launch_bounds__(256) void p2p_accum_kernel(const double* __restrict
         acc[15] += d2;
         acc[16] += 1.0;
     }
+}
+
+template <bool kFused>
+__global__ __launch_bounds__(256) void p2p_accum_kernel(const double* __restrict__ src, int N,
+                                                        const double* __restrict__ tgt64,
+                                                        const int32_t* __restrict__ active,
+                                                        const double* __restrict__ Qm,
+                                                        const int32_t* __restrict__ done, double r2,
+                                                        unsigned long long* __restrict__ best,
+                                                        int32_t* __restrict__ prevnn, double* __restrict__ partial,
+                                                        int nblk, PassCtl pc) {
+    const int nact = kFused ? pc.ctl[0] : 0;
+    if (kFused && (int)blockIdx.y >= nact) return;
+    const int slot = active[blockIdx.y];
+    if (done[slot]) return;
+    __shared__ double red[4][kP2PTerms];
+    double acc[kP2PTerms];
+    p2p_block_terms<false>(slot, blockIdx.x, src, N, tgt64, Qm, r2, best, prevnn, acc);
     block_partial<kP2PTerms, kFused>(acc, red, p2p_slot,
                                      partial + ((size_t)slot * nblk + blockIdx.x) * kPartialStride);
     if constexpr (kFused) finish_pass<kEstP2P>(slot, nact, partial, nblk, pc);
@@ -1530,6 +1592,296 @@ __global__ __launch_bounds__(64) void icp_solve_kernel(const int32_t* __restrict
         reduce_partials(partial, slot, nblk, s);
     }
     if (threadIdx.x == 0) solve_start<kEst>(slot, s, N, pass, max_iter, rel_fit, rel_rmse, a);
+}
+
+// --------------------------------------------------------------------------
+// Persistent pass loop (default): the whole ICP loop of every start of the
+// batch in ONE launch, each start advancing at its own pace.
+//
+// Work of one pass of start b, as dataflow inside the launch:
+//  * search items (b, bx), bx < sblk * S: workgroup = the 512 queries of query
+//    block bx / S (wave w: 128 of them), tile split bx % S -- exactly the
+//    block / split of nn_search_kernel; each wave first forms its queries
+//    itself (fp64 pose -> fp32 in the target's frame, seed bound from the
+//    previous correspondence), exactly as xform_queries_kernel does;
+//  * the workgroup whose search item completes an accumulation block (the
+//    last of its 2 query blocks x S splits to arrive: ticket) accumulates that
+//    block exactly as gicp_accum_kernel / p2p_accum_kernel (same threads, same
+//    order), writes the next seeds and resets best[] for the next pass;
+//  * the workgroup completing the start's last accumulation block (ticket)
+//    reduces the partials and solves exactly as icp_solve_kernel, then
+//    publishes pass p + 1 of start b: sched[b] = (p + 1, S', item 0).
+// Idle workgroups poll sched[] (one 64-lane load per 64 starts) and take an
+// item with one atomic add.  A taken item never waits on anything, so there
+// is no deadlock whatever the residency; every workgroup leaves when all B
+// starts are finished (or, as a guard, after timeout_ticks of s_memrealtime).
+// Results are bit-identical to the launch-per-kernel loop: same queries,
+// same search (splits never change answers), same sums in the same order.
+// Hand-offs (MI355X_MICROARCH.md, inter-workgroup visibility, "sc1 loads in
+// place of the acquire"): every word another workgroup reads inside the
+// launch (best, prevnn, partials, pose, tickets, sched) is stored and loaded
+// by relaxed agent-scope atomics (global sc1: write-through, L1 bypassed);
+// every storing wave drains (s_waitcnt vmcnt(0)) and the workgroup barrier
+// precedes the one lane's ticket add / publish; the receiver is told by the
+// value its own atomic returned and loads only after it.  Device-local
+// memory is never stale in another XCD's L2 (probes), so no L2 write-back or
+// invalidate is needed; option persist_fences adds agent release / acquire
+// fences around every hand-off (A/B: identical results, slower).
+// --------------------------------------------------------------------------
+struct PersistArgs {
+    // search
+    const double* src;  // source xyz64, Morton order
+    int N;
+    const float4 *p4, *tlo, *thi, *qbox, *slo, *shi;
+    int ntiles, nsuper, super_cull, seed_stride, reseed;
+    float r2s;
+    Org3 org;
+    // accumulation
+    const double *scov, *tgt64, *tcov;
+    double r2;
+    unsigned long long* best;
+    int32_t* prevnn;
+    double* partial;
+    // solve
+    SolveArgs a;
+    int max_iter;
+    double rel_fit, rel_rmse;
+    // schedule
+    unsigned long long* sched;  // per start: (pass << 40) | (S << 32) | next item
+    int32_t* tick_blk;          // per (start, accumulation block): search items arrived
+    int32_t* tick_start;        // per start: accumulation blocks arrived
+    int32_t* pctl;              // [0] finished starts, [1] error (timeout)
+    int B, sblk, nblk, want_items;
+    long long timeout_ticks;
+    unsigned long long* counters;
+    int fences;  // agent release / acquire fences around every hand-off (A/B; see above)
+};
+
+__host__ __device__ __forceinline__ int sched_pass(unsigned long long v) { return (int)(v >> 40); }
+__host__ __device__ __forceinline__ int sched_splits(unsigned long long v) { return (int)((v >> 32) & 0xffu); }
+__host__ __device__ __forceinline__ unsigned sched_item(unsigned long long v) { return (unsigned)v; }
+__host__ __device__ __forceinline__ unsigned long long sched_word(int pass, int S) {
+    return ((unsigned long long)pass << 40) | ((unsigned long long)S << 32);
+}
+// tile splits of a pass: about want_items search items over the running starts
+__host__ __device__ __forceinline__ int persist_splits(int nact, int sblk, int want_items) {
+    const int per = max(1, nact) * sblk;
+    return min(64, max(1, (want_items + per - 1) / per));
+}
+
+__device__ __forceinline__ unsigned long long readlane_u64(unsigned long long v, int k) {
+    const unsigned lo = __builtin_amdgcn_readlane((unsigned)v, k);
+    const unsigned hi = __builtin_amdgcn_readlane((unsigned)(v >> 32), k);
+    return ((unsigned long long)hi << 32) | lo;
+}
+
+// One search item: the 512 queries of query block grp (wave w: 128 of
+// them), tile split `split` of S.  Queries formed as xform_queries_kernel
+// does, searched as nn_search_kernel does, merged into best[].
+__device__ __forceinline__ void persist_search_item(const PersistArgs& P, int slot, int S, int grp, int split,
+                                                 float4* stage_w) {
+    const int lane = threadIdx.x & 63, wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int N = P.N;
+    const float4 s0lo = lane < P.nsuper ? P.slo[lane] : make_float4(0.f, 0.f, 0.f, 0.f);
+    const float4 s0hi = lane < P.nsuper ? P.shi[lane] : make_float4(0.f, 0.f, 0.f, 0.f);
+    double Q[12];
+#pragma unroll
+    for (int t = 0; t < 12; ++t) {  // wave-uniform: kept in scalar registers
+        const unsigned long long v = ld_u64<true>(reinterpret_cast<const unsigned long long*>(P.a.Q) + 12 * slot + t);
+        Q[t] = __longlong_as_double((long long)readlane_u64(v, 0));
+    }
+    const int i0 = grp * kCBlockQ + wid * (64 * kCQPT) + lane;
+    float qx[kCQPT], qy[kCQPT], qz[kCQPT], bound[kCQPT], bd[kCQPT];
+    int bj[kCQPT];
+#pragma unroll
+    for (int k = 0; k < kCQPT; ++k) {
+        const int i = i0 + 64 * k;
+        float x = 0.f, y = 0.f, z = 0.f, b = 0.0f;  // past N: bound 0, never takes anything
+        if (i < N) {
+            const double p[3] = {P.src[3 * i], P.src[3 * i + 1], P.src[3 * i + 2]};
+            double q[3];
+            xform(Q, p, q);
+            x = (float)(q[0] - P.org.x), y = (float)(q[1] - P.org.y), z = (float)(q[2] - P.org.z);
+            b = P.r2s;
+            const int jp = ld_i32<true>(P.prevnn + (size_t)slot * N + i);
+            if (jp >= 0) {
+                b = fminf(b, d2f(x, y, z, P.p4[jp]) * kSeedSlack + 1e-30f);
+            } else if (jp == kNoSeed || P.reseed) {
+                for (int t = 0; t < P.ntiles; t += P.seed_stride)
+                    b = fminf(b, d2f(x, y, z, P.p4[t * kTile]) * kSeedSlack + 1e-30f);
+            }
+        }
+        qx[k] = x;
+        qy[k] = y;
+        qz[k] = z;
+        bound[k] = b;
+    }
+    const int visited = culled_search<false>(stage_w, P.p4, P.tlo, P.thi, P.qbox, P.ntiles, P.slo, P.shi, P.nsuper,
+                                             P.super_cull, S, split, qx, qy, qz, bound, bd, bj, s0lo, s0hi);
+    if (lane == 0 && P.counters) {
+        unsigned long long* cs = P.counters + kCounterStride * ((blockIdx.x * kCWaves + wid) % kCounterSlots);
+        atomicAdd(cs, (unsigned long long)visited);
+        atomicMax(cs + 1, (unsigned long long)visited);
+    }
+    unsigned long long* out = P.best + (size_t)slot * N;
+#pragma unroll
+    for (int k = 0; k < kCQPT; ++k) {
+        const int i = i0 + 64 * k;
+        if (i >= N || bj[k] < 0) continue;  // best[] holds kNone already
+        const unsigned long long v = ((unsigned long long)__float_as_uint(bd[k]) << 32) | (unsigned)bj[k];
+        if (S == 1)
+            st_u64<true>(out + i, v);
+        else
+            __hip_atomic_fetch_min(out + i, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+}
+
+// Accumulation block ablk of start slot (the whole workgroup), as
+// gicp_accum_kernel / p2p_accum_kernel: its partial, next seeds, best[] reset.
+template <int kEst>
+__device__ __forceinline__ void persist_accumulate(const PersistArgs& P, int slot, int ablk) {
+    constexpr int NV = kEst == kEstGICP ? kNacc : kP2PTerms;
+    __shared__ double red[4][NV];
+    double acc[NV];
+    double* part = P.partial + ((size_t)slot * P.nblk + ablk) * kPartialStride;
+    if constexpr (kEst == kEstGICP) {
+        gicp_block_terms<true>(slot, ablk, P.src, P.scov, P.N, P.tgt64, P.tcov, P.a.Q, P.a.R, P.r2, P.best, P.prevnn,
+                               acc);
+        block_partial<NV, true>(acc, red, [](int v) { return v; }, part);
+    } else {
+        p2p_block_terms<true>(slot, ablk, P.src, P.N, P.tgt64, P.a.Q, P.r2, P.best, P.prevnn, acc);
+        block_partial<NV, true>(acc, red, p2p_slot, part);
+    }
+}
+
+// The start's reduction, convergence test and solve (wave 0), as
+// icp_solve_kernel; then pass + 1 is published, or the start counted done.
+template <int kEst>
+__device__ __forceinline__ void persist_solve(const PersistArgs& P, int slot, int pass) {
+    const int lane = threadIdx.x & 63;
+    double s[kNacc];
+    reduce_partials<true>(P.partial, slot, P.nblk, s);
+    if (lane != 0) return;
+    st_i32<true>(P.tick_start + slot, 0);
+    const bool fin = solve_start<kEst, true>(slot, s, P.N, pass, P.max_iter, P.rel_fit, P.rel_rmse, P.a);
+    if (P.fences) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the pose (sc1) has landed before the publish
+    if (fin) {
+        __hip_atomic_fetch_add(P.pctl, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    } else {
+        const int nact = P.B - ld_i32<true>(P.pctl);
+        __hip_atomic_store(P.sched + slot, sched_word(pass + 1, persist_splits(nact, P.sblk, P.want_items)),
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+}
+
+// Wave 0: the next search item (slot, pass, splits, item), slot -1 when all
+// starts are done (or on the timeout guard).
+__device__ __forceinline__ void persist_take(const PersistArgs& P, long long t_begin, int* sh) {
+    const int lane = threadIdx.x & 63;
+    int gb = -1;
+    unsigned long long gv = 0;
+    const int rot = (int)((blockIdx.x * 7u) & 63u);  // spread the workgroups over the starts
+    for (;;) {
+        if (ld_i32<true>(P.pctl) >= P.B || ld_i32<true>(P.pctl + 1) != 0) break;
+        for (int b0 = 0; b0 < P.B && gb < 0; b0 += 64) {
+            const int b = b0 + lane;
+            bool av = false;
+            if (b < P.B) {
+                const unsigned long long v = ld_u64<true>(P.sched + b);
+                av = sched_item(v) < (unsigned)(P.sblk * sched_splits(v));
+            }
+            unsigned long long m = __ballot(av);
+            while (m) {
+                const unsigned long long mr = rot ? ((m >> rot) | (m << (64 - rot))) : m;
+                const int k = (__builtin_ctzll(mr) + rot) & 63;
+                m &= ~(1ull << k);
+                unsigned long long old = 0;
+                if (lane == k)
+                    old = __hip_atomic_fetch_add(P.sched + b0 + k, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                old = readlane_u64(old, k);
+                if (sched_item(old) < (unsigned)(P.sblk * sched_splits(old))) {
+                    gb = b0 + k;
+                    gv = old;
+                    break;
+                }
+            }
+        }
+        if (gb >= 0) break;
+        if ((long long)__builtin_amdgcn_s_memrealtime() - t_begin > P.timeout_ticks) {
+            if (lane == 0) st_i32<true>(P.pctl + 1, 1);
+            break;
+        }
+        __builtin_amdgcn_s_sleep(8);
+    }
+    if (lane == 0) {
+        sh[0] = gb;
+        sh[1] = sched_pass(gv);
+        sh[2] = sched_splits(gv);
+        sh[3] = (int)sched_item(gv);
+    }
+    if (gb >= 0 && P.fences) {  // the pose / seeds of the pass were published before the item
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+}
+
+// tid 0: arrive at a ticket after every wave's stores have landed (release);
+// returns (to every thread, through sh_last) whether this was the last of
+// `expect` arrivals, the last arriver having taken the acquire.
+__device__ __forceinline__ bool persist_arrive(int32_t* ticket, int expect, int32_t* reset, int* sh_last,
+                                               int fences) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's stores / merges have landed
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        if (reset) st_i32<true>(reset, 0);
+        if (fences) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const int t = __hip_atomic_fetch_add(ticket, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const int last = t == expect - 1;
+        if (last && fences) {
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        *sh_last = last;
+    }
+    __syncthreads();
+    return *sh_last != 0;
+}
+
+template <int kEst>
+__global__ __launch_bounds__(256) void icp_persistent_kernel(PersistArgs P) {
+    __shared__ float4 stage[kCWaves][kTile];
+    __shared__ int sh[4];
+    __shared__ int sh_last;
+    const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const long long t_begin = (long long)__builtin_amdgcn_s_memrealtime();
+    for (;;) {
+        // ---- 1. take the next search item (wave 0)
+        if (wid == 0) persist_take(P, t_begin, sh);
+        __syncthreads();
+        const int slot = __builtin_amdgcn_readfirstlane(sh[0]);
+        if (slot < 0) return;
+        const int pass = __builtin_amdgcn_readfirstlane(sh[1]);
+        const int S = __builtin_amdgcn_readfirstlane(sh[2]);
+        const int bx = __builtin_amdgcn_readfirstlane(sh[3]);
+        const int grp = bx / S, split = bx - grp * S;
+        // ---- 2. the item's queries and culled search
+        persist_search_item(P, slot, S, grp, split, stage[wid]);
+        // ---- 3. arrival at the accumulation block; the last arriver accumulates it
+        const int qpb = 256 * accum_qpt(P.N);  // queries per accumulation block
+        const int ablk = grp * kCBlockQ / qpb;
+        const int q_end = min(P.N, (ablk + 1) * qpb);
+        const int nsearch = (q_end + kCBlockQ - 1) / kCBlockQ - ablk * qpb / kCBlockQ;  // query blocks in it
+        if (!persist_arrive(P.tick_blk + (size_t)slot * P.nblk + ablk, nsearch * S, nullptr, &sh_last, P.fences))
+            continue;
+        persist_accumulate<kEst>(P, slot, ablk);
+        // ---- 4. arrival at the start; the last arriver solves and publishes the next pass
+        if (!persist_arrive(P.tick_start + slot, P.nblk, P.tick_blk + (size_t)slot * P.nblk + ablk, &sh_last,
+                            P.fences))
+            continue;
+        if (wid == 0) persist_solve<kEst>(P, slot, pass);
+    }
 }
 
 // Kernel-level 1-NN (orpcd_nn1_radius): the same culled search on Morton-
@@ -1725,6 +2077,73 @@ hipError_t launch_gicp_solve(const orpcd_ctx* c, int nact, int pass, const orpcd
     if (e != hipSuccess) return e;
     const double r2 = p.max_correspondence_distance * p.max_correspondence_distance;
     return launch_xform(c, nact, r2, s, false);  // queries of the next pass (done starts skip)
+}
+
+// Resident 256-thread workgroups of the persistent kernel on this device.
+int persist_grid(int device, int est) {
+    int per_cu = 0, cus = 0;
+    const void* f = est == kEstP2P ? (const void*)icp_persistent_kernel<kEstP2P>
+                                   : (const void*)icp_persistent_kernel<kEstGICP>;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, f, 256, 0) != hipSuccess) return 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess) return 0;
+    return per_cu * cus;
+}
+
+int persist_first_splits(const orpcd_ctx* c, int B, int grid) {
+    const int sblk = (int)((c->src.n + kCBlockQ - 1) / kCBlockQ);
+    return persist_splits(B, sblk, c->opt.persist_items > 0 ? c->opt.persist_items : grid);
+}
+
+unsigned long long persist_sched_word(int pass, int S) { return sched_word(pass, S); }
+
+// The persistent pass loop of the batch set up by batch_setup (sched[] holds
+// pass 0 of every start, the tickets and pctl are zero, best[] is kNone).
+hipError_t launch_icp_persistent(const orpcd_ctx* c, int B, int grid, const orpcd_gicp_params& p, hipStream_t s) {
+    const int N = (int)c->src.n;
+    const double r2 = p.max_correspondence_distance * p.max_correspondence_distance;
+    PersistArgs P{};
+    P.src = c->src.xyz64.p;
+    P.N = N;
+    P.p4 = c->tgt.p4.p;
+    P.tlo = c->tgt.tlo.p;
+    P.thi = c->tgt.thi.p;
+    P.qbox = c->tgt.qbox.p;
+    P.slo = c->tgt.slo.p;
+    P.shi = c->tgt.shi.p;
+    P.ntiles = (int)c->tgt.ntiles;
+    P.nsuper = (int)c->tgt.nsuper;
+    P.super_cull = c->opt.super_cull;
+    P.seed_stride = seed_stride_for(c->tgt.ntiles, c->opt.seed_reps);
+    P.reseed = c->opt.reseed;
+    P.r2s = search_r2(r2);
+    P.org = org_of(c->tgt);
+    P.scov = c->scov.p;
+    P.tgt64 = c->tgt.xyz64.p;
+    P.tcov = c->tcov.p;
+    P.r2 = r2;
+    P.best = c->best.p;
+    P.prevnn = c->prevnn.p;
+    P.partial = c->partial.p;
+    P.a = solve_args(c);
+    P.max_iter = p.max_iteration;
+    P.rel_fit = p.relative_fitness;
+    P.rel_rmse = p.relative_rmse;
+    P.sched = c->sched.p;
+    P.tick_blk = c->tick_blk.p;
+    P.tick_start = c->tick_start.p;
+    P.pctl = c->pctl.p;
+    P.B = B;
+    P.sblk = (N + kCBlockQ - 1) / kCBlockQ;
+    P.nblk = accum_blocks(N);
+    P.want_items = c->opt.persist_items > 0 ? c->opt.persist_items : grid;
+    P.timeout_ticks = (long long)c->opt.persist_timeout_s * 100000000LL;  // s_memrealtime: 100 MHz
+    P.counters = c->count_tiles ? c->counters.p : nullptr;
+    P.fences = c->opt.persist_fences;
+    if (c->est == kEstP2P)
+        icp_persistent_kernel<kEstP2P><<<(unsigned)grid, 256, 0, s>>>(P);
+    else
+        icp_persistent_kernel<kEstGICP><<<(unsigned)grid, 256, 0, s>>>(P);
+    return hipGetLastError();
 }
 
 hipError_t launch_reduce_partials(const orpcd_ctx* c, int slot, double* sums29, hipStream_t s) {

@@ -199,6 +199,12 @@ struct orpcd_ctx {
     orpcd::DevBuf<int32_t> ctl;     // 2 + B: pipelined pass control (gicp_kernels.hip, PassCtl)
     unsigned long long* prog_h = nullptr;  // host-mapped progress word of the pipelined passes
     unsigned long long* prog_d = nullptr;  // its device address
+    // persistent pass loop (gicp_kernels.hip, icp_persistent_kernel)
+    orpcd::DevBuf<unsigned long long> sched;  // B: (pass << 40) | (splits << 32) | next search item
+    orpcd::DevBuf<int32_t> tick_blk;          // B*nblk: search items arrived per accumulation block
+    orpcd::DevBuf<int32_t> tick_start;        // B: accumulation blocks arrived per start
+    orpcd::DevBuf<int32_t> pctl;              // [0] finished starts, [1] error flag
+    int persist_grid[2] = {0, 0};             // resident workgroups (GICP, PointToPoint kernels)
     orpcd::DevBuf<double> out_fit, out_rmse;
     orpcd::DevBuf<int32_t> out_iters;
     orpcd::DevBuf<int64_t> out_ncorr;
@@ -211,6 +217,7 @@ struct orpcd_ctx {
 
     orpcd::HostBuf<double> h64;
     orpcd::HostBuf<int32_t> h32;
+    orpcd::HostBuf<unsigned long long> h64sched;  // staging of the persistent loop's sched[] / pctl
 
     // FastGlobal path (fgr_kernels.hip); index 0 = source, 1 = target
     struct FgrBufs {
@@ -260,6 +267,14 @@ struct orpcd_ctx {
         int lookahead = 4;        // pipelined: passes enqueued beyond the last one known complete
         int seed_reps = 64;       // pass-0 seed: nearest of ~this many tile representatives per query
                                   // (C2 sweep 8..512: equal within noise; 64 keeps the transform cheap)
+        int persist = 0;          // 1: the whole ICP loop in one persistent launch (icp_persistent_kernel):
+                                  // bit-identical, but slower at C2 (1 / 8 / 30 / 64 starts: 0.76 / 8.3 /
+                                  // 26.8 / 37.3 ms vs 0.52 / 4.7 / 16.2 / 26.9): its 190 VGPRs allow 2
+                                  // waves/SIMD, so a pass's search gets far fewer tile splits than the
+                                  // 16k-32k dispatched waves of nn_search_kernel.  0: one launch per kernel
+        int persist_items = 0;    // search items per pass to aim for (0: the resident workgroups)
+        int persist_timeout_s = 60;  // guard: the persistent loop gives up (error) after this long
+        int persist_fences = 0;   // 1: agent release/acquire fences around the persistent loop's hand-offs
     } opt;
     std::vector<hipEvent_t> ev_pool;
     orpcd::KernelStats stats;
@@ -312,6 +327,10 @@ hipError_t launch_gicp_solve_sums(const orpcd_ctx* c, const double* sums29, int6
                                   const orpcd_gicp_params& p, hipStream_t s);
 hipError_t launch_nn1(const double* q, int64_t nq, const CloudLayout& t, double r2, int32_t* idx, double* d2,
                       hipStream_t s);
+int persist_grid(int device, int est);
+int persist_first_splits(const orpcd_ctx* c, int B, int grid);
+unsigned long long persist_sched_word(int pass, int S);
+hipError_t launch_icp_persistent(const orpcd_ctx* c, int B, int grid, const orpcd_gicp_params& p, hipStream_t s);
 
 // fgr_kernels.hip
 constexpr int kFeatDim = 36;  // 33 FPFH bins padded for the 16x16x4 f64 MFMA

@@ -346,8 +346,16 @@ int fgr_device(orpcd_ctx* c, const double* src, int64_t n, const double* tgt, in
 // queries.  Host staging in c->h64 / c->h32 (layout used by gicp_batch).
 // init16 != null (PointToPoint refinement): base pose G_b = init16[b] (column
 // convention, as registration_icp applies `init`), no covariances.
+// The whole ICP loop in one persistent launch (icp_persistent_kernel): the
+// default, except under ORPCD_TRACE (per-pass timings need per-pass launches)
+// and for the alternative search kernels.
+bool persistent_ok(const orpcd_ctx* c) {
+    static const bool trace = getenv("ORPCD_TRACE") != nullptr;
+    return c->opt.persist && !trace && c->opt.search_kernel == 0;
+}
+
 int batch_setup(orpcd_ctx* c, const double* R0, const double* t0, int B, const orpcd_gicp_params* p,
-                const double* init16 = nullptr) {
+                const double* init16 = nullptr, bool persist = false) {
     const int64_t N = c->src.n;
     const int nblk = accum_blocks(N);
     if (!init16) CTX_CHECK(c, c->scov.ensure((size_t)B * N * 6));
@@ -431,13 +439,33 @@ int batch_setup(orpcd_ctx* c, const double* R0, const double* t0, int B, const o
     // posed-frame source covariances for every start (rigid equivariance)
     c->est = init16 ? kEstP2P : kEstGICP;
     if (!init16) CTX_CHECK(c, launch_normals_cov(c->sraw.p, N, c->scratch64c.p, B, p->epsilon, nullptr, c->scov.p, s));
-    CTX_CHECK(c, launch_xform(c, B, p->max_correspondence_distance * p->max_correspondence_distance, s));
-
+    if (!persist) {
+        CTX_CHECK(c, launch_xform(c, B, p->max_correspondence_distance * p->max_correspondence_distance, s));
+        return ORPCD_OK;
+    }
+    // persistent loop: pass 0 of every start open, tickets zero, best[] = kNone
+    // (the loop's queries are formed by its own search items)
+    if (c->persist_grid[c->est] == 0) c->persist_grid[c->est] = persist_grid(c->device, c->est);
+    CTX_REQUIRE(c, c->persist_grid[c->est] > 0, "gicp: the persistent kernel cannot be resident on this device");
+    CTX_CHECK(c, c->sched.ensure((size_t)B));
+    CTX_CHECK(c, c->tick_blk.ensure((size_t)B * nblk));
+    CTX_CHECK(c, c->tick_start.ensure((size_t)B));
+    CTX_CHECK(c, c->pctl.ensure(2));
+    CTX_CHECK(c, c->h64sched.ensure((size_t)B));
+    const int S0 = persist_first_splits(c, B, c->persist_grid[c->est]);
+    for (int b = 0; b < B; ++b) c->h64sched.p[b] = persist_sched_word(0, S0);
+    CTX_CHECK(c, hipMemcpyAsync(c->sched.p, c->h64sched.p, (size_t)B * 8, hipMemcpyHostToDevice, s));
+    CTX_CHECK(c, hipMemsetAsync(c->tick_blk.p, 0, (size_t)B * nblk * 4, s));
+    CTX_CHECK(c, hipMemsetAsync(c->tick_start.p, 0, (size_t)B * 4, s));
+    CTX_CHECK(c, hipMemsetAsync(c->pctl.p, 0, 8, s));
+    CTX_CHECK(c, hipMemsetAsync(c->best.p, 0xff, (size_t)B * N * 8, s));
     return ORPCD_OK;
 }
 
 int run_passes(orpcd_ctx* c, int B, const orpcd_gicp_params* p, double* T_out, double* rmse_out,
                double* fitness_out, int32_t* iters_out, int64_t* ncorr_out);
+int run_passes_persistent(orpcd_ctx* c, int B, const orpcd_gicp_params* p, double* T_out, double* rmse_out,
+                          double* fitness_out, int32_t* iters_out, int64_t* ncorr_out);
 int run_passes_pipelined(orpcd_ctx* c, int B, const orpcd_gicp_params* p, double* T_out, double* rmse_out,
                          double* fitness_out, int32_t* iters_out, int64_t* ncorr_out);
 int read_outputs(orpcd_ctx* c, int B, unsigned long long tiles_before, double* T_out, double* rmse_out,
@@ -502,6 +530,11 @@ int orpcd_ctx_destroy(orpcd_ctx* c) {
     c->done.release();
     c->active.release();
     c->ctl.release();
+    c->sched.release();
+    c->tick_blk.release();
+    c->tick_start.release();
+    c->pctl.release();
+    c->h64sched.release();
     if (c->prog_h) (void)hipHostFree(c->prog_h);
     c->out_iters.release();
     c->out_ncorr.release();
@@ -566,8 +599,10 @@ int orpcd_gicp_batch(orpcd_ctx* c, const double* R0, const double* t0, int32_t B
         if (rc) return rc;
     }
     CTX_REQUIRE(c, c->src_cov, "gicp_batch: the source has no covariances (set it with orpcd_set_source)");
-    int rc = batch_setup(c, R0, t0, B, p);
+    const bool persist = persistent_ok(c);
+    int rc = batch_setup(c, R0, t0, B, p, nullptr, persist);
     if (rc) return rc;
+    if (persist) return run_passes_persistent(c, B, p, T_out, rmse_out, fitness_out, iters_out, ncorr_out);
     return run_passes(c, B, p, T_out, rmse_out, fitness_out, iters_out, ncorr_out);
 }
 
@@ -595,8 +630,10 @@ int orpcd_icp_p2p_batch(orpcd_ctx* c, const double* init, int32_t B, const orpcd
     CTX_REQUIRE(c, p->max_iteration >= 0, "icp_p2p_batch: max_iteration must be >= 0");
     for (int64_t t = 0; t < 16 * (int64_t)B; ++t) CTX_REQUIRE(c, std::isfinite(init[t]), "icp_p2p_batch: non-finite init");
     CTX_CHECK(c, hipSetDevice(c->device));
-    int rc = batch_setup(c, nullptr, nullptr, B, p, init);
+    const bool persist = persistent_ok(c);
+    int rc = batch_setup(c, nullptr, nullptr, B, p, init, persist);
     if (rc) return rc;
+    if (persist) return run_passes_persistent(c, B, p, T_out, rmse_out, fitness_out, iters_out, ncorr_out);
     return run_passes(c, B, p, T_out, rmse_out, fitness_out, iters_out, ncorr_out);
 }
 
@@ -650,7 +687,47 @@ int read_outputs(orpcd_ctx* c, int B, unsigned long long tiles_before, double* T
     return ORPCD_OK;
 }
 
-// The pipelined ICP loop (opt.pipeline, default): every pass is enqueued
+// The persistent ICP loop (opt.persist, default): one launch runs every pass
+// of every start (icp_persistent_kernel); the host waits for it once.
+int run_passes_persistent(orpcd_ctx* c, int B, const orpcd_gicp_params* p, double* T_out, double* rmse_out,
+                          double* fitness_out, int32_t* iters_out, int64_t* ncorr_out) {
+    hipStream_t s = c->stream;
+    unsigned long long tiles_before = 0, unused = 0;
+    if (c->profiling) CTX_CHECK(c, read_counters(c, tiles_before, unused, false));
+    const bool timed = c->profiling;
+    c->count_tiles = timed;
+    if (timed) {
+        while (c->ev_pool.size() < 2) {
+            hipEvent_t e;
+            CTX_CHECK(c, hipEventCreateWithFlags(&e, hipEventDisableSystemFence));  // timing only
+            c->ev_pool.push_back(e);
+        }
+        CTX_CHECK(c, hipEventRecord(c->ev_pool[0], s));
+    }
+    CTX_CHECK(c, launch_icp_persistent(c, B, c->persist_grid[c->est], *p, s));
+    if (timed) CTX_CHECK(c, hipEventRecord(c->ev_pool[1], s));
+    int32_t* hctl = reinterpret_cast<int32_t*>(c->h64sched.p);  // >= B u64 words: room for pctl[0..1]
+    CTX_CHECK(c, hipMemcpyAsync(hctl, c->pctl.p, 8, hipMemcpyDeviceToHost, s));
+    CTX_CHECK(c, hipStreamSynchronize(s));
+    if (hctl[1] != 0 || hctl[0] != B) {
+        c->err = "gicp: the persistent pass loop did not finish every start (device timeout guard, " +
+                 std::to_string(hctl[0]) + " of " + std::to_string(B) + " finished)";
+        return ORPCD_EDEVICE;
+    }
+    if (timed) {
+        float ms = 0.f;
+        CTX_CHECK(c, hipEventElapsedTime(&ms, c->ev_pool[0], c->ev_pool[1]));
+        c->stats.launches += 1;
+        c->stats.ms += ms;
+    }
+    int rc = read_outputs(c, B, tiles_before, T_out, rmse_out, fitness_out, iters_out, ncorr_out);
+    if (rc) return rc;
+    if (iters_out)
+        for (int b = 0; b < B; ++b) c->stats.passes += iters_out[b] + 1;
+    return ORPCD_OK;
+}
+
+// The pipelined ICP loop (opt.pipeline): every pass is enqueued
 // without a host round trip.  The device keeps the running starts (PassCtl:
 // solve fused into the accumulation's last block, compaction of active[],
 // splits re-derived by the search from the device count) and publishes
@@ -1301,6 +1378,10 @@ int orpcd_set_option(orpcd_ctx* c, const char* key, double value) {
     else if (k == "pipeline" && (v == 0 || v == 1)) c->opt.pipeline = v;
     else if (k == "lookahead" && v >= 1 && v <= 64) c->opt.lookahead = v;
     else if (k == "seed_reps" && v >= 1) c->opt.seed_reps = v;
+    else if (k == "persist" && (v == 0 || v == 1)) c->opt.persist = v;
+    else if (k == "persist_items" && v >= 0) c->opt.persist_items = v;
+    else if (k == "persist_timeout_s" && v >= 1 && v <= 3600) c->opt.persist_timeout_s = v;
+    else if (k == "persist_fences" && (v == 0 || v == 1)) c->opt.persist_fences = v;
     else {
         c->err = "set_option: unknown key or bad value: " + k;
         return ORPCD_EINVAL;

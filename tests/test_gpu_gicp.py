@@ -241,6 +241,7 @@ def test_pipelined_passes_identical(ctx, lookahead):
     inits = np.repeat(np.eye(4)[None], 5, axis=0)
     inits[:, :3, 3] = rng.normal(size=(5, 3)) * 0.02
     try:
+        ctx.set_option("persist", 0)
         ctx.set_option("pipeline", 1)
         ctx.set_option("lookahead", lookahead)
         got = [ctx.gicp_batch(R0, t0), ctx.gicp_batch(R0[:9], t0[:9], max_iteration=7)]
@@ -262,6 +263,70 @@ def test_pipelined_passes_identical(ctx, lookahead):
     for g, r in zip(got, ref):
         for k in ("T", "rmse", "fitness", "iters"):
             assert np.array_equal(g[k], r[k]), k
+
+
+@pytest.mark.parametrize("items", [0, 1, 100000])
+def test_persistent_loop_identical(ctx, items):
+    """The persistent pass loop (option persist: every pass of every start in
+    one launch, starts advancing independently, splits re-chosen per pass) against
+    the launch-per-kernel loop: bit-identical T, rmse, fitness, iterations and
+    inlier counts, for GICP batches of 70 starts (finishing at many different
+    passes, max_iteration reached and not), a single start, and PointToPoint
+    refinement.  items: search items aimed at per pass (0: one per resident
+    workgroup; 1: no tile splits; 100000: 64 splits)."""
+    src, tgt = small_pair(3000, 2800, seed=21)
+    rng = np.random.default_rng(5)
+    R0 = np.array([rot_xyz(*rng.uniform(-90, 90, 3)) for _ in range(70)])
+    t0 = rng.normal(size=(70, 3)) * 0.1
+    inits = np.repeat(np.eye(4)[None], 5, axis=0)
+    inits[:, :3, 3] = rng.normal(size=(5, 3)) * 0.02
+
+    def run():
+        ctx.set_target(tgt)
+        ctx.set_source(src)
+        out = [ctx.gicp_batch(R0, t0), ctx.gicp_batch(R0[:9], t0[:9], max_iteration=7),
+               ctx.gicp_batch(R0[3:4], t0[3:4])]
+        ctx.set_target_points(tgt)
+        ctx.set_source_points(src)
+        out.append(ctx.icp_p2p_batch(inits, max_iteration=30))
+        return out
+
+    try:
+        ctx.set_option("persist", 1)
+        ctx.set_option("persist_items", items)
+        got = run()
+        ctx.set_option("persist", 0)
+        ref = run()
+    finally:
+        ctx.set_option("persist", 0)
+        ctx.set_option("persist_items", 0)
+    assert len(set(got[0]["iters"].tolist())) > 5
+    for g, r in zip(got, ref):
+        for k in ("T", "rmse", "fitness", "iters", "ncorr"):
+            assert np.array_equal(g[k], r[k]), k
+
+
+def test_persistent_loop_c2_size_identical(ctx):
+    """At the bench's size (50k <-> 50k, 8 posed starts to convergence): the
+    persistent loop reproduces the launch-per-kernel loop bit for bit."""
+    from workloads import c2_pair
+    from orpcd_amd import Preprocessor
+    s, t = c2_pair(50_000)
+    s = Preprocessor([]).preprocess(s)
+    t = Preprocessor([]).preprocess(t)
+    rng = np.random.default_rng(1000)
+    R0 = np.array([rot_xyz(*rng.uniform(-90, 90, 3)) for _ in range(8)])
+    t0 = rng.normal(size=(8, 3)) * 0.1
+    ctx.set_target(t)
+    ctx.set_source(s)
+    ref = ctx.gicp_batch(R0, t0)
+    try:
+        ctx.set_option("persist", 1)
+        got = ctx.gicp_batch(R0, t0)
+    finally:
+        ctx.set_option("persist", 0)
+    for k in ("T", "rmse", "fitness", "iters", "ncorr"):
+        assert np.array_equal(got[k], ref[k]), k
 
 
 def test_gicp_matches_g4_fixtures(ctx):
