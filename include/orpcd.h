@@ -15,6 +15,9 @@
  *       GeneralizedICP.optimize            Optimizer/generalizedICP.py:47-83
  *       -> o3d registration_generalized_icp Optimizer/generalizedICP.py:59-70
  *       batched over the multistart loop   Aligner/Aligner.py:178-202
+ *   orpcd_set_targets / orpcd_gicp_batch_targets
+ *       the multistarts of one compass iteration's six candidates
+ *                                          Aligner/Aligner.py:206-226, 263-298
  *   orpcd_set_source_rows / orpcd_gicp_shard_*
  *       one GeneralizedICP.optimize with the source rows split over GPUs
  *                                          Optimizer/generalizedICP.py:59-70
@@ -99,6 +102,18 @@ typedef struct {
 int orpcd_gicp_batch(orpcd_ctx* ctx, const double* R0, const double* t0, int32_t B,
                      const orpcd_gicp_params* params, double* T_out, double* rmse_out,
                      double* fitness_out, int32_t* iters_out, int64_t* ncorr_out);
+
+/* Several targets per batch: the six scale candidates of one compass
+ * iteration (Aligner.py:263-298, each compass_step scaling the target,
+ * :221-222) as ONE device batch instead of six.  orpcd_set_targets uploads
+ * ntargets (<= 8) clouds, xyz = their rows concatenated, m[k] rows each;
+ * orpcd_gicp_batch_targets runs start b against target target_of_start[b]
+ * (outputs in start order, as orpcd_gicp_batch).  orpcd_set_target is the
+ * one-target case; orpcd_gicp_batch = every start against target 0.         */
+int orpcd_set_targets(orpcd_ctx* ctx, const double* xyz, const int64_t* m, int32_t ntargets, double epsilon);
+int orpcd_gicp_batch_targets(orpcd_ctx* ctx, const double* R0, const double* t0, const int32_t* target_of_start,
+                             int32_t B, const orpcd_gicp_params* params, double* T_out, double* rmse_out,
+                             double* fitness_out, int32_t* iters_out, int64_t* ncorr_out);
 
 /* --------------------------------------- PointToPoint ICP refinement (§8f)
  * Aligner.refine_registration (Aligner.py:319-364, icp_type="PointToPoint")

@@ -442,15 +442,17 @@ __global__ __launch_bounds__(256) void xform_queries_kernel(const double* __rest
                                                             const int32_t* __restrict__ active,
                                                             const double* __restrict__ Qm,
                                                             const int32_t* __restrict__ done,
-                                                            const float4* __restrict__ p4, int ntiles,
-                                                            int seed_stride, const int32_t* __restrict__ prevnn,
+                                                            const TargetDesc* __restrict__ tdesc, TgtBounds tb,
+                                                            const int32_t* __restrict__ prevnn,
                                                             float r2s, int reseed, float4* __restrict__ q32,
                                                             unsigned long long* __restrict__ best,
                                                             const int32_t* __restrict__ nact_dev,
-                                                            float4* __restrict__ gbox, Org3 org) {
+                                                            float4* __restrict__ gbox) {
     if (nact_dev && (int)blockIdx.y >= *nact_dev) return;  // pipelined: grid sized for an upper bound
     const int slot = active[blockIdx.y];
     if (done[slot]) return;
+    const TargetDesc& tg = tdesc[target_of_row(tb, blockIdx.y)];
+    const float4* __restrict__ p4 = tg.p4;
     const int i = blockIdx.x * 256 + threadIdx.x;
     const bool valid = i < N;
     const float inf = 3.0e38f;
@@ -463,13 +465,13 @@ __global__ __launch_bounds__(256) void xform_queries_kernel(const double* __rest
         const double p[3] = {src[3 * i], src[3 * i + 1], src[3 * i + 2]};
         double q[3];
         xform(Q, p, q);
-        x = (float)(q[0] - org.x), y = (float)(q[1] - org.y), z = (float)(q[2] - org.z);
+        x = (float)(q[0] - tg.ox), y = (float)(q[1] - tg.oy), z = (float)(q[2] - tg.oz);
         bound = r2s;
         const int jp = prevnn[(size_t)slot * N + i];
         if (jp >= 0) {
             bound = fminf(bound, d2f(x, y, z, p4[jp]) * kSeedSlack + 1e-30f);
         } else if (jp == kNoSeed || reseed) {
-            for (int t = 0; t < ntiles; t += seed_stride)
+            for (int t = 0; t < tg.ntiles; t += tg.seed_stride)
                 bound = fminf(bound, d2f(x, y, z, p4[t * kTile]) * kSeedSlack + 1e-30f);
         }
         q32[(size_t)slot * N + i] = make_float4(x, y, z, bound);
@@ -498,12 +500,18 @@ __global__ __launch_bounds__(256) void xform_queries_kernel(const double* __rest
 // Search kernel: grid = (blocks per start * S, running starts), 4 waves/block.
 // --------------------------------------------------------------------------
 __device__ __forceinline__ void nn_search_body(
-    const float4* __restrict__ q32, int N, const float4* __restrict__ p4, const float4* __restrict__ tlo,
-    const float4* __restrict__ thi, const float4* __restrict__ qbox, int ntiles, const float4* __restrict__ slo, const float4* __restrict__ shi,
-    int nsuper, int super_cull, const int32_t* __restrict__ active, const int32_t* __restrict__ done, int S,
-    unsigned long long* __restrict__ best, unsigned long long* __restrict__ counters, int by, int bx, int wid,
-    float4* stage_w, const float4* __restrict__ gbox) {
+    const float4* __restrict__ q32, int N, const TargetDesc& tg, int super_cull, const int32_t* __restrict__ active,
+    const int32_t* __restrict__ done, int S, unsigned long long* __restrict__ best,
+    unsigned long long* __restrict__ counters, int by, int bx, int wid, float4* stage_w,
+    const float4* __restrict__ gbox) {
     const int lane = threadIdx.x & 63;
+    const float4* __restrict__ p4 = tg.p4;
+    const float4* __restrict__ tlo = tg.tlo;
+    const float4* __restrict__ thi = tg.thi;
+    const float4* __restrict__ qbox = tg.qbox;
+    const float4* __restrict__ slo = tg.slo;
+    const float4* __restrict__ shi = tg.shi;
+    const int ntiles = tg.ntiles, nsuper = tg.nsuper;
     // first culling round's super-tile boxes: independent of the start and
     // its queries, so their load overlaps the slot and query loads
     // (xyz only, by raw buffer loads: lanes past nsuper read zeros, unguarded;
@@ -586,16 +594,11 @@ __device__ __forceinline__ void nn_search_body(
     }
 }
 
-// Two register budgets of the same search (orpcd_set_option "search_occupancy"):
-// the compiler's choice (88 VGPRs, 5 waves/SIMD) and a cap at 6 waves/SIMD
-// (74 VGPRs, no spills).
 #define ORPCD_NN_SEARCH_ARGS                                                                                   \
-    const float4 *__restrict__ q32, int N, const float4 *__restrict__ p4, const float4 *__restrict__ tlo,    \
-        const float4 *__restrict__ thi, const float4 *__restrict__ qbox, int ntiles, const float4 *__restrict__ slo,                          \
-        const float4 *__restrict__ shi, int nsuper, int super_cull, const int32_t *__restrict__ active,      \
-        const int32_t *__restrict__ done, int S, unsigned long long *__restrict__ best,                      \
-        unsigned long long *__restrict__ counters, const int32_t *__restrict__ nact_dev, int sblk, int want,   \
-        const float4 *__restrict__ gbox
+    const float4 *__restrict__ q32, int N, const TargetDesc *__restrict__ tdesc, TgtBounds tb, int super_cull,  \
+        const int32_t *__restrict__ active, const int32_t *__restrict__ done, int S,                          \
+        unsigned long long *__restrict__ best, unsigned long long *__restrict__ counters,                       \
+        const int32_t *__restrict__ nact_dev, int sblk, int want, const float4 *__restrict__ gbox
 
 // Block -> (start, query group x split).  Unpipelined: the grid is
 // (sblk * S, running starts) as the host counted them.  Pipelined (nact_dev):
@@ -621,14 +624,16 @@ __device__ __forceinline__ bool map_search_block(const int32_t* __restrict__ nac
     return true;
 }
 
+// Two register budgets of the same search (orpcd_set_option "search_occupancy"):
+// the compiler's choice (5 waves/SIMD) and a cap at 6 waves/SIMD.
 __global__ __launch_bounds__(kCBlock) __attribute__((amdgpu_waves_per_eu(5, 8))) void nn_search_kernel(
     ORPCD_NN_SEARCH_ARGS) {
     __shared__ float4 stage[kCWaves][kTile];
     const int wid = threadIdx.x >> 6;
     int by, bx;
     if (!map_search_block(nact_dev, sblk, want, by, bx, S)) return;
-    nn_search_body(q32, N, p4, tlo, thi, qbox, ntiles, slo, shi, nsuper, super_cull, active, done, S, best, counters,
-                   by, bx, wid, stage[wid], gbox);
+    nn_search_body(q32, N, tdesc[target_of_row(tb, by)], super_cull, active, done, S, best, counters, by, bx, wid,
+                   stage[wid], gbox);
 }
 __global__ __launch_bounds__(kCBlock) __attribute__((amdgpu_waves_per_eu(6, 8))) void nn_search_kernel_o6(
     ORPCD_NN_SEARCH_ARGS) {
@@ -636,8 +641,8 @@ __global__ __launch_bounds__(kCBlock) __attribute__((amdgpu_waves_per_eu(6, 8)))
     const int wid = threadIdx.x >> 6;
     int by, bx;
     if (!map_search_block(nact_dev, sblk, want, by, bx, S)) return;
-    nn_search_body(q32, N, p4, tlo, thi, qbox, ntiles, slo, shi, nsuper, super_cull, active, done, S, best, counters,
-                   by, bx, wid, stage[wid], gbox);
+    nn_search_body(q32, N, tdesc[target_of_row(tb, by)], super_cull, active, done, S, best, counters, by, bx, wid,
+                   stage[wid], gbox);
 }
 #undef ORPCD_NN_SEARCH_ARGS
 
@@ -1478,8 +1483,8 @@ __device__ __forceinline__ void gicp_block_terms(int slot, int ablk, const doubl
 
 template <bool kFused>
 __global__ __launch_bounds__(256) void gicp_accum_kernel(
-    const double* __restrict__ src, const double* __restrict__ scov, int N, const double* __restrict__ tgt64,
-    const double* __restrict__ tcov, const int32_t* __restrict__ active, const double* __restrict__ Qm,
+    const double* __restrict__ src, const double* __restrict__ scov, int N, const TargetDesc* __restrict__ tdesc,
+    TgtBounds tb, const int32_t* __restrict__ active, const double* __restrict__ Qm,
     const double* __restrict__ Rm, const int32_t* __restrict__ done, double r2,
     unsigned long long* __restrict__ best, int32_t* __restrict__ prevnn, double* __restrict__ partial,
     int nblk, PassCtl pc) {
@@ -1487,9 +1492,10 @@ __global__ __launch_bounds__(256) void gicp_accum_kernel(
     if (kFused && (int)blockIdx.y >= nact) return;
     const int slot = active[blockIdx.y];
     if (done[slot]) return;
+    const TargetDesc& tg = tdesc[target_of_row(tb, blockIdx.y)];
     __shared__ double red[4][kNacc];
     double acc[kNacc];
-    gicp_block_terms<false>(slot, blockIdx.x, src, scov, N, tgt64, tcov, Qm, Rm, r2, best, prevnn, acc);
+    gicp_block_terms<false>(slot, blockIdx.x, src, scov, N, tg.xyz64, tg.tcov, Qm, Rm, r2, best, prevnn, acc);
     block_partial<kNacc, kFused>(acc, red, [](int v) { return v; },
                                  partial + ((size_t)slot * nblk + blockIdx.x) * kPartialStride);
     if constexpr (kFused) finish_pass<kEstGICP>(slot, nact, partial, nblk, pc);
@@ -1542,7 +1548,7 @@ __device__ __forceinline__ void p2p_block_terms(int slot, int ablk, const double
 
 template <bool kFused>
 __global__ __launch_bounds__(256) void p2p_accum_kernel(const double* __restrict__ src, int N,
-                                                        const double* __restrict__ tgt64,
+                                                        const TargetDesc* __restrict__ tdesc, TgtBounds tb,
                                                         const int32_t* __restrict__ active,
                                                         const double* __restrict__ Qm,
                                                         const int32_t* __restrict__ done, double r2,
@@ -1555,7 +1561,8 @@ __global__ __launch_bounds__(256) void p2p_accum_kernel(const double* __restrict
     if (done[slot]) return;
     __shared__ double red[4][kP2PTerms];
     double acc[kP2PTerms];
-    p2p_block_terms<false>(slot, blockIdx.x, src, N, tgt64, Qm, r2, best, prevnn, acc);
+    p2p_block_terms<false>(slot, blockIdx.x, src, N, tdesc[target_of_row(tb, blockIdx.y)].xyz64, Qm, r2, best,
+                           prevnn, acc);
     block_partial<kP2PTerms, kFused>(acc, red, p2p_slot,
                                      partial + ((size_t)slot * nblk + blockIdx.x) * kPartialStride);
     if constexpr (kFused) finish_pass<kEstP2P>(slot, nact, partial, nblk, pc);
@@ -1947,18 +1954,56 @@ int search_splits(int nact, int blocks_per_start, int want) {
 int accum_blocks(int64_t N) { return (int)((N + 256 * accum_qpt(N) - 1) / (256 * accum_qpt(N))); }
 
 // the cooperative search needs 16-bit tile ids in its LDS candidate list
-static bool use_coop(const orpcd_ctx* c) { return c->opt.search_kernel == 1 && c->tgt.ntiles <= 65535; }
+static bool use_coop(const orpcd_ctx* c) {
+    return c->opt.search_kernel == 1 && c->tgt.ntiles <= 65535 && c->batch_ntgt == 1;
+}
 // the two-phase search keeps a candidate list of every query group
-static bool use_two_phase(const orpcd_ctx* c) { return c->opt.search_kernel == 2 && c->two_phase_ok; }
+static bool use_two_phase(const orpcd_ctx* c) {
+    return c->opt.search_kernel == 2 && c->two_phase_ok && c->batch_ntgt == 1;
+}
 
-hipError_t launch_xform(const orpcd_ctx* c, int nact, double r2, hipStream_t s, bool dev_nact) {
+hipError_t launch_xform(const orpcd_ctx* c, int nact, double r2, hipStream_t s, bool dev_nact, const TgtBounds& tb) {
     if (use_coop(c) || use_two_phase(c)) return hipSuccess;  // these searches transform their own queries
     const int N = (int)c->src.n;
     xform_queries_kernel<<<dim3((unsigned)((N + 255) / 256), (unsigned)nact), 256, 0, s>>>(
-        c->src.xyz64.p, N, c->active.p, c->Q.p, c->done.p, c->tgt.p4.p, (int)c->tgt.ntiles,
-        seed_stride_for(c->tgt.ntiles, c->opt.seed_reps), c->prevnn.p, search_r2(r2), c->opt.reseed, c->q32.p,
-        c->best.p, dev_nact ? c->ctl.p : nullptr, c->gbox.p, org_of(c->tgt));
+        c->src.xyz64.p, N, c->active.p, c->Q.p, c->done.p, c->tdesc.p, tb, c->prevnn.p, search_r2(r2),
+        c->opt.reseed, c->q32.p, c->best.p, dev_nact ? c->ctl.p : nullptr, c->gbox.p);
     return hipGetLastError();
+}
+
+TgtBounds one_target() {
+    TgtBounds tb{};
+    tb.n = 1;
+    return tb;
+}
+
+TgtBounds target_bounds(const orpcd_ctx* c, const int32_t* act, int nact) {
+    TgtBounds tb{};
+    tb.n = c->batch_ntgt;
+    for (int k = 0; k < tb.n; ++k) {
+        int r = 0;  // act is increasing: the rows whose slot precedes target k + 1's first
+        while (r < nact && act[r] < c->batch_first[k + 1]) ++r;
+        tb.row_end[k] = r;
+    }
+    return tb;
+}
+
+void write_target_desc(const CloudLayout& L, const double* tcov, int seed_reps, TargetDesc& d) {
+    d.p4 = L.p4.p;
+    d.tlo = L.tlo.p;
+    d.thi = L.thi.p;
+    d.qbox = L.qbox.p;
+    d.slo = L.slo.p;
+    d.shi = L.shi.p;
+    d.xyz64 = L.xyz64.p;
+    d.tcov = tcov;
+    d.ntiles = (int)L.ntiles;
+    d.nsuper = (int)L.nsuper;
+    d.seed_stride = seed_stride_for(L.ntiles, seed_reps);
+    d.pad = 0;
+    d.ox = L.org[0];
+    d.oy = L.org[1];
+    d.oz = L.org[2];
 }
 
 static SolveArgs solve_args(const orpcd_ctx* c) {
@@ -1966,7 +2011,9 @@ static SolveArgs solve_args(const orpcd_ctx* c) {
                      c->done.p, c->out_fit.p, c->out_rmse.p, c->out_iters.p, c->out_ncorr.p};
 }
 
-bool pipelined_ok(const orpcd_ctx* c) { return !use_coop(c) && !use_two_phase(c) && c->opt.pipeline; }
+bool pipelined_ok(const orpcd_ctx* c) {
+    return !use_coop(c) && !use_two_phase(c) && c->opt.pipeline && c->batch_ntgt == 1;
+}
 
 // One pipelined pass (see PassCtl): search over the device's running starts,
 // accumulation with the fused solve + compaction, the next pass's queries.
@@ -1981,11 +2028,10 @@ hipError_t launch_gicp_pass_pipelined(const orpcd_ctx* c, int nact_host, int pas
     const int64_t grid = std::max<int64_t>((int64_t)nact_host * sblk * S, (want + kCWaves - 1) / kCWaves);
     hipError_t e;
     auto kern = c->opt.search_occupancy == 6 ? nn_search_kernel_o6 : nn_search_kernel;
-    kern<<<dim3((unsigned)grid), kCBlock, 0, s>>>(c->q32.p, N, c->tgt.p4.p, c->tgt.tlo.p, c->tgt.thi.p, c->tgt.qbox.p,
-                                                  (int)c->tgt.ntiles, c->tgt.slo.p, c->tgt.shi.p, (int)c->tgt.nsuper,
-                                                  c->opt.super_cull, c->active.p, c->done.p, 1, c->best.p,
-                                                  c->count_tiles ? c->counters.p : nullptr, c->ctl.p, sblk, want,
-                                                  c->gbox.p);
+    const TgtBounds tb = one_target();  // pipelined passes: single-target batches only
+    kern<<<dim3((unsigned)grid), kCBlock, 0, s>>>(c->q32.p, N, c->tdesc.p, tb, c->opt.super_cull, c->active.p,
+                                                  c->done.p, 1, c->best.p, c->count_tiles ? c->counters.p : nullptr,
+                                                  c->ctl.p, sblk, want, c->gbox.p);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     if (mid && (e = hipEventRecord(mid, s)) != hipSuccess) return e;
     const int ablk = accum_blocks(N);
@@ -1993,19 +2039,20 @@ hipError_t launch_gicp_pass_pipelined(const orpcd_ctx* c, int nact_host, int pas
                      p.relative_rmse, (int64_t)N, solve_args(c)};
     if (c->est == kEstP2P)
         p2p_accum_kernel<true><<<dim3((unsigned)ablk, (unsigned)nact_host), 256, 0, s>>>(
-            c->src.xyz64.p, N, c->tgt.xyz64.p, c->active.p, c->Q.p, c->done.p, r2, c->best.p, c->prevnn.p,
+            c->src.xyz64.p, N, c->tdesc.p, tb, c->active.p, c->Q.p, c->done.p, r2, c->best.p, c->prevnn.p,
             c->partial.p, ablk, pc);
     else
         gicp_accum_kernel<true><<<dim3((unsigned)ablk, (unsigned)nact_host), 256, 0, s>>>(
-            c->src.xyz64.p, c->scov.p, N, c->tgt.xyz64.p, c->tcov.p, c->active.p, c->Q.p, c->R.p, c->done.p, r2,
-            c->best.p, c->prevnn.p, c->partial.p, ablk, pc);
+            c->src.xyz64.p, c->scov.p, N, c->tdesc.p, tb, c->active.p, c->Q.p, c->R.p, c->done.p, r2, c->best.p,
+            c->prevnn.p, c->partial.p, ablk, pc);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     if (after_accum && (e = hipEventRecord(after_accum, s)) != hipSuccess) return e;
     if (pass >= p.max_iteration) return hipSuccess;  // every start is done after this pass
-    return launch_xform(c, nact_host, r2, s, true);
+    return launch_xform(c, nact_host, r2, s, true, tb);
 }
 
-hipError_t launch_gicp_pass(const orpcd_ctx* c, int nact, int pass, double r2, hipStream_t s, hipEvent_t mid) {
+hipError_t launch_gicp_pass(const orpcd_ctx* c, int nact, int pass, double r2, hipStream_t s, hipEvent_t mid,
+                            const TgtBounds& tb) {
     const int N = (int)c->src.n;
     const int sblk = (N + kCBlockQ - 1) / kCBlockQ;
     hipError_t e;
@@ -2048,8 +2095,7 @@ hipError_t launch_gicp_pass(const orpcd_ctx* c, int nact, int pass, double r2, h
     // best[] was reset to kNone by xform_queries_kernel
     auto kern = c->opt.search_occupancy == 6 ? nn_search_kernel_o6 : nn_search_kernel;
     kern<<<dim3((unsigned)(sblk * S), (unsigned)nact), kCBlock, 0, s>>>(
-        c->q32.p, N, c->tgt.p4.p, c->tgt.tlo.p, c->tgt.thi.p, c->tgt.qbox.p, (int)c->tgt.ntiles, c->tgt.slo.p, c->tgt.shi.p,
-        (int)c->tgt.nsuper, c->opt.super_cull, c->active.p, c->done.p, S, c->best.p,
+        c->q32.p, N, c->tdesc.p, tb, c->opt.super_cull, c->active.p, c->done.p, S, c->best.p,
         c->count_tiles ? c->counters.p : nullptr, nullptr, sblk, want, c->gbox.p);
     }
     if ((e = hipGetLastError()) != hipSuccess) return e;
@@ -2057,17 +2103,18 @@ hipError_t launch_gicp_pass(const orpcd_ctx* c, int nact, int pass, double r2, h
     const int ablk = accum_blocks(N);
     if (c->est == kEstP2P) {
         p2p_accum_kernel<false><<<dim3((unsigned)ablk, (unsigned)nact), 256, 0, s>>>(
-            c->src.xyz64.p, N, c->tgt.xyz64.p, c->active.p, c->Q.p, c->done.p, r2, c->best.p, c->prevnn.p,
+            c->src.xyz64.p, N, c->tdesc.p, tb, c->active.p, c->Q.p, c->done.p, r2, c->best.p, c->prevnn.p,
             c->partial.p, ablk, PassCtl{});
         return hipGetLastError();
     }
     gicp_accum_kernel<false><<<dim3((unsigned)ablk, (unsigned)nact), 256, 0, s>>>(
-        c->src.xyz64.p, c->scov.p, N, c->tgt.xyz64.p, c->tcov.p, c->active.p, c->Q.p, c->R.p, c->done.p, r2,
-        c->best.p, c->prevnn.p, c->partial.p, ablk, PassCtl{});
+        c->src.xyz64.p, c->scov.p, N, c->tdesc.p, tb, c->active.p, c->Q.p, c->R.p, c->done.p, r2, c->best.p,
+        c->prevnn.p, c->partial.p, ablk, PassCtl{});
     return hipGetLastError();
 }
 
-hipError_t launch_gicp_solve(const orpcd_ctx* c, int nact, int pass, const orpcd_gicp_params& p, hipStream_t s) {
+hipError_t launch_gicp_solve(const orpcd_ctx* c, int nact, int pass, const orpcd_gicp_params& p, hipStream_t s,
+                             const TgtBounds& tb) {
     const SolveArgs a = solve_args(c);
     auto solve = c->est == kEstP2P ? icp_solve_kernel<1> : icp_solve_kernel<0>;
     solve<<<(unsigned)nact, 64, 0, s>>>(c->active.p, c->partial.p, accum_blocks(c->src.n), nullptr,
@@ -2076,7 +2123,7 @@ hipError_t launch_gicp_solve(const orpcd_ctx* c, int nact, int pass, const orpcd
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     const double r2 = p.max_correspondence_distance * p.max_correspondence_distance;
-    return launch_xform(c, nact, r2, s, false);  // queries of the next pass (done starts skip)
+    return launch_xform(c, nact, r2, s, false, tb);  // queries of the next pass (done starts skip)
 }
 
 // Resident 256-thread workgroups of the persistent kernel on this device.
@@ -2159,7 +2206,7 @@ hipError_t launch_gicp_solve_sums(const orpcd_ctx* c, const double* sums29, int6
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     const double r2 = p.max_correspondence_distance * p.max_correspondence_distance;
-    return launch_xform(c, 1, r2, s, false);
+    return launch_xform(c, 1, r2, s, false, one_target());
 }
 
 hipError_t launch_nn1(const double* q, int64_t nq, const CloudLayout& t, double r2, int32_t* idx, double* d2,

@@ -160,6 +160,38 @@ struct KernelStats {
     double launches = 0, ms = 0, pairs = 0, iterations = 0, passes = 0, tiles = 0, accum_ms = 0;
 };
 
+// ------------------------------------------------- several targets per batch
+// A batch may hold starts against up to kMaxTargets targets (the six scale
+// candidates of one speculative compass iteration, Aligner.py:263-298, run
+// as ONE device batch).  The starts of a batch are ordered by target (slots
+// [first[k], first[k+1]) use target k); since the running-start list keeps
+// that order when it is compacted, a launch learns a block's target from the
+// block's row `by` and per-launch row bounds passed by value (TgtBounds), with
+// no memory load; the target's device pointers come from a TargetDesc array
+// in device memory, static while the batch runs.
+constexpr int kMaxTargets = 8;
+
+struct TargetDesc {
+    const float4 *p4, *tlo, *thi, *qbox, *slo, *shi;  // fp32 search layout (CloudLayout)
+    const double *xyz64, *tcov;                        // fp64 points and GICP covariances (Morton order)
+    int ntiles, nsuper, seed_stride, pad;
+    double ox, oy, oz;                                 // fp32 frame origin (CloudLayout::org)
+};
+
+struct TgtBounds {
+    int row_end[kMaxTargets];  // launch rows [row_end[k-1], row_end[k]) run against target k
+    int n;                     // targets in the batch (1: every row is target 0)
+};
+
+// target of launch row `by` (scalar compares over kernel-argument bounds)
+__host__ __device__ __forceinline__ int target_of_row(const TgtBounds& tb, int by) {
+    int k = 0;
+#pragma unroll
+    for (int i = 0; i < kMaxTargets - 1; ++i)
+        if (i + 1 < tb.n && by >= tb.row_end[i]) k = i + 1;
+    return k;
+}
+
 }  // namespace orpcd
 
 struct orpcd_ctx {
@@ -167,11 +199,18 @@ struct orpcd_ctx {
     hipStream_t stream = nullptr;
     std::string err;
 
-    // target (set per scale candidate), Morton order
-    orpcd::CloudLayout tgt;
-    orpcd::DevBuf<double> tcov;     // M*6 GICP covariance (Morton order)
-    double tgt_eps = -1.0;
-    std::vector<double> tgt_host;   // input-order copy (epsilon re-derivation)
+    // targets (set per scale candidate), Morton order; target 0 is `tgt`
+    orpcd::CloudLayout tgts[orpcd::kMaxTargets];
+    orpcd::DevBuf<double> tcovs[orpcd::kMaxTargets];  // M*6 GICP covariance (Morton order)
+    double tgt_eps[orpcd::kMaxTargets] = {-1.0, -1.0, -1.0, -1.0, -1.0, -1.0, -1.0, -1.0};
+    std::vector<double> tgt_host[orpcd::kMaxTargets];  // input-order copies (epsilon re-derivation)
+    int ntgt = 0;                                      // targets set (orpcd_set_target: 1)
+    orpcd::CloudLayout& tgt = tgts[0];
+    orpcd::DevBuf<double>& tcov = tcovs[0];
+    orpcd::DevBuf<orpcd::TargetDesc> tdesc;  // kMaxTargets device descriptors of the targets
+    orpcd::TargetDesc tdesc_h[orpcd::kMaxTargets] = {};  // their host copies (staging of the uploads)
+    int batch_ntgt = 1;                      // targets of the running batch
+    int batch_first[orpcd::kMaxTargets + 1] = {0};  // its slots [first[k], first[k+1]) use target k
 
     // source (set per align), Morton order
     orpcd::CloudLayout src;
@@ -316,12 +355,18 @@ hipError_t launch_fps(const double* xyz, int64_t n, int first, int k, int max_bl
 
 // gicp_kernels.hip
 int accum_blocks(int64_t N);
-hipError_t launch_xform(const orpcd_ctx* c, int nact, double r2, hipStream_t s, bool dev_nact = false);
+hipError_t launch_xform(const orpcd_ctx* c, int nact, double r2, hipStream_t s, bool dev_nact, const TgtBounds& tb);
+TgtBounds one_target();
+// bounds of the launch rows act[0..nact) (increasing slots) over the batch's targets
+TgtBounds target_bounds(const orpcd_ctx* c, const int32_t* act, int nact);
+void write_target_desc(const CloudLayout& L, const double* tcov, int seed_reps, TargetDesc& d);
 bool pipelined_ok(const orpcd_ctx* c);
 hipError_t launch_gicp_pass_pipelined(const orpcd_ctx* c, int nact_host, int pass, const orpcd_gicp_params& p,
                                       hipStream_t s, hipEvent_t mid, hipEvent_t after_accum);
-hipError_t launch_gicp_pass(const orpcd_ctx* c, int nact, int pass, double r2, hipStream_t s, hipEvent_t mid);
-hipError_t launch_gicp_solve(const orpcd_ctx* c, int nact, int pass, const orpcd_gicp_params& p, hipStream_t s);
+hipError_t launch_gicp_pass(const orpcd_ctx* c, int nact, int pass, double r2, hipStream_t s, hipEvent_t mid,
+                            const TgtBounds& tb);
+hipError_t launch_gicp_solve(const orpcd_ctx* c, int nact, int pass, const orpcd_gicp_params& p, hipStream_t s,
+                             const TgtBounds& tb);
 hipError_t launch_reduce_partials(const orpcd_ctx* c, int slot, double* sums29, hipStream_t s);
 hipError_t launch_gicp_solve_sums(const orpcd_ctx* c, const double* sums29, int64_t n_total, int pass,
                                   const orpcd_gicp_params& p, hipStream_t s);

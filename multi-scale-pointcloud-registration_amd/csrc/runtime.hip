@@ -84,20 +84,40 @@ int upload_layout(orpcd_ctx* c, const double* xyz, int64_t n, CloudLayout& L, bo
     return layout_from_device(c, xyz, c->scratch64a.p, n, L, tiles, margin);
 }
 
-// Target: Morton layout + tiles + GICP covariances (KNN-20 normals).
-int upload_target(orpcd_ctx* c, const double* xyz, int64_t m, double eps) {
+// Target k: Morton layout + tiles + GICP covariances (KNN-20 normals), and
+// its device descriptor (TargetDesc, read by the kernels of every batch).
+int upload_target_k(orpcd_ctx* c, int k, const double* xyz, int64_t m, double eps) {
     double margin = 0.0;
-    int rc = upload_layout(c, xyz, m, c->tgt, true, &margin);
+    int rc = upload_layout(c, xyz, m, c->tgts[k], true, &margin);
     if (rc) return rc;
-    CTX_CHECK(c, c->tcov.ensure((size_t)m * 6));
+    CTX_CHECK(c, c->tcovs[k].ensure((size_t)m * 6));
     CTX_CHECK(c, c->scratch64b.ensure((size_t)m * 6));
     if (eps >= 0.0) {
-        CTX_CHECK(c, launch_knn_tiles(c->tgt, c->scratch64a.p, 20, -1.0, margin, false, c->scratch64b.p, nullptr,
+        CTX_CHECK(c, launch_knn_tiles(c->tgts[k], c->scratch64a.p, 20, -1.0, margin, false, c->scratch64b.p, nullptr,
                                       nullptr, nullptr, c->stream));
-        CTX_CHECK(c, launch_normals_cov(c->scratch64b.p, m, nullptr, 1, eps, nullptr, c->tcov.p, c->stream));
+        CTX_CHECK(c, launch_normals_cov(c->scratch64b.p, m, nullptr, 1, eps, nullptr, c->tcovs[k].p, c->stream));
     }
-    c->tgt_eps = eps;
-    c->tgt_host.assign(xyz, xyz + 3 * m);
+    c->tgt_eps[k] = eps;
+    c->tgt_host[k].assign(xyz, xyz + 3 * m);
+    CTX_CHECK(c, c->tdesc.ensure(kMaxTargets));
+    write_target_desc(c->tgts[k], c->tcovs[k].p, c->opt.seed_reps, c->tdesc_h[k]);
+    CTX_CHECK(c, hipMemcpyAsync(c->tdesc.p + k, &c->tdesc_h[k], sizeof(TargetDesc), hipMemcpyHostToDevice,
+                                c->stream));
+    return ORPCD_OK;
+}
+
+int upload_target(orpcd_ctx* c, const double* xyz, int64_t m, double eps) {
+    return upload_target_k(c, 0, xyz, m, eps);
+}
+
+// every target of the batch with covariances for `eps` (they depend on it)
+int targets_for_epsilon(orpcd_ctx* c, int ntgt, double eps) {
+    for (int k = 0; k < ntgt; ++k) {
+        if (c->tgt_eps[k] == eps) continue;
+        std::vector<double> host = c->tgt_host[k];
+        int rc = upload_target_k(c, k, host.data(), c->tgts[k].n, eps);
+        if (rc) return rc;
+    }
     return ORPCD_OK;
 }
 
@@ -440,7 +460,8 @@ int batch_setup(orpcd_ctx* c, const double* R0, const double* t0, int B, const o
     c->est = init16 ? kEstP2P : kEstGICP;
     if (!init16) CTX_CHECK(c, launch_normals_cov(c->sraw.p, N, c->scratch64c.p, B, p->epsilon, nullptr, c->scov.p, s));
     if (!persist) {
-        CTX_CHECK(c, launch_xform(c, B, p->max_correspondence_distance * p->max_correspondence_distance, s));
+        CTX_CHECK(c, launch_xform(c, B, p->max_correspondence_distance * p->max_correspondence_distance, s, false,
+                                  target_bounds(c, hAct, B)));
         return ORPCD_OK;
     }
     // persistent loop: pass 0 of every start open, tickets zero, best[] = kNone
@@ -515,10 +536,14 @@ int orpcd_ctx_destroy(orpcd_ctx* c) {
     if (!c) return ORPCD_EINVAL;
     (void)hipSetDevice(c->device);
     (void)hipStreamSynchronize(c->stream);
-    c->tgt.release();
+    for (int k = 0; k < kMaxTargets; ++k) {
+        c->tgts[k].release();
+        c->tcovs[k].release();
+    }
+    c->tdesc.release();
     c->src.release();
     c->aux.release();
-    for (auto* b : {&c->tcov, &c->sraw, &c->scov, &c->G, &c->T, &c->Q, &c->R, &c->prev, &c->partial, &c->out_fit,
+    for (auto* b : {&c->sraw, &c->scov, &c->G, &c->T, &c->Q, &c->R, &c->prev, &c->partial, &c->out_fit,
                     &c->out_rmse, &c->scratch64a, &c->scratch64b, &c->scratch64c})
         b->release();
     c->prevnn.release();
@@ -558,9 +583,34 @@ int orpcd_set_target(orpcd_ctx* c, const double* xyz, int64_t m, double epsilon)
     CTX_REQUIRE(c, m < kMaxPoints, "set_target: too many points");
     CTX_REQUIRE(c, finite_cloud(xyz, m), "set_target: non-finite coordinates");
     CTX_CHECK(c, hipSetDevice(c->device));
+    c->ntgt = 0;
     int rc = upload_target(c, xyz, m, epsilon);
     if (rc) return rc;
     CTX_CHECK(c, hipStreamSynchronize(c->stream));
+    c->ntgt = 1;
+    return ORPCD_OK;
+}
+
+int orpcd_set_targets(orpcd_ctx* c, const double* xyz, const int64_t* m, int32_t ntargets, double epsilon) {
+    if (!c) return ORPCD_EINVAL;
+    CTX_REQUIRE(c, xyz && m, "set_targets: null argument");
+    CTX_REQUIRE(c, ntargets >= 1 && ntargets <= kMaxTargets, "set_targets: 1 to 8 targets");
+    int64_t off = 0;
+    for (int k = 0; k < ntargets; ++k) {
+        CTX_REQUIRE(c, m[k] > 0 && m[k] < kMaxPoints, "set_targets: empty target cloud or too many points");
+        CTX_REQUIRE(c, finite_cloud(xyz + 3 * off, m[k]), "set_targets: non-finite coordinates");
+        off += m[k];
+    }
+    CTX_CHECK(c, hipSetDevice(c->device));
+    c->ntgt = 0;
+    off = 0;
+    for (int k = 0; k < ntargets; ++k) {
+        int rc = upload_target_k(c, k, xyz + 3 * off, m[k], epsilon);
+        if (rc) return rc;
+        off += m[k];
+    }
+    CTX_CHECK(c, hipStreamSynchronize(c->stream));
+    c->ntgt = ntargets;
     return ORPCD_OK;
 }
 
@@ -584,26 +634,70 @@ int orpcd_set_source(orpcd_ctx* c, const double* xyz, int64_t n) {
 
 int orpcd_gicp_batch(orpcd_ctx* c, const double* R0, const double* t0, int32_t B, const orpcd_gicp_params* p,
                      double* T_out, double* rmse_out, double* fitness_out, int32_t* iters_out, int64_t* ncorr_out) {
+    return orpcd_gicp_batch_targets(c, R0, t0, nullptr, B, p, T_out, rmse_out, fitness_out, iters_out, ncorr_out);
+}
+
+int orpcd_gicp_batch_targets(orpcd_ctx* c, const double* R0, const double* t0, const int32_t* target_of_start,
+                             int32_t B, const orpcd_gicp_params* p, double* T_out, double* rmse_out,
+                             double* fitness_out, int32_t* iters_out, int64_t* ncorr_out) {
     if (!c) return ORPCD_EINVAL;
     CTX_REQUIRE(c, R0 && t0 && p && T_out && rmse_out, "gicp_batch: null argument");
     CTX_REQUIRE(c, B > 0, "gicp_batch: B must be > 0");
     CTX_REQUIRE(c, c->src.n > 0, "gicp_batch: no source (call orpcd_set_source)");
-    CTX_REQUIRE(c, c->tgt.n > 0, "gicp_batch: no target (call orpcd_set_target)");
+    CTX_REQUIRE(c, c->ntgt > 0 && c->tgt.n > 0, "gicp_batch: no target (call orpcd_set_target)");
     CTX_REQUIRE(c, p->max_correspondence_distance > 0, "gicp_batch: max_correspondence_distance must be > 0");
     CTX_REQUIRE(c, p->max_iteration >= 0, "gicp_batch: max_iteration must be >= 0");
     CTX_REQUIRE(c, p->epsilon >= 0, "gicp_batch: epsilon must be >= 0");
-    CTX_CHECK(c, hipSetDevice(c->device));
-    if (c->tgt_eps != p->epsilon) {  // target covariances depend on epsilon
-        std::vector<double> host = c->tgt_host;
-        int rc = upload_target(c, host.data(), c->tgt.n, p->epsilon);
-        if (rc) return rc;
-    }
     CTX_REQUIRE(c, c->src_cov, "gicp_batch: the source has no covariances (set it with orpcd_set_source)");
-    const bool persist = persistent_ok(c);
-    int rc = batch_setup(c, R0, t0, B, p, nullptr, persist);
+    // slots ordered by target (stable): start b runs in slot pos[b]
+    int first[kMaxTargets + 1] = {0};
+    std::vector<int> pos((size_t)B);
+    int ntg = 1;
+    if (target_of_start) {
+        for (int b = 0; b < B; ++b)
+            CTX_REQUIRE(c, target_of_start[b] >= 0 && target_of_start[b] < c->ntgt,
+                        "gicp_batch_targets: target index out of range (orpcd_set_targets)");
+        ntg = c->ntgt;
+        int cnt[kMaxTargets] = {0};
+        for (int b = 0; b < B; ++b) ++cnt[target_of_start[b]];
+        for (int k = 0; k < ntg; ++k) first[k + 1] = first[k] + cnt[k];
+        int fill[kMaxTargets];
+        for (int k = 0; k < ntg; ++k) fill[k] = first[k];
+        for (int b = 0; b < B; ++b) pos[b] = fill[target_of_start[b]]++;
+    } else {
+        first[1] = B;
+        for (int b = 0; b < B; ++b) pos[b] = b;
+    }
+    CTX_CHECK(c, hipSetDevice(c->device));
+    int rc = targets_for_epsilon(c, ntg, p->epsilon);  // target covariances depend on epsilon
     if (rc) return rc;
-    if (persist) return run_passes_persistent(c, B, p, T_out, rmse_out, fitness_out, iters_out, ncorr_out);
-    return run_passes(c, B, p, T_out, rmse_out, fitness_out, iters_out, ncorr_out);
+    c->batch_ntgt = ntg;
+    for (int k = 0; k <= ntg; ++k) c->batch_first[k] = first[k];
+    std::vector<double> sR((size_t)B * 9), st((size_t)B * 3);
+    for (int b = 0; b < B; ++b) {
+        std::memcpy(&sR[(size_t)pos[b] * 9], R0 + 9 * b, 9 * sizeof(double));
+        std::memcpy(&st[(size_t)pos[b] * 3], t0 + 3 * b, 3 * sizeof(double));
+    }
+    const bool persist = ntg == 1 && persistent_ok(c);
+    rc = batch_setup(c, sR.data(), st.data(), B, p, nullptr, persist);
+    if (rc) return rc;
+    std::vector<double> oT((size_t)B * 16), orm((size_t)B), ofit((size_t)B);
+    std::vector<int32_t> oit((size_t)B);
+    std::vector<int64_t> onc((size_t)B);
+    rc = persist ? run_passes_persistent(c, B, p, oT.data(), orm.data(), ofit.data(), oit.data(), onc.data())
+                 : run_passes(c, B, p, oT.data(), orm.data(), ofit.data(), oit.data(), onc.data());
+    c->batch_ntgt = 1;
+    c->batch_first[1] = 0;
+    if (rc) return rc;
+    for (int b = 0; b < B; ++b) {
+        const int q = pos[b];
+        std::memcpy(T_out + 16 * b, &oT[(size_t)q * 16], 16 * sizeof(double));
+        rmse_out[b] = orm[q];
+        if (fitness_out) fitness_out[b] = ofit[q];
+        if (iters_out) iters_out[b] = oit[q];
+        if (ncorr_out) ncorr_out[b] = onc[q];
+    }
+    return ORPCD_OK;
 }
 
 int orpcd_set_source_points(orpcd_ctx* c, const double* xyz, int64_t n) {
@@ -864,9 +958,10 @@ int run_passes(orpcd_ctx* c, int B, const orpcd_gicp_params* p, double* T_out, d
     for (int pass = 0; pass <= p->max_iteration && nact > 0; ++pass) {
         hipEvent_t* ev = timed ? &c->ev_pool[3 * pending] : nullptr;
         if (timed) CTX_CHECK(c, hipEventRecord(ev[0], s));
-        CTX_CHECK(c, launch_gicp_pass(c, nact, pass, r2, s, timed ? ev[1] : nullptr));
+        const TgtBounds tb = target_bounds(c, hAct, nact);
+        CTX_CHECK(c, launch_gicp_pass(c, nact, pass, r2, s, timed ? ev[1] : nullptr, tb));
         if (trace) CTX_CHECK(c, hipEventRecord(ev[2], s));  // accumulation time: traced runs only
-        CTX_CHECK(c, launch_gicp_solve(c, nact, pass, *p, s));
+        CTX_CHECK(c, launch_gicp_solve(c, nact, pass, *p, s, tb));
         ++pending;
         c->stats.passes += nact;
         // the host learns which starts finished only every few passes; a
@@ -1069,12 +1164,10 @@ int orpcd_gicp_shard_begin(orpcd_ctx* c, const double* R0, const double* t0, con
     CTX_REQUIRE(c, p->max_correspondence_distance > 0 && p->max_iteration >= 0 && p->epsilon >= 0,
                 "gicp_shard_begin: bad parameters");
     CTX_CHECK(c, hipSetDevice(c->device));
-    if (c->tgt_eps != p->epsilon) {
-        std::vector<double> host = c->tgt_host;
-        int rc = upload_target(c, host.data(), c->tgt.n, p->epsilon);
-        if (rc) return rc;
-    }
-    int rc = batch_setup(c, R0, t0, 1, p);
+    int rc = targets_for_epsilon(c, 1, p->epsilon);
+    if (rc) return rc;
+    c->batch_ntgt = 1;
+    rc = batch_setup(c, R0, t0, 1, p);
     if (rc) return rc;
     CTX_CHECK(c, c->scratch64c.ensure(kNacc));
     c->shard.begun = true;
@@ -1107,7 +1200,8 @@ int orpcd_gicp_shard_pass(orpcd_ctx* c, double* sums_out, int32_t* active) {
         CTX_CHECK(c, read_counters(c, tiles0, unused, false));
         CTX_CHECK(c, hipEventRecord(c->ev_pool[0], c->stream));
     }
-    CTX_CHECK(c, launch_gicp_pass(c, 1, c->shard.pass, r2, c->stream, timed ? c->ev_pool[1] : nullptr));
+    CTX_CHECK(c, launch_gicp_pass(c, 1, c->shard.pass, r2, c->stream, timed ? c->ev_pool[1] : nullptr,
+                                  one_target()));
     if (timed) CTX_CHECK(c, hipEventRecord(c->ev_pool[2], c->stream));
     CTX_CHECK(c, launch_reduce_partials(c, 0, c->scratch64c.p, c->stream));
     CTX_CHECK(c, hipMemcpyAsync(sums_out, c->scratch64c.p, kNacc * 8, hipMemcpyDeviceToHost, c->stream));

@@ -127,15 +127,60 @@ class Aligner:
         T[:3, 3] = np.dot(t0, Tc[:3, :3]).ravel() + Tc[:3, 3]
         return T
 
+    def _draw_block(self, n: int):
+        """n consecutive initialize_rotation() draws (Aligner.py:125-162), bit for
+        bit: the same scalar np.random calls in the same order (three uniform,
+        then randn(3), per attempt) and the same translation expression; the
+        cos / sin of all 3n angles by one ufunc call each and the n products
+        r_1 (r_2 r_3) by one stacked matmul, which give the scalar calls' and
+        np.dot's values (checked against the sequential draws in
+        tests/test_host.py::test_draw_block_matches_initialize_rotation)."""
+        deg, uni, randn = self._deg, np.random.uniform, np.random.randn
+        th = np.empty((n, 3))
+        t0s = []
+        for k in range(n):
+            th[k, 0] = uni(low=-deg, high=deg)
+            th[k, 1] = uni(low=-deg, high=deg)
+            th[k, 2] = uni(low=-deg, high=deg)
+            t0s.append(self._mu + randn(3) * self._std)
+        c, s = np.cos(th), np.sin(th)
+        r = np.zeros((3, n, 3, 3))
+        r[0, :, 0, 0] = 1.0
+        r[0, :, 1, 1], r[0, :, 1, 2], r[0, :, 2, 1], r[0, :, 2, 2] = c[:, 0], -s[:, 0], s[:, 0], c[:, 0]
+        r[1, :, 1, 1] = 1.0
+        r[1, :, 0, 0], r[1, :, 0, 2], r[1, :, 2, 0], r[1, :, 2, 2] = c[:, 1], s[:, 1], -s[:, 1], c[:, 1]
+        r[2, :, 2, 2] = 1.0
+        r[2, :, 0, 0], r[2, :, 0, 1], r[2, :, 1, 0], r[2, :, 1, 1] = c[:, 2], -s[:, 2], s[:, 2], c[:, 2]
+        R = np.matmul(r[0], np.matmul(r[1], r[2]))
+        return list(R), t0s
+
+    class _BlockStates:
+        """The RNG state after attempt n of a drawn block, rebuilt on demand:
+        [-1] is the state after the whole block (kept); any other n (needed only
+        when attempt n fails, Aligner.py:188-190 raising inside optimize) is
+        reached by replaying the block's first n + 1 draws from the state before
+        it.  One get_state per block instead of one per attempt (~60 us each)."""
+
+        def __init__(self, aligner, before, after, n):
+            self._al, self._before, self._after, self._n = aligner, before, after, n
+
+        def __getitem__(self, k):
+            k = k + self._n if k < 0 else k
+            if k == self._n - 1:
+                return self._after
+            cur = np.random.get_state()
+            np.random.set_state(self._before)
+            for _ in range(k + 1):
+                self._al.initialize_rotation()
+            st = np.random.get_state()
+            np.random.set_state(cur)
+            return st
+
     def _draw_starts(self):
         """The attempts' (R0, t0) in the reference's order, and the RNG state after each."""
-        R0s, t0s, states = [], [], []
-        for _ in range(self._attempts):  # same draws, same order as the sequential loop
-            R, t = self.initialize_rotation()
-            R0s.append(R)
-            t0s.append(t)
-            states.append(np.random.get_state())
-        return R0s, t0s, states
+        before = np.random.get_state()
+        R0s, t0s = self._draw_block(self._attempts)  # same draws, same order as the sequential loop
+        return R0s, t0s, Aligner._BlockStates(self, before, np.random.get_state(), self._attempts)
 
     def _run_tables(self, source, targets, draws):
         """Per target k, the gathered per-attempt table of the starts draws[k]:

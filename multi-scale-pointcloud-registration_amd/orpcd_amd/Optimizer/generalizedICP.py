@@ -56,8 +56,6 @@ class GeneralizedICP(IOptimizer):
         self._relative_rmse = float(relative_rmse)
         self._device = device
         self._ctx = None
-        self._pool = []          # device contexts of optimize_batch_multi (the first is self.context)
-        self._executor = None
         self.last_result = None
 
     # the device context is created lazily (so the object can be built on a
@@ -104,41 +102,30 @@ class GeneralizedICP(IOptimizer):
         return r
 
     def optimize_batch_multi(self, source: np.ndarray, targets, R0s, t0s) -> list:
-        """``optimize_batch`` for several targets at once: batch k runs on its
-        own device context (own stream) from its own host thread, so the
-        batches execute concurrently on the GPU (the speculative compass of
-        ``Aligner``).  Returns the per-target result dicts."""
-        from concurrent.futures import ThreadPoolExecutor
-
-        n = len(targets)
-        while len(self._pool) < n:
-            self._pool.append(self.context if not self._pool else _native.Context(self.context.device))
-        # the concurrent batches share the GPU: each splits its search over a
-        # share of the waves one batch alone would use
-        waves = max(4096, self.search_waves // n)
-        for ctx in self._pool[:n]:
-            ctx.set_option("search_waves", waves)
-        if self._executor is None or self._executor._max_workers < n:
-            self._executor = ThreadPoolExecutor(max_workers=n)
-
-        def run(k):
-            ctx = self._pool[k]
-            ctx.set_target(targets[k], self._epsilon)
+        """``optimize_batch`` for several targets at once (the speculative
+        compass of ``Aligner``): up to 8 targets run as ONE device batch
+        (orpcd_set_targets + orpcd_gicp_batch_targets), start (k, b) being
+        ``source @ R0s[k][b] + t0s[k][b]`` against ``targets[k]``; more targets
+        run in groups of 8.  Returns the per-target result dicts."""
+        ctx = self.context
+        out = []
+        for g in range(0, len(targets), 8):
+            tg, Rg, tg0 = targets[g:g + 8], R0s[g:g + 8], t0s[g:g + 8]
+            ctx.set_targets(tg, self._epsilon)
             ctx.set_source(source)
-            r = ctx.gicp_batch(R0s[k], t0s[k], **self._params())
+            sizes = [len(r) for r in Rg]
+            tids = np.repeat(np.arange(len(tg), dtype=np.int32), sizes)
+            r = ctx.gicp_batch_targets(np.concatenate([np.asarray(x).reshape(-1, 3, 3) for x in Rg]),
+                                       np.concatenate([np.asarray(x).reshape(-1, 3) for x in tg0]), tids,
+                                       **self._params())
             T = r["T"].copy()
             T[:, :3, :3] = np.transpose(T[:, :3, :3], (0, 2, 1))
-            r["T"] = T
-            return r
-
-        try:
-            out = list(self._executor.map(run, range(n)))  # ctypes releases the GIL during each call
-        finally:
-            self.context.set_option("search_waves", self.search_waves)  # single batches: the full target
+            lo = 0
+            for n in sizes:
+                out.append({k: (T if k == "T" else v)[lo:lo + n] for k, v in r.items()})
+                lo += n
         self.last_result = out[-1]
         return out
-
-    search_waves = 32768  # split target of one batch alone (orpcd_set_option "search_waves" default)
 
     zero_rmse_message = _ZERO_RMSE_MSG
 

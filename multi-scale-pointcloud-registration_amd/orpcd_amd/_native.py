@@ -59,7 +59,7 @@ EXPORTED = ("orpcd_abi_version", "orpcd_device_count", "orpcd_ctx_create", "orpc
             "orpcd_nn1_radius", "orpcd_estimate_normals", "orpcd_fpfh", "orpcd_fpfh_from_normals", "orpcd_fgr", "orpcd_feature_nn",
             "orpcd_fgr_optimize", "orpcd_set_source_points", "orpcd_icp_p2p_batch",
             "orpcd_sor", "orpcd_voxel_down_sample", "orpcd_farthest_downsample",
-            "orpcd_set_option",
+            "orpcd_set_option", "orpcd_set_targets", "orpcd_gicp_batch_targets",
             "orpcd_profiling", "orpcd_stats", "orpcd_reset_stats")
 
 
@@ -85,6 +85,9 @@ def load_library():
         L.orpcd_set_source.argtypes = [vp, _f64p, c_i64]
         L.orpcd_gicp_batch.argtypes = [vp, _f64p, _f64p, ctypes.c_int32, ctypes.POINTER(GicpParams), _f64p, _f64p,
                                        _f64p, _i32p, _i64p]
+        L.orpcd_set_targets.argtypes = [vp, _f64p, _i64p, ctypes.c_int32, c_dbl]
+        L.orpcd_gicp_batch_targets.argtypes = [vp, _f64p, _f64p, _i32p, ctypes.c_int32, ctypes.POINTER(GicpParams),
+                                               _f64p, _f64p, _f64p, _i32p, _i64p]
         L.orpcd_set_source_rows.argtypes = [vp, _f64p, c_i64, c_i64, c_i64]
         L.orpcd_gicp_shard_begin.argtypes = [vp, _f64p, _f64p, ctypes.POINTER(GicpParams), c_i64]
         L.orpcd_gicp_shard_pass.argtypes = [vp, _f64p, _i32p]
@@ -183,6 +186,18 @@ class Context:
         self._check(self._L.orpcd_set_target(self._h, xyz, len(xyz), float(epsilon)), "orpcd_set_target")
         self._target_key = key
 
+    def set_targets(self, targets, epsilon: float = 1e-3, cache: bool = True):
+        """Up to 8 targets for gicp_batch_targets (target k = targets[k])."""
+        ts = [_c3(t) for t in targets]
+        key = (tuple(self._key(t) for t in ts), float(epsilon), "multi")
+        if cache and key == self._target_key:
+            return
+        self._target_key = None
+        m = np.array([len(t) for t in ts], np.int64)
+        xyz = np.ascontiguousarray(np.concatenate(ts, axis=0))
+        self._check(self._L.orpcd_set_targets(self._h, xyz, m, len(ts), float(epsilon)), "orpcd_set_targets")
+        self._target_key = key if len(ts) > 1 else (self._key(ts[0]), float(epsilon))
+
     def set_target_points(self, xyz: np.ndarray, cache: bool = True):
         """The target's search layout (covariances skipped) for PointToPoint ICP."""
         xyz = _c3(xyz)
@@ -224,6 +239,24 @@ class Context:
         ncorr = np.zeros(B, np.int64)
         self._check(self._L.orpcd_gicp_batch(self._h, R0.reshape(-1), t0.reshape(-1), B, ctypes.byref(p),
                                              T.reshape(-1), rmse, fit, iters, ncorr), "orpcd_gicp_batch")
+        return dict(T=T, rmse=rmse, fitness=fit, iters=iters, ncorr=ncorr)
+
+    def gicp_batch_targets(self, R0: np.ndarray, t0: np.ndarray, target_of_start, max_correspondence_distance=0.5,
+                           max_iteration=100, relative_fitness=1e-6, relative_rmse=1e-6, epsilon=1e-3) -> dict:
+        """gicp_batch with start b against target target_of_start[b] (set_targets)."""
+        R0 = np.ascontiguousarray(R0, dtype=np.float64).reshape(-1, 3, 3)
+        B = R0.shape[0]
+        t0 = np.ascontiguousarray(t0, dtype=np.float64).reshape(B, 3)
+        tids = np.ascontiguousarray(target_of_start, dtype=np.int32).reshape(B)
+        p = GicpParams(float(max_correspondence_distance), int(max_iteration), float(relative_fitness),
+                       float(relative_rmse), float(epsilon))
+        T = np.zeros((B, 4, 4))
+        rmse, fit = np.zeros(B), np.zeros(B)
+        iters = np.zeros(B, np.int32)
+        ncorr = np.zeros(B, np.int64)
+        self._check(self._L.orpcd_gicp_batch_targets(self._h, R0.reshape(-1), t0.reshape(-1), tids, B,
+                                                     ctypes.byref(p), T.reshape(-1), rmse, fit, iters, ncorr),
+                    "orpcd_gicp_batch_targets")
         return dict(T=T, rmse=rmse, fitness=fit, iters=iters, ncorr=ncorr)
 
     def icp_p2p_batch(self, init: np.ndarray, max_correspondence_distance=0.5, max_iteration=200,

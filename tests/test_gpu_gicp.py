@@ -434,3 +434,47 @@ def test_gicp_full_c5_size_two_passes_match_oracle(ctx, oracle):
     r = ctx.gicp_batch(np.eye(3)[None], np.zeros((1, 3)), max_iteration=2)
     o = oracle.gicp(s, t, 0.5, 2)
     _cmp_gicp(dict(T=r["T"][0], rmse=r["rmse"][0], fitness=r["fitness"][0], iters=r["iters"][0]), o, 0)
+
+
+def test_multi_target_batch_matches_single_target_batches(ctx):
+    """orpcd_set_targets + orpcd_gicp_batch_targets (the six scale candidates
+    of a speculative compass iteration as ONE device batch, starts of
+    different targets interleaved in the input order): every start's result
+    is bit-identical to running its target's starts as their own batch."""
+    src, tgt = small_pair(2500, 2300, seed=31)
+    scales = [np.array([1.0, 1.0, 1.0]) + d for d in (0.1, -0.1, 0.05, 0.0, -0.07, 0.12)]
+    targets = [tgt * sc for sc in scales]
+    rng = np.random.default_rng(8)
+    B = 23
+    R0 = np.array([rot_xyz(*rng.uniform(-90, 90, 3)) for _ in range(B)])
+    t0 = rng.normal(size=(B, 3)) * 0.1
+    tids = rng.integers(0, len(targets), B).astype(np.int32)
+    tids[:len(targets)] = np.arange(len(targets))  # every target used
+    ctx.set_source(src)
+    ctx.set_targets(targets)
+    got = ctx.gicp_batch_targets(R0, t0, tids)
+    for k, t in enumerate(targets):
+        sel = np.nonzero(tids == k)[0]
+        ctx.set_target(t)
+        ref = ctx.gicp_batch(R0[sel], t0[sel])
+        for key in ("T", "rmse", "fitness", "iters", "ncorr"):
+            assert np.array_equal(got[key][sel], ref[key]), (k, key)
+    with pytest.raises(ValueError):
+        ctx.set_targets(targets)
+        ctx.gicp_batch_targets(R0[:2], t0[:2], np.array([0, len(targets)], np.int32))
+
+
+def test_speculative_align_uses_one_batch_per_compass_iteration(oracle):
+    """align() with the speculative compass on the multi-target batch agrees
+    with the CPU restatement of the reference's sequential compass."""
+    from orpcd_amd import Aligner, GeneralizedICP, Preprocessor
+    src, tgt = small_pair(900, 1000, seed=14)
+    tgt = tgt * np.array([1.1, 0.95, 1.0])
+    np.random.seed(3)
+    o = oracle.OracleAligner(oracle.OracleGeneralizedICP(), attempts=5)
+    To, mo, sfo, eo = o.align(src.copy(), tgt.copy())
+    np.random.seed(3)
+    al = Aligner(Preprocessor([]), Preprocessor([]), GeneralizedICP(), attempts=5)
+    T, m, sf, e = al.align(src.copy(), tgt.copy(), refine_registration=False)
+    assert np.array_equal(sf, sfo) and len(e) == len(eo)
+    assert abs(m - mo) <= 1e-5 and np.abs(T - To).max() <= 1e-4

@@ -38,6 +38,37 @@ def test_rng_replay_matches_reference_G1():
             assert np.array_equal(R, g[f"R_{seed}"][n]) and np.array_equal(t, g[f"t_{seed}"][n])
 
 
+@pytest.mark.parametrize("seed,n", [(0, 64), (1, 1), (42, 31), (7, 384)])
+def test_draw_block_matches_initialize_rotation(seed, n):
+    """The batched draw of a multistart's starts is the reference's sequence of
+    initialize_rotation() calls bit for bit (R0, t0 and the RNG state after),
+    and the lazily rebuilt per-attempt states equal get_state() after each
+    sequential draw (G1 covers the first 64 of seeds 0/1/42 as well)."""
+    from orpcd_amd import Aligner, Preprocessor
+    al = Aligner(Preprocessor([]), Preprocessor([]), optimizer=None, attempts=n)
+    np.random.seed(seed)
+    ref, states = [], []
+    for _ in range(n):
+        ref.append(al.initialize_rotation())
+        states.append(np.random.get_state())
+    after_ref = np.random.uniform(size=5)
+    np.random.seed(seed)
+    R0s, t0s, lazy = al._draw_starts()
+    after = np.random.uniform(size=5)
+    assert np.array_equal(after, after_ref)
+    for k in range(n):
+        assert np.array_equal(R0s[k], ref[k][0]) and np.array_equal(t0s[k], ref[k][1]), k
+    if seed == 0:
+        g = np.load(f"{GOLDEN}/g1_rng.npz")
+        assert np.array_equal(np.array(R0s), g["R_0"][:n]) and np.array_equal(np.array(t0s), g["t_0"][:n])
+    probe = np.random.get_state()
+    for k in sorted({0, n // 2, n - 1, -1}):
+        st, want = lazy[k], states[k]
+        assert st[0] == want[0] and np.array_equal(st[1], want[1]) and st[2:] == want[2:], k
+    cur = np.random.get_state()  # rebuilding a state leaves the current stream untouched
+    assert np.array_equal(cur[1], probe[1]) and cur[2:] == probe[2:]
+
+
 def test_preprocess_matches_reference_G2():
     from orpcd_amd import Preprocessor
     from orpcd_amd.Preprocessor.Downsamplers import RandomDownsampler
