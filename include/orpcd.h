@@ -237,6 +237,13 @@ int orpcd_fgr_optimize(orpcd_ctx* ctx, const double* src, int64_t n, const doubl
  *   "scan_blocks"   persistent grid of search_kernel 2                    */
 int orpcd_set_option(orpcd_ctx* ctx, const char* key, double value);
 
+/* Test entry: n 6x6 systems (per system 27 doubles: the JTJ upper triangle
+ * row-major (21), then JTr (6)) solved as the GICP update is (det check,
+ * LDLT, TransformVector6dToMatrix4d) by the single-lane and by the
+ * wave-parallel device code; per system 23 doubles each: det, x (6), the 4x4
+ * update (16).  The two must agree bit for bit.                            */
+int orpcd_test_solve6(orpcd_ctx* ctx, const double* sums27, int32_t n, double* out_serial, double* out_wave);
+
 /* ------------------------------------------------------------ measurement
  * Live kernel timing (hipEvents on the context's stream).  When enabled,
  * every launch of the dominant correspondence kernel is bracketed.

@@ -249,6 +249,7 @@ __device__ inline Sym3 gicp_cov_from_normal(const double n[3], double eps) {
 
 // Inverse of a symmetric positive-definite 3x3 (cofactors / det).
 __device__ __forceinline__ Sym3 sym3_inverse(const Sym3& a) {
+#pragma clang fp contract(off)  // no fused multiply-add: the same rounding in every caller
     double c00 = a.yy * a.zz - a.yz * a.yz;
     double c01 = a.xz * a.yz - a.xy * a.zz;
     double c02 = a.xy * a.yz - a.xz * a.yy;
@@ -266,6 +267,7 @@ __device__ __forceinline__ Sym3 sym3_inverse(const Sym3& a) {
 
 // R S R^T for symmetric S.
 __device__ __forceinline__ Sym3 rotate_sym(const double R[9], const Sym3& S) {
+#pragma clang fp contract(off)  // no fused multiply-add: the same rounding in every caller
     double A[3][3] = {{S.xx, S.xy, S.xz}, {S.xy, S.yy, S.yz}, {S.xz, S.yz, S.zz}};
     double RA[3][3];
 #pragma unroll
@@ -326,6 +328,7 @@ __device__ __forceinline__ void swap_cols6(double A[6][6], int k, int p) {
 
 // Eigen PartialPivLU determinant (SolveLinearSystemPSD's check_det).
 __device__ inline double det6(const double Ain[36]) {
+#pragma clang fp contract(off)  // no fused multiply-add: the same rounding in every caller
     double A[6][6];
 #pragma unroll
     for (int i = 0; i < 36; ++i) A[i / 6][i % 6] = Ain[i];
@@ -359,6 +362,7 @@ __device__ inline double det6(const double Ain[36]) {
 
 // Eigen LDLT (diagonal pivoting) solve of A x = b.
 __device__ inline void ldlt_solve6(const double Ain[36], const double b[6], double x[6]) {
+#pragma clang fp contract(off)  // no fused multiply-add: the same rounding in every caller
     double A[6][6];
 #pragma unroll
     for (int i = 0; i < 36; ++i) A[i / 6][i % 6] = Ain[i];
@@ -434,6 +438,7 @@ __device__ inline void ldlt_solve6(const double Ain[36], const double b[6], doub
 
 // O3D utility/Eigen.cpp TransformVector6dToMatrix4d (via Eigen quaternions).
 __device__ inline void vec6_to_m4(const double x[6], double T[16]) {
+#pragma clang fp contract(off)  // no fused multiply-add: the same rounding in every caller
     double zw = cos(x[2] * 0.5), zz = sin(x[2] * 0.5);
     double yw = cos(x[1] * 0.5), yy = sin(x[1] * 0.5);
     double xw = cos(x[0] * 0.5), xx = sin(x[0] * 0.5);
@@ -470,6 +475,7 @@ __device__ inline void vec6_to_m4(const double x[6], double T[16]) {
 }
 
 __device__ __forceinline__ void m4_mul(const double A[16], const double B[16], double C[16]) {
+#pragma clang fp contract(off)  // no fused multiply-add: the same rounding in every caller
     for (int i = 0; i < 4; ++i)
         for (int j = 0; j < 4; ++j) {
             double s = 0.0;
@@ -483,6 +489,7 @@ __device__ __forceinline__ void m4_mul(const double A[16], const double B[16], d
 // values descending; a vanished singular value's U column is completed
 // orthonormally.  Single-lane code (the solve runs one lane per start).
 __device__ inline void svd3_jacobi(const double A[3][3], double U[3][3], double s[3], double V[3][3]) {
+#pragma clang fp contract(off)  // no fused multiply-add: the same rounding in every caller
     double a[3][3], v[3][3] = {{1, 0, 0}, {0, 1, 0}, {0, 0, 1}};
     for (int i = 0; i < 3; ++i)
         for (int j = 0; j < 3; ++j) a[i][j] = A[i][j];
@@ -551,6 +558,7 @@ __device__ inline void svd3_jacobi(const double A[3][3], double U[3][3], double 
 }
 
 __device__ __forceinline__ double det3(const double a[3][3]) {
+#pragma clang fp contract(off)  // no fused multiply-add: the same rounding in every caller
     return a[0][0] * (a[1][1] * a[2][2] - a[1][2] * a[2][1]) - a[0][1] * (a[1][0] * a[2][2] - a[1][2] * a[2][0]) +
            a[0][2] * (a[1][0] * a[2][1] - a[1][1] * a[2][0]);
 }
@@ -560,6 +568,7 @@ __device__ __forceinline__ double det3(const double a[3][3]) {
 // sigma = sum(dst src^T)/n - mean_dst mean_src^T; R = U diag(1,1,+-1) V^T;
 // t = mean_dst - R mean_src.  T: 4x4 row-major, column convention.
 __device__ inline void umeyama_from_moments(const double* s, double n, double T[16]) {
+#pragma clang fp contract(off)  // no fused multiply-add: the same rounding in every caller
     const double inv = 1.0 / n;
     const double ms[3] = {s[0] * inv, s[1] * inv, s[2] * inv};
     const double md[3] = {s[3] * inv, s[4] * inv, s[5] * inv};
@@ -574,6 +583,217 @@ __device__ inline void umeyama_from_moments(const double* s, double n, double T[
     }
     T[12] = T[13] = T[14] = 0.0;
     T[15] = 1.0;
+}
+
+// ------------------------------------------------- wave-parallel 6x6 solve
+// det6 / ldlt_solve6 / vec6_to_m4 spread over one wave: lane r < 6 holds row
+// r of the 6x6 system.  Every matrix element sees the same operations, in the
+// same order, with the same operands as in the single-lane code above (pivot
+// scans on the broadcast values, eliminations row-parallel, sums in index
+// order), so the results are bit-identical (orpcd_test_solve6, tests/
+// test_gpu_gicp.py::test_wave_solve_bit_identical); the transcendental half-
+// angle terms run on six lanes at once.  All 64 lanes call these (uniform
+// control flow); outputs are wave-uniform.
+__device__ __forceinline__ double rl64(double v, int k) {
+    const long long b = __double_as_longlong(v);
+    const unsigned lo = __builtin_amdgcn_readlane((unsigned)b, k);
+    const unsigned hi = __builtin_amdgcn_readlane((unsigned)(b >> 32), k);
+    return __longlong_as_double(((long long)hi << 32) | lo);
+}
+
+// rows k and p (wave-uniform) exchange lanes
+__device__ __forceinline__ void wave_swap_rows6(double a[6], int k, int p, int lane) {
+#pragma unroll
+    for (int j = 0; j < 6; ++j) {
+        const double ak = rl64(a[j], k), ap = rl64(a[j], p);
+        a[j] = lane == k ? ap : (lane == p ? ak : a[j]);
+    }
+}
+
+__device__ inline double det6_wave(const double row[6], int lane) {
+#pragma clang fp contract(off)  // no fused multiply-add: the same rounding in every caller
+    double a[6];
+#pragma unroll
+    for (int j = 0; j < 6; ++j) a[j] = row[j];
+    double det = 1.0;
+    bool zero = false;
+#pragma unroll
+    for (int k = 0; k < 6; ++k) {
+        int piv = k;
+        double best = fabs(rl64(a[k], k));
+#pragma unroll
+        for (int i = k + 1; i < 6; ++i) {
+            const double v = fabs(rl64(a[k], i));
+            if (v > best) {
+                best = v;
+                piv = i;
+            }
+        }
+        piv = __builtin_amdgcn_readfirstlane(piv);
+        if (piv != k) {
+            wave_swap_rows6(a, k, piv, lane);
+            det = -det;
+        }
+        const double akk = rl64(a[k], k);
+        zero = zero || akk == 0.0;
+        double rk[6];
+#pragma unroll
+        for (int j = k + 1; j < 6; ++j) rk[j] = rl64(a[j], k);
+        if (lane > k && lane < 6) {
+            const double f = a[k] / akk;
+#pragma unroll
+            for (int j = k + 1; j < 6; ++j) a[j] -= f * rk[j];
+        }
+        det *= akk;
+    }
+    return zero ? 0.0 : det;
+}
+
+__device__ inline void ldlt_solve6_wave(const double row[6], const double b[6], double x[6], int lane) {
+#pragma clang fp contract(off)  // no fused multiply-add: the same rounding in every caller
+    double a[6];
+#pragma unroll
+    for (int j = 0; j < 6; ++j) a[j] = row[j];
+    int tr[6];
+#pragma unroll
+    for (int k = 0; k < 6; ++k) {
+        int idx = k;
+        double big = fabs(rl64(a[k], k));
+#pragma unroll
+        for (int i = k + 1; i < 6; ++i) {
+            const double v = fabs(rl64(a[i], i));
+            if (v > big) {
+                big = v;
+                idx = i;
+            }
+        }
+        idx = __builtin_amdgcn_readfirstlane(idx);
+        tr[k] = idx;
+        if (idx != k) {
+            wave_swap_rows6(a, k, idx, lane);
+#pragma unroll
+            for (int m = k + 1; m < 6; ++m) {  // the column exchange, inside every row
+                if (idx == m) {
+                    const double t = a[k];
+                    a[k] = a[m];
+                    a[m] = t;
+                }
+            }
+        }
+        double tmp[6];
+#pragma unroll
+        for (int j = 0; j < k; ++j) tmp[j] = rl64(a[j], j) * rl64(a[j], k);
+        double s = 0.0;
+#pragma unroll
+        for (int j = 0; j < k; ++j) s += rl64(a[j], k) * tmp[j];
+        if (lane == k) a[k] -= s;
+        if (lane > k && lane < 6) {
+            double t = 0.0;
+#pragma unroll
+            for (int j = 0; j < k; ++j) t += a[j] * tmp[j];
+            a[k] -= t;
+        }
+        const double akk = rl64(a[k], k);
+        if (fabs(akk) > 0.0 && lane > k && lane < 6) a[k] /= akk;
+    }
+    // substitutions (ldlt_solve6's order): y = P b, L y' = y, D, L^T, P^T
+    double y[6];
+#pragma unroll
+    for (int i = 0; i < 6; ++i) y[i] = b[i];
+    auto swap_y = [&](int k, int p) {
+#pragma unroll
+        for (int m = 0; m < 6; ++m) {
+            if (m <= k) continue;
+            const bool sw = m == p;
+            const double u = y[k], c = y[m];
+            y[k] = sw ? c : u;
+            y[m] = sw ? u : c;
+        }
+    };
+#pragma unroll
+    for (int k = 0; k < 6; ++k)
+        if (tr[k] != k) swap_y(k, tr[k]);
+    // forward, column by column: y[i] -= A[i][j] y[j] in increasing j for every i
+    double yl = 0.0;  // lane i: its y[i]
+#pragma unroll
+    for (int i = 0; i < 6; ++i)
+        if (lane == i) yl = y[i];
+#pragma unroll
+    for (int j = 0; j < 5; ++j) {
+        const double yj = rl64(yl, j);
+        if (lane > j && lane < 6) yl -= a[j] * yj;
+    }
+    double dl = a[0];  // lane i: A[i][i]
+#pragma unroll
+    for (int i = 1; i < 6; ++i)
+        if (lane == i) dl = a[i];
+    const double tol = 2.2250738585072014e-308;
+    yl = fabs(dl) > tol ? yl / dl : 0.0;
+#pragma unroll
+    for (int i = 0; i < 6; ++i) y[i] = rl64(yl, i);
+    // backward: y[i] -= A[j][i] y[j] for j = i+1 .. 5 (uniform, sequential as ldlt_solve6)
+#pragma unroll
+    for (int i = 5; i >= 0; --i)
+#pragma unroll
+        for (int j = i + 1; j < 6; ++j) y[i] -= rl64(a[i], j) * y[j];
+#pragma unroll
+    for (int k = 5; k >= 0; --k)
+        if (tr[k] != k) swap_y(k, tr[k]);
+#pragma unroll
+    for (int i = 0; i < 6; ++i) x[i] = y[i];
+}
+
+// vec6_to_m4 with its six half-angle cos / sin on lanes 0..5
+__device__ inline void vec6_to_m4_wave(const double x[6], double T[16], int lane) {
+#pragma clang fp contract(off)  // no fused multiply-add: the same rounding in every caller
+    const double h = lane < 2 ? x[2] : (lane < 4 ? x[1] : x[0]);
+    const double v = (lane & 1) ? sin(h * 0.5) : cos(h * 0.5);
+    double zw = rl64(v, 0), zz = rl64(v, 1);
+    double yw = rl64(v, 2), yy = rl64(v, 3);
+    double xw = rl64(v, 4), xx = rl64(v, 5);
+    double aw = zw * yw - 0.0 * 0.0 - 0.0 * yy - zz * 0.0;
+    double ax = zw * 0.0 + 0.0 * yw + 0.0 * 0.0 - zz * yy;
+    double ay = zw * yy + 0.0 * yw + zz * 0.0 - 0.0 * 0.0;
+    double az = zw * 0.0 + zz * yw + 0.0 * yy - 0.0 * 0.0;
+    double qw = aw * xw - ax * xx - ay * 0.0 - az * 0.0;
+    double qx = aw * xx + ax * xw + ay * 0.0 - az * 0.0;
+    double qy = aw * 0.0 + ay * xw + az * xx - ax * 0.0;
+    double qz = aw * 0.0 + az * xw + ax * 0.0 - ay * xx;
+    double tx = 2 * qx, ty = 2 * qy, tz = 2 * qz;
+    double twx = tx * qw, twy = ty * qw, twz = tz * qw;
+    double txx = tx * qx, txy = ty * qx, txz = tz * qx;
+    double tyy = ty * qy, tyz = tz * qy, tzz = tz * qz;
+    T[0] = 1 - (tyy + tzz);
+    T[1] = txy - twz;
+    T[2] = txz + twy;
+    T[3] = x[3];
+    T[4] = txy + twz;
+    T[5] = 1 - (txx + tzz);
+    T[6] = tyz - twx;
+    T[7] = x[4];
+    T[8] = txz - twy;
+    T[9] = tyz + twx;
+    T[10] = 1 - (txx + tyy);
+    T[11] = x[5];
+    T[12] = 0.0;
+    T[13] = 0.0;
+    T[14] = 0.0;
+    T[15] = 1.0;
+}
+
+// lane r < 6: row r of the symmetric 6x6 whose upper triangle is
+// s[ut(a, b)] (a <= b, ut = row-major upper-triangle index)
+__device__ __forceinline__ void sym6_row(const double* s, int lane, double row[6]) {
+#pragma unroll
+    for (int c = 0; c < 6; ++c) {
+        double v = 0.0;
+#pragma unroll
+        for (int r = 0; r < 6; ++r) {
+            const int a = r <= c ? r : c, b = r <= c ? c : r;
+            if (lane == r) v = s[a * 6 - a * (a - 1) / 2 + (b - a)];
+        }
+        row[c] = v;
+    }
 }
 
 // ------------------------------------------------------- wave reductions

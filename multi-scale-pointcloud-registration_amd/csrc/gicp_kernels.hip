@@ -411,6 +411,7 @@ __device__ __forceinline__ int culled_search(float4* stage, const float4* __rest
 }
 
 __device__ __forceinline__ void xform(const double Q[12], const double p[3], double q[3]) {
+#pragma clang fp contract(off)  // no fused multiply-add: the same rounding in every caller
     q[0] = Q[0] * p[0] + Q[1] * p[1] + Q[2] * p[2] + Q[3];
     q[1] = Q[4] * p[0] + Q[5] * p[1] + Q[6] * p[2] + Q[7];
     q[2] = Q[8] * p[0] + Q[9] * p[1] + Q[10] * p[2] + Q[11];
@@ -1275,56 +1276,114 @@ struct SolveArgs {
 // --------------------------------------------------------------------------
 // kAt: the pose state (prev, T, Q, R) is read and written by a different
 // workgroup every pass of the same launch (persistent loop): atomic accesses.
-// Returns true when the start finished.
+// Called by all 64 lanes of one wave with the same (uniform) sums; the 6x6
+// system is solved wave-parallel (det6_wave / ldlt_solve6_wave, bit-identical
+// to the single-lane det6 / ldlt_solve6); lane 0 stores.  Returns true when
+// the start finished.
 template <int kEst, bool kAt = false>  // kEst 0: GeneralizedICP, 1: PointToPoint
 __device__ bool solve_start(int slot, const double s[kNacc], int64_t N, int pass, int max_iter, double rel_fit,
                             double rel_rmse, const SolveArgs& a) {
+#pragma clang fp contract(off)  // no fused multiply-add: the same rounding in every caller
+    const int lane = threadIdx.x & 63;
     const double cnt = s[28];
     const double fit = cnt > 0 ? cnt / (double)N : 0.0;
     const double rmse = cnt > 0 ? sqrt(s[27] / cnt) : 0.0;
     const double pf = ld_f64<kAt>(a.prev + 2 * slot), pr = ld_f64<kAt>(a.prev + 2 * slot + 1);
     const bool converged = pass >= 1 && fabs(pf - fit) < rel_fit && fabs(pr - rmse) < rel_rmse;
     if (converged || pass >= max_iter) {
-        a.out_fit[slot] = fit;
-        a.out_rmse[slot] = rmse;
-        a.out_iters[slot] = pass;
-        a.out_ncorr[slot] = (int64_t)cnt;
-        __hip_atomic_store(a.done + slot, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (lane == 0) {
+            a.out_fit[slot] = fit;
+            a.out_rmse[slot] = rmse;
+            a.out_iters[slot] = pass;
+            a.out_ncorr[slot] = (int64_t)cnt;
+            __hip_atomic_store(a.done + slot, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
         return true;
     }
-    st_f64<kAt>(a.prev + 2 * slot, fit);
-    st_f64<kAt>(a.prev + 2 * slot + 1, rmse);
+    if (lane == 0) {
+        st_f64<kAt>(a.prev + 2 * slot, fit);
+        st_f64<kAt>(a.prev + 2 * slot + 1, rmse);
+    }
 
     double upd[16] = {1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1};
     if (cnt > 0 && kEst == 1) {
-        umeyama_from_moments(s, cnt, upd);
+        umeyama_from_moments(s, cnt, upd);  // every lane, the same values
     } else if (cnt > 0) {
-        double JTJ[36], b[6];
-        for (int r = 0; r < 6; ++r)
-            for (int c = 0; c < 6; ++c) JTJ[6 * r + c] = r <= c ? s[ut(r, c)] : s[ut(c, r)];
+        double row[6], b[6];
+        sym6_row(s, lane, row);
         for (int r = 0; r < 6; ++r) b[r] = -s[21 + r];
-        const double det = det6(JTJ);
+        const double det = det6_wave(row, lane);
         if (!(fabs(det) < 1e-6 || isnan(det) || isinf(det))) {
             double x[6];
-            ldlt_solve6(JTJ, b, x);
-            vec6_to_m4(x, upd);
+            ldlt_solve6_wave(row, b, x, lane);
+            vec6_to_m4_wave(x, upd, lane);
         }
     }
     double Tcur[16], Tn[16];
     for (int t = 0; t < 16; ++t) Tcur[t] = ld_f64<kAt>(a.T + 16 * slot + t);
     m4_mul(upd, Tcur, Tn);
-    for (int t = 0; t < 16; ++t) st_f64<kAt>(a.T + 16 * slot + t, Tn[t]);
+    if (lane == 0)
+        for (int t = 0; t < 16; ++t) st_f64<kAt>(a.T + 16 * slot + t, Tn[t]);
     // Q = Tn * [G; 0 0 0 1]  (3x4), R = Tn[:3,:3]
     const double* G = a.G + 12 * slot;
     for (int r = 0; r < 3; ++r) {
         for (int c = 0; c < 4; ++c) {
             double v = Tn[4 * r + 0] * G[c] + Tn[4 * r + 1] * G[4 + c] + Tn[4 * r + 2] * G[8 + c];
             if (c == 3) v += Tn[4 * r + 3];
-            st_f64<kAt>(a.Q + 12 * slot + 4 * r + c, v);
+            if (lane == 0) st_f64<kAt>(a.Q + 12 * slot + 4 * r + c, v);
         }
-        for (int c = 0; c < 3; ++c) st_f64<kAt>(a.R + 9 * slot + 3 * r + c, Tn[4 * r + c]);
+        if (lane == 0)
+            for (int c = 0; c < 3; ++c) st_f64<kAt>(a.R + 9 * slot + 3 * r + c, Tn[4 * r + c]);
     }
     return false;
+}
+
+// Test entry (orpcd_test_solve6): for each of n systems (21 upper JTJ + 6 JTr),
+// det, x and the update matrix by the single-lane code (out_serial) and by the
+// wave-parallel code (out_wave); 23 doubles each.
+__global__ __launch_bounds__(64) void solve6_test_kernel(const double* __restrict__ sums, int n,
+                                                         double* __restrict__ out_serial,
+                                                         double* __restrict__ out_wave) {
+    const int sys = blockIdx.x, lane = threadIdx.x;
+    if (sys >= n) return;
+    const double* s = sums + (size_t)27 * sys;
+    double bb[6];
+    for (int r = 0; r < 6; ++r) bb[r] = -s[21 + r];
+    if (lane == 0) {
+        double JTJ[36], x[6] = {0, 0, 0, 0, 0, 0};
+        double upd[16] = {1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1};
+        for (int r = 0; r < 6; ++r)
+            for (int c = 0; c < 6; ++c) JTJ[6 * r + c] = r <= c ? s[ut(r, c)] : s[ut(c, r)];
+        const double det = det6(JTJ);
+        if (!(fabs(det) < 1e-6 || isnan(det) || isinf(det))) {
+            ldlt_solve6(JTJ, bb, x);
+            vec6_to_m4(x, upd);
+        }
+        double* o = out_serial + (size_t)23 * sys;
+        o[0] = det;
+        for (int i = 0; i < 6; ++i) o[1 + i] = x[i];
+        for (int i = 0; i < 16; ++i) o[7 + i] = upd[i];
+    }
+    double row[6], x[6] = {0, 0, 0, 0, 0, 0};
+    double upd[16] = {1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1};
+    sym6_row(s, lane, row);
+    const double det = det6_wave(row, lane);
+    if (!(fabs(det) < 1e-6 || isnan(det) || isinf(det))) {
+        ldlt_solve6_wave(row, bb, x, lane);
+        vec6_to_m4_wave(x, upd, lane);
+    }
+    if (lane == 0) {
+        double* o = out_wave + (size_t)23 * sys;
+        o[0] = det;
+        for (int i = 0; i < 6; ++i) o[1 + i] = x[i];
+        for (int i = 0; i < 16; ++i) o[7 + i] = upd[i];
+    }
+}
+
+hipError_t launch_solve6_test(const double* sums, int n, double* out_serial, double* out_wave, hipStream_t s) {
+    if (n <= 0) return hipSuccess;
+    solve6_test_kernel<<<(unsigned)n, 64, 0, s>>>(sums, n, out_serial, out_wave);
+    return hipGetLastError();
 }
 
 // --------------------------------------------------------------------------
@@ -1371,9 +1430,9 @@ __device__ __forceinline__ void finish_pass(int slot, int nact, const double* __
     double s[kNacc];
     reduce_partials<true>(partial, slot, nblk, s);
     int last_solve = 0;
+    if (lane == 0) pc.ctl[2 + slot] = 0;  // for the next pass (read after the launch boundary)
+    solve_start<kEst>(slot, s, pc.N, pc.pass, pc.max_iter, pc.rel_fit, pc.rel_rmse, pc.a);
     if (lane == 0) {
-        pc.ctl[2 + slot] = 0;  // for the next pass (read after the launch boundary)
-        solve_start<kEst>(slot, s, pc.N, pc.pass, pc.max_iter, pc.rel_fit, pc.rel_rmse, pc.a);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // done[slot] (sc1) has landed
         last_solve = __hip_atomic_fetch_add(pc.ctl + 1, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == nact - 1;
     }
@@ -1411,6 +1470,7 @@ __device__ __forceinline__ void gicp_block_terms(int slot, int ablk, const doubl
                                                  const double* __restrict__ Qm, const double* __restrict__ Rm,
                                                  double r2, unsigned long long* __restrict__ best,
                                                  int32_t* __restrict__ prevnn, double acc[kNacc]) {
+#pragma clang fp contract(off)  // no fused multiply-add: the same rounding in every caller
 #pragma unroll
     for (int v = 0; v < kNacc; ++v) acc[v] = 0.0;
     double Q[12], R[9];
@@ -1513,6 +1573,7 @@ __device__ __forceinline__ void p2p_block_terms(int slot, int ablk, const double
                                                 const double* __restrict__ tgt64, const double* __restrict__ Qm,
                                                 double r2, unsigned long long* __restrict__ best,
                                                 int32_t* __restrict__ prevnn, double acc[kP2PTerms]) {
+#pragma clang fp contract(off)  // no fused multiply-add: the same rounding in every caller
 #pragma unroll
     for (int v = 0; v < kP2PTerms; ++v) acc[v] = 0.0;
     double Q[12];
@@ -1598,7 +1659,7 @@ __global__ __launch_bounds__(64) void icp_solve_kernel(const int32_t* __restrict
     } else {
         reduce_partials(partial, slot, nblk, s);
     }
-    if (threadIdx.x == 0) solve_start<kEst>(slot, s, N, pass, max_iter, rel_fit, rel_rmse, a);
+    solve_start<kEst>(slot, s, N, pass, max_iter, rel_fit, rel_rmse, a);
 }
 
 // --------------------------------------------------------------------------
@@ -1768,9 +1829,9 @@ __device__ __forceinline__ void persist_solve(const PersistArgs& P, int slot, in
     const int lane = threadIdx.x & 63;
     double s[kNacc];
     reduce_partials<true>(P.partial, slot, P.nblk, s);
+    const bool fin = solve_start<kEst, true>(slot, s, P.N, pass, P.max_iter, P.rel_fit, P.rel_rmse, P.a);
     if (lane != 0) return;
     st_i32<true>(P.tick_start + slot, 0);
-    const bool fin = solve_start<kEst, true>(slot, s, P.N, pass, P.max_iter, P.rel_fit, P.rel_rmse, P.a);
     if (P.fences) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the pose (sc1) has landed before the publish
     if (fin) {

@@ -372,6 +372,7 @@ hipError_t launch_gicp_solve_sums(const orpcd_ctx* c, const double* sums29, int6
                                   const orpcd_gicp_params& p, hipStream_t s);
 hipError_t launch_nn1(const double* q, int64_t nq, const CloudLayout& t, double r2, int32_t* idx, double* d2,
                       hipStream_t s);
+hipError_t launch_solve6_test(const double* sums, int n, double* out_serial, double* out_wave, hipStream_t s);
 int persist_grid(int device, int est);
 int persist_first_splits(const orpcd_ctx* c, int B, int grid);
 unsigned long long persist_sched_word(int pass, int S);

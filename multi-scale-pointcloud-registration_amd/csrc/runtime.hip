@@ -1483,6 +1483,23 @@ int orpcd_set_option(orpcd_ctx* c, const char* key, double value) {
     return ORPCD_OK;
 }
 
+int orpcd_test_solve6(orpcd_ctx* c, const double* sums27, int32_t n, double* out_serial, double* out_wave) {
+    if (!c) return ORPCD_EINVAL;
+    CTX_REQUIRE(c, sums27 && out_serial && out_wave && n >= 0, "test_solve6: bad arguments");
+    if (n == 0) return ORPCD_OK;
+    CTX_CHECK(c, hipSetDevice(c->device));
+    CTX_CHECK(c, c->scratch64c.ensure((size_t)n * (27 + 46)));
+    double* dsum = c->scratch64c.p;
+    double* dser = dsum + (size_t)n * 27;
+    double* dwav = dser + (size_t)n * 23;
+    CTX_CHECK(c, hipMemcpyAsync(dsum, sums27, (size_t)n * 27 * 8, hipMemcpyHostToDevice, c->stream));
+    CTX_CHECK(c, launch_solve6_test(dsum, n, dser, dwav, c->stream));
+    CTX_CHECK(c, hipMemcpyAsync(out_serial, dser, (size_t)n * 23 * 8, hipMemcpyDeviceToHost, c->stream));
+    CTX_CHECK(c, hipMemcpyAsync(out_wave, dwav, (size_t)n * 23 * 8, hipMemcpyDeviceToHost, c->stream));
+    CTX_CHECK(c, hipStreamSynchronize(c->stream));
+    return ORPCD_OK;
+}
+
 int orpcd_profiling(orpcd_ctx* c, int32_t enable) {
     if (!c) return ORPCD_EINVAL;
     c->profiling = enable != 0;

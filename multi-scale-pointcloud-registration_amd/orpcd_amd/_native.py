@@ -59,7 +59,7 @@ EXPORTED = ("orpcd_abi_version", "orpcd_device_count", "orpcd_ctx_create", "orpc
             "orpcd_nn1_radius", "orpcd_estimate_normals", "orpcd_fpfh", "orpcd_fpfh_from_normals", "orpcd_fgr", "orpcd_feature_nn",
             "orpcd_fgr_optimize", "orpcd_set_source_points", "orpcd_icp_p2p_batch",
             "orpcd_sor", "orpcd_voxel_down_sample", "orpcd_farthest_downsample",
-            "orpcd_set_option", "orpcd_set_targets", "orpcd_gicp_batch_targets",
+            "orpcd_set_option", "orpcd_set_targets", "orpcd_gicp_batch_targets", "orpcd_test_solve6",
             "orpcd_profiling", "orpcd_stats", "orpcd_reset_stats")
 
 
@@ -88,6 +88,7 @@ def load_library():
         L.orpcd_set_targets.argtypes = [vp, _f64p, _i64p, ctypes.c_int32, c_dbl]
         L.orpcd_gicp_batch_targets.argtypes = [vp, _f64p, _f64p, _i32p, ctypes.c_int32, ctypes.POINTER(GicpParams),
                                                _f64p, _f64p, _f64p, _i32p, _i64p]
+        L.orpcd_test_solve6.argtypes = [vp, _f64p, ctypes.c_int32, _f64p, _f64p]
         L.orpcd_set_source_rows.argtypes = [vp, _f64p, c_i64, c_i64, c_i64]
         L.orpcd_gicp_shard_begin.argtypes = [vp, _f64p, _f64p, ctypes.POINTER(GicpParams), c_i64]
         L.orpcd_gicp_shard_pass.argtypes = [vp, _f64p, _i32p]
@@ -258,6 +259,14 @@ class Context:
                                                      ctypes.byref(p), T.reshape(-1), rmse, fit, iters, ncorr),
                     "orpcd_gicp_batch_targets")
         return dict(T=T, rmse=rmse, fitness=fit, iters=iters, ncorr=ncorr)
+
+    def test_solve6(self, sums27: np.ndarray):
+        """(serial, wave) results of orpcd_test_solve6: (n, 23) each."""
+        sums27 = np.ascontiguousarray(sums27, dtype=np.float64).reshape(-1, 27)
+        n = len(sums27)
+        a, b = np.zeros((n, 23)), np.zeros((n, 23))
+        self._check(self._L.orpcd_test_solve6(self._h, sums27, n, a, b), "orpcd_test_solve6")
+        return a, b
 
     def icp_p2p_batch(self, init: np.ndarray, max_correspondence_distance=0.5, max_iteration=200,
                       relative_fitness=1e-6, relative_rmse=1e-6) -> dict:

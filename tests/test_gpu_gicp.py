@@ -478,3 +478,57 @@ def test_speculative_align_uses_one_batch_per_compass_iteration(oracle):
     T, m, sf, e = al.align(src.copy(), tgt.copy(), refine_registration=False)
     assert np.array_equal(sf, sfo) and len(e) == len(eo)
     assert abs(m - mo) <= 1e-5 and np.abs(T - To).max() <= 1e-4
+
+
+def _sym_upper(A):
+    iu = np.triu_indices(6)
+    return A[iu]
+
+
+def test_wave_solve_bit_identical(ctx, oracle):
+    """The wave-parallel 6x6 solve (det check, LDLT with diagonal pivoting,
+    substitutions, TransformVector6dToMatrix4d) reproduces the single-lane
+    device code bit for bit: random SPD systems over 12 decades of scale,
+    rank-deficient and near-singular ones around the |det| < 1e-6 rejection,
+    pivoting-heavy ones, GICP normal equations from real correspondences,
+    and degenerate inputs (zeros, NaN, inf)."""
+    rng = np.random.default_rng(17)
+    systems = []
+    for k in range(1500):
+        M = rng.normal(size=(6, 6)) * 10.0 ** rng.uniform(-6, 6)
+        A = M @ M.T + np.eye(6) * 10.0 ** rng.uniform(-12, 0)
+        systems.append(np.r_[_sym_upper(A), rng.normal(size=6) * 10.0 ** rng.uniform(-3, 3)])
+    for k in range(600):  # rank 5 + tiny noise: det around the 1e-6 threshold
+        M = rng.normal(size=(6, 5)) * 10.0 ** rng.uniform(-2, 2)
+        A = M @ M.T + np.diag(rng.uniform(0, 1, 6)) * 10.0 ** rng.uniform(-14, -4)
+        systems.append(np.r_[_sym_upper(A), rng.normal(size=6)])
+    for k in range(400):  # strongly varying diagonal: many pivot exchanges
+        d = 10.0 ** rng.uniform(-8, 8, 6)
+        M = rng.normal(size=(6, 6)) * 1e-3
+        A = np.diag(d) + M @ M.T
+        systems.append(np.r_[_sym_upper(A), rng.normal(size=6) * d])
+    src, tgt = small_pair(800, 900, seed=2)  # GICP normal equations of real passes
+    tcov = oracle.estimate_normals(tgt, 20, -1.0, 1e-3)[2]
+    scov = oracle.estimate_normals(src, 20, -1.0, 1e-3)[2]
+    for k in range(40):
+        R = rot_xyz(*rng.uniform(-20, 20, 3))
+        p = src @ R.T + rng.normal(size=3) * 0.05
+        c = np.einsum("ij,njk,lk->nil", R, scov, R)
+        idx, _ = oracle.nn1_radius(p, tgt, 0.5)
+        JTJ, JTr, _ = oracle.gicp_step(p, c, tgt, tcov, idx)
+        systems.append(np.r_[_sym_upper(JTJ), JTr])
+    z = np.zeros(27)
+    systems.append(z)
+    e = z.copy()
+    e[:21] = _sym_upper(np.eye(6))
+    e[0] = 0.0  # zero first pivot
+    systems.append(e)
+    for bad in (np.nan, np.inf, -np.inf):
+        b = np.r_[_sym_upper(np.eye(6) * 3.0), np.ones(6)]
+        b[rng.integers(0, 27)] = bad
+        systems.append(b)
+    S = np.array(systems)
+    ser, wav = ctx.test_solve6(S)
+    assert np.array_equal(ser.view(np.int64), wav.view(np.int64)), np.argwhere(ser.view(np.int64) != wav.view(np.int64))[:5]
+    accepted = ~(np.abs(ser[:, 0]) < 1e-6) & np.isfinite(ser[:, 0])
+    assert accepted.sum() > 1000 and (~accepted).sum() > 50  # both branches exercised
