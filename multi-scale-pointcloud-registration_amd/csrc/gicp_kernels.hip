@@ -116,6 +116,13 @@ __device__ __forceinline__ void st_i32(int32_t* p, int v) {
     else *p = v;
 }
 
+// A load through a pointer the compiler cannot prove global (one read from a
+// TargetDesc): as a global load, not a flat one -- flat loads count against
+// both vmcnt and lgkmcnt, so every later wait drained all of them.
+__device__ __forceinline__ double ldg_f64(const double* p) {
+    return *(const __attribute__((address_space(1))) double*)p;
+}
+
 // --------------------------------------------------------------------------
 // Culled exact nearest search for the 2 queries of every lane of one wave,
 // restricted to tiles t with t % S == s.  s0lo/s0hi: super-tile `lane`'s box
@@ -1179,7 +1186,7 @@ size_t coop_smem_bytes(int W, int64_t ntiles) { return (size_t)ntiles * 2 + 16; 
 // queries per thread.  A function of N only, so the fixed-order reduction is
 // the same for every batch composition.  Measured at C2: 1 (4x the blocks, 4x
 // the partials for the solve) 18.5 ms per multistart, 2: 17.9, 4: 17.8.
-__host__ __device__ __forceinline__ int accum_qpt(int64_t) { return 4; }
+constexpr __host__ __device__ __forceinline__ int accum_qpt(int64_t) { return 4; }
 
 template <int Ctrl>
 __device__ __forceinline__ double dpp_f64(double v) {
@@ -1243,13 +1250,21 @@ __device__ __forceinline__ void reduce_partials(const double* __restrict__ parti
     for (int v = 0; v < kNacc; ++v) s[v] = 0.0;
     for (int b = lane; b < nblk; b += 64) {
         const double* pp = partial + ((size_t)slot * nblk + b) * kPartialStride;
+        if (kSc1) {
 #pragma unroll
-        for (int v = 0; v < kNacc; ++v) {
-            if (kSc1)
+            for (int v = 0; v < kNacc; ++v)
                 s[v] += __longlong_as_double((long long)__hip_atomic_load(
                     reinterpret_cast<const unsigned long long*>(pp) + v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-            else
-                s[v] += pp[v];
+        } else {
+            // every 16 B load of the partial issued before the first add: one
+            // memory round trip (the partials were written on other XCDs and
+            // miss this L2), not one per pair of terms
+            static_assert(kPartialStride >= kNacc + 1 && kPartialStride % 2 == 0, "partial stride");
+            double2 t[(kNacc + 1) / 2];
+#pragma unroll
+            for (int u = 0; u < (kNacc + 1) / 2; ++u) t[u] = reinterpret_cast<const double2*>(pp)[u];
+#pragma unroll
+            for (int v = 0; v < kNacc; ++v) s[v] += (v & 1) ? t[v >> 1].y : t[v >> 1].x;
         }
     }
 #pragma unroll
@@ -1280,15 +1295,43 @@ struct SolveArgs {
 // system is solved wave-parallel (det6_wave / ldlt_solve6_wave, bit-identical
 // to the single-lane det6 / ldlt_solve6); lane 0 stores.  Returns true when
 // the start finished.
+// A start's pose state as the solve reads it (previous fitness / rmse, T, G).
+// One vector load per lane (lane 0-1 prev, 2-17 T, 18-29 G), issued by the
+// caller before its reduction so that it overlaps it, then broadcast by
+// readlanes (no scalar loads: their SGPR pressure serialised them).
+struct PoseIn {
+    double pf, pr, T[16], G[12];
+};
+
+template <bool kAt>
+__device__ __forceinline__ double pose_lane_load(int slot, const SolveArgs& a) {
+    const int lane = threadIdx.x & 63;
+    const double* p = lane < 2 ? a.prev + 2 * slot + lane
+                      : lane < 18 ? a.T + 16 * slot + (lane - 2)
+                      : lane < 30 ? a.G + 12 * slot + (lane - 18)
+                                  : a.prev + 2 * slot;
+    return ld_f64<kAt>(p);
+}
+
+// every lane of the wave (readlane)
+__device__ __forceinline__ void pose_from_lanes(double v, PoseIn& p) {
+    p.pf = rl64(v, 0);
+    p.pr = rl64(v, 1);
+#pragma unroll
+    for (int t = 0; t < 16; ++t) p.T[t] = rl64(v, 2 + t);
+#pragma unroll
+    for (int t = 0; t < 12; ++t) p.G[t] = rl64(v, 18 + t);
+}
+
 template <int kEst, bool kAt = false>  // kEst 0: GeneralizedICP, 1: PointToPoint
 __device__ bool solve_start(int slot, const double s[kNacc], int64_t N, int pass, int max_iter, double rel_fit,
-                            double rel_rmse, const SolveArgs& a) {
+                            double rel_rmse, const SolveArgs& a, const PoseIn& pin) {
 #pragma clang fp contract(off)  // no fused multiply-add: the same rounding in every caller
     const int lane = threadIdx.x & 63;
     const double cnt = s[28];
     const double fit = cnt > 0 ? cnt / (double)N : 0.0;
     const double rmse = cnt > 0 ? sqrt(s[27] / cnt) : 0.0;
-    const double pf = ld_f64<kAt>(a.prev + 2 * slot), pr = ld_f64<kAt>(a.prev + 2 * slot + 1);
+    const double pf = pin.pf, pr = pin.pr;
     const bool converged = pass >= 1 && fabs(pf - fit) < rel_fit && fabs(pr - rmse) < rel_rmse;
     if (converged || pass >= max_iter) {
         if (lane == 0) {
@@ -1314,18 +1357,24 @@ __device__ bool solve_start(int slot, const double s[kNacc], int64_t N, int pass
         for (int r = 0; r < 6; ++r) b[r] = -s[21 + r];
         const double det = det6_wave(row, lane);
         if (!(fabs(det) < 1e-6 || isnan(det) || isinf(det))) {
-            double x[6];
-            ldlt_solve6_wave(row, b, x, lane);
+            // LDLT as the single-lane routine on every lane (uniform values):
+            // 6.5k cycles against 8.7k for ldlt_solve6_wave, whose readlane
+            // chains outweigh the row parallelism (tools/solve_bench.hip);
+            // det6_wave (2.2k vs 2.5k) and vec6_to_m4_wave (1.2k vs 3.1k) pay.
+            // All are bit-identical to each other (test_wave_solve_bit_identical).
+            double JTJ[36], x[6];
+            for (int i = 0, k = 0; i < 6; ++i)
+                for (int j = i; j < 6; ++j, ++k) JTJ[6 * i + j] = JTJ[6 * j + i] = s[k];
+            ldlt_solve6(JTJ, b, x);
             vec6_to_m4_wave(x, upd, lane);
         }
     }
-    double Tcur[16], Tn[16];
-    for (int t = 0; t < 16; ++t) Tcur[t] = ld_f64<kAt>(a.T + 16 * slot + t);
-    m4_mul(upd, Tcur, Tn);
+    double Tn[16];
+    m4_mul(upd, pin.T, Tn);
     if (lane == 0)
         for (int t = 0; t < 16; ++t) st_f64<kAt>(a.T + 16 * slot + t, Tn[t]);
     // Q = Tn * [G; 0 0 0 1]  (3x4), R = Tn[:3,:3]
-    const double* G = a.G + 12 * slot;
+    const double* G = pin.G;
     for (int r = 0; r < 3; ++r) {
         for (int c = 0; c < 4; ++c) {
             double v = Tn[4 * r + 0] * G[c] + Tn[4 * r + 1] * G[4 + c] + Tn[4 * r + 2] * G[8 + c];
@@ -1336,6 +1385,14 @@ __device__ bool solve_start(int slot, const double s[kNacc], int64_t N, int pass
             for (int c = 0; c < 3; ++c) st_f64<kAt>(a.R + 9 * slot + 3 * r + c, Tn[4 * r + c]);
     }
     return false;
+}
+
+template <int kEst, bool kAt = false>
+__device__ __forceinline__ bool solve_start(int slot, const double s[kNacc], int64_t N, int pass, int max_iter,
+                                            double rel_fit, double rel_rmse, const SolveArgs& a) {
+    PoseIn pin;
+    pose_from_lanes(pose_lane_load<kAt>(slot, a), pin);
+    return solve_start<kEst, kAt>(slot, s, N, pass, max_iter, rel_fit, rel_rmse, a, pin);
 }
 
 // Test entry (orpcd_test_solve6): for each of n systems (21 upper JTJ + 6 JTr),
@@ -1478,23 +1535,49 @@ __device__ __forceinline__ void gicp_block_terms(int slot, int ablk, const doubl
     for (int t = 0; t < 12; ++t) Q[t] = ld_f64<kPersist>(Qm + 12 * slot + t);
 #pragma unroll
     for (int t = 0; t < 9; ++t) R[t] = ld_f64<kPersist>(Rm + 9 * slot + t);
-    const int qpt = accum_qpt(N);
-    for (int k = 0; k < qpt; ++k) {
-        const int i = (ablk * qpt + k) * 256 + threadIdx.x;
-        if (i >= N) break;
-        const unsigned long long v = ld_u64<kPersist>(best + (size_t)slot * N + i);
-        const int j = v == kNone ? -1 : (int)(unsigned)(v & 0xffffffffu);
-        st_i32<kPersist>(prevnn + (size_t)slot * N + i, j >= 0 ? j : kNoMatch);
-        if constexpr (kPersist) st_u64<true>(best + (size_t)slot * N + i, kNone);
-        if (j < 0) continue;
-        const double p[3] = {src[3 * i], src[3 * i + 1], src[3 * i + 2]};
+    // Loads in two rounds for all of the thread's queries (best, source point
+    // and covariance; then the target point and covariance of each match),
+    // not three dependent round trips per query; the terms are then added in
+    // query order exactly as before.  Loads of a missing match read index 0.
+    constexpr int kQ = 4;
+    static_assert(kQ == accum_qpt(0), "accumulation queries per thread");
+    unsigned long long bv[kQ];
+    double p[kQ][3], cs[kQ][6], t3[kQ][3], ct[kQ][6];
+#pragma unroll
+    for (int k = 0; k < kQ; ++k) {
+        const int i = (ablk * kQ + k) * 256 + threadIdx.x;
+        const int ii = i < N ? i : 0;
+        bv[k] = i < N ? ld_u64<kPersist>(best + (size_t)slot * N + i) : kNone;
+#pragma unroll
+        for (int c = 0; c < 3; ++c) p[k][c] = src[3 * ii + c];
+        const double* cs6 = scov + ((size_t)slot * N + ii) * 6;
+#pragma unroll
+        for (int c = 0; c < 6; ++c) cs[k][c] = cs6[c];
+    }
+#pragma unroll
+    for (int k = 0; k < kQ; ++k) {
+        const int i = (ablk * kQ + k) * 256 + threadIdx.x;
+        const int j = bv[k] == kNone ? -1 : (int)(unsigned)(bv[k] & 0xffffffffu);
+        if (i < N) {
+            st_i32<kPersist>(prevnn + (size_t)slot * N + i, j >= 0 ? j : kNoMatch);
+            if constexpr (kPersist) st_u64<true>(best + (size_t)slot * N + i, kNone);
+        }
+        const int jj = j >= 0 ? j : 0;
+#pragma unroll
+        for (int c = 0; c < 3; ++c) t3[k][c] = ldg_f64(tgt64 + 3 * jj + c);
+#pragma unroll
+        for (int c = 0; c < 6; ++c) ct[k][c] = ldg_f64(tcov + (size_t)jj * 6 + c);
+    }
+#pragma unroll
+    for (int k = 0; k < kQ; ++k) {
+        if (bv[k] == kNone) continue;  // also every i >= N
         double q[3];
-        xform(Q, p, q);
-        const double d[3] = {q[0] - tgt64[3 * j], q[1] - tgt64[3 * j + 1], q[2] - tgt64[3 * j + 2]};
+        xform(Q, p[k], q);
+        const double d[3] = {q[0] - t3[k][0], q[1] - t3[k][1], q[2] - t3[k][2]};
         const double d2 = d[0] * d[0] + d[1] * d[1] + d[2] * d[2];
         if (!(d2 < r2)) continue;
-        const double* cs6 = scov + ((size_t)slot * N + i) * 6;
-        const double* ct6 = tcov + (size_t)j * 6;
+        const double* cs6 = cs[k];
+        const double* ct6 = ct[k];
         Sym3 Cs{cs6[0], cs6[1], cs6[2], cs6[3], cs6[4], cs6[5]};
         Cs = rotate_sym(R, Cs);
         const Sym3 Mm{Cs.xx + ct6[0], Cs.xy + ct6[1], Cs.xz + ct6[2], Cs.yy + ct6[3], Cs.yz + ct6[4],
@@ -1646,12 +1729,15 @@ __global__ __launch_bounds__(64) void reduce_partials_kernel(const double* __res
 }
 
 template <int kEst>  // 0: GeneralizedICP, 1: PointToPoint
-__global__ __launch_bounds__(64) void icp_solve_kernel(const int32_t* __restrict__ active,
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 2))) void icp_solve_kernel(const int32_t* __restrict__ active,
                                                         const double* __restrict__ partial, int nblk,
                                                         const double* __restrict__ sums_in, int64_t N, int pass,
                                                         int max_iter, double rel_fit, double rel_rmse, SolveArgs a) {
     const int slot = active[blockIdx.x];
-    if (a.done[slot]) return;
+    // the done flag, the partials and the pose are loaded together (one memory
+    // round trip after active[]); a finished start only wasted the loads
+    const int finished = __hip_atomic_load(a.done + slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const double pose = pose_lane_load<false>(slot, a);
     double s[kNacc];
     if (sums_in) {
 #pragma unroll
@@ -1659,7 +1745,10 @@ __global__ __launch_bounds__(64) void icp_solve_kernel(const int32_t* __restrict
     } else {
         reduce_partials(partial, slot, nblk, s);
     }
-    solve_start<kEst>(slot, s, N, pass, max_iter, rel_fit, rel_rmse, a);
+    if (finished) return;
+    PoseIn pin;
+    pose_from_lanes(pose, pin);
+    solve_start<kEst>(slot, s, N, pass, max_iter, rel_fit, rel_rmse, a, pin);
 }
 
 // --------------------------------------------------------------------------
