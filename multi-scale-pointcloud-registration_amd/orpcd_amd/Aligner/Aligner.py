@@ -137,12 +137,15 @@ class Aligner:
         tests/test_host.py::test_draw_block_matches_initialize_rotation)."""
         deg, uni, randn = self._deg, np.random.uniform, np.random.randn
         th = np.empty((n, 3))
-        t0s = []
+        g = np.empty((n, 3))
         for k in range(n):
-            th[k, 0] = uni(low=-deg, high=deg)
-            th[k, 1] = uni(low=-deg, high=deg)
-            th[k, 2] = uni(low=-deg, high=deg)
-            t0s.append(self._mu + randn(3) * self._std)
+            # uniform(size=3) consumes the stream as three scalar uniform()
+            # calls and returns the same values (low + (high - low) * double);
+            # the Gaussians stay one randn(3) per attempt (its cached second
+            # deviate makes the order matter)
+            th[k] = uni(-deg, deg, 3)
+            g[k] = randn(3)
+        t0s = list(self._mu + g * self._std)  # elementwise, as per attempt
         c, s = np.cos(th), np.sin(th)
         r = np.zeros((3, n, 3, 3))
         r[0, :, 0, 0] = 1.0
@@ -183,23 +186,32 @@ class Aligner:
         return R0s, t0s, Aligner._BlockStates(self, before, np.random.get_state(), self._attempts)
 
     def _run_tables(self, source, targets, draws):
-        """Per target k, the gathered per-attempt table of the starts draws[k]:
-        this rank runs its shard of every target's starts (concurrently when
-        the optimizer offers optimize_batch_multi), then one all-gather per
-        target."""
-        B = self._attempts
+        """Per target k, the gathered per-attempt table of the starts draws[k].
+        The K tables are sharded as ONE flat list of K x B starts (target-major):
+        this rank runs its contiguous block, which touches one or two targets
+        rather than all K (so it sets up only those targets), as one batch
+        (optimize_batch_multi when it spans several); one all-gather of the
+        flat table follows."""
+        B, K = self._attempts, len(draws)
         rank, ws = parallel.world()
-        lo, hi = parallel.shard(B, rank, ws)
-        locals_ = [np.zeros((0, parallel.REC)) for _ in targets]
+        lo, hi = parallel.shard(K * B, rank, ws)
+        local = np.zeros((0, parallel.REC))
         if hi > lo:
-            R0 = [np.array(d[0][lo:hi]) for d in draws]
-            t0 = [np.array(d[1][lo:hi]) for d in draws]
-            if len(targets) > 1 and hasattr(self._optimizer, "optimize_batch_multi"):
-                res = self._optimizer.optimize_batch_multi(source, targets, R0, t0)
+            ks, R0, t0 = [], [], []
+            for k in range(K):
+                a, b = max(lo - k * B, 0), min(hi - k * B, B)
+                if b > a:
+                    ks.append(k)
+                    R0.append(np.array(draws[k][0][a:b]))
+                    t0.append(np.array(draws[k][1][a:b]))
+            tg = targets(ks) if callable(targets) else [targets[k] for k in ks]
+            if len(tg) > 1 and hasattr(self._optimizer, "optimize_batch_multi"):
+                res = self._optimizer.optimize_batch_multi(source, tg, R0, t0)
             else:
-                res = [self._optimizer.optimize_batch(source, tg, r, t) for tg, r, t in zip(targets, R0, t0)]
-            locals_ = [parallel.pack(r) for r in res]
-        return [parallel.unpack(parallel.allgather_records(loc, B)) for loc in locals_]
+                res = [self._optimizer.optimize_batch(source, g, r, t) for g, r, t in zip(tg, R0, t0)]
+            local = np.concatenate([parallel.pack(r) for r in res])
+        table = parallel.allgather_records(local, K * B)
+        return [parallel.unpack(table[k * B:(k + 1) * B]) for k in range(K)]
 
     def _select(self, table, draw):
         """Aligner.py:178-202 over a finished table, in attempt order: strict <,
@@ -227,6 +239,26 @@ class Aligner:
                                  iters=int(table["iters"].sum()), rmse=table["rmse"].copy()))
         return self._select(table, draw)
 
+    def _scaled_targets(self, target, scales):
+        """[target * s for s in scales] (s of shape (1, 3)) as consecutive views
+        of one contiguous block that is reused across calls: the products are
+        taken column by column, elementwise as the broadcast product (the
+        broadcast over rows of 3 and fresh 1.2 MB allocations cost ~1 ms per
+        50k-point candidate; this ~0.1 ms).  An optimizer keeping a reference
+        to a target past its call must copy it (ours key their caches on the
+        content)."""
+        target = np.asarray(target, dtype=np.float64)
+        shape = (len(scales),) + target.shape
+        buf = getattr(self, "_scaled_buf", None)
+        if buf is None or buf.shape[1:] != target.shape or buf.shape[0] < len(scales):
+            buf = self._scaled_buf = np.empty((max(len(scales), 6),) + target.shape)
+        out = buf[: shape[0]]
+        for k, s in enumerate(scales):
+            s = np.asarray(s, dtype=np.float64).reshape(-1)
+            for c in range(target.shape[1]):
+                np.multiply(target[:, c], s[c], out=out[k, :, c])
+        return [out[k] for k in range(len(scales))]
+
     def _compass_iteration_speculative(self, source, target, scale_factors, optimal_metric):
         """One compass iteration (Aligner.py:270-297) with all six candidates'
         multistarts drawn up front (the RNG blocks the reference would draw if
@@ -242,7 +274,10 @@ class Aligner:
         state0 = np.random.get_state()
         draws = [self._draw_starts() for _ in steps]
         t_start = time.perf_counter()
-        tables = self._run_tables(source, [target * (scale_factors + d) for d in steps], draws)
+        # only the candidates this rank runs are scaled (target * (sf + d),
+        # Aligner.py:264-265), into one reused contiguous block
+        tables = self._run_tables(
+            source, lambda ks: self._scaled_targets(target, [scale_factors + steps[k] for k in ks]), draws)
         seconds = time.perf_counter() - t_start
         np.random.set_state(state0)
         new_metric = None

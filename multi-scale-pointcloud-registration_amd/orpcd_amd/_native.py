@@ -133,6 +133,19 @@ def _c3(a) -> np.ndarray:
     return a
 
 
+def _consecutive(ts):
+    """The (sum M_k, 3) array covering C-contiguous (M_k, 3) float64 clouds that
+    lie back to back in one buffer (the Aligner's scaled candidates), else
+    None (the caller concatenates)."""
+    addr = ts[0].ctypes.data
+    for t in ts:
+        if t.ctypes.data != addr or not t.flags.c_contiguous:
+            return None
+        addr += t.nbytes
+    return np.lib.stride_tricks.as_strided(ts[0], shape=(sum(len(t) for t in ts), 3), strides=ts[0].strides,
+                                           writeable=False)
+
+
 class Context:
     """One device context (stream + device-resident clouds).  Not thread-safe."""
 
@@ -195,7 +208,9 @@ class Context:
             return
         self._target_key = None
         m = np.array([len(t) for t in ts], np.int64)
-        xyz = np.ascontiguousarray(np.concatenate(ts, axis=0))
+        xyz = _consecutive(ts)
+        if xyz is None:
+            xyz = np.ascontiguousarray(np.concatenate(ts, axis=0))
         self._check(self._L.orpcd_set_targets(self._h, xyz, m, len(ts), float(epsilon)), "orpcd_set_targets")
         self._target_key = key if len(ts) > 1 else (self._key(ts[0]), float(epsilon))
 

@@ -4,8 +4,11 @@
 (Aligner.py:178-202) are independent: every rank replays the identical host RNG stream, runs a
 contiguous block of attempts on its own GPU, and one all-gather of a fixed
 160-byte record per attempt gives every rank the full table, on which each
-applies the reference's strict-< argmin in attempt order.  No other data-path
-collective exists.
+applies the reference's strict-< argmin in attempt order.  A speculative
+compass iteration (six candidate multistarts) is sharded as one flat,
+target-major list of 6 x attempts starts with one all-gather, so a rank's
+block spans one or two candidate targets.  No other data-path collective
+exists.
 
 2. Row sharding of one start (C5: one GICP over 1M points).  Each rank owns
 a contiguous block of source rows (covariances still from the full cloud's

@@ -18,18 +18,18 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, out_dir):
+def _worker(rank, world, port, out_dir, speculative=False):
     sys.path[:0] = [PKG, os.path.join(REPO, "tests", "golden"), os.path.join(REPO, "tests")]
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     import torch.distributed as dist
     dist.init_process_group("gloo", rank=rank, world_size=world)
     from orpcd_amd import Aligner, Preprocessor
     from scripted import ScriptedOptimizer
-    from test_host import BatchedScripted
+    from test_host import BatchedScripted, SpeculativeScripted
     g = np.load(f"{GOLDEN}/g3_aligner_trace.npz")
     np.random.seed(7)
     inner = ScriptedOptimizer(g["goal"], mode="scripted")
-    opt = BatchedScripted(inner)
+    opt = (SpeculativeScripted if speculative else BatchedScripted)(inner)
     al = Aligner(Preprocessor([]), Preprocessor([]), opt, attempts=4)
     T, m, sf, err = al.align(g["src"].copy(), g["tgt"].copy(), refine_registration=False)
     np.savez(os.path.join(out_dir, f"rank{rank}.npz"), T=T, m=m, sf=sf, err=np.asarray(err),
@@ -53,6 +53,23 @@ def test_sharded_multistart_matches_reference_trace(tmp_path, world):
     # attempts (4 per multistart) were split over the ranks, each multistart
     per_ms = np.sum(np.stack(shards), axis=0)
     assert np.all(per_ms == 4) and all(np.all(s < 4) for s in shards)
+
+
+@pytest.mark.parametrize("world", [2, 3, 5])
+def test_sharded_speculative_compass_matches_reference_trace(tmp_path, world):
+    """The speculative compass over ranks: each compass iteration's 6 x 4
+    starts are sharded as one flat list (a rank's block spans one or two
+    candidates), one all-gather per iteration; every rank reproduces the
+    reference's align() (G3) and its RNG position."""
+    import torch.multiprocessing as mp
+    mp.start_processes(_worker, args=(world, _free_port(), str(tmp_path), True), nprocs=world, join=True,
+                       start_method="spawn")
+    g = np.load(f"{GOLDEN}/g3_aligner_trace.npz")
+    for r in range(world):
+        z = np.load(tmp_path / f"rank{r}.npz")
+        assert np.array_equal(z["T"], g["scripted_T"]) and z["m"] == g["scripted_metric"]
+        assert np.array_equal(z["sf"], g["scripted_sf"]) and np.array_equal(z["err"], g["scripted_errors"])
+        assert np.array_equal(z["rng"], g["scripted_rng_after"])
 
 
 def test_record_pack_roundtrip():

@@ -8,8 +8,9 @@ per multistart -- on one GPU, and its strong-scaling projection to G ranks.
    table of per-start records is kept, in call order.
 2. Rank r of G (r = 0..G-1): the same align() (same seed, hence the same
    control flow and RNG stream) with parallel.world() -> (r, G): the rank
-   runs only its contiguous block of every multistart's starts
-   (parallel.shard) on this GPU, alone.  The all-gather is replayed from
+   runs only its contiguous block of every call's starts (parallel.shard of
+   the initial multistart, or of a compass iteration's six candidates as one
+   flat list) on this GPU, alone.  The all-gather is replayed from
    step 1's tables after checking that the rank's own rows are bit-identical
    to them (sharding never changes a start's result).  Each rank's time per
    _run_tables call (one compass iteration's six candidate shards, or the
