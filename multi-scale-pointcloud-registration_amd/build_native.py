@@ -38,8 +38,12 @@ def _stale(target, deps):
     return any(os.path.getmtime(d) > t for d in deps)
 
 
+# instrumented variants (ORPCD_EXTRA_FLAGS) keep objects of their own per flag set
+OBJ_DIR = OBJ + ("_" + "".join(c if c.isalnum() else "_" for c in "".join(EXTRA)) if EXTRA else "")
+
+
 def _compile(src, force):
-    obj = os.path.join(OBJ + ("_x" if EXTRA else ""), os.path.basename(src) + ".o")
+    obj = os.path.join(OBJ_DIR, os.path.basename(src) + ".o")
     if force or _stale(obj, [src] + _headers()):
         cmd = [HIPCC] + CXXFLAGS + ["-c", src, "-o", obj]
         r = subprocess.run(cmd, capture_output=True, text=True)
@@ -49,7 +53,7 @@ def _compile(src, force):
 
 
 def build(force: bool = False, verbose: bool = False) -> str:
-    os.makedirs(OBJ + ("_x" if EXTRA else ""), exist_ok=True)
+    os.makedirs(OBJ_DIR, exist_ok=True)
     os.makedirs(LIBDIR, exist_ok=True)
     srcs = sorted(glob.glob(os.path.join(CSRC, "*.hip")))
     with ThreadPoolExecutor(max_workers=min(8, len(srcs))) as ex:

@@ -37,6 +37,10 @@
 //  * icp_solve_kernel: per start, fixed-order reduction, convergence test,
 //    6x6 LDLT solve and pose update; then xform_queries_kernel writes the fp32
 //    queries of the next pass (fp64 transform, one rounding).
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+
 #include "device_math.h"
 #include "orpcd_internal.h"
 #include "wave_ops.h"
@@ -442,6 +446,46 @@ static inline float search_r2(double r2) { return (float)(r2 * (1.0 + 1e-5)) * 1
 // any closer one) is re-found by the scan (1e-4 >> the 2^-17 key truncation)
 constexpr float kSeedSlack = 1.0001f;
 
+// ---------------------------------------------------------------------------
+// Cost-ordered search dispatch (opt.sched).  The search of pass p measures
+// each wave's duration (s_memrealtime, 10 ns ticks) and sums it per (start,
+// 128-query group) into wcost[p & 1] and over the pass into wtot[p & 1].  The
+// query transform of pass p + 1 (one thread per group) splits a group into
+// S = ceil(cost / (pass total / sched_items)) waves (1..64; the uniform host
+// split at pass 0, when no cost is known), files its S work items under the
+// cost class of one split (log2 of cost / S, heaviest = class 0) and the
+// search of pass p + 1 takes item k of the class-major list as wave k: the
+// heaviest waves are dispatched first and no wave is much longer than the
+// pass total / sched_items, so the launch no longer ends with a few long
+// waves on an idle chip (measured per-wave timelines: the last 1% of a
+// launch's waves held 15-35% of its span).  Splits and order never change
+// an answer (every split returns the lexicographic (masked d^2, index)
+// minimum over its tiles, merged by atomicMin).
+// item: slot << 48 | target << 44 | group << 20 | split << 8 | S
+__host__ __device__ __forceinline__ unsigned long long sched_item(int slot, int k, int wg, int split, int S) {
+    return ((unsigned long long)slot << 48) | ((unsigned long long)k << 44) | ((unsigned long long)wg << 20) |
+           ((unsigned long long)split << 8) | (unsigned long long)S;
+}
+struct SchedX {                          // query transform side (pass p + 1)
+    const unsigned* wcost_prev;          // the previous pass's per-group costs (B x NG)
+    unsigned* wcost_cur;                 // this pass's: zeroed for the search
+    const unsigned long long* wtot_prev; // the previous pass's total (kSchedTot words)
+    unsigned* cnt;                       // this pass's items per class (zeroed by the previous search)
+    unsigned long long* list;            // class-major items, cap per class
+    int cap, NG, have_cost, S0;          // S0: the host's uniform split (no cost known)
+    float inv_want;                      // 1 / sched_items
+};
+struct SchedS {                          // search side (pass p)
+    const unsigned* cnt;                 // this pass's items per class
+    unsigned* cnt_next;                  // the next pass's: zeroed here (block 0)
+    const unsigned long long* list;
+    unsigned* wcost;                     // this pass's per-group costs
+    unsigned long long* wtot;            // this pass's total
+    unsigned long long* wtot_next;       // the next pass's: zeroed here (block 0; read by this
+                                         // pass's transform, which ran before)
+    int cap, NG, B;
+};
+
 // fp32 queries of every running start for the next pass: q = fp32(Q * p),
 // and in q.w the query's search bound: d^2 to its previous correspondence
 // (x 1 + 1e-4), or, without one, to the nearest of a strided set of tile
@@ -455,11 +499,12 @@ __global__ __launch_bounds__(256) void xform_queries_kernel(const double* __rest
                                                             float r2s, int reseed, float4* __restrict__ q32,
                                                             unsigned long long* __restrict__ best,
                                                             const int32_t* __restrict__ nact_dev,
-                                                            float4* __restrict__ gbox) {
+                                                            float4* __restrict__ gbox, SchedX sx) {
     if (nact_dev && (int)blockIdx.y >= *nact_dev) return;  // pipelined: grid sized for an upper bound
     const int slot = active[blockIdx.y];
     if (done[slot]) return;
-    const TargetDesc& tg = tdesc[target_of_row(tb, blockIdx.y)];
+    const int tk = target_of_row(tb, blockIdx.y);
+    const TargetDesc& tg = tdesc[tk];
     const float4* __restrict__ p4 = tg.p4;
     const int i = blockIdx.x * 256 + threadIdx.x;
     const bool valid = i < N;
@@ -502,51 +547,118 @@ __global__ __launch_bounds__(256) void xform_queries_kernel(const double* __rest
                            __uint_as_float(max(__float_as_uint(a[6]), __float_as_uint(b[6]))));
         g[1] = make_float4(fmaxf(a[3], b[3]), fmaxf(a[4], b[4]), fmaxf(a[5], b[5]), 0.0f);
     }
+    if (!sx.list || blockIdx.x != 0) return;
+    // ordered dispatch: block 0 of each start files the work items of all the
+    // start's 128-query groups (they depend only on the previous pass's
+    // costs).  Counts per class are aggregated in LDS first, so a pass takes
+    // kSchedClasses global atomics per start (one counter per class shared by
+    // every group had serialised ~12k atomics per pass on a few addresses).
+    __shared__ float s_target;
+    __shared__ unsigned lcnt[kSchedClasses], lbase[kSchedClasses];
+    if (threadIdx.x < kSchedClasses) lcnt[threadIdx.x] = 0u;
+    if (threadIdx.x < 64) {
+        float t = 0.0f;
+        if (sx.have_cost) {
+            t = (float)sx.wtot_prev[lane];
+#pragma unroll
+            for (int o = 32; o >= 1; o >>= 1) t += __shfl_xor(t, o);
+        }
+        if (lane == 0) s_target = fmaxf(t * sx.inv_want, 1.0f);
+    }
+    __syncthreads();
+    const int NG = sx.NG;
+    const unsigned* cost = sx.wcost_prev + (size_t)slot * NG;
+    auto plan = [&](int g, int& S, int& cls) {
+        S = sx.S0;
+        cls = kSchedClasses - 1;
+        if (sx.have_cost) {
+            const unsigned C = cost[g];
+            S = min(64, max(1, (int)ceilf((float)C / s_target)));
+            const unsigned per = C / (unsigned)S + 1u;
+            cls = max(0, kSchedClasses - 1 - (31 - __builtin_clz(per)));  // log2 of a split's cost, heaviest first
+        }
+    };
+    for (int g = threadIdx.x; g < NG; g += blockDim.x) {  // 1: items per class
+        int S, cls;
+        plan(g, S, cls);
+        atomicAdd(lcnt + cls, (unsigned)S);
+    }
+    __syncthreads();
+    if (threadIdx.x < kSchedClasses) {
+        const unsigned n = lcnt[threadIdx.x];
+        lbase[threadIdx.x] = n ? atomicAdd(sx.cnt + threadIdx.x, n) : 0u;
+        lcnt[threadIdx.x] = 0u;
+    }
+    __syncthreads();
+    for (int g = threadIdx.x; g < NG; g += blockDim.x) {  // 2: the items
+        int S, cls;
+        plan(g, S, cls);
+        const unsigned at = lbase[cls] + atomicAdd(lcnt + cls, (unsigned)S);
+        sx.wcost_cur[(size_t)slot * NG + g] = 0u;
+        unsigned long long* out = sx.list + (size_t)cls * sx.cap + at;
+        for (int k = 0; k < S; ++k) out[k] = sched_item(slot, tk, g, k, S);
+    }
 }
+
+#ifdef ORPCD_WAVETIME
+// per-wave timeline of nn_search_kernel launches (instrumented builds only):
+// (entry, exit) in s_memrealtime ticks (100 MHz), and (start row, block, wave,
+// quarters scanned)
+constexpr unsigned kWtMax = 1u << 20;
+__device__ unsigned long long g_wt[3 * kWtMax];
+#endif
 
 // --------------------------------------------------------------------------
 // Search kernel: grid = (blocks per start * S, running starts), 4 waves/block.
 // --------------------------------------------------------------------------
-__device__ __forceinline__ void nn_search_body(
-    const float4* __restrict__ q32, int N, const TargetDesc& tg, int super_cull, const int32_t* __restrict__ active,
-    const int32_t* __restrict__ done, int S, unsigned long long* __restrict__ best,
-    unsigned long long* __restrict__ counters, int by, int bx, int wid, float4* stage_w,
-    const float4* __restrict__ gbox) {
+// first culling round's super-tile boxes: independent of the start and its
+// queries, so their load overlaps the slot and query loads (xyz only, by raw
+// buffer loads: lanes past nsuper read zeros, unguarded; a guarded 16 B load
+// whose unused .w register was reused forced a wait for it before the query
+// loads were issued)
+// The search layout of one target, read once from its TargetDesc.
+struct SearchTgt {
+    const float4 *p4, *tlo, *thi, *qbox, *slo, *shi;
+    int ntiles, nsuper;
+};
+__device__ __forceinline__ SearchTgt search_tgt(const TargetDesc& tg) {
+    return SearchTgt{tg.p4, tg.tlo, tg.thi, tg.qbox, tg.slo, tg.shi, tg.ntiles, tg.nsuper};
+}
+
+__device__ __forceinline__ void load_super0(const SearchTgt& tg, float4& s0lo, float4& s0hi) {
     const int lane = threadIdx.x & 63;
-    const float4* __restrict__ p4 = tg.p4;
-    const float4* __restrict__ tlo = tg.tlo;
-    const float4* __restrict__ thi = tg.thi;
-    const float4* __restrict__ qbox = tg.qbox;
-    const float4* __restrict__ slo = tg.slo;
-    const float4* __restrict__ shi = tg.shi;
-    const int ntiles = tg.ntiles, nsuper = tg.nsuper;
-    // first culling round's super-tile boxes: independent of the start and
-    // its queries, so their load overlaps the slot and query loads
-    // (xyz only, by raw buffer loads: lanes past nsuper read zeros, unguarded;
-    // a guarded 16 B load whose unused .w register was reused forced a wait
-    // for it before the query loads were issued)
-    float4 s0lo, s0hi;
-    {
-        const int nb = nsuper * (int)sizeof(float4);
-        const auto lo = __builtin_amdgcn_raw_buffer_load_b96(
-            __builtin_amdgcn_make_buffer_rsrc(const_cast<float4*>(slo), (short)0, nb, 0x00020000), lane * 16, 0, 0);
-        const auto hi = __builtin_amdgcn_raw_buffer_load_b96(
-            __builtin_amdgcn_make_buffer_rsrc(const_cast<float4*>(shi), (short)0, nb, 0x00020000), lane * 16, 0, 0);
-        s0lo = make_float4(__uint_as_float(lo[0]), __uint_as_float(lo[1]), __uint_as_float(lo[2]), 0.f);
-        s0hi = make_float4(__uint_as_float(hi[0]), __uint_as_float(hi[1]), __uint_as_float(hi[2]), 0.f);
-    }
-    const int slot = active[by];
-    if (done[slot]) return;
+    const int nb = tg.nsuper * (int)sizeof(float4);
+    const auto lo = __builtin_amdgcn_raw_buffer_load_b96(
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<float4*>(tg.slo), (short)0, nb, 0x00020000), lane * 16, 0, 0);
+    const auto hi = __builtin_amdgcn_raw_buffer_load_b96(
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<float4*>(tg.shi), (short)0, nb, 0x00020000), lane * 16, 0, 0);
+    s0lo = make_float4(__uint_as_float(lo[0]), __uint_as_float(lo[1]), __uint_as_float(lo[2]), 0.f);
+    s0hi = make_float4(__uint_as_float(hi[0]), __uint_as_float(hi[1]), __uint_as_float(hi[2]), 0.f);
+}
+
+// One wave's search: split `split` of S of the 128-query group wg of start
+// `slot` (queries wg * 128 + lane + 64 k).  Returns quarters scanned.
+__device__ __forceinline__ int search_group(const float4* __restrict__ q32, int N, const SearchTgt tg,
+                                            int super_cull, int S, int split, int slot, int wg,
+                                            unsigned long long* __restrict__ best,
+                                            unsigned long long* __restrict__ counters, unsigned cslot,
+                                            float4* stage_w, const float4* __restrict__ gbox, float4 s0lo,
+                                            float4 s0hi) {
+    const int lane = threadIdx.x & 63;
 #ifdef ORPCD_PHASES
     const unsigned long long ph_t0 = __builtin_readcyclecounter();
 #endif
-    const int grp = bx / S, split = bx - grp * S;
-    if (grp * kCBlockQ + wid * (64 * kCQPT) >= N) return;  // a wave past the last query group (no gbox entry)
-    const int i0 = grp * kCBlockQ + wid * (64 * kCQPT) + lane;
+    // wave-uniform by construction; readfirstlane keeps them (and the group's
+    // box record address) in scalar registers
+    slot = __builtin_amdgcn_readfirstlane(slot);
+    wg = __builtin_amdgcn_readfirstlane(wg);
+    S = __builtin_amdgcn_readfirstlane(S);
+    split = __builtin_amdgcn_readfirstlane(split);
+    const int i0 = wg * (64 * kCQPT) + lane;
     float qx[kCQPT], qy[kCQPT], qz[kCQPT], bound[kCQPT], bd[kCQPT];
     int bj[kCQPT];
     const float4* qs = q32 + (size_t)slot * N;
-    const float4* gb = gbox + ((size_t)slot * ((N + 127) / 128) + grp * kCWaves + __builtin_amdgcn_readfirstlane(wid)) * 2;
+    const float4* gb = gbox + ((size_t)slot * ((N + 127) / 128) + wg) * 2;
     // the queries by raw buffer loads: a lane past N reads zeros (bound 0: never
     // takes anything) without a guard.  Guarded global loads were each put in
     // a branch with its own wait, which serialised the two.
@@ -565,15 +677,16 @@ __device__ __forceinline__ void nn_search_body(
     const float wq = __uint_as_float(wave_umax(__float_as_uint(qx[0] + qy[1])));  // the query loads have landed
     const unsigned long long ph_t1 = __builtin_readcyclecounter() + (wq == 1.2345f ? 1 : 0);
     unsigned long long ph_cull[5] = {0, 0, 0, 0, 0};
-    const int visited = culled_search<true>(stage_w, p4, tlo, thi, qbox, ntiles, slo, shi, nsuper, super_cull, S, split, qx,
-                                      qy, qz, bound, bd, bj, s0lo, s0hi, gb, ph_cull);
+    const int visited = culled_search<true>(stage_w, tg.p4, tg.tlo, tg.thi, tg.qbox, tg.ntiles, tg.slo, tg.shi,
+                                            tg.nsuper, super_cull, S, split, qx, qy, qz, bound, bd, bj, s0lo, s0hi,
+                                            gb, ph_cull);
 #else
-    const int visited =
-        culled_search<true>(stage_w, p4, tlo, thi, qbox, ntiles, slo, shi, nsuper, super_cull, S, split, qx, qy, qz, bound,
-                      bd, bj, s0lo, s0hi, gb);
+    const int visited = culled_search<true>(stage_w, tg.p4, tg.tlo, tg.thi, tg.qbox, tg.ntiles, tg.slo, tg.shi,
+                                            tg.nsuper, super_cull, S, split, qx, qy, qz, bound, bd, bj, s0lo, s0hi,
+                                            gb);
 #endif
     if (lane == 0 && counters) {  // spread over kCounterSlots cache lines (one address serialises)
-        unsigned long long* cs = counters + kCounterStride * ((bx * kCWaves + wid + by) % kCounterSlots);
+        unsigned long long* cs = counters + kCounterStride * (cslot % kCounterSlots);
         atomicAdd(cs, (unsigned long long)visited);
         atomicMax(cs + 1, (unsigned long long)visited);
 #ifdef ORPCD_PHASES
@@ -599,6 +712,109 @@ __device__ __forceinline__ void nn_search_body(
             out[i] = v;
         else if (v != kNone)
             atomicMin(out + i, v);
+    }
+    return visited;
+}
+
+// Uniform-split dispatch: grid = (blocks per start * S, running starts), 4 waves/block.
+__device__ __forceinline__ void nn_search_body(
+    const float4* __restrict__ q32, int N, const TargetDesc& tg, int super_cull, const int32_t* __restrict__ active,
+    const int32_t* __restrict__ done, int S, unsigned long long* __restrict__ best,
+    unsigned long long* __restrict__ counters, int by, int bx, int wid, float4* stage_w,
+    const float4* __restrict__ gbox) {
+#ifdef ORPCD_WAVETIME
+    const unsigned long long wt0 = __builtin_amdgcn_s_memrealtime();
+#endif
+    const SearchTgt st = search_tgt(tg);
+    float4 s0lo, s0hi;
+    load_super0(st, s0lo, s0hi);
+    const int slot = active[by];
+    if (done[slot]) return;
+    const int grp = bx / S, split = bx - grp * S;
+    const int wg = grp * kCWaves + wid;
+    if (wg * (64 * kCQPT) >= N) return;  // a wave past the last query group (no gbox entry)
+    const int visited = search_group(q32, N, st, super_cull, S, split, slot, wg, best, counters,
+                                     (unsigned)(bx * kCWaves + wid + by), stage_w, gbox, s0lo, s0hi);
+    (void)visited;
+#ifdef ORPCD_WAVETIME
+    if ((threadIdx.x & 63) == 0) {  // a fixed slot per wave: no shared counter to serialise on
+        const unsigned k = ((unsigned)blockIdx.y * gridDim.x + blockIdx.x) * kCWaves + wid;
+        if (k < kWtMax) {
+            g_wt[3 * k] = wt0;
+            g_wt[3 * k + 1] = __builtin_amdgcn_s_memrealtime();
+            g_wt[3 * k + 2] = ((unsigned long long)by << 48) | ((unsigned long long)bx << 24) |
+                              ((unsigned long long)wid << 20) | (unsigned long long)(visited & 0xFFFFF);
+        }
+    }
+#endif
+}
+
+// Ordered dispatch (SchedS): wave k of the launch takes item k of the
+// class-major list, heaviest class first; the wave's duration is added to its
+// group's cost and to the pass total for the next pass's schedule.
+__global__ __launch_bounds__(kCBlock) __attribute__((amdgpu_waves_per_eu(5, 8))) void nn_search_sched_kernel(
+    const float4* __restrict__ q32, int N, const TargetDesc* __restrict__ tdesc, int super_cull,
+    unsigned long long* __restrict__ best, unsigned long long* __restrict__ counters,
+    const float4* __restrict__ gbox, SchedS sa) {
+    __shared__ float4 stage[kCWaves][kTile];
+    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+    const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    if (blockIdx.x == 0 && wid == 0) {
+        if (lane < kSchedClasses) sa.cnt_next[lane] = 0u;
+        sa.wtot_next[lane] = 0ull;  // kSchedTot == 64
+    }
+    const unsigned w = __builtin_amdgcn_readfirstlane(blockIdx.x * kCWaves + wid);
+    unsigned base = 0, off = 0;
+    int cls = -1;
+#pragma unroll
+    for (int c = 0; c < kSchedClasses; ++c) {
+        const unsigned n = __builtin_amdgcn_readfirstlane(sa.cnt[c]);
+        if (cls < 0 && w < base + n) {
+            cls = c;
+            off = w - base;
+        }
+        base += n;
+    }
+    if (cls < 0) return;  // past the pass's items
+#ifdef ORPCD_SCHED_CHECK
+    if (base > (unsigned)sa.cap || off >= (unsigned)sa.cap) {
+        if (lane == 0 && w < 4) printf("[sched] counts %u exceed cap %d (w %u cls %d off %u)\n", base, sa.cap, w, cls, off);
+        return;
+    }
+#endif
+    const unsigned long long itv = sa.list[(size_t)cls * sa.cap + off];
+    // wave-uniform: scalar registers (readfirstlane returns int: widen through
+    // unsigned, or a low word with bit 31 set would sign-extend into the high one)
+    const unsigned long long it =
+        ((unsigned long long)(unsigned)__builtin_amdgcn_readfirstlane((unsigned)(itv >> 32)) << 32) |
+        (unsigned long long)(unsigned)__builtin_amdgcn_readfirstlane((unsigned)itv);
+    const int slot = (int)(it >> 48), tk = (int)((it >> 44) & 15u), wg = (int)((it >> 20) & 0xFFFFFFu);
+    const int split = (int)((it >> 8) & 0xFFu), S = (int)(it & 0xFFu);
+#ifdef ORPCD_SCHED_CHECK
+    if (slot >= sa.B || wg >= sa.NG || tk >= kMaxTargets || S < 1 || S > 64 || split >= S || wg * 128 >= N) {
+        if (lane == 0) printf("[sched] bad item w %u cls %d off %u: slot %d tk %d wg %d split %d S %d\n", w, cls, off, slot, tk, wg, split, S);
+        return;
+    }
+#endif
+    const SearchTgt st = search_tgt(tdesc[tk]);
+    float4 s0lo, s0hi;
+    load_super0(st, s0lo, s0hi);
+    const int visited = search_group(q32, N, st, super_cull, S, split, slot, wg, best, counters, w, stage[wid], gbox,
+                                     s0lo, s0hi);
+    (void)visited;
+    if (lane == 0) {
+        const unsigned long long t1 = __builtin_amdgcn_s_memrealtime();
+        const unsigned d = (unsigned)min(t1 - t0, 0xFFFFFFull);
+        atomicAdd(sa.wcost + (size_t)slot * sa.NG + wg, d);
+        atomicAdd(sa.wtot + (w & (kSchedTot - 1)), (unsigned long long)d);
+#ifdef ORPCD_WAVETIME
+        if (w < kWtMax) {
+            g_wt[3 * w] = t0;
+            g_wt[3 * w + 1] = t1;
+            g_wt[3 * w + 2] = ((unsigned long long)slot << 48) | ((unsigned long long)wg << 24) |
+                              ((unsigned long long)(S > 15 ? 15 : S) << 20) | (unsigned long long)(visited & 0xFFFFF);
+        }
+#endif
     }
 }
 
@@ -2112,12 +2328,53 @@ static bool use_two_phase(const orpcd_ctx* c) {
     return c->opt.search_kernel == 2 && c->two_phase_ok && c->batch_ntgt == 1;
 }
 
-hipError_t launch_xform(const orpcd_ctx* c, int nact, double r2, hipStream_t s, bool dev_nact, const TgtBounds& tb) {
+// uniform splits of a launch over nact running starts (the pass-0 split of
+// the ordered dispatch too)
+static int uniform_splits(const orpcd_ctx* c, int nact) {
+    const int sblk = (int)((c->src.n + kCBlockQ - 1) / kCBlockQ);
+    const int want = nact <= c->opt.small_batch ? c->opt.search_waves / 2 : c->opt.search_waves;
+    return search_splits(nact, sblk, want);
+}
+
+// the ordered dispatch serves the default per-kernel pass loop (not the
+// cooperative / two-phase searches, the persistent or the pipelined loops)
+bool sched_wanted(const orpcd_ctx* c, bool persist) {
+    static const bool trace = getenv("ORPCD_TRACE") != nullptr;
+    return c->opt.sched && c->opt.search_kernel == 0 && !persist && (trace || !pipelined_ok(c));
+}
+
+// items per class: every item of a pass may fall in one class.  Pass 0:
+// S0 * groups <= search_waves + groups (search_splits rounds up); later
+// passes: sum ceil(cost / (total / sched_items)) <= sched_items + groups,
+// doubled against float rounding of the per-group quotients.
+int sched_capacity(const orpcd_ctx* c, int B) {
+    const int64_t NG = (c->src.n + 127) / 128;
+    return (int)(std::max<int64_t>(c->opt.sched_items, c->opt.search_waves) + 2 * (int64_t)B * NG + 64);
+}
+
+hipError_t launch_xform(const orpcd_ctx* c, int nact, int pass, double r2, hipStream_t s, bool dev_nact,
+                        const TgtBounds& tb) {
     if (use_coop(c) || use_two_phase(c)) return hipSuccess;  // these searches transform their own queries
     const int N = (int)c->src.n;
+    SchedX sx{};
+    if (c->sched_live && !dev_nact) {
+        const size_t B = (size_t)c->sched_B;
+        const size_t NG = (size_t)(N + 127) / 128;
+        const int par = pass & 1;
+        sx.wcost_prev = c->wcost.p + (size_t)(par ^ 1) * B * NG;
+        sx.wcost_cur = c->wcost.p + (size_t)par * B * NG;
+        sx.wtot_prev = c->wtot.p + (size_t)(par ^ 1) * kSchedTot;
+        sx.cnt = c->wcnt.p + (size_t)par * kSchedClasses;
+        sx.list = c->wlist.p;
+        sx.cap = c->sched_cap;
+        sx.NG = (int)NG;
+        sx.have_cost = pass > 0;
+        sx.S0 = uniform_splits(c, nact);
+        sx.inv_want = 1.0f / (float)c->opt.sched_items;
+    }
     xform_queries_kernel<<<dim3((unsigned)((N + 255) / 256), (unsigned)nact), 256, 0, s>>>(
         c->src.xyz64.p, N, c->active.p, c->Q.p, c->done.p, c->tdesc.p, tb, c->prevnn.p, search_r2(r2),
-        c->opt.reseed, c->q32.p, c->best.p, dev_nact ? c->ctl.p : nullptr, c->gbox.p);
+        c->opt.reseed, c->q32.p, c->best.p, dev_nact ? c->ctl.p : nullptr, c->gbox.p, sx);
     return hipGetLastError();
 }
 
@@ -2198,8 +2455,33 @@ hipError_t launch_gicp_pass_pipelined(const orpcd_ctx* c, int nact_host, int pas
     if ((e = hipGetLastError()) != hipSuccess) return e;
     if (after_accum && (e = hipEventRecord(after_accum, s)) != hipSuccess) return e;
     if (pass >= p.max_iteration) return hipSuccess;  // every start is done after this pass
-    return launch_xform(c, nact_host, r2, s, true, tb);
+    return launch_xform(c, nact_host, pass + 1, r2, s, true, tb);
 }
+
+#ifdef ORPCD_WAVETIME
+// append the records of the last search launch (n wave slots) to $ORPCD_WAVETIME
+static hipError_t dump_wavetime(int pass, int nact, int S, unsigned n, hipStream_t s) {
+    const char* path = getenv("ORPCD_WAVETIME");
+    if (!path) return hipSuccess;
+    hipError_t e;
+    if ((e = hipStreamSynchronize(s)) != hipSuccess) return e;
+    n = std::min(n, kWtMax);
+    std::vector<unsigned long long> h((size_t)3 * n), keep;
+    void* dp = nullptr;
+    if ((e = hipGetSymbolAddress(&dp, HIP_SYMBOL(g_wt))) != hipSuccess) return e;
+    if ((e = hipMemcpy(h.data(), dp, h.size() * 8, hipMemcpyDeviceToHost)) != hipSuccess) return e;
+    if ((e = hipMemset(dp, 0, h.size() * 8)) != hipSuccess) return e;
+    for (unsigned k = 0; k < n; ++k)  // waves that searched (others exited early)
+        if (h[3 * k] != 0) keep.insert(keep.end(), h.begin() + 3 * k, h.begin() + 3 * k + 3);
+    if (FILE* f = fopen(path, "ab")) {
+        const int hdr[4] = {pass, nact, S, (int)(keep.size() / 3)};
+        fwrite(hdr, 4, 4, f);
+        fwrite(keep.data(), 8, keep.size(), f);
+        fclose(f);
+    }
+    return hipSuccess;
+}
+#endif
 
 hipError_t launch_gicp_pass(const orpcd_ctx* c, int nact, int pass, double r2, hipStream_t s, hipEvent_t mid,
                             const TgtBounds& tb) {
@@ -2237,16 +2519,44 @@ hipError_t launch_gicp_pass(const orpcd_ctx* c, int nact, int pass, double r2, h
             c->tgt.p4.p, c->tgt.tlo.p, c->tgt.thi.p, (int)c->tgt.ntiles, c->tgt.slo.p, c->tgt.shi.p,
             (int)c->tgt.nsuper, c->active.p, c->done.p, c->best.p, c->count_tiles ? c->counters.p : nullptr,
             org_of(c->tgt));
+    } else if (c->sched_live) {
+        // ordered dispatch: the items were filed by this pass's query transform;
+        // the grid covers their upper bound (surplus waves exit at once)
+        const int64_t NG = (N + 127) / 128;
+        const int64_t items = pass == 0 ? (int64_t)uniform_splits(c, nact) * nact * NG
+                                        : (int64_t)c->opt.sched_items + 2 * (int64_t)nact * NG + 64;
+        const int64_t B = c->sched_B;
+        const int par = pass & 1;
+        SchedS sa{};
+        sa.cnt = c->wcnt.p + (size_t)par * kSchedClasses;
+        sa.cnt_next = c->wcnt.p + (size_t)(par ^ 1) * kSchedClasses;
+        sa.list = c->wlist.p;
+        sa.wcost = c->wcost.p + (size_t)par * B * NG;
+        sa.wtot = c->wtot.p + (size_t)par * kSchedTot;
+        sa.wtot_next = c->wtot.p + (size_t)(par ^ 1) * kSchedTot;
+        sa.cap = c->sched_cap;
+        sa.NG = (int)NG;
+        sa.B = (int)B;
+        const int64_t grid = (std::min<int64_t>(items, c->sched_cap) + kCWaves - 1) / kCWaves;
+        nn_search_sched_kernel<<<dim3((unsigned)grid), kCBlock, 0, s>>>(
+            c->q32.p, N, c->tdesc.p, c->opt.super_cull, c->best.p, c->count_tiles ? c->counters.p : nullptr,
+            c->gbox.p, sa);
+#ifdef ORPCD_WAVETIME
+        if ((e = dump_wavetime(pass, nact, 0, (unsigned)(grid * kCWaves), s)) != hipSuccess) return e;
+#endif
     } else {
     // few running starts: half the wave target (8 starts: 16k waves 8.16 ms vs
     // 32k 8.40 ms per batch; 30 starts keep 32k).  Splits never change answers.
+    const int S = uniform_splits(c, nact);
     const int want = nact <= c->opt.small_batch ? c->opt.search_waves / 2 : c->opt.search_waves;
-    const int S = search_splits(nact, sblk, want);
     // best[] was reset to kNone by xform_queries_kernel
     auto kern = c->opt.search_occupancy == 6 ? nn_search_kernel_o6 : nn_search_kernel;
     kern<<<dim3((unsigned)(sblk * S), (unsigned)nact), kCBlock, 0, s>>>(
         c->q32.p, N, c->tdesc.p, tb, c->opt.super_cull, c->active.p, c->done.p, S, c->best.p,
         c->count_tiles ? c->counters.p : nullptr, nullptr, sblk, want, c->gbox.p);
+#ifdef ORPCD_WAVETIME
+    if ((e = dump_wavetime(pass, nact, S, (unsigned)(sblk * S) * (unsigned)nact * kCWaves, s)) != hipSuccess) return e;
+#endif
     }
     if ((e = hipGetLastError()) != hipSuccess) return e;
     if (mid && (e = hipEventRecord(mid, s)) != hipSuccess) return e;
@@ -2273,7 +2583,7 @@ hipError_t launch_gicp_solve(const orpcd_ctx* c, int nact, int pass, const orpcd
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     const double r2 = p.max_correspondence_distance * p.max_correspondence_distance;
-    return launch_xform(c, nact, r2, s, false, tb);  // queries of the next pass (done starts skip)
+    return launch_xform(c, nact, pass + 1, r2, s, false, tb);  // queries of the next pass (done starts skip)
 }
 
 // Resident 256-thread workgroups of the persistent kernel on this device.
@@ -2356,7 +2666,7 @@ hipError_t launch_gicp_solve_sums(const orpcd_ctx* c, const double* sums29, int6
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     const double r2 = p.max_correspondence_distance * p.max_correspondence_distance;
-    return launch_xform(c, 1, r2, s, false, one_target());
+    return launch_xform(c, 1, pass + 1, r2, s, false, one_target());
 }
 
 hipError_t launch_nn1(const double* q, int64_t nq, const CloudLayout& t, double r2, int32_t* idx, double* d2,

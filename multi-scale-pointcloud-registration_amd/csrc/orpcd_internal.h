@@ -23,6 +23,8 @@ constexpr int kNacc = 29;                      // JTJ(21) + JTr(6) + sum d2 + co
 constexpr int kEstGICP = 0, kEstP2P = 1;       // transformation estimation of a batch
 constexpr int kPartialStride = 32;             // doubles per block partial
 constexpr float kFarCoord = 1.0e18f;           // padding coordinate
+constexpr int kSchedClasses = 16;              // cost classes of the ordered search dispatch (log2 of a wave's cost)
+constexpr int kSchedTot = 64;                  // words the summed wave costs of a pass are spread over
 constexpr int kCounterSlots = 256;             // profiling counters: {tiles, max tiles/wave} per slot
 constexpr int kCounterStride = 16;             // u64 per slot (128 B: one cache line each)
 // Largest cloud the ABI accepts: the raw buffer descriptors of the search
@@ -248,6 +250,18 @@ struct orpcd_ctx {
     orpcd::DevBuf<int32_t> out_iters;
     orpcd::DevBuf<int64_t> out_ncorr;
     orpcd::DevBuf<unsigned long long> counters;  // kCounterSlots x {tiles visited, max per wave}
+    // cost-ordered search dispatch (opt.sched; gicp_kernels.hip, SchedIn / SchedOut):
+    // the search of pass p sums each wave's duration into wcost[p & 1] (per
+    // start and 128-query group) and wtot[p & 1]; the query transform of pass
+    // p + 1 turns them into per-group splits and cost classes and appends the
+    // pass's work items to wlist (class-major, sched_cap per class)
+    orpcd::DevBuf<unsigned> wcost;               // 2 x B x NG (10 ns ticks)
+    orpcd::DevBuf<unsigned long long> wtot;      // 2 x kSchedTot
+    orpcd::DevBuf<unsigned> wcnt;                // 2 x kSchedClasses: items per class
+    orpcd::DevBuf<unsigned long long> wlist;     // kSchedClasses x sched_cap packed items
+    int sched_cap = 0;
+    int sched_B = 0;                             // starts of the batch (wcost parity stride B x NG)
+    bool sched_live = false;                     // the running batch uses the ordered dispatch
 
     // kernel-level entry points
     orpcd::CloudLayout aux;
@@ -314,6 +328,9 @@ struct orpcd_ctx {
         int persist_items = 0;    // search items per pass to aim for (0: the resident workgroups)
         int persist_timeout_s = 60;  // guard: the persistent loop gives up (error) after this long
         int persist_fences = 0;   // 1: agent release/acquire fences around the persistent loop's hand-offs
+        int sched = 1;            // 1: search waves dispatched heaviest first, heavy query groups split
+                                  // further (costs measured in the previous pass); 0: uniform splits
+        int sched_items = 10240;  // ordered dispatch: split a group until its waves cost <= pass total / this
     } opt;
     std::vector<hipEvent_t> ev_pool;
     orpcd::KernelStats stats;
@@ -355,7 +372,10 @@ hipError_t launch_fps(const double* xyz, int64_t n, int first, int k, int max_bl
 
 // gicp_kernels.hip
 int accum_blocks(int64_t N);
-hipError_t launch_xform(const orpcd_ctx* c, int nact, double r2, hipStream_t s, bool dev_nact, const TgtBounds& tb);
+hipError_t launch_xform(const orpcd_ctx* c, int nact, int pass, double r2, hipStream_t s, bool dev_nact,
+                        const TgtBounds& tb);
+bool sched_wanted(const orpcd_ctx* c, bool persist);
+int sched_capacity(const orpcd_ctx* c, int B);
 TgtBounds one_target();
 // bounds of the launch rows act[0..nact) (increasing slots) over the batch's targets
 TgtBounds target_bounds(const orpcd_ctx* c, const int32_t* act, int nact);

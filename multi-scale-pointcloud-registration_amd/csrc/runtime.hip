@@ -395,6 +395,19 @@ int batch_setup(orpcd_ctx* c, const double* R0, const double* t0, int B, const o
     c->two_phase_ok = c->opt.search_kernel == 2 && worst_items <= ((size_t)1 << 29);  // <= 2 GiB of items
     if (c->two_phase_ok) CTX_CHECK(c, c->items.ensure(worst_items));
     CTX_CHECK(c, c->item_counts.ensure((size_t)2 * B * ((N + 127) / 128) + 2));
+    c->sched_live = sched_wanted(c, persist);
+    if (c->sched_live) {
+        const size_t NG = (size_t)(N + 127) / 128;
+        c->sched_cap = sched_capacity(c, B);
+        c->sched_B = B;
+        CTX_CHECK(c, c->wcost.ensure(2 * (size_t)B * NG));
+        CTX_CHECK(c, c->wtot.ensure(2 * (size_t)kSchedTot));
+        CTX_CHECK(c, c->wcnt.ensure(2 * (size_t)kSchedClasses));
+        CTX_CHECK(c, c->wlist.ensure((size_t)kSchedClasses * c->sched_cap));
+        CTX_CHECK(c, hipMemsetAsync(c->wcost.p, 0, 2 * (size_t)B * NG * 4, c->stream));
+        CTX_CHECK(c, hipMemsetAsync(c->wtot.p, 0, 2 * (size_t)kSchedTot * 8, c->stream));
+        CTX_CHECK(c, hipMemsetAsync(c->wcnt.p, 0, 2 * (size_t)kSchedClasses * 4, c->stream));
+    }
     CTX_CHECK(c, c->done.ensure((size_t)B));
     CTX_CHECK(c, c->active.ensure((size_t)B));
     CTX_CHECK(c, c->ctl.ensure((size_t)B + 2));
@@ -460,7 +473,7 @@ int batch_setup(orpcd_ctx* c, const double* R0, const double* t0, int B, const o
     c->est = init16 ? kEstP2P : kEstGICP;
     if (!init16) CTX_CHECK(c, launch_normals_cov(c->sraw.p, N, c->scratch64c.p, B, p->epsilon, nullptr, c->scov.p, s));
     if (!persist) {
-        CTX_CHECK(c, launch_xform(c, B, p->max_correspondence_distance * p->max_correspondence_distance, s, false,
+        CTX_CHECK(c, launch_xform(c, B, 0, p->max_correspondence_distance * p->max_correspondence_distance, s, false,
                                   target_bounds(c, hAct, B)));
         return ORPCD_OK;
     }
@@ -1476,6 +1489,8 @@ int orpcd_set_option(orpcd_ctx* c, const char* key, double value) {
     else if (k == "persist_items" && v >= 0) c->opt.persist_items = v;
     else if (k == "persist_timeout_s" && v >= 1 && v <= 3600) c->opt.persist_timeout_s = v;
     else if (k == "persist_fences" && (v == 0 || v == 1)) c->opt.persist_fences = v;
+    else if (k == "sched" && (v == 0 || v == 1)) c->opt.sched = v;
+    else if (k == "sched_items" && v >= 64 && v <= (1 << 22)) c->opt.sched_items = v;
     else {
         c->err = "set_option: unknown key or bad value: " + k;
         return ORPCD_EINVAL;

@@ -16,13 +16,18 @@ Any other IOptimizer (including the reference's own) is called per attempt,
 exactly as the reference does.
 
 With a batched optimizer the compass search is also speculative
-(``speculative_compass=True``, keyword-only): each compass iteration draws the
-six candidates' RNG blocks up front, runs the six multistarts concurrently
-(one device context and stream each) and replays the reference's candidate
-order, so the results and the RNG stream are identical to the sequential
-search while the device runs the candidates side by side.
+(``speculative_compass=True``, keyword-only).  Every multistart the reference
+evaluates draws the next ``attempts`` starts of one RNG stream, so the
+stream is a sequence of blocks whatever the search decides; the build draws
+them once (``_Tape``), runs the multistarts the reference MAY evaluate next
+(the initial multistart with the first compass iteration, then each compass
+iteration's six candidates, optionally followed along the "all six fail"
+path by the next iteration at delta / 2: ``speculative_depth``) as one
+device batch, and replays the reference's decisions in order.  Results, the
+RNG position and delta are identical to the sequential search.
 """
 import copy
+import threading
 import time
 from typing import List, Tuple
 
@@ -48,12 +53,13 @@ from ..utils.logger_factory import LoggerFactory
 class Aligner:
     transfromation: np.ndarray = np.eye(4)
     scale_factors: np.ndarray = np.ones((1, 3))
+    prefetch_rng = True  # draw the next batch's RNG blocks on a helper thread while the device runs
 
     def __init__(self, source_preprocessor, target_preprocessor, optimizer: IOptimizer,
                  attempts: int = __MULTISTART_ATTEMPTS__, deg: float = __ALIGNER_DEG__, mu: float = __ALIGNER_MU__,
                  std: float = __ALIGNER_STD__, delta: float = __ALIGNER_DELTA__, max_iter: int = __ALIGNER_MAX_ITER__,
                  eps: float = __ALIGNER_EPS__, visualize_intermediate_steps: bool = False, *,
-                 speculative_compass: bool = True):
+                 speculative_compass: bool = True, speculative_depth: int = None):
         self._LOG = LoggerFactory.get_logger(log_name=self.__class__.__name__)
         checks = [("attempts", attempts, lambda v: v <= 0, __MULTISTART_ATTEMPTS__),
                   ("deg", deg, lambda v: v <= 0, __ALIGNER_DEG__),
@@ -84,6 +90,11 @@ class Aligner:
         self.last_refine = None
         self._refine_ctx = None  # device context for refine_registration when the optimizer has none
         self._speculative_compass = speculative_compass
+        # compass iterations per device batch along the "all six fail" path:
+        # None = 2 when a one-iteration batch per device is small (<= 96 starts
+        # of 50k points: latency-bound, so a second iteration is nearly free),
+        # else 1
+        self._speculative_depth = speculative_depth
         self.speculative_history: List[dict] = []  # candidates run ahead but not reached by the reference's order
 
     # ----------------------------------------------------------------- RNG
@@ -127,7 +138,7 @@ class Aligner:
         T[:3, 3] = np.dot(t0, Tc[:3, :3]).ravel() + Tc[:3, 3]
         return T
 
-    def _draw_block(self, n: int):
+    def _draw_block(self, n: int, rs=None):
         """n consecutive initialize_rotation() draws (Aligner.py:125-162), bit for
         bit: the same scalar np.random calls in the same order (three uniform,
         then randn(3), per attempt) and the same translation expression; the
@@ -135,7 +146,8 @@ class Aligner:
         r_1 (r_2 r_3) by one stacked matmul, which give the scalar calls' and
         np.dot's values (checked against the sequential draws in
         tests/test_host.py::test_draw_block_matches_initialize_rotation)."""
-        deg, uni, randn = self._deg, np.random.uniform, np.random.randn
+        rs = np.random if rs is None else rs  # the global legacy RandomState, or a copy of it
+        deg, uni, randn = self._deg, rs.uniform, rs.randn
         th = np.empty((n, 3))
         g = np.empty((n, 3))
         for k in range(n):
@@ -185,13 +197,14 @@ class Aligner:
         R0s, t0s = self._draw_block(self._attempts)  # same draws, same order as the sequential loop
         return R0s, t0s, Aligner._BlockStates(self, before, np.random.get_state(), self._attempts)
 
-    def _run_tables(self, source, targets, draws):
+    def _run_tables(self, source, targets, draws, keys=None):
         """Per target k, the gathered per-attempt table of the starts draws[k].
         The K tables are sharded as ONE flat list of K x B starts (target-major):
         this rank runs its contiguous block, which touches one or two targets
         rather than all K (so it sets up only those targets), as one batch
         (optimize_batch_multi when it spans several); one all-gather of the
-        flat table follows."""
+        flat table follows.  `keys` (the multistarts' (block, scale) identities)
+        is for instrumentation only."""
         B, K = self._attempts, len(draws)
         rank, ws = parallel.world()
         lo, hi = parallel.shard(K * B, rank, ws)
@@ -259,39 +272,139 @@ class Aligner:
                 np.multiply(target[:, c], s[c], out=out[k, :, c])
         return [out[k] for k in range(len(scales))]
 
-    def _compass_iteration_speculative(self, source, target, scale_factors, optimal_metric):
-        """One compass iteration (Aligner.py:270-297) with all six candidates'
-        multistarts drawn up front (the RNG blocks the reference would draw if
-        it evaluated them all, in its candidate order +x, -x, +y, -y, +z, -z)
-        and run concurrently; the reference's decisions are then replayed in
-        order: the first candidate with metric <= optimal is accepted and
-        np.random is left exactly where the reference leaves it (after that
-        candidate's block, or at a failing attempt).  Results are identical to
-        the sequential compass; candidates after the accepted one are extra
-        device work (recorded in speculative_history)."""
+    class _Tape:
+        """The reference's RNG stream as consecutive multistart blocks.
+
+        Every multistart the reference evaluates draws the next ``attempts``
+        starts (Aligner.py:178-186), whichever compass candidate it belongs
+        to: block 0 is the initial multistart (:245), a compass iteration at
+        block position p draws blocks p .. p+5 for +x, -x, +y, -y, +z, -z
+        (:270-297) as far as it gets; accepting candidate k moves the position
+        to p+k+1, failing all six to p+6.  Blocks are drawn once, in stream
+        order, from a private copy of the global state (``prefetch`` draws
+        ahead on a helper thread while the device runs); ``state_after``
+        gives the global state the reference leaves after a block."""
+
+        def __init__(self, aligner):
+            self._al = aligner
+            self._rs = np.random.RandomState()
+            self._rs.set_state(np.random.get_state())
+            self._states = [self._rs.get_state()]  # [j]: the state before block j
+            self._blocks = []
+            self._lock = threading.Lock()
+            self._thread = None
+
+        def _extend(self, j):
+            with self._lock:
+                while len(self._blocks) <= j:
+                    self._blocks.append(self._al._draw_block(self._al._attempts, self._rs))
+                    self._states.append(self._rs.get_state())
+
+        def draw(self, j):
+            """Block j as _draw_starts returns it: (R0s, t0s, per-attempt states)."""
+            self._extend(j)
+            R0s, t0s = self._blocks[j]
+            return R0s, t0s, Aligner._BlockStates(self._al, self._states[j], self._states[j + 1], self._al._attempts)
+
+        def state_after(self, j):
+            self._extend(j)
+            return self._states[j + 1]
+
+        def prefetch(self, j):
+            self.join()
+            if Aligner.prefetch_rng and len(self._blocks) <= j:
+                self._thread = threading.Thread(target=self._extend, args=(j,), daemon=True)
+                self._thread.start()
+
+        def join(self):
+            if self._thread is not None:
+                self._thread.join()
+                self._thread = None
+
+    def _compass_steps(self, delta):
+        """The candidate steps of one compass iteration in the reference's order
+        +x, -x, +y, -y, +z, -z (Aligner.py:270-291: delta * e_axis, -delta * e_axis)."""
         directions = np.eye(3)
-        steps = [sign * self._delta * directions[:, axis] for axis in range(3) for sign in (1.0, -1.0)]
-        state0 = np.random.get_state()
-        draws = [self._draw_starts() for _ in steps]
-        t_start = time.perf_counter()
-        # only the candidates this rank runs are scaled (target * (sf + d),
-        # Aligner.py:264-265), into one reused contiguous block
-        tables = self._run_tables(
-            source, lambda ks: self._scaled_targets(target, [scale_factors + steps[k] for k in ks]), draws)
-        seconds = time.perf_counter() - t_start
-        np.random.set_state(state0)
-        new_metric = None
-        for k, (d, table, draw) in enumerate(zip(steps, tables, draws)):
-            np.random.set_state(draw[2][-1])  # as if the blocks up to k had been drawn in sequence
-            rec = dict(B=self._attempts, seconds=seconds / len(steps), iters=int(table["iters"].sum()),
-                       rmse=table["rmse"].copy())
-            self.history.append(rec)
-            T, new_metric = self._select(table, draw)
-            if new_metric <= optimal_metric:
-                self.speculative_history.extend(
-                    dict(B=self._attempts, iters=int(t["iters"].sum())) for t in tables[k + 1:])
-                return d, T, new_metric
-        return None, None, new_metric
+        return [sign * delta * directions[:, axis] for axis in range(3) for sign in (1.0, -1.0)]
+
+    def _depth(self, n_points):
+        if self._speculative_depth is not None:
+            return max(1, int(self._speculative_depth))
+        _, ws = parallel.world()
+        return 2 if 6 * self._attempts * n_points <= 96 * 50_000 * ws else 1
+
+    def _plan(self, pos, scale_factors, delta, iteration, depth, initial):
+        """The multistarts (block, target scale) the reference may evaluate
+        next from this state: the initial multistart if pending, then `depth`
+        compass iterations along the fail path (delta halving, scale factors
+        unchanged) while the reference's loop condition holds."""
+        items = [(0, np.ones((1, 3)))] if initial else []
+        for _ in range(depth):
+            if not (delta >= self._eps and iteration <= self._max_iter):  # Aligner.py:262
+                break
+            items.extend((pos + k, scale_factors + step) for k, step in enumerate(self._compass_steps(delta)))
+            pos, iteration, delta = pos + 6, iteration + 1, delta / 2
+        return items
+
+    def _align_speculative(self, source, target):
+        """Aligner.py:245-298 (initial multistart + compass search) over planned
+        device batches.  Returns (T, metric, scale factors, errors) and leaves
+        np.random and delta exactly where the reference leaves them."""
+        tape = Aligner._Tape(self)
+        depth = self._depth(len(source))
+        done = {}  # (block, scale bytes) -> (table, seconds)
+        used = set()
+
+        def run(items):
+            draws = [tape.draw(b) for b, _ in items]
+            tape.prefetch(max(b for b, _ in items) + 6 * depth)  # the next batch's blocks, drawn while the device runs
+            t_start = time.perf_counter()
+            tables = self._run_tables(
+                source, lambda ks: self._scaled_targets(target, [items[k][1] for k in ks]), draws,
+                keys=[(b, sc.tobytes()) for b, sc in items])
+            sec = (time.perf_counter() - t_start) / len(items)
+            for (b, sc), tb in zip(items, tables):
+                done[(b, sc.tobytes())] = (tb, sec)
+
+        def select(block, scale):
+            key = (block, scale.tobytes())
+            table, sec = done[key]
+            used.add(key)
+            self.history.append(dict(B=self._attempts, seconds=sec, iters=int(table["iters"].sum()),
+                                     rmse=table["rmse"].copy()))
+            return self._select(table, tape.draw(block))
+
+        scale_factors = np.ones((1, 3))
+        iteration, pos = 0, 1
+        try:
+            run(self._plan(1, scale_factors, self._delta, iteration, depth, initial=True))
+            start = time.time()
+            transformation, metric = select(0, np.ones((1, 3)))
+            self._LOG.info(f"Multi-start registration time: {time.time() - start}")
+            errors = [metric]
+            while self._delta >= self._eps and iteration <= self._max_iter:
+                iteration += 1
+                steps = self._compass_steps(self._delta)
+                if any((pos + k, (scale_factors + st).tobytes()) not in done for k, st in enumerate(steps)):
+                    run(self._plan(pos, scale_factors, self._delta, iteration - 1, depth, initial=False))
+                for k, step in enumerate(steps):
+                    new_transformation, new_metric = select(pos + k, scale_factors + step)
+                    if new_metric <= metric:  # Aligner.py:273,287
+                        metric, transformation = new_metric, new_transformation
+                        scale_factors += step
+                        errors.append(new_metric)
+                        pos += k + 1
+                        break
+                else:
+                    pos += 6
+                if new_metric > metric:  # Aligner.py:296-297
+                    self._delta = self._delta / 2
+            np.random.set_state(tape.state_after(pos - 1))
+        finally:
+            tape.join()
+            self.speculative_history.extend(dict(B=self._attempts, iters=int(tb["iters"].sum()))
+                                            for key, (tb, _) in done.items() if key not in used)
+        return transformation, metric, scale_factors, errors
 
     # -------------------------------------------------------------- compass
     def compass_step(self, source, target, scale_factors, delta):
@@ -306,6 +419,13 @@ class Aligner:
         """Aligner.py:228-317."""
         source = self._source_preprocessor.preprocess(source)
         target = self._target_preprocessor.preprocess(target)
+        # speculation needs an optimizer whose result is a pure function of its
+        # inputs and that can run several targets at once (optimize_batch_multi)
+        if self._speculative_compass and hasattr(self._optimizer, "optimize_batch_multi"):
+            optimal_transformation, optimal_metric, optimal_scale_factors, errors = self._align_speculative(
+                source, target)
+            return self._finish(source, target, optimal_transformation, optimal_metric, optimal_scale_factors,
+                                errors, refine_registration, icp_type)
         iteration = 0
         optimal_scale_factors = np.ones((1, 3))
         start = time.time()
@@ -313,22 +433,8 @@ class Aligner:
         self._LOG.info(f"Multi-start registration time: {time.time() - start}")
         errors = [optimal_metric]
         directions = np.eye(3)
-        # speculation needs an optimizer whose result is a pure function of its
-        # inputs and that can run several targets at once (optimize_batch_multi)
-        speculate = self._speculative_compass and hasattr(self._optimizer, "optimize_batch_multi")
         while self._delta >= self._eps and iteration <= self._max_iter:
             iteration += 1
-            if speculate:
-                step, new_rotation, new_metric = self._compass_iteration_speculative(
-                    source, target, optimal_scale_factors, optimal_metric)
-                if step is not None:
-                    optimal_metric = new_metric
-                    optimal_transformation = new_rotation
-                    optimal_scale_factors += step
-                    errors.append(new_metric)
-                if new_metric > optimal_metric:
-                    self._delta = self._delta / 2
-                continue
             for axis in range(3):
                 scale_plus = self._delta * directions[:, axis]
                 new_scale_factors, new_rotation, new_metric = self.compass_step(
@@ -350,6 +456,12 @@ class Aligner:
                     break
             if new_metric > optimal_metric:
                 self._delta = self._delta / 2
+        return self._finish(source, target, optimal_transformation, optimal_metric, optimal_scale_factors, errors,
+                            refine_registration, icp_type)
+
+    def _finish(self, source, target, optimal_transformation, optimal_metric, optimal_scale_factors, errors,
+                refine_registration, icp_type):
+        """Aligner.py:299-317."""
         if refine_registration:
             target = target * optimal_scale_factors
             optimal_transformation, optimal_metric = self.refine_registration(

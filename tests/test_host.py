@@ -179,22 +179,30 @@ def test_transfrom_matches_reference_formula():
 class SpeculativeScripted(BatchedScripted):
     """Adds optimize_batch_multi, which turns on the Aligner's speculative compass."""
 
+    def __init__(self, inner):
+        super().__init__(inner)
+        self.multi_calls = []
+
     def optimize_batch_multi(self, source, targets, R0s, t0s):
+        self.multi_calls.append(sum(len(r) for r in R0s))
         return [self.optimize_batch(source, tg, r, t) for tg, r, t in zip(targets, R0s, t0s)]
 
 
+@pytest.mark.parametrize("depth", [None, 1, 2, 3])
 @pytest.mark.parametrize("mode,attempts,seed", [("scripted", 4, 7), ("constant", 2, 3)])
-def test_speculative_compass_matches_reference_G3(mode, attempts, seed):
-    """The speculative compass (all six candidates drawn and run up front, the
-    reference's order replayed) reproduces the reference's align() exactly:
-    T, metric, scale factors, errors, the RNG position and delta (G3).  The
-    scripted optimizer is a pure function of its inputs in these modes."""
+def test_speculative_compass_matches_reference_G3(mode, attempts, seed, depth):
+    """The speculative compass (the initial multistart with the first compass
+    iteration, every iteration's six candidates and `depth` - 1 further
+    iterations along the fail path drawn and run up front, the reference's
+    order replayed) reproduces the reference's align() exactly: T, metric,
+    scale factors, errors, the RNG position and delta (G3).  The scripted
+    optimizer is a pure function of its inputs in these modes."""
     from orpcd_amd import Aligner, Preprocessor
     from scripted import ScriptedOptimizer
     g = np.load(f"{GOLDEN}/g3_aligner_trace.npz")
     np.random.seed(seed)
     opt = SpeculativeScripted(ScriptedOptimizer(g["goal"], mode=mode))
-    al = Aligner(Preprocessor([]), Preprocessor([]), opt, attempts=attempts)
+    al = Aligner(Preprocessor([]), Preprocessor([]), opt, attempts=attempts, speculative_depth=depth)
     T, m, sf, err = al.align(g["src"].copy(), g["tgt"].copy(), refine_registration=False)
     assert np.array_equal(T, g[f"{mode}_T"]) and m == g[f"{mode}_metric"]
     assert np.array_equal(sf, g[f"{mode}_sf"]) and np.array_equal(err, g[f"{mode}_errors"])
@@ -203,3 +211,23 @@ def test_speculative_compass_matches_reference_G3(mode, attempts, seed):
     # the replayed multistarts are exactly the reference's calls, in order
     assert len(al.history) * attempts == len(g[f"{mode}_call_rmse"])
     assert np.array_equal(np.concatenate([h["rmse"] for h in al.history]), g[f"{mode}_call_rmse"])
+    # one device batch per plan: the initial multistart never runs alone
+    assert opt.multi_calls[0] >= 7 * attempts
+
+
+def test_speculative_plan_follows_the_fail_path():
+    """_plan: the initial multistart, then compass iterations along the fail
+    path (blocks p .. p+5, then p+6 .. p+11 at delta / 2, same scale factors),
+    cut where the reference's loop condition (delta >= eps, iteration <=
+    max_iter) stops."""
+    from orpcd_amd import Aligner, Preprocessor
+    al = Aligner(Preprocessor([]), Preprocessor([]), None, attempts=4, delta=0.2, eps=0.05, max_iter=100)
+    sf = np.ones((1, 3))
+    items = al._plan(1, sf, 0.2, 0, 3, initial=True)
+    assert [b for b, _ in items] == list(range(19))
+    assert np.array_equal(items[0][1], np.ones((1, 3)))
+    assert np.array_equal(items[1][1], sf + [0.2, 0, 0]) and np.array_equal(items[6][1], sf + [0, 0, -0.2])
+    assert np.array_equal(items[7][1], sf + [0.1, 0, 0]) and np.array_equal(items[18][1], sf + [0, 0, -0.05])
+    assert len(al._plan(1, sf, 0.05, 0, 3, initial=False)) == 6  # 0.025 < eps: no second iteration
+    assert len(al._plan(5, sf, 0.2, 100, 3, initial=False)) == 6  # iteration 101 > max_iter
+    assert al._plan(5, sf, 0.2, 101, 3, initial=False) == []

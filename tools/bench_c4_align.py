@@ -8,13 +8,16 @@ per multistart -- on one GPU, and its strong-scaling projection to G ranks.
    table of per-start records is kept, in call order.
 2. Rank r of G (r = 0..G-1): the same align() (same seed, hence the same
    control flow and RNG stream) with parallel.world() -> (r, G): the rank
-   runs only its contiguous block of every call's starts (parallel.shard of
-   the initial multistart, or of a compass iteration's six candidates as one
-   flat list) on this GPU, alone.  The all-gather is replayed from
-   step 1's tables after checking that the rank's own rows are bit-identical
-   to them (sharding never changes a start's result).  Each rank's time per
-   _run_tables call (one compass iteration's six candidate shards, or the
-   initial multistart) is recorded.
+   runs only its contiguous block of every device batch's flat list of
+   starts (parallel.shard) on this GPU, alone, with the speculative depth
+   the G-rank run would choose (auto: 2, i.e. each batch also holds the next
+   compass iteration along the "all six fail" path; --depth overrides).  The
+   all-gather is replayed from step 1's rows of every multistart (keyed by
+   RNG block and target scale) after checking that the rank's own rows are
+   bit-identical to them (sharding never changes a start's result); a
+   multistart step 1 never ran was speculated past the reference's path and
+   is never selected.  Each rank's time per device batch (_run_tables call)
+   is recorded.
 3. Projection: the ranks synchronise at every all-gather, so
    T_G = sum over calls of max over ranks of that call's time
        + every all-gather at `--allgather-us` (one RCCL all-gather of
@@ -43,27 +46,32 @@ def main():
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--allgather-us", type=float, default=50.0)
     ap.add_argument("--out", default=None)
+    ap.add_argument("--depth", type=int, default=None, help="speculative_depth of the ranks (default: auto)")
+    ap.add_argument("--no-prefetch", action="store_true")
     a = ap.parse_args()
     from orpcd_amd import Aligner, GeneralizedICP, Preprocessor, parallel
     from workloads import c2_pair
 
     src, tgt = c2_pair(a.points)
+    Aligner.prefetch_rng = not a.no_prefetch
     opt = GeneralizedICP()
     real_world, real_gather = parallel.world, parallel.allgather_records
     orig_run_tables = Aligner._run_tables
     calls = []  # per _run_tables call: seconds
+    cur_keys = []  # the multistarts of the running call
 
-    def timed_run_tables(self, source, targets, draws):
+    def timed_run_tables(self, source, targets, draws, keys=None):
+        cur_keys[:] = keys
         t0 = time.perf_counter()
-        r = orig_run_tables(self, source, targets, draws)
+        r = orig_run_tables(self, source, targets, draws, keys=keys)
         calls.append(time.perf_counter() - t0)
         return r
 
     Aligner._run_tables = timed_run_tables
 
-    def align_once():
+    def align_once(depth=None):
         np.random.seed(a.seed)
-        al = Aligner(Preprocessor([]), Preprocessor([]), opt, attempts=a.attempts)
+        al = Aligner(Preprocessor([]), Preprocessor([]), opt, attempts=a.attempts, speculative_depth=depth)
         calls.clear()
         t0 = time.perf_counter()
         T, m, sf, err = al.align(src.copy(), tgt.copy(), refine_registration=False)
@@ -73,41 +81,59 @@ def main():
 
     # ---- 1. one GPU (warm-up run first: contexts, covariances, code objects)
     align_once()
-    tables = []
+    rows = {}  # (block, scale) -> the multistart's gathered rows
+    ngather = [0]
 
     def recording_gather(local, B):
         t = real_gather(local, B)
-        tables.append(t.copy())
+        n = B // len(cur_keys)
+        for i, key in enumerate(cur_keys):
+            rows[key] = t[i * n:(i + 1) * n].copy()
+        ngather[0] += 1
         return t
 
     parallel.allgather_records = recording_gather
     t1, calls1, res1, iters1 = align_once()
-    # ---- 2. every rank's shard alone
-    rank_wall, rank_calls = [], []
+    n1 = ngather[0]
+    # ---- 2. every rank's shard alone; the all-gather returns the 1-GPU rows
+    # of every multistart (a multistart the 1-GPU run never evaluated was
+    # speculated past the reference's path: its rows are never selected and
+    # are filled with rmse = inf)
+    rank_wall, rank_calls, rank_gathers = [], [], []
     for r in range(a.ranks):
         k = [0]
 
         def replay(local, B, r=r):
-            full = tables[k[0]]
+            n = B // len(cur_keys)
+            full = np.zeros((B, parallel.REC))
+            known = np.zeros(B, bool)
+            for i, key in enumerate(cur_keys):
+                if key in rows:
+                    full[i * n:(i + 1) * n] = rows[key]
+                    known[i * n:(i + 1) * n] = True
+                else:
+                    full[i * n:(i + 1) * n, 0] = np.inf
             lo, hi = parallel.shard(B, r, a.ranks)
-            assert np.array_equal(local, full[lo:hi]), f"rank {r} call {k[0]}: sharded rows differ"
+            m = known[lo:hi]
+            assert np.array_equal(local[m], full[lo:hi][m]), f"rank {r} call {k[0]}: sharded rows differ"
+            full[lo:hi] = local
             k[0] += 1
             return full
 
         parallel.world = lambda r=r: (r, a.ranks)
         parallel.allgather_records = replay
-        w, c, res, _ = align_once()
+        w, c, res, _ = align_once(a.depth)
         assert res["sf"] == res1["sf"] and res["metric"] == res1["metric"], (r, res, res1)
-        assert k[0] == len(tables)
         rank_wall.append(w)
         rank_calls.append(c)
+        rank_gathers.append(k[0])
     parallel.world, parallel.allgather_records = real_world, real_gather
     Aligner._run_tables = orig_run_tables
-    ncalls = len(calls1)
+    ncalls = len(rank_calls[0])
     assert all(len(c) == ncalls for c in rank_calls)
     per_call_max = [max(rc[i] for rc in rank_calls) for i in range(ncalls)]
     host_outside = max(w - sum(c) for w, c in zip(rank_wall, rank_calls))
-    ag = len(tables) * a.allgather_us * 1e-6
+    ag = rank_gathers[0] * a.allgather_us * 1e-6
     tG = sum(per_call_max) + ag + host_outside
     out = {
         "metric": f"C4 Aligner.align() pattern search wall-clock, {a.attempts} starts/multistart, "
@@ -116,12 +142,16 @@ def main():
         "t_1gpu_s": round(t1, 4),
         "gicp_iters_1gpu": int(iters1),
         "gicp_iters_per_s_1gpu": round(iters1 / t1, 1),
-        "multistart_calls": ncalls, "allgathers": len(tables),
+        "calls_1gpu": len(calls1), "calls_ranks": ncalls, "allgathers": rank_gathers[0],
         "t_projected_s": round(tG, 4),
         "t_projected_parts_s": {"sum_per_call_max": round(sum(per_call_max), 4), "allgathers": round(ag, 4),
                                 "host_outside_calls": round(host_outside, 4)},
         "rank_wall_s": [round(w, 4) for w in rank_wall],
+        "per_call_1gpu_s": [round(x, 5) for x in calls1],
+        "per_call_rank_s": [[round(x, 5) for x in c] for c in rank_calls],
+
         "projected_speedup": round(t1 / tG, 2),
+        "speculative_depth": {"1gpu": "auto", "ranks": a.depth or "auto"}, "prefetch_rng": not a.no_prefetch,
         "result": res1,
         "note": "every rank's shard timed alone on one MI355X (same seed, same control flow); its rows were "
                 "checked bit-identical to the 1-GPU table; all-gathers replayed and charged",
