@@ -486,73 +486,15 @@ struct SchedS {                          // search side (pass p)
     int cap, NG, B;
 };
 
-// fp32 queries of every running start for the next pass: q = fp32(Q * p),
-// and in q.w the query's search bound: d^2 to its previous correspondence
-// (x 1 + 1e-4), or, without one, to the nearest of a strided set of tile
-// representatives (real targets, so either bound is valid), capped at r2s.
-__global__ __launch_bounds__(256) void xform_queries_kernel(const double* __restrict__ src, int N,
-                                                            const int32_t* __restrict__ active,
-                                                            const double* __restrict__ Qm,
-                                                            const int32_t* __restrict__ done,
-                                                            const TargetDesc* __restrict__ tdesc, TgtBounds tb,
-                                                            const int32_t* __restrict__ prevnn,
-                                                            float r2s, int reseed, float4* __restrict__ q32,
-                                                            unsigned long long* __restrict__ best,
-                                                            const int32_t* __restrict__ nact_dev,
-                                                            float4* __restrict__ gbox, SchedX sx) {
-    if (nact_dev && (int)blockIdx.y >= *nact_dev) return;  // pipelined: grid sized for an upper bound
-    const int slot = active[blockIdx.y];
-    if (done[slot]) return;
-    const int tk = target_of_row(tb, blockIdx.y);
-    const TargetDesc& tg = tdesc[tk];
-    const float4* __restrict__ p4 = tg.p4;
-    const int i = blockIdx.x * 256 + threadIdx.x;
-    const bool valid = i < N;
-    const float inf = 3.0e38f;
-    float x = inf, y = inf, z = inf, bound = 0.0f;
-    if (valid) {
-        best[(size_t)slot * N + i] = kNone;  // split searches merge into it by atomicMin
-        double Q[12];
-#pragma unroll
-        for (int t = 0; t < 12; ++t) Q[t] = Qm[12 * slot + t];
-        const double p[3] = {src[3 * i], src[3 * i + 1], src[3 * i + 2]};
-        double q[3];
-        xform(Q, p, q);
-        x = (float)(q[0] - tg.ox), y = (float)(q[1] - tg.oy), z = (float)(q[2] - tg.oz);
-        bound = r2s;
-        const int jp = prevnn[(size_t)slot * N + i];
-        if (jp >= 0) {
-            bound = fminf(bound, d2f(x, y, z, p4[jp]) * kSeedSlack + 1e-30f);
-        } else if (jp == kNoSeed || reseed) {
-            for (int t = 0; t < tg.ntiles; t += tg.seed_stride)
-                bound = fminf(bound, d2f(x, y, z, p4[t * kTile]) * kSeedSlack + 1e-30f);
-        }
-        q32[(size_t)slot * N + i] = make_float4(x, y, z, bound);
-    }
-    if (!gbox) return;
-    // box and worst bound of each search wave's 128 queries (waves 0-1 and
-    // 2-3 of this block): what the search would reduce, computed once here
-    __shared__ float part[4][7];
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    const float r[7] = {wave_fmin(x), wave_fmin(y), wave_fmin(z), wave_fmax(valid ? x : -inf),
-                        wave_fmax(valid ? y : -inf), wave_fmax(valid ? z : -inf),
-                        __uint_as_float(wave_umax(__float_as_uint(bound)))};
-    if (lane < 7) part[w][lane] = r[lane];
-    __syncthreads();
-    if (threadIdx.x < 2 && (blockIdx.x * 2 + threadIdx.x) * 128 < N) {
-        const float* a = part[2 * threadIdx.x];
-        const float* b = part[2 * threadIdx.x + 1];
-        float4* g = gbox + ((size_t)slot * ((N + 127) / 128) + blockIdx.x * 2 + threadIdx.x) * 2;
-        g[0] = make_float4(fminf(a[0], b[0]), fminf(a[1], b[1]), fminf(a[2], b[2]),
-                           __uint_as_float(max(__float_as_uint(a[6]), __float_as_uint(b[6]))));
-        g[1] = make_float4(fmaxf(a[3], b[3]), fmaxf(a[4], b[4]), fmaxf(a[5], b[5]), 0.0f);
-    }
-    if (!sx.list || blockIdx.x != 0) return;
-    // ordered dispatch: block 0 of each start files the work items of all the
-    // start's 128-query groups (they depend only on the previous pass's
-    // costs).  Counts per class are aggregated in LDS first, so a pass takes
-    // kSchedClasses global atomics per start (one counter per class shared by
-    // every group had serialised ~12k atomics per pass on a few addresses).
+// The ordered dispatch's work items of start `slot` (one block per start,
+// launched beside the query transform's blocks).
+__device__ __forceinline__ void plan_start_items(const SchedX& sx, int slot, int tk) {
+    const int lane = threadIdx.x & 63;
+    // The items depend only on the previous pass's costs, so this block runs
+    // beside the transform blocks (as the sequel of one of them it lengthened
+    // the transform by 3-5 us).  Counts per class are aggregated in LDS first:
+    // a pass takes kSchedClasses global atomics per start (one counter per
+    // class bumped by every group serialised ~12k atomics on a few addresses).
     __shared__ float s_target;
     __shared__ unsigned lcnt[kSchedClasses], lbase[kSchedClasses];
     if (threadIdx.x < kSchedClasses) lcnt[threadIdx.x] = 0u;
@@ -597,6 +539,74 @@ __global__ __launch_bounds__(256) void xform_queries_kernel(const double* __rest
         sx.wcost_cur[(size_t)slot * NG + g] = 0u;
         unsigned long long* out = sx.list + (size_t)cls * sx.cap + at;
         for (int k = 0; k < S; ++k) out[k] = sched_item(slot, tk, g, k, S);
+    }
+}
+
+// fp32 queries of every running start for the next pass: q = fp32(Q * p),
+// and in q.w the query's search bound: d^2 to its previous correspondence
+// (x 1 + 1e-4), or, without one, to the nearest of a strided set of tile
+// representatives (real targets, so either bound is valid), capped at r2s.
+__global__ __launch_bounds__(256) void xform_queries_kernel(const double* __restrict__ src, int N,
+                                                            const int32_t* __restrict__ active,
+                                                            const double* __restrict__ Qm,
+                                                            const int32_t* __restrict__ done,
+                                                            const TargetDesc* __restrict__ tdesc, TgtBounds tb,
+                                                            const int32_t* __restrict__ prevnn,
+                                                            float r2s, int reseed, float4* __restrict__ q32,
+                                                            unsigned long long* __restrict__ best,
+                                                            const int32_t* __restrict__ nact_dev,
+                                                            float4* __restrict__ gbox, SchedX sx) {
+    if (nact_dev && (int)blockIdx.y >= *nact_dev) return;  // pipelined: grid sized for an upper bound
+    const int slot = active[blockIdx.y];
+    if (done[slot]) return;
+    const int tk = target_of_row(tb, blockIdx.y);
+    if (sx.list && blockIdx.x == 0) {  // the extra block (dispatched first): the pass's work items of this start
+        plan_start_items(sx, slot, tk);
+        return;
+    }
+    const int bx = blockIdx.x - (sx.list ? 1 : 0);  // this block's 256 queries
+    const TargetDesc& tg = tdesc[tk];
+    const float4* __restrict__ p4 = tg.p4;
+    const int i = bx * 256 + threadIdx.x;
+    const bool valid = i < N;
+    const float inf = 3.0e38f;
+    float x = inf, y = inf, z = inf, bound = 0.0f;
+    if (valid) {
+        best[(size_t)slot * N + i] = kNone;  // split searches merge into it by atomicMin
+        double Q[12];
+#pragma unroll
+        for (int t = 0; t < 12; ++t) Q[t] = Qm[12 * slot + t];
+        const double p[3] = {src[3 * i], src[3 * i + 1], src[3 * i + 2]};
+        double q[3];
+        xform(Q, p, q);
+        x = (float)(q[0] - tg.ox), y = (float)(q[1] - tg.oy), z = (float)(q[2] - tg.oz);
+        bound = r2s;
+        const int jp = prevnn[(size_t)slot * N + i];
+        if (jp >= 0) {
+            bound = fminf(bound, d2f(x, y, z, p4[jp]) * kSeedSlack + 1e-30f);
+        } else if (jp == kNoSeed || reseed) {
+            for (int t = 0; t < tg.ntiles; t += tg.seed_stride)
+                bound = fminf(bound, d2f(x, y, z, p4[t * kTile]) * kSeedSlack + 1e-30f);
+        }
+        q32[(size_t)slot * N + i] = make_float4(x, y, z, bound);
+    }
+    if (!gbox) return;
+    // box and worst bound of each search wave's 128 queries (waves 0-1 and
+    // 2-3 of this block): what the search would reduce, computed once here
+    __shared__ float part[4][7];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const float r[7] = {wave_fmin(x), wave_fmin(y), wave_fmin(z), wave_fmax(valid ? x : -inf),
+                        wave_fmax(valid ? y : -inf), wave_fmax(valid ? z : -inf),
+                        __uint_as_float(wave_umax(__float_as_uint(bound)))};
+    if (lane < 7) part[w][lane] = r[lane];
+    __syncthreads();
+    if (threadIdx.x < 2 && (bx * 2 + threadIdx.x) * 128 < N) {
+        const float* a = part[2 * threadIdx.x];
+        const float* b = part[2 * threadIdx.x + 1];
+        float4* g = gbox + ((size_t)slot * ((N + 127) / 128) + bx * 2 + threadIdx.x) * 2;
+        g[0] = make_float4(fminf(a[0], b[0]), fminf(a[1], b[1]), fminf(a[2], b[2]),
+                           __uint_as_float(max(__float_as_uint(a[6]), __float_as_uint(b[6]))));
+        g[1] = make_float4(fmaxf(a[3], b[3]), fmaxf(a[4], b[4]), fmaxf(a[5], b[5]), 0.0f);
     }
 }
 
@@ -2338,9 +2348,15 @@ static int uniform_splits(const orpcd_ctx* c, int nact) {
 
 // the ordered dispatch serves the default per-kernel pass loop (not the
 // cooperative / two-phase searches, the persistent or the pipelined loops)
-bool sched_wanted(const orpcd_ctx* c, bool persist) {
+// of batches of at least sched_min_starts starts: below that its planning
+// (one block per start, beside the transform) and the wave's item lookup
+// cost more than the order gains (C2: 1 start 0.53 -> 0.65 ms, 8 starts
+// 4.53 -> 4.59 ms; 30 starts 16.6 -> 15.0 ms, 104 starts 43.7 -> 37.8 ms;
+// C5 1 start 1478 -> 1304 iterations/s)
+bool sched_wanted(const orpcd_ctx* c, bool persist, int B) {
     static const bool trace = getenv("ORPCD_TRACE") != nullptr;
-    return c->opt.sched && c->opt.search_kernel == 0 && !persist && (trace || !pipelined_ok(c));
+    return c->opt.sched && B >= c->opt.sched_min_starts && c->opt.search_kernel == 0 && !persist &&
+           (trace || !pipelined_ok(c));
 }
 
 // items per class: every item of a pass may fall in one class.  Pass 0:
@@ -2372,7 +2388,7 @@ hipError_t launch_xform(const orpcd_ctx* c, int nact, int pass, double r2, hipSt
         sx.S0 = uniform_splits(c, nact);
         sx.inv_want = 1.0f / (float)c->opt.sched_items;
     }
-    xform_queries_kernel<<<dim3((unsigned)((N + 255) / 256), (unsigned)nact), 256, 0, s>>>(
+    xform_queries_kernel<<<dim3((unsigned)((N + 255) / 256) + (sx.list ? 1u : 0u), (unsigned)nact), 256, 0, s>>>(
         c->src.xyz64.p, N, c->active.p, c->Q.p, c->done.p, c->tdesc.p, tb, c->prevnn.p, search_r2(r2),
         c->opt.reseed, c->q32.p, c->best.p, dev_nact ? c->ctl.p : nullptr, c->gbox.p, sx);
     return hipGetLastError();

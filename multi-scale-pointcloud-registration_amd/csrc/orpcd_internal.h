@@ -331,6 +331,8 @@ struct orpcd_ctx {
         int sched = 1;            // 1: search waves dispatched heaviest first, heavy query groups split
                                   // further (costs measured in the previous pass); 0: uniform splits
         int sched_items = 10240;  // ordered dispatch: split a group until its waves cost <= pass total / this
+                                  // (C2 sweep 5120 / 10240 / 20480: 15.4 / 15.0 / 16.6 ms at 30 starts)
+        int sched_min_starts = 16;  // ordered dispatch only for batches of at least this many starts
     } opt;
     std::vector<hipEvent_t> ev_pool;
     orpcd::KernelStats stats;
@@ -374,7 +376,7 @@ hipError_t launch_fps(const double* xyz, int64_t n, int first, int k, int max_bl
 int accum_blocks(int64_t N);
 hipError_t launch_xform(const orpcd_ctx* c, int nact, int pass, double r2, hipStream_t s, bool dev_nact,
                         const TgtBounds& tb);
-bool sched_wanted(const orpcd_ctx* c, bool persist);
+bool sched_wanted(const orpcd_ctx* c, bool persist, int B);
 int sched_capacity(const orpcd_ctx* c, int B);
 TgtBounds one_target();
 // bounds of the launch rows act[0..nact) (increasing slots) over the batch's targets

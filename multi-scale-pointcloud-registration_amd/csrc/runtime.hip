@@ -395,7 +395,7 @@ int batch_setup(orpcd_ctx* c, const double* R0, const double* t0, int B, const o
     c->two_phase_ok = c->opt.search_kernel == 2 && worst_items <= ((size_t)1 << 29);  // <= 2 GiB of items
     if (c->two_phase_ok) CTX_CHECK(c, c->items.ensure(worst_items));
     CTX_CHECK(c, c->item_counts.ensure((size_t)2 * B * ((N + 127) / 128) + 2));
-    c->sched_live = sched_wanted(c, persist);
+    c->sched_live = sched_wanted(c, persist, B);
     if (c->sched_live) {
         const size_t NG = (size_t)(N + 127) / 128;
         c->sched_cap = sched_capacity(c, B);
@@ -1491,6 +1491,7 @@ int orpcd_set_option(orpcd_ctx* c, const char* key, double value) {
     else if (k == "persist_fences" && (v == 0 || v == 1)) c->opt.persist_fences = v;
     else if (k == "sched" && (v == 0 || v == 1)) c->opt.sched = v;
     else if (k == "sched_items" && v >= 64 && v <= (1 << 22)) c->opt.sched_items = v;
+    else if (k == "sched_min_starts" && v >= 1) c->opt.sched_min_starts = v;
     else {
         c->err = "set_option: unknown key or bad value: " + k;
         return ORPCD_EINVAL;

@@ -29,6 +29,7 @@ def main():
     ap.add_argument("--cpu-iters", type=int, default=2)
     ap.add_argument("--parity", type=int, default=1, help="also run the full oracle GICP and compare")
     ap.add_argument("--out", default=None)
+    ap.add_argument("--opt", default="{}", help="runtime options (orpcd_set_option), JSON")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -42,6 +43,8 @@ def main():
     from workloads import c5_pair
     src, tgt = c5_pair(args.points)
     ctx = _native.Context()
+    for k, v in json.loads(args.opt).items():
+        ctx.set_option(k, v)
     params = dict(max_correspondence_distance=0.5, max_iteration=args.iters)
 
     t0 = time.perf_counter()
