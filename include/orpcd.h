@@ -45,6 +45,9 @@
  *       the feature matching inside registration_fgr_based_on_feature_matching
  *   orpcd_fgr_optimize
  *       FastGlobalOptimizer.optimize       Optimizer/fastGlobalOptimizer.py:146-190
+ *   orpcd_rng_draw_attempts
+ *       the np.random draws of initialize_rotation, attempt after attempt
+ *                                          Aligner/Aligner.py:125-162, 178-186
  */
 #ifndef ORPCD_H
 #define ORPCD_H
@@ -243,6 +246,15 @@ int orpcd_set_option(orpcd_ctx* ctx, const char* key, double value);
  * wave-parallel device code; per system 23 doubles each: det, x (6), the 4x4
  * update (16).  The two must agree bit for bit.                            */
 int orpcd_test_solve6(orpcd_ctx* ctx, const double* sums27, int32_t n, double* out_serial, double* out_wave);
+
+/* --------------------------------------------------------- host RNG replay
+ * n consecutive Aligner.initialize_rotation() draws (Aligner.py:129-131,160)
+ * from numpy's legacy MT19937 RandomState, bit for bit: per attempt three
+ * uniform(low, high) (theta, n x 3) then randn(3) (normal, n x 3).  The
+ * state is numpy's get_state() tuple: key (624 words), pos, has_gauss,
+ * cached gaussian; it is advanced in place.  Host code only (no device).   */
+int orpcd_rng_draw_attempts(uint32_t* key, int32_t* pos, int32_t* has_gauss, double* gauss, int64_t n,
+                            double low, double high, double* theta, double* normal);
 
 /* ------------------------------------------------------------ measurement
  * Live kernel timing (hipEvents on the context's stream).  When enabled,

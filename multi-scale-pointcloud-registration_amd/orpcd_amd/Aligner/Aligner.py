@@ -27,7 +27,6 @@ device batch, and replays the reference's decisions in order.  Results, the
 RNG position and delta are identical to the sequential search.
 """
 import copy
-import threading
 import time
 from typing import List, Tuple
 
@@ -53,7 +52,6 @@ from ..utils.logger_factory import LoggerFactory
 class Aligner:
     transfromation: np.ndarray = np.eye(4)
     scale_factors: np.ndarray = np.ones((1, 3))
-    prefetch_rng = True  # draw the next batch's RNG blocks on a helper thread while the device runs
 
     def __init__(self, source_preprocessor, target_preprocessor, optimizer: IOptimizer,
                  attempts: int = __MULTISTART_ATTEMPTS__, deg: float = __ALIGNER_DEG__, mu: float = __ALIGNER_MU__,
@@ -140,23 +138,30 @@ class Aligner:
 
     def _draw_block(self, n: int, rs=None):
         """n consecutive initialize_rotation() draws (Aligner.py:125-162), bit for
-        bit: the same scalar np.random calls in the same order (three uniform,
-        then randn(3), per attempt) and the same translation expression; the
-        cos / sin of all 3n angles by one ufunc call each and the n products
-        r_1 (r_2 r_3) by one stacked matmul, which give the scalar calls' and
-        np.dot's values (checked against the sequential draws in
-        tests/test_host.py::test_draw_block_matches_initialize_rotation)."""
-        rs = np.random if rs is None else rs  # the global legacy RandomState, or a copy of it
-        deg, uni, randn = self._deg, rs.uniform, rs.randn
-        th = np.empty((n, 3))
-        g = np.empty((n, 3))
-        for k in range(n):
-            # uniform(size=3) consumes the stream as three scalar uniform()
-            # calls and returns the same values (low + (high - low) * double);
-            # the Gaussians stay one randn(3) per attempt (its cached second
-            # deviate makes the order matter)
-            th[k] = uni(-deg, deg, 3)
-            g[k] = randn(3)
+        bit: the same stream consumption (three uniform, then randn(3), per
+        attempt) and the same translation expression; the cos / sin of all 3n
+        angles by one ufunc call each and the n products r_1 (r_2 r_3) by one
+        stacked matmul, which give the scalar calls' and np.dot's values
+        (checked against the sequential draws in
+        tests/test_host.py::test_draw_block_matches_initialize_rotation).
+        rs: the global legacy RandomState (default; advanced through numpy's
+        API), another RandomState, or a _native.LegacyDraws (the same stream
+        replayed in C++, ~25 ns instead of ~4.6 us per attempt)."""
+        deg = self._deg
+        if isinstance(rs, _native.LegacyDraws):
+            th, g = rs.draw(n, -deg, deg)
+        else:
+            rs = np.random if rs is None else rs
+            uni, randn = rs.uniform, rs.randn
+            th = np.empty((n, 3))
+            g = np.empty((n, 3))
+            for k in range(n):
+                # uniform(size=3) consumes the stream as three scalar uniform()
+                # calls and returns the same values (low + (high - low) * double);
+                # the Gaussians stay one randn(3) per attempt (its cached second
+                # deviate makes the order matter)
+                th[k] = uni(-deg, deg, 3)
+                g[k] = randn(3)
         t0s = list(self._mu + g * self._std)  # elementwise, as per attempt
         c, s = np.cos(th), np.sin(th)
         r = np.zeros((3, n, 3, 3))
@@ -194,8 +199,11 @@ class Aligner:
     def _draw_starts(self):
         """The attempts' (R0, t0) in the reference's order, and the RNG state after each."""
         before = np.random.get_state()
-        R0s, t0s = self._draw_block(self._attempts)  # same draws, same order as the sequential loop
-        return R0s, t0s, Aligner._BlockStates(self, before, np.random.get_state(), self._attempts)
+        rs = _native.LegacyDraws(before)
+        R0s, t0s = self._draw_block(self._attempts, rs)  # same draws, same order as the sequential loop
+        after = rs.state()
+        np.random.set_state(after)
+        return R0s, t0s, Aligner._BlockStates(self, before, after, self._attempts)
 
     def _run_tables(self, source, targets, draws, keys=None):
         """Per target k, the gathered per-attempt table of the starts draws[k].
@@ -281,24 +289,21 @@ class Aligner:
         block position p draws blocks p .. p+5 for +x, -x, +y, -y, +z, -z
         (:270-297) as far as it gets; accepting candidate k moves the position
         to p+k+1, failing all six to p+6.  Blocks are drawn once, in stream
-        order, from a private copy of the global state (``prefetch`` draws
-        ahead on a helper thread while the device runs); ``state_after``
-        gives the global state the reference leaves after a block."""
+        order, by the native replay of numpy's legacy generator
+        (_native.LegacyDraws) from the global state at align() entry;
+        ``state_after`` gives the global state the reference leaves after a
+        block."""
 
         def __init__(self, aligner):
             self._al = aligner
-            self._rs = np.random.RandomState()
-            self._rs.set_state(np.random.get_state())
-            self._states = [self._rs.get_state()]  # [j]: the state before block j
+            self._rs = _native.LegacyDraws(np.random.get_state())
+            self._states = [self._rs.state()]  # [j]: the state before block j
             self._blocks = []
-            self._lock = threading.Lock()
-            self._thread = None
 
         def _extend(self, j):
-            with self._lock:
-                while len(self._blocks) <= j:
-                    self._blocks.append(self._al._draw_block(self._al._attempts, self._rs))
-                    self._states.append(self._rs.get_state())
+            while len(self._blocks) <= j:
+                self._blocks.append(self._al._draw_block(self._al._attempts, self._rs))
+                self._states.append(self._rs.state())
 
         def draw(self, j):
             """Block j as _draw_starts returns it: (R0s, t0s, per-attempt states)."""
@@ -309,17 +314,6 @@ class Aligner:
         def state_after(self, j):
             self._extend(j)
             return self._states[j + 1]
-
-        def prefetch(self, j):
-            self.join()
-            if Aligner.prefetch_rng and len(self._blocks) <= j:
-                self._thread = threading.Thread(target=self._extend, args=(j,), daemon=True)
-                self._thread.start()
-
-        def join(self):
-            if self._thread is not None:
-                self._thread.join()
-                self._thread = None
 
     def _compass_steps(self, delta):
         """The candidate steps of one compass iteration in the reference's order
@@ -357,7 +351,6 @@ class Aligner:
 
         def run(items):
             draws = [tape.draw(b) for b, _ in items]
-            tape.prefetch(max(b for b, _ in items) + 6 * depth)  # the next batch's blocks, drawn while the device runs
             t_start = time.perf_counter()
             tables = self._run_tables(
                 source, lambda ks: self._scaled_targets(target, [items[k][1] for k in ks]), draws,
@@ -401,7 +394,6 @@ class Aligner:
                     self._delta = self._delta / 2
             np.random.set_state(tape.state_after(pos - 1))
         finally:
-            tape.join()
             self.speculative_history.extend(dict(B=self._attempts, iters=int(tb["iters"].sum()))
                                             for key, (tb, _) in done.items() if key not in used)
         return transformation, metric, scale_factors, errors

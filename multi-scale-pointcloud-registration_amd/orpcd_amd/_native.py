@@ -60,7 +60,37 @@ EXPORTED = ("orpcd_abi_version", "orpcd_device_count", "orpcd_ctx_create", "orpc
             "orpcd_fgr_optimize", "orpcd_set_source_points", "orpcd_icp_p2p_batch",
             "orpcd_sor", "orpcd_voxel_down_sample", "orpcd_farthest_downsample",
             "orpcd_set_option", "orpcd_set_targets", "orpcd_gicp_batch_targets", "orpcd_test_solve6",
-            "orpcd_profiling", "orpcd_stats", "orpcd_reset_stats")
+            "orpcd_profiling", "orpcd_stats", "orpcd_reset_stats", "orpcd_rng_draw_attempts")
+
+
+class LegacyDraws:
+    """numpy's legacy MT19937 RandomState, advanced by orpcd_rng_draw_attempts:
+    ``draw(n, low, high)`` returns (theta (n, 3), normal (n, 3)) exactly as n
+    consecutive ``(uniform(low, high, 3), randn(3))`` calls on the RandomState
+    whose ``get_state()`` tuple it was built from; ``state()`` is the tuple
+    after them (for ``set_state``)."""
+
+    def __init__(self, state):
+        name, key, pos, has_gauss, gauss = state
+        if name != "MT19937":
+            raise ValueError(f"legacy RandomState state expected, got {name}")
+        self._key = np.array(key, dtype=np.uint32)
+        self._pos = np.array([pos], dtype=np.int32)
+        self._hg = np.array([has_gauss], dtype=np.int32)
+        self._g = np.array([gauss], dtype=np.float64)
+        self._L = load_library()
+
+    def draw(self, n: int, low: float, high: float):
+        theta = np.empty((n, 3))
+        normal = np.empty((n, 3))
+        rc = self._L.orpcd_rng_draw_attempts(self._key, self._pos, self._hg, self._g, int(n), float(low),
+                                             float(high), theta, normal)
+        if rc != ORPCD_OK:
+            raise NativeError(f"orpcd_rng_draw_attempts failed (status {rc})")
+        return theta, normal
+
+    def state(self):
+        return ("MT19937", self._key.copy(), int(self._pos[0]), int(self._hg[0]), float(self._g[0]))
 
 
 def load_library():
@@ -114,6 +144,8 @@ def load_library():
         L.orpcd_profiling.argtypes = [vp, ctypes.c_int32]
         L.orpcd_stats.argtypes = [vp, _f64p, ctypes.c_int32]
         L.orpcd_reset_stats.argtypes = [vp]
+        L.orpcd_rng_draw_attempts.argtypes = [np.ctypeslib.ndpointer(dtype=np.uint32, flags="C_CONTIGUOUS"),
+                                              _i32p, _i32p, _f64p, c_i64, c_dbl, c_dbl, _f64p, _f64p]
         if L.orpcd_abi_version() != 1:
             raise NativeError("liborpcd_hip.so ABI mismatch")
         _lib = L

@@ -231,3 +231,38 @@ def test_speculative_plan_follows_the_fail_path():
     assert len(al._plan(1, sf, 0.05, 0, 3, initial=False)) == 6  # 0.025 < eps: no second iteration
     assert len(al._plan(5, sf, 0.2, 100, 3, initial=False)) == 6  # iteration 101 > max_iter
     assert al._plan(5, sf, 0.2, 101, 3, initial=False) == []
+
+
+def test_radius_scaler_matches_reference_formula():
+    """RadiusScaler (radiusScaler.py:25-30): mean, then max(cdist(center,
+    cloud)); the build takes the max of the squared norms before the sqrt and
+    must give the same bits."""
+    from scipy.spatial.distance import cdist
+    from orpcd_amd.Preprocessor.Scalers import RadiusScaler
+    rng = np.random.default_rng(3)
+    for k in range(20):
+        cloud = rng.normal(size=(5000 + 37 * k, 3)) * rng.uniform(1e-3, 1e3) + rng.normal(size=3) * 50
+        sc = RadiusScaler()
+        out = sc.process(cloud)
+        center = np.mean(cloud, axis=0, keepdims=True)
+        radius = np.max(cdist(center, cloud))
+        assert np.array_equal(sc.mean, center) and sc.scale == radius
+        assert np.array_equal(out, (cloud - center) / radius)
+
+
+@pytest.mark.parametrize("seed", [0, 5, 42])
+def test_native_rng_replay_matches_numpy(seed):
+    """_native.LegacyDraws (orpcd_rng_draw_attempts) replays numpy's legacy
+    RandomState bit for bit: the draws of uniform(low, high, 3) + randn(3) per
+    attempt and the state after them, across block sizes (odd counts leave a
+    cached gaussian) and from states with and without a cached gaussian."""
+    from orpcd_amd._native import LegacyDraws
+    rs = np.random.RandomState(seed)
+    ld = LegacyDraws(rs.get_state())
+    for n in (1, 2, 7, 64, 333, 1000):
+        th, g = ld.draw(n, -np.pi / 2, np.pi / 2)
+        for k in range(n):
+            assert np.array_equal(th[k], rs.uniform(-np.pi / 2, np.pi / 2, 3)), (n, k)
+            assert np.array_equal(g[k], rs.randn(3)), (n, k)
+        a, b = ld.state(), rs.get_state()
+        assert a[0] == b[0] and np.array_equal(a[1], b[1]) and a[2:] == b[2:]

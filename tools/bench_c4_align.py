@@ -47,13 +47,11 @@ def main():
     ap.add_argument("--allgather-us", type=float, default=50.0)
     ap.add_argument("--out", default=None)
     ap.add_argument("--depth", type=int, default=None, help="speculative_depth of the ranks (default: auto)")
-    ap.add_argument("--no-prefetch", action="store_true")
     a = ap.parse_args()
     from orpcd_amd import Aligner, GeneralizedICP, Preprocessor, parallel
     from workloads import c2_pair
 
     src, tgt = c2_pair(a.points)
-    Aligner.prefetch_rng = not a.no_prefetch
     opt = GeneralizedICP()
     real_world, real_gather = parallel.world, parallel.allgather_records
     orig_run_tables = Aligner._run_tables
@@ -151,7 +149,7 @@ def main():
         "per_call_rank_s": [[round(x, 5) for x in c] for c in rank_calls],
 
         "projected_speedup": round(t1 / tG, 2),
-        "speculative_depth": {"1gpu": "auto", "ranks": a.depth or "auto"}, "prefetch_rng": not a.no_prefetch,
+        "speculative_depth": {"1gpu": "auto", "ranks": a.depth or "auto"},
         "result": res1,
         "note": "every rank's shard timed alone on one MI355X (same seed, same control flow); its rows were "
                 "checked bit-identical to the 1-GPU table; all-gathers replayed and charged",
