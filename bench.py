@@ -110,12 +110,16 @@ def main():
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-        s = torch.tensor([st["ms"], st["launches"], st["pairs"]], dtype=torch.float64, device=dev)
+        s = torch.tensor([st["ms"], st["launches"], st["pairs"], st["sched_launches"]], dtype=torch.float64,
+                         device=dev)
         dist.all_reduce(s, op=dist.ReduceOp.SUM)
-        st["ms"], st["launches"], st["pairs"] = (float(x) for x in s.tolist())
+        st["ms"], st["launches"], st["pairs"], st["sched_launches"] = (float(x) for x in s.tolist())
 
     value = iters / elapsed
-    traffic, traffic_src = pmc_traffic()
+    # the search kernel that ran: the ordered dispatch for batches of >= 16
+    # starts (option sched_min_starts), else the uniform-split kernel
+    kname = "nn_search_sched_kernel" if st["sched_launches"] * 2 > st["launches"] else "nn_search_kernel"
+    traffic, traffic_src = pmc_traffic("orpcd::" + kname)
     avg_ms = st["ms"] / max(st["launches"], 1)
     flops_per_launch = st["pairs"] / max(st["launches"], 1) * FLOP_PER_PAIR
     achieved = flops_per_launch / (avg_ms * 1e-3) / 1e12 if avg_ms > 0 else 0.0
@@ -175,7 +179,7 @@ def main():
             "roofline": {"bound": "mfma", "achieved": round(achieved, 3), "peak": FP32_PEAK_TFLOPS,
                          "unit": "TFLOP/s", "frac": round(achieved / FP32_PEAK_TFLOPS, 4), "traffic": traffic,
                          "traffic_source": traffic_src,
-                         "kernel": "nn_search_kernel", "avg_launch_ms": round(avg_ms, 4),
+                         "kernel": kname, "avg_launch_ms": round(avg_ms, 4),
                          "search_kernel_ms_total": round(st["ms"], 3),
                          "launches": int(st["launches"]), "flop_per_pair": FLOP_PER_PAIR,
                          "pairs_per_launch": round(st["pairs"] / max(st["launches"], 1)),
@@ -196,7 +200,7 @@ def main():
         dist.destroy_process_group()
 
 
-def pmc_traffic(kernel="orpcd::nn_search_kernel"):
+def pmc_traffic(kernel):
     """HBM bytes per launch of `kernel` from the newest committed PMC summary
     (profiles/rNN_hbm.json: FETCH_SIZE x2 + WRITE_SIZE, MI355X_MICROARCH.md
     §HBM), collected by rocprofv3 --pmc on this same bench command."""

@@ -262,7 +262,9 @@ int orpcd_rng_draw_attempts(uint32_t* key, int32_t* pos, int32_t* has_gauss, dou
  * stats[0] = launches, [1] = total ms, [2] = query-target pairs evaluated
  * by the culled scan, [3] = GICP iterations completed, [4] = correspondence
  * passes (start x pass), [5] = 64-point target tiles scanned, [6] = total
- * ms of the fp64 accumulation kernel.  [1] times the search kernel only.   */
+ * ms of the fp64 accumulation kernel, [7] = how many of the timed launches
+ * ran the ordered-dispatch search (nn_search_sched_kernel; the rest ran
+ * nn_search_kernel).  [1] times the search kernel only.                    */
 int orpcd_profiling(orpcd_ctx* ctx, int32_t enable);
 int orpcd_stats(orpcd_ctx* ctx, double* stats_out, int32_t n);
 int orpcd_reset_stats(orpcd_ctx* ctx);

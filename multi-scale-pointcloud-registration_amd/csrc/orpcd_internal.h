@@ -160,6 +160,7 @@ struct VoxelBufs {  // preprocessing scratch (voxel, SOR, FPS)
 
 struct KernelStats {
     double launches = 0, ms = 0, pairs = 0, iterations = 0, passes = 0, tiles = 0, accum_ms = 0;
+    double sched_launches = 0;  // timed launches of the ordered-dispatch search (nn_search_sched_kernel)
 };
 
 // ------------------------------------------------- several targets per batch

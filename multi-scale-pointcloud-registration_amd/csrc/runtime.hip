@@ -992,6 +992,7 @@ int run_passes(orpcd_ctx* c, int B, const orpcd_gicp_params* p, double* T_out, d
                 if (trace) CTX_CHECK(c, hipEventElapsedTime(&ms2, c->ev_pool[3 * q + 1], c->ev_pool[3 * q + 2]));
                 if (c->profiling) {
                     c->stats.launches += 1;
+                    if (c->sched_live) c->stats.sched_launches += 1;
                     c->stats.ms += ms;
                     c->stats.accum_ms += ms2;
                 }
@@ -1524,9 +1525,9 @@ int orpcd_profiling(orpcd_ctx* c, int32_t enable) {
 
 int orpcd_stats(orpcd_ctx* c, double* out, int32_t n) {
     if (!c || !out) return ORPCD_EINVAL;
-    const double v[7] = {c->stats.launches, c->stats.ms, c->stats.pairs, c->stats.iterations, c->stats.passes,
-                         c->stats.tiles, c->stats.accum_ms};
-    for (int i = 0; i < n && i < 7; ++i) out[i] = v[i];
+    const double v[8] = {c->stats.launches, c->stats.ms, c->stats.pairs, c->stats.iterations, c->stats.passes,
+                         c->stats.tiles, c->stats.accum_ms, c->stats.sched_launches};
+    for (int i = 0; i < n && i < 8; ++i) out[i] = v[i];
     return ORPCD_OK;
 }
 

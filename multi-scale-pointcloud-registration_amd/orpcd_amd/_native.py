@@ -501,10 +501,10 @@ class Context:
         self._check(self._L.orpcd_profiling(self._h, int(bool(enable))), "orpcd_profiling")
 
     def stats(self) -> dict:
-        out = np.zeros(7)
-        self._check(self._L.orpcd_stats(self._h, out, 7), "orpcd_stats")
+        out = np.zeros(8)
+        self._check(self._L.orpcd_stats(self._h, out, 8), "orpcd_stats")
         return dict(launches=out[0], ms=out[1], pairs=out[2], iterations=out[3], passes=out[4], tiles=out[5],
-                    accum_ms=out[6])
+                    accum_ms=out[6], sched_launches=out[7])
 
     def reset_stats(self):
         self._check(self._L.orpcd_reset_stats(self._h), "orpcd_reset_stats")
