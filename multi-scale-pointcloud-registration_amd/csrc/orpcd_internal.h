@@ -172,7 +172,7 @@ struct KernelStats {
 // block's row `by` and per-launch row bounds passed by value (TgtBounds), with
 // no memory load; the target's device pointers come from a TargetDesc array
 // in device memory, static while the batch runs.
-constexpr int kMaxTargets = 8;
+constexpr int kMaxTargets = 16;
 
 struct TargetDesc {
     const float4 *p4, *tlo, *thi, *qbox, *slo, *shi;  // fp32 search layout (CloudLayout)
@@ -205,7 +205,8 @@ struct orpcd_ctx {
     // targets (set per scale candidate), Morton order; target 0 is `tgt`
     orpcd::CloudLayout tgts[orpcd::kMaxTargets];
     orpcd::DevBuf<double> tcovs[orpcd::kMaxTargets];  // M*6 GICP covariance (Morton order)
-    double tgt_eps[orpcd::kMaxTargets] = {-1.0, -1.0, -1.0, -1.0, -1.0, -1.0, -1.0, -1.0};
+    double tgt_eps[orpcd::kMaxTargets] = {-1.0, -1.0, -1.0, -1.0, -1.0, -1.0, -1.0, -1.0,
+                                          -1.0, -1.0, -1.0, -1.0, -1.0, -1.0, -1.0, -1.0};
     std::vector<double> tgt_host[orpcd::kMaxTargets];  // input-order copies (epsilon re-derivation)
     int ntgt = 0;                                      // targets set (orpcd_set_target: 1)
     orpcd::CloudLayout& tgt = tgts[0];

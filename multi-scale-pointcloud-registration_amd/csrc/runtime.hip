@@ -607,7 +607,7 @@ int orpcd_set_target(orpcd_ctx* c, const double* xyz, int64_t m, double epsilon)
 int orpcd_set_targets(orpcd_ctx* c, const double* xyz, const int64_t* m, int32_t ntargets, double epsilon) {
     if (!c) return ORPCD_EINVAL;
     CTX_REQUIRE(c, xyz && m, "set_targets: null argument");
-    CTX_REQUIRE(c, ntargets >= 1 && ntargets <= kMaxTargets, "set_targets: 1 to 8 targets");
+    CTX_REQUIRE(c, ntargets >= 1 && ntargets <= kMaxTargets, "set_targets: 1 to 16 targets");
     int64_t off = 0;
     for (int k = 0; k < ntargets; ++k) {
         CTX_REQUIRE(c, m[k] > 0 && m[k] < kMaxPoints, "set_targets: empty target cloud or too many points");

@@ -57,7 +57,7 @@ class Aligner:
                  attempts: int = __MULTISTART_ATTEMPTS__, deg: float = __ALIGNER_DEG__, mu: float = __ALIGNER_MU__,
                  std: float = __ALIGNER_STD__, delta: float = __ALIGNER_DELTA__, max_iter: int = __ALIGNER_MAX_ITER__,
                  eps: float = __ALIGNER_EPS__, visualize_intermediate_steps: bool = False, *,
-                 speculative_compass: bool = True, speculative_depth: int = None):
+                 speculative_compass: bool = True, speculative_depth: int = None, shard_interleave: bool = False):
         self._LOG = LoggerFactory.get_logger(log_name=self.__class__.__name__)
         checks = [("attempts", attempts, lambda v: v <= 0, __MULTISTART_ATTEMPTS__),
                   ("deg", deg, lambda v: v <= 0, __ALIGNER_DEG__),
@@ -93,6 +93,7 @@ class Aligner:
         # of 50k points: latency-bound, so a second iteration is nearly free),
         # else 1
         self._speculative_depth = speculative_depth
+        self._shard_interleave = shard_interleave
         self.speculative_history: List[dict] = []  # candidates run ahead but not reached by the reference's order
 
     # ----------------------------------------------------------------- RNG
@@ -205,34 +206,49 @@ class Aligner:
         np.random.set_state(after)
         return R0s, t0s, Aligner._BlockStates(self, before, after, self._attempts)
 
+    def _positions(self, K):
+        """Flat-list positions of the K multistarts' B attempts each: target-major
+        blocks (k * B + a), or interleaved (a * K + k, shard_interleave=True)."""
+        B = self._attempts
+        if self._shard_interleave:
+            return [k + K * np.arange(B) for k in range(K)]
+        return [k * B + np.arange(B) for k in range(K)]
+
     def _run_tables(self, source, targets, draws, keys=None):
         """Per target k, the gathered per-attempt table of the starts draws[k].
-        The K tables are sharded as ONE flat list of K x B starts (target-major):
-        this rank runs its contiguous block, which touches one or two targets
-        rather than all K (so it sets up only those targets), as one batch
-        (optimize_batch_multi when it spans several); one all-gather of the
-        flat table follows.  `keys` (the multistarts' (block, scale) identities)
-        is for instrumentation only."""
+        The K tables are sharded as ONE flat list of K x B starts: this rank
+        runs its contiguous block of positions as one batch
+        (optimize_batch_multi when it spans several targets); one all-gather
+        of the flat table follows.  Positions are target-major by default, so
+        a rank's block touches one or two targets rather than all K (it sets
+        up only those); with shard_interleave they are attempt-major, so every
+        rank runs an equal slice of every multistart (all K targets) and
+        costly candidates spread over the ranks.  `keys` (the multistarts'
+        (block, scale) identities) is for instrumentation only."""
         B, K = self._attempts, len(draws)
         rank, ws = parallel.world()
         lo, hi = parallel.shard(K * B, rank, ws)
+        pos = self._positions(K)
         local = np.zeros((0, parallel.REC))
         if hi > lo:
-            ks, R0, t0 = [], [], []
+            ks, R0, t0, sel = [], [], [], []
             for k in range(K):
-                a, b = max(lo - k * B, 0), min(hi - k * B, B)
-                if b > a:
+                at = np.nonzero((pos[k] >= lo) & (pos[k] < hi))[0]  # this rank's attempts of multistart k
+                if len(at):
                     ks.append(k)
-                    R0.append(np.array(draws[k][0][a:b]))
-                    t0.append(np.array(draws[k][1][a:b]))
+                    sel.append(pos[k][at])
+                    R0.append(np.array([draws[k][0][i] for i in at]))
+                    t0.append(np.array([draws[k][1][i] for i in at]))
             tg = targets(ks) if callable(targets) else [targets[k] for k in ks]
             if len(tg) > 1 and hasattr(self._optimizer, "optimize_batch_multi"):
                 res = self._optimizer.optimize_batch_multi(source, tg, R0, t0)
             else:
                 res = [self._optimizer.optimize_batch(source, g, r, t) for g, r, t in zip(tg, R0, t0)]
-            local = np.concatenate([parallel.pack(r) for r in res])
+            local = np.zeros((hi - lo, parallel.REC))
+            for p_k, r in zip(sel, res):
+                local[p_k - lo] = parallel.pack(r)
         table = parallel.allgather_records(local, K * B)
-        return [parallel.unpack(table[k * B:(k + 1) * B]) for k in range(K)]
+        return [parallel.unpack(table[pos[k]]) for k in range(K)]
 
     def _select(self, table, draw):
         """Aligner.py:178-202 over a finished table, in attempt order: strict <,

@@ -103,14 +103,14 @@ class GeneralizedICP(IOptimizer):
 
     def optimize_batch_multi(self, source: np.ndarray, targets, R0s, t0s) -> list:
         """``optimize_batch`` for several targets at once (the speculative
-        compass of ``Aligner``): up to 8 targets run as ONE device batch
+        compass of ``Aligner``): up to 16 targets run as ONE device batch
         (orpcd_set_targets + orpcd_gicp_batch_targets), start (k, b) being
         ``source @ R0s[k][b] + t0s[k][b]`` against ``targets[k]``; more targets
-        run in groups of 8.  Returns the per-target result dicts."""
+        run in groups of 16.  Returns the per-target result dicts."""
         ctx = self.context
         out = []
-        for g in range(0, len(targets), 8):
-            tg, Rg, tg0 = targets[g:g + 8], R0s[g:g + 8], t0s[g:g + 8]
+        for g in range(0, len(targets), 16):
+            tg, Rg, tg0 = targets[g:g + 16], R0s[g:g + 16], t0s[g:g + 16]
             ctx.set_targets(tg, self._epsilon)
             ctx.set_source(source)
             sizes = [len(r) for r in Rg]

@@ -233,7 +233,7 @@ class Context:
         self._target_key = key
 
     def set_targets(self, targets, epsilon: float = 1e-3, cache: bool = True):
-        """Up to 8 targets for gicp_batch_targets (target k = targets[k])."""
+        """Up to 16 targets for gicp_batch_targets (target k = targets[k])."""
         ts = [_c3(t) for t in targets]
         key = (tuple(self._key(t) for t in ts), float(epsilon), "multi")
         if cache and key == self._target_key:

@@ -18,7 +18,7 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, out_dir, speculative=False):
+def _worker(rank, world, port, out_dir, speculative=False, interleave=False):
     sys.path[:0] = [PKG, os.path.join(REPO, "tests", "golden"), os.path.join(REPO, "tests")]
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     import torch.distributed as dist
@@ -30,7 +30,7 @@ def _worker(rank, world, port, out_dir, speculative=False):
     np.random.seed(7)
     inner = ScriptedOptimizer(g["goal"], mode="scripted")
     opt = (SpeculativeScripted if speculative else BatchedScripted)(inner)
-    al = Aligner(Preprocessor([]), Preprocessor([]), opt, attempts=4)
+    al = Aligner(Preprocessor([]), Preprocessor([]), opt, attempts=4, shard_interleave=interleave)
     T, m, sf, err = al.align(g["src"].copy(), g["tgt"].copy(), refine_registration=False)
     np.savez(os.path.join(out_dir, f"rank{rank}.npz"), T=T, m=m, sf=sf, err=np.asarray(err),
              batches=np.asarray(opt.batches), rng=np.random.uniform(size=4))
@@ -55,15 +55,17 @@ def test_sharded_multistart_matches_reference_trace(tmp_path, world):
     assert np.all(per_ms == 4) and all(np.all(s < 4) for s in shards)
 
 
-@pytest.mark.parametrize("world", [2, 3, 5])
-def test_sharded_speculative_compass_matches_reference_trace(tmp_path, world):
-    """The speculative compass over ranks: each compass iteration's 6 x 4
-    starts are sharded as one flat list (a rank's block spans one or two
-    candidates), one all-gather per iteration; every rank reproduces the
-    reference's align() (G3) and its RNG position."""
+@pytest.mark.parametrize("world,interleave", [(2, False), (3, False), (5, False), (3, True)])
+def test_sharded_speculative_compass_matches_reference_trace(tmp_path, world, interleave):
+    """The speculative compass over ranks: each device batch's multistarts
+    (the initial one, compass iterations' 6 x 4 starts) are sharded as one
+    flat list -- target-major (a rank's block spans one or two candidates) or
+    interleaved (every rank an equal slice of every candidate) -- with one
+    all-gather per batch; every rank reproduces the reference's align() (G3)
+    and its RNG position."""
     import torch.multiprocessing as mp
-    mp.start_processes(_worker, args=(world, _free_port(), str(tmp_path), True), nprocs=world, join=True,
-                       start_method="spawn")
+    mp.start_processes(_worker, args=(world, _free_port(), str(tmp_path), True, interleave), nprocs=world,
+                       join=True, start_method="spawn")
     g = np.load(f"{GOLDEN}/g3_aligner_trace.npz")
     for r in range(world):
         z = np.load(tmp_path / f"rank{r}.npz")

@@ -47,6 +47,7 @@ def main():
     ap.add_argument("--allgather-us", type=float, default=50.0)
     ap.add_argument("--out", default=None)
     ap.add_argument("--depth", type=int, default=None, help="speculative_depth of the ranks (default: auto)")
+    ap.add_argument("--interleave", action="store_true", help="ranks shard the flat start list attempt-major")
     a = ap.parse_args()
     from orpcd_amd import Aligner, GeneralizedICP, Preprocessor, parallel
     from workloads import c2_pair
@@ -69,7 +70,8 @@ def main():
 
     def align_once(depth=None):
         np.random.seed(a.seed)
-        al = Aligner(Preprocessor([]), Preprocessor([]), opt, attempts=a.attempts, speculative_depth=depth)
+        al = Aligner(Preprocessor([]), Preprocessor([]), opt, attempts=a.attempts, speculative_depth=depth,
+                     shard_interleave=a.interleave and parallel.world()[1] > 1)
         calls.clear()
         t0 = time.perf_counter()
         T, m, sf, err = al.align(src.copy(), tgt.copy(), refine_registration=False)
@@ -82,11 +84,14 @@ def main():
     rows = {}  # (block, scale) -> the multistart's gathered rows
     ngather = [0]
 
+    def positions(K, interleave):  # as Aligner._positions
+        return [k + K * np.arange(a.attempts) if interleave else k * a.attempts + np.arange(a.attempts)
+                for k in range(K)]
+
     def recording_gather(local, B):
         t = real_gather(local, B)
-        n = B // len(cur_keys)
-        for i, key in enumerate(cur_keys):
-            rows[key] = t[i * n:(i + 1) * n].copy()
+        for key, p in zip(cur_keys, positions(len(cur_keys), False)):  # the 1-GPU run: target-major
+            rows[key] = t[p].copy()
         ngather[0] += 1
         return t
 
@@ -102,15 +107,14 @@ def main():
         k = [0]
 
         def replay(local, B, r=r):
-            n = B // len(cur_keys)
             full = np.zeros((B, parallel.REC))
             known = np.zeros(B, bool)
-            for i, key in enumerate(cur_keys):
+            for key, p in zip(cur_keys, positions(len(cur_keys), a.interleave)):
                 if key in rows:
-                    full[i * n:(i + 1) * n] = rows[key]
-                    known[i * n:(i + 1) * n] = True
+                    full[p] = rows[key]
+                    known[p] = True
                 else:
-                    full[i * n:(i + 1) * n, 0] = np.inf
+                    full[p, 0] = np.inf
             lo, hi = parallel.shard(B, r, a.ranks)
             m = known[lo:hi]
             assert np.array_equal(local[m], full[lo:hi][m]), f"rank {r} call {k[0]}: sharded rows differ"
@@ -149,7 +153,7 @@ def main():
         "per_call_rank_s": [[round(x, 5) for x in c] for c in rank_calls],
 
         "projected_speedup": round(t1 / tG, 2),
-        "speculative_depth": {"1gpu": "auto", "ranks": a.depth or "auto"},
+        "speculative_depth": {"1gpu": "auto", "ranks": a.depth or "auto"}, "shard_interleave": a.interleave,
         "result": res1,
         "note": "every rank's shard timed alone on one MI355X (same seed, same control flow); its rows were "
                 "checked bit-identical to the 1-GPU table; all-gathers replayed and charged",
