@@ -39,6 +39,7 @@
 //    queries of the next pass (fp64 transform, one rounding).
 #include <cstdio>
 #include <cstdlib>
+#include <type_traits>
 #include <vector>
 
 #include "device_math.h"
@@ -445,6 +446,10 @@ static inline float search_r2(double r2) { return (float)(r2 * (1.0 + 1e-5)) * 1
 // seed slack: bound = d^2(seed) * (1 + 1e-4) so the seed target itself (and
 // any closer one) is re-found by the scan (1e-4 >> the 2^-17 key truncation)
 constexpr float kSeedSlack = 1.0001f;
+__device__ __forceinline__ float seed_bound(float d2) {
+#pragma clang fp contract(off)  // the same rounding in every transform kernel (a bound: answers never depend on it)
+    return d2 * kSeedSlack + 1e-30f;
+}
 
 // ---------------------------------------------------------------------------
 // Cost-ordered search dispatch (opt.sched).  The search of pass p measures
@@ -488,7 +493,8 @@ struct SchedS {                          // search side (pass p)
 
 // The ordered dispatch's work items of start `slot` (one block per start,
 // launched beside the query transform's blocks).
-__device__ __forceinline__ void plan_start_items(const SchedX& sx, int slot, int tk) {
+template <class Gate = bool (*)()>
+__device__ __forceinline__ void plan_start_items(const SchedX& sx, int slot, int tk, Gate gate = nullptr) {
     const int lane = threadIdx.x & 63;
     // The items depend only on the previous pass's costs, so this block runs
     // beside the transform blocks (as the sequel of one of them it lengthened
@@ -526,6 +532,9 @@ __device__ __forceinline__ void plan_start_items(const SchedX& sx, int slot, int
         atomicAdd(lcnt + cls, (unsigned)S);
     }
     __syncthreads();
+    if constexpr (!std::is_same<Gate, bool (*)()>::value) {
+        if (!gate()) return;  // fused solve: the start finished in this pass's solve: no items
+    }
     if (threadIdx.x < kSchedClasses) {
         const unsigned n = lcnt[threadIdx.x];
         lbase[threadIdx.x] = n ? atomicAdd(sx.cnt + threadIdx.x, n) : 0u;
@@ -539,6 +548,29 @@ __device__ __forceinline__ void plan_start_items(const SchedX& sx, int slot, int
         sx.wcost_cur[(size_t)slot * NG + g] = 0u;
         unsigned long long* out = sx.list + (size_t)cls * sx.cap + at;
         for (int k = 0; k < S; ++k) out[k] = sched_item(slot, tk, g, k, S);
+    }
+}
+
+// box and worst bound of each search wave's 128 queries (waves 0-1 and 2-3
+// of this 256-query block bx): what the search would reduce, computed once
+// by the query transform.  Every thread of the block calls it.
+__device__ __forceinline__ void write_gbox(float x, float y, float z, float bound, bool valid, int slot, int bx, int N,
+                                           float4* __restrict__ gbox) {
+    const float inf = 3.0e38f;
+    __shared__ float part[4][7];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const float r[7] = {wave_fmin(x), wave_fmin(y), wave_fmin(z), wave_fmax(valid ? x : -inf),
+                        wave_fmax(valid ? y : -inf), wave_fmax(valid ? z : -inf),
+                        __uint_as_float(wave_umax(__float_as_uint(bound)))};
+    if (lane < 7) part[w][lane] = r[lane];
+    __syncthreads();
+    if (threadIdx.x < 2 && (bx * 2 + threadIdx.x) * 128 < N) {
+        const float* a = part[2 * threadIdx.x];
+        const float* b = part[2 * threadIdx.x + 1];
+        float4* g = gbox + ((size_t)slot * ((N + 127) / 128) + bx * 2 + threadIdx.x) * 2;
+        g[0] = make_float4(fminf(a[0], b[0]), fminf(a[1], b[1]), fminf(a[2], b[2]),
+                           __uint_as_float(max(__float_as_uint(a[6]), __float_as_uint(b[6]))));
+        g[1] = make_float4(fmaxf(a[3], b[3]), fmaxf(a[4], b[4]), fmaxf(a[5], b[5]), 0.0f);
     }
 }
 
@@ -583,31 +615,15 @@ __global__ __launch_bounds__(256) void xform_queries_kernel(const double* __rest
         bound = r2s;
         const int jp = prevnn[(size_t)slot * N + i];
         if (jp >= 0) {
-            bound = fminf(bound, d2f(x, y, z, p4[jp]) * kSeedSlack + 1e-30f);
+            bound = fminf(bound, seed_bound(d2f(x, y, z, p4[jp])));
         } else if (jp == kNoSeed || reseed) {
             for (int t = 0; t < tg.ntiles; t += tg.seed_stride)
-                bound = fminf(bound, d2f(x, y, z, p4[t * kTile]) * kSeedSlack + 1e-30f);
+                bound = fminf(bound, seed_bound(d2f(x, y, z, p4[t * kTile])));
         }
         q32[(size_t)slot * N + i] = make_float4(x, y, z, bound);
     }
     if (!gbox) return;
-    // box and worst bound of each search wave's 128 queries (waves 0-1 and
-    // 2-3 of this block): what the search would reduce, computed once here
-    __shared__ float part[4][7];
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    const float r[7] = {wave_fmin(x), wave_fmin(y), wave_fmin(z), wave_fmax(valid ? x : -inf),
-                        wave_fmax(valid ? y : -inf), wave_fmax(valid ? z : -inf),
-                        __uint_as_float(wave_umax(__float_as_uint(bound)))};
-    if (lane < 7) part[w][lane] = r[lane];
-    __syncthreads();
-    if (threadIdx.x < 2 && (bx * 2 + threadIdx.x) * 128 < N) {
-        const float* a = part[2 * threadIdx.x];
-        const float* b = part[2 * threadIdx.x + 1];
-        float4* g = gbox + ((size_t)slot * ((N + 127) / 128) + bx * 2 + threadIdx.x) * 2;
-        g[0] = make_float4(fminf(a[0], b[0]), fminf(a[1], b[1]), fminf(a[2], b[2]),
-                           __uint_as_float(max(__float_as_uint(a[6]), __float_as_uint(b[6]))));
-        g[1] = make_float4(fmaxf(a[3], b[3]), fmaxf(a[4], b[4]), fmaxf(a[5], b[5]), 0.0f);
-    }
+    write_gbox(x, y, z, bound, valid, slot, bx, N, gbox);
 }
 
 #ifdef ORPCD_WAVETIME
@@ -934,10 +950,10 @@ __global__ __launch_bounds__(1024) void nn_search_coop_kernel(
                 float bound = r2s;
                 const int jp = prevnn[(size_t)slot * N + i];
                 if (jp >= 0) {
-                    bound = fminf(bound, d2f(x, y, z, p4[jp]) * kSeedSlack + 1e-30f);
+                    bound = fminf(bound, seed_bound(d2f(x, y, z, p4[jp])));
                 } else if (jp == kNoSeed || reseed) {
                     for (int t = 0; t < ntiles; t += seed_stride)
-                        bound = fminf(bound, d2f(x, y, z, p4[t * kTile]) * kSeedSlack + 1e-30f);
+                        bound = fminf(bound, seed_bound(d2f(x, y, z, p4[t * kTile])));
                 }
                 qv = make_float4(x, y, z, bound);
             }
@@ -1151,10 +1167,10 @@ __global__ __launch_bounds__(256) void cull_groups_kernel(
             float b = r2s;
             const int jp = prevnn[(size_t)slot * N + i];
             if (jp >= 0) {
-                b = fminf(b, d2f(x, y, z, p4[jp]) * kSeedSlack + 1e-30f);
+                b = fminf(b, seed_bound(d2f(x, y, z, p4[jp])));
             } else if (jp == kNoSeed || reseed) {
                 for (int t = 0; t < ntiles; t += seed_stride)
-                    b = fminf(b, d2f(x, y, z, p4[t * kTile]) * kSeedSlack + 1e-30f);
+                    b = fminf(b, seed_bound(d2f(x, y, z, p4[t * kTile])));
             }
             qv = make_float4(x, y, z, b);
             q32[(size_t)slot * N + i] = qv;
@@ -1977,6 +1993,132 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 2))) void
     solve_start<kEst>(slot, s, N, pass, max_iter, rel_fit, rel_rmse, a, pin);
 }
 
+// ---------------------------------------------------------------------------
+// Fused solve + query transform (opt.fuse_solve): one launch per pass instead
+// of icp_solve_kernel followed by xform_queries_kernel.  Per start row:
+//   a solver     (wave 0): the partials, the 6x6 solve, the pose
+//                update (sc1 stores, as the pipelined loop's solve), then a
+//                relaxed agent flag ready[slot] = pass + 1 (MI355X_MICROARCH.md
+//                inter-workgroup hand-off, first row: every store sc1 and
+//                drained by s_waitcnt vmcnt(0), one lane signals, the polling
+//                lane then a workgroup barrier, every load of the handed-off
+//                bytes sc1);
+//   a planner    the ordered dispatch's (if live): it counts its items
+//                from the previous costs, then waits for the flag and files
+//                them only if the start is still running;
+//   transform    blocks: the pose-independent loads (source point,
+//                previous correspondence and its target point) are issued
+//                before the wait, so the solve overlaps them.
+// Blocks are dispatched in linear order and every solver precedes every
+// waiting block, so the solvers are resident or done before anything waits
+// on them; the wait is bounded (error flag, checked by the host at every sync).
+// ---------------------------------------------------------------------------
+struct FuseArgs {
+    const double* partial;
+    int nblk;
+    int pass;  // the pass just accumulated: this launch solves it and forms pass + 1's queries
+    int max_iter;
+    double rel_fit, rel_rmse;
+    int64_t N;
+    SolveArgs a;
+    int32_t* ready;  // per slot: the last pass whose pose was published
+    unsigned* err;   // a wait that timed out
+    int nact;        // launch rows
+};
+
+__device__ __forceinline__ void wait_ready(const FuseArgs& f, int slot, int tag) {
+    if (threadIdx.x == 0) {
+        unsigned spins = 0;
+        while (__hip_atomic_load(f.ready + slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < tag) {
+            __builtin_amdgcn_s_sleep(2);
+            if (++spins > (1u << 24)) {  // ~seconds: never in a sound run
+                atomicOr(f.err, 1u);
+                break;
+            }
+        }
+    }
+    __syncthreads();
+}
+
+template <int kEst>
+__global__ __launch_bounds__(256) void solve_xform_kernel(const double* __restrict__ src, int N,
+                                                          const int32_t* __restrict__ active,
+                                                          const TargetDesc* __restrict__ tdesc, TgtBounds tb,
+                                                          const int32_t* __restrict__ prevnn, float r2s, int reseed,
+                                                          float4* __restrict__ q32,
+                                                          unsigned long long* __restrict__ best,
+                                                          float4* __restrict__ gbox, SchedX sx, FuseArgs f) {
+    // 1-D grid: every start's solver first (all dispatched at once, before
+    // any block that waits), then the planners, then the transform blocks row
+    // by row (a row-major 2-D grid put row r's solver behind every earlier
+    // row's transform blocks: the solves ran one after another)
+    const int nact = f.nact, xb = (N + 255) / 256;
+    const int b = blockIdx.x;
+    const int nsp = nact * (sx.list ? 2 : 1);
+    const int row = b < nact ? b : b < nsp ? b - nact : (b - nsp) / xb;
+    const int slot = active[row];
+    const int tag = f.pass + 1;
+    if (b < nact) {  // the solver
+        if (threadIdx.x >= 64) return;
+        const int finished = __hip_atomic_load(f.a.done + slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const double pose = pose_lane_load<false>(slot, f.a);
+        double s[kNacc];
+        reduce_partials(f.partial, slot, f.nblk, s);
+        if (!finished) {
+            PoseIn pin;
+            pose_from_lanes(pose, pin);
+            solve_start<kEst, true>(slot, s, f.N, f.pass, f.max_iter, f.rel_fit, f.rel_rmse, f.a, pin);
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the sc1 pose / done stores have landed
+        if (threadIdx.x == 0) __hip_atomic_store(f.ready + slot, tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        return;
+    }
+    const int tk = target_of_row(tb, row);
+    if (b < nsp) {  // the planner: items only if the start keeps running
+        plan_start_items(sx, slot, tk, [&]() {
+            wait_ready(f, slot, tag);
+            return __hip_atomic_load(f.a.done + slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0;
+        });
+        return;
+    }
+    const int bx = (b - nsp) - row * xb;
+    const TargetDesc& tg = tdesc[tk];
+    const float4* __restrict__ p4 = tg.p4;
+    const int i = bx * 256 + threadIdx.x;
+    const bool valid = i < N;
+    // pose-independent loads first: they overlap the solve
+    double p[3] = {0.0, 0.0, 0.0};
+    int jp = -1;
+    float4 tj = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (valid) {
+        p[0] = src[3 * i], p[1] = src[3 * i + 1], p[2] = src[3 * i + 2];
+        jp = prevnn[(size_t)slot * N + i];
+        if (jp >= 0) tj = p4[jp];
+    }
+    wait_ready(f, slot, tag);
+    if (__hip_atomic_load(f.a.done + slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return;  // block-uniform
+    const float inf = 3.0e38f;
+    float x = inf, y = inf, z = inf, bound = 0.0f;
+    if (valid) {
+        best[(size_t)slot * N + i] = kNone;  // split searches merge into it by atomicMin
+        double Q[12];
+#pragma unroll
+        for (int t = 0; t < 12; ++t) Q[t] = ld_f64<true>(f.a.Q + 12 * slot + t);  // sc1: written by the solver
+        double q[3];
+        xform(Q, p, q);
+        x = (float)(q[0] - tg.ox), y = (float)(q[1] - tg.oy), z = (float)(q[2] - tg.oz);
+        bound = r2s;
+        if (jp >= 0) {
+            bound = fminf(bound, seed_bound(d2f(x, y, z, tj)));
+        } else if (jp == kNoSeed || reseed) {
+            for (int t = 0; t < tg.ntiles; t += tg.seed_stride)
+                bound = fminf(bound, seed_bound(d2f(x, y, z, p4[t * kTile])));
+        }
+        q32[(size_t)slot * N + i] = make_float4(x, y, z, bound);
+    }
+    write_gbox(x, y, z, bound, valid, slot, bx, N, gbox);
+}
+
 // --------------------------------------------------------------------------
 // Persistent pass loop (default): the whole ICP loop of every start of the
 // batch in ONE launch, each start advancing at its own pace.
@@ -2088,10 +2230,10 @@ __device__ __forceinline__ void persist_search_item(const PersistArgs& P, int sl
             b = P.r2s;
             const int jp = ld_i32<true>(P.prevnn + (size_t)slot * N + i);
             if (jp >= 0) {
-                b = fminf(b, d2f(x, y, z, P.p4[jp]) * kSeedSlack + 1e-30f);
+                b = fminf(b, seed_bound(d2f(x, y, z, P.p4[jp])));
             } else if (jp == kNoSeed || P.reseed) {
                 for (int t = 0; t < P.ntiles; t += P.seed_stride)
-                    b = fminf(b, d2f(x, y, z, P.p4[t * kTile]) * kSeedSlack + 1e-30f);
+                    b = fminf(b, seed_bound(d2f(x, y, z, P.p4[t * kTile])));
             }
         }
         qx[k] = x;
@@ -2292,7 +2434,7 @@ __global__ __launch_bounds__(kCBlock) void nn1_kernel(const double* __restrict__
         float b = valid ? r2s : 0.0f;
         if (valid)
             for (int t = 0; t < ntiles; t += seed_stride)
-                b = fminf(b, d2f(qx[k], qy[k], qz[k], p4[t * kTile]) * kSeedSlack + 1e-30f);
+                b = fminf(b, seed_bound(d2f(qx[k], qy[k], qz[k], p4[t * kTile])));
         bound[k] = b;
     }
     culled_search<false>(stage[wid], p4, tlo, thi, qbox, ntiles, slo, shi, nsuper, 1, 1, 0, qx, qy, qz, bound, bd, bj,
@@ -2368,26 +2510,32 @@ int sched_capacity(const orpcd_ctx* c, int B) {
     return (int)(std::max<int64_t>(c->opt.sched_items, c->opt.search_waves) + 2 * (int64_t)B * NG + 64);
 }
 
+// the ordered dispatch's planner arguments for the queries of `pass` (none
+// when the batch runs the uniform dispatch)
+static SchedX sched_x(const orpcd_ctx* c, int nact, int pass) {
+    SchedX sx{};
+    if (!c->sched_live) return sx;
+    const size_t B = (size_t)c->sched_B;
+    const size_t NG = (size_t)(c->src.n + 127) / 128;
+    const int par = pass & 1;
+    sx.wcost_prev = c->wcost.p + (size_t)(par ^ 1) * B * NG;
+    sx.wcost_cur = c->wcost.p + (size_t)par * B * NG;
+    sx.wtot_prev = c->wtot.p + (size_t)(par ^ 1) * kSchedTot;
+    sx.cnt = c->wcnt.p + (size_t)par * kSchedClasses;
+    sx.list = c->wlist.p;
+    sx.cap = c->sched_cap;
+    sx.NG = (int)NG;
+    sx.have_cost = pass > 0;
+    sx.S0 = uniform_splits(c, nact);
+    sx.inv_want = 1.0f / (float)c->opt.sched_items;
+    return sx;
+}
+
 hipError_t launch_xform(const orpcd_ctx* c, int nact, int pass, double r2, hipStream_t s, bool dev_nact,
                         const TgtBounds& tb) {
     if (use_coop(c) || use_two_phase(c)) return hipSuccess;  // these searches transform their own queries
     const int N = (int)c->src.n;
-    SchedX sx{};
-    if (c->sched_live && !dev_nact) {
-        const size_t B = (size_t)c->sched_B;
-        const size_t NG = (size_t)(N + 127) / 128;
-        const int par = pass & 1;
-        sx.wcost_prev = c->wcost.p + (size_t)(par ^ 1) * B * NG;
-        sx.wcost_cur = c->wcost.p + (size_t)par * B * NG;
-        sx.wtot_prev = c->wtot.p + (size_t)(par ^ 1) * kSchedTot;
-        sx.cnt = c->wcnt.p + (size_t)par * kSchedClasses;
-        sx.list = c->wlist.p;
-        sx.cap = c->sched_cap;
-        sx.NG = (int)NG;
-        sx.have_cost = pass > 0;
-        sx.S0 = uniform_splits(c, nact);
-        sx.inv_want = 1.0f / (float)c->opt.sched_items;
-    }
+    const SchedX sx = dev_nact ? SchedX{} : sched_x(c, nact, pass);
     xform_queries_kernel<<<dim3((unsigned)((N + 255) / 256) + (sx.list ? 1u : 0u), (unsigned)nact), 256, 0, s>>>(
         c->src.xyz64.p, N, c->active.p, c->Q.p, c->done.p, c->tdesc.p, tb, c->prevnn.p, search_r2(r2),
         c->opt.reseed, c->q32.p, c->best.p, dev_nact ? c->ctl.p : nullptr, c->gbox.p, sx);
@@ -2592,6 +2740,24 @@ hipError_t launch_gicp_pass(const orpcd_ctx* c, int nact, int pass, double r2, h
 hipError_t launch_gicp_solve(const orpcd_ctx* c, int nact, int pass, const orpcd_gicp_params& p, hipStream_t s,
                              const TgtBounds& tb) {
     const SolveArgs a = solve_args(c);
+    if (c->fuse_live) {  // one launch: the solve and the next pass's queries (solve_xform_kernel)
+        const int N = (int)c->src.n;
+        const double r2 = p.max_correspondence_distance * p.max_correspondence_distance;
+        const SchedX sx = sched_x(c, nact, pass + 1);
+        const FuseArgs f{c->partial.p,    accum_blocks(N), pass, p.max_iteration, p.relative_fitness,
+                         p.relative_rmse, (int64_t)N,      a,    c->ready.p,      c->fuse_err.p,
+                         nact};
+        const dim3 grid((unsigned)((int64_t)nact * ((N + 255) / 256 + (sx.list ? 2 : 1))));
+        if (c->est == kEstP2P)
+            solve_xform_kernel<kEstP2P><<<grid, 256, 0, s>>>(c->src.xyz64.p, N, c->active.p, c->tdesc.p, tb,
+                                                              c->prevnn.p, search_r2(r2), c->opt.reseed, c->q32.p,
+                                                              c->best.p, c->gbox.p, sx, f);
+        else
+            solve_xform_kernel<kEstGICP><<<grid, 256, 0, s>>>(c->src.xyz64.p, N, c->active.p, c->tdesc.p, tb,
+                                                               c->prevnn.p, search_r2(r2), c->opt.reseed, c->q32.p,
+                                                               c->best.p, c->gbox.p, sx, f);
+        return hipGetLastError();
+    }
     auto solve = c->est == kEstP2P ? icp_solve_kernel<1> : icp_solve_kernel<0>;
     solve<<<(unsigned)nact, 64, 0, s>>>(c->active.p, c->partial.p, accum_blocks(c->src.n), nullptr,
                                                     c->src.n, pass, p.max_iteration, p.relative_fitness,

@@ -264,6 +264,10 @@ struct orpcd_ctx {
     int sched_cap = 0;
     int sched_B = 0;                             // starts of the batch (wcost parity stride B x NG)
     bool sched_live = false;                     // the running batch uses the ordered dispatch
+    // fused solve + query transform (opt.fuse_solve; gicp_kernels.hip, solve_xform_kernel)
+    orpcd::DevBuf<int32_t> ready;                // B: the last pass whose pose the solver published
+    orpcd::DevBuf<unsigned> fuse_err;            // 1: a transform block's wait for its solver timed out
+    bool fuse_live = false;                      // the running batch uses it
 
     // kernel-level entry points
     orpcd::CloudLayout aux;
@@ -335,6 +339,7 @@ struct orpcd_ctx {
         int sched_items = 10240;  // ordered dispatch: split a group until its waves cost <= pass total / this
                                   // (C2 sweep 5120 / 10240 / 20480: 15.4 / 15.0 / 16.6 ms at 30 starts)
         int sched_min_starts = 16;  // ordered dispatch only for batches of at least this many starts
+        int fuse_solve = 1;       // 1: the 6x6 solve runs inside the next pass's query transform launch
     } opt;
     std::vector<hipEvent_t> ev_pool;
     orpcd::KernelStats stats;

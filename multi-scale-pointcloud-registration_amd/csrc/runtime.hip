@@ -34,6 +34,14 @@ using namespace orpcd;
         }                             \
     } while (0)
 
+#define CTX_REQUIRE_DEV(ctx, cond, msg) \
+    do {                                \
+        if (!(cond)) {                  \
+            (ctx)->err = (msg);         \
+            return ORPCD_EDEVICE;       \
+        }                               \
+    } while (0)
+
 namespace {
 
 bool finite_cloud(const double* xyz, int64_t n) {
@@ -396,6 +404,14 @@ int batch_setup(orpcd_ctx* c, const double* R0, const double* t0, int B, const o
     if (c->two_phase_ok) CTX_CHECK(c, c->items.ensure(worst_items));
     CTX_CHECK(c, c->item_counts.ensure((size_t)2 * B * ((N + 127) / 128) + 2));
     c->sched_live = sched_wanted(c, persist, B);
+    c->fuse_live = c->opt.fuse_solve && !persist && c->opt.search_kernel == 0 &&
+                   (getenv("ORPCD_TRACE") != nullptr || !pipelined_ok(c));
+    if (c->fuse_live) {
+        CTX_CHECK(c, c->ready.ensure((size_t)B));
+        CTX_CHECK(c, c->fuse_err.ensure(1));
+        CTX_CHECK(c, hipMemsetAsync(c->ready.p, 0, (size_t)B * 4, c->stream));
+        CTX_CHECK(c, hipMemsetAsync(c->fuse_err.p, 0, 4, c->stream));
+    }
     if (c->sched_live) {
         const size_t NG = (size_t)(N + 127) / 128;
         c->sched_cap = sched_capacity(c, B);
@@ -982,9 +998,12 @@ int run_passes(orpcd_ctx* c, int B, const orpcd_gicp_params* p, double* T_out, d
         const bool sync = (pass % every) == every - 1 || pass == p->max_iteration;
         if (!sync) continue;
         CTX_CHECK(c, hipMemcpyAsync(hDone, c->done.p, (size_t)B * 4, hipMemcpyDeviceToHost, s));
+        unsigned ferr = 0;
+        if (c->fuse_live) CTX_CHECK(c, hipMemcpyAsync(&ferr, c->fuse_err.p, 4, hipMemcpyDeviceToHost, s));
         unsigned long long tiles_now[2] = {0, 0};
         if (trace) CTX_CHECK(c, read_counters(c, tiles_now[0], tiles_now[1], true));
         CTX_CHECK(c, hipStreamSynchronize(s));
+        CTX_REQUIRE_DEV(c, ferr == 0, "gicp: a query transform block timed out waiting for its start's solve");
         if (timed) {
             for (int q = 0; q < pending; ++q) {
                 float ms = 0.f, ms2 = 0.f;
@@ -1493,6 +1512,7 @@ int orpcd_set_option(orpcd_ctx* c, const char* key, double value) {
     else if (k == "sched" && (v == 0 || v == 1)) c->opt.sched = v;
     else if (k == "sched_items" && v >= 64 && v <= (1 << 22)) c->opt.sched_items = v;
     else if (k == "sched_min_starts" && v >= 1) c->opt.sched_min_starts = v;
+    else if (k == "fuse_solve" && (v == 0 || v == 1)) c->opt.fuse_solve = v;
     else {
         c->err = "set_option: unknown key or bad value: " + k;
         return ORPCD_EINVAL;
