@@ -339,7 +339,8 @@ struct orpcd_ctx {
         int sched_items = 10240;  // ordered dispatch: split a group until its waves cost <= pass total / this
                                   // (C2 sweep 5120 / 10240 / 20480: 15.4 / 15.0 / 16.6 ms at 30 starts)
         int sched_min_starts = 16;  // ordered dispatch only for batches of at least this many starts
-        int fuse_solve = 1;       // 1: the 6x6 solve runs inside the next pass's query transform launch
+        int fuse_solve = 0;       // 1: the 6x6 solve runs inside the next pass's query transform launch
+                                  // (bit-identical; measured slower at C2: 30 starts 15.05 -> 15.45 ms)
     } opt;
     std::vector<hipEvent_t> ev_pool;
     orpcd::KernelStats stats;
