@@ -247,6 +247,15 @@ int orpcd_set_option(orpcd_ctx* ctx, const char* key, double value);
  * update (16).  The two must agree bit for bit.                            */
 int orpcd_test_solve6(orpcd_ctx* ctx, const double* sums27, int32_t n, double* out_serial, double* out_wave);
 
+/* Test entry: the correspondences of the last pass of each start of the last
+ * single-target batch (orpcd_gicp_batch / orpcd_icp_p2p_batch):
+ * idx_out[b * N + i] = input index of the nearest target of source point i
+ * (input order) in start b's final pass, -1 when none lay inside the search
+ * radius (before the strict fp64 d^2 < r^2 test of the accumulation).  With
+ * option "exact_nn" these are the oracle's KD-tree answers
+ * (oracle/orpcd_oracle.cpp KDTree::nn1: lexicographic (d^2, index) minimum). */
+int orpcd_gicp_correspondences(orpcd_ctx* ctx, int32_t B, int32_t* idx_out);
+
 /* --------------------------------------------------------- host RNG replay
  * n consecutive Aligner.initialize_rotation() draws (Aligner.py:129-131,160)
  * from numpy's legacy MT19937 RandomState, bit for bit: per attempt three

@@ -128,6 +128,64 @@ __device__ __forceinline__ double ldg_f64(const double* p) {
     return *(const __attribute__((address_space(1))) double*)p;
 }
 
+// ---------------------------------------------------------------------------
+// Exact nearest neighbour (opt.exact_nn).  The fp32 search orders candidates
+// by d32, which differs from the oracle's fp64 distance d64 (KD-tree, the
+// lexicographic (d64^2, input index) minimum) by at most
+//     |d32 - d64| <= delta = u (2A + 3.5 d) (1 + 3u),  u = 2^-24,
+// A = |q32| (the query in the target's fp32 frame): the fp32 roundings of the
+// query and target coordinates (u |q32| + u |t32|, |t32| <= A + d), the
+// subtraction (u d) and the three roundings of the squared sum (1.5 u d).
+// If the exact winner t* differs from the fp32 winner j, then d32(t*) <=
+// d64(t*) + delta <= d64(j) + delta <= d32(j) + 2 delta: its key is at most
+// band_hi(key(j)).  The search therefore finds every query's runner-up key
+// (in-scan, and across the splits of a query group: the loser of every
+// atomicMin merge); a query whose runner-up lies within the band of its
+// winner is filed for an fp64 re-search (nn_exact_kernel), every other
+// query's fp32 winner is provably the fp64 one.  band_hi adds 1% on delta,
+// the key truncation (2^-17 relative on the winner's d^2) and 2^-19 for its
+// own fp32 rounding.
+// ---------------------------------------------------------------------------
+constexpr float kU = 5.9604645e-08f;  // 2^-24
+__device__ __forceinline__ float exact_band_hi(float x, float A) {
+#pragma clang fp contract(off)  // identical rounding in the query transform and the search
+    const float d = __builtin_sqrtf(x * 1.0000080f);  // x (1 + 2^-17 + margin): the masked key's upper end
+    const float dl = kU * (4.04f * A + 7.07f * d);      // 2 delta (+1%)
+    const float r = d + dl;
+    return r * r * 1.0000020f;  // (1 + 2^-19): this function's own fp32 rounding
+}
+__device__ __forceinline__ float qnorm(float x, float y, float z) {
+#pragma clang fp contract(off)
+    return __builtin_sqrtf(x * x + y * y + z * z) * 1.0000005f;
+}
+// sentinel bound of a query in exact mode: strictly above band_hi of every
+// key below the plain bound, so a runner-up can never be the sentinel
+__device__ __forceinline__ float exact_sentinel(float bound, float A) {
+#pragma clang fp contract(off)
+    return exact_band_hi(bound, A) * 1.00003f + 1e-30f;  // > 2^-17: survives the key mask
+}
+// per-wave culling slack cw >= band_hi(x) - x for every x <= W (the wave's
+// largest sentinel) and query norm <= Amax; band_hi(x) - x is increasing in x
+__device__ __forceinline__ float exact_cull_slack(float W, float Amax) {
+#pragma clang fp contract(off)
+    return (exact_band_hi(W, Amax) - W) * 1.0001f + W * 1e-6f + 1e-30f;
+}
+template <bool kExact>
+__device__ __forceinline__ float plus_cw(float v, float cw) {
+    if constexpr (kExact) return v + cw;
+    else return v;
+}
+__device__ __forceinline__ unsigned umed3(unsigned a, unsigned b, unsigned c) {
+    return max(min(a, b), min(max(a, b), c));  // v_med3_u32
+}
+struct ExactArgs {
+    unsigned* sec;                // B x N: runner-up key near the winner (0xFFFFFFFF: none; reset by the transform)
+    unsigned long long* list;     // queries with a near runner-up: slot << 40 | target << 32 | query
+    unsigned* cnt;                // entries of this pass's list (by pass parity)
+    unsigned* cnt_next;           // the next pass's (zeroed by nn_exact_kernel)
+    unsigned long long* total;    // queries re-searched (statistics)
+};
+
 // --------------------------------------------------------------------------
 // Culled exact nearest search for the 2 queries of every lane of one wave,
 // restricted to tiles t with t % S == s.  s0lo/s0hi: super-tile `lane`'s box
@@ -135,7 +193,12 @@ __device__ __forceinline__ double ldg_f64(const double* p) {
 // bound on d^2 (<= 0: invalid query).  Returns quarters scanned; bj[] = Morton
 // index of the chosen target or -1, bd[] its fp32 d^2 (key-truncated).
 // --------------------------------------------------------------------------
-template <bool kGBox>
+// kExact: the bound is the exact-mode sentinel, candidates are culled against
+// key + cw (see exact_band_hi), the in-scan minimum runs over the query's
+// whole search (tie order among equal masked keys is then immaterial: such
+// keys are within the band and re-searched in fp64), and sk[] returns the
+// second-smallest key scanned (0xFFFFFFFF: none).
+template <bool kGBox, bool kExact = false>
 __device__ __forceinline__ int culled_search(float4* stage, const float4* __restrict__ p4,
                                              const float4* __restrict__ tlo, const float4* __restrict__ thi,
                                              const float4* __restrict__ qbox, int ntiles, const float4* __restrict__ slo,
@@ -143,12 +206,14 @@ __device__ __forceinline__ int culled_search(float4* stage, const float4* __rest
                                              const float qx[2], const float qy[2],
                                              const float qz[2], const float bound[2], float bd[2], int bj[2],
                                              float4 s0lo, float4 s0hi, const float4* gbox = nullptr,
-                                             unsigned long long* phase_cull_out = nullptr) {
+                                             unsigned long long* phase_cull_out = nullptr,
+                                             unsigned* sk = nullptr) {
     const int lane = threadIdx.x & 63;
     const bool v0 = bound[0] > 0.0f, v1 = bound[1] > 0.0f;
     unsigned k0 = v0 ? __float_as_uint(bound[0]) : 0u;  // best key (0: never improves)
     unsigned k1 = v1 ? __float_as_uint(bound[1]) : 0u;
     int t0 = -1, t1 = -1;                               // tile of the best key
+    unsigned s0 = 0xFFFFFFFFu, s1 = 0xFFFFFFFFu;        // exact: second-smallest key
     bj[0] = bj[1] = -1;
     bd[0] = bd[1] = 0.0f;
     const float inf = 3.0e38f;
@@ -156,11 +221,19 @@ __device__ __forceinline__ int culled_search(float4* stage, const float4* __rest
     // (gbox: lo.xyz | max bound bits, hi.xyz), else reduced here
     unsigned Wk;
     float lox, loy, loz, hix, hiy, hiz;
+    float cw = 0.0f;  // exact: culling slack of this wave (scalar)
     if constexpr (kGBox) {
         const float4 g0 = gbox[0], g1 = gbox[1];
         Wk = __float_as_uint(g0.w) & kKeyMask;
         lox = g0.x, loy = g0.y, loz = g0.z, hix = g1.x, hiy = g1.y, hiz = g1.z;
+        if constexpr (kExact) {
+            const float ax = fmaxf(fabsf(lox), fabsf(hix)), ay = fmaxf(fabsf(loy), fabsf(hiy)),
+                        az = fmaxf(fabsf(loz), fabsf(hiz));
+            cw = exact_cull_slack(__uint_as_float(__float_as_uint(g0.w)), qnorm(ax, ay, az));
+            cw = __uint_as_float(__builtin_amdgcn_readfirstlane(__float_as_uint(cw)));
+        }
     } else {
+        static_assert(kGBox || !kExact, "exact mode needs the transform's wave boxes");
         Wk = wave_umax((k0 > k1 ? k0 : k1) & kKeyMask);
         lox = wave_fmin(fminf(v0 ? qx[0] : inf, v1 ? qx[1] : inf));
         loy = wave_fmin(fminf(v0 ? qy[0] : inf, v1 ? qy[1] : inf));
@@ -170,7 +243,7 @@ __device__ __forceinline__ int culled_search(float4* stage, const float4* __rest
         hiz = wave_fmax(fmaxf(v0 ? qz[0] : -inf, v1 ? qz[1] : -inf));
     }
     if (Wk == 0u) return 0;  // no query of this wave can take anything
-    float W = __uint_as_float(Wk);
+    float W = plus_cw<kExact>(__uint_as_float(Wk), cw);
     int visited = 0;
 
     // candidate cursor: rounds of 64 tiles, one tile per lane; wave-box test by
@@ -285,8 +358,8 @@ __device__ __forceinline__ int culled_search(float4* stage, const float4* __rest
             const float hy = __uint_as_float(__builtin_amdgcn_readlane(__float_as_uint(b.y), k));
             const float hz = __uint_as_float(__builtin_amdgcn_readlane(__float_as_uint(b.z), k));
             const f2 bd2 = box_d2_2q(f2{qx[0], qx[1]}, f2{qy[0], qy[1]}, f2{qz[0], qz[1]}, lx, ly, lz, hx, hy, hz);
-            const bool need0 = bd2.x < __uint_as_float(k0 & kKeyMask);
-            const bool need1 = bd2.y < __uint_as_float(k1 & kKeyMask);
+            const bool need0 = bd2.x < plus_cw<kExact>(__uint_as_float(k0 & kKeyMask), cw);
+            const bool need1 = bd2.y < plus_cw<kExact>(__uint_as_float(k1 & kKeyMask), cw);
 #ifdef ORPCD_PHASES
             {
                 const unsigned long long b0 = __ballot(need0), b1 = __ballot(need1);
@@ -337,7 +410,8 @@ __device__ __forceinline__ int culled_search(float4* stage, const float4* __rest
             pre = p4[nxt * kTile + lane];
             if (lane < 8) preq = qbox[nxt * 8 + lane];
         }
-        unsigned m0 = 0xFFFFFFFFu, m1 = 0xFFFFFFFFu;
+        // exact: the running minimum of the whole search (from k0), else of this tile
+        unsigned m0 = kExact ? k0 : 0xFFFFFFFFu, m1 = kExact ? k1 : 0xFFFFFFFFu;
         const f2 qx0 = {qx[0], qx[0]}, qy0 = {qy[0], qy[0]}, qz0 = {qz[0], qz[0]};
         const f2 qx1 = {qx[1], qx[1]}, qy1 = {qy[1], qy[1]}, qz1 = {qz[1], qz[1]};
         const float4* qb = reinterpret_cast<const float4*>(sx + 192);
@@ -348,8 +422,8 @@ __device__ __forceinline__ int culled_search(float4* stage, const float4* __rest
             // quarters); the 2^-20 slack keeps the test conservative against
             // the scan's own fp32 rounding
             const float4 lo = qb[qd], hi = qb[4 + qd];
-            const float b0 = __uint_as_float((k0 < m0 ? k0 : m0) & kKeyMask);
-            const float b1 = __uint_as_float((k1 < m1 ? k1 : m1) & kKeyMask);
+            const float b0 = plus_cw<kExact>(__uint_as_float((k0 < m0 ? k0 : m0) & kKeyMask), cw);
+            const float b1 = plus_cw<kExact>(__uint_as_float((k1 < m1 ? k1 : m1) & kKeyMask), cw);
             const f2 qd2 = box_d2_2q(f2{qx[0], qx[1]}, f2{qy[0], qy[1]}, f2{qz[0], qz[1]}, lo.x, lo.y, lo.z, hi.x,
                                      hi.y, hi.z);
             const bool need = qd2.x * kQuarterSlack < b0 || qd2.y * kQuarterSlack < b1;
@@ -374,8 +448,19 @@ __device__ __forceinline__ int culled_search(float4* stage, const float4* __rest
                 const unsigned c0 = (__float_as_uint(d0.y) & kKeyMask) | (unsigned)(kk + 1);
                 const unsigned a1 = (__float_as_uint(d1.x) & kKeyMask) | (unsigned)kk;
                 const unsigned c1 = (__float_as_uint(d1.y) & kKeyMask) | (unsigned)(kk + 1);
-                m0 = min(m0, min(a0, c0));
-                m1 = min(m1, min(a1, c1));
+                if constexpr (kExact) {  // (minimum, runner-up) of every key scanned
+                    s0 = umed3(m0, s0, a0);
+                    m0 = min(m0, a0);
+                    s0 = umed3(m0, s0, c0);
+                    m0 = min(m0, c0);
+                    s1 = umed3(m1, s1, a1);
+                    m1 = min(m1, a1);
+                    s1 = umed3(m1, s1, c1);
+                    m1 = min(m1, c1);
+                } else {
+                    m0 = min(m0, min(a0, c0));
+                    m1 = min(m1, min(a1, c1));
+                }
             }
         }
         asm volatile("" ::: "memory");  // all reads of this tile precede the next stage write
@@ -383,16 +468,27 @@ __device__ __forceinline__ int culled_search(float4* stage, const float4* __rest
 #ifdef ORPCD_PHASES
         ph_impr += __any((m0 & kKeyMask) < (k0 & kKeyMask) || (m1 & kKeyMask) < (k1 & kKeyMask)) ? 1 : 0;
 #endif
-        if ((m0 & kKeyMask) < (k0 & kKeyMask)) {
-            k0 = m0;
-            t0 = tile;
-        }
-        if ((m1 & kKeyMask) < (k1 & kKeyMask)) {
-            k1 = m1;
-            t1 = tile;
+        if constexpr (kExact) {  // the minimum moved into this tile
+            if (m0 != k0) {
+                k0 = m0;
+                t0 = tile;
+            }
+            if (m1 != k1) {
+                k1 = m1;
+                t1 = tile;
+            }
+        } else {
+            if ((m0 & kKeyMask) < (k0 & kKeyMask)) {
+                k0 = m0;
+                t0 = tile;
+            }
+            if ((m1 & kKeyMask) < (k1 & kKeyMask)) {
+                k1 = m1;
+                t1 = tile;
+            }
         }
         Wk = wave_umax((k0 > k1 ? k0 : k1) & kKeyMask);
-        W = __uint_as_float(Wk);
+        W = plus_cw<kExact>(__uint_as_float(Wk), cw);
         // the prefetched candidate was chosen under the previous bound: re-test
         while (nxt >= 0 && !(lbn < W)) {
             nxt = next_candidate(lbn);
@@ -409,6 +505,10 @@ __device__ __forceinline__ int culled_search(float4* stage, const float4* __rest
     if (t1 >= 0) {
         bj[1] = t1 * kTile + (int)(k1 & 63u);
         bd[1] = __uint_as_float(k1 & kKeyMask);
+    }
+    if constexpr (kExact) {
+        sk[0] = s0;
+        sk[1] = s1;
     }
 #ifdef ORPCD_PHASES
     if (phase_cull_out) {
@@ -450,6 +550,7 @@ __device__ __forceinline__ float seed_bound(float d2) {
 #pragma clang fp contract(off)  // the same rounding in every transform kernel (a bound: answers never depend on it)
     return d2 * kSeedSlack + 1e-30f;
 }
+
 
 // ---------------------------------------------------------------------------
 // Cost-ordered search dispatch (opt.sched).  The search of pass p measures
@@ -587,7 +688,7 @@ __global__ __launch_bounds__(256) void xform_queries_kernel(const double* __rest
                                                             float r2s, int reseed, float4* __restrict__ q32,
                                                             unsigned long long* __restrict__ best,
                                                             const int32_t* __restrict__ nact_dev,
-                                                            float4* __restrict__ gbox, SchedX sx) {
+                                                            float4* __restrict__ gbox, SchedX sx, ExactArgs ex) {
     if (nact_dev && (int)blockIdx.y >= *nact_dev) return;  // pipelined: grid sized for an upper bound
     const int slot = active[blockIdx.y];
     if (done[slot]) return;
@@ -619,6 +720,10 @@ __global__ __launch_bounds__(256) void xform_queries_kernel(const double* __rest
         } else if (jp == kNoSeed || reseed) {
             for (int t = 0; t < tg.ntiles; t += tg.seed_stride)
                 bound = fminf(bound, seed_bound(d2f(x, y, z, p4[t * kTile])));
+        }
+        if (ex.sec) {  // exact mode: the sentinel bound; the split merge state of the pass
+            bound = exact_sentinel(bound, qnorm(x, y, z));
+            ex.sec[(size_t)slot * N + i] = 0xFFFFFFFFu;
         }
         q32[(size_t)slot * N + i] = make_float4(x, y, z, bound);
     }
@@ -664,12 +769,13 @@ __device__ __forceinline__ void load_super0(const SearchTgt& tg, float4& s0lo, f
 
 // One wave's search: split `split` of S of the 128-query group wg of start
 // `slot` (queries wg * 128 + lane + 64 k).  Returns quarters scanned.
+template <bool kExact = false>
 __device__ __forceinline__ int search_group(const float4* __restrict__ q32, int N, const SearchTgt tg,
                                             int super_cull, int S, int split, int slot, int wg,
                                             unsigned long long* __restrict__ best,
                                             unsigned long long* __restrict__ counters, unsigned cslot,
                                             float4* stage_w, const float4* __restrict__ gbox, float4 s0lo,
-                                            float4 s0hi) {
+                                            float4 s0hi, ExactArgs ex = ExactArgs{}, int tk = 0) {
     const int lane = threadIdx.x & 63;
 #ifdef ORPCD_PHASES
     const unsigned long long ph_t0 = __builtin_readcyclecounter();
@@ -683,6 +789,7 @@ __device__ __forceinline__ int search_group(const float4* __restrict__ q32, int 
     const int i0 = wg * (64 * kCQPT) + lane;
     float qx[kCQPT], qy[kCQPT], qz[kCQPT], bound[kCQPT], bd[kCQPT];
     int bj[kCQPT];
+    unsigned sk[kCQPT];
     const float4* qs = q32 + (size_t)slot * N;
     const float4* gb = gbox + ((size_t)slot * ((N + 127) / 128) + wg) * 2;
     // the queries by raw buffer loads: a lane past N reads zeros (bound 0: never
@@ -707,9 +814,9 @@ __device__ __forceinline__ int search_group(const float4* __restrict__ q32, int 
                                             tg.nsuper, super_cull, S, split, qx, qy, qz, bound, bd, bj, s0lo, s0hi,
                                             gb, ph_cull);
 #else
-    const int visited = culled_search<true>(stage_w, tg.p4, tg.tlo, tg.thi, tg.qbox, tg.ntiles, tg.slo, tg.shi,
-                                            tg.nsuper, super_cull, S, split, qx, qy, qz, bound, bd, bj, s0lo, s0hi,
-                                            gb);
+    const int visited = culled_search<true, kExact>(stage_w, tg.p4, tg.tlo, tg.thi, tg.qbox, tg.ntiles, tg.slo,
+                                                    tg.shi, tg.nsuper, super_cull, S, split, qx, qy, qz, bound, bd,
+                                                    bj, s0lo, s0hi, gb, nullptr, sk);
 #endif
     if (lane == 0 && counters) {  // spread over kCounterSlots cache lines (one address serialises)
         unsigned long long* cs = counters + kCounterStride * (cslot % kCounterSlots);
@@ -728,26 +835,68 @@ __device__ __forceinline__ int search_group(const float4* __restrict__ q32, int 
 #endif
     }
     unsigned long long* out = best + (size_t)slot * N;
+    if constexpr (kExact) {
+        // the query's runner-up over all splits is the minimum of every
+        // split's runner-up and of every merge's loser; only keys within the
+        // band of the key they lost to can matter (sec[], reset by the query
+        // transform), so only those are published -- rarely.  The band test
+        // against the final winner is nn_exact_kernel's.  Both merges are
+        // issued before either result is used (one round trip per wave).
+        unsigned long long v[kCQPT], old[kCQPT];
 #pragma unroll
-    for (int k = 0; k < kCQPT; ++k) {
-        const int i = i0 + 64 * k;
-        if (i >= N) continue;
-        const unsigned long long v =
-            bj[k] < 0 ? kNone : ((unsigned long long)__float_as_uint(bd[k]) << 32) | (unsigned)bj[k];
-        if (S == 1)
-            out[i] = v;
-        else if (v != kNone)
-            atomicMin(out + i, v);
+        for (int k = 0; k < kCQPT; ++k) {
+            const int i = i0 + 64 * k;
+            v[k] = bj[k] < 0 || i >= N ? kNone : ((unsigned long long)__float_as_uint(bd[k]) << 32) | (unsigned)bj[k];
+            old[k] = kNone;
+            if (v[k] == kNone) continue;
+            if (S == 1)
+                out[i] = v[k];
+            else
+                old[k] = atomicMin(out + i, v[k]);
+        }
+#pragma unroll
+        for (int k = 0; k < kCQPT; ++k) {
+            if (v[k] == kNone) continue;
+            const int i = i0 + 64 * k;
+            const float A = qnorm(qx[k], qy[k], qz[k]);
+            unsigned s2 = __uint_as_float(sk[k] & kKeyMask) <= exact_band_hi(bd[k], A) ? sk[k] : 0xFFFFFFFFu;
+            if (old[k] != kNone) {
+                const unsigned long long lose = old[k] < v[k] ? v[k] : old[k], win = old[k] < v[k] ? old[k] : v[k];
+                const unsigned lk = (unsigned)(lose >> 32);
+                if (__uint_as_float(lk) <= exact_band_hi(__uint_as_float((unsigned)(win >> 32)), A)) s2 = min(s2, lk);
+            }
+            if (s2 == 0xFFFFFFFFu) continue;
+            // the query's first publisher lists it for nn_exact_kernel
+            const bool first = S == 1 || atomicMin(ex.sec + (size_t)slot * N + i, s2) == 0xFFFFFFFFu;
+            if (S == 1) ex.sec[(size_t)slot * N + i] = s2;
+            if (first) {
+                const unsigned at = atomicAdd(ex.cnt, 1u);
+                ex.list[at] = ((unsigned long long)slot << 40) | ((unsigned long long)tk << 32) | (unsigned)i;
+            }
+        }
+    } else {
+#pragma unroll
+        for (int k = 0; k < kCQPT; ++k) {
+            const int i = i0 + 64 * k;
+            if (i >= N) continue;
+            const unsigned long long v =
+                bj[k] < 0 ? kNone : ((unsigned long long)__float_as_uint(bd[k]) << 32) | (unsigned)bj[k];
+            if (S == 1)
+                out[i] = v;
+            else if (v != kNone)
+                atomicMin(out + i, v);
+        }
     }
     return visited;
 }
 
 // Uniform-split dispatch: grid = (blocks per start * S, running starts), 4 waves/block.
+template <bool kExact = false>
 __device__ __forceinline__ void nn_search_body(
     const float4* __restrict__ q32, int N, const TargetDesc& tg, int super_cull, const int32_t* __restrict__ active,
     const int32_t* __restrict__ done, int S, unsigned long long* __restrict__ best,
     unsigned long long* __restrict__ counters, int by, int bx, int wid, float4* stage_w,
-    const float4* __restrict__ gbox) {
+    const float4* __restrict__ gbox, ExactArgs ex = ExactArgs{}, int tk = 0) {
 #ifdef ORPCD_WAVETIME
     const unsigned long long wt0 = __builtin_amdgcn_s_memrealtime();
 #endif
@@ -759,8 +908,8 @@ __device__ __forceinline__ void nn_search_body(
     const int grp = bx / S, split = bx - grp * S;
     const int wg = grp * kCWaves + wid;
     if (wg * (64 * kCQPT) >= N) return;  // a wave past the last query group (no gbox entry)
-    const int visited = search_group(q32, N, st, super_cull, S, split, slot, wg, best, counters,
-                                     (unsigned)(bx * kCWaves + wid + by), stage_w, gbox, s0lo, s0hi);
+    const int visited = search_group<kExact>(q32, N, st, super_cull, S, split, slot, wg, best, counters,
+                                             (unsigned)(bx * kCWaves + wid + by), stage_w, gbox, s0lo, s0hi, ex, tk);
     (void)visited;
 #ifdef ORPCD_WAVETIME
     if ((threadIdx.x & 63) == 0) {  // a fixed slot per wave: no shared counter to serialise on
@@ -778,10 +927,11 @@ __device__ __forceinline__ void nn_search_body(
 // Ordered dispatch (SchedS): wave k of the launch takes item k of the
 // class-major list, heaviest class first; the wave's duration is added to its
 // group's cost and to the pass total for the next pass's schedule.
-__global__ __launch_bounds__(kCBlock) __attribute__((amdgpu_waves_per_eu(5, 8))) void nn_search_sched_kernel(
+template <bool kExact>  // exact: 4 waves/SIMD (at 5 the runner-up registers spill)
+__global__ __launch_bounds__(kCBlock) __attribute__((amdgpu_waves_per_eu(kExact ? 4 : 5, 8))) void nn_search_sched_kernel(
     const float4* __restrict__ q32, int N, const TargetDesc* __restrict__ tdesc, int super_cull,
     unsigned long long* __restrict__ best, unsigned long long* __restrict__ counters,
-    const float4* __restrict__ gbox, SchedS sa) {
+    const float4* __restrict__ gbox, SchedS sa, ExactArgs ex) {
     __shared__ float4 stage[kCWaves][kTile];
     const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
     const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -825,8 +975,8 @@ __global__ __launch_bounds__(kCBlock) __attribute__((amdgpu_waves_per_eu(5, 8)))
     const SearchTgt st = search_tgt(tdesc[tk]);
     float4 s0lo, s0hi;
     load_super0(st, s0lo, s0hi);
-    const int visited = search_group(q32, N, st, super_cull, S, split, slot, wg, best, counters, w, stage[wid], gbox,
-                                     s0lo, s0hi);
+    const int visited = search_group<kExact>(q32, N, st, super_cull, S, split, slot, wg, best, counters, w,
+                                             stage[wid], gbox, s0lo, s0hi, ex, tk);
     (void)visited;
     if (lane == 0) {
         const unsigned long long t1 = __builtin_amdgcn_s_memrealtime();
@@ -848,7 +998,7 @@ __global__ __launch_bounds__(kCBlock) __attribute__((amdgpu_waves_per_eu(5, 8)))
     const float4 *__restrict__ q32, int N, const TargetDesc *__restrict__ tdesc, TgtBounds tb, int super_cull,  \
         const int32_t *__restrict__ active, const int32_t *__restrict__ done, int S,                          \
         unsigned long long *__restrict__ best, unsigned long long *__restrict__ counters,                       \
-        const int32_t *__restrict__ nact_dev, int sblk, int want, const float4 *__restrict__ gbox
+        const int32_t *__restrict__ nact_dev, int sblk, int want, const float4 *__restrict__ gbox, ExactArgs ex
 
 // Block -> (start, query group x split).  Unpipelined: the grid is
 // (sblk * S, running starts) as the host counted them.  Pipelined (nact_dev):
@@ -876,14 +1026,16 @@ __device__ __forceinline__ bool map_search_block(const int32_t* __restrict__ nac
 
 // Two register budgets of the same search (orpcd_set_option "search_occupancy"):
 // the compiler's choice (5 waves/SIMD) and a cap at 6 waves/SIMD.
-__global__ __launch_bounds__(kCBlock) __attribute__((amdgpu_waves_per_eu(5, 8))) void nn_search_kernel(
+template <bool kExact>  // exact: 4 waves/SIMD (at 5 the runner-up registers spill)
+__global__ __launch_bounds__(kCBlock) __attribute__((amdgpu_waves_per_eu(kExact ? 4 : 5, 8))) void nn_search_kernel(
     ORPCD_NN_SEARCH_ARGS) {
     __shared__ float4 stage[kCWaves][kTile];
     const int wid = threadIdx.x >> 6;
     int by, bx;
     if (!map_search_block(nact_dev, sblk, want, by, bx, S)) return;
-    nn_search_body(q32, N, tdesc[target_of_row(tb, by)], super_cull, active, done, S, best, counters, by, bx, wid,
-                   stage[wid], gbox);
+    const int tk = target_of_row(tb, by);
+    nn_search_body<kExact>(q32, N, tdesc[tk], super_cull, active, done, S, best, counters, by, bx, wid, stage[wid],
+                           gbox, ex, tk);
 }
 __global__ __launch_bounds__(kCBlock) __attribute__((amdgpu_waves_per_eu(6, 8))) void nn_search_kernel_o6(
     ORPCD_NN_SEARCH_ARGS) {
@@ -895,6 +1047,119 @@ __global__ __launch_bounds__(kCBlock) __attribute__((amdgpu_waves_per_eu(6, 8)))
                    stage[wid], gbox);
 }
 #undef ORPCD_NN_SEARCH_ARGS
+
+// --------------------------------------------------------------------------
+// Exact mode, second stage (one wave per 64 queries of a running start, after
+// the search): a query whose published runner-up lies within the fp32 error
+// band of its winner (exact_band_hi) is re-searched in fp64 by the whole wave.
+// Every target whose fp64 distance is at most the fp32 winner's passes the
+// box tests (its fp32 distance is within delta above; a box d^2 never exceeds
+// a member point's); the surviving tiles are scanned in fp64 in the oracle's
+// operation order ((dx^2 + dy^2) + dz^2, no contraction) and the
+// lexicographic (d^2, input index) minimum replaces the winner in best[] --
+// KDTree::nn1 of oracle/orpcd_oracle.cpp:192-217.
+// --------------------------------------------------------------------------
+__device__ __forceinline__ double d2_oracle(const double q[3], const double* __restrict__ t) {
+#pragma clang fp contract(off)
+    const double dx = q[0] - t[0], dy = q[1] - t[1], dz = q[2] - t[2];
+    return dx * dx + dy * dy + dz * dz;
+}
+__device__ __forceinline__ float box_d2_plain(float x, float y, float z, float4 lo, float4 hi) {
+#pragma clang fp contract(off)
+    return box_d2(x, y, z, lo.x, lo.y, lo.z, hi.x, hi.y, hi.z);
+}
+
+__global__ __launch_bounds__(256) void nn_exact_kernel(const double* __restrict__ src, int N,
+                                                       const double* __restrict__ Qm,
+                                                       const TargetDesc* __restrict__ tdesc,
+                                                       const float4* __restrict__ q32, ExactArgs ex,
+                                                       unsigned long long* __restrict__ best) {
+#pragma clang fp contract(off)
+    const int lane = threadIdx.x & 63;
+    const unsigned gw = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6), nw = gridDim.x * (blockDim.x >> 6);
+    const unsigned n = __builtin_amdgcn_readfirstlane(*ex.cnt);
+    if (gw == 0 && lane == 0) *ex.cnt_next = 0u;
+    // listed queries: the band test against the final winner, one per lane;
+    // entries are dealt round-robin over the waves (a search wave lists its
+    // near-ties consecutively, and they cluster in space)
+    for (unsigned r = 0; (size_t)r * 64 * nw < n; ++r) {
+        const unsigned e = (r * 64 + lane) * nw + gw;
+        unsigned long long ent = 0;
+        bool file = false;
+        if (e < n) {
+            ent = ex.list[e];
+            const size_t qi = (size_t)(ent >> 40) * N + (unsigned)ent;
+            const unsigned long long m = best[qi];
+            const float4 qq = q32[qi];
+            file = m != kNone && __uint_as_float(ex.sec[qi] & kKeyMask) <=
+                                     exact_band_hi(__uint_as_float((unsigned)(m >> 32)), qnorm(qq.x, qq.y, qq.z));
+        }
+        unsigned long long fm = __ballot(file);
+        if (lane == 0 && fm) atomicAdd(ex.total, (unsigned long long)__builtin_popcountll(fm));
+        while (fm) {  // the wave re-searches each filed query of its 64 entries
+            const int l = __builtin_ctzll(fm);
+            fm &= fm - 1;
+            const unsigned long long en = ((unsigned long long)__builtin_amdgcn_readlane((unsigned)(ent >> 32), l) << 32) |
+                                          (unsigned)__builtin_amdgcn_readlane((unsigned)ent, l);
+            const int slot = (int)(en >> 40), tk = (int)((en >> 32) & 0xFFu), i = (int)(unsigned)en;
+            const TargetDesc& tg = tdesc[tk];
+            double Q[12];
+#pragma unroll
+            for (int t = 0; t < 12; ++t) Q[t] = Qm[12 * slot + t];
+            const double* __restrict__ t64 = tg.xyz64;
+            const double p[3] = {src[3 * i], src[3 * i + 1], src[3 * i + 2]};
+            double q[3];
+            xform(Q, p, q);
+            const float x = (float)(q[0] - tg.ox), y = (float)(q[1] - tg.oy), z = (float)(q[2] - tg.oz);
+            unsigned long long* bp = best + (size_t)slot * N + i;
+            const unsigned long long bv = *bp;
+            const int j = (int)(unsigned)bv;
+            double bD = d2_oracle(q, t64 + 3 * (size_t)j);
+            int bI = __float_as_int(tg.p4[j].w), bM = j;
+            // box bound: d32 <= d64 + u (2A + 3.5 d) for every target with d64 <= d64(j); x2
+            const double dj = sqrt(bD);
+            const double rb = dj + 5.9604644775390625e-08 * (4.0 * (double)qnorm(x, y, z) + 7.0 * dj);
+            const float Tb = (float)(rb * rb * (1.0 + 1.0 / 65536.0)) * 1.0001f;
+            for (int sb = 0; sb < tg.nsuper; sb += 64) {
+                const int u = sb + lane;
+                const bool su_ok = u < tg.nsuper && box_d2_plain(x, y, z, tg.slo[u], tg.shi[u]) <= Tb;
+                unsigned long long sm = __ballot(su_ok);
+                while (sm) {
+                    const int su = sb + __builtin_ctzll(sm);
+                    sm &= sm - 1;
+                    const int t = su * kSuper + lane;
+                    const bool t_ok = t < tg.ntiles && box_d2_plain(x, y, z, tg.tlo[t], tg.thi[t]) <= Tb;
+                    unsigned long long tm = __ballot(t_ok);
+                    while (tm) {
+                        const int tt = su * kSuper + __builtin_ctzll(tm);
+                        tm &= tm - 1;
+                        const int k = tt * kTile + lane;  // Morton position (padding: input index -1)
+                        const int in = __float_as_int(tg.p4[k].w);
+                        if (in >= 0) {
+                            const double D = d2_oracle(q, t64 + 3 * (size_t)k);
+                            if (D < bD || (D == bD && in < bI)) {
+                                bD = D;
+                                bI = in;
+                                bM = k;
+                            }
+                        }
+                    }
+                }
+            }
+#pragma unroll
+            for (int o = 32; o >= 1; o >>= 1) {  // lexicographic (d^2, input index) over the wave
+                const double oD = __shfl_xor(bD, o);
+                const int oI = __shfl_xor(bI, o), oM = __shfl_xor(bM, o);
+                if (oD < bD || (oD == bD && oI < bI)) {
+                    bD = oD;
+                    bI = oI;
+                    bM = oM;
+                }
+            }
+            if (lane == 0) *bp = (bv & 0xFFFFFFFF00000000ull) | (unsigned)bM;
+        }
+    }
+}
 
 // --------------------------------------------------------------------------
 // Cooperative search (default): one workgroup of W waves per group of 128
@@ -2531,6 +2796,19 @@ static SchedX sched_x(const orpcd_ctx* c, int nact, int pass) {
     return sx;
 }
 
+// exact mode: the runner-up array and the statistics counter
+static ExactArgs exact_args(const orpcd_ctx* c, int pass) {
+    ExactArgs ex{};
+    if (!c->exact_live) return ex;
+    ex.sec = c->xsec.p;
+    ex.list = c->xlist.p;
+    ex.cnt = c->xcnt.p + (pass & 1);
+    ex.cnt_next = c->xcnt.p + ((pass + 1) & 1);
+    ex.total = c->xtotal.p;
+    return ex;
+}
+constexpr int kExactBlocks = 256;  // re-search grid: 1024 waves, 64 listed queries per wave and round
+
 hipError_t launch_xform(const orpcd_ctx* c, int nact, int pass, double r2, hipStream_t s, bool dev_nact,
                         const TgtBounds& tb) {
     if (use_coop(c) || use_two_phase(c)) return hipSuccess;  // these searches transform their own queries
@@ -2538,7 +2816,7 @@ hipError_t launch_xform(const orpcd_ctx* c, int nact, int pass, double r2, hipSt
     const SchedX sx = dev_nact ? SchedX{} : sched_x(c, nact, pass);
     xform_queries_kernel<<<dim3((unsigned)((N + 255) / 256) + (sx.list ? 1u : 0u), (unsigned)nact), 256, 0, s>>>(
         c->src.xyz64.p, N, c->active.p, c->Q.p, c->done.p, c->tdesc.p, tb, c->prevnn.p, search_r2(r2),
-        c->opt.reseed, c->q32.p, c->best.p, dev_nact ? c->ctl.p : nullptr, c->gbox.p, sx);
+        c->opt.reseed, c->q32.p, c->best.p, dev_nact ? c->ctl.p : nullptr, c->gbox.p, sx, exact_args(c, pass));
     return hipGetLastError();
 }
 
@@ -2583,7 +2861,7 @@ static SolveArgs solve_args(const orpcd_ctx* c) {
 }
 
 bool pipelined_ok(const orpcd_ctx* c) {
-    return !use_coop(c) && !use_two_phase(c) && c->opt.pipeline && c->batch_ntgt == 1;
+    return !use_coop(c) && !use_two_phase(c) && c->opt.pipeline && c->batch_ntgt == 1 && !c->opt.exact_nn;
 }
 
 // One pipelined pass (see PassCtl): search over the device's running starts,
@@ -2598,11 +2876,11 @@ hipError_t launch_gicp_pass_pipelined(const orpcd_ctx* c, int nact_host, int pas
     const int S = search_splits(nact_host, sblk, want);
     const int64_t grid = std::max<int64_t>((int64_t)nact_host * sblk * S, (want + kCWaves - 1) / kCWaves);
     hipError_t e;
-    auto kern = c->opt.search_occupancy == 6 ? nn_search_kernel_o6 : nn_search_kernel;
+    auto kern = c->opt.search_occupancy == 6 ? nn_search_kernel_o6 : nn_search_kernel<false>;
     const TgtBounds tb = one_target();  // pipelined passes: single-target batches only
     kern<<<dim3((unsigned)grid), kCBlock, 0, s>>>(c->q32.p, N, c->tdesc.p, tb, c->opt.super_cull, c->active.p,
                                                   c->done.p, 1, c->best.p, c->count_tiles ? c->counters.p : nullptr,
-                                                  c->ctl.p, sblk, want, c->gbox.p);
+                                                  c->ctl.p, sblk, want, c->gbox.p, ExactArgs{});
     if ((e = hipGetLastError()) != hipSuccess) return e;
     if (mid && (e = hipEventRecord(mid, s)) != hipSuccess) return e;
     const int ablk = accum_blocks(N);
@@ -2702,9 +2980,10 @@ hipError_t launch_gicp_pass(const orpcd_ctx* c, int nact, int pass, double r2, h
         sa.NG = (int)NG;
         sa.B = (int)B;
         const int64_t grid = (std::min<int64_t>(items, c->sched_cap) + kCWaves - 1) / kCWaves;
-        nn_search_sched_kernel<<<dim3((unsigned)grid), kCBlock, 0, s>>>(
-            c->q32.p, N, c->tdesc.p, c->opt.super_cull, c->best.p, c->count_tiles ? c->counters.p : nullptr,
-            c->gbox.p, sa);
+        auto kern = c->exact_live ? nn_search_sched_kernel<true> : nn_search_sched_kernel<false>;
+        kern<<<dim3((unsigned)grid), kCBlock, 0, s>>>(c->q32.p, N, c->tdesc.p, c->opt.super_cull, c->best.p,
+                                                      c->count_tiles ? c->counters.p : nullptr, c->gbox.p, sa,
+                                                      exact_args(c, pass));
 #ifdef ORPCD_WAVETIME
         if ((e = dump_wavetime(pass, nact, 0, (unsigned)(grid * kCWaves), s)) != hipSuccess) return e;
 #endif
@@ -2714,15 +2993,21 @@ hipError_t launch_gicp_pass(const orpcd_ctx* c, int nact, int pass, double r2, h
     const int S = uniform_splits(c, nact);
     const int want = nact <= c->opt.small_batch ? c->opt.search_waves / 2 : c->opt.search_waves;
     // best[] was reset to kNone by xform_queries_kernel
-    auto kern = c->opt.search_occupancy == 6 ? nn_search_kernel_o6 : nn_search_kernel;
+    auto kern = c->exact_live ? nn_search_kernel<true>
+                : c->opt.search_occupancy == 6 ? nn_search_kernel_o6 : nn_search_kernel<false>;
     kern<<<dim3((unsigned)(sblk * S), (unsigned)nact), kCBlock, 0, s>>>(
         c->q32.p, N, c->tdesc.p, tb, c->opt.super_cull, c->active.p, c->done.p, S, c->best.p,
-        c->count_tiles ? c->counters.p : nullptr, nullptr, sblk, want, c->gbox.p);
+        c->count_tiles ? c->counters.p : nullptr, nullptr, sblk, want, c->gbox.p, exact_args(c, pass));
 #ifdef ORPCD_WAVETIME
     if ((e = dump_wavetime(pass, nact, S, (unsigned)(sblk * S) * (unsigned)nact * kCWaves, s)) != hipSuccess) return e;
 #endif
     }
     if ((e = hipGetLastError()) != hipSuccess) return e;
+    if (c->exact_live) {  // fp64 re-search of the queries the search could not certify
+        nn_exact_kernel<<<kExactBlocks, 256, 0, s>>>(c->src.xyz64.p, N, c->Q.p, c->tdesc.p, c->q32.p,
+                                                     exact_args(c, pass), c->best.p);
+        if ((e = hipGetLastError()) != hipSuccess) return e;
+    }
     if (mid && (e = hipEventRecord(mid, s)) != hipSuccess) return e;
     const int ablk = accum_blocks(N);
     if (c->est == kEstP2P) {

@@ -161,6 +161,8 @@ struct VoxelBufs {  // preprocessing scratch (voxel, SOR, FPS)
 struct KernelStats {
     double launches = 0, ms = 0, pairs = 0, iterations = 0, passes = 0, tiles = 0, accum_ms = 0;
     double sched_launches = 0;  // timed launches of the ordered-dispatch search (nn_search_sched_kernel)
+    double exact_filed = 0;     // exact_nn: queries re-searched in fp64 (nn_exact_kernel), every pass
+    double exact_queries = 0;   // exact_nn: queries searched, every pass
 };
 
 // ------------------------------------------------- several targets per batch
@@ -268,6 +270,13 @@ struct orpcd_ctx {
     orpcd::DevBuf<int32_t> ready;                // B: the last pass whose pose the solver published
     orpcd::DevBuf<unsigned> fuse_err;            // 1: a transform block's wait for its solver timed out
     bool fuse_live = false;                      // the running batch uses it
+    // exact nearest neighbours (opt.exact_nn): queries the fp32 search cannot
+    // certify are filed and re-searched in fp64 (nn_exact_kernel)
+    orpcd::DevBuf<unsigned> xsec;                // B x N: runner-up key near the winner (0xFFFFFFFF: none)
+    orpcd::DevBuf<unsigned long long> xlist;     // B x N: queries with a published runner-up
+    orpcd::DevBuf<unsigned> xcnt;                // 2: list entries, by pass parity
+    orpcd::DevBuf<unsigned long long> xtotal;    // queries re-searched in fp64 (statistics)
+    bool exact_live = false;                     // the running batch runs exact
 
     // kernel-level entry points
     orpcd::CloudLayout aux;
@@ -339,6 +348,9 @@ struct orpcd_ctx {
         int sched_items = 10240;  // ordered dispatch: split a group until its waves cost <= pass total / this
                                   // (C2 sweep 5120 / 10240 / 20480: 15.4 / 15.0 / 16.6 ms at 30 starts)
         int sched_min_starts = 16;  // ordered dispatch only for batches of at least this many starts
+        int exact_nn = 0;         // 1: every correspondence is the fp64 nearest target (the oracle's
+                                  // lexicographic (d^2, input index) minimum): fp32 search + runner-up
+                                  // band test + fp64 re-search of the uncertified queries
         int fuse_solve = 0;       // 1: the 6x6 solve runs inside the next pass's query transform launch
                                   // (bit-identical; measured slower at C2: 30 starts 15.05 -> 15.45 ms)
     } opt;

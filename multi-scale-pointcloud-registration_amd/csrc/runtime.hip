@@ -379,7 +379,7 @@ int fgr_device(orpcd_ctx* c, const double* src, int64_t n, const double* tgt, in
 // and for the alternative search kernels.
 bool persistent_ok(const orpcd_ctx* c) {
     static const bool trace = getenv("ORPCD_TRACE") != nullptr;
-    return c->opt.persist && !trace && c->opt.search_kernel == 0;
+    return c->opt.persist && !trace && c->opt.search_kernel == 0 && !c->opt.exact_nn;
 }
 
 int batch_setup(orpcd_ctx* c, const double* R0, const double* t0, int B, const orpcd_gicp_params* p,
@@ -404,8 +404,18 @@ int batch_setup(orpcd_ctx* c, const double* R0, const double* t0, int B, const o
     if (c->two_phase_ok) CTX_CHECK(c, c->items.ensure(worst_items));
     CTX_CHECK(c, c->item_counts.ensure((size_t)2 * B * ((N + 127) / 128) + 2));
     c->sched_live = sched_wanted(c, persist, B);
-    c->fuse_live = c->opt.fuse_solve && !persist && c->opt.search_kernel == 0 &&
+    c->fuse_live = c->opt.fuse_solve && !persist && c->opt.search_kernel == 0 && !c->opt.exact_nn &&
                    (getenv("ORPCD_TRACE") != nullptr || !pipelined_ok(c));
+    c->exact_live = c->opt.exact_nn != 0;
+    if (c->exact_live) {
+        CTX_REQUIRE(c, c->opt.search_kernel == 0, "exact_nn: needs the split search (search_kernel 0)");
+        CTX_CHECK(c, c->xsec.ensure((size_t)B * N));
+        CTX_CHECK(c, c->xtotal.ensure(1));
+        CTX_CHECK(c, c->xlist.ensure((size_t)B * N));
+        CTX_CHECK(c, c->xcnt.ensure(2));
+        CTX_CHECK(c, hipMemsetAsync(c->xcnt.p, 0, 8, c->stream));
+        CTX_CHECK(c, hipMemsetAsync(c->xtotal.p, 0, 8, c->stream));
+    }
     if (c->fuse_live) {
         CTX_CHECK(c, c->ready.ensure((size_t)B));
         CTX_CHECK(c, c->fuse_err.ensure(1));
@@ -993,6 +1003,7 @@ int run_passes(orpcd_ctx* c, int B, const orpcd_gicp_params* p, double* T_out, d
         CTX_CHECK(c, launch_gicp_solve(c, nact, pass, *p, s, tb));
         ++pending;
         c->stats.passes += nact;
+        if (c->exact_live) c->stats.exact_queries += (double)nact * (double)c->src.n;
         // the host learns which starts finished only every few passes; a
         // finished start's blocks exit at once in the passes in between
         const bool sync = (pass % every) == every - 1 || pass == p->max_iteration;
@@ -1045,6 +1056,11 @@ int run_passes(orpcd_ctx* c, int B, const orpcd_gicp_params* p, double* T_out, d
             if (!hDone[hAct[b]]) hAct[k++] = hAct[b];
         if (k != nact && k > 0) CTX_CHECK(c, hipMemcpyAsync(c->active.p, hAct, (size_t)k * 4, hipMemcpyHostToDevice, s));
         nact = k;
+    }
+    if (c->exact_live) {  // entries re-searched over the batch (nn_exact_kernel adds each pass's count)
+        unsigned long long tot = 0;
+        CTX_CHECK(c, hipMemcpy(&tot, c->xtotal.p, 8, hipMemcpyDeviceToHost));
+        c->stats.exact_filed += (double)tot;
     }
     return read_outputs(c, B, tiles_before, T_out, rmse_out, fitness_out, iters_out, ncorr_out);
 }
@@ -1513,10 +1529,31 @@ int orpcd_set_option(orpcd_ctx* c, const char* key, double value) {
     else if (k == "sched_items" && v >= 64 && v <= (1 << 22)) c->opt.sched_items = v;
     else if (k == "sched_min_starts" && v >= 1) c->opt.sched_min_starts = v;
     else if (k == "fuse_solve" && (v == 0 || v == 1)) c->opt.fuse_solve = v;
+    else if (k == "exact_nn" && (v == 0 || v == 1)) c->opt.exact_nn = v;
     else {
         c->err = "set_option: unknown key or bad value: " + k;
         return ORPCD_EINVAL;
     }
+    return ORPCD_OK;
+}
+
+int orpcd_gicp_correspondences(orpcd_ctx* c, int32_t B, int32_t* idx_out) {
+    if (!c) return ORPCD_EINVAL;
+    CTX_REQUIRE(c, idx_out && B > 0, "gicp_correspondences: bad arguments");
+    const int64_t N = c->src.n;
+    CTX_REQUIRE(c, N > 0 && c->prevnn.n >= (size_t)B * N, "gicp_correspondences: no batch of that size ran");
+    CTX_REQUIRE(c, c->ntgt == 1, "gicp_correspondences: single-target batches only");
+    CTX_CHECK(c, hipSetDevice(c->device));
+    CTX_CHECK(c, hipStreamSynchronize(c->stream));
+    std::vector<int32_t> nn((size_t)B * N), sp((size_t)N), tp((size_t)c->tgt.n);
+    CTX_CHECK(c, hipMemcpy(nn.data(), c->prevnn.p, nn.size() * 4, hipMemcpyDeviceToHost));
+    CTX_CHECK(c, hipMemcpy(sp.data(), c->src.perm.p, sp.size() * 4, hipMemcpyDeviceToHost));
+    CTX_CHECK(c, hipMemcpy(tp.data(), c->tgt.perm.p, tp.size() * 4, hipMemcpyDeviceToHost));
+    for (int b = 0; b < B; ++b)
+        for (int64_t k = 0; k < N; ++k) {  // Morton query k is source point sp[k]
+            const int32_t j = nn[(size_t)b * N + k];
+            idx_out[(size_t)b * N + sp[k]] = j >= 0 && j < (int32_t)c->tgt.n ? tp[j] : -1;
+        }
     return ORPCD_OK;
 }
 
@@ -1545,9 +1582,10 @@ int orpcd_profiling(orpcd_ctx* c, int32_t enable) {
 
 int orpcd_stats(orpcd_ctx* c, double* out, int32_t n) {
     if (!c || !out) return ORPCD_EINVAL;
-    const double v[8] = {c->stats.launches, c->stats.ms, c->stats.pairs, c->stats.iterations, c->stats.passes,
-                         c->stats.tiles, c->stats.accum_ms, c->stats.sched_launches};
-    for (int i = 0; i < n && i < 8; ++i) out[i] = v[i];
+    const double v[10] = {c->stats.launches, c->stats.ms,       c->stats.pairs,          c->stats.iterations,
+                          c->stats.passes,   c->stats.tiles,    c->stats.accum_ms,       c->stats.sched_launches,
+                          c->stats.exact_filed, c->stats.exact_queries};
+    for (int i = 0; i < n && i < 10; ++i) out[i] = v[i];
     return ORPCD_OK;
 }
 

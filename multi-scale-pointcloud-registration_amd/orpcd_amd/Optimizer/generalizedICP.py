@@ -39,6 +39,7 @@ class GeneralizedICP(IOptimizer):
         relative_fitness: float = __ICP_RELATIVE_FITNESS__,
         relative_rmse: float = __ICP_RELATIVE_RMSE__,
         device: Optional[int] = None,
+        exact_nn: bool = False,
     ):
         self._LOG = LoggerFactory.get_logger(log_name=self.__class__.__name__)
         if max_correspondence_distance <= 0:
@@ -55,6 +56,10 @@ class GeneralizedICP(IOptimizer):
         self._relative_fitness = float(relative_fitness)
         self._relative_rmse = float(relative_rmse)
         self._device = device
+        # exact_nn: every correspondence is the fp64 nearest target, as the
+        # oracle's KD-tree finds it (fp32 search + fp64 re-search of the
+        # queries whose runner-up is within the fp32 error band)
+        self._exact_nn = bool(exact_nn)
         self._ctx = None
         self.last_result = None
 
@@ -64,6 +69,8 @@ class GeneralizedICP(IOptimizer):
     def context(self) -> _native.Context:
         if self._ctx is None:
             self._ctx = _native.default_context(self._device)
+        # the process-wide context is shared: this optimizer's search mode every time
+        self._ctx.set_option("exact_nn", 1 if self._exact_nn else 0)
         return self._ctx
 
     def _params(self):

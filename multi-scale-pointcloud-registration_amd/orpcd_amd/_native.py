@@ -60,6 +60,7 @@ EXPORTED = ("orpcd_abi_version", "orpcd_device_count", "orpcd_ctx_create", "orpc
             "orpcd_fgr_optimize", "orpcd_set_source_points", "orpcd_icp_p2p_batch",
             "orpcd_sor", "orpcd_voxel_down_sample", "orpcd_farthest_downsample",
             "orpcd_set_option", "orpcd_set_targets", "orpcd_gicp_batch_targets", "orpcd_test_solve6",
+            "orpcd_gicp_correspondences",
             "orpcd_profiling", "orpcd_stats", "orpcd_reset_stats", "orpcd_rng_draw_attempts")
 
 
@@ -119,6 +120,7 @@ def load_library():
         L.orpcd_gicp_batch_targets.argtypes = [vp, _f64p, _f64p, _i32p, ctypes.c_int32, ctypes.POINTER(GicpParams),
                                                _f64p, _f64p, _f64p, _i32p, _i64p]
         L.orpcd_test_solve6.argtypes = [vp, _f64p, ctypes.c_int32, _f64p, _f64p]
+        L.orpcd_gicp_correspondences.argtypes = [vp, ctypes.c_int32, _i32p]
         L.orpcd_set_source_rows.argtypes = [vp, _f64p, c_i64, c_i64, c_i64]
         L.orpcd_gicp_shard_begin.argtypes = [vp, _f64p, _f64p, ctypes.POINTER(GicpParams), c_i64]
         L.orpcd_gicp_shard_pass.argtypes = [vp, _f64p, _i32p]
@@ -306,6 +308,13 @@ class Context:
                                                      ctypes.byref(p), T.reshape(-1), rmse, fit, iters, ncorr),
                     "orpcd_gicp_batch_targets")
         return dict(T=T, rmse=rmse, fitness=fit, iters=iters, ncorr=ncorr)
+
+    def gicp_correspondences(self, B: int, N: int) -> np.ndarray:
+        """(B, N) input index of each source point's nearest target in the
+        last pass of each start of the last single-target batch (-1: none)."""
+        out = np.zeros((int(B), int(N)), dtype=np.int32)
+        self._check(self._L.orpcd_gicp_correspondences(self._h, int(B), out), "orpcd_gicp_correspondences")
+        return out
 
     def test_solve6(self, sums27: np.ndarray):
         """(serial, wave) results of orpcd_test_solve6: (n, 23) each."""
@@ -501,10 +510,10 @@ class Context:
         self._check(self._L.orpcd_profiling(self._h, int(bool(enable))), "orpcd_profiling")
 
     def stats(self) -> dict:
-        out = np.zeros(8)
-        self._check(self._L.orpcd_stats(self._h, out, 8), "orpcd_stats")
+        out = np.zeros(10)
+        self._check(self._L.orpcd_stats(self._h, out, 10), "orpcd_stats")
         return dict(launches=out[0], ms=out[1], pairs=out[2], iterations=out[3], passes=out[4], tiles=out[5],
-                    accum_ms=out[6], sched_launches=out[7])
+                    accum_ms=out[6], sched_launches=out[7], exact_filed=out[8], exact_queries=out[9])
 
     def reset_stats(self):
         self._check(self._L.orpcd_reset_stats(self._h), "orpcd_reset_stats")

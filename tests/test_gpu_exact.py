@@ -1,0 +1,162 @@
+"""GPU parity of the exact-nearest-neighbour mode (option ``exact_nn``).
+
+With ``exact_nn`` every correspondence is the oracle's: the fp64 lexicographic
+(d^2, input index) minimum of oracle/orpcd_oracle.cpp KDTree::nn1 (:192-217).
+The fp32 search tracks each query's runner-up; a query whose runner-up (or
+another split's winner) lies within the fp32 error band of its winner is
+re-searched in fp64 (nn_exact_kernel); every other query's fp32 winner is
+provably the fp64 one.  Tolerances:
+  * correspondences: identical indices (integer work: bit-exact);
+  * per-optimize GICP at full C2 size: identical iteration counts, T within
+    1e-9 elementwise and inlier RMSE within 1e-12 -- the two sides differ only
+    in the summation order of the 29 normal-equation terms and in how the
+    posed points are formed (oracle: pcd.Transform per iteration; GPU: the
+    composed pose), ~1e-16 relative per pass.
+"""
+import numpy as np
+import pytest
+
+from workloads import rot_xyz, small_pair
+
+pytestmark = pytest.mark.gpu
+
+
+def _posed(src, R0, t0):
+    """The query transform's fp64 arithmetic (xform, no contraction):
+    q_i = ((Q_i0 p0 + Q_i1 p1) + Q_i2 p2) + Q_i3 with Q = [R0^T | t0]."""
+    p0, p1, p2 = src[:, 0], src[:, 1], src[:, 2]
+    return np.stack([((R0[0, i] * p0 + R0[1, i] * p1) + R0[2, i] * p2) + t0[i] for i in range(3)], axis=1)
+
+
+@pytest.fixture
+def exact(ctx):
+    ctx.set_option("exact_nn", 1)
+    yield ctx
+    ctx.set_option("exact_nn", 0)
+
+
+def _c2():
+    from orpcd_amd import Preprocessor
+    from workloads import c2_pair
+    s, t = c2_pair(50_000)
+    return Preprocessor([]).preprocess(s), Preprocessor([]).preprocess(t)
+
+
+def _check_corr(ctx, oracle, src, tgt, R0, t0, radius):
+    B = len(R0)
+    g = ctx.gicp_correspondences(B, len(src))
+    r2 = radius * radius
+    for b in range(B):
+        q = _posed(src, R0[b], t0[b])
+        oi, _ = oracle.nn1_radius(q, tgt, radius)
+        diff = np.nonzero(oi != g[b])[0]
+        for i in diff:  # only the fp32 search radius' margin may differ: a target with r^2 <= d^2 (< 1.0001 r^2)
+            assert oi[i] == -1 and g[b][i] >= 0, (b, i, oi[i], g[b][i])
+            d2 = ((q[i] - tgt[g[b][i]]) ** 2).sum()
+            assert r2 <= d2 <= r2 * 1.001, (b, i, d2)
+    return g
+
+
+@pytest.mark.parametrize("B", [3, 20])  # uniform splits / ordered dispatch (>= 16 starts)
+def test_exact_correspondences_c2_size(exact, oracle, B):
+    """Pass-0 correspondences of posed C2 starts: the oracle's KD-tree answers, index for index."""
+    s, t = _c2()
+    rng = np.random.default_rng(1000 + B)
+    R0 = np.array([rot_xyz(*rng.uniform(-90, 90, 3)) for _ in range(B)])
+    t0 = rng.normal(size=(B, 3)) * 0.1
+    exact.set_target(t)
+    exact.set_source(s)
+    exact.reset_stats()
+    exact.gicp_batch(R0, t0, max_iteration=0)
+    _check_corr(exact, oracle, s, t, R0, t0, 0.5)
+
+
+def test_exact_ties_resolve_to_lowest_input_index(exact, oracle):
+    """Exact fp64 ties (lattice targets, queries at cell/face/edge centres: 8-, 4-
+    and 2-way ties, every coordinate and distance exact in fp32 and fp64) go to the
+    lowest input index, as KDTree::nn1 does; the fast mode resolves them by
+    Morton position instead."""
+    h = 0.125
+    k = np.arange(-8, 9) * h
+    lat = np.stack(np.meshgrid(k, k, k, indexing="ij"), -1).reshape(-1, 3)
+    rng = np.random.default_rng(5)
+    tgt = lat[rng.permutation(len(lat))]                    # input order != Morton order
+    c = (np.arange(-8, 8) + 0.5) * h
+    cells = np.stack(np.meshgrid(c, c, c, indexing="ij"), -1).reshape(-1, 3)
+    faces = cells.copy()
+    faces[:, 2] = np.round(faces[:, 2] / h - 0.5) * h      # z on the lattice: 4-way ties
+    edges = faces.copy()
+    edges[:, 1] = np.round(edges[:, 1] / h - 0.5) * h      # y too: 2-way ties
+    src = np.concatenate([cells, faces, edges])
+    src = src[rng.permutation(len(src))]
+    exact.set_target(tgt)
+    exact.set_source(src)
+    R0, t0 = np.eye(3)[None], np.zeros((1, 3))
+    exact.gicp_batch(R0, t0, max_iteration=0)
+    g = _check_corr(exact, oracle, src, tgt, R0, t0, 0.5)
+    d2 = ((src - tgt[g[0]]) ** 2).sum(1)
+    assert np.all(np.isin(np.round(d2 / (h * h) * 4), [1, 2, 3]))  # every query tied (2, 4 or 8 ways)
+
+
+def test_exact_gicp_full_c2_size_matches_oracle(exact, oracle):
+    """Three of the bench's posed starts at full C2 size, to convergence: with
+    exact correspondences the trajectories are the oracle's (compare
+    test_gpu_gicp.py::test_gicp_full_c2_size_posed_starts_match_oracle, whose
+    fp32 near-tie flips allow 1e-5 / 2e-4)."""
+    s, t = _c2()
+    rng = np.random.default_rng(1000)
+    R0 = np.array([rot_xyz(*rng.uniform(-90, 90, 3)) for _ in range(3)])
+    t0 = rng.normal(size=(3, 3)) * 0.1
+    exact.set_target(t)
+    exact.set_source(s)
+    exact.reset_stats()
+    r = exact.gicp_batch(R0, t0)
+    st = exact.stats()
+    for b in range(3):
+        o = oracle.gicp(np.dot(s, R0[b]) + t0[b], t, 0.5, 100)
+        assert r["iters"][b] == o["iters"], (b, r["iters"][b], o["iters"])
+        assert abs(r["rmse"][b] - o["rmse"]) <= 1e-12, (b, r["rmse"][b], o["rmse"])
+        assert np.abs(r["T"][b] - o["T"]).max() <= 1e-9, (b, np.abs(r["T"][b] - o["T"]).max())
+        assert r["ncorr"][b] == o["ncorr"]
+    assert 0 < st["exact_filed"] < 0.05 * st["exact_queries"], st  # the band test files a small share
+
+
+def test_exact_mode_small_pairs_and_multi_target(exact, oracle):
+    """Ragged small clouds (not tile multiples), several posed starts, and a
+    multi-target batch: per start the oracle's iterations, T to 1e-9."""
+    src, tgt = small_pair(1500, 1800, seed=3)
+    rng = np.random.default_rng(7)
+    B = 6
+    R0 = np.array([rot_xyz(*rng.uniform(-90, 90, 3)) for _ in range(B)])
+    t0 = rng.normal(size=(B, 3)) * 0.1
+    exact.set_target(tgt)
+    exact.set_source(src)
+    r = exact.gicp_batch(R0, t0)
+    for b in range(B):
+        o = oracle.gicp(np.dot(src, R0[b]) + t0[b], tgt, 0.5, 100)
+        assert r["iters"][b] == o["iters"]
+        assert np.abs(r["T"][b] - o["T"]).max() <= 1e-9
+        assert abs(r["rmse"][b] - o["rmse"]) <= 1e-12
+    # two targets in one batch: each start's result equals its single-target run
+    tgt2 = tgt * np.array([1.1, 1.0, 0.95])
+    exact.set_targets([tgt, tgt2])
+    which = np.array([0, 1, 0, 1, 1, 0], dtype=np.int32)
+    rm = exact.gicp_batch_targets(R0, t0, which)
+    for b in range(B):
+        o = oracle.gicp(np.dot(src, R0[b]) + t0[b], [tgt, tgt2][which[b]], 0.5, 100)
+        assert rm["iters"][b] == o["iters"]
+        assert np.abs(rm["T"][b] - o["T"]).max() <= 1e-9
+
+
+def test_exact_option_rejected_with_other_searches(ctx):
+    src, tgt = small_pair(500, seed=2)
+    ctx.set_target(tgt)
+    ctx.set_source(src)
+    ctx.set_option("exact_nn", 1)
+    ctx.set_option("search_kernel", 1)
+    try:
+        with pytest.raises(Exception):
+            ctx.gicp_batch(np.eye(3)[None], np.zeros((1, 3)))
+    finally:
+        ctx.set_option("search_kernel", 0)
+        ctx.set_option("exact_nn", 0)

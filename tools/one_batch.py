@@ -40,6 +40,10 @@ def main():
     import hashlib
     h = hashlib.sha1(np.ascontiguousarray(r["T"]).tobytes() + r["rmse"].tobytes() + r["iters"].tobytes()).hexdigest()
     print("iters", int(r["iters"].sum()), "result sha1", h[:16])
+    st = ctx.stats()
+    if st["exact_queries"] > 0:
+        print(f"exact_nn: {st['exact_filed'] / reps:.0f} queries re-searched per batch of "
+              f"{st['exact_queries'] / reps:.0f} ({100 * st['exact_filed'] / st['exact_queries']:.3f}%)")
     ctx.close()
 
 
