@@ -127,12 +127,16 @@ def main():
     cpu = None
     align_s = None
     parity = None
+    exact = None
     if rank == 0 and world == 1:
         if args.cpu_seconds > 0:
             cpu = cpu_baseline(source, target, args)
             # "final RMSE vs ref": the GPU's per-start inlier RMSE of step 0 against the
             # oracle's on the same starts (stated full-size tolerance 1e-5)
             o = np.array(cpu.pop("oracle_rmse"))
+            o_iters = np.array(cpu.pop("oracle_iters"))
+            if len(o):
+                exact = exact_mode_run(source, target, args, local_rank, o, o_iters)
             if rmse_step0 is not None and len(o):
                 d = np.abs(rmse_step0[: len(o)] - o)
                 parity = {"starts": int(len(o)), "max_abs_d_rmse": float(d.max()),
@@ -192,12 +196,47 @@ def main():
                              / (avg_ms * 1e-3) / 1e12, 1) if avg_ms > 0 else None},
             "cpu_baseline": cpu,
             "parity_vs_oracle": parity,
+            "exact_nn": exact,
             "gicp_iterations": int(iters),
             "align": align_s,
         }
         print(json.dumps(line))
     if dist is not None:
         dist.destroy_process_group()
+
+
+def exact_mode_run(source, target, args, device, oracle_rmse, oracle_iters):
+    """The same steps with GeneralizedICP(exact_nn=True): every correspondence the
+    oracle's (fp64 KD-tree answer).  Its rate, and step 0's starts
+    against the oracle: per start the RMSE difference and the iteration counts."""
+    from orpcd_amd import Aligner, GeneralizedICP, Preprocessor
+
+    opt = GeneralizedICP(device=device, exact_nn=True)
+    ctx = opt.context
+    al = Aligner(Preprocessor([]), Preprocessor([]), opt, attempts=args.attempts)
+    np.random.seed(1000)
+    al.multistart_registration(source, target)  # step 0 (warm-up and parity)
+    r0 = np.array(al.history[-1]["rmse"])
+    it0 = np.array(al.history[-1]["iters_per_start"]) if "iters_per_start" in al.history[-1] else None
+    ctx.reset_stats()
+    t0 = time.perf_counter()
+    iters = 0
+    for k in range(args.steps):
+        np.random.seed(1000 + args.warmup + k)
+        al.multistart_registration(source, target)
+        iters += al.history[-1]["iters"]
+    el = time.perf_counter() - t0
+    st = ctx.stats()
+    n = len(oracle_rmse)
+    d = np.abs(r0[:n] - oracle_rmse)
+    out = {"value": round(iters / el, 3), "unit": "GICP iterations/s", "ms_per_step": round(el / args.steps * 1e3, 3),
+           "steps": args.steps, "gicp_iterations": int(iters),
+           "requeried_fraction": round(st["exact_filed"] / max(st["exact_queries"], 1), 5),
+           "parity_vs_oracle": {"starts": int(n), "max_abs_d_rmse": float(d.max()),
+                                "within_1e-9": int((d <= 1e-9).sum())}}
+    if it0 is not None:
+        out["parity_vs_oracle"]["iterations_identical"] = int((it0[:n] == oracle_iters).sum())
+    return out
 
 
 def pmc_traffic(kernel):
@@ -226,16 +265,18 @@ def cpu_baseline(source, target, args):
     t0 = time.perf_counter()
     iters = 0
     done = 0
-    oracle_rmse = []
+    oracle_rmse, oracle_iters = [], []
     for R0, t0_ in starts:
         r = O.gicp(np.dot(source, R0) + t0_, target, 0.5, 100)
         iters += r["iters"]
         oracle_rmse.append(float(r["rmse"]))
+        oracle_iters.append(int(r["iters"]))
         done += 1
         if time.perf_counter() - t0 > args.cpu_seconds:
             break
     el = time.perf_counter() - t0
-    return {"oracle_rmse": oracle_rmse, "value": round(iters / el, 3), "unit": "GICP iterations/s",
+    return {"oracle_rmse": oracle_rmse, "oracle_iters": oracle_iters, "value": round(iters / el, 3),
+            "unit": "GICP iterations/s",
             "cores": O.num_threads(),
             "kind": "port",
             "sample": f"{done} of {args.attempts} starts of step 0 (same R0,t0), {iters} GICP iterations, "

@@ -273,7 +273,8 @@ class Aligner:
         t_start = time.perf_counter()
         table = self._run_tables(source, [target], [draw])[0]
         self.history.append(dict(B=self._attempts, seconds=time.perf_counter() - t_start,
-                                 iters=int(table["iters"].sum()), rmse=table["rmse"].copy()))
+                                 iters=int(table["iters"].sum()), rmse=table["rmse"].copy(),
+                                 iters_per_start=table["iters"].copy()))
         return self._select(table, draw)
 
     def _scaled_targets(self, target, scales):
