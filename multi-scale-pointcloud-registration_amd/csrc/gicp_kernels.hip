@@ -146,6 +146,15 @@ __device__ __forceinline__ double ldg_f64(const double* p) {
 // the key truncation (2^-17 relative on the winner's d^2) and 2^-19 for its
 // own fp32 rounding.
 // ---------------------------------------------------------------------------
+#ifndef ORPCD_SCAN_UNROLL_EXACT
+#define ORPCD_SCAN_UNROLL_EXACT 2
+#endif
+#ifndef ORPCD_SCAN_UNROLL_FAST
+#define ORPCD_SCAN_UNROLL_FAST 8
+#endif
+#ifndef ORPCD_EXACT_WAVES
+#define ORPCD_EXACT_WAVES 5
+#endif
 constexpr float kU = 5.9604645e-08f;  // 2^-24
 __device__ __forceinline__ float exact_band_hi(float x, float A) {
 #pragma clang fp contract(off)  // identical rounding in the query transform and the search
@@ -208,6 +217,9 @@ __device__ __forceinline__ int culled_search(float4* stage, const float4* __rest
                                              float4 s0lo, float4 s0hi, const float4* gbox = nullptr,
                                              unsigned long long* phase_cull_out = nullptr,
                                              unsigned* sk = nullptr) {
+    // exact: the scan unrolled by 2 only, so the runner-up tracking fits the
+    // 5-waves/SIMD register budget without spills (fully unrolled: 11-15 spills)
+    constexpr int kScanUnroll = kExact ? ORPCD_SCAN_UNROLL_EXACT : ORPCD_SCAN_UNROLL_FAST;
     const int lane = threadIdx.x & 63;
     const bool v0 = bound[0] > 0.0f, v1 = bound[1] > 0.0f;
     unsigned k0 = v0 ? __float_as_uint(bound[0]) : 0u;  // best key (0: never improves)
@@ -429,7 +441,7 @@ __device__ __forceinline__ int culled_search(float4* stage, const float4* __rest
             const bool need = qd2.x * kQuarterSlack < b0 || qd2.y * kQuarterSlack < b1;
             if (!__any(need)) continue;
             ++visited;
-#pragma unroll
+#pragma unroll kScanUnroll
             for (int kk = qd * kQuarter; kk < (qd + 1) * kQuarter; kk += 2) {
                 const f2 tx = *reinterpret_cast<const f2*>(sx + kk);
                 const f2 ty = *reinterpret_cast<const f2*>(sx + 64 + kk);
@@ -927,8 +939,8 @@ __device__ __forceinline__ void nn_search_body(
 // Ordered dispatch (SchedS): wave k of the launch takes item k of the
 // class-major list, heaviest class first; the wave's duration is added to its
 // group's cost and to the pass total for the next pass's schedule.
-template <bool kExact>  // exact: 4 waves/SIMD (at 5 the runner-up registers spill)
-__global__ __launch_bounds__(kCBlock) __attribute__((amdgpu_waves_per_eu(kExact ? 4 : 5, 8))) void nn_search_sched_kernel(
+template <bool kExact>
+__global__ __launch_bounds__(kCBlock) __attribute__((amdgpu_waves_per_eu(kExact ? ORPCD_EXACT_WAVES : 5, 8))) void nn_search_sched_kernel(
     const float4* __restrict__ q32, int N, const TargetDesc* __restrict__ tdesc, int super_cull,
     unsigned long long* __restrict__ best, unsigned long long* __restrict__ counters,
     const float4* __restrict__ gbox, SchedS sa, ExactArgs ex) {
@@ -1026,8 +1038,8 @@ __device__ __forceinline__ bool map_search_block(const int32_t* __restrict__ nac
 
 // Two register budgets of the same search (orpcd_set_option "search_occupancy"):
 // the compiler's choice (5 waves/SIMD) and a cap at 6 waves/SIMD.
-template <bool kExact>  // exact: 4 waves/SIMD (at 5 the runner-up registers spill)
-__global__ __launch_bounds__(kCBlock) __attribute__((amdgpu_waves_per_eu(kExact ? 4 : 5, 8))) void nn_search_kernel(
+template <bool kExact>
+__global__ __launch_bounds__(kCBlock) __attribute__((amdgpu_waves_per_eu(kExact ? ORPCD_EXACT_WAVES : 5, 8))) void nn_search_kernel(
     ORPCD_NN_SEARCH_ARGS) {
     __shared__ float4 stage[kCWaves][kTile];
     const int wid = threadIdx.x >> 6;
