@@ -146,14 +146,17 @@ __device__ __forceinline__ double ldg_f64(const double* p) {
 // the key truncation (2^-17 relative on the winner's d^2) and 2^-19 for its
 // own fp32 rounding.
 // ---------------------------------------------------------------------------
+// exact mode's search: 4 waves/SIMD, fully unrolled scan (measured at C2, 8 / 30
+// starts: 9.78 / 21.45 ms; 5 waves with the scan unrolled by 2 or 4, which fit
+// without spills: 9.74-9.94 / 21.98-22.29 ms; re-search grid 1024 blocks: 22.53)
 #ifndef ORPCD_SCAN_UNROLL_EXACT
-#define ORPCD_SCAN_UNROLL_EXACT 2
+#define ORPCD_SCAN_UNROLL_EXACT 8
 #endif
 #ifndef ORPCD_SCAN_UNROLL_FAST
 #define ORPCD_SCAN_UNROLL_FAST 8
 #endif
 #ifndef ORPCD_EXACT_WAVES
-#define ORPCD_EXACT_WAVES 5
+#define ORPCD_EXACT_WAVES 4
 #endif
 constexpr float kU = 5.9604645e-08f;  // 2^-24
 __device__ __forceinline__ float exact_band_hi(float x, float A) {
@@ -217,8 +220,6 @@ __device__ __forceinline__ int culled_search(float4* stage, const float4* __rest
                                              float4 s0lo, float4 s0hi, const float4* gbox = nullptr,
                                              unsigned long long* phase_cull_out = nullptr,
                                              unsigned* sk = nullptr) {
-    // exact: the scan unrolled by 2 only, so the runner-up tracking fits the
-    // 5-waves/SIMD register budget without spills (fully unrolled: 11-15 spills)
     constexpr int kScanUnroll = kExact ? ORPCD_SCAN_UNROLL_EXACT : ORPCD_SCAN_UNROLL_FAST;
     const int lane = threadIdx.x & 63;
     const bool v0 = bound[0] > 0.0f, v1 = bound[1] > 0.0f;
@@ -2819,7 +2820,10 @@ static ExactArgs exact_args(const orpcd_ctx* c, int pass) {
     ex.total = c->xtotal.p;
     return ex;
 }
-constexpr int kExactBlocks = 256;  // re-search grid: 1024 waves, 64 listed queries per wave and round
+#ifndef ORPCD_EXACT_BLOCKS
+#define ORPCD_EXACT_BLOCKS 256
+#endif
+constexpr int kExactBlocks = ORPCD_EXACT_BLOCKS;  // re-search grid: 1024 waves, 64 listed queries per wave and round
 
 hipError_t launch_xform(const orpcd_ctx* c, int nact, int pass, double r2, hipStream_t s, bool dev_nact,
                         const TgtBounds& tb) {
