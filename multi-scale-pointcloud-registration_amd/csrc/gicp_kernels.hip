@@ -176,17 +176,6 @@ __device__ __forceinline__ float exact_sentinel(float bound, float A) {
 #pragma clang fp contract(off)
     return exact_band_hi(bound, A) * 1.00003f + 1e-30f;  // > 2^-17: survives the key mask
 }
-// per-wave culling slack cw >= band_hi(x) - x for every x <= W (the wave's
-// largest sentinel) and query norm <= Amax; band_hi(x) - x is increasing in x
-__device__ __forceinline__ float exact_cull_slack(float W, float Amax) {
-#pragma clang fp contract(off)
-    return (exact_band_hi(W, Amax) - W) * 1.0001f + W * 1e-6f + 1e-30f;
-}
-template <bool kExact>
-__device__ __forceinline__ float plus_cw(float v, float cw) {
-    if constexpr (kExact) return v + cw;
-    else return v;
-}
 __device__ __forceinline__ unsigned umed3(unsigned a, unsigned b, unsigned c) {
     return max(min(a, b), min(max(a, b), c));  // v_med3_u32
 }
@@ -206,7 +195,7 @@ struct ExactArgs {
 // index of the chosen target or -1, bd[] its fp32 d^2 (key-truncated).
 // --------------------------------------------------------------------------
 // kExact: the bound is the exact-mode sentinel, candidates are culled against
-// key + cw (see exact_band_hi), the in-scan minimum runs over the query's
+// band_hi of the query's best key (see exact_band_hi), the in-scan minimum runs over the query's
 // whole search (tie order among equal masked keys is then immaterial: such
 // keys are within the band and re-searched in fp64), and sk[] returns the
 // second-smallest key scanned (0xFFFFFFFF: none).
@@ -234,17 +223,13 @@ __device__ __forceinline__ int culled_search(float4* stage, const float4* __rest
     // (gbox: lo.xyz | max bound bits, hi.xyz), else reduced here
     unsigned Wk;
     float lox, loy, loz, hix, hiy, hiz;
-    float cw = 0.0f;  // exact: culling slack of this wave (scalar)
+    // exact: each query's culling bound, band_hi of its best key (the sentinel
+    // before it has one): every candidate within the band is scanned
+    float e0 = kExact && v0 ? bound[0] : 0.0f, e1 = kExact && v1 ? bound[1] : 0.0f;
     if constexpr (kGBox) {
         const float4 g0 = gbox[0], g1 = gbox[1];
         Wk = __float_as_uint(g0.w) & kKeyMask;
         lox = g0.x, loy = g0.y, loz = g0.z, hix = g1.x, hiy = g1.y, hiz = g1.z;
-        if constexpr (kExact) {
-            const float ax = fmaxf(fabsf(lox), fabsf(hix)), ay = fmaxf(fabsf(loy), fabsf(hiy)),
-                        az = fmaxf(fabsf(loz), fabsf(hiz));
-            cw = exact_cull_slack(__uint_as_float(__float_as_uint(g0.w)), qnorm(ax, ay, az));
-            cw = __uint_as_float(__builtin_amdgcn_readfirstlane(__float_as_uint(cw)));
-        }
     } else {
         static_assert(kGBox || !kExact, "exact mode needs the transform's wave boxes");
         Wk = wave_umax((k0 > k1 ? k0 : k1) & kKeyMask);
@@ -256,7 +241,7 @@ __device__ __forceinline__ int culled_search(float4* stage, const float4* __rest
         hiz = wave_fmax(fmaxf(v0 ? qz[0] : -inf, v1 ? qz[1] : -inf));
     }
     if (Wk == 0u) return 0;  // no query of this wave can take anything
-    float W = plus_cw<kExact>(__uint_as_float(Wk), cw);
+    float W = __uint_as_float(Wk);
     int visited = 0;
 
     // candidate cursor: rounds of 64 tiles, one tile per lane; wave-box test by
@@ -371,8 +356,8 @@ __device__ __forceinline__ int culled_search(float4* stage, const float4* __rest
             const float hy = __uint_as_float(__builtin_amdgcn_readlane(__float_as_uint(b.y), k));
             const float hz = __uint_as_float(__builtin_amdgcn_readlane(__float_as_uint(b.z), k));
             const f2 bd2 = box_d2_2q(f2{qx[0], qx[1]}, f2{qy[0], qy[1]}, f2{qz[0], qz[1]}, lx, ly, lz, hx, hy, hz);
-            const bool need0 = bd2.x < plus_cw<kExact>(__uint_as_float(k0 & kKeyMask), cw);
-            const bool need1 = bd2.y < plus_cw<kExact>(__uint_as_float(k1 & kKeyMask), cw);
+            const bool need0 = bd2.x < (kExact ? e0 : __uint_as_float(k0 & kKeyMask));
+            const bool need1 = bd2.y < (kExact ? e1 : __uint_as_float(k1 & kKeyMask));
 #ifdef ORPCD_PHASES
             {
                 const unsigned long long b0 = __ballot(need0), b1 = __ballot(need1);
@@ -435,8 +420,8 @@ __device__ __forceinline__ int culled_search(float4* stage, const float4* __rest
             // quarters); the 2^-20 slack keeps the test conservative against
             // the scan's own fp32 rounding
             const float4 lo = qb[qd], hi = qb[4 + qd];
-            const float b0 = plus_cw<kExact>(__uint_as_float((k0 < m0 ? k0 : m0) & kKeyMask), cw);
-            const float b1 = plus_cw<kExact>(__uint_as_float((k1 < m1 ? k1 : m1) & kKeyMask), cw);
+            const float b0 = kExact ? e0 : __uint_as_float((k0 < m0 ? k0 : m0) & kKeyMask);
+            const float b1 = kExact ? e1 : __uint_as_float((k1 < m1 ? k1 : m1) & kKeyMask);
             const f2 qd2 = box_d2_2q(f2{qx[0], qx[1]}, f2{qy[0], qy[1]}, f2{qz[0], qz[1]}, lo.x, lo.y, lo.z, hi.x,
                                      hi.y, hi.z);
             const bool need = qd2.x * kQuarterSlack < b0 || qd2.y * kQuarterSlack < b1;
@@ -481,14 +466,16 @@ __device__ __forceinline__ int culled_search(float4* stage, const float4* __rest
 #ifdef ORPCD_PHASES
         ph_impr += __any((m0 & kKeyMask) < (k0 & kKeyMask) || (m1 & kKeyMask) < (k1 & kKeyMask)) ? 1 : 0;
 #endif
-        if constexpr (kExact) {  // the minimum moved into this tile
+        if constexpr (kExact) {  // the minimum moved into this tile: its band is the new bound
             if (m0 != k0) {
                 k0 = m0;
                 t0 = tile;
+                e0 = exact_band_hi(__uint_as_float(k0 & kKeyMask), qnorm(qx[0], qy[0], qz[0]));
             }
             if (m1 != k1) {
                 k1 = m1;
                 t1 = tile;
+                e1 = exact_band_hi(__uint_as_float(k1 & kKeyMask), qnorm(qx[1], qy[1], qz[1]));
             }
         } else {
             if ((m0 & kKeyMask) < (k0 & kKeyMask)) {
@@ -500,8 +487,12 @@ __device__ __forceinline__ int culled_search(float4* stage, const float4* __rest
                 t1 = tile;
             }
         }
-        Wk = wave_umax((k0 > k1 ? k0 : k1) & kKeyMask);
-        W = plus_cw<kExact>(__uint_as_float(Wk), cw);
+        if constexpr (kExact) {
+            W = __uint_as_float(wave_umax(max(__float_as_uint(e0), __float_as_uint(e1))));
+        } else {
+            Wk = wave_umax((k0 > k1 ? k0 : k1) & kKeyMask);
+            W = __uint_as_float(Wk);
+        }
         // the prefetched candidate was chosen under the previous bound: re-test
         while (nxt >= 0 && !(lbn < W)) {
             nxt = next_candidate(lbn);
