@@ -160,3 +160,74 @@ def test_exact_option_rejected_with_other_searches(ctx):
     finally:
         ctx.set_option("search_kernel", 0)
         ctx.set_option("exact_nn", 0)
+
+
+def _init(deg, t):
+    T = np.eye(4)
+    T[:3, :3] = rot_xyz(*deg)
+    T[:3, 3] = t
+    return T
+
+
+def test_exact_refinement_p2p_matches_oracle(exact, oracle):
+    """PointToPoint ICP (the refinement row) in exact mode: the oracle's
+    iterations, T to 1e-9 (its correspondences come from the same search)."""
+    from orpcd_amd import Preprocessor
+    from workloads import c2_pair
+    s, t = c2_pair(20_000)
+    s, t = Preprocessor([]).preprocess(s), Preprocessor([]).preprocess(t)
+    inits = np.stack([np.eye(4), _init((4, -3, 5), (0.02, 0.0, -0.01)), _init((-10, 8, 3), (0.0, 0.05, 0.0))])
+    exact.set_target_points(t)
+    exact.set_source_points(s)
+    g = exact.icp_p2p_batch(inits, max_correspondence_distance=0.5, max_iteration=60)
+    for b in range(len(inits)):
+        o = oracle.icp_p2p(s, t, 0.5, inits[b], 60)
+        assert g["iters"][b] == o["iters"], (b, g["iters"][b], o["iters"])
+        assert np.abs(g["T"][b] - o["T"]).max() <= 1e-9
+        assert abs(g["rmse"][b] - o["rmse"]) <= 1e-12
+
+
+@pytest.mark.parametrize("offset", [1e4, -3e5])
+def test_exact_far_from_origin_correspondences(exact, oracle, offset):
+    """Clouds far from the world origin (|x| ~ 1e4 .. 3e5, the fp32 frame's
+    origin at the target's box centre): the correspondences are still the
+    oracle's, index for index."""
+    src, tgt = small_pair(3000, 3500, seed=6)
+    src, tgt = src + offset, tgt + offset
+    rng = np.random.default_rng(2)
+    R0 = np.array([rot_xyz(*rng.uniform(-30, 30, 3)) for _ in range(4)])
+    ov = np.full(3, offset)
+    t0 = np.array([ov - ov @ R for R in R0])  # rotate about the cloud, not the world origin
+    exact.set_target(tgt)
+    exact.set_source(src)
+    exact.gicp_batch(R0, t0, max_iteration=0)
+    _check_corr(exact, oracle, src, tgt, R0, t0, 0.5)
+
+
+def test_exact_row_sharded_gicp_matches_oracle(exact, oracle):
+    """One GICP split by source rows over emulated ranks (the C5 path) in exact
+    mode: the ranks agree bit for bit and match the oracle's trajectory."""
+    from orpcd_amd import _native, parallel
+    src, tgt = small_pair(6007, 5003, seed=11)
+    ctxs = [_native.Context(0) for _ in range(2)]
+    for k, c in enumerate(ctxs):
+        c.set_option("exact_nn", 1)
+        lo, hi = parallel.shard(len(src), k, 2)
+        c.set_target(tgt, 1e-3)
+        c.set_source_rows(src, lo, hi)
+        c.shard_begin(np.eye(3), np.zeros(3), n_total=len(src), max_correspondence_distance=0.3)
+    while True:
+        parts = [c.shard_pass() for c in ctxs]
+        if not parts[0][1]:
+            break
+        total = np.sum([s for s, _ in parts], axis=0)
+        done = {c.shard_update(total) for c in ctxs}
+        if done.pop():
+            break
+    res = [c.shard_result() for c in ctxs]
+    assert np.array_equal(res[0]["T"], res[1]["T"]) and res[0]["rmse"] == res[1]["rmse"]
+    o = oracle.gicp(src, tgt, 0.3)
+    assert res[0]["iters"] == o["iters"]
+    assert np.abs(res[0]["T"] - o["T"]).max() <= 1e-9 and abs(res[0]["rmse"] - o["rmse"]) <= 1e-12
+    for c in ctxs:
+        c.close()
