@@ -1073,13 +1073,16 @@ __device__ __forceinline__ float box_d2_plain(float x, float y, float z, float4 
     return box_d2(x, y, z, lo.x, lo.y, lo.z, hi.x, hi.y, hi.z);
 }
 
+constexpr int kExactList = 512;  // candidate tiles listed per wave before a scan
+
 __global__ __launch_bounds__(256) void nn_exact_kernel(const double* __restrict__ src, int N,
                                                        const double* __restrict__ Qm,
                                                        const TargetDesc* __restrict__ tdesc,
                                                        const float4* __restrict__ q32, ExactArgs ex,
                                                        unsigned long long* __restrict__ best) {
 #pragma clang fp contract(off)
-    const int lane = threadIdx.x & 63;
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    __shared__ int tlist[4][kExactList];  // a wave's listed candidate tiles
     const unsigned gw = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6), nw = gridDim.x * (blockDim.x >> 6);
     const unsigned n = __builtin_amdgcn_readfirstlane(*ex.cnt);
     if (gw == 0 && lane == 0) *ex.cnt_next = 0u;
@@ -1124,32 +1127,72 @@ __global__ __launch_bounds__(256) void nn_exact_kernel(const double* __restrict_
             const double dj = sqrt(bD);
             const double rb = dj + 5.9604644775390625e-08 * (4.0 * (double)qnorm(x, y, z) + 7.0 * dj);
             const float Tb = (float)(rb * rb * (1.0 + 1.0 / 65536.0)) * 1.0001f;
+            // candidate tiles: their boxes are tested four surviving super-tiles
+            // at a time, the survivors listed in LDS, then scanned four tiles at a
+            // time (every lane's four loads in flight together): the chain of
+            // dependent round trips, not the arithmetic, bounds this search
+            int nt = 0;  // listed tiles (wave-uniform)
+            auto scan_listed = [&]() {
+                for (int c = 0; c < nt; c += 4) {
+                    int kk[4], in[4];
+                    double tx[4], ty[4], tz[4];
+#pragma unroll
+                    for (int u4 = 0; u4 < 4; ++u4) {
+                        kk[u4] = c + u4 < nt ? tlist[wid][c + u4] * kTile + lane : -1;
+                        const int k = kk[u4] >= 0 ? kk[u4] : 0;
+                        in[u4] = __float_as_int(tg.p4[k].w);
+                        tx[u4] = t64[3 * (size_t)k];
+                        ty[u4] = t64[3 * (size_t)k + 1];
+                        tz[u4] = t64[3 * (size_t)k + 2];
+                    }
+#pragma unroll
+                    for (int u4 = 0; u4 < 4; ++u4) {
+                        if (kk[u4] < 0 || in[u4] < 0) continue;  // past the list / padding
+                        const double tp[3] = {tx[u4], ty[u4], tz[u4]};
+                        const double D = d2_oracle(q, tp);
+                        if (D < bD || (D == bD && in[u4] < bI)) {
+                            bD = D;
+                            bI = in[u4];
+                            bM = kk[u4];
+                        }
+                    }
+                }
+                nt = 0;
+            };
             for (int sb = 0; sb < tg.nsuper; sb += 64) {
                 const int u = sb + lane;
                 const bool su_ok = u < tg.nsuper && box_d2_plain(x, y, z, tg.slo[u], tg.shi[u]) <= Tb;
                 unsigned long long sm = __ballot(su_ok);
                 while (sm) {
-                    const int su = sb + __builtin_ctzll(sm);
-                    sm &= sm - 1;
-                    const int t = su * kSuper + lane;
-                    const bool t_ok = t < tg.ntiles && box_d2_plain(x, y, z, tg.tlo[t], tg.thi[t]) <= Tb;
-                    unsigned long long tm = __ballot(t_ok);
-                    while (tm) {
-                        const int tt = su * kSuper + __builtin_ctzll(tm);
-                        tm &= tm - 1;
-                        const int k = tt * kTile + lane;  // Morton position (padding: input index -1)
-                        const int in = __float_as_int(tg.p4[k].w);
-                        if (in >= 0) {
-                            const double D = d2_oracle(q, t64 + 3 * (size_t)k);
-                            if (D < bD || (D == bD && in < bI)) {
-                                bD = D;
-                                bI = in;
-                                bM = k;
-                            }
-                        }
+                    int su4[4];
+                    bool ok[4];
+#pragma unroll
+                    for (int u4 = 0; u4 < 4; ++u4) {
+                        su4[u4] = sm ? sb + __builtin_ctzll(sm) : -1;
+                        sm &= sm - 1;
+                        const int t = su4[u4] * kSuper + lane;
+                        ok[u4] = su4[u4] >= 0 && t < tg.ntiles;
+                        const float4 lo = ok[u4] ? tg.tlo[t] : make_float4(0.f, 0.f, 0.f, 0.f);
+                        const float4 hi = ok[u4] ? tg.thi[t] : lo;
+                        ok[u4] = ok[u4] && box_d2_plain(x, y, z, lo, hi) <= Tb;
                     }
+#pragma unroll
+                    for (int u4 = 0; u4 < 4; ++u4) {
+                        unsigned long long tm = __ballot(ok[u4]);
+                        const int cnt = __builtin_popcountll(tm);
+                        if (nt + cnt > kExactList) scan_listed();  // the list is full: scan it first
+                        const int pos = nt + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(tm >> 32),
+                                                                         __builtin_amdgcn_mbcnt_lo((unsigned)tm, 0));
+                        if (ok[u4]) tlist[wid][pos] = su4[u4] * kSuper + lane;
+                        nt += cnt;
+                    }
+                    __builtin_amdgcn_wave_barrier();
                 }
             }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            scan_listed();
 #pragma unroll
             for (int o = 32; o >= 1; o >>= 1) {  // lexicographic (d^2, input index) over the wave
                 const double oD = __shfl_xor(bD, o);
