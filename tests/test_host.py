@@ -266,3 +266,23 @@ def test_native_rng_replay_matches_numpy(seed):
             assert np.array_equal(g[k], rs.randn(3)), (n, k)
         a, b = ld.state(), rs.get_state()
         assert a[0] == b[0] and np.array_equal(a[1], b[1]) and a[2:] == b[2:]
+
+
+def test_generalized_icp_sets_its_search_mode_on_the_shared_context():
+    """GeneralizedICP(exact_nn=...) selects the search mode on the process-wide
+    context every time it hands the context out, so two optimizers with
+    different modes can share it (bench.py runs both)."""
+    from orpcd_amd import GeneralizedICP
+
+    class FakeCtx:
+        def __init__(self):
+            self.options = []
+
+        def set_option(self, key, value):
+            self.options.append((key, value))
+
+    fake = FakeCtx()
+    fast, exact = GeneralizedICP(), GeneralizedICP(exact_nn=True)
+    fast._ctx = exact._ctx = fake
+    assert exact.context is fake and fake.options[-1] == ("exact_nn", 1)
+    assert fast.context is fake and fake.options[-1] == ("exact_nn", 0)
