@@ -231,3 +231,40 @@ def test_exact_row_sharded_gicp_matches_oracle(exact, oracle):
     assert np.abs(res[0]["T"] - o["T"]).max() <= 1e-9 and abs(res[0]["rmse"] - o["rmse"]) <= 1e-12
     for c in ctxs:
         c.close()
+
+
+def test_exact_align_matches_oracle_aligner(oracle):
+    """Full Aligner.align (speculative compass, multi-target batches; refine
+    off) with GeneralizedICP(exact_nn=True) on a small anisotropic pair: the
+    oracle Aligner's decisions, metric and T to round-off."""
+    from orpcd_amd import Aligner, GeneralizedICP, Preprocessor
+    src, tgt = small_pair(800, 900, seed=6)
+    tgt = tgt * np.array([1.15, 1.0, 0.9])
+    np.random.seed(0)
+    o = oracle.OracleAligner(oracle.OracleGeneralizedICP(), attempts=4)
+    To, mo, sfo, eo = o.align(src.copy(), tgt.copy())
+    np.random.seed(0)
+    al = Aligner(Preprocessor([]), Preprocessor([]), GeneralizedICP(exact_nn=True), attempts=4)
+    T, m, sf, e = al.align(src.copy(), tgt.copy(), refine_registration=False)
+    assert np.array_equal(sf, sfo) and len(e) == len(eo)
+    assert np.abs(np.asarray(e) - np.asarray(eo)).max() <= 1e-12
+    assert abs(m - mo) <= 1e-12 and np.abs(T - To).max() <= 1e-9
+
+
+def test_exact_multi_target_ordered_dispatch(exact, oracle):
+    """20 starts over two targets in one batch (the ordered dispatch, >= 16
+    starts, as the speculative compass runs): every start is the oracle's."""
+    src, tgt = small_pair(2500, 2200, seed=9)
+    tgt2 = tgt * np.array([0.95, 1.05, 1.0])
+    rng = np.random.default_rng(11)
+    B = 20
+    R0 = np.array([rot_xyz(*rng.uniform(-60, 60, 3)) for _ in range(B)])
+    t0 = rng.normal(size=(B, 3)) * 0.05
+    which = (np.arange(B) % 2).astype(np.int32)
+    exact.set_source(src)
+    exact.set_targets([tgt, tgt2])
+    r = exact.gicp_batch_targets(R0, t0, which)
+    for b in range(0, B, 3):
+        o = oracle.gicp(np.dot(src, R0[b]) + t0[b], [tgt, tgt2][which[b]], 0.5, 100)
+        assert r["iters"][b] == o["iters"], (b, r["iters"][b], o["iters"])
+        assert np.abs(r["T"][b] - o["T"]).max() <= 1e-9 and abs(r["rmse"][b] - o["rmse"]) <= 1e-12
