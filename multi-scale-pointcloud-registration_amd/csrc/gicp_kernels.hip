@@ -1740,7 +1740,13 @@ size_t coop_smem_bytes(int W, int64_t ntiles) { return (size_t)ntiles * 2 + 16; 
 // queries per thread.  A function of N only, so the fixed-order reduction is
 // the same for every batch composition.  Measured at C2: 1 (4x the blocks, 4x
 // the partials for the solve) 18.5 ms per multistart, 2: 17.9, 4: 17.8.
-constexpr __host__ __device__ __forceinline__ int accum_qpt(int64_t) { return 4; }
+// queries per accumulation thread; fixed (not per batch) so that a start's
+// sums never depend on the batch it runs in.  C2 batches of 1/8/30/64 starts:
+// 4: 0.54/4.72/15.07/24.36 ms, 2: 0.53/4.71/15.13/24.37, 1: 0.56/4.83/15.71/25.31
+#ifndef ORPCD_ACCUM_QPT
+#define ORPCD_ACCUM_QPT 4
+#endif
+constexpr __host__ __device__ __forceinline__ int accum_qpt(int64_t) { return ORPCD_ACCUM_QPT; }
 
 template <int Ctrl>
 __device__ __forceinline__ double dpp_f64(double v) {
@@ -2093,8 +2099,7 @@ __device__ __forceinline__ void gicp_block_terms(int slot, int ablk, const doubl
     // and covariance; then the target point and covariance of each match),
     // not three dependent round trips per query; the terms are then added in
     // query order exactly as before.  Loads of a missing match read index 0.
-    constexpr int kQ = 4;
-    static_assert(kQ == accum_qpt(0), "accumulation queries per thread");
+    constexpr int kQ = accum_qpt(0);
     unsigned long long bv[kQ];
     double p[kQ][3], cs[kQ][6], t3[kQ][3], ct[kQ][6];
 #pragma unroll
