@@ -268,3 +268,26 @@ def test_exact_multi_target_ordered_dispatch(exact, oracle):
         o = oracle.gicp(np.dot(src, R0[b]) + t0[b], [tgt, tgt2][which[b]], 0.5, 100)
         assert r["iters"][b] == o["iters"], (b, r["iters"][b], o["iters"])
         assert np.abs(r["T"][b] - o["T"]).max() <= 1e-9 and abs(r["rmse"][b] - o["rmse"]) <= 1e-12
+
+
+def test_exact_tiny_clouds_and_iteration_caps(exact, oracle):
+    """Edge sizes in exact mode: a 2-point source, a 7-point target (one
+    ragged tile), 1 and 3 iterations: the oracle's results to round-off."""
+    src, tgt = small_pair(400, seed=5)
+    for it in (1, 3):
+        exact.set_target(tgt)
+        exact.set_source(src)
+        r = exact.gicp_batch(np.eye(3)[None], np.zeros((1, 3)), max_iteration=it)
+        o = oracle.gicp(src, tgt, 0.5, it)
+        assert r["iters"][0] == o["iters"] == it
+        assert np.abs(r["T"][0] - o["T"]).max() <= 1e-12 and abs(r["rmse"][0] - o["rmse"]) <= 1e-14
+    exact.set_source(src[:2])
+    r = exact.gicp_batch(np.eye(3)[None], np.zeros((1, 3)))
+    o = oracle.gicp(src[:2], tgt, 0.5, 100)
+    assert r["iters"][0] == o["iters"] and np.abs(r["T"][0] - o["T"]).max() <= 1e-9
+    exact.set_target(tgt[:7])
+    exact.set_source(src)
+    r = exact.gicp_batch(np.eye(3)[None], np.zeros((1, 3)), max_iteration=5)
+    o = oracle.gicp(src, tgt[:7], 0.5, 5)
+    assert r["iters"][0] == o["iters"] and np.abs(r["T"][0] - o["T"]).max() <= 1e-9
+    assert abs(r["rmse"][0] - o["rmse"]) <= 1e-12
