@@ -277,6 +277,7 @@ struct orpcd_ctx {
     orpcd::DevBuf<unsigned> xcnt;                // 2: list entries, by pass parity
     orpcd::DevBuf<unsigned long long> xtotal;    // queries re-searched in fp64 (statistics)
     bool exact_live = false;                     // the running batch runs exact
+    int last_B = 0;                              // starts of the last batch (orpcd_gicp_correspondences)
 
     // kernel-level entry points
     orpcd::CloudLayout aux;

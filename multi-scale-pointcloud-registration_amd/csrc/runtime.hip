@@ -386,6 +386,7 @@ int batch_setup(orpcd_ctx* c, const double* R0, const double* t0, int B, const o
                 const double* init16 = nullptr, bool persist = false) {
     const int64_t N = c->src.n;
     const int nblk = accum_blocks(N);
+    c->last_B = 0;  // set once the batch is set up
     if (!init16) CTX_CHECK(c, c->scov.ensure((size_t)B * N * 6));
     CTX_CHECK(c, c->prevnn.ensure((size_t)B * N));
     CTX_CHECK(c, c->best.ensure((size_t)B * N));
@@ -495,6 +496,7 @@ int batch_setup(orpcd_ctx* c, const double* R0, const double* t0, int B, const o
     CTX_CHECK(c, hipMemsetAsync(c->ctl.p, 0, ((size_t)B + 2) * 4, s));
     CTX_CHECK(c, hipMemsetD32Async((hipDeviceptr_t)c->ctl.p, B, 1, s));
 
+    c->last_B = B;
     // posed-frame source covariances for every start (rigid equivariance)
     c->est = init16 ? kEstP2P : kEstGICP;
     if (!init16) CTX_CHECK(c, launch_normals_cov(c->sraw.p, N, c->scratch64c.p, B, p->epsilon, nullptr, c->scov.p, s));
@@ -1541,7 +1543,8 @@ int orpcd_gicp_correspondences(orpcd_ctx* c, int32_t B, int32_t* idx_out) {
     if (!c) return ORPCD_EINVAL;
     CTX_REQUIRE(c, idx_out && B > 0, "gicp_correspondences: bad arguments");
     const int64_t N = c->src.n;
-    CTX_REQUIRE(c, N > 0 && c->prevnn.n >= (size_t)B * N, "gicp_correspondences: no batch of that size ran");
+    CTX_REQUIRE(c, N > 0 && B == c->last_B && c->prevnn.n >= (size_t)B * N,
+                "gicp_correspondences: B must be the last batch's number of starts");
     CTX_REQUIRE(c, c->ntgt == 1, "gicp_correspondences: single-target batches only");
     CTX_CHECK(c, hipSetDevice(c->device));
     CTX_CHECK(c, hipStreamSynchronize(c->stream));
