@@ -354,8 +354,16 @@ struct orpcd_ctx {
                                   // band test + fp64 re-search of the uncertified queries
         int fuse_solve = 0;       // 1: the 6x6 solve runs inside the next pass's query transform launch
                                   // (bit-identical; measured slower at C2: 30 starts 15.05 -> 15.45 ms)
+        int sync_lag = 0;         // 1: the host check of the done flags lags one sync interval: the flags
+                                  // are copied and an event recorded, and the host waits on the PREVIOUS
+                                  // interval's event, so the stream never drains at a check (finished
+                                  // starts' blocks exit as between checks).  Bit-identical; measured equal
+                                  // at C2 (30 starts 15.0 ms either way) and slower for 8 starts (4.61 ->
+                                  // 4.84 ms: up to two intervals of empty passes after the last start
+                                  // converges).  0: drain and check
     } opt;
     std::vector<hipEvent_t> ev_pool;
+    hipEvent_t sync_ev[2] = {nullptr, nullptr};  // lagged done-flag checks (sync_lag)
     orpcd::KernelStats stats;
 
     // row-sharded single start (orpcd_gicp_shard_*)

@@ -444,7 +444,7 @@ int batch_setup(orpcd_ctx* c, const double* R0, const double* t0, int B, const o
     CTX_CHECK(c, c->out_ncorr.ensure((size_t)B));
     CTX_CHECK(c, c->scratch64c.ensure((size_t)B * 9));
     CTX_CHECK(c, c->h64.ensure((size_t)B * 80));
-    CTX_CHECK(c, c->h32.ensure((size_t)B * 4));
+    CTX_CHECK(c, c->h32.ensure((size_t)B * 6));  // [4B, 6B): second active / done lists (sync_lag)
 
     // host: base pose G_b = [R0_b^T | t0_b] (source @ R0 + t0 in column form)
     double* hG = c->h64.p;
@@ -611,6 +611,8 @@ int orpcd_ctx_destroy(orpcd_ctx* c) {
     c->fgr.release();
     c->vox.release();
     for (hipEvent_t e : c->ev_pool) (void)hipEventDestroy(e);
+    for (hipEvent_t e : c->sync_ev)
+        if (e) (void)hipEventDestroy(e);
     (void)hipStreamDestroy(c->stream);
     delete c;
     return ORPCD_OK;
@@ -963,6 +965,87 @@ int run_passes_pipelined(orpcd_ctx* c, int B, const orpcd_gicp_params* p, double
     return ORPCD_OK;
 }
 
+// The pass loop with the host's done-flag check one interval behind
+// (opt.sync_lag).  Every `every` passes the done flags are copied to a pinned
+// buffer and an event is recorded; the host then waits on the PREVIOUS
+// interval's event, compacts the running starts from that snapshot and
+// enqueues the next interval, so the stream always holds an interval of
+// passes and never drains at a check.  Starts that finished since the
+// snapshot stay listed one interval longer; every kernel's blocks exit at
+// once for them (done[]), exactly as between checks of the drained loop, and
+// the answers do not depend on the listed set (bit-identical results).
+// Double buffers: the done snapshots (one per interval in flight) and the
+// active lists (a list is rewritten only after its upload has run: the
+// upload precedes the event the host waits on two checks later).
+int run_passes_lagged(orpcd_ctx* c, int B, const orpcd_gicp_params* p, int every, bool timed) {
+    hipStream_t s = c->stream;
+    const double r2 = p->max_correspondence_distance * p->max_correspondence_distance;
+    int32_t* act[2] = {c->h32.p, c->h32.p + 4 * (size_t)B};
+    int32_t* dn[2] = {c->h32.p + B, c->h32.p + 5 * (size_t)B};
+    for (int g = 0; g < 2; ++g)
+        if (!c->sync_ev[g]) CTX_CHECK(c, hipEventCreateWithFlags(&c->sync_ev[g], hipEventDisableTiming));
+    if (timed) {
+        while ((int)c->ev_pool.size() < 6 * every) {
+            hipEvent_t e;
+            CTX_CHECK(c, hipEventCreateWithFlags(&e, hipEventDisableSystemFence));  // timing only
+            c->ev_pool.push_back(e);
+        }
+    }
+    auto take_timings = [&](int g, int n) -> int {  // interval g's per-pass search events (complete)
+        for (int q = 0; q < n; ++q) {
+            float ms = 0.f;
+            hipEvent_t* ev = &c->ev_pool[3 * (g * every + q)];
+            CTX_CHECK(c, hipEventElapsedTime(&ms, ev[0], ev[1]));
+            c->stats.launches += 1;
+            if (c->sched_live) c->stats.sched_launches += 1;
+            c->stats.ms += ms;
+        }
+        return ORPCD_OK;
+    };
+    int cur = 0, gen = 0, nact = B;
+    int pend[2] = {0, 0};
+    bool inflight = false;  // interval gen ^ 1 awaits its check
+    for (int pass = 0; pass <= p->max_iteration && nact > 0; ++pass) {
+        hipEvent_t* ev = timed ? &c->ev_pool[3 * (gen * every + pend[gen])] : nullptr;
+        if (timed) CTX_CHECK(c, hipEventRecord(ev[0], s));
+        const TgtBounds tb = target_bounds(c, act[cur], nact);
+        CTX_CHECK(c, launch_gicp_pass(c, nact, pass, r2, s, timed ? ev[1] : nullptr, tb));
+        CTX_CHECK(c, launch_gicp_solve(c, nact, pass, *p, s, tb));
+        ++pend[gen];
+        c->stats.passes += nact;
+        if (c->exact_live) c->stats.exact_queries += (double)nact * (double)c->src.n;
+        if ((pass % every) != every - 1 && pass != p->max_iteration) continue;
+        CTX_CHECK(c, hipMemcpyAsync(dn[gen], c->done.p, (size_t)B * 4, hipMemcpyDeviceToHost, s));
+        CTX_CHECK(c, hipEventRecord(c->sync_ev[gen], s));
+        const int o = gen ^ 1;
+        if (inflight) {
+            CTX_CHECK(c, hipEventSynchronize(c->sync_ev[o]));
+            if (timed && take_timings(o, pend[o])) return ORPCD_EDEVICE;
+            pend[o] = 0;
+            int k = 0;
+            for (int b = 0; b < nact; ++b)
+                if (!dn[o][act[cur][b]]) act[cur ^ 1][k++] = act[cur][b];
+            if (k != nact && k > 0) {
+                CTX_CHECK(c, hipMemcpyAsync(c->active.p, act[cur ^ 1], (size_t)k * 4, hipMemcpyHostToDevice, s));
+                cur ^= 1;
+            }
+            nact = k;
+        }
+        inflight = true;
+        gen = o;
+    }
+    CTX_CHECK(c, hipStreamSynchronize(s));
+    if (timed) {
+        if (take_timings(gen ^ 1, pend[gen ^ 1]) || take_timings(gen, pend[gen])) return ORPCD_EDEVICE;
+    }
+    if (c->exact_live) {  // entries re-searched over the batch (nn_exact_kernel adds each pass's count)
+        unsigned long long tot = 0;
+        CTX_CHECK(c, hipMemcpy(&tot, c->xtotal.p, 8, hipMemcpyDeviceToHost));
+        c->stats.exact_filed += (double)tot;
+    }
+    return ORPCD_OK;
+}
+
 // The ICP loop of every start of the batch set up by batch_setup (GICP or
 // PointToPoint by c->est).  GICP outputs T (the ICP transform relative to the
 // posed source); PointToPoint outputs T * G (registration_icp's result, init
@@ -994,6 +1077,11 @@ int run_passes(orpcd_ctx* c, int B, const orpcd_gicp_params* p, double* T_out, d
             CTX_CHECK(c, hipEventCreateWithFlags(&e, hipEventDisableSystemFence));  // timing only: no cache writeback per record
             c->ev_pool.push_back(e);
         }
+    }
+    if (!trace && !c->fuse_live && c->opt.sync_lag) {
+        const int rc = run_passes_lagged(c, B, p, every, timed);
+        if (rc) return rc;
+        return read_outputs(c, B, tiles_before, T_out, rmse_out, fitness_out, iters_out, ncorr_out);
     }
     int pending = 0;  // timed passes since the last host sync
     for (int pass = 0; pass <= p->max_iteration && nact > 0; ++pass) {
@@ -1531,6 +1619,7 @@ int orpcd_set_option(orpcd_ctx* c, const char* key, double value) {
     else if (k == "sched_items" && v >= 64 && v <= (1 << 22)) c->opt.sched_items = v;
     else if (k == "sched_min_starts" && v >= 1) c->opt.sched_min_starts = v;
     else if (k == "fuse_solve" && (v == 0 || v == 1)) c->opt.fuse_solve = v;
+    else if (k == "sync_lag" && (v == 0 || v == 1)) c->opt.sync_lag = v;
     else if (k == "exact_nn" && (v == 0 || v == 1)) c->opt.exact_nn = v;
     else {
         c->err = "set_option: unknown key or bad value: " + k;

@@ -265,6 +265,50 @@ def test_pipelined_passes_identical(ctx, lookahead):
             assert np.array_equal(g[k], r[k]), k
 
 
+@pytest.mark.parametrize("every", [1, 3, 8])
+def test_lagged_sync_identical(ctx, every):
+    """Done-flag checks one interval behind (sync_lag: the stream never drains at
+    a check; finished starts stay listed one interval longer) against the drained
+    loop: bit-identical T, rmse, fitness, iterations and correspondences for 70
+    starts finishing at many passes, a batch cut by max_iteration, an exact_nn
+    batch and PointToPoint refinement."""
+    src, tgt = small_pair(3000, 2800, seed=23)
+    rng = np.random.default_rng(6)
+    R0 = np.array([rot_xyz(*rng.uniform(-90, 90, 3)) for _ in range(70)])
+    t0 = rng.normal(size=(70, 3)) * 0.1
+    inits = np.repeat(np.eye(4)[None], 5, axis=0)
+    inits[:, :3, 3] = rng.normal(size=(5, 3)) * 0.02
+
+    def run(lag):
+        ctx.set_option("sync_lag", lag)
+        ctx.set_option("sync_every", every)
+        ctx.set_target(tgt)
+        ctx.set_source(src)
+        out = [ctx.gicp_batch(R0, t0), ctx.gicp_batch(R0[:9], t0[:9], max_iteration=7)]
+        ctx.set_option("exact_nn", 1)
+        out.append(ctx.gicp_batch(R0[:12], t0[:12]))
+        idx = ctx.gicp_correspondences(12, len(src))
+        ctx.set_option("exact_nn", 0)
+        ctx.set_target_points(tgt)
+        ctx.set_source_points(src)
+        out.append(ctx.icp_p2p_batch(inits, max_iteration=30))
+        return out, idx
+
+    try:
+        got, gidx = run(1)
+        ref, ridx = run(0)
+    finally:
+        ctx.set_option("sync_lag", 0)
+        ctx.set_option("sync_every", 8)
+        ctx.set_option("exact_nn", 0)
+    assert len(set(got[0]["iters"].tolist())) > 5
+    assert (got[1]["iters"] == 7).any()
+    assert np.array_equal(gidx, ridx)
+    for g, r in zip(got, ref):
+        for k in ("T", "rmse", "fitness", "iters"):
+            assert np.array_equal(g[k], r[k]), k
+
+
 @pytest.mark.parametrize("items", [0, 1, 100000])
 def test_persistent_loop_identical(ctx, items):
     """The persistent pass loop (option persist: every pass of every start in
