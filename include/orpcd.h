@@ -237,7 +237,27 @@ int orpcd_fgr_optimize(orpcd_ctx* ctx, const double* src, int64_t n, const doubl
  *   "search_kernel" 0: split search (default); 1: one workgroup per query
  *                   group; 2: cull once per group + persistent scan.  All
  *                   three return identical correspondences.
- *   "scan_blocks"   persistent grid of search_kernel 2                    */
+ *   "scan_blocks"   persistent grid of search_kernel 2
+ *   "small_batch"   at most this many running starts: half the search_waves
+ *                   target
+ *   "sched"         0/1: search waves dispatched heaviest first by the
+ *                   previous pass's measured cost (ordered dispatch)
+ *   "sched_items", "sched_min_starts"  its split granularity, and the batch
+ *                   size from which it is used
+ *   "seed_reps"     pass-0 search bound: nearest of ~this many tile
+ *                   representatives per query
+ *   "exact_nn"      0/1: every correspondence is the fp64 nearest target
+ *                   (the oracle's lexicographic (d^2, input index) minimum)
+ *   "pipeline", "lookahead"  passes enqueued ahead with the solve fused into
+ *                   the accumulation and the running starts kept on device
+ *   "persist", "persist_items", "persist_timeout_s", "persist_fences"
+ *                   the whole ICP loop in one persistent launch
+ *   "fuse_solve"    0/1: the 6x6 solve inside the next pass's query transform
+ *   "sync_lag"      0/1: host checks of the done flags one interval behind
+ *                   (the stream never drains at a check)
+ * Apart from exact_nn, every knob returns bit-identical results; only the
+ * speed differs.
+ * An unknown key or a value out of range returns ORPCD_EINVAL.            */
 int orpcd_set_option(orpcd_ctx* ctx, const char* key, double value);
 
 /* Test entry: n 6x6 systems (per system 27 doubles: the JTJ upper triangle
