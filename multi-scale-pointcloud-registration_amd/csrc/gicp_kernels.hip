@@ -2183,8 +2183,15 @@ __device__ __forceinline__ void gicp_block_terms(int slot, int ablk, const doubl
     }
 }
 
+// ORPCD_ACCUM_WAVES: a register budget for the accumulation (A/B builds); unset,
+// the compiler's choice (214 VGPRs, 2 waves/SIMD)
+#ifdef ORPCD_ACCUM_WAVES
+#define ORPCD_ACCUM_ATTR __attribute__((amdgpu_waves_per_eu(ORPCD_ACCUM_WAVES, 8)))
+#else
+#define ORPCD_ACCUM_ATTR
+#endif
 template <bool kFused>
-__global__ __launch_bounds__(256) void gicp_accum_kernel(
+__global__ __launch_bounds__(256) ORPCD_ACCUM_ATTR void gicp_accum_kernel(
     const double* __restrict__ src, const double* __restrict__ scov, int N, const TargetDesc* __restrict__ tdesc,
     TgtBounds tb, const int32_t* __restrict__ active, const double* __restrict__ Qm,
     const double* __restrict__ Rm, const int32_t* __restrict__ done, double r2,
