@@ -46,6 +46,14 @@
 #include "orpcd_internal.h"
 #include "wave_ops.h"
 
+// Issue priority of a search wave outside its tile scans (s_setprio): the
+// culling chain (dependent box loads, ballots) outranks the VALU-heavy scans
+// of the other waves on its SIMD.  3 measured: 8 starts 4.63 -> 4.50 ms, 64
+// starts 24.45 -> 24.02 ms, 1 / 16 / 30 starts equal; bit-identical.  0: off.
+#ifndef ORPCD_CULL_PRIO
+#define ORPCD_CULL_PRIO 3
+#endif
+
 namespace orpcd {
 
 typedef float f2 __attribute__((ext_vector_type(2)));
@@ -211,6 +219,9 @@ __device__ __forceinline__ int culled_search(float4* stage, const float4* __rest
                                              unsigned* sk = nullptr) {
     constexpr int kScanUnroll = kExact ? ORPCD_SCAN_UNROLL_EXACT : ORPCD_SCAN_UNROLL_FAST;
     const int lane = threadIdx.x & 63;
+#if ORPCD_CULL_PRIO > 0
+    __builtin_amdgcn_s_setprio(ORPCD_CULL_PRIO);  // culling at raised issue priority
+#endif
     const bool v0 = bound[0] > 0.0f, v1 = bound[1] > 0.0f;
     unsigned k0 = v0 ? __float_as_uint(bound[0]) : 0u;  // best key (0: never improves)
     unsigned k1 = v1 ? __float_as_uint(bound[1]) : 0u;
@@ -408,6 +419,9 @@ __device__ __forceinline__ int culled_search(float4* stage, const float4* __rest
             pre = p4[nxt * kTile + lane];
             if (lane < 8) preq = qbox[nxt * 8 + lane];
         }
+#if ORPCD_CULL_PRIO > 0
+        __builtin_amdgcn_s_setprio(0);  // the scan yields issue slots to waves in their culling chain
+#endif
         // exact: the running minimum of the whole search (from k0), else of this tile
         unsigned m0 = kExact ? k0 : 0xFFFFFFFFu, m1 = kExact ? k1 : 0xFFFFFFFFu;
         const f2 qx0 = {qx[0], qx[0]}, qy0 = {qy[0], qy[0]}, qz0 = {qz[0], qz[0]};
@@ -462,6 +476,9 @@ __device__ __forceinline__ int culled_search(float4* stage, const float4* __rest
             }
         }
         asm volatile("" ::: "memory");  // all reads of this tile precede the next stage write
+#if ORPCD_CULL_PRIO > 0
+        __builtin_amdgcn_s_setprio(ORPCD_CULL_PRIO);
+#endif
         // a tile improves a query only if its masked d^2 is strictly smaller
 #ifdef ORPCD_PHASES
         ph_impr += __any((m0 & kKeyMask) < (k0 & kKeyMask) || (m1 & kKeyMask) < (k1 & kKeyMask)) ? 1 : 0;
