@@ -18,10 +18,16 @@ scaling: the multistart is partitioned into independent starts; the only
 collective is that all-gather).
 
 value = GICP iterations completed (all starts, all ranks) / max-over-ranks
-wall time of the K timed steps.  Also reported: the dominant kernel's
-roofline (live hipEvent timing inside the library on its own stream), a CPU
-baseline (the oracle: C++/OpenMP KD-tree GICP on the host cores, bounded
-sample of the same starts), and one full Aligner.align() wall-clock on rank 0.
+wall time of the K timed steps, in the default (exact) correspondence mode:
+every correspondence is the fp64 KD-tree answer Open3D would return
+(GeneralizedICP(exact_nn=True)), so each start's trajectory is
+the oracle's.  Also reported (rank 0, N=1): the dominant kernel's roofline
+(live hipEvent timing inside the library on its own stream), the same steps
+with every cloud re-uploaded (setup-inclusive rate) and in the fp32-answer
+mode (exact_nn=False), a CPU baseline (the oracle: C++/OpenMP KD-tree GICP on
+the host cores, bounded sample of the same starts) with per-start parity, and
+one full Aligner.align() wall-clock compared with the committed complete
+oracle align() (tests/golden/g7_align_c2.npz).
 """
 import argparse
 import json
@@ -35,7 +41,7 @@ REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(REPO, "multi-scale-pointcloud-registration_amd"))
 sys.path.insert(0, REPO)
 
-FP32_PEAK_TFLOPS = 157.3    # MI355X FP32 (vector == matrix rate), MI355X_MICROARCH.md
+FP32_PEAK_TFLOPS = 157.3    # MI355X FP32 VALU (packed v_pk_* math), MI355X_MICROARCH.md
 FLOP_PER_PAIR = 8           # 3 sub + 3 mul/fma(=5) per query-target distance
 
 
@@ -85,14 +91,16 @@ def main():
             torch.cuda.synchronize()
             dist.barrier()
 
-    def step(k):
+    def step(k, al=aligner):
         np.random.seed(1000 + k)  # identical draws on every rank
-        aligner.multistart_registration(source, target)
-        return aligner.history[-1]["iters"]
+        al.multistart_registration(source, target)
+        return al.history[-1]["iters"]
 
     for k in range(args.warmup):
         step(k)
-    rmse_step0 = np.array(aligner.history[0]["rmse"]) if args.warmup > 0 else None  # seed 1000's starts
+    h0 = aligner.history[0] if args.warmup > 0 else None  # seed 1000's starts
+    rmse_step0 = np.array(h0["rmse"]) if h0 else None
+    iters_step0 = np.array(h0["iters_per_start"]) if h0 and "iters_per_start" in h0 else None
     ctx.reset_stats()
     ctx.profiling(True)
     barrier()
@@ -127,22 +135,26 @@ def main():
     cpu = None
     align_s = None
     parity = None
-    exact = None
+    fast = None
+    setup = None
     if rank == 0 and world == 1:
+        setup = setup_inclusive_run(ctx, step, args)
+        o = o_iters = None
         if args.cpu_seconds > 0:
             cpu = cpu_baseline(source, target, args)
-            # "final RMSE vs ref": the GPU's per-start inlier RMSE of step 0 against the
-            # oracle's on the same starts (stated full-size tolerance 1e-5)
+            # "final RMSE vs ref" per start: the GPU's inlier RMSE of step 0 against the
+            # oracle's on the same starts (exact mode: identical iterations, |d rmse| ~1e-13)
             o = np.array(cpu.pop("oracle_rmse"))
             o_iters = np.array(cpu.pop("oracle_iters"))
-            if len(o):
-                exact = exact_mode_run(source, target, args, local_rank, o, o_iters)
             if rmse_step0 is not None and len(o):
                 d = np.abs(rmse_step0[: len(o)] - o)
                 parity = {"starts": int(len(o)), "max_abs_d_rmse": float(d.max()),
-                          "within_1e-5": int((d <= 1e-5).sum()),
+                          "within_1e-9": int((d <= 1e-9).sum()),
                           "multistart_min_rmse_gpu": float(rmse_step0[: len(o)].min()),
                           "multistart_min_rmse_oracle": float(o.min())}
+                if iters_step0 is not None:
+                    parity["iterations_identical"] = int((iters_step0[: len(o)] == o_iters).sum())
+        fast = fast_mode_run(source, target, args, local_rank, o, o_iters)
         if args.align:
             # one cold align() (device contexts of the speculative compass created
             # inside it), then the same align() warm: the figure reported
@@ -157,10 +169,7 @@ def main():
                            scale_factors=[round(float(x), 6) for x in sf.ravel()],
                            multistarts=len(al.history), gicp_iters=int(sum(h["iters"] for h in al.history)),
                            speculative_extra_multistarts=len(al.speculative_history))
-            if cpu:  # the CPU oracle at its measured GICP rate over the same iterations (an estimate: a full
-                # CPU align() of ~25k GICP iterations takes minutes; labelled as such)
-                align_s["cpu_estimated_seconds"] = round(align_s["gicp_iters"] / cpu["value"], 1)
-                align_s["speedup_vs_cpu_estimate"] = round(align_s["cpu_estimated_seconds"] / align_s["seconds"], 1)
+            align_s.update(align_vs_fixture(T, metric, sf, errors, align_s["seconds"]))
 
     if rank == 0:
         line = {
@@ -180,7 +189,7 @@ def main():
                        "points": args.points, "attempts_per_step": total_attempts,
                        "attempts_per_gpu": args.attempts,
                        "parallelism": f"multistart starts sharded over {world} GPU(s), one all-gather per step"},
-            "roofline": {"bound": "mfma", "achieved": round(achieved, 3), "peak": FP32_PEAK_TFLOPS,
+            "roofline": {"bound": "valu_fp32", "achieved": round(achieved, 3), "peak": FP32_PEAK_TFLOPS,
                          "unit": "TFLOP/s", "frac": round(achieved / FP32_PEAK_TFLOPS, 4), "traffic": traffic,
                          "traffic_source": traffic_src,
                          "kernel": kname, "avg_launch_ms": round(avg_ms, 4),
@@ -196,7 +205,8 @@ def main():
                              / (avg_ms * 1e-3) / 1e12, 1) if avg_ms > 0 else None},
             "cpu_baseline": cpu,
             "parity_vs_oracle": parity,
-            "exact_nn": exact,
+            "setup_inclusive": setup,
+            "fast_mode": fast,
             "gicp_iterations": int(iters),
             "align": align_s,
         }
@@ -205,20 +215,34 @@ def main():
         dist.destroy_process_group()
 
 
-def exact_mode_run(source, target, args, device, oracle_rmse, oracle_iters):
-    """The same steps with GeneralizedICP(exact_nn=True): every correspondence the
-    oracle's (fp64 KD-tree answer).  Its rate, and step 0's starts
-    against the oracle: per start the RMSE difference and the iteration counts."""
+def setup_inclusive_run(ctx, step, args):
+    """The timed steps again with both clouds re-uploaded before every step
+    (host float64 -> HBM, Morton layout, tile boxes, KNN-20 covariances): the
+    rate a caller sees when every multistart brings new clouds.  `value`
+    keeps the clouds resident, as the Aligner does within one align()."""
+    k = max(1, args.steps // 2)
+    t0 = time.perf_counter()
+    iters = 0
+    for j in range(k):
+        ctx._target_key = ctx._source_key = None  # forget the content-hash cache: upload again
+        iters += step(args.warmup + j)
+    el = time.perf_counter() - t0
+    return {"value": round(iters / el, 3), "unit": "GICP iterations/s", "ms_per_step": round(el / k * 1e3, 3),
+            "steps": k, "note": "source and target uploaded, laid out and covariances recomputed every step"}
+
+
+def fast_mode_run(source, target, args, device, oracle_rmse, oracle_iters):
+    """The same steps with GeneralizedICP(exact_nn=False): the fp32 search's
+    answer (near-ties within 2^-17 relative resolved by Morton position, not
+    the KD-tree's fp64 order).  Its rate, and step 0's starts against the
+    oracle (stated tolerance of this mode: converged RMSE within 1e-5)."""
     from orpcd_amd import Aligner, GeneralizedICP, Preprocessor
 
-    opt = GeneralizedICP(device=device, exact_nn=True)
-    ctx = opt.context
+    opt = GeneralizedICP(device=device, exact_nn=False)
     al = Aligner(Preprocessor([]), Preprocessor([]), opt, attempts=args.attempts)
     np.random.seed(1000)
     al.multistart_registration(source, target)  # step 0 (warm-up and parity)
     r0 = np.array(al.history[-1]["rmse"])
-    it0 = np.array(al.history[-1]["iters_per_start"]) if "iters_per_start" in al.history[-1] else None
-    ctx.reset_stats()
     t0 = time.perf_counter()
     iters = 0
     for k in range(args.steps):
@@ -226,16 +250,36 @@ def exact_mode_run(source, target, args, device, oracle_rmse, oracle_iters):
         al.multistart_registration(source, target)
         iters += al.history[-1]["iters"]
     el = time.perf_counter() - t0
-    st = ctx.stats()
-    n = len(oracle_rmse)
-    d = np.abs(r0[:n] - oracle_rmse)
     out = {"value": round(iters / el, 3), "unit": "GICP iterations/s", "ms_per_step": round(el / args.steps * 1e3, 3),
-           "steps": args.steps, "gicp_iterations": int(iters),
-           "requeried_fraction": round(st["exact_filed"] / max(st["exact_queries"], 1), 5),
-           "parity_vs_oracle": {"starts": int(n), "max_abs_d_rmse": float(d.max()),
-                                "within_1e-9": int((d <= 1e-9).sum())}}
-    if it0 is not None:
-        out["parity_vs_oracle"]["iterations_identical"] = int((it0[:n] == oracle_iters).sum())
+           "steps": args.steps, "gicp_iterations": int(iters)}
+    if oracle_rmse is not None and len(oracle_rmse):
+        n = len(oracle_rmse)
+        d = np.abs(r0[:n] - oracle_rmse)
+        out["parity_vs_oracle"] = {"starts": int(n), "max_abs_d_rmse": float(d.max()),
+                                   "within_1e-5": int((d <= 1e-5).sum())}
+    GeneralizedICP(device=device).context  # the shared context back in the default (exact) mode
+    return out
+
+
+def align_vs_fixture(T, metric, sf, errors, gpu_seconds):
+    """The GPU align() against the committed COMPLETE CPU-oracle align() at C2
+    (tests/golden/g7_align_c2.npz, made by tests/golden/make_golden_align.py:
+    every optimize call on the oracle, same inputs and RNG stream)."""
+    path = os.path.join(REPO, "tests", "golden", "g7_align_c2.npz")
+    if not os.path.exists(path):
+        return {"parity_vs_oracle": None}
+    z = np.load(path)
+    meta = json.load(open(path.replace(".npz", ".json")))
+    e = np.asarray(errors, dtype=np.float64)
+    out = {"parity_vs_oracle": {
+        "scale_factors_identical": bool(np.array_equal(np.asarray(sf).reshape(1, 3), z["sf"])),
+        "d_rmse": abs(float(metric) - float(z["metric"])), "max_abs_dT": float(np.abs(np.asarray(T) - z["T"]).max()),
+        "compass_errors_max_abs_diff": float(np.abs(e - z["errors"]).max()) if len(e) == len(z["errors"]) else None,
+        "oracle_rmse": float(z["metric"]), "fixture": "tests/golden/g7_align_c2.npz"},
+        "cpu_seconds_measured": {"value": meta["seconds"], "cores": meta["cores"],
+                                 "where": "the complete oracle align() run that made the fixture (builder container)",
+                                 "r02_gpu_box_seconds": 252.6}}
+    out["speedup_vs_cpu_measured"] = round(meta["seconds"] / gpu_seconds, 1)
     return out
 
 
@@ -261,6 +305,8 @@ def cpu_baseline(source, target, args):
     sys.path.insert(0, os.path.join(REPO, "oracle"))
     import oracle as O
 
+    cores = len(os.sched_getaffinity(0))  # the host cores this process may run on (all of them)
+    O.set_num_threads(cores)
     np.random.seed(1000)
     al = O.OracleAligner(None, attempts=args.attempts)
     starts = [al.initialize_rotation() for _ in range(args.attempts)]
@@ -280,9 +326,21 @@ def cpu_baseline(source, target, args):
     return {"oracle_rmse": oracle_rmse, "oracle_iters": oracle_iters, "value": round(iters / el, 3),
             "unit": "GICP iterations/s",
             "cores": O.num_threads(),
+            "cpu_model": cpu_model(),
             "kind": "port",
             "sample": f"{done} of {args.attempts} starts of step 0 (same R0,t0), {iters} GICP iterations, "
-                      f"{el:.1f} s, {os.cpu_count()} host cpus visible"}
+                      f"{el:.1f} s; OpenMP threads = the {cores} cores of this process's affinity mask "
+                      f"({os.cpu_count()} host cpus visible)"}
+
+
+def cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return None
 
 
 if __name__ == "__main__":

@@ -109,7 +109,7 @@ int orpcd_gicp_batch(orpcd_ctx* ctx, const double* R0, const double* t0, int32_t
 /* Several targets per batch: the six scale candidates of one compass
  * iteration (Aligner.py:263-298, each compass_step scaling the target,
  * :221-222) as ONE device batch instead of six.  orpcd_set_targets uploads
- * ntargets (<= 8) clouds, xyz = their rows concatenated, m[k] rows each;
+ * ntargets (<= 16) clouds, xyz = their rows concatenated, m[k] rows each;
  * orpcd_gicp_batch_targets runs start b against target target_of_start[b]
  * (outputs in start order, as orpcd_gicp_batch).  orpcd_set_target is the
  * one-target case; orpcd_gicp_batch = every start against target 0.         */
@@ -231,13 +231,8 @@ int orpcd_fgr_optimize(orpcd_ctx* ctx, const double* src, int64_t n, const doubl
  *   "search_waves"  split a start's tiles over waves until ~this many run
  *   "sync_every"    passes between host checks of the per-start done flags
  *   "super_cull"    0/1: first culling level over 64-tile super-tiles
- *   "search_occupancy" 0 or 6: register budget of the search kernel
  *   "reseed"        0/1: representative seeding for queries that found no
  *                   target within radius in the previous pass
- *   "search_kernel" 0: split search (default); 1: one workgroup per query
- *                   group; 2: cull once per group + persistent scan.  All
- *                   three return identical correspondences.
- *   "scan_blocks"   persistent grid of search_kernel 2
  *   "small_batch"   at most this many running starts: half the search_waves
  *                   target
  *   "sched"         0/1: search waves dispatched heaviest first by the
@@ -246,15 +241,11 @@ int orpcd_fgr_optimize(orpcd_ctx* ctx, const double* src, int64_t n, const doubl
  *                   size from which it is used
  *   "seed_reps"     pass-0 search bound: nearest of ~this many tile
  *                   representatives per query
- *   "exact_nn"      0/1: every correspondence is the fp64 nearest target
- *                   (the oracle's lexicographic (d^2, input index) minimum)
- *   "pipeline", "lookahead"  passes enqueued ahead with the solve fused into
- *                   the accumulation and the running starts kept on device
- *   "persist", "persist_items", "persist_timeout_s", "persist_fences"
- *                   the whole ICP loop in one persistent launch
- *   "fuse_solve"    0/1: the 6x6 solve inside the next pass's query transform
- *   "sync_lag"      0/1: host checks of the done flags one interval behind
- *                   (the stream never drains at a check)
+ *   "exact_nn"      1 (default): every correspondence is the fp64 nearest
+ *                   target (the oracle's lexicographic (d^2, input index)
+ *                   minimum, i.e. Open3D's KD-tree answer); 0: the fp32
+ *                   search's answer (candidates within 2^-17 relative in d^2
+ *                   resolved by Morton position)
  * Apart from exact_nn, every knob returns bit-identical results; only the
  * speed differs.
  * An unknown key or a value out of range returns ORPCD_EINVAL.            */
@@ -268,7 +259,8 @@ int orpcd_set_option(orpcd_ctx* ctx, const char* key, double value);
 int orpcd_test_solve6(orpcd_ctx* ctx, const double* sums27, int32_t n, double* out_serial, double* out_wave);
 
 /* Test entry: the correspondences of the last pass of each start of the last
- * single-target batch (orpcd_gicp_batch / orpcd_icp_p2p_batch):
+ * batch (orpcd_gicp_batch / orpcd_gicp_batch_targets / orpcd_icp_p2p_batch;
+ * for a multi-target batch, b indexes the starts in the caller's order):
  * idx_out[b * N + i] = input index of the nearest target of source point i
  * (input order) in start b's final pass, -1 when none lay inside the search
  * radius (before the strict fp64 d^2 < r^2 test of the accumulation).  With
@@ -293,7 +285,9 @@ int orpcd_rng_draw_attempts(uint32_t* key, int32_t* pos, int32_t* has_gauss, dou
  * passes (start x pass), [5] = 64-point target tiles scanned, [6] = total
  * ms of the fp64 accumulation kernel, [7] = how many of the timed launches
  * ran the ordered-dispatch search (nn_search_sched_kernel; the rest ran
- * nn_search_kernel).  [1] times the search kernel only.                    */
+ * nn_search_kernel), [8] = queries re-searched in fp64 (exact_nn), [9] =
+ * queries searched while exact_nn was on.  [1] times the search kernel (and,
+ * in exact mode, the fp64 re-search that follows it) only.                 */
 int orpcd_profiling(orpcd_ctx* ctx, int32_t enable);
 int orpcd_stats(orpcd_ctx* ctx, double* stats_out, int32_t n);
 int orpcd_reset_stats(orpcd_ctx* ctx);

@@ -39,7 +39,6 @@
 //    queries of the next pass (fp64 transform, one rounding).
 #include <cstdio>
 #include <cstdlib>
-#include <type_traits>
 #include <vector>
 
 #include "device_math.h"
@@ -95,39 +94,6 @@ constexpr int kNoSeed = -1;   // prevnn before the first pass (representative se
 constexpr int kNoMatch = -2;  // no target within the search radius last pass
 constexpr unsigned kKeyMask = 0xFFFFFFC0u;  // d^2 bits kept in a scan key (low 6 = tile-local index)
 constexpr float kQuarterSlack = 1.0f - 1.0f / 1048576.0f;  // quarter test: box d^2 x (1 - 2^-20) vs the bound
-
-// Accesses of state that another workgroup publishes inside the SAME launch
-// (the persistent pass loop): relaxed agent-scope atomics (global sc1
-// loads / stores), ordered by the release / acquire hand-offs around them.
-// kAt = false: plain accesses (the data was written before a kernel boundary).
-template <bool kAt>
-__device__ __forceinline__ unsigned long long ld_u64(const unsigned long long* p) {
-    if constexpr (kAt) return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    else return *p;
-}
-template <bool kAt>
-__device__ __forceinline__ void st_u64(unsigned long long* p, unsigned long long v) {
-    if constexpr (kAt) __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    else *p = v;
-}
-template <bool kAt>
-__device__ __forceinline__ double ld_f64(const double* p) {
-    return __longlong_as_double((long long)ld_u64<kAt>(reinterpret_cast<const unsigned long long*>(p)));
-}
-template <bool kAt>
-__device__ __forceinline__ void st_f64(double* p, double v) {
-    st_u64<kAt>(reinterpret_cast<unsigned long long*>(p), (unsigned long long)__double_as_longlong(v));
-}
-template <bool kAt>
-__device__ __forceinline__ int ld_i32(const int32_t* p) {
-    if constexpr (kAt) return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    else return *p;
-}
-template <bool kAt>
-__device__ __forceinline__ void st_i32(int32_t* p, int v) {
-    if constexpr (kAt) __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    else *p = v;
-}
 
 // A load through a pointer the compiler cannot prove global (one read from a
 // TargetDesc): as a global load, not a flat one -- flat loads count against
@@ -615,8 +581,7 @@ struct SchedS {                          // search side (pass p)
 
 // The ordered dispatch's work items of start `slot` (one block per start,
 // launched beside the query transform's blocks).
-template <class Gate = bool (*)()>
-__device__ __forceinline__ void plan_start_items(const SchedX& sx, int slot, int tk, Gate gate = nullptr) {
+__device__ __forceinline__ void plan_start_items(const SchedX& sx, int slot, int tk) {
     const int lane = threadIdx.x & 63;
     // The items depend only on the previous pass's costs, so this block runs
     // beside the transform blocks (as the sequel of one of them it lengthened
@@ -654,9 +619,6 @@ __device__ __forceinline__ void plan_start_items(const SchedX& sx, int slot, int
         atomicAdd(lcnt + cls, (unsigned)S);
     }
     __syncthreads();
-    if constexpr (!std::is_same<Gate, bool (*)()>::value) {
-        if (!gate()) return;  // fused solve: the start finished in this pass's solve: no items
-    }
     if (threadIdx.x < kSchedClasses) {
         const unsigned n = lcnt[threadIdx.x];
         lbase[threadIdx.x] = n ? atomicAdd(sx.cnt + threadIdx.x, n) : 0u;
@@ -708,9 +670,7 @@ __global__ __launch_bounds__(256) void xform_queries_kernel(const double* __rest
                                                             const int32_t* __restrict__ prevnn,
                                                             float r2s, int reseed, float4* __restrict__ q32,
                                                             unsigned long long* __restrict__ best,
-                                                            const int32_t* __restrict__ nact_dev,
                                                             float4* __restrict__ gbox, SchedX sx, ExactArgs ex) {
-    if (nact_dev && (int)blockIdx.y >= *nact_dev) return;  // pipelined: grid sized for an upper bound
     const int slot = active[blockIdx.y];
     if (done[slot]) return;
     const int tk = target_of_row(tb, blockIdx.y);
@@ -1015,59 +975,20 @@ __global__ __launch_bounds__(kCBlock) __attribute__((amdgpu_waves_per_eu(kExact 
     }
 }
 
-#define ORPCD_NN_SEARCH_ARGS                                                                                   \
-    const float4 *__restrict__ q32, int N, const TargetDesc *__restrict__ tdesc, TgtBounds tb, int super_cull,  \
-        const int32_t *__restrict__ active, const int32_t *__restrict__ done, int S,                          \
-        unsigned long long *__restrict__ best, unsigned long long *__restrict__ counters,                       \
-        const int32_t *__restrict__ nact_dev, int sblk, int want, const float4 *__restrict__ gbox, ExactArgs ex
-
-// Block -> (start, query group x split).  Unpipelined: the grid is
-// (sblk * S, running starts) as the host counted them.  Pipelined (nact_dev):
-// a 1-D grid sized for an upper bound of the running starts; the device's
-// count sets the splits, S = ceil(want / (nact * sblk * waves)) capped at 64
-// and at what the grid holds, and the surplus blocks exit.
-__device__ __forceinline__ bool map_search_block(const int32_t* __restrict__ nact_dev, int sblk, int want, int& by,
-                                                 int& bx, int& S) {
-    if (!nact_dev) {
-        by = blockIdx.y;
-        bx = blockIdx.x;
-        return true;
-    }
-    const int nact = *nact_dev;
-    if (nact <= 0) return false;
-    const int per = nact * sblk;
-    const int waves = per * kCWaves;
-    S = min(min(64, max(1, (int)gridDim.x / per)), max(1, (want + waves - 1) / waves));
-    const int b = blockIdx.x;
-    if (b >= per * S) return false;
-    by = b / (sblk * S);
-    bx = b - by * (sblk * S);
-    return true;
-}
-
-// Two register budgets of the same search (orpcd_set_option "search_occupancy"):
-// the compiler's choice (5 waves/SIMD) and a cap at 6 waves/SIMD.
+// Uniform-split search: grid = (sblk * S, running starts), 4 waves/block;
+// block (bx, by) is split bx % S of query block bx / S of launch row by.
 template <bool kExact>
 __global__ __launch_bounds__(kCBlock) __attribute__((amdgpu_waves_per_eu(kExact ? ORPCD_EXACT_WAVES : 5, 8))) void nn_search_kernel(
-    ORPCD_NN_SEARCH_ARGS) {
+    const float4* __restrict__ q32, int N, const TargetDesc* __restrict__ tdesc, TgtBounds tb, int super_cull,
+    const int32_t* __restrict__ active, const int32_t* __restrict__ done, int S, unsigned long long* __restrict__ best,
+    unsigned long long* __restrict__ counters, const float4* __restrict__ gbox, ExactArgs ex) {
     __shared__ float4 stage[kCWaves][kTile];
     const int wid = threadIdx.x >> 6;
-    int by, bx;
-    if (!map_search_block(nact_dev, sblk, want, by, bx, S)) return;
+    const int by = blockIdx.y, bx = blockIdx.x;
     const int tk = target_of_row(tb, by);
     nn_search_body<kExact>(q32, N, tdesc[tk], super_cull, active, done, S, best, counters, by, bx, wid, stage[wid],
                            gbox, ex, tk);
 }
-__global__ __launch_bounds__(kCBlock) __attribute__((amdgpu_waves_per_eu(6, 8))) void nn_search_kernel_o6(
-    ORPCD_NN_SEARCH_ARGS) {
-    __shared__ float4 stage[kCWaves][kTile];
-    const int wid = threadIdx.x >> 6;
-    int by, bx;
-    if (!map_search_block(nact_dev, sblk, want, by, bx, S)) return;
-    nn_search_body(q32, N, tdesc[target_of_row(tb, by)], super_cull, active, done, S, best, counters, by, bx, wid,
-                   stage[wid], gbox);
-}
-#undef ORPCD_NN_SEARCH_ARGS
 
 // --------------------------------------------------------------------------
 // Exact mode, second stage (one wave per 64 queries of a running start, after
@@ -1225,527 +1146,6 @@ __global__ __launch_bounds__(256) void nn_exact_kernel(const double* __restrict_
     }
 }
 
-// --------------------------------------------------------------------------
-// Cooperative search (default): one workgroup of W waves per group of 128
-// Morton-consecutive queries of one start.  The queries are transformed here
-// (fp64 pose -> fp32, bound from the previous correspondence; no separate
-// query kernel), the group's candidate tiles are culled ONCE (the waves split
-// the super-tiles; tiles whose box is within the group's worst bound are
-// appended to an LDS list), then the waves pull tiles from the list (LDS
-// cursor) and scan them; per query the waves' results merge by an LDS 64-bit
-// min on (masked d^2, Morton index) and one plain store writes best[].  The
-// answer is the same as nn_search_kernel's: among candidates whose d^2 agree
-// in the top 26 bits the lowest Morton index wins.
-// --------------------------------------------------------------------------
-constexpr int kGroupQ = 64 * kCQPT;  // queries per group (2 per lane)
-constexpr int kCoopMaxW = 16;        // waves per workgroup at most
-
-struct CoopShared {
-    float4 q[kGroupQ];                 // x, y, z, bound
-    unsigned long long mb[kGroupQ];    // merged (masked d^2 << 32 | Morton index)
-    int ncand, cursor;
-};
-
-__global__ __launch_bounds__(1024) void nn_search_coop_kernel(
-    const double* __restrict__ src, int N, const double* __restrict__ Qm, const int32_t* __restrict__ prevnn,
-    float r2s, int reseed, int seed_stride, const float4* __restrict__ p4, const float4* __restrict__ tlo,
-    const float4* __restrict__ thi, int ntiles, const float4* __restrict__ slo, const float4* __restrict__ shi,
-    int nsuper, const int32_t* __restrict__ active, const int32_t* __restrict__ done,
-    unsigned long long* __restrict__ best, unsigned long long* __restrict__ counters, Org3 org) {
-    const int slot = active[blockIdx.y];
-    if (done[slot]) return;
-    extern __shared__ uint16_t cand[];  // candidate tiles of the group (dynamic: ntiles entries)
-    __shared__ CoopShared sh;
-    __shared__ float stage_all[kCoopMaxW * 3 * kTile];  // per wave: x[64] | y[64] | z[64]
-    const int W = blockDim.x >> 6;
-    const int lane = threadIdx.x & 63, wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    float* stage = stage_all + wid * (3 * kTile);
-    const int g0 = blockIdx.x * kGroupQ;
-
-    // ---- 1. the group's queries (wave 0): q = fp32(Q p), bound from the seed
-    if (wid == 0) {
-        double Q[12];
-#pragma unroll
-        for (int t = 0; t < 12; ++t) Q[t] = Qm[12 * slot + t];
-#pragma unroll
-        for (int k = 0; k < kCQPT; ++k) {
-            const int i = g0 + lane + 64 * k;
-            float4 qv = make_float4(0.f, 0.f, 0.f, 0.f);  // bound 0: padding never takes anything
-            if (i < N) {
-                const double pp[3] = {src[3 * i], src[3 * i + 1], src[3 * i + 2]};
-                double q[3];
-                xform(Q, pp, q);
-                const float x = (float)(q[0] - org.x), y = (float)(q[1] - org.y), z = (float)(q[2] - org.z);
-                float bound = r2s;
-                const int jp = prevnn[(size_t)slot * N + i];
-                if (jp >= 0) {
-                    bound = fminf(bound, seed_bound(d2f(x, y, z, p4[jp])));
-                } else if (jp == kNoSeed || reseed) {
-                    for (int t = 0; t < ntiles; t += seed_stride)
-                        bound = fminf(bound, seed_bound(d2f(x, y, z, p4[t * kTile])));
-                }
-                qv = make_float4(x, y, z, bound);
-            }
-            sh.q[lane + 64 * k] = qv;
-            sh.mb[lane + 64 * k] = kNone;
-        }
-        if (lane == 0) {
-            sh.ncand = 0;
-            sh.cursor = 0;
-        }
-    }
-    __syncthreads();
-    float qx[kCQPT], qy[kCQPT], qz[kCQPT];
-    unsigned kk[kCQPT];  // running best key per query: masked d^2 | tile-local index
-    int jj[kCQPT];       // its Morton index (-1: the seed bound only)
-#pragma unroll
-    for (int k = 0; k < kCQPT; ++k) {
-        const float4 qv = sh.q[lane + 64 * k];
-        qx[k] = qv.x;
-        qy[k] = qv.y;
-        qz[k] = qv.z;
-        kk[k] = qv.w > 0.0f ? __float_as_uint(qv.w) : 0u;
-        jj[k] = -1;
-    }
-    const bool v0 = kk[0] != 0u, v1 = kk[1] != 0u;
-    const unsigned Wk = wave_umax((kk[0] > kk[1] ? kk[0] : kk[1]) & kKeyMask);
-    int visited = 0;
-    if (Wk != 0u) {  // block-uniform: every wave read the same queries
-        const float Wb = __uint_as_float(Wk);
-        const float inf = 3.0e38f;
-        const float lox = wave_fmin(fminf(v0 ? qx[0] : inf, v1 ? qx[1] : inf));
-        const float loy = wave_fmin(fminf(v0 ? qy[0] : inf, v1 ? qy[1] : inf));
-        const float loz = wave_fmin(fminf(v0 ? qz[0] : inf, v1 ? qz[1] : inf));
-        const float hix = wave_fmax(fmaxf(v0 ? qx[0] : -inf, v1 ? qx[1] : -inf));
-        const float hiy = wave_fmax(fmaxf(v0 ? qy[0] : -inf, v1 ? qy[1] : -inf));
-        const float hiz = wave_fmax(fmaxf(v0 ? qz[0] : -inf, v1 ? qz[1] : -inf));
-        auto box_gap = [&](float4 a, float4 b) {
-            const float dx = fmaxf(0.0f, fmaxf(a.x - hix, lox - b.x));
-            const float dy = fmaxf(0.0f, fmaxf(a.y - hiy, loy - b.y));
-            const float dz = fmaxf(0.0f, fmaxf(a.z - hiz, loz - b.z));
-            return dx * dx + dy * dy + dz * dz;
-        };
-        // ---- 2. culling, once per group: the waves split the surviving super-tiles
-        int surv = 0;  // survivors seen so far (block-uniform order)
-        for (int sb = 0; sb < nsuper; sb += 64) {
-            const int u = sb + lane;
-            const float sl = u < nsuper ? box_gap(slo[u], shi[u]) : inf;
-            unsigned long long smask = __ballot(sl < Wb);
-            while (smask) {
-                const int su = sb + __builtin_ctzll(smask);
-                smask &= smask - 1;
-                if ((surv++ % W) != wid) continue;
-                const int t = su * kSuper + lane;
-                const float lb = t < ntiles ? box_gap(tlo[t], thi[t]) : inf;
-                const unsigned long long tm = __ballot(lb < Wb);
-                if (tm == 0ull) continue;
-                int base = 0;
-                if (lane == 0) base = atomicAdd(&sh.ncand, __popcll(tm));
-                base = __shfl(base, 0, 64);
-                if (lb < Wb) cand[base + __builtin_amdgcn_mbcnt_hi((unsigned)(tm >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)tm, 0u))] = (uint16_t)t;
-            }
-        }
-    }
-    __syncthreads();
-    const int ncand = sh.ncand;
-    // ---- 3. scan: the waves pull candidate tiles from the list
-    auto take = [&]() -> int {
-        int k = 0;
-        if (lane == 0) k = atomicAdd(&sh.cursor, 1);
-        k = __builtin_amdgcn_readfirstlane(k);
-        return k < ncand ? __builtin_amdgcn_readfirstlane((int)cand[k]) : -1;
-    };
-    int tile = ncand > 0 ? take() : -1;
-    float4 pre = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (tile >= 0) pre = p4[tile * kTile + lane];
-    while (tile >= 0) {
-        const int nxt = take();
-        const float4 cur = pre;
-        if (nxt >= 0) pre = p4[nxt * kTile + lane];  // in flight while this tile is tested / scanned
-        const float4 a = tlo[tile], b = thi[tile];     // uniform address: scalar loads
-        const bool need = box_d2(qx[0], qy[0], qz[0], a.x, a.y, a.z, b.x, b.y, b.z) < __uint_as_float(kk[0] & kKeyMask) ||
-                          box_d2(qx[1], qy[1], qz[1], a.x, a.y, a.z, b.x, b.y, b.z) < __uint_as_float(kk[1] & kKeyMask);
-        if (__any(need)) {
-            stage[lane] = cur.x;
-            stage[64 + lane] = cur.y;
-            stage[128 + lane] = cur.z;
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-            unsigned m0 = 0xFFFFFFFFu, m1 = 0xFFFFFFFFu;
-            const f2 qx0 = {qx[0], qx[0]}, qy0 = {qy[0], qy[0]}, qz0 = {qz[0], qz[0]};
-            const f2 qx1 = {qx[1], qx[1]}, qy1 = {qy[1], qy[1]}, qz1 = {qz[1], qz[1]};
-#pragma unroll 8
-            for (int c = 0; c < kTile; c += 2) {
-                const f2 tx = *reinterpret_cast<const f2*>(stage + c);
-                const f2 ty = *reinterpret_cast<const f2*>(stage + 64 + c);
-                const f2 tz = *reinterpret_cast<const f2*>(stage + 128 + c);
-                f2 dx = qx0 - tx, dy = qy0 - ty, dz = qz0 - tz;
-                f2 d0 = dx * dx;
-                d0 = pk_fma(dy, dy, d0);
-                d0 = pk_fma(dz, dz, d0);
-                dx = qx1 - tx;
-                dy = qy1 - ty;
-                dz = qz1 - tz;
-                f2 d1 = dx * dx;
-                d1 = pk_fma(dy, dy, d1);
-                d1 = pk_fma(dz, dz, d1);
-                const unsigned a0 = (__float_as_uint(d0.x) & kKeyMask) | (unsigned)c;
-                const unsigned c0 = (__float_as_uint(d0.y) & kKeyMask) | (unsigned)(c + 1);
-                const unsigned a1 = (__float_as_uint(d1.x) & kKeyMask) | (unsigned)c;
-                const unsigned c1 = (__float_as_uint(d1.y) & kKeyMask) | (unsigned)(c + 1);
-                m0 = min(m0, min(a0, c0));
-                m1 = min(m1, min(a1, c1));
-            }
-            asm volatile("" ::: "memory");  // all reads of this tile precede the next stage write
-            const int gi0 = tile * kTile + (int)(m0 & 63u), gi1 = tile * kTile + (int)(m1 & 63u);
-            if ((m0 & kKeyMask) < (kk[0] & kKeyMask) ||
-                ((m0 & kKeyMask) == (kk[0] & kKeyMask) && jj[0] >= 0 && gi0 < jj[0])) {
-                kk[0] = m0;
-                jj[0] = gi0;
-            }
-            if ((m1 & kKeyMask) < (kk[1] & kKeyMask) ||
-                ((m1 & kKeyMask) == (kk[1] & kKeyMask) && jj[1] >= 0 && gi1 < jj[1])) {
-                kk[1] = m1;
-                jj[1] = gi1;
-            }
-            ++visited;
-        }
-        tile = nxt;
-    }
-    // ---- 4. merge over the waves, one store per query
-#pragma unroll
-    for (int k = 0; k < kCQPT; ++k)
-        if (jj[k] >= 0)
-            atomicMin(&sh.mb[lane + 64 * k], ((unsigned long long)(kk[k] & kKeyMask) << 32) | (unsigned)jj[k]);
-    if (lane == 0 && counters) {
-        unsigned long long* cs = counters + kCounterStride * ((blockIdx.x * W + wid + blockIdx.y) % kCounterSlots);
-        atomicAdd(cs, 4ull * visited);  // full tiles: 4 quarters each
-        atomicMax(cs + 1, 4ull * visited);
-    }
-    __syncthreads();
-    if (wid == 0) {
-        unsigned long long* out = best + (size_t)slot * N;
-#pragma unroll
-        for (int k = 0; k < kCQPT; ++k) {
-            const int i = g0 + lane + 64 * k;
-            if (i < N) out[i] = sh.mb[lane + 64 * k];
-        }
-    }
-}
-
-// --------------------------------------------------------------------------
-// Two-phase search (default, search_kernel = 2).
-//
-// cull_groups_kernel: one wave per group of 128 Morton-consecutive queries of
-// one start.  It transforms the group's queries (fp64 pose -> fp32, bound
-// from the previous correspondence or the tile representatives), writes them
-// to q32, resets best[] for them, and culls the target ONCE for the group:
-// super-tiles and tiles against the group box and its worst bound, then each
-// surviving tile against every query's own bound.  The tiles that may hold a
-// query's nearest target become work items (start, group, tile), appended
-// contiguously per group to a global list.
-//
-// scan_items_kernel: a persistent grid of waves pulls chunks of items from
-// the list (one atomic per chunk).  Consecutive items of a group reuse the
-// queries already in registers; the next item's tile is loaded while the
-// current one is scanned (the same packed fp32 scan and 32-bit keys as
-// nn_search_kernel).  When a wave leaves a group it merges its answers into
-// best[] by a 64-bit atomicMin on (masked d^2, Morton index), so the result
-// is the same as the one-kernel searches': among candidates whose d^2 agree
-// in the top 26 bits the lowest Morton index wins.
-//
-// Work is thus culled once per group (not once per split wave) and spread
-// evenly over the waves, whatever the number of running starts.
-// --------------------------------------------------------------------------
-constexpr int kCullBuf = 128;  // per-wave LDS staging of a group's items
-
-// grid: (ceil(groups per start / 4), running starts); one wave per group.
-// Group gidx = blockIdx.y * gblk + group writes its candidate tiles to
-// items[gidx * ntiles ...] and their number to gcount[gidx] (0 when the
-// start is done or nothing can improve).
-__global__ __launch_bounds__(256) void cull_groups_kernel(
-    const double* __restrict__ src, int N, const double* __restrict__ Qm, const int32_t* __restrict__ prevnn,
-    float r2s, int reseed, int seed_stride, const float4* __restrict__ p4, const float4* __restrict__ tlo,
-    const float4* __restrict__ thi, int ntiles, const float4* __restrict__ slo, const float4* __restrict__ shi,
-    int nsuper, const int32_t* __restrict__ active, const int32_t* __restrict__ done, int gblk,
-    float4* __restrict__ q32, unsigned long long* __restrict__ best, unsigned* __restrict__ items,
-    unsigned* __restrict__ gcount, Org3 org) {
-    __shared__ unsigned buf[4][kCullBuf];
-    const int lane = threadIdx.x & 63, wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int group = blockIdx.x * 4 + wid;
-    if (group >= gblk) return;  // wave-uniform
-    const size_t gidx = (size_t)blockIdx.y * gblk + group;
-    const int slot = active[blockIdx.y];
-    const int g0 = group * kGroupQ;
-    if (done[slot]) {
-        if (lane == 0) gcount[gidx] = 0u;
-        return;
-    }
-    double Q[12];
-#pragma unroll
-    for (int t = 0; t < 12; ++t) Q[t] = Qm[12 * slot + t];
-    float qx[kCQPT], qy[kCQPT], qz[kCQPT], bound[kCQPT];
-#pragma unroll
-    for (int k = 0; k < kCQPT; ++k) {
-        const int i = g0 + lane + 64 * k;
-        float4 qv = make_float4(0.f, 0.f, 0.f, 0.f);  // bound 0: padding never takes anything
-        if (i < N) {
-            const double pp[3] = {src[3 * i], src[3 * i + 1], src[3 * i + 2]};
-            double q[3];
-            xform(Q, pp, q);
-            const float x = (float)(q[0] - org.x), y = (float)(q[1] - org.y), z = (float)(q[2] - org.z);
-            float b = r2s;
-            const int jp = prevnn[(size_t)slot * N + i];
-            if (jp >= 0) {
-                b = fminf(b, seed_bound(d2f(x, y, z, p4[jp])));
-            } else if (jp == kNoSeed || reseed) {
-                for (int t = 0; t < ntiles; t += seed_stride)
-                    b = fminf(b, seed_bound(d2f(x, y, z, p4[t * kTile])));
-            }
-            qv = make_float4(x, y, z, b);
-            q32[(size_t)slot * N + i] = qv;
-            best[(size_t)slot * N + i] = kNone;
-        }
-        qx[k] = qv.x;
-        qy[k] = qv.y;
-        qz[k] = qv.z;
-        bound[k] = qv.w;
-    }
-    const bool v0 = bound[0] > 0.0f, v1 = bound[1] > 0.0f;
-    const unsigned b0 = v0 ? __float_as_uint(bound[0]) : 0u, b1 = v1 ? __float_as_uint(bound[1]) : 0u;
-    const unsigned Wk = wave_umax(b0 > b1 ? b0 : b1);
-    unsigned* out = items + gidx * (size_t)ntiles;
-    unsigned* wb = buf[wid];
-    int nb = 0, nout = 0;  // staged in wb / written to out (wave-uniform)
-    auto flush = [&]() {
-        for (int k = lane; k < nb; k += 64) out[nout + k] = wb[k];
-        nout += nb;
-        nb = 0;
-    };
-    if (Wk != 0u) {
-        const float Wb = __uint_as_float(Wk);
-        const float inf = 3.0e38f;
-        const float lox = wave_fmin(fminf(v0 ? qx[0] : inf, v1 ? qx[1] : inf));
-        const float loy = wave_fmin(fminf(v0 ? qy[0] : inf, v1 ? qy[1] : inf));
-        const float loz = wave_fmin(fminf(v0 ? qz[0] : inf, v1 ? qz[1] : inf));
-        const float hix = wave_fmax(fmaxf(v0 ? qx[0] : -inf, v1 ? qx[1] : -inf));
-        const float hiy = wave_fmax(fmaxf(v0 ? qy[0] : -inf, v1 ? qy[1] : -inf));
-        const float hiz = wave_fmax(fmaxf(v0 ? qz[0] : -inf, v1 ? qz[1] : -inf));
-        auto box_gap = [&](float4 a, float4 b) {
-            const float dx = fmaxf(0.0f, fmaxf(a.x - hix, lox - b.x));
-            const float dy = fmaxf(0.0f, fmaxf(a.y - hiy, loy - b.y));
-            const float dz = fmaxf(0.0f, fmaxf(a.z - hiz, loz - b.z));
-            return dx * dx + dy * dy + dz * dz;
-        };
-        for (int sb = 0; sb < nsuper; sb += 64) {
-            const int u = sb + lane;
-            const float sl = u < nsuper ? box_gap(slo[u], shi[u]) : inf;
-            unsigned long long smask = __ballot(sl < Wb);
-            while (smask) {
-                const int su = sb + __builtin_ctzll(smask);
-                smask &= smask - 1;
-                const int t = su * kSuper + lane;
-                float4 a = make_float4(0.f, 0.f, 0.f, 0.f), b = a;
-                float lb = inf;
-                if (t < ntiles) {
-                    a = tlo[t];
-                    b = thi[t];
-                    lb = box_gap(a, b);
-                }
-                unsigned long long tm = __ballot(lb < Wb);
-                unsigned long long keep = 0ull;
-                while (tm) {  // per-query test of each surviving tile
-                    const int k = __builtin_ctzll(tm);
-                    tm &= tm - 1;
-                    const float lx = __uint_as_float(__builtin_amdgcn_readlane(__float_as_uint(a.x), k));
-                    const float ly = __uint_as_float(__builtin_amdgcn_readlane(__float_as_uint(a.y), k));
-                    const float lz = __uint_as_float(__builtin_amdgcn_readlane(__float_as_uint(a.z), k));
-                    const float hx = __uint_as_float(__builtin_amdgcn_readlane(__float_as_uint(b.x), k));
-                    const float hy = __uint_as_float(__builtin_amdgcn_readlane(__float_as_uint(b.y), k));
-                    const float hz = __uint_as_float(__builtin_amdgcn_readlane(__float_as_uint(b.z), k));
-                    const bool need = box_d2(qx[0], qy[0], qz[0], lx, ly, lz, hx, hy, hz) < bound[0] ||
-                                      box_d2(qx[1], qy[1], qz[1], lx, ly, lz, hx, hy, hz) < bound[1];
-                    if (__any(need)) keep |= 1ull << k;
-                }
-                if (keep == 0ull) continue;
-                const int nk = __popcll(keep);
-                if (nb + nk > kCullBuf) flush();
-                if ((keep >> lane) & 1ull)
-                    wb[nb + __builtin_amdgcn_mbcnt_hi((unsigned)(keep >> 32),
-                                                      __builtin_amdgcn_mbcnt_lo((unsigned)keep, 0u))] = (unsigned)t;
-                nb += nk;
-            }
-        }
-        flush();
-    }
-    if (lane == 0) gcount[gidx] = (unsigned)nout;
-}
-
-// Exclusive prefix of the G group counts -> offs[0..G] (offs[G] = total), one
-// workgroup of 1024 threads, each owning a contiguous run of counts.
-__global__ __launch_bounds__(1024) void items_prefix_kernel(const unsigned* __restrict__ gcount, int G,
-                                                            unsigned* __restrict__ offs) {
-    __shared__ unsigned part[1024];
-    const int t = threadIdx.x;
-    const int per = (G + 1023) / 1024;
-    const int lo = min(G, t * per), hi = min(G, lo + per);
-    unsigned sum = 0;
-    for (int g = lo; g < hi; ++g) sum += gcount[g];
-    part[t] = sum;
-    __syncthreads();
-    for (int off = 1; off < 1024; off <<= 1) {  // inclusive Hillis-Steele scan of the run sums
-        const unsigned v = t >= off ? part[t - off] : 0u;
-        __syncthreads();
-        part[t] += v;
-        __syncthreads();
-    }
-    unsigned run = t > 0 ? part[t - 1] : 0u;
-    for (int g = lo; g < hi; ++g) {
-        offs[g] = run;
-        run += gcount[g];
-    }
-    if (t == 1023) offs[G] = part[1023];
-}
-
-// Persistent scan: wave w owns items [w*total/W, (w+1)*total/W) of the
-// concatenated per-group lists; consecutive items of a group share the
-// queries in registers; answers merge into best[] by 64-bit atomicMin.
-__global__ __launch_bounds__(256) void scan_items_kernel(const float4* __restrict__ q32, int N, int gblk,
-                                                         const int32_t* __restrict__ active,
-                                                         const float4* __restrict__ p4,
-                                                         const float4* __restrict__ tlo,
-                                                         const float4* __restrict__ thi, int ntiles,
-                                                         const unsigned* __restrict__ items,
-                                                         const unsigned* __restrict__ offs, int G,
-                                                         unsigned long long* __restrict__ best,
-                                                         unsigned long long* __restrict__ counters) {
-    __shared__ float stage_all[4 * 3 * kTile];
-    const int lane = threadIdx.x & 63, wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    float* stage = stage_all + wid * (3 * kTile);
-    const unsigned total = offs[G];
-    const unsigned nw = gridDim.x * 4, w = blockIdx.x * 4 + wid;
-    const unsigned e0 = (unsigned)(((unsigned long long)total * w) / nw);
-    const unsigned e1 = (unsigned)(((unsigned long long)total * (w + 1)) / nw);
-    if (e0 >= e1) return;
-    // the group holding e0: last g with offs[g] <= e0 (binary search, uniform)
-    int lo = 0, hi = G - 1;
-    while (lo < hi) {
-        const int mid = (lo + hi + 1) >> 1;
-        if (offs[mid] <= e0) lo = mid;
-        else hi = mid - 1;
-    }
-    int g = lo;
-    unsigned gend = offs[g + 1];
-    int cur_g = -1, slot = 0, gbase = 0;
-    float qx[kCQPT], qy[kCQPT], qz[kCQPT];
-    unsigned kk[kCQPT];
-    int jj[kCQPT];
-#pragma unroll
-    for (int k = 0; k < kCQPT; ++k) {
-        qx[k] = qy[k] = qz[k] = 0.f;
-        kk[k] = 0u;
-        jj[k] = -1;
-    }
-    auto merge = [&]() {
-        if (cur_g < 0) return;
-#pragma unroll
-        for (int k = 0; k < kCQPT; ++k) {
-            const int i = gbase + lane + 64 * k;
-            if (jj[k] >= 0 && i < N)
-                atomicMin(best + (size_t)slot * N + i, ((unsigned long long)(kk[k] & kKeyMask) << 32) | (unsigned)jj[k]);
-        }
-    };
-    // item e -> (group, tile); advances g past empty groups
-    auto tile_of = [&](unsigned e) -> int {
-        while (e >= gend) {
-            ++g;
-            gend = offs[g + 1];
-        }
-        return (int)items[(size_t)g * ntiles + (e - offs[g])];
-    };
-    int visited = 0;
-    int tile = tile_of(e0), tg = g;
-    float4 pre = p4[tile * kTile + lane];
-    for (unsigned e = e0; e < e1; ++e) {
-        const int ctile = tile, cg = tg;
-        const float4 cur = pre;
-        if (e + 1 < e1) {
-            tile = tile_of(e + 1);
-            tg = g;
-            pre = p4[tile * kTile + lane];  // in flight during this tile
-        }
-        if (cg != cur_g) {
-            merge();
-            cur_g = cg;
-            slot = active[cg / gblk];
-            gbase = (cg % gblk) * kGroupQ;
-#pragma unroll
-            for (int q = 0; q < kCQPT; ++q) {
-                const int i = gbase + lane + 64 * q;
-                const float4 qv = i < N ? q32[(size_t)slot * N + i] : make_float4(0.f, 0.f, 0.f, 0.f);
-                qx[q] = qv.x;
-                qy[q] = qv.y;
-                qz[q] = qv.z;
-                kk[q] = qv.w > 0.0f ? __float_as_uint(qv.w) : 0u;
-                jj[q] = -1;
-            }
-        }
-        const float4 a = tlo[ctile], b = thi[ctile];
-        const bool need =
-            box_d2(qx[0], qy[0], qz[0], a.x, a.y, a.z, b.x, b.y, b.z) < __uint_as_float(kk[0] & kKeyMask) ||
-            box_d2(qx[1], qy[1], qz[1], a.x, a.y, a.z, b.x, b.y, b.z) < __uint_as_float(kk[1] & kKeyMask);
-        if (!__any(need)) continue;
-        stage[lane] = cur.x;
-        stage[64 + lane] = cur.y;
-        stage[128 + lane] = cur.z;
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        unsigned m0 = 0xFFFFFFFFu, m1 = 0xFFFFFFFFu;
-        const f2 qx0 = {qx[0], qx[0]}, qy0 = {qy[0], qy[0]}, qz0 = {qz[0], qz[0]};
-        const f2 qx1 = {qx[1], qx[1]}, qy1 = {qy[1], qy[1]}, qz1 = {qz[1], qz[1]};
-#pragma unroll 8
-        for (int c = 0; c < kTile; c += 2) {
-            const f2 tx = *reinterpret_cast<const f2*>(stage + c);
-            const f2 ty = *reinterpret_cast<const f2*>(stage + 64 + c);
-            const f2 tz = *reinterpret_cast<const f2*>(stage + 128 + c);
-            f2 dx = qx0 - tx, dy = qy0 - ty, dz = qz0 - tz;
-            f2 d0 = dx * dx;
-            d0 = pk_fma(dy, dy, d0);
-            d0 = pk_fma(dz, dz, d0);
-            dx = qx1 - tx;
-            dy = qy1 - ty;
-            dz = qz1 - tz;
-            f2 d1 = dx * dx;
-            d1 = pk_fma(dy, dy, d1);
-            d1 = pk_fma(dz, dz, d1);
-            const unsigned a0 = (__float_as_uint(d0.x) & kKeyMask) | (unsigned)c;
-            const unsigned c0k = (__float_as_uint(d0.y) & kKeyMask) | (unsigned)(c + 1);
-            const unsigned a1 = (__float_as_uint(d1.x) & kKeyMask) | (unsigned)c;
-            const unsigned c1k = (__float_as_uint(d1.y) & kKeyMask) | (unsigned)(c + 1);
-            m0 = min(m0, min(a0, c0k));
-            m1 = min(m1, min(a1, c1k));
-        }
-        asm volatile("" ::: "memory");  // all reads of this tile precede the next stage write
-        const int gi0 = ctile * kTile + (int)(m0 & 63u), gi1 = ctile * kTile + (int)(m1 & 63u);
-        if ((m0 & kKeyMask) < (kk[0] & kKeyMask) ||
-            ((m0 & kKeyMask) == (kk[0] & kKeyMask) && jj[0] >= 0 && gi0 < jj[0])) {
-            kk[0] = m0;
-            jj[0] = gi0;
-        }
-        if ((m1 & kKeyMask) < (kk[1] & kKeyMask) ||
-            ((m1 & kKeyMask) == (kk[1] & kKeyMask) && jj[1] >= 0 && gi1 < jj[1])) {
-            kk[1] = m1;
-            jj[1] = gi1;
-        }
-        ++visited;
-    }
-    merge();
-    if (lane == 0 && counters) {
-        unsigned long long* cs = counters + kCounterStride * ((blockIdx.x * 4 + wid) % kCounterSlots);
-        atomicAdd(cs, 4ull * visited);  // full tiles: 4 quarters each
-        atomicMax(cs + 1, 4ull * visited);
-    }
-}
-
-size_t coop_smem_bytes(int W, int64_t ntiles) { return (size_t)ntiles * 2 + 16; }
 
 // --------------------------------------------------------------------------
 // Accumulation kernels: accum_qpt(N) queries per thread (grid = (blocks per start,
@@ -1790,9 +1190,7 @@ __device__ __forceinline__ double wave_sum_fixed(double v) {
 }
 
 // Block reduction of NV per-thread values into partial[slot, block][slot_of(v)].
-// kSc1: the partial is stored write-through (sc1), to be read in the same
-// launch by the start's last-arriving block (pipelined passes).
-template <int NV, bool kSc1 = false, typename SlotOf>
+template <int NV, typename SlotOf>
 __device__ __forceinline__ void block_partial(const double* acc, double (*red)[NV], SlotOf slot_of,
                                               double* __restrict__ out) {
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
@@ -1807,19 +1205,12 @@ __device__ __forceinline__ void block_partial(const double* acc, double (*red)[N
 #pragma unroll
         for (int v = 0; v < NV; ++v)
             if (slot_of(v) == (int)threadIdx.x) s = ((red[0][v] + red[1][v]) + red[2][v]) + red[3][v];
-        if (kSc1)
-            __hip_atomic_store(reinterpret_cast<unsigned long long*>(out) + threadIdx.x,
-                               (unsigned long long)__double_as_longlong(s), __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_AGENT);
-        else
-            out[threadIdx.x] = s;
+        out[threadIdx.x] = s;
     }
 }
 
 // Fixed-order reduction of one start's block partials (lane-strided, then
-// the wave).  kSc1: the partials were stored sc1 in this launch and are read
-// with sc1 loads (L1 bypassed) behind the caller's agent acquire.
-template <bool kSc1 = false>
+// the wave).
 __device__ __forceinline__ void reduce_partials(const double* __restrict__ partial, int slot, int nblk,
                                                 double s[kNacc]) {
     const int lane = threadIdx.x & 63;
@@ -1827,22 +1218,15 @@ __device__ __forceinline__ void reduce_partials(const double* __restrict__ parti
     for (int v = 0; v < kNacc; ++v) s[v] = 0.0;
     for (int b = lane; b < nblk; b += 64) {
         const double* pp = partial + ((size_t)slot * nblk + b) * kPartialStride;
-        if (kSc1) {
+        // every 16 B load of the partial issued before the first add: one
+        // memory round trip (the partials were written on other XCDs and miss
+        // this L2), not one per pair of terms
+        static_assert(kPartialStride >= kNacc + 1 && kPartialStride % 2 == 0, "partial stride");
+        double2 t[(kNacc + 1) / 2];
 #pragma unroll
-            for (int v = 0; v < kNacc; ++v)
-                s[v] += __longlong_as_double((long long)__hip_atomic_load(
-                    reinterpret_cast<const unsigned long long*>(pp) + v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-        } else {
-            // every 16 B load of the partial issued before the first add: one
-            // memory round trip (the partials were written on other XCDs and
-            // miss this L2), not one per pair of terms
-            static_assert(kPartialStride >= kNacc + 1 && kPartialStride % 2 == 0, "partial stride");
-            double2 t[(kNacc + 1) / 2];
+        for (int u = 0; u < (kNacc + 1) / 2; ++u) t[u] = reinterpret_cast<const double2*>(pp)[u];
 #pragma unroll
-            for (int u = 0; u < (kNacc + 1) / 2; ++u) t[u] = reinterpret_cast<const double2*>(pp)[u];
-#pragma unroll
-            for (int v = 0; v < kNacc; ++v) s[v] += (v & 1) ? t[v >> 1].y : t[v >> 1].x;
-        }
+        for (int v = 0; v < kNacc; ++v) s[v] += (v & 1) ? t[v >> 1].y : t[v >> 1].x;
     }
 #pragma unroll
     for (int v = 0; v < kNacc; ++v) s[v] = wave_sum_fixed(s[v]);
@@ -1863,11 +1247,8 @@ struct SolveArgs {
 
 // --------------------------------------------------------------------------
 // One start's convergence test (RegistrationICP), 6x6 solve (or Umeyama) and
-// pose update from its 29 reduced sums.  Lane 0 only.  done[] is stored sc1:
-// the pipelined pass compacts the running starts in the same launch.
+// pose update from its 29 reduced sums.
 // --------------------------------------------------------------------------
-// kAt: the pose state (prev, T, Q, R) is read and written by a different
-// workgroup every pass of the same launch (persistent loop): atomic accesses.
 // Called by all 64 lanes of one wave with the same (uniform) sums; the 6x6
 // system is solved wave-parallel (det6_wave / ldlt_solve6_wave, bit-identical
 // to the single-lane det6 / ldlt_solve6); lane 0 stores.  Returns true when
@@ -1880,14 +1261,13 @@ struct PoseIn {
     double pf, pr, T[16], G[12];
 };
 
-template <bool kAt>
 __device__ __forceinline__ double pose_lane_load(int slot, const SolveArgs& a) {
     const int lane = threadIdx.x & 63;
     const double* p = lane < 2 ? a.prev + 2 * slot + lane
                       : lane < 18 ? a.T + 16 * slot + (lane - 2)
                       : lane < 30 ? a.G + 12 * slot + (lane - 18)
                                   : a.prev + 2 * slot;
-    return ld_f64<kAt>(p);
+    return *p;
 }
 
 // every lane of the wave (readlane)
@@ -1900,7 +1280,7 @@ __device__ __forceinline__ void pose_from_lanes(double v, PoseIn& p) {
     for (int t = 0; t < 12; ++t) p.G[t] = rl64(v, 18 + t);
 }
 
-template <int kEst, bool kAt = false>  // kEst 0: GeneralizedICP, 1: PointToPoint
+template <int kEst>  // kEst 0: GeneralizedICP, 1: PointToPoint
 __device__ bool solve_start(int slot, const double s[kNacc], int64_t N, int pass, int max_iter, double rel_fit,
                             double rel_rmse, const SolveArgs& a, const PoseIn& pin) {
 #pragma clang fp contract(off)  // no fused multiply-add: the same rounding in every caller
@@ -1916,13 +1296,13 @@ __device__ bool solve_start(int slot, const double s[kNacc], int64_t N, int pass
             a.out_rmse[slot] = rmse;
             a.out_iters[slot] = pass;
             a.out_ncorr[slot] = (int64_t)cnt;
-            __hip_atomic_store(a.done + slot, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            a.done[slot] = 1;
         }
         return true;
     }
     if (lane == 0) {
-        st_f64<kAt>(a.prev + 2 * slot, fit);
-        st_f64<kAt>(a.prev + 2 * slot + 1, rmse);
+        a.prev[2 * slot] = fit;
+        a.prev[2 * slot + 1] = rmse;
     }
 
     double upd[16] = {1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1};
@@ -1949,27 +1329,19 @@ __device__ bool solve_start(int slot, const double s[kNacc], int64_t N, int pass
     double Tn[16];
     m4_mul(upd, pin.T, Tn);
     if (lane == 0)
-        for (int t = 0; t < 16; ++t) st_f64<kAt>(a.T + 16 * slot + t, Tn[t]);
+        for (int t = 0; t < 16; ++t) a.T[16 * slot + t] = Tn[t];
     // Q = Tn * [G; 0 0 0 1]  (3x4), R = Tn[:3,:3]
     const double* G = pin.G;
     for (int r = 0; r < 3; ++r) {
         for (int c = 0; c < 4; ++c) {
             double v = Tn[4 * r + 0] * G[c] + Tn[4 * r + 1] * G[4 + c] + Tn[4 * r + 2] * G[8 + c];
             if (c == 3) v += Tn[4 * r + 3];
-            if (lane == 0) st_f64<kAt>(a.Q + 12 * slot + 4 * r + c, v);
+            if (lane == 0) a.Q[12 * slot + 4 * r + c] = v;
         }
         if (lane == 0)
-            for (int c = 0; c < 3; ++c) st_f64<kAt>(a.R + 9 * slot + 3 * r + c, Tn[4 * r + c]);
+            for (int c = 0; c < 3; ++c) a.R[9 * slot + 3 * r + c] = Tn[4 * r + c];
     }
     return false;
-}
-
-template <int kEst, bool kAt = false>
-__device__ __forceinline__ bool solve_start(int slot, const double s[kNacc], int64_t N, int pass, int max_iter,
-                                            double rel_fit, double rel_rmse, const SolveArgs& a) {
-    PoseIn pin;
-    pose_from_lanes(pose_lane_load<kAt>(slot, a), pin);
-    return solve_start<kEst, kAt>(slot, s, N, pass, max_iter, rel_fit, rel_rmse, a, pin);
 }
 
 // Test entry (orpcd_test_solve6): for each of n systems (21 upper JTJ + 6 JTr),
@@ -2020,84 +1392,9 @@ hipError_t launch_solve6_test(const double* sums, int n, double* out_serial, dou
     return hipGetLastError();
 }
 
-// --------------------------------------------------------------------------
-// Pipelined passes: the host enqueues passes without waiting; the device
-// keeps the list of running starts.
-//   ctl[0]       running starts (active[0 .. ctl[0]) ), read by every kernel
-//                of the next pass to map its blocks
-//   ctl[1]       starts solved in the current pass
-//   ctl[2+slot]  accumulation blocks of the start that have arrived
-//   progress     host-mapped word: (passes completed << 32) | running starts
-// The last-arriving accumulation block of a start reduces the partials and
-// solves (in the order of icp_solve_kernel: identical results); the block
-// that solves the pass's last start compacts active[] and publishes.
-// Hand-offs (MI355X_MICROARCH.md, inter-workgroup visibility): sc1 partial and
-// done[] stores, every storing wave drained, then one relaxed agent atomic;
-// the last arriver takes an agent acquire before its sc1 loads.
-// --------------------------------------------------------------------------
-struct PassCtl {
-    int32_t* ctl;
-    unsigned long long* progress;
-    int32_t* active;
-    int pass, max_iter;
-    double rel_fit, rel_rmse;
-    int64_t N;
-    SolveArgs a;
-};
-
-template <int kEst>
-__device__ __forceinline__ void finish_pass(int slot, int nact, const double* __restrict__ partial, int nblk,
-                                            const PassCtl& pc) {
-    __shared__ int last;
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's sc1 partial stores have landed
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        const int t = __hip_atomic_fetch_add(pc.ctl + 2 + slot, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        last = t == nblk - 1;
-    }
-    __syncthreads();
-    if (!last || threadIdx.x >= 64) return;
-    // wave 0 of the start's last block
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    const int lane = threadIdx.x;
-    double s[kNacc];
-    reduce_partials<true>(partial, slot, nblk, s);
-    int last_solve = 0;
-    if (lane == 0) pc.ctl[2 + slot] = 0;  // for the next pass (read after the launch boundary)
-    solve_start<kEst>(slot, s, pc.N, pc.pass, pc.max_iter, pc.rel_fit, pc.rel_rmse, pc.a);
-    if (lane == 0) {
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // done[slot] (sc1) has landed
-        last_solve = __hip_atomic_fetch_add(pc.ctl + 1, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == nact - 1;
-    }
-    if (!__builtin_amdgcn_readfirstlane(last_solve)) return;
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    // compact the running starts in place, order kept
-    int k = 0;
-    for (int b0 = 0; b0 < nact; b0 += 64) {
-        const int b = b0 + lane;
-        const int sl = b < nact ? pc.active[b] : -1;
-        const bool run = sl >= 0 && __hip_atomic_load(pc.a.done + sl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0;
-        const unsigned long long m = __ballot(run);
-        const int pos = k + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m, 0));
-        if (run) pc.active[pos] = sl;  // pos <= b: every lane read its entry before any write of this round
-        k += __builtin_popcountll(m);
-    }
-    if (lane == 0) {
-        pc.ctl[0] = k;
-        pc.ctl[1] = 0;
-        __hip_atomic_store(pc.progress, ((unsigned long long)(pc.pass + 1) << 32) | (unsigned)k, __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_SYSTEM);
-    }
-}
-
 // The GICP normal-equation terms of accumulation block `ablk` of start
 // `slot` (queries (ablk * qpt + k) * 256 + threadIdx.x): this thread's sums,
-// in query order k.  Writes the next pass's seed (prevnn).  kPersist: the
-// correspondences and the pose were published inside the launch (atomic
-// accesses), and best[] is reset for the next pass's atomicMin merges.
-template <bool kPersist>
+// in query order k.  Writes the next pass's seed (prevnn).
 __device__ __forceinline__ void gicp_block_terms(int slot, int ablk, const double* __restrict__ src,
                                                  const double* __restrict__ scov, int N,
                                                  const double* __restrict__ tgt64, const double* __restrict__ tcov,
@@ -2109,9 +1406,9 @@ __device__ __forceinline__ void gicp_block_terms(int slot, int ablk, const doubl
     for (int v = 0; v < kNacc; ++v) acc[v] = 0.0;
     double Q[12], R[9];
 #pragma unroll
-    for (int t = 0; t < 12; ++t) Q[t] = ld_f64<kPersist>(Qm + 12 * slot + t);
+    for (int t = 0; t < 12; ++t) Q[t] = Qm[12 * slot + t];
 #pragma unroll
-    for (int t = 0; t < 9; ++t) R[t] = ld_f64<kPersist>(Rm + 9 * slot + t);
+    for (int t = 0; t < 9; ++t) R[t] = Rm[9 * slot + t];
     // Loads in two rounds for all of the thread's queries (best, source point
     // and covariance; then the target point and covariance of each match),
     // not three dependent round trips per query; the terms are then added in
@@ -2123,7 +1420,7 @@ __device__ __forceinline__ void gicp_block_terms(int slot, int ablk, const doubl
     for (int k = 0; k < kQ; ++k) {
         const int i = (ablk * kQ + k) * 256 + threadIdx.x;
         const int ii = i < N ? i : 0;
-        bv[k] = i < N ? ld_u64<kPersist>(best + (size_t)slot * N + i) : kNone;
+        bv[k] = i < N ? best[(size_t)slot * N + i] : kNone;
 #pragma unroll
         for (int c = 0; c < 3; ++c) p[k][c] = src[3 * ii + c];
         const double* cs6 = scov + ((size_t)slot * N + ii) * 6;
@@ -2134,10 +1431,7 @@ __device__ __forceinline__ void gicp_block_terms(int slot, int ablk, const doubl
     for (int k = 0; k < kQ; ++k) {
         const int i = (ablk * kQ + k) * 256 + threadIdx.x;
         const int j = bv[k] == kNone ? -1 : (int)(unsigned)(bv[k] & 0xffffffffu);
-        if (i < N) {
-            st_i32<kPersist>(prevnn + (size_t)slot * N + i, j >= 0 ? j : kNoMatch);
-            if constexpr (kPersist) st_u64<true>(best + (size_t)slot * N + i, kNone);
-        }
+        if (i < N) prevnn[(size_t)slot * N + i] = j >= 0 ? j : kNoMatch;
         const int jj = j >= 0 ? j : 0;
 #pragma unroll
         for (int c = 0; c < 3; ++c) t3[k][c] = ldg_f64(tgt64 + 3 * jj + c);
@@ -2207,24 +1501,19 @@ __device__ __forceinline__ void gicp_block_terms(int slot, int ablk, const doubl
 #else
 #define ORPCD_ACCUM_ATTR
 #endif
-template <bool kFused>
 __global__ __launch_bounds__(256) ORPCD_ACCUM_ATTR void gicp_accum_kernel(
     const double* __restrict__ src, const double* __restrict__ scov, int N, const TargetDesc* __restrict__ tdesc,
     TgtBounds tb, const int32_t* __restrict__ active, const double* __restrict__ Qm,
     const double* __restrict__ Rm, const int32_t* __restrict__ done, double r2,
     unsigned long long* __restrict__ best, int32_t* __restrict__ prevnn, double* __restrict__ partial,
-    int nblk, PassCtl pc) {
-    const int nact = kFused ? pc.ctl[0] : 0;
-    if (kFused && (int)blockIdx.y >= nact) return;
+    int nblk) {
     const int slot = active[blockIdx.y];
     if (done[slot]) return;
     const TargetDesc& tg = tdesc[target_of_row(tb, blockIdx.y)];
     __shared__ double red[4][kNacc];
     double acc[kNacc];
-    gicp_block_terms<false>(slot, blockIdx.x, src, scov, N, tg.xyz64, tg.tcov, Qm, Rm, r2, best, prevnn, acc);
-    block_partial<kNacc, kFused>(acc, red, [](int v) { return v; },
-                                 partial + ((size_t)slot * nblk + blockIdx.x) * kPartialStride);
-    if constexpr (kFused) finish_pass<kEstGICP>(slot, nact, partial, nblk, pc);
+    gicp_block_terms(slot, blockIdx.x, src, scov, N, tg.xyz64, tg.tcov, Qm, Rm, r2, best, prevnn, acc);
+    block_partial<kNacc>(acc, red, [](int v) { return v; }, partial + ((size_t)slot * nblk + blockIdx.x) * kPartialStride);
 }
 
 // PointToPoint accumulation (TransformationEstimationPointToPoint, Eigen::
@@ -2234,7 +1523,6 @@ __global__ __launch_bounds__(256) ORPCD_ACCUM_ATTR void gicp_accum_kernel(
 constexpr int kP2PTerms = 17;
 __device__ __forceinline__ int p2p_slot(int v) { return v < 15 ? v : 12 + v; }  // 15 -> 27, 16 -> 28
 
-template <bool kPersist>
 __device__ __forceinline__ void p2p_block_terms(int slot, int ablk, const double* __restrict__ src, int N,
                                                 const double* __restrict__ tgt64, const double* __restrict__ Qm,
                                                 double r2, unsigned long long* __restrict__ best,
@@ -2244,15 +1532,14 @@ __device__ __forceinline__ void p2p_block_terms(int slot, int ablk, const double
     for (int v = 0; v < kP2PTerms; ++v) acc[v] = 0.0;
     double Q[12];
 #pragma unroll
-    for (int t = 0; t < 12; ++t) Q[t] = ld_f64<kPersist>(Qm + 12 * slot + t);
+    for (int t = 0; t < 12; ++t) Q[t] = Qm[12 * slot + t];
     const int qpt = accum_qpt(N);
     for (int k = 0; k < qpt; ++k) {
         const int i = (ablk * qpt + k) * 256 + threadIdx.x;
         if (i >= N) break;
-        const unsigned long long v = ld_u64<kPersist>(best + (size_t)slot * N + i);
+        const unsigned long long v = best[(size_t)slot * N + i];
         const int j = v == kNone ? -1 : (int)(unsigned)(v & 0xffffffffu);
-        st_i32<kPersist>(prevnn + (size_t)slot * N + i, j >= 0 ? j : kNoMatch);
-        if constexpr (kPersist) st_u64<true>(best + (size_t)slot * N + i, kNone);
+        prevnn[(size_t)slot * N + i] = j >= 0 ? j : kNoMatch;
         if (j < 0) continue;
         const double p[3] = {src[3 * i], src[3 * i + 1], src[3 * i + 2]};
         double q[3];
@@ -2273,7 +1560,6 @@ __device__ __forceinline__ void p2p_block_terms(int slot, int ablk, const double
     }
 }
 
-template <bool kFused>
 __global__ __launch_bounds__(256) void p2p_accum_kernel(const double* __restrict__ src, int N,
                                                         const TargetDesc* __restrict__ tdesc, TgtBounds tb,
                                                         const int32_t* __restrict__ active,
@@ -2281,25 +1567,20 @@ __global__ __launch_bounds__(256) void p2p_accum_kernel(const double* __restrict
                                                         const int32_t* __restrict__ done, double r2,
                                                         unsigned long long* __restrict__ best,
                                                         int32_t* __restrict__ prevnn, double* __restrict__ partial,
-                                                        int nblk, PassCtl pc) {
-    const int nact = kFused ? pc.ctl[0] : 0;
-    if (kFused && (int)blockIdx.y >= nact) return;
+                                                        int nblk) {
     const int slot = active[blockIdx.y];
     if (done[slot]) return;
     __shared__ double red[4][kP2PTerms];
     double acc[kP2PTerms];
-    p2p_block_terms<false>(slot, blockIdx.x, src, N, tdesc[target_of_row(tb, blockIdx.y)].xyz64, Qm, r2, best,
+    p2p_block_terms(slot, blockIdx.x, src, N, tdesc[target_of_row(tb, blockIdx.y)].xyz64, Qm, r2, best,
                            prevnn, acc);
-    block_partial<kP2PTerms, kFused>(acc, red, p2p_slot,
-                                     partial + ((size_t)slot * nblk + blockIdx.x) * kPartialStride);
-    if constexpr (kFused) finish_pass<kEstP2P>(slot, nact, partial, nblk, pc);
+    block_partial<kP2PTerms>(acc, red, p2p_slot, partial + ((size_t)slot * nblk + blockIdx.x) * kPartialStride);
 }
 
 // --------------------------------------------------------------------------
 // Per-start reduction of the block partials, convergence test
-// (RegistrationICP), and the 6x6 solve + pose update.  One wave per start
-// (the unpipelined loop; the pipelined pass runs the same code in the
-// accumulation kernel's last block).  sums_in != null: the sums are given
+// (RegistrationICP), and the 6x6 solve + pose update.  One wave per start.
+// sums_in != null: the sums are given
 // (row-sharded mode, already all-reduced over ranks) and the partials are
 // not read.
 // --------------------------------------------------------------------------
@@ -2319,8 +1600,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 2))) void
     const int slot = active[blockIdx.x];
     // the done flag, the partials and the pose are loaded together (one memory
     // round trip after active[]); a finished start only wasted the loads
-    const int finished = __hip_atomic_load(a.done + slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const double pose = pose_lane_load<false>(slot, a);
+    const int finished = a.done[slot];
+    const double pose = pose_lane_load(slot, a);
     double s[kNacc];
     if (sums_in) {
 #pragma unroll
@@ -2332,422 +1613,6 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 2))) void
     PoseIn pin;
     pose_from_lanes(pose, pin);
     solve_start<kEst>(slot, s, N, pass, max_iter, rel_fit, rel_rmse, a, pin);
-}
-
-// ---------------------------------------------------------------------------
-// Fused solve + query transform (opt.fuse_solve): one launch per pass instead
-// of icp_solve_kernel followed by xform_queries_kernel.  Per start row:
-//   a solver     (wave 0): the partials, the 6x6 solve, the pose
-//                update (sc1 stores, as the pipelined loop's solve), then a
-//                relaxed agent flag ready[slot] = pass + 1 (MI355X_MICROARCH.md
-//                inter-workgroup hand-off, first row: every store sc1 and
-//                drained by s_waitcnt vmcnt(0), one lane signals, the polling
-//                lane then a workgroup barrier, every load of the handed-off
-//                bytes sc1);
-//   a planner    the ordered dispatch's (if live): it counts its items
-//                from the previous costs, then waits for the flag and files
-//                them only if the start is still running;
-//   transform    blocks: the pose-independent loads (source point,
-//                previous correspondence and its target point) are issued
-//                before the wait, so the solve overlaps them.
-// Blocks are dispatched in linear order and every solver precedes every
-// waiting block, so the solvers are resident or done before anything waits
-// on them; the wait is bounded (error flag, checked by the host at every sync).
-// ---------------------------------------------------------------------------
-struct FuseArgs {
-    const double* partial;
-    int nblk;
-    int pass;  // the pass just accumulated: this launch solves it and forms pass + 1's queries
-    int max_iter;
-    double rel_fit, rel_rmse;
-    int64_t N;
-    SolveArgs a;
-    int32_t* ready;  // per slot: the last pass whose pose was published
-    unsigned* err;   // a wait that timed out
-    int nact;        // launch rows
-};
-
-__device__ __forceinline__ void wait_ready(const FuseArgs& f, int slot, int tag) {
-    if (threadIdx.x == 0) {
-        unsigned spins = 0;
-        while (__hip_atomic_load(f.ready + slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < tag) {
-            __builtin_amdgcn_s_sleep(2);
-            if (++spins > (1u << 24)) {  // ~seconds: never in a sound run
-                atomicOr(f.err, 1u);
-                break;
-            }
-        }
-    }
-    __syncthreads();
-}
-
-template <int kEst>
-__global__ __launch_bounds__(256) void solve_xform_kernel(const double* __restrict__ src, int N,
-                                                          const int32_t* __restrict__ active,
-                                                          const TargetDesc* __restrict__ tdesc, TgtBounds tb,
-                                                          const int32_t* __restrict__ prevnn, float r2s, int reseed,
-                                                          float4* __restrict__ q32,
-                                                          unsigned long long* __restrict__ best,
-                                                          float4* __restrict__ gbox, SchedX sx, FuseArgs f) {
-    // 1-D grid: every start's solver first (all dispatched at once, before
-    // any block that waits), then the planners, then the transform blocks row
-    // by row (a row-major 2-D grid put row r's solver behind every earlier
-    // row's transform blocks: the solves ran one after another)
-    const int nact = f.nact, xb = (N + 255) / 256;
-    const int b = blockIdx.x;
-    const int nsp = nact * (sx.list ? 2 : 1);
-    const int row = b < nact ? b : b < nsp ? b - nact : (b - nsp) / xb;
-    const int slot = active[row];
-    const int tag = f.pass + 1;
-    if (b < nact) {  // the solver
-        if (threadIdx.x >= 64) return;
-        const int finished = __hip_atomic_load(f.a.done + slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        const double pose = pose_lane_load<false>(slot, f.a);
-        double s[kNacc];
-        reduce_partials(f.partial, slot, f.nblk, s);
-        if (!finished) {
-            PoseIn pin;
-            pose_from_lanes(pose, pin);
-            solve_start<kEst, true>(slot, s, f.N, f.pass, f.max_iter, f.rel_fit, f.rel_rmse, f.a, pin);
-        }
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the sc1 pose / done stores have landed
-        if (threadIdx.x == 0) __hip_atomic_store(f.ready + slot, tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        return;
-    }
-    const int tk = target_of_row(tb, row);
-    if (b < nsp) {  // the planner: items only if the start keeps running
-        plan_start_items(sx, slot, tk, [&]() {
-            wait_ready(f, slot, tag);
-            return __hip_atomic_load(f.a.done + slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0;
-        });
-        return;
-    }
-    const int bx = (b - nsp) - row * xb;
-    const TargetDesc& tg = tdesc[tk];
-    const float4* __restrict__ p4 = tg.p4;
-    const int i = bx * 256 + threadIdx.x;
-    const bool valid = i < N;
-    // pose-independent loads first: they overlap the solve
-    double p[3] = {0.0, 0.0, 0.0};
-    int jp = -1;
-    float4 tj = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (valid) {
-        p[0] = src[3 * i], p[1] = src[3 * i + 1], p[2] = src[3 * i + 2];
-        jp = prevnn[(size_t)slot * N + i];
-        if (jp >= 0) tj = p4[jp];
-    }
-    wait_ready(f, slot, tag);
-    if (__hip_atomic_load(f.a.done + slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return;  // block-uniform
-    const float inf = 3.0e38f;
-    float x = inf, y = inf, z = inf, bound = 0.0f;
-    if (valid) {
-        best[(size_t)slot * N + i] = kNone;  // split searches merge into it by atomicMin
-        double Q[12];
-#pragma unroll
-        for (int t = 0; t < 12; ++t) Q[t] = ld_f64<true>(f.a.Q + 12 * slot + t);  // sc1: written by the solver
-        double q[3];
-        xform(Q, p, q);
-        x = (float)(q[0] - tg.ox), y = (float)(q[1] - tg.oy), z = (float)(q[2] - tg.oz);
-        bound = r2s;
-        if (jp >= 0) {
-            bound = fminf(bound, seed_bound(d2f(x, y, z, tj)));
-        } else if (jp == kNoSeed || reseed) {
-            for (int t = 0; t < tg.ntiles; t += tg.seed_stride)
-                bound = fminf(bound, seed_bound(d2f(x, y, z, p4[t * kTile])));
-        }
-        q32[(size_t)slot * N + i] = make_float4(x, y, z, bound);
-    }
-    write_gbox(x, y, z, bound, valid, slot, bx, N, gbox);
-}
-
-// --------------------------------------------------------------------------
-// Persistent pass loop (default): the whole ICP loop of every start of the
-// batch in ONE launch, each start advancing at its own pace.
-//
-// Work of one pass of start b, as dataflow inside the launch:
-//  * search items (b, bx), bx < sblk * S: workgroup = the 512 queries of query
-//    block bx / S (wave w: 128 of them), tile split bx % S -- exactly the
-//    block / split of nn_search_kernel; each wave first forms its queries
-//    itself (fp64 pose -> fp32 in the target's frame, seed bound from the
-//    previous correspondence), exactly as xform_queries_kernel does;
-//  * the workgroup whose search item completes an accumulation block (the
-//    last of its 2 query blocks x S splits to arrive: ticket) accumulates that
-//    block exactly as gicp_accum_kernel / p2p_accum_kernel (same threads, same
-//    order), writes the next seeds and resets best[] for the next pass;
-//  * the workgroup completing the start's last accumulation block (ticket)
-//    reduces the partials and solves exactly as icp_solve_kernel, then
-//    publishes pass p + 1 of start b: sched[b] = (p + 1, S', item 0).
-// Idle workgroups poll sched[] (one 64-lane load per 64 starts) and take an
-// item with one atomic add.  A taken item never waits on anything, so there
-// is no deadlock whatever the residency; every workgroup leaves when all B
-// starts are finished (or, as a guard, after timeout_ticks of s_memrealtime).
-// Results are bit-identical to the launch-per-kernel loop: same queries,
-// same search (splits never change answers), same sums in the same order.
-// Hand-offs (MI355X_MICROARCH.md, inter-workgroup visibility, "sc1 loads in
-// place of the acquire"): every word another workgroup reads inside the
-// launch (best, prevnn, partials, pose, tickets, sched) is stored and loaded
-// by relaxed agent-scope atomics (global sc1: write-through, L1 bypassed);
-// every storing wave drains (s_waitcnt vmcnt(0)) and the workgroup barrier
-// precedes the one lane's ticket add / publish; the receiver is told by the
-// value its own atomic returned and loads only after it.  Device-local
-// memory is never stale in another XCD's L2 (probes), so no L2 write-back or
-// invalidate is needed; option persist_fences adds agent release / acquire
-// fences around every hand-off (A/B: identical results, slower).
-// --------------------------------------------------------------------------
-struct PersistArgs {
-    // search
-    const double* src;  // source xyz64, Morton order
-    int N;
-    const float4 *p4, *tlo, *thi, *qbox, *slo, *shi;
-    int ntiles, nsuper, super_cull, seed_stride, reseed;
-    float r2s;
-    Org3 org;
-    // accumulation
-    const double *scov, *tgt64, *tcov;
-    double r2;
-    unsigned long long* best;
-    int32_t* prevnn;
-    double* partial;
-    // solve
-    SolveArgs a;
-    int max_iter;
-    double rel_fit, rel_rmse;
-    // schedule
-    unsigned long long* sched;  // per start: (pass << 40) | (S << 32) | next item
-    int32_t* tick_blk;          // per (start, accumulation block): search items arrived
-    int32_t* tick_start;        // per start: accumulation blocks arrived
-    int32_t* pctl;              // [0] finished starts, [1] error (timeout)
-    int B, sblk, nblk, want_items;
-    long long timeout_ticks;
-    unsigned long long* counters;
-    int fences;  // agent release / acquire fences around every hand-off (A/B; see above)
-};
-
-__host__ __device__ __forceinline__ int sched_pass(unsigned long long v) { return (int)(v >> 40); }
-__host__ __device__ __forceinline__ int sched_splits(unsigned long long v) { return (int)((v >> 32) & 0xffu); }
-__host__ __device__ __forceinline__ unsigned sched_item(unsigned long long v) { return (unsigned)v; }
-__host__ __device__ __forceinline__ unsigned long long sched_word(int pass, int S) {
-    return ((unsigned long long)pass << 40) | ((unsigned long long)S << 32);
-}
-// tile splits of a pass: about want_items search items over the running starts
-__host__ __device__ __forceinline__ int persist_splits(int nact, int sblk, int want_items) {
-    const int per = max(1, nact) * sblk;
-    return min(64, max(1, (want_items + per - 1) / per));
-}
-
-__device__ __forceinline__ unsigned long long readlane_u64(unsigned long long v, int k) {
-    const unsigned lo = __builtin_amdgcn_readlane((unsigned)v, k);
-    const unsigned hi = __builtin_amdgcn_readlane((unsigned)(v >> 32), k);
-    return ((unsigned long long)hi << 32) | lo;
-}
-
-// One search item: the 512 queries of query block grp (wave w: 128 of
-// them), tile split `split` of S.  Queries formed as xform_queries_kernel
-// does, searched as nn_search_kernel does, merged into best[].
-__device__ __forceinline__ void persist_search_item(const PersistArgs& P, int slot, int S, int grp, int split,
-                                                 float4* stage_w) {
-    const int lane = threadIdx.x & 63, wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int N = P.N;
-    const float4 s0lo = lane < P.nsuper ? P.slo[lane] : make_float4(0.f, 0.f, 0.f, 0.f);
-    const float4 s0hi = lane < P.nsuper ? P.shi[lane] : make_float4(0.f, 0.f, 0.f, 0.f);
-    double Q[12];
-#pragma unroll
-    for (int t = 0; t < 12; ++t) {  // wave-uniform: kept in scalar registers
-        const unsigned long long v = ld_u64<true>(reinterpret_cast<const unsigned long long*>(P.a.Q) + 12 * slot + t);
-        Q[t] = __longlong_as_double((long long)readlane_u64(v, 0));
-    }
-    const int i0 = grp * kCBlockQ + wid * (64 * kCQPT) + lane;
-    float qx[kCQPT], qy[kCQPT], qz[kCQPT], bound[kCQPT], bd[kCQPT];
-    int bj[kCQPT];
-#pragma unroll
-    for (int k = 0; k < kCQPT; ++k) {
-        const int i = i0 + 64 * k;
-        float x = 0.f, y = 0.f, z = 0.f, b = 0.0f;  // past N: bound 0, never takes anything
-        if (i < N) {
-            const double p[3] = {P.src[3 * i], P.src[3 * i + 1], P.src[3 * i + 2]};
-            double q[3];
-            xform(Q, p, q);
-            x = (float)(q[0] - P.org.x), y = (float)(q[1] - P.org.y), z = (float)(q[2] - P.org.z);
-            b = P.r2s;
-            const int jp = ld_i32<true>(P.prevnn + (size_t)slot * N + i);
-            if (jp >= 0) {
-                b = fminf(b, seed_bound(d2f(x, y, z, P.p4[jp])));
-            } else if (jp == kNoSeed || P.reseed) {
-                for (int t = 0; t < P.ntiles; t += P.seed_stride)
-                    b = fminf(b, seed_bound(d2f(x, y, z, P.p4[t * kTile])));
-            }
-        }
-        qx[k] = x;
-        qy[k] = y;
-        qz[k] = z;
-        bound[k] = b;
-    }
-    const int visited = culled_search<false>(stage_w, P.p4, P.tlo, P.thi, P.qbox, P.ntiles, P.slo, P.shi, P.nsuper,
-                                             P.super_cull, S, split, qx, qy, qz, bound, bd, bj, s0lo, s0hi);
-    if (lane == 0 && P.counters) {
-        unsigned long long* cs = P.counters + kCounterStride * ((blockIdx.x * kCWaves + wid) % kCounterSlots);
-        atomicAdd(cs, (unsigned long long)visited);
-        atomicMax(cs + 1, (unsigned long long)visited);
-    }
-    unsigned long long* out = P.best + (size_t)slot * N;
-#pragma unroll
-    for (int k = 0; k < kCQPT; ++k) {
-        const int i = i0 + 64 * k;
-        if (i >= N || bj[k] < 0) continue;  // best[] holds kNone already
-        const unsigned long long v = ((unsigned long long)__float_as_uint(bd[k]) << 32) | (unsigned)bj[k];
-        if (S == 1)
-            st_u64<true>(out + i, v);
-        else
-            __hip_atomic_fetch_min(out + i, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-}
-
-// Accumulation block ablk of start slot (the whole workgroup), as
-// gicp_accum_kernel / p2p_accum_kernel: its partial, next seeds, best[] reset.
-template <int kEst>
-__device__ __forceinline__ void persist_accumulate(const PersistArgs& P, int slot, int ablk) {
-    constexpr int NV = kEst == kEstGICP ? kNacc : kP2PTerms;
-    __shared__ double red[4][NV];
-    double acc[NV];
-    double* part = P.partial + ((size_t)slot * P.nblk + ablk) * kPartialStride;
-    if constexpr (kEst == kEstGICP) {
-        gicp_block_terms<true>(slot, ablk, P.src, P.scov, P.N, P.tgt64, P.tcov, P.a.Q, P.a.R, P.r2, P.best, P.prevnn,
-                               acc);
-        block_partial<NV, true>(acc, red, [](int v) { return v; }, part);
-    } else {
-        p2p_block_terms<true>(slot, ablk, P.src, P.N, P.tgt64, P.a.Q, P.r2, P.best, P.prevnn, acc);
-        block_partial<NV, true>(acc, red, p2p_slot, part);
-    }
-}
-
-// The start's reduction, convergence test and solve (wave 0), as
-// icp_solve_kernel; then pass + 1 is published, or the start counted done.
-template <int kEst>
-__device__ __forceinline__ void persist_solve(const PersistArgs& P, int slot, int pass) {
-    const int lane = threadIdx.x & 63;
-    double s[kNacc];
-    reduce_partials<true>(P.partial, slot, P.nblk, s);
-    const bool fin = solve_start<kEst, true>(slot, s, P.N, pass, P.max_iter, P.rel_fit, P.rel_rmse, P.a);
-    if (lane != 0) return;
-    st_i32<true>(P.tick_start + slot, 0);
-    if (P.fences) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the pose (sc1) has landed before the publish
-    if (fin) {
-        __hip_atomic_fetch_add(P.pctl, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    } else {
-        const int nact = P.B - ld_i32<true>(P.pctl);
-        __hip_atomic_store(P.sched + slot, sched_word(pass + 1, persist_splits(nact, P.sblk, P.want_items)),
-                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-}
-
-// Wave 0: the next search item (slot, pass, splits, item), slot -1 when all
-// starts are done (or on the timeout guard).
-__device__ __forceinline__ void persist_take(const PersistArgs& P, long long t_begin, int* sh) {
-    const int lane = threadIdx.x & 63;
-    int gb = -1;
-    unsigned long long gv = 0;
-    const int rot = (int)((blockIdx.x * 7u) & 63u);  // spread the workgroups over the starts
-    for (;;) {
-        if (ld_i32<true>(P.pctl) >= P.B || ld_i32<true>(P.pctl + 1) != 0) break;
-        for (int b0 = 0; b0 < P.B && gb < 0; b0 += 64) {
-            const int b = b0 + lane;
-            bool av = false;
-            if (b < P.B) {
-                const unsigned long long v = ld_u64<true>(P.sched + b);
-                av = sched_item(v) < (unsigned)(P.sblk * sched_splits(v));
-            }
-            unsigned long long m = __ballot(av);
-            while (m) {
-                const unsigned long long mr = rot ? ((m >> rot) | (m << (64 - rot))) : m;
-                const int k = (__builtin_ctzll(mr) + rot) & 63;
-                m &= ~(1ull << k);
-                unsigned long long old = 0;
-                if (lane == k)
-                    old = __hip_atomic_fetch_add(P.sched + b0 + k, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                old = readlane_u64(old, k);
-                if (sched_item(old) < (unsigned)(P.sblk * sched_splits(old))) {
-                    gb = b0 + k;
-                    gv = old;
-                    break;
-                }
-            }
-        }
-        if (gb >= 0) break;
-        if ((long long)__builtin_amdgcn_s_memrealtime() - t_begin > P.timeout_ticks) {
-            if (lane == 0) st_i32<true>(P.pctl + 1, 1);
-            break;
-        }
-        __builtin_amdgcn_s_sleep(8);
-    }
-    if (lane == 0) {
-        sh[0] = gb;
-        sh[1] = sched_pass(gv);
-        sh[2] = sched_splits(gv);
-        sh[3] = (int)sched_item(gv);
-    }
-    if (gb >= 0 && P.fences) {  // the pose / seeds of the pass were published before the item
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-}
-
-// tid 0: arrive at a ticket after every wave's stores have landed (release);
-// returns (to every thread, through sh_last) whether this was the last of
-// `expect` arrivals, the last arriver having taken the acquire.
-__device__ __forceinline__ bool persist_arrive(int32_t* ticket, int expect, int32_t* reset, int* sh_last,
-                                               int fences) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's stores / merges have landed
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        if (reset) st_i32<true>(reset, 0);
-        if (fences) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        const int t = __hip_atomic_fetch_add(ticket, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        const int last = t == expect - 1;
-        if (last && fences) {
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        }
-        *sh_last = last;
-    }
-    __syncthreads();
-    return *sh_last != 0;
-}
-
-template <int kEst>
-__global__ __launch_bounds__(256) void icp_persistent_kernel(PersistArgs P) {
-    __shared__ float4 stage[kCWaves][kTile];
-    __shared__ int sh[4];
-    __shared__ int sh_last;
-    const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const long long t_begin = (long long)__builtin_amdgcn_s_memrealtime();
-    for (;;) {
-        // ---- 1. take the next search item (wave 0)
-        if (wid == 0) persist_take(P, t_begin, sh);
-        __syncthreads();
-        const int slot = __builtin_amdgcn_readfirstlane(sh[0]);
-        if (slot < 0) return;
-        const int pass = __builtin_amdgcn_readfirstlane(sh[1]);
-        const int S = __builtin_amdgcn_readfirstlane(sh[2]);
-        const int bx = __builtin_amdgcn_readfirstlane(sh[3]);
-        const int grp = bx / S, split = bx - grp * S;
-        // ---- 2. the item's queries and culled search
-        persist_search_item(P, slot, S, grp, split, stage[wid]);
-        // ---- 3. arrival at the accumulation block; the last arriver accumulates it
-        const int qpb = 256 * accum_qpt(P.N);  // queries per accumulation block
-        const int ablk = grp * kCBlockQ / qpb;
-        const int q_end = min(P.N, (ablk + 1) * qpb);
-        const int nsearch = (q_end + kCBlockQ - 1) / kCBlockQ - ablk * qpb / kCBlockQ;  // query blocks in it
-        if (!persist_arrive(P.tick_blk + (size_t)slot * P.nblk + ablk, nsearch * S, nullptr, &sh_last, P.fences))
-            continue;
-        persist_accumulate<kEst>(P, slot, ablk);
-        // ---- 4. arrival at the start; the last arriver solves and publishes the next pass
-        if (!persist_arrive(P.tick_start + slot, P.nblk, P.tick_blk + (size_t)slot * P.nblk + ablk, &sh_last,
-                            P.fences))
-            continue;
-        if (wid == 0) persist_solve<kEst>(P, slot, pass);
-    }
 }
 
 // Kernel-level 1-NN (orpcd_nn1_radius): the same culled search on Morton-
@@ -2812,15 +1677,6 @@ int search_splits(int nact, int blocks_per_start, int want) {
 
 int accum_blocks(int64_t N) { return (int)((N + 256 * accum_qpt(N) - 1) / (256 * accum_qpt(N))); }
 
-// the cooperative search needs 16-bit tile ids in its LDS candidate list
-static bool use_coop(const orpcd_ctx* c) {
-    return c->opt.search_kernel == 1 && c->tgt.ntiles <= 65535 && c->batch_ntgt == 1;
-}
-// the two-phase search keeps a candidate list of every query group
-static bool use_two_phase(const orpcd_ctx* c) {
-    return c->opt.search_kernel == 2 && c->two_phase_ok && c->batch_ntgt == 1;
-}
-
 // uniform splits of a launch over nact running starts (the pass-0 split of
 // the ordered dispatch too)
 static int uniform_splits(const orpcd_ctx* c, int nact) {
@@ -2829,18 +1685,13 @@ static int uniform_splits(const orpcd_ctx* c, int nact) {
     return search_splits(nact, sblk, want);
 }
 
-// the ordered dispatch serves the default per-kernel pass loop (not the
-// cooperative / two-phase searches, the persistent or the pipelined loops)
-// of batches of at least sched_min_starts starts: below that its planning
+// the ordered dispatch serves batches of at least sched_min_starts starts:
+// below that its planning
 // (one block per start, beside the transform) and the wave's item lookup
 // cost more than the order gains (C2: 1 start 0.53 -> 0.65 ms, 8 starts
 // 4.53 -> 4.59 ms; 30 starts 16.6 -> 15.0 ms, 104 starts 43.7 -> 37.8 ms;
 // C5 1 start 1478 -> 1304 iterations/s)
-bool sched_wanted(const orpcd_ctx* c, bool persist, int B) {
-    static const bool trace = getenv("ORPCD_TRACE") != nullptr;
-    return c->opt.sched && B >= c->opt.sched_min_starts && c->opt.search_kernel == 0 && !persist &&
-           (trace || !pipelined_ok(c));
-}
+bool sched_wanted(const orpcd_ctx* c, int B) { return c->opt.sched && B >= c->opt.sched_min_starts; }
 
 // items per class: every item of a pass may fall in one class.  Pass 0:
 // S0 * groups <= search_waves + groups (search_splits rounds up); later
@@ -2888,14 +1739,12 @@ static ExactArgs exact_args(const orpcd_ctx* c, int pass) {
 #endif
 constexpr int kExactBlocks = ORPCD_EXACT_BLOCKS;  // re-search grid: 1024 waves, 64 listed queries per wave and round
 
-hipError_t launch_xform(const orpcd_ctx* c, int nact, int pass, double r2, hipStream_t s, bool dev_nact,
-                        const TgtBounds& tb) {
-    if (use_coop(c) || use_two_phase(c)) return hipSuccess;  // these searches transform their own queries
+hipError_t launch_xform(const orpcd_ctx* c, int nact, int pass, double r2, hipStream_t s, const TgtBounds& tb) {
     const int N = (int)c->src.n;
-    const SchedX sx = dev_nact ? SchedX{} : sched_x(c, nact, pass);
+    const SchedX sx = sched_x(c, nact, pass);
     xform_queries_kernel<<<dim3((unsigned)((N + 255) / 256) + (sx.list ? 1u : 0u), (unsigned)nact), 256, 0, s>>>(
         c->src.xyz64.p, N, c->active.p, c->Q.p, c->done.p, c->tdesc.p, tb, c->prevnn.p, search_r2(r2),
-        c->opt.reseed, c->q32.p, c->best.p, dev_nact ? c->ctl.p : nullptr, c->gbox.p, sx, exact_args(c, pass));
+        c->opt.reseed, c->q32.p, c->best.p, c->gbox.p, sx, exact_args(c, pass));
     return hipGetLastError();
 }
 
@@ -2939,46 +1788,6 @@ static SolveArgs solve_args(const orpcd_ctx* c) {
                      c->done.p, c->out_fit.p, c->out_rmse.p, c->out_iters.p, c->out_ncorr.p};
 }
 
-bool pipelined_ok(const orpcd_ctx* c) {
-    return !use_coop(c) && !use_two_phase(c) && c->opt.pipeline && c->batch_ntgt == 1 && !c->opt.exact_nn;
-}
-
-// One pipelined pass (see PassCtl): search over the device's running starts,
-// accumulation with the fused solve + compaction, the next pass's queries.
-// nact_host is an upper bound of the running starts (grid sizes only).
-hipError_t launch_gicp_pass_pipelined(const orpcd_ctx* c, int nact_host, int pass, const orpcd_gicp_params& p,
-                                      hipStream_t s, hipEvent_t mid, hipEvent_t after_accum) {
-    const int N = (int)c->src.n;
-    const double r2 = p.max_correspondence_distance * p.max_correspondence_distance;
-    const int sblk = (N + kCBlockQ - 1) / kCBlockQ;
-    const int want = c->opt.search_waves;
-    const int S = search_splits(nact_host, sblk, want);
-    const int64_t grid = std::max<int64_t>((int64_t)nact_host * sblk * S, (want + kCWaves - 1) / kCWaves);
-    hipError_t e;
-    auto kern = c->opt.search_occupancy == 6 ? nn_search_kernel_o6 : nn_search_kernel<false>;
-    const TgtBounds tb = one_target();  // pipelined passes: single-target batches only
-    kern<<<dim3((unsigned)grid), kCBlock, 0, s>>>(c->q32.p, N, c->tdesc.p, tb, c->opt.super_cull, c->active.p,
-                                                  c->done.p, 1, c->best.p, c->count_tiles ? c->counters.p : nullptr,
-                                                  c->ctl.p, sblk, want, c->gbox.p, ExactArgs{});
-    if ((e = hipGetLastError()) != hipSuccess) return e;
-    if (mid && (e = hipEventRecord(mid, s)) != hipSuccess) return e;
-    const int ablk = accum_blocks(N);
-    const PassCtl pc{c->ctl.p,          c->prog_d,          c->active.p, pass, p.max_iteration, p.relative_fitness,
-                     p.relative_rmse, (int64_t)N, solve_args(c)};
-    if (c->est == kEstP2P)
-        p2p_accum_kernel<true><<<dim3((unsigned)ablk, (unsigned)nact_host), 256, 0, s>>>(
-            c->src.xyz64.p, N, c->tdesc.p, tb, c->active.p, c->Q.p, c->done.p, r2, c->best.p, c->prevnn.p,
-            c->partial.p, ablk, pc);
-    else
-        gicp_accum_kernel<true><<<dim3((unsigned)ablk, (unsigned)nact_host), 256, 0, s>>>(
-            c->src.xyz64.p, c->scov.p, N, c->tdesc.p, tb, c->active.p, c->Q.p, c->R.p, c->done.p, r2, c->best.p,
-            c->prevnn.p, c->partial.p, ablk, pc);
-    if ((e = hipGetLastError()) != hipSuccess) return e;
-    if (after_accum && (e = hipEventRecord(after_accum, s)) != hipSuccess) return e;
-    if (pass >= p.max_iteration) return hipSuccess;  // every start is done after this pass
-    return launch_xform(c, nact_host, pass + 1, r2, s, true, tb);
-}
-
 #ifdef ORPCD_WAVETIME
 // append the records of the last search launch (n wave slots) to $ORPCD_WAVETIME
 static hipError_t dump_wavetime(int pass, int nact, int S, unsigned n, hipStream_t s) {
@@ -3009,38 +1818,7 @@ hipError_t launch_gicp_pass(const orpcd_ctx* c, int nact, int pass, double r2, h
     const int N = (int)c->src.n;
     const int sblk = (N + kCBlockQ - 1) / kCBlockQ;
     hipError_t e;
-    if (use_two_phase(c)) {
-        const int gblk = (N + kGroupQ - 1) / kGroupQ;
-        const int G = nact * gblk;
-        unsigned* gcount = c->item_counts.p;
-        unsigned* offs = gcount + G;
-        cull_groups_kernel<<<dim3((unsigned)((gblk + 3) / 4), (unsigned)nact), 256, 0, s>>>(
-            c->src.xyz64.p, N, c->Q.p, c->prevnn.p, search_r2(r2), c->opt.reseed, seed_stride_for(c->tgt.ntiles),
-            c->tgt.p4.p, c->tgt.tlo.p, c->tgt.thi.p, (int)c->tgt.ntiles, c->tgt.slo.p, c->tgt.shi.p,
-            (int)c->tgt.nsuper, c->active.p, c->done.p, gblk, c->q32.p, c->best.p, c->items.p, gcount,
-            org_of(c->tgt));
-        if ((e = hipGetLastError()) != hipSuccess) return e;
-        items_prefix_kernel<<<1, 1024, 0, s>>>(gcount, G, offs);
-        if ((e = hipGetLastError()) != hipSuccess) return e;
-        scan_items_kernel<<<(unsigned)c->opt.scan_blocks, 256, 0, s>>>(
-            c->q32.p, N, gblk, c->active.p, c->tgt.p4.p, c->tgt.tlo.p, c->tgt.thi.p, (int)c->tgt.ntiles,
-            c->items.p, offs, G, c->best.p, c->count_tiles ? c->counters.p : nullptr);
-    } else if (use_coop(c)) {
-        const int gblk = (N + kGroupQ - 1) / kGroupQ;  // 128-query groups per start
-        const int64_t groups = (int64_t)nact * gblk;
-        const int W = (int)std::min<int64_t>(kCoopMaxW, std::max<int64_t>(1, (c->opt.search_waves + groups - 1) / groups));
-        const size_t smem = coop_smem_bytes(W, c->tgt.ntiles);
-        if (smem > 32 * 1024) {  // large targets: raise the dynamic LDS limit of the launch
-            if ((e = hipFuncSetAttribute((const void*)nn_search_coop_kernel,
-                                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem)) != hipSuccess)
-                return e;
-        }
-        nn_search_coop_kernel<<<dim3((unsigned)gblk, (unsigned)nact), 64 * W, smem, s>>>(
-            c->src.xyz64.p, N, c->Q.p, c->prevnn.p, search_r2(r2), c->opt.reseed, seed_stride_for(c->tgt.ntiles),
-            c->tgt.p4.p, c->tgt.tlo.p, c->tgt.thi.p, (int)c->tgt.ntiles, c->tgt.slo.p, c->tgt.shi.p,
-            (int)c->tgt.nsuper, c->active.p, c->done.p, c->best.p, c->count_tiles ? c->counters.p : nullptr,
-            org_of(c->tgt));
-    } else if (c->sched_live) {
+    if (c->sched_live) {    } else if (c->sched_live) {
         // ordered dispatch: the items were filed by this pass's query transform;
         // the grid covers their upper bound (surplus waves exit at once)
         const int64_t NG = (N + 127) / 128;
@@ -3070,13 +1848,11 @@ hipError_t launch_gicp_pass(const orpcd_ctx* c, int nact, int pass, double r2, h
     // few running starts: half the wave target (8 starts: 16k waves 8.16 ms vs
     // 32k 8.40 ms per batch; 30 starts keep 32k).  Splits never change answers.
     const int S = uniform_splits(c, nact);
-    const int want = nact <= c->opt.small_batch ? c->opt.search_waves / 2 : c->opt.search_waves;
     // best[] was reset to kNone by xform_queries_kernel
-    auto kern = c->exact_live ? nn_search_kernel<true>
-                : c->opt.search_occupancy == 6 ? nn_search_kernel_o6 : nn_search_kernel<false>;
+    auto kern = c->exact_live ? nn_search_kernel<true> : nn_search_kernel<false>;
     kern<<<dim3((unsigned)(sblk * S), (unsigned)nact), kCBlock, 0, s>>>(
         c->q32.p, N, c->tdesc.p, tb, c->opt.super_cull, c->active.p, c->done.p, S, c->best.p,
-        c->count_tiles ? c->counters.p : nullptr, nullptr, sblk, want, c->gbox.p, exact_args(c, pass));
+        c->count_tiles ? c->counters.p : nullptr, c->gbox.p, exact_args(c, pass));
 #ifdef ORPCD_WAVETIME
     if ((e = dump_wavetime(pass, nact, S, (unsigned)(sblk * S) * (unsigned)nact * kCWaves, s)) != hipSuccess) return e;
 #endif
@@ -3090,38 +1866,20 @@ hipError_t launch_gicp_pass(const orpcd_ctx* c, int nact, int pass, double r2, h
     if (mid && (e = hipEventRecord(mid, s)) != hipSuccess) return e;
     const int ablk = accum_blocks(N);
     if (c->est == kEstP2P) {
-        p2p_accum_kernel<false><<<dim3((unsigned)ablk, (unsigned)nact), 256, 0, s>>>(
+        p2p_accum_kernel<<<dim3((unsigned)ablk, (unsigned)nact), 256, 0, s>>>(
             c->src.xyz64.p, N, c->tdesc.p, tb, c->active.p, c->Q.p, c->done.p, r2, c->best.p, c->prevnn.p,
-            c->partial.p, ablk, PassCtl{});
+            c->partial.p, ablk);
         return hipGetLastError();
     }
-    gicp_accum_kernel<false><<<dim3((unsigned)ablk, (unsigned)nact), 256, 0, s>>>(
+    gicp_accum_kernel<<<dim3((unsigned)ablk, (unsigned)nact), 256, 0, s>>>(
         c->src.xyz64.p, c->scov.p, N, c->tdesc.p, tb, c->active.p, c->Q.p, c->R.p, c->done.p, r2, c->best.p,
-        c->prevnn.p, c->partial.p, ablk, PassCtl{});
+        c->prevnn.p, c->partial.p, ablk);
     return hipGetLastError();
 }
 
 hipError_t launch_gicp_solve(const orpcd_ctx* c, int nact, int pass, const orpcd_gicp_params& p, hipStream_t s,
                              const TgtBounds& tb) {
     const SolveArgs a = solve_args(c);
-    if (c->fuse_live) {  // one launch: the solve and the next pass's queries (solve_xform_kernel)
-        const int N = (int)c->src.n;
-        const double r2 = p.max_correspondence_distance * p.max_correspondence_distance;
-        const SchedX sx = sched_x(c, nact, pass + 1);
-        const FuseArgs f{c->partial.p,    accum_blocks(N), pass, p.max_iteration, p.relative_fitness,
-                         p.relative_rmse, (int64_t)N,      a,    c->ready.p,      c->fuse_err.p,
-                         nact};
-        const dim3 grid((unsigned)((int64_t)nact * ((N + 255) / 256 + (sx.list ? 2 : 1))));
-        if (c->est == kEstP2P)
-            solve_xform_kernel<kEstP2P><<<grid, 256, 0, s>>>(c->src.xyz64.p, N, c->active.p, c->tdesc.p, tb,
-                                                              c->prevnn.p, search_r2(r2), c->opt.reseed, c->q32.p,
-                                                              c->best.p, c->gbox.p, sx, f);
-        else
-            solve_xform_kernel<kEstGICP><<<grid, 256, 0, s>>>(c->src.xyz64.p, N, c->active.p, c->tdesc.p, tb,
-                                                               c->prevnn.p, search_r2(r2), c->opt.reseed, c->q32.p,
-                                                               c->best.p, c->gbox.p, sx, f);
-        return hipGetLastError();
-    }
     auto solve = c->est == kEstP2P ? icp_solve_kernel<1> : icp_solve_kernel<0>;
     solve<<<(unsigned)nact, 64, 0, s>>>(c->active.p, c->partial.p, accum_blocks(c->src.n), nullptr,
                                                     c->src.n, pass, p.max_iteration, p.relative_fitness,
@@ -3129,74 +1887,7 @@ hipError_t launch_gicp_solve(const orpcd_ctx* c, int nact, int pass, const orpcd
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     const double r2 = p.max_correspondence_distance * p.max_correspondence_distance;
-    return launch_xform(c, nact, pass + 1, r2, s, false, tb);  // queries of the next pass (done starts skip)
-}
-
-// Resident 256-thread workgroups of the persistent kernel on this device.
-int persist_grid(int device, int est) {
-    int per_cu = 0, cus = 0;
-    const void* f = est == kEstP2P ? (const void*)icp_persistent_kernel<kEstP2P>
-                                   : (const void*)icp_persistent_kernel<kEstGICP>;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, f, 256, 0) != hipSuccess) return 0;
-    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess) return 0;
-    return per_cu * cus;
-}
-
-int persist_first_splits(const orpcd_ctx* c, int B, int grid) {
-    const int sblk = (int)((c->src.n + kCBlockQ - 1) / kCBlockQ);
-    return persist_splits(B, sblk, c->opt.persist_items > 0 ? c->opt.persist_items : grid);
-}
-
-unsigned long long persist_sched_word(int pass, int S) { return sched_word(pass, S); }
-
-// The persistent pass loop of the batch set up by batch_setup (sched[] holds
-// pass 0 of every start, the tickets and pctl are zero, best[] is kNone).
-hipError_t launch_icp_persistent(const orpcd_ctx* c, int B, int grid, const orpcd_gicp_params& p, hipStream_t s) {
-    const int N = (int)c->src.n;
-    const double r2 = p.max_correspondence_distance * p.max_correspondence_distance;
-    PersistArgs P{};
-    P.src = c->src.xyz64.p;
-    P.N = N;
-    P.p4 = c->tgt.p4.p;
-    P.tlo = c->tgt.tlo.p;
-    P.thi = c->tgt.thi.p;
-    P.qbox = c->tgt.qbox.p;
-    P.slo = c->tgt.slo.p;
-    P.shi = c->tgt.shi.p;
-    P.ntiles = (int)c->tgt.ntiles;
-    P.nsuper = (int)c->tgt.nsuper;
-    P.super_cull = c->opt.super_cull;
-    P.seed_stride = seed_stride_for(c->tgt.ntiles, c->opt.seed_reps);
-    P.reseed = c->opt.reseed;
-    P.r2s = search_r2(r2);
-    P.org = org_of(c->tgt);
-    P.scov = c->scov.p;
-    P.tgt64 = c->tgt.xyz64.p;
-    P.tcov = c->tcov.p;
-    P.r2 = r2;
-    P.best = c->best.p;
-    P.prevnn = c->prevnn.p;
-    P.partial = c->partial.p;
-    P.a = solve_args(c);
-    P.max_iter = p.max_iteration;
-    P.rel_fit = p.relative_fitness;
-    P.rel_rmse = p.relative_rmse;
-    P.sched = c->sched.p;
-    P.tick_blk = c->tick_blk.p;
-    P.tick_start = c->tick_start.p;
-    P.pctl = c->pctl.p;
-    P.B = B;
-    P.sblk = (N + kCBlockQ - 1) / kCBlockQ;
-    P.nblk = accum_blocks(N);
-    P.want_items = c->opt.persist_items > 0 ? c->opt.persist_items : grid;
-    P.timeout_ticks = (long long)c->opt.persist_timeout_s * 100000000LL;  // s_memrealtime: 100 MHz
-    P.counters = c->count_tiles ? c->counters.p : nullptr;
-    P.fences = c->opt.persist_fences;
-    if (c->est == kEstP2P)
-        icp_persistent_kernel<kEstP2P><<<(unsigned)grid, 256, 0, s>>>(P);
-    else
-        icp_persistent_kernel<kEstGICP><<<(unsigned)grid, 256, 0, s>>>(P);
-    return hipGetLastError();
+    return launch_xform(c, nact, pass + 1, r2, s, tb);  // queries of the next pass (done starts skip)
 }
 
 hipError_t launch_reduce_partials(const orpcd_ctx* c, int slot, double* sums29, hipStream_t s) {
@@ -3212,7 +1903,7 @@ hipError_t launch_gicp_solve_sums(const orpcd_ctx* c, const double* sums29, int6
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     const double r2 = p.max_correspondence_distance * p.max_correspondence_distance;
-    return launch_xform(c, 1, pass + 1, r2, s, false, one_target());
+    return launch_xform(c, 1, pass + 1, r2, s, one_target());
 }
 
 hipError_t launch_nn1(const double* q, int64_t nq, const CloudLayout& t, double r2, int32_t* idx, double* d2,

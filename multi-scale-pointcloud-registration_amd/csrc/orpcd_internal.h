@@ -228,9 +228,6 @@ struct orpcd_ctx {
     orpcd::DevBuf<double> scov;     // B*N*6 posed-frame source covariance
     orpcd::DevBuf<int32_t> prevnn;  // B*N previous correspondence (Morton target index)
     orpcd::DevBuf<unsigned long long> best;  // B*N packed (d^2 bits, target) of the current pass
-    orpcd::DevBuf<unsigned> items;           // two-phase search: candidate tiles per query group
-    orpcd::DevBuf<unsigned> item_counts;     // per group: candidate count, then the exclusive offsets
-    bool two_phase_ok = false;               // the batch's worst-case item list fits
     orpcd::DevBuf<float4> q32;      // B*N fp32 queries of the current pass (x,y,z,0)
     orpcd::DevBuf<float4> gbox;     // B*ceil(N/128)*2: per search wave, its queries' box + worst bound
     orpcd::DevBuf<double> G;        // B*12 base pose (3x4, column convention)
@@ -241,15 +238,6 @@ struct orpcd_ctx {
     orpcd::DevBuf<double> partial;  // B*nblk*32
     orpcd::DevBuf<int32_t> done;    // B
     orpcd::DevBuf<int32_t> active;  // B
-    orpcd::DevBuf<int32_t> ctl;     // 2 + B: pipelined pass control (gicp_kernels.hip, PassCtl)
-    unsigned long long* prog_h = nullptr;  // host-mapped progress word of the pipelined passes
-    unsigned long long* prog_d = nullptr;  // its device address
-    // persistent pass loop (gicp_kernels.hip, icp_persistent_kernel)
-    orpcd::DevBuf<unsigned long long> sched;  // B: (pass << 40) | (splits << 32) | next search item
-    orpcd::DevBuf<int32_t> tick_blk;          // B*nblk: search items arrived per accumulation block
-    orpcd::DevBuf<int32_t> tick_start;        // B: accumulation blocks arrived per start
-    orpcd::DevBuf<int32_t> pctl;              // [0] finished starts, [1] error flag
-    int persist_grid[2] = {0, 0};             // resident workgroups (GICP, PointToPoint kernels)
     orpcd::DevBuf<double> out_fit, out_rmse;
     orpcd::DevBuf<int32_t> out_iters;
     orpcd::DevBuf<int64_t> out_ncorr;
@@ -266,10 +254,6 @@ struct orpcd_ctx {
     int sched_cap = 0;
     int sched_B = 0;                             // starts of the batch (wcost parity stride B x NG)
     bool sched_live = false;                     // the running batch uses the ordered dispatch
-    // fused solve + query transform (opt.fuse_solve; gicp_kernels.hip, solve_xform_kernel)
-    orpcd::DevBuf<int32_t> ready;                // B: the last pass whose pose the solver published
-    orpcd::DevBuf<unsigned> fuse_err;            // 1: a transform block's wait for its solver timed out
-    bool fuse_live = false;                      // the running batch uses it
     // exact nearest neighbours (opt.exact_nn): queries the fp32 search cannot
     // certify are filed and re-searched in fp64 (nn_exact_kernel)
     orpcd::DevBuf<unsigned> xsec;                // B x N: runner-up key near the winner (0xFFFFFFFF: none)
@@ -278,6 +262,8 @@ struct orpcd_ctx {
     orpcd::DevBuf<unsigned long long> xtotal;    // queries re-searched in fp64 (statistics)
     bool exact_live = false;                     // the running batch runs exact
     int last_B = 0;                              // starts of the last batch (orpcd_gicp_correspondences)
+    std::vector<int> last_slot;                  // its start b -> slot (caller order -> target-ordered slots)
+    std::vector<int> last_slot_tgt;              // its slot -> target index
 
     // kernel-level entry points
     orpcd::CloudLayout aux;
@@ -286,7 +272,6 @@ struct orpcd_ctx {
 
     orpcd::HostBuf<double> h64;
     orpcd::HostBuf<int32_t> h32;
-    orpcd::HostBuf<unsigned long long> h64sched;  // staging of the persistent loop's sched[] / pctl
 
     // FastGlobal path (fgr_kernels.hip); index 0 = source, 1 = target
     struct FgrBufs {
@@ -326,44 +311,19 @@ struct orpcd_ctx {
         int sync_every = 8;       // passes between host checks of the done flags (C2 sweep: 4 17.6 ms, 8-16 17.3)
         int super_cull = 1;       // first culling level over 64-tile super-tiles
         int reseed = 0;           // representative seeding also after pass 0
-        int search_occupancy = 0; // 0: compiler's register budget; 6: capped at 6 waves/SIMD
-        int search_kernel = 0;    // 0: split search (measured best, tools/ab_search.py);
-                                  // 1: cooperative (one workgroup per query group, queries fused);
-                                  // 2: two-phase (cull once per group, persistent scan of the items)
-        int scan_blocks = 1280;   // persistent grid of the two-phase scan (256-thread blocks)
-        int pipeline = 0;         // 1: passes enqueued ahead, running starts kept on the device;
-                                  // 0: host sync every sync_every passes (also under ORPCD_TRACE)
-        int lookahead = 4;        // pipelined: passes enqueued beyond the last one known complete
         int seed_reps = 64;       // pass-0 seed: nearest of ~this many tile representatives per query
                                   // (C2 sweep 8..512: equal within noise; 64 keeps the transform cheap)
-        int persist = 0;          // 1: the whole ICP loop in one persistent launch (icp_persistent_kernel):
-                                  // bit-identical, but slower at C2 (1 / 8 / 30 / 64 starts: 0.76 / 8.3 /
-                                  // 26.8 / 37.3 ms vs 0.52 / 4.7 / 16.2 / 26.9): its 190 VGPRs allow 2
-                                  // waves/SIMD, so a pass's search gets far fewer tile splits than the
-                                  // 16k-32k dispatched waves of nn_search_kernel.  0: one launch per kernel
-        int persist_items = 0;    // search items per pass to aim for (0: the resident workgroups)
-        int persist_timeout_s = 60;  // guard: the persistent loop gives up (error) after this long
-        int persist_fences = 0;   // 1: agent release/acquire fences around the persistent loop's hand-offs
         int sched = 1;            // 1: search waves dispatched heaviest first, heavy query groups split
                                   // further (costs measured in the previous pass); 0: uniform splits
         int sched_items = 10240;  // ordered dispatch: split a group until its waves cost <= pass total / this
                                   // (C2 sweep 5120 / 10240 / 20480: 15.4 / 15.0 / 16.6 ms at 30 starts)
         int sched_min_starts = 16;  // ordered dispatch only for batches of at least this many starts
-        int exact_nn = 0;         // 1: every correspondence is the fp64 nearest target (the oracle's
-                                  // lexicographic (d^2, input index) minimum): fp32 search + runner-up
-                                  // band test + fp64 re-search of the uncertified queries
-        int fuse_solve = 0;       // 1: the 6x6 solve runs inside the next pass's query transform launch
-                                  // (bit-identical; measured slower at C2: 30 starts 15.05 -> 15.45 ms)
-        int sync_lag = 0;         // 1: the host check of the done flags lags one sync interval: the flags
-                                  // are copied and an event recorded, and the host waits on the PREVIOUS
-                                  // interval's event, so the stream never drains at a check (finished
-                                  // starts' blocks exit as between checks).  Bit-identical; measured equal
-                                  // at C2 (30 starts 15.0 ms either way) and slower for 8 starts (4.61 ->
-                                  // 4.84 ms: up to two intervals of empty passes after the last start
-                                  // converges).  0: drain and check
+        int exact_nn = 1;         // 1 (default): every correspondence is the fp64 nearest target (the
+                                  // oracle's lexicographic (d^2, input index) minimum): fp32 search +
+                                  // runner-up band test + fp64 re-search of the uncertified queries;
+                                  // 0: the fp32 search's answer (ties within 2^-17 relative by position)
     } opt;
     std::vector<hipEvent_t> ev_pool;
-    hipEvent_t sync_ev[2] = {nullptr, nullptr};  // lagged done-flag checks (sync_lag)
     orpcd::KernelStats stats;
 
     // row-sharded single start (orpcd_gicp_shard_*)
@@ -403,17 +363,13 @@ hipError_t launch_fps(const double* xyz, int64_t n, int first, int k, int max_bl
 
 // gicp_kernels.hip
 int accum_blocks(int64_t N);
-hipError_t launch_xform(const orpcd_ctx* c, int nact, int pass, double r2, hipStream_t s, bool dev_nact,
-                        const TgtBounds& tb);
-bool sched_wanted(const orpcd_ctx* c, bool persist, int B);
+hipError_t launch_xform(const orpcd_ctx* c, int nact, int pass, double r2, hipStream_t s, const TgtBounds& tb);
+bool sched_wanted(const orpcd_ctx* c, int B);
 int sched_capacity(const orpcd_ctx* c, int B);
 TgtBounds one_target();
 // bounds of the launch rows act[0..nact) (increasing slots) over the batch's targets
 TgtBounds target_bounds(const orpcd_ctx* c, const int32_t* act, int nact);
 void write_target_desc(const CloudLayout& L, const double* tcov, int seed_reps, TargetDesc& d);
-bool pipelined_ok(const orpcd_ctx* c);
-hipError_t launch_gicp_pass_pipelined(const orpcd_ctx* c, int nact_host, int pass, const orpcd_gicp_params& p,
-                                      hipStream_t s, hipEvent_t mid, hipEvent_t after_accum);
 hipError_t launch_gicp_pass(const orpcd_ctx* c, int nact, int pass, double r2, hipStream_t s, hipEvent_t mid,
                             const TgtBounds& tb);
 hipError_t launch_gicp_solve(const orpcd_ctx* c, int nact, int pass, const orpcd_gicp_params& p, hipStream_t s,
@@ -424,10 +380,6 @@ hipError_t launch_gicp_solve_sums(const orpcd_ctx* c, const double* sums29, int6
 hipError_t launch_nn1(const double* q, int64_t nq, const CloudLayout& t, double r2, int32_t* idx, double* d2,
                       hipStream_t s);
 hipError_t launch_solve6_test(const double* sums, int n, double* out_serial, double* out_wave, hipStream_t s);
-int persist_grid(int device, int est);
-int persist_first_splits(const orpcd_ctx* c, int B, int grid);
-unsigned long long persist_sched_word(int pass, int S);
-hipError_t launch_icp_persistent(const orpcd_ctx* c, int B, int grid, const orpcd_gicp_params& p, hipStream_t s);
 
 // fgr_kernels.hip
 constexpr int kFeatDim = 36;  // 33 FPFH bins padded for the 16x16x4 f64 MFMA

@@ -2,14 +2,12 @@
 // and the batched GICP driver.  Host orchestration only; all arithmetic on
 // the hot path runs in the kernels of knn_kernels.hip / gicp_kernels.hip.
 #include <algorithm>
-#include <chrono>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <new>
 #include <random>
-#include <thread>
 #include <utility>
 
 #include "orpcd_internal.h"
@@ -32,14 +30,6 @@ using namespace orpcd;
             (ctx)->err = (msg);       \
             return ORPCD_EINVAL;      \
         }                             \
-    } while (0)
-
-#define CTX_REQUIRE_DEV(ctx, cond, msg) \
-    do {                                \
-        if (!(cond)) {                  \
-            (ctx)->err = (msg);         \
-            return ORPCD_EDEVICE;       \
-        }                               \
     } while (0)
 
 namespace {
@@ -374,19 +364,12 @@ int fgr_device(orpcd_ctx* c, const double* src, int64_t n, const double* tgt, in
 // queries.  Host staging in c->h64 / c->h32 (layout used by gicp_batch).
 // init16 != null (PointToPoint refinement): base pose G_b = init16[b] (column
 // convention, as registration_icp applies `init`), no covariances.
-// The whole ICP loop in one persistent launch (icp_persistent_kernel): the
-// default, except under ORPCD_TRACE (per-pass timings need per-pass launches)
-// and for the alternative search kernels.
-bool persistent_ok(const orpcd_ctx* c) {
-    static const bool trace = getenv("ORPCD_TRACE") != nullptr;
-    return c->opt.persist && !trace && c->opt.search_kernel == 0 && !c->opt.exact_nn;
-}
-
 int batch_setup(orpcd_ctx* c, const double* R0, const double* t0, int B, const orpcd_gicp_params* p,
-                const double* init16 = nullptr, bool persist = false) {
+                const double* init16 = nullptr) {
     const int64_t N = c->src.n;
     const int nblk = accum_blocks(N);
     c->last_B = 0;  // set once the batch is set up
+    c->last_slot.clear();
     if (!init16) CTX_CHECK(c, c->scov.ensure((size_t)B * N * 6));
     CTX_CHECK(c, c->prevnn.ensure((size_t)B * N));
     CTX_CHECK(c, c->best.ensure((size_t)B * N));
@@ -398,30 +381,15 @@ int batch_setup(orpcd_ctx* c, const double* R0, const double* t0, int B, const o
     CTX_CHECK(c, c->R.ensure((size_t)B * 9));
     CTX_CHECK(c, c->prev.ensure((size_t)B * 2));
     CTX_CHECK(c, c->partial.ensure((size_t)B * nblk * kPartialStride));
-    // two-phase search (only when selected): worst case every tile a candidate
-    // of every group; a batch whose list would not fit runs the split search
-    const size_t worst_items = (size_t)B * ((N + 127) / 128) * (size_t)c->tgt.ntiles;
-    c->two_phase_ok = c->opt.search_kernel == 2 && worst_items <= ((size_t)1 << 29);  // <= 2 GiB of items
-    if (c->two_phase_ok) CTX_CHECK(c, c->items.ensure(worst_items));
-    CTX_CHECK(c, c->item_counts.ensure((size_t)2 * B * ((N + 127) / 128) + 2));
-    c->sched_live = sched_wanted(c, persist, B);
-    c->fuse_live = c->opt.fuse_solve && !persist && c->opt.search_kernel == 0 && !c->opt.exact_nn &&
-                   (getenv("ORPCD_TRACE") != nullptr || !pipelined_ok(c));
+    c->sched_live = sched_wanted(c, B);
     c->exact_live = c->opt.exact_nn != 0;
     if (c->exact_live) {
-        CTX_REQUIRE(c, c->opt.search_kernel == 0, "exact_nn: needs the split search (search_kernel 0)");
         CTX_CHECK(c, c->xsec.ensure((size_t)B * N));
         CTX_CHECK(c, c->xtotal.ensure(1));
         CTX_CHECK(c, c->xlist.ensure((size_t)B * N));
         CTX_CHECK(c, c->xcnt.ensure(2));
         CTX_CHECK(c, hipMemsetAsync(c->xcnt.p, 0, 8, c->stream));
         CTX_CHECK(c, hipMemsetAsync(c->xtotal.p, 0, 8, c->stream));
-    }
-    if (c->fuse_live) {
-        CTX_CHECK(c, c->ready.ensure((size_t)B));
-        CTX_CHECK(c, c->fuse_err.ensure(1));
-        CTX_CHECK(c, hipMemsetAsync(c->ready.p, 0, (size_t)B * 4, c->stream));
-        CTX_CHECK(c, hipMemsetAsync(c->fuse_err.p, 0, 4, c->stream));
     }
     if (c->sched_live) {
         const size_t NG = (size_t)(N + 127) / 128;
@@ -437,14 +405,13 @@ int batch_setup(orpcd_ctx* c, const double* R0, const double* t0, int B, const o
     }
     CTX_CHECK(c, c->done.ensure((size_t)B));
     CTX_CHECK(c, c->active.ensure((size_t)B));
-    CTX_CHECK(c, c->ctl.ensure((size_t)B + 2));
     CTX_CHECK(c, c->out_fit.ensure((size_t)B));
     CTX_CHECK(c, c->out_rmse.ensure((size_t)B));
     CTX_CHECK(c, c->out_iters.ensure((size_t)B));
     CTX_CHECK(c, c->out_ncorr.ensure((size_t)B));
     CTX_CHECK(c, c->scratch64c.ensure((size_t)B * 9));
     CTX_CHECK(c, c->h64.ensure((size_t)B * 80));
-    CTX_CHECK(c, c->h32.ensure((size_t)B * 6));  // [4B, 6B): second active / done lists (sync_lag)
+    CTX_CHECK(c, c->h32.ensure((size_t)B * 4));
 
     // host: base pose G_b = [R0_b^T | t0_b] (source @ R0 + t0 in column form)
     double* hG = c->h64.p;
@@ -492,44 +459,18 @@ int batch_setup(orpcd_ctx* c, const double* R0, const double* t0, int B, const o
     CTX_CHECK(c, hipMemcpyAsync(c->active.p, hAct, (size_t)B * 4, hipMemcpyHostToDevice, s));
     CTX_CHECK(c, hipMemcpyAsync(c->done.p, hDone, (size_t)B * 4, hipMemcpyHostToDevice, s));
     CTX_CHECK(c, hipMemsetAsync(c->prevnn.p, 0xff, (size_t)B * N * 4, s));
-    // pipelined pass control: B running starts, no arrivals
-    CTX_CHECK(c, hipMemsetAsync(c->ctl.p, 0, ((size_t)B + 2) * 4, s));
-    CTX_CHECK(c, hipMemsetD32Async((hipDeviceptr_t)c->ctl.p, B, 1, s));
 
     c->last_B = B;
     // posed-frame source covariances for every start (rigid equivariance)
     c->est = init16 ? kEstP2P : kEstGICP;
     if (!init16) CTX_CHECK(c, launch_normals_cov(c->sraw.p, N, c->scratch64c.p, B, p->epsilon, nullptr, c->scov.p, s));
-    if (!persist) {
-        CTX_CHECK(c, launch_xform(c, B, 0, p->max_correspondence_distance * p->max_correspondence_distance, s, false,
-                                  target_bounds(c, hAct, B)));
-        return ORPCD_OK;
-    }
-    // persistent loop: pass 0 of every start open, tickets zero, best[] = kNone
-    // (the loop's queries are formed by its own search items)
-    if (c->persist_grid[c->est] == 0) c->persist_grid[c->est] = persist_grid(c->device, c->est);
-    CTX_REQUIRE(c, c->persist_grid[c->est] > 0, "gicp: the persistent kernel cannot be resident on this device");
-    CTX_CHECK(c, c->sched.ensure((size_t)B));
-    CTX_CHECK(c, c->tick_blk.ensure((size_t)B * nblk));
-    CTX_CHECK(c, c->tick_start.ensure((size_t)B));
-    CTX_CHECK(c, c->pctl.ensure(2));
-    CTX_CHECK(c, c->h64sched.ensure((size_t)B));
-    const int S0 = persist_first_splits(c, B, c->persist_grid[c->est]);
-    for (int b = 0; b < B; ++b) c->h64sched.p[b] = persist_sched_word(0, S0);
-    CTX_CHECK(c, hipMemcpyAsync(c->sched.p, c->h64sched.p, (size_t)B * 8, hipMemcpyHostToDevice, s));
-    CTX_CHECK(c, hipMemsetAsync(c->tick_blk.p, 0, (size_t)B * nblk * 4, s));
-    CTX_CHECK(c, hipMemsetAsync(c->tick_start.p, 0, (size_t)B * 4, s));
-    CTX_CHECK(c, hipMemsetAsync(c->pctl.p, 0, 8, s));
-    CTX_CHECK(c, hipMemsetAsync(c->best.p, 0xff, (size_t)B * N * 8, s));
+    CTX_CHECK(c, launch_xform(c, B, 0, p->max_correspondence_distance * p->max_correspondence_distance, s,
+                              target_bounds(c, hAct, B)));
     return ORPCD_OK;
 }
 
 int run_passes(orpcd_ctx* c, int B, const orpcd_gicp_params* p, double* T_out, double* rmse_out,
                double* fitness_out, int32_t* iters_out, int64_t* ncorr_out);
-int run_passes_persistent(orpcd_ctx* c, int B, const orpcd_gicp_params* p, double* T_out, double* rmse_out,
-                          double* fitness_out, int32_t* iters_out, int64_t* ncorr_out);
-int run_passes_pipelined(orpcd_ctx* c, int B, const orpcd_gicp_params* p, double* T_out, double* rmse_out,
-                         double* fitness_out, int32_t* iters_out, int64_t* ncorr_out);
 int read_outputs(orpcd_ctx* c, int B, unsigned long long tiles_before, double* T_out, double* rmse_out,
                  double* fitness_out, int32_t* iters_out, int64_t* ncorr_out);
 
@@ -559,11 +500,7 @@ int orpcd_ctx_create(int device, orpcd_ctx** out) {
     if (hipSetDevice(device) != hipSuccess ||
         hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
         c->counters.ensure(kCounterSlots * kCounterStride) != hipSuccess ||
-        hipMemset(c->counters.p, 0, kCounterSlots * kCounterStride * 8) != hipSuccess ||
-        hipHostMalloc(reinterpret_cast<void**>(&c->prog_h), 64, hipHostMallocMapped | hipHostMallocCoherent) !=
-            hipSuccess ||
-        hipHostGetDevicePointer(reinterpret_cast<void**>(&c->prog_d), c->prog_h, 0) != hipSuccess) {
-        if (c->prog_h) (void)hipHostFree(c->prog_h);
+        hipMemset(c->counters.p, 0, kCounterSlots * kCounterStride * 8) != hipSuccess) {
         if (c->stream) (void)hipStreamDestroy(c->stream);
         c->counters.release();
         delete c;
@@ -589,19 +526,17 @@ int orpcd_ctx_destroy(orpcd_ctx* c) {
         b->release();
     c->prevnn.release();
     c->best.release();
-    c->items.release();
-    c->item_counts.release();
     c->q32.release();
     c->gbox.release();
     c->done.release();
     c->active.release();
-    c->ctl.release();
-    c->sched.release();
-    c->tick_blk.release();
-    c->tick_start.release();
-    c->pctl.release();
-    c->h64sched.release();
-    if (c->prog_h) (void)hipHostFree(c->prog_h);
+    for (auto* b : {&c->wcost, &c->wcnt}) b->release();
+    c->wtot.release();
+    c->wlist.release();
+    c->xsec.release();
+    c->xlist.release();
+    c->xcnt.release();
+    c->xtotal.release();
     c->out_iters.release();
     c->out_ncorr.release();
     c->scratch32.release();
@@ -611,8 +546,6 @@ int orpcd_ctx_destroy(orpcd_ctx* c) {
     c->fgr.release();
     c->vox.release();
     for (hipEvent_t e : c->ev_pool) (void)hipEventDestroy(e);
-    for (hipEvent_t e : c->sync_ev)
-        if (e) (void)hipEventDestroy(e);
     (void)hipStreamDestroy(c->stream);
     delete c;
     return ORPCD_OK;
@@ -627,6 +560,7 @@ int orpcd_set_target(orpcd_ctx* c, const double* xyz, int64_t m, double epsilon)
     CTX_REQUIRE(c, finite_cloud(xyz, m), "set_target: non-finite coordinates");
     CTX_CHECK(c, hipSetDevice(c->device));
     c->ntgt = 0;
+    c->last_B = 0;  // the last batch's correspondences refer to the old targets
     int rc = upload_target(c, xyz, m, epsilon);
     if (rc) return rc;
     CTX_CHECK(c, hipStreamSynchronize(c->stream));
@@ -646,6 +580,7 @@ int orpcd_set_targets(orpcd_ctx* c, const double* xyz, const int64_t* m, int32_t
     }
     CTX_CHECK(c, hipSetDevice(c->device));
     c->ntgt = 0;
+    c->last_B = 0;
     off = 0;
     for (int k = 0; k < ntargets; ++k) {
         int rc = upload_target_k(c, k, xyz + 3 * off, m[k], epsilon);
@@ -664,6 +599,7 @@ int orpcd_set_source(orpcd_ctx* c, const double* xyz, int64_t n) {
     CTX_REQUIRE(c, finite_cloud(xyz, n), "set_source: non-finite coordinates");
     CTX_CHECK(c, hipSetDevice(c->device));
     c->src_cov = false;
+    c->last_B = 0;
     double margin = 0.0;
     int rc = upload_layout(c, xyz, n, c->src, true, &margin);
     if (rc) return rc;
@@ -721,17 +657,19 @@ int orpcd_gicp_batch_targets(orpcd_ctx* c, const double* R0, const double* t0, c
         std::memcpy(&sR[(size_t)pos[b] * 9], R0 + 9 * b, 9 * sizeof(double));
         std::memcpy(&st[(size_t)pos[b] * 3], t0 + 3 * b, 3 * sizeof(double));
     }
-    const bool persist = ntg == 1 && persistent_ok(c);
-    rc = batch_setup(c, sR.data(), st.data(), B, p, nullptr, persist);
+    rc = batch_setup(c, sR.data(), st.data(), B, p);
     if (rc) return rc;
     std::vector<double> oT((size_t)B * 16), orm((size_t)B), ofit((size_t)B);
     std::vector<int32_t> oit((size_t)B);
     std::vector<int64_t> onc((size_t)B);
-    rc = persist ? run_passes_persistent(c, B, p, oT.data(), orm.data(), ofit.data(), oit.data(), onc.data())
-                 : run_passes(c, B, p, oT.data(), orm.data(), ofit.data(), oit.data(), onc.data());
+    rc = run_passes(c, B, p, oT.data(), orm.data(), ofit.data(), oit.data(), onc.data());
     c->batch_ntgt = 1;
     c->batch_first[1] = 0;
     if (rc) return rc;
+    c->last_slot = pos;
+    c->last_slot_tgt.assign((size_t)B, 0);
+    for (int k = 0; k < ntg; ++k)
+        for (int q = first[k]; q < first[k + 1]; ++q) c->last_slot_tgt[q] = k;
     for (int b = 0; b < B; ++b) {
         const int q = pos[b];
         std::memcpy(T_out + 16 * b, &oT[(size_t)q * 16], 16 * sizeof(double));
@@ -750,6 +688,7 @@ int orpcd_set_source_points(orpcd_ctx* c, const double* xyz, int64_t n) {
     CTX_REQUIRE(c, finite_cloud(xyz, n), "set_source_points: non-finite coordinates");
     CTX_CHECK(c, hipSetDevice(c->device));
     c->src_cov = false;
+    c->last_B = 0;
     int rc = upload_layout(c, xyz, n, c->src, true);
     if (rc) return rc;
     CTX_CHECK(c, hipStreamSynchronize(c->stream));
@@ -767,10 +706,11 @@ int orpcd_icp_p2p_batch(orpcd_ctx* c, const double* init, int32_t B, const orpcd
     CTX_REQUIRE(c, p->max_iteration >= 0, "icp_p2p_batch: max_iteration must be >= 0");
     for (int64_t t = 0; t < 16 * (int64_t)B; ++t) CTX_REQUIRE(c, std::isfinite(init[t]), "icp_p2p_batch: non-finite init");
     CTX_CHECK(c, hipSetDevice(c->device));
-    const bool persist = persistent_ok(c);
-    int rc = batch_setup(c, nullptr, nullptr, B, p, init, persist);
+    int rc = batch_setup(c, nullptr, nullptr, B, p, init);
     if (rc) return rc;
-    if (persist) return run_passes_persistent(c, B, p, T_out, rmse_out, fitness_out, iters_out, ncorr_out);
+    c->last_slot.resize((size_t)B);
+    for (int b = 0; b < B; ++b) c->last_slot[b] = b;
+    c->last_slot_tgt.assign((size_t)B, 0);
     return run_passes(c, B, p, T_out, rmse_out, fitness_out, iters_out, ncorr_out);
 }
 
@@ -824,228 +764,6 @@ int read_outputs(orpcd_ctx* c, int B, unsigned long long tiles_before, double* T
     return ORPCD_OK;
 }
 
-// The persistent ICP loop (opt.persist, default): one launch runs every pass
-// of every start (icp_persistent_kernel); the host waits for it once.
-int run_passes_persistent(orpcd_ctx* c, int B, const orpcd_gicp_params* p, double* T_out, double* rmse_out,
-                          double* fitness_out, int32_t* iters_out, int64_t* ncorr_out) {
-    hipStream_t s = c->stream;
-    unsigned long long tiles_before = 0, unused = 0;
-    if (c->profiling) CTX_CHECK(c, read_counters(c, tiles_before, unused, false));
-    const bool timed = c->profiling;
-    c->count_tiles = timed;
-    if (timed) {
-        while (c->ev_pool.size() < 2) {
-            hipEvent_t e;
-            CTX_CHECK(c, hipEventCreateWithFlags(&e, hipEventDisableSystemFence));  // timing only
-            c->ev_pool.push_back(e);
-        }
-        CTX_CHECK(c, hipEventRecord(c->ev_pool[0], s));
-    }
-    CTX_CHECK(c, launch_icp_persistent(c, B, c->persist_grid[c->est], *p, s));
-    if (timed) CTX_CHECK(c, hipEventRecord(c->ev_pool[1], s));
-    int32_t* hctl = reinterpret_cast<int32_t*>(c->h64sched.p);  // >= B u64 words: room for pctl[0..1]
-    CTX_CHECK(c, hipMemcpyAsync(hctl, c->pctl.p, 8, hipMemcpyDeviceToHost, s));
-    CTX_CHECK(c, hipStreamSynchronize(s));
-    if (hctl[1] != 0 || hctl[0] != B) {
-        c->err = "gicp: the persistent pass loop did not finish every start (device timeout guard, " +
-                 std::to_string(hctl[0]) + " of " + std::to_string(B) + " finished)";
-        return ORPCD_EDEVICE;
-    }
-    if (timed) {
-        float ms = 0.f;
-        CTX_CHECK(c, hipEventElapsedTime(&ms, c->ev_pool[0], c->ev_pool[1]));
-        c->stats.launches += 1;
-        c->stats.ms += ms;
-    }
-    int rc = read_outputs(c, B, tiles_before, T_out, rmse_out, fitness_out, iters_out, ncorr_out);
-    if (rc) return rc;
-    if (iters_out)
-        for (int b = 0; b < B; ++b) c->stats.passes += iters_out[b] + 1;
-    return ORPCD_OK;
-}
-
-// The pipelined ICP loop (opt.pipeline): every pass is enqueued
-// without a host round trip.  The device keeps the running starts (PassCtl:
-// solve fused into the accumulation's last block, compaction of active[],
-// splits re-derived by the search from the device count) and publishes
-// (passes completed, running starts) in a host-mapped word.  The host reads
-// that word only to shrink the grids, to stop enqueueing once no start runs,
-// and to stay at most opt.lookahead passes ahead; passes enqueued after the
-// last start finished exit at once.
-int run_passes_pipelined(orpcd_ctx* c, int B, const orpcd_gicp_params* p, double* T_out, double* rmse_out,
-                         double* fitness_out, int32_t* iters_out, int64_t* ncorr_out) {
-    hipStream_t s = c->stream;
-    unsigned long long tiles_before = 0, unused = 0;
-    if (c->profiling) CTX_CHECK(c, read_counters(c, tiles_before, unused, false));
-    const bool timed = c->profiling;
-    c->count_tiles = timed;
-    const int npass = p->max_iteration + 1;
-    if (timed) {
-        while ((int)c->ev_pool.size() < 3 * npass) {
-            hipEvent_t e;
-            CTX_CHECK(c, hipEventCreateWithFlags(&e, hipEventDisableSystemFence));  // timing only
-            c->ev_pool.push_back(e);
-        }
-    }
-    volatile unsigned long long* prog = c->prog_h;
-    *prog = 0;  // no pipelined kernel of this batch has run yet (the stream is idle after batch_setup's copies)
-    int nact_host = B, launched = 0;
-    // Wait on the progress word until `ready(v)`.  Bounded: the stream is
-    // polled for an asynchronous fault (or for having drained without
-    // publishing what is awaited), and the wait gives up after 120 s.
-    auto wait_progress = [&](auto ready, unsigned long long& v) -> int {
-        const auto t0 = std::chrono::steady_clock::now();
-        for (unsigned spin = 0;; ++spin) {
-            v = *prog;
-            if (ready(v)) return ORPCD_OK;
-            if ((spin & 1023u) == 1023u) {
-                const hipError_t q = hipStreamQuery(s);
-                if (q != hipSuccess && q != hipErrorNotReady) {
-                    c->err = std::string("pipelined passes: device error: ") + hipGetErrorString(q);
-                    return ORPCD_EDEVICE;
-                }
-                if (q == hipSuccess) {  // drained: the word is final
-                    v = *prog;
-                    if (ready(v)) return ORPCD_OK;
-                    c->err = "pipelined passes: the stream drained without publishing the awaited pass";
-                    return ORPCD_EDEVICE;
-                }
-                if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(120)) {
-                    c->err = "pipelined passes: timed out waiting for the device";
-                    return ORPCD_EDEVICE;
-                }
-            }
-            std::this_thread::yield();
-        }
-    };
-    for (int pass = 0; pass < npass; ++pass) {
-        unsigned long long v = *prog;
-        int pdone = (int)(v >> 32), nrun = (int)(v & 0xffffffffu);
-        if (pdone > 0 && nrun > 0 && pass - pdone >= c->opt.lookahead) {  // far enough ahead: wait
-            const int la = c->opt.lookahead;
-            const int rc = wait_progress(
-                [pass, la](unsigned long long w) {
-                    const int pd = (int)(w >> 32), nr = (int)(w & 0xffffffffu);
-                    return !(pd > 0 && nr > 0 && pass - pd >= la);
-                },
-                v);
-            if (rc) return rc;
-            pdone = (int)(v >> 32);
-            nrun = (int)(v & 0xffffffffu);
-        }
-        if (pdone == 0 && pass >= c->opt.lookahead) {  // nothing complete yet: bound the queue anyway
-            const int rc = wait_progress([](unsigned long long w) { return (w >> 32) != 0; }, v);
-            if (rc) return rc;
-            pdone = (int)(v >> 32);
-            nrun = (int)(v & 0xffffffffu);
-        }
-        if (pdone > 0) {
-            if (nrun == 0) break;
-            nact_host = std::min(nact_host, nrun);
-        }
-        hipEvent_t* ev = timed ? &c->ev_pool[3 * pass] : nullptr;
-        if (timed) CTX_CHECK(c, hipEventRecord(ev[0], s));
-        CTX_CHECK(c, launch_gicp_pass_pipelined(c, nact_host, pass, *p, s, timed ? ev[1] : nullptr, nullptr));
-        ++launched;
-    }
-    CTX_CHECK(c, hipStreamSynchronize(s));
-    const int passes_run = (int)(*prog >> 32);  // passes with a running start
-    if (timed) {
-        for (int q = 0; q < std::min(launched, passes_run); ++q) {
-            float ms = 0.f, ms2 = 0.f;
-            CTX_CHECK(c, hipEventElapsedTime(&ms, c->ev_pool[3 * q], c->ev_pool[3 * q + 1]));
-            c->stats.launches += 1;
-            c->stats.ms += ms;
-            c->stats.accum_ms += ms2;
-        }
-    }
-    int rc = read_outputs(c, B, tiles_before, T_out, rmse_out, fitness_out, iters_out, ncorr_out);
-    if (rc) return rc;
-    for (int b = 0; b < B; ++b) c->stats.passes += (iters_out ? iters_out[b] : 0) + 1;
-    return ORPCD_OK;
-}
-
-// The pass loop with the host's done-flag check one interval behind
-// (opt.sync_lag).  Every `every` passes the done flags are copied to a pinned
-// buffer and an event is recorded; the host then waits on the PREVIOUS
-// interval's event, compacts the running starts from that snapshot and
-// enqueues the next interval, so the stream always holds an interval of
-// passes and never drains at a check.  Starts that finished since the
-// snapshot stay listed one interval longer; every kernel's blocks exit at
-// once for them (done[]), exactly as between checks of the drained loop, and
-// the answers do not depend on the listed set (bit-identical results).
-// Double buffers: the done snapshots (one per interval in flight) and the
-// active lists (a list is rewritten only after its upload has run: the
-// upload precedes the event the host waits on two checks later).
-int run_passes_lagged(orpcd_ctx* c, int B, const orpcd_gicp_params* p, int every, bool timed) {
-    hipStream_t s = c->stream;
-    const double r2 = p->max_correspondence_distance * p->max_correspondence_distance;
-    int32_t* act[2] = {c->h32.p, c->h32.p + 4 * (size_t)B};
-    int32_t* dn[2] = {c->h32.p + B, c->h32.p + 5 * (size_t)B};
-    for (int g = 0; g < 2; ++g)
-        if (!c->sync_ev[g]) CTX_CHECK(c, hipEventCreateWithFlags(&c->sync_ev[g], hipEventDisableTiming));
-    if (timed) {
-        while ((int)c->ev_pool.size() < 6 * every) {
-            hipEvent_t e;
-            CTX_CHECK(c, hipEventCreateWithFlags(&e, hipEventDisableSystemFence));  // timing only
-            c->ev_pool.push_back(e);
-        }
-    }
-    auto take_timings = [&](int g, int n) -> int {  // interval g's per-pass search events (complete)
-        for (int q = 0; q < n; ++q) {
-            float ms = 0.f;
-            hipEvent_t* ev = &c->ev_pool[3 * (g * every + q)];
-            CTX_CHECK(c, hipEventElapsedTime(&ms, ev[0], ev[1]));
-            c->stats.launches += 1;
-            if (c->sched_live) c->stats.sched_launches += 1;
-            c->stats.ms += ms;
-        }
-        return ORPCD_OK;
-    };
-    int cur = 0, gen = 0, nact = B;
-    int pend[2] = {0, 0};
-    bool inflight = false;  // interval gen ^ 1 awaits its check
-    for (int pass = 0; pass <= p->max_iteration && nact > 0; ++pass) {
-        hipEvent_t* ev = timed ? &c->ev_pool[3 * (gen * every + pend[gen])] : nullptr;
-        if (timed) CTX_CHECK(c, hipEventRecord(ev[0], s));
-        const TgtBounds tb = target_bounds(c, act[cur], nact);
-        CTX_CHECK(c, launch_gicp_pass(c, nact, pass, r2, s, timed ? ev[1] : nullptr, tb));
-        CTX_CHECK(c, launch_gicp_solve(c, nact, pass, *p, s, tb));
-        ++pend[gen];
-        c->stats.passes += nact;
-        if (c->exact_live) c->stats.exact_queries += (double)nact * (double)c->src.n;
-        if ((pass % every) != every - 1 && pass != p->max_iteration) continue;
-        CTX_CHECK(c, hipMemcpyAsync(dn[gen], c->done.p, (size_t)B * 4, hipMemcpyDeviceToHost, s));
-        CTX_CHECK(c, hipEventRecord(c->sync_ev[gen], s));
-        const int o = gen ^ 1;
-        if (inflight) {
-            CTX_CHECK(c, hipEventSynchronize(c->sync_ev[o]));
-            if (timed && take_timings(o, pend[o])) return ORPCD_EDEVICE;
-            pend[o] = 0;
-            int k = 0;
-            for (int b = 0; b < nact; ++b)
-                if (!dn[o][act[cur][b]]) act[cur ^ 1][k++] = act[cur][b];
-            if (k != nact && k > 0) {
-                CTX_CHECK(c, hipMemcpyAsync(c->active.p, act[cur ^ 1], (size_t)k * 4, hipMemcpyHostToDevice, s));
-                cur ^= 1;
-            }
-            nact = k;
-        }
-        inflight = true;
-        gen = o;
-    }
-    CTX_CHECK(c, hipStreamSynchronize(s));
-    if (timed) {
-        if (take_timings(gen ^ 1, pend[gen ^ 1]) || take_timings(gen, pend[gen])) return ORPCD_EDEVICE;
-    }
-    if (c->exact_live) {  // entries re-searched over the batch (nn_exact_kernel adds each pass's count)
-        unsigned long long tot = 0;
-        CTX_CHECK(c, hipMemcpy(&tot, c->xtotal.p, 8, hipMemcpyDeviceToHost));
-        c->stats.exact_filed += (double)tot;
-    }
-    return ORPCD_OK;
-}
-
 // The ICP loop of every start of the batch set up by batch_setup (GICP or
 // PointToPoint by c->est).  GICP outputs T (the ICP transform relative to the
 // posed source); PointToPoint outputs T * G (registration_icp's result, init
@@ -1066,8 +784,6 @@ int run_passes(orpcd_ctx* c, int B, const orpcd_gicp_params* p, double* T_out, d
     if (c->profiling) CTX_CHECK(c, read_counters(c, tiles_before, unused, false));
     int nact = B;
     static const bool trace = getenv("ORPCD_TRACE") != nullptr;
-    if (!trace && pipelined_ok(c)) return run_passes_pipelined(c, B, p, T_out, rmse_out, fitness_out, iters_out,
-                                                                ncorr_out);
     const bool timed = c->profiling || trace;
     const int every = trace ? 1 : std::max(1, c->opt.sync_every);
     c->count_tiles = timed;
@@ -1077,11 +793,6 @@ int run_passes(orpcd_ctx* c, int B, const orpcd_gicp_params* p, double* T_out, d
             CTX_CHECK(c, hipEventCreateWithFlags(&e, hipEventDisableSystemFence));  // timing only: no cache writeback per record
             c->ev_pool.push_back(e);
         }
-    }
-    if (!trace && !c->fuse_live && c->opt.sync_lag) {
-        const int rc = run_passes_lagged(c, B, p, every, timed);
-        if (rc) return rc;
-        return read_outputs(c, B, tiles_before, T_out, rmse_out, fitness_out, iters_out, ncorr_out);
     }
     int pending = 0;  // timed passes since the last host sync
     for (int pass = 0; pass <= p->max_iteration && nact > 0; ++pass) {
@@ -1099,12 +810,9 @@ int run_passes(orpcd_ctx* c, int B, const orpcd_gicp_params* p, double* T_out, d
         const bool sync = (pass % every) == every - 1 || pass == p->max_iteration;
         if (!sync) continue;
         CTX_CHECK(c, hipMemcpyAsync(hDone, c->done.p, (size_t)B * 4, hipMemcpyDeviceToHost, s));
-        unsigned ferr = 0;
-        if (c->fuse_live) CTX_CHECK(c, hipMemcpyAsync(&ferr, c->fuse_err.p, 4, hipMemcpyDeviceToHost, s));
         unsigned long long tiles_now[2] = {0, 0};
         if (trace) CTX_CHECK(c, read_counters(c, tiles_now[0], tiles_now[1], true));
         CTX_CHECK(c, hipStreamSynchronize(s));
-        CTX_REQUIRE_DEV(c, ferr == 0, "gicp: a query transform block timed out waiting for its start's solve");
         if (timed) {
             for (int q = 0; q < pending; ++q) {
                 float ms = 0.f, ms2 = 0.f;
@@ -1605,21 +1313,20 @@ int orpcd_set_option(orpcd_ctx* c, const char* key, double value) {
     else if (k == "super_cull" && (v == 0 || v == 1)) c->opt.super_cull = v;
     else if (k == "small_batch" && v >= 0) c->opt.small_batch = v;
     else if (k == "reseed" && (v == 0 || v == 1)) c->opt.reseed = v;
-    else if (k == "search_occupancy" && (v == 0 || v == 6)) c->opt.search_occupancy = v;
-    else if (k == "search_kernel" && v >= 0 && v <= 2) c->opt.search_kernel = v;
-    else if (k == "scan_blocks" && v >= 1 && v <= 65536) c->opt.scan_blocks = v;
-    else if (k == "pipeline" && (v == 0 || v == 1)) c->opt.pipeline = v;
-    else if (k == "lookahead" && v >= 1 && v <= 64) c->opt.lookahead = v;
-    else if (k == "seed_reps" && v >= 1) c->opt.seed_reps = v;
-    else if (k == "persist" && (v == 0 || v == 1)) c->opt.persist = v;
-    else if (k == "persist_items" && v >= 0) c->opt.persist_items = v;
-    else if (k == "persist_timeout_s" && v >= 1 && v <= 3600) c->opt.persist_timeout_s = v;
-    else if (k == "persist_fences" && (v == 0 || v == 1)) c->opt.persist_fences = v;
+    else if (k == "seed_reps" && v >= 1) {
+        c->opt.seed_reps = v;
+        // the seed stride lives in the targets' descriptors: rewrite them
+        CTX_CHECK(c, hipSetDevice(c->device));
+        for (int t = 0; t < c->ntgt; ++t) {
+            write_target_desc(c->tgts[t], c->tcovs[t].p, v, c->tdesc_h[t]);
+            CTX_CHECK(c, hipMemcpyAsync(c->tdesc.p + t, &c->tdesc_h[t], sizeof(TargetDesc), hipMemcpyHostToDevice,
+                                        c->stream));
+        }
+        CTX_CHECK(c, hipStreamSynchronize(c->stream));
+    }
     else if (k == "sched" && (v == 0 || v == 1)) c->opt.sched = v;
     else if (k == "sched_items" && v >= 64 && v <= (1 << 22)) c->opt.sched_items = v;
     else if (k == "sched_min_starts" && v >= 1) c->opt.sched_min_starts = v;
-    else if (k == "fuse_solve" && (v == 0 || v == 1)) c->opt.fuse_solve = v;
-    else if (k == "sync_lag" && (v == 0 || v == 1)) c->opt.sync_lag = v;
     else if (k == "exact_nn" && (v == 0 || v == 1)) c->opt.exact_nn = v;
     else {
         c->err = "set_option: unknown key or bad value: " + k;
@@ -1632,20 +1339,27 @@ int orpcd_gicp_correspondences(orpcd_ctx* c, int32_t B, int32_t* idx_out) {
     if (!c) return ORPCD_EINVAL;
     CTX_REQUIRE(c, idx_out && B > 0, "gicp_correspondences: bad arguments");
     const int64_t N = c->src.n;
-    CTX_REQUIRE(c, N > 0 && B == c->last_B && c->prevnn.n >= (size_t)B * N,
-                "gicp_correspondences: B must be the last batch's number of starts");
-    CTX_REQUIRE(c, c->ntgt == 1, "gicp_correspondences: single-target batches only");
+    CTX_REQUIRE(c, N > 0 && B == c->last_B && c->prevnn.n >= (size_t)B * N && c->last_slot.size() == (size_t)B,
+                "gicp_correspondences: B must be the last batch's number of starts (and no cloud set since)");
     CTX_CHECK(c, hipSetDevice(c->device));
     CTX_CHECK(c, hipStreamSynchronize(c->stream));
-    std::vector<int32_t> nn((size_t)B * N), sp((size_t)N), tp((size_t)c->tgt.n);
+    std::vector<int32_t> nn((size_t)B * N), sp((size_t)N);
+    std::vector<std::vector<int32_t>> tp((size_t)kMaxTargets);
     CTX_CHECK(c, hipMemcpy(nn.data(), c->prevnn.p, nn.size() * 4, hipMemcpyDeviceToHost));
     CTX_CHECK(c, hipMemcpy(sp.data(), c->src.perm.p, sp.size() * 4, hipMemcpyDeviceToHost));
-    CTX_CHECK(c, hipMemcpy(tp.data(), c->tgt.perm.p, tp.size() * 4, hipMemcpyDeviceToHost));
-    for (int b = 0; b < B; ++b)
-        for (int64_t k = 0; k < N; ++k) {  // Morton query k is source point sp[k]
-            const int32_t j = nn[(size_t)b * N + k];
-            idx_out[(size_t)b * N + sp[k]] = j >= 0 && j < (int32_t)c->tgt.n ? tp[j] : -1;
+    for (int b = 0; b < B; ++b) {
+        const int q = c->last_slot[b], k = c->last_slot_tgt[q];
+        std::vector<int32_t>& perm = tp[k];
+        const int64_t M = c->tgts[k].n;
+        if (perm.empty()) {
+            perm.resize((size_t)M);
+            CTX_CHECK(c, hipMemcpy(perm.data(), c->tgts[k].perm.p, (size_t)M * 4, hipMemcpyDeviceToHost));
         }
+        for (int64_t i = 0; i < N; ++i) {  // Morton query i is source point sp[i]
+            const int32_t j = nn[(size_t)q * N + i];
+            idx_out[(size_t)b * N + sp[i]] = j >= 0 && j < (int32_t)M ? perm[j] : -1;
+        }
+    }
     return ORPCD_OK;
 }
 

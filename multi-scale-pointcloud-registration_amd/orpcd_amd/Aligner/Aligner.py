@@ -381,7 +381,7 @@ class Aligner:
             table, sec = done[key]
             used.add(key)
             self.history.append(dict(B=self._attempts, seconds=sec, iters=int(table["iters"].sum()),
-                                     rmse=table["rmse"].copy()))
+                                     rmse=table["rmse"].copy(), iters_per_start=table["iters"].copy()))
             return self._select(table, tape.draw(block))
 
         scale_factors = np.ones((1, 3))

@@ -39,7 +39,7 @@ class GeneralizedICP(IOptimizer):
         relative_fitness: float = __ICP_RELATIVE_FITNESS__,
         relative_rmse: float = __ICP_RELATIVE_RMSE__,
         device: Optional[int] = None,
-        exact_nn: bool = False,
+        exact_nn: bool = True,
     ):
         self._LOG = LoggerFactory.get_logger(log_name=self.__class__.__name__)
         if max_correspondence_distance <= 0:
@@ -56,9 +56,11 @@ class GeneralizedICP(IOptimizer):
         self._relative_fitness = float(relative_fitness)
         self._relative_rmse = float(relative_rmse)
         self._device = device
-        # exact_nn: every correspondence is the fp64 nearest target, as the
-        # oracle's KD-tree finds it (fp32 search + fp64 re-search of the
-        # queries whose runner-up is within the fp32 error band)
+        # exact_nn (default): every correspondence is the fp64 nearest target,
+        # as Open3D's KD-tree (SearchHybrid, generalizedICP.py:59-70) and the
+        # oracle find it (fp32 search + fp64 re-search of the queries whose
+        # runner-up is within the fp32 error band).  False: the
+        # fp32 search's answer (near-ties within 2^-17 resolved by position).
         self._exact_nn = bool(exact_nn)
         self._ctx = None
         self.last_result = None

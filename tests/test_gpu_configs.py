@@ -1,0 +1,83 @@
+"""BASELINE.json configs exercised at their own sizes on the GPU, against the
+CPU oracle:
+
+* C3 (configs[2]): FastGlobalOptimizer on the 100k synthetic pair with the
+  reference's defaults (normals r=0.1/k=20, FPFH r=0.1/k=20, max_corr 0.5,
+  Q4 target features from the source; fastGlobalOptimizer.py:23-34,
+  :137-142, :158-174).  Gate: the same mutual-match and tuple counts (so the
+  same tuples), T elementwise <= 1e-9, inlier RMSE <= 1e-9 relative, the same
+  inlier count.
+* C4 (configs[3]): the C2 pair with attempts=64, sharded over 8 ranks in
+  contiguous blocks of 8 starts (parallel.shard, Aligner.py:178-202).  A
+  start's result never depends on its batch mates, so every rank's block run
+  as its own batch must reproduce the 64-start batch bit for bit (that is
+  what makes the all-gathered table rank-count independent); a subset of the
+  starts is checked against the oracle at the per-start gate (exact mode:
+  identical iterations, T <= 1e-6, RMSE <= 1e-7).
+"""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def _radius_scale(c):
+    center = c.mean(axis=0, keepdims=True)
+    return (c - center) / np.max(np.linalg.norm(c - center, axis=1))
+
+
+def test_c3_fgr_defaults_match_oracle(ctx, oracle):
+    from orpcd_amd import FastGlobalOptimizer
+    from workloads import c3_pair
+    src, tgt = c3_pair(100_000)
+    src, tgt = _radius_scale(src), _radius_scale(tgt)  # what the Aligner hands over (RadiusScaler)
+    opt = FastGlobalOptimizer(seed=0)                  # the reference's defaults, Q4 on
+    T, rmse = opt.optimize(src, tgt)
+    g = opt.last_result
+    _, fs = oracle.fpfh(src, 0.1, 20, 0.1, 20)
+    o = oracle.fgr(src, tgt, fs, fs[:len(tgt)], seed=0)  # Q4: the target's features are the source's
+    assert g["n_mutual"] == o["n_mutual"] and g["n_tuple_corr"] == o["n_tuple_corr"], (g, o)
+    assert np.abs(g["T"] - o["T"]).max() <= 1e-9, np.abs(g["T"] - o["T"]).max()
+    assert g["ncorr"] == o["ncorr"]
+    assert abs(g["rmse"] - o["rmse"]) <= 1e-9 * o["rmse"] + 1e-15
+    To = np.copy(o["T"])
+    To[:3, :3] = To[:3, :3].T                          # the plugin's row convention (Q1)
+    assert np.abs(T - To).max() <= 1e-9 and rmse == g["rmse"]
+    print(f"C3: n_mutual {g['n_mutual']} tuples {g['n_tuple_corr']} rmse {rmse:.9g} "
+          f"|dT| {np.abs(g['T'] - o['T']).max():.1e}")
+
+
+def _c2():
+    from orpcd_amd import Preprocessor
+    from workloads import c2_pair
+    s, t = c2_pair(50_000)
+    return Preprocessor([]).preprocess(s), Preprocessor([]).preprocess(t)
+
+
+def test_c4_rank_blocks_bit_identical_and_match_oracle(ctx, oracle):
+    from orpcd_amd import parallel
+    s, t = _c2()
+    np.random.seed(0)
+    al = oracle.OracleAligner(None, attempts=64)
+    starts = [al.initialize_rotation() for _ in range(64)]  # the first multistart's 64 draws (Aligner.py:178-186)
+    R0 = np.array([r for r, _ in starts])
+    t0 = np.array([v for _, v in starts])
+    ctx.set_option("exact_nn", 1)
+    ctx.set_target(t)
+    ctx.set_source(s)
+    full = ctx.gicp_batch(R0, t0)
+    keys = ("T", "rmse", "fitness", "iters", "ncorr")
+    for rank in range(8):
+        lo, hi = parallel.shard(64, rank, 8)
+        assert hi - lo == 8
+        blk = ctx.gicp_batch(R0[lo:hi], t0[lo:hi])  # < 16 starts: the uniform-split search, not the ordered one
+        for k in keys:
+            assert np.array_equal(blk[k], full[k][lo:hi]), (rank, k)
+    # the all-gathered table of 8 ranks IS the 64-start table; its argmin is the reference's
+    table = parallel.unpack(np.concatenate([parallel.pack({k: full[k][lo:hi] for k in keys})
+                                            for lo, hi in (parallel.shard(64, r, 8) for r in range(8))]))
+    assert np.array_equal(table["rmse"], full["rmse"]) and np.array_equal(table["T"], full["T"])
+    for b in (0, 13, 27, 41, 63):  # one start from each of five rank blocks
+        o = oracle.gicp(np.dot(s, R0[b]) + t0[b], t, 0.5, 100)
+        assert full["iters"][b] == o["iters"], (b, full["iters"][b], o["iters"])
+        assert np.abs(full["T"][b] - o["T"]).max() <= 1e-6 and abs(full["rmse"][b] - o["rmse"]) <= 1e-7

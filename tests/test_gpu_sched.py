@@ -29,9 +29,11 @@ def _same(a, b):
         assert np.array_equal(a[k], b[k]), k
 
 
-def test_sched_matches_uniform_multistart(ctx):
+@pytest.mark.parametrize("exact_nn", [1, 0])
+def test_sched_matches_uniform_multistart(ctx, exact_nn):
     """40 posed starts (>= sched_min_starts) finishing at many passes, max
-    iteration reached and not, and a small sched_items (many splits)."""
+    iteration reached and not, and a small sched_items (many splits); both
+    search modes."""
     src, tgt = small_pair(6000, 5500, seed=41)
     rng = np.random.default_rng(12)
     R0 = np.array([rot_xyz(*rng.uniform(-90, 90, 3)) for _ in range(40)])
@@ -42,12 +44,16 @@ def test_sched_matches_uniform_multistart(ctx):
     def run():
         return [ctx.gicp_batch(R0, t0), ctx.gicp_batch(R0[:20], t0[:20], max_iteration=9)]
 
-    ref = _run(ctx, {"sched": 0}, run)
-    for opts in ({"sched": 1}, {"sched": 1, "sched_items": 64}, {"sched": 1, "sched_items": 200000}):
-        got = _run(ctx, opts, run)
-        assert len(set(got[0]["iters"].tolist())) > 5
-        for g, r in zip(got, ref):
-            _same(g, r)
+    ctx.set_option("exact_nn", exact_nn)
+    try:
+        ref = _run(ctx, {"sched": 0}, run)
+        for opts in ({"sched": 1}, {"sched": 1, "sched_items": 64}, {"sched": 1, "sched_items": 200000}):
+            got = _run(ctx, opts, run)
+            assert len(set(got[0]["iters"].tolist())) > 5
+            for g, r in zip(got, ref):
+                _same(g, r)
+    finally:
+        ctx.set_option("exact_nn", 1)
 
 
 def test_sched_matches_uniform_multi_target(ctx):
@@ -79,33 +85,3 @@ def test_sched_many_groups_single_start(ctx):
     ref = _run(ctx, {"sched": 0}, lambda: ctx.gicp_batch(R0, t0, max_iteration=6))
     got = _run(ctx, {"sched": 1, "sched_min_starts": 1}, lambda: ctx.gicp_batch(R0, t0, max_iteration=6))
     _same(got, ref)
-
-
-def test_fused_solve_matches_separate_kernels(ctx):
-    """Option fuse_solve (the solve inside the next pass's transform launch,
-    handed off by a per-start flag) against the separate solve kernel, with
-    and without the ordered dispatch, GICP and PointToPoint: bit-identical."""
-    src, tgt = small_pair(5000, 4600, seed=45)
-    rng = np.random.default_rng(14)
-    R0 = np.array([rot_xyz(*rng.uniform(-90, 90, 3)) for _ in range(24)])
-    t0 = rng.normal(size=(24, 3)) * 0.1
-    inits = np.repeat(np.eye(4)[None], 4, axis=0)
-    inits[:, :3, 3] = rng.normal(size=(4, 3)) * 0.02
-
-    def run():
-        ctx.set_target(tgt)
-        ctx.set_source(src)
-        out = [ctx.gicp_batch(R0, t0), ctx.gicp_batch(R0[:5], t0[:5], max_iteration=6)]
-        ctx.set_target_points(tgt)
-        ctx.set_source_points(src)
-        out.append(ctx.icp_p2p_batch(inits, max_iteration=30))
-        return out
-
-    try:
-        ref = _run(ctx, {"fuse_solve": 0}, run)
-        for opts in ({"fuse_solve": 1}, {"fuse_solve": 1, "sched": 0}):
-            got = _run(ctx, opts, run)
-            for g, r in zip(got, ref):
-                _same(g, r)
-    finally:
-        ctx.set_option("fuse_solve", 0)

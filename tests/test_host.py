@@ -282,7 +282,7 @@ def test_generalized_icp_sets_its_search_mode_on_the_shared_context():
             self.options.append((key, value))
 
     fake = FakeCtx()
-    fast, exact = GeneralizedICP(), GeneralizedICP(exact_nn=True)
+    fast, exact = GeneralizedICP(exact_nn=False), GeneralizedICP()  # exact is the default
     fast._ctx = exact._ctx = fake
     assert exact.context is fake and fake.options[-1] == ("exact_nn", 1)
     assert fast.context is fake and fake.options[-1] == ("exact_nn", 0)

@@ -1,5 +1,5 @@
 """One C2 multistart (30 starts, GICP) with the given runtime options, for
-profiling a single configuration:  python tools/one_batch.py '{"search_kernel":1}' [--reps 2]"""
+profiling a single configuration:  python tools/one_batch.py '{"exact_nn":0}' [--reps 2]"""
 import json
 import time
 import os
