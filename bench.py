@@ -305,7 +305,7 @@ def cpu_baseline(source, target, args):
     sys.path.insert(0, os.path.join(REPO, "oracle"))
     import oracle as O
 
-    cores = len(os.sched_getaffinity(0))  # the host cores this process may run on (all of them)
+    cores, how = usable_cpus()  # the host cores this process may run on (all of them)
     O.set_num_threads(cores)
     np.random.seed(1000)
     al = O.OracleAligner(None, attempts=args.attempts)
@@ -329,8 +329,25 @@ def cpu_baseline(source, target, args):
             "cpu_model": cpu_model(),
             "kind": "port",
             "sample": f"{done} of {args.attempts} starts of step 0 (same R0,t0), {iters} GICP iterations, "
-                      f"{el:.1f} s; OpenMP threads = the {cores} cores of this process's affinity mask "
-                      f"({os.cpu_count()} host cpus visible)"}
+                      f"{el:.1f} s; OpenMP threads = the {cores} cpus this process may use ({how}; "
+                      f"{os.cpu_count()} host cpus visible)"}
+
+
+def usable_cpus():
+    """CPUs this process can actually run on: its affinity mask, capped by the
+    cgroup CPU quota (a container granted 16 of 256 cpus sees all 256 in its
+    mask; 256 OpenMP threads on a 16-cpu quota run ~50x slower than 16)."""
+    n = len(os.sched_getaffinity(0))
+    how = f"affinity mask {n}"
+    try:
+        quota, period = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if quota != "max":
+            q = max(1, -(-int(quota) // int(period)))
+            if q < n:
+                n, how = q, how + f", cgroup cpu quota {q}"
+    except (OSError, ValueError):
+        pass
+    return n, how
 
 
 def cpu_model():

@@ -426,15 +426,16 @@ __device__ __forceinline__ int culled_search(float4* stage, const float4* __rest
                 const unsigned c0 = (__float_as_uint(d0.y) & kKeyMask) | (unsigned)(kk + 1);
                 const unsigned a1 = (__float_as_uint(d1.x) & kKeyMask) | (unsigned)kk;
                 const unsigned c1 = (__float_as_uint(d1.y) & kKeyMask) | (unsigned)(kk + 1);
-                if constexpr (kExact) {  // (minimum, runner-up) of every key scanned
-                    s0 = umed3(m0, s0, a0);
-                    m0 = min(m0, a0);
-                    s0 = umed3(m0, s0, c0);
-                    m0 = min(m0, c0);
-                    s1 = umed3(m1, s1, a1);
-                    m1 = min(m1, a1);
-                    s1 = umed3(m1, s1, c1);
-                    m1 = min(m1, c1);
+                if constexpr (kExact) {
+                    // (minimum, runner-up) of every key scanned: with m <= s, the
+                    // second smallest of {m, s, a, c} is min(s, med3(m, a, c))
+                    // (if s is among the two smallest, m is the smallest and
+                    // a, c >= s; otherwise it is the second smallest of {m, a,
+                    // c} <= s): 3 ops per query and key pair instead of 4
+                    s0 = min(s0, umed3(m0, a0, c0));
+                    m0 = min(m0, min(a0, c0));
+                    s1 = min(s1, umed3(m1, a1, c1));
+                    m1 = min(m1, min(a1, c1));
                 } else {
                     m0 = min(m0, min(a0, c0));
                     m1 = min(m1, min(a1, c1));
@@ -1734,10 +1735,6 @@ static ExactArgs exact_args(const orpcd_ctx* c, int pass) {
     ex.total = c->xtotal.p;
     return ex;
 }
-#ifndef ORPCD_EXACT_BLOCKS
-#define ORPCD_EXACT_BLOCKS 256
-#endif
-constexpr int kExactBlocks = ORPCD_EXACT_BLOCKS;  // re-search grid: 1024 waves, 64 listed queries per wave and round
 
 hipError_t launch_xform(const orpcd_ctx* c, int nact, int pass, double r2, hipStream_t s, const TgtBounds& tb) {
     const int N = (int)c->src.n;
@@ -1818,7 +1815,7 @@ hipError_t launch_gicp_pass(const orpcd_ctx* c, int nact, int pass, double r2, h
     const int N = (int)c->src.n;
     const int sblk = (N + kCBlockQ - 1) / kCBlockQ;
     hipError_t e;
-    if (c->sched_live) {    } else if (c->sched_live) {
+    if (c->sched_live) {
         // ordered dispatch: the items were filed by this pass's query transform;
         // the grid covers their upper bound (surplus waves exit at once)
         const int64_t NG = (N + 127) / 128;
@@ -1845,21 +1842,22 @@ hipError_t launch_gicp_pass(const orpcd_ctx* c, int nact, int pass, double r2, h
         if ((e = dump_wavetime(pass, nact, 0, (unsigned)(grid * kCWaves), s)) != hipSuccess) return e;
 #endif
     } else {
-    // few running starts: half the wave target (8 starts: 16k waves 8.16 ms vs
-    // 32k 8.40 ms per batch; 30 starts keep 32k).  Splits never change answers.
-    const int S = uniform_splits(c, nact);
-    // best[] was reset to kNone by xform_queries_kernel
-    auto kern = c->exact_live ? nn_search_kernel<true> : nn_search_kernel<false>;
-    kern<<<dim3((unsigned)(sblk * S), (unsigned)nact), kCBlock, 0, s>>>(
-        c->q32.p, N, c->tdesc.p, tb, c->opt.super_cull, c->active.p, c->done.p, S, c->best.p,
-        c->count_tiles ? c->counters.p : nullptr, c->gbox.p, exact_args(c, pass));
+        // few running starts: half the wave target (8 starts: 16k waves 8.16 ms
+        // vs 32k 8.40 ms per batch; 30 starts keep 32k).  Splits never change
+        // answers.  best[] was reset to kNone by xform_queries_kernel.
+        const int S = uniform_splits(c, nact);
+        auto kern = c->exact_live ? nn_search_kernel<true> : nn_search_kernel<false>;
+        kern<<<dim3((unsigned)(sblk * S), (unsigned)nact), kCBlock, 0, s>>>(
+            c->q32.p, N, c->tdesc.p, tb, c->opt.super_cull, c->active.p, c->done.p, S, c->best.p,
+            c->count_tiles ? c->counters.p : nullptr, c->gbox.p, exact_args(c, pass));
 #ifdef ORPCD_WAVETIME
-    if ((e = dump_wavetime(pass, nact, S, (unsigned)(sblk * S) * (unsigned)nact * kCWaves, s)) != hipSuccess) return e;
+        if ((e = dump_wavetime(pass, nact, S, (unsigned)(sblk * S) * (unsigned)nact * kCWaves, s)) != hipSuccess)
+            return e;
 #endif
     }
     if ((e = hipGetLastError()) != hipSuccess) return e;
     if (c->exact_live) {  // fp64 re-search of the queries the search could not certify
-        nn_exact_kernel<<<kExactBlocks, 256, 0, s>>>(c->src.xyz64.p, N, c->Q.p, c->tdesc.p, c->q32.p,
+        nn_exact_kernel<<<(unsigned)c->opt.exact_blocks, 256, 0, s>>>(c->src.xyz64.p, N, c->Q.p, c->tdesc.p, c->q32.p,
                                                      exact_args(c, pass), c->best.p);
         if ((e = hipGetLastError()) != hipSuccess) return e;
     }

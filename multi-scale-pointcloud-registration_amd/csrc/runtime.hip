@@ -1328,6 +1328,7 @@ int orpcd_set_option(orpcd_ctx* c, const char* key, double value) {
     else if (k == "sched_items" && v >= 64 && v <= (1 << 22)) c->opt.sched_items = v;
     else if (k == "sched_min_starts" && v >= 1) c->opt.sched_min_starts = v;
     else if (k == "exact_nn" && (v == 0 || v == 1)) c->opt.exact_nn = v;
+    else if (k == "exact_blocks" && v >= 1 && v <= 65536) c->opt.exact_blocks = v;
     else {
         c->err = "set_option: unknown key or bad value: " + k;
         return ORPCD_EINVAL;

@@ -40,6 +40,7 @@ class GeneralizedICP(IOptimizer):
         relative_rmse: float = __ICP_RELATIVE_RMSE__,
         device: Optional[int] = None,
         exact_nn: bool = True,
+        rigid_cache: bool = True,
     ):
         self._LOG = LoggerFactory.get_logger(log_name=self.__class__.__name__)
         if max_correspondence_distance <= 0:
@@ -62,6 +63,11 @@ class GeneralizedICP(IOptimizer):
         # runner-up is within the fp32 error band).  False: the
         # fp32 search's answer (near-ties within 2^-17 resolved by position).
         self._exact_nn = bool(exact_nn)
+        # the drop-in path (one optimize() per attempt, as the reference's
+        # Aligner calls it): recognise a rigid image of the last cloud and
+        # reuse its device layout and covariances (_rigid_image)
+        self._rigid_cache = bool(rigid_cache)
+        self._base = None
         self._ctx = None
         self.last_result = None
 
@@ -80,11 +86,44 @@ class GeneralizedICP(IOptimizer):
                     max_iteration=self._max_iterations, relative_fitness=self._relative_fitness,
                     relative_rmse=self._relative_rmse, epsilon=self._epsilon)
 
+    def _rigid_image(self, source: np.ndarray):
+        """(R, t) with source == base @ R + t to round-off, when the base cloud
+        cached by an earlier call is a rigid image of `source` -- what the
+        reference's Aligner passes attempt after attempt (source_initialized =
+        source @ R0 + t0, Aligner.py:183-190).  None otherwise.
+
+        R, t come from a least-squares fit on 64 spread points and are then
+        verified on EVERY point (|source - (base @ R + t)| <= 1e-12 relative to
+        the cloud's extent, R orthonormal to 1e-12): a start is then run on the
+        cached base with pose (R, t), so its KNN-20 covariances are the base's
+        rotated (rigid invariance) instead of being recomputed
+        on the posed copy."""
+        base = self._base
+        if base is None or base.shape != source.shape or len(source) < 4:
+            return None
+        idx = np.linspace(0, len(source) - 1, num=min(64, len(source))).astype(np.int64)
+        A = np.c_[base[idx], np.ones(len(idx))]
+        M, *_ = np.linalg.lstsq(A, source[idx], rcond=None)
+        R, t = M[:3], M[3]
+        if not np.all(np.isfinite(M)) or np.abs(R.T @ R - np.eye(3)).max() > 1e-12:
+            return None
+        scale = 1.0 + float(np.abs(source).max())
+        if np.abs(source - (base @ R + t)).max() > 1e-12 * scale:
+            return None
+        return R, t
+
     def optimize(self, source: np.ndarray, target: np.ndarray, **kwargs) -> Tuple[np.ndarray, float]:
         ctx = self.context
         ctx.set_target(target, self._epsilon)
-        ctx.set_source(source)
-        r = ctx.gicp_batch(np.eye(3)[None], np.zeros((1, 3)), **self._params())
+        src = np.ascontiguousarray(source, dtype=np.float64)
+        pose = self._rigid_image(src) if self._rigid_cache else None
+        if pose is None:  # a new cloud: it becomes the base (layout and KNN-20 covariances once)
+            self._base = src.copy()
+            ctx.set_source(self._base)
+            pose = (np.eye(3), np.zeros(3))
+        else:
+            ctx.set_source(self._base)  # cached on the device (content key)
+        r = ctx.gicp_batch(pose[0][None], pose[1][None], **self._params())
         self.last_result = r
         roto_translation = np.copy(r["T"][0])
         roto_translation[:3, :3] = roto_translation[:3, :3].T

@@ -286,3 +286,52 @@ def test_generalized_icp_sets_its_search_mode_on_the_shared_context():
     fast._ctx = exact._ctx = fake
     assert exact.context is fake and fake.options[-1] == ("exact_nn", 1)
     assert fast.context is fake and fake.options[-1] == ("exact_nn", 0)
+
+
+def test_generalized_icp_drop_in_reuses_rigid_images():
+    """GeneralizedICP.optimize called once per attempt (the reference's own
+    Aligner, Aligner.py:183-190): a source that is a rigid image of the last
+    cloud runs on that cloud's cached device layout with the recovered pose;
+    anything else (deformed, reordered) becomes the new base."""
+    from orpcd_amd import GeneralizedICP
+    from workloads import rot_xyz, small_pair
+
+    class FakeCtx:
+        def __init__(self):
+            self.sources, self.poses = [], []
+
+        def set_option(self, key, value):
+            pass
+
+        def set_target(self, xyz, eps):
+            pass
+
+        def set_source(self, xyz):
+            self.sources.append(xyz)
+
+        def gicp_batch(self, R0, t0, **kw):
+            self.poses.append((R0[0].copy(), t0[0].copy()))
+            return dict(T=np.eye(4)[None], rmse=np.array([0.5]))
+
+    src, tgt = small_pair(500, seed=3)
+    opt = GeneralizedICP()
+    fake = opt._ctx = FakeCtx()
+    opt.optimize(src, tgt)
+    R0, t0 = rot_xyz(30, -40, 70), np.array([0.1, -0.2, 0.05])
+    posed = np.dot(src.copy(), R0) + t0                # Aligner.py:183-185
+    T, rmse = opt.optimize(posed, tgt)
+    assert fake.sources[1] is fake.sources[0]         # the cached base, not the posed copy
+    R, t = fake.poses[1]
+    assert np.abs(R - R0).max() < 1e-13 and np.abs(t - t0).max() < 1e-13
+    bent = posed.copy()
+    bent[7] += 1e-6                                   # not rigid: a new base
+    opt.optimize(bent, tgt)
+    assert fake.sources[2] is not fake.sources[0] and np.array_equal(fake.sources[2], bent)
+    assert np.array_equal(fake.poses[2][0], np.eye(3))
+    opt.optimize(posed[::-1].copy(), tgt)             # reordered: a new base
+    assert np.array_equal(fake.poses[3][0], np.eye(3))
+    off = GeneralizedICP(rigid_cache=False)
+    fake2 = off._ctx = FakeCtx()
+    off.optimize(src, tgt)
+    off.optimize(posed, tgt)
+    assert np.array_equal(fake2.sources[1], posed) and np.array_equal(fake2.poses[1][0], np.eye(3))
