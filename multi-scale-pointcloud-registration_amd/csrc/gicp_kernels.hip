@@ -101,6 +101,14 @@ constexpr float kQuarterSlack = 1.0f - 1.0f / 1048576.0f;  // quarter test: box 
 __device__ __forceinline__ double ldg_f64(const double* p) {
     return *(const __attribute__((address_space(1))) double*)p;
 }
+__device__ __forceinline__ float4 ldg_f4(const float4* p) {
+    typedef float v4 __attribute__((ext_vector_type(4)));
+    const v4 v = *(const __attribute__((address_space(1))) v4*)p;
+    return make_float4(v.x, v.y, v.z, v.w);
+}
+__device__ __forceinline__ float ldg_f32(const float* p) {
+    return *(const __attribute__((address_space(1))) float*)p;
+}
 
 // ---------------------------------------------------------------------------
 // Exact nearest neighbour (opt.exact_nn).  The fp32 search orders candidates
@@ -992,15 +1000,26 @@ __global__ __launch_bounds__(kCBlock) __attribute__((amdgpu_waves_per_eu(kExact 
 }
 
 // --------------------------------------------------------------------------
-// Exact mode, second stage (one wave per 64 queries of a running start, after
-// the search): a query whose published runner-up lies within the fp32 error
-// band of its winner (exact_band_hi) is re-searched in fp64 by the whole wave.
-// Every target whose fp64 distance is at most the fp32 winner's passes the
-// box tests (its fp32 distance is within delta above; a box d^2 never exceeds
-// a member point's); the surviving tiles are scanned in fp64 in the oracle's
-// operation order ((dx^2 + dy^2) + dz^2, no contraction) and the
-// lexicographic (d^2, input index) minimum replaces the winner in best[] --
-// KDTree::nn1 of oracle/orpcd_oracle.cpp:192-217.
+// Exact mode, second stage (after the search): a listed query whose published
+// runner-up lies within the fp32 error band of its winner (exact_band_hi) is
+// re-searched in fp64 by a whole wave: the surviving tiles are scanned in
+// fp64 in the oracle's operation order ((dx^2 + dy^2) + dz^2, no contraction)
+// and the lexicographic (d^2, input index) minimum replaces the winner in
+// best[] -- KDTree::nn1 of oracle/orpcd_oracle.cpp:192-217.
+//
+// Candidates: every target t with d64(t) <= d64(j) (j: the fp32 winner) has
+// d32(t) <= d32(j) + 2 delta, i.e. at most band_hi of j's key (exact_band_hi,
+// the search's own certification bound), and a box d^2 never exceeds a member
+// point's, so tiles are culled against band_hi(key(j)) (x 1.0001 against the
+// box test's own rounding).  j itself is within it: the scan's minimum over
+// the candidates is the oracle's answer without j's fp64 distance first.
+//
+// The kernel is a chain of dependent round trips, so it is laid out to be
+// short: one list entry per wave (round 2 dealt 64 entries per wave and a
+// wave re-searched its filed ones one after another), the entry read beside
+// the entry count, then in one round everything that depends only on the
+// entry (winner, fp32 query, runner-up, pose, source point, the first 64
+// super-tile boxes), then the tile boxes, then the tile points.
 // --------------------------------------------------------------------------
 __device__ __forceinline__ double d2_oracle(const double q[3], const double* __restrict__ t) {
 #pragma clang fp contract(off)
@@ -1023,128 +1042,132 @@ __global__ __launch_bounds__(256) void nn_exact_kernel(const double* __restrict_
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     __shared__ int tlist[4][kExactList];  // a wave's listed candidate tiles
     const unsigned gw = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6), nw = gridDim.x * (blockDim.x >> 6);
+    // the first entry is read beside the count (the list holds at least one
+    // entry per wave of the grid; an entry past the count is ignored)
+    unsigned long long ent0 = ex.list[gw];
     const unsigned n = __builtin_amdgcn_readfirstlane(*ex.cnt);
     if (gw == 0 && lane == 0) *ex.cnt_next = 0u;
-    // listed queries: the band test against the final winner, one per lane;
-    // entries are dealt round-robin over the waves (a search wave lists its
-    // near-ties consecutively, and they cluster in space)
-    for (unsigned r = 0; (size_t)r * 64 * nw < n; ++r) {
-        const unsigned e = (r * 64 + lane) * nw + gw;
-        unsigned long long ent = 0;
-        bool file = false;
-        if (e < n) {
-            ent = ex.list[e];
-            const size_t qi = (size_t)(ent >> 40) * N + (unsigned)ent;
-            const unsigned long long m = best[qi];
-            const float4 qq = q32[qi];
-            file = m != kNone && __uint_as_float(ex.sec[qi] & kKeyMask) <=
-                                     exact_band_hi(__uint_as_float((unsigned)(m >> 32)), qnorm(qq.x, qq.y, qq.z));
-        }
-        unsigned long long fm = __ballot(file);
-        if (lane == 0 && fm) atomicAdd(ex.total, (unsigned long long)__builtin_popcountll(fm));
-        while (fm) {  // the wave re-searches each filed query of its 64 entries
-            const int l = __builtin_ctzll(fm);
-            fm &= fm - 1;
-            const unsigned long long en = ((unsigned long long)__builtin_amdgcn_readlane((unsigned)(ent >> 32), l) << 32) |
-                                          (unsigned)__builtin_amdgcn_readlane((unsigned)ent, l);
-            const int slot = (int)(en >> 40), tk = (int)((en >> 32) & 0xFFu), i = (int)(unsigned)en;
-            const TargetDesc& tg = tdesc[tk];
-            double Q[12];
+    unsigned filed = 0;  // this wave's re-searched queries (statistics)
+    for (unsigned e = gw; e < n; e += nw) {
+        if (e != gw) ent0 = ex.list[e];
+        const unsigned long long ent =
+            ((unsigned long long)(unsigned)__builtin_amdgcn_readfirstlane((unsigned)(ent0 >> 32)) << 32) |
+            (unsigned)__builtin_amdgcn_readfirstlane((unsigned)ent0);
+        const int slot = (int)(ent >> 40), tk = (int)((ent >> 32) & 0xFFu), i = (int)(unsigned)ent;
+        const size_t qi = (size_t)slot * N + i;
+        const TargetDesc& tg = tdesc[tk];
+        // the entry's independent loads, one round
+        const unsigned long long bv = best[qi];
+        const float4 qq = q32[qi];
+        const unsigned sk = ex.sec[qi];
+        double Q[12];
 #pragma unroll
-            for (int t = 0; t < 12; ++t) Q[t] = Qm[12 * slot + t];
-            const double* __restrict__ t64 = tg.xyz64;
-            const double p[3] = {src[3 * i], src[3 * i + 1], src[3 * i + 2]};
-            double q[3];
-            xform(Q, p, q);
-            const float x = (float)(q[0] - tg.ox), y = (float)(q[1] - tg.oy), z = (float)(q[2] - tg.oz);
-            unsigned long long* bp = best + (size_t)slot * N + i;
-            const unsigned long long bv = *bp;
-            const int j = (int)(unsigned)bv;
-            double bD = d2_oracle(q, t64 + 3 * (size_t)j);
-            int bI = __float_as_int(tg.p4[j].w), bM = j;
-            // box bound: d32 <= d64 + u (2A + 3.5 d) for every target with d64 <= d64(j); x2
-            const double dj = sqrt(bD);
-            const double rb = dj + 5.9604644775390625e-08 * (4.0 * (double)qnorm(x, y, z) + 7.0 * dj);
-            const float Tb = (float)(rb * rb * (1.0 + 1.0 / 65536.0)) * 1.0001f;
-            // candidate tiles: their boxes are tested four surviving super-tiles
-            // at a time, the survivors listed in LDS, then scanned four tiles at a
-            // time (every lane's four loads in flight together): the chain of
-            // dependent round trips, not the arithmetic, bounds this search
-            int nt = 0;  // listed tiles (wave-uniform)
-            auto scan_listed = [&]() {
-                for (int c = 0; c < nt; c += 4) {
-                    int kk[4], in[4];
-                    double tx[4], ty[4], tz[4];
+        for (int t = 0; t < 12; ++t) Q[t] = Qm[12 * slot + t];
+        const double p[3] = {src[3 * i], src[3 * i + 1], src[3 * i + 2]};
+        const int nsuper = tg.nsuper;
+        float4 s0lo, s0hi;
+        load_super0(search_tgt(tg), s0lo, s0hi);
+        double q[3];
+        xform(Q, p, q);
+        // one round trip for all of it: left alone, the compiler sinks the
+        // pose, source and box loads past the band test (a second round trip)
+        asm volatile("" ::"v"(bv), "v"(qq.x), "v"(qq.y), "v"(qq.z), "v"(sk), "v"(q[0]), "v"(q[1]), "v"(q[2]),
+                     "v"(s0lo.x), "v"(s0lo.y), "v"(s0lo.z), "v"(s0hi.x), "v"(s0hi.y), "v"(s0hi.z));
+        if (bv == kNone) continue;
+        // the band test against the final winner; its band is also the culling bound
+        const float band = exact_band_hi(__uint_as_float((unsigned)(bv >> 32)), qnorm(qq.x, qq.y, qq.z));
+        if (!(__uint_as_float(sk & kKeyMask) <= band)) continue;
+        ++filed;
+        const float Tb = band * 1.0001f;
+        const float x = qq.x, y = qq.y, z = qq.z;  // the search's fp32 query: (float)(Q p - origin)
+        const double* __restrict__ t64 = tg.xyz64;
+        double bD = 3.0e300;
+        int bI = 0x7FFFFFFF, bM = (int)(unsigned)bv;
+        int nt = 0;  // listed tiles (wave-uniform)
+        auto scan_listed = [&]() {  // four tiles at a time: every lane's four loads in flight together
+            for (int c = 0; c < nt; c += 4) {
+                int kk[4], in[4];
+                double tx[4], ty[4], tz[4];
 #pragma unroll
-                    for (int u4 = 0; u4 < 4; ++u4) {
-                        kk[u4] = c + u4 < nt ? tlist[wid][c + u4] * kTile + lane : -1;
-                        const int k = kk[u4] >= 0 ? kk[u4] : 0;
-                        in[u4] = __float_as_int(tg.p4[k].w);
-                        tx[u4] = t64[3 * (size_t)k];
-                        ty[u4] = t64[3 * (size_t)k + 1];
-                        tz[u4] = t64[3 * (size_t)k + 2];
-                    }
-#pragma unroll
-                    for (int u4 = 0; u4 < 4; ++u4) {
-                        if (kk[u4] < 0 || in[u4] < 0) continue;  // past the list / padding
-                        const double tp[3] = {tx[u4], ty[u4], tz[u4]};
-                        const double D = d2_oracle(q, tp);
-                        if (D < bD || (D == bD && in[u4] < bI)) {
-                            bD = D;
-                            bI = in[u4];
-                            bM = kk[u4];
-                        }
-                    }
+                for (int u4 = 0; u4 < 4; ++u4) {
+                    kk[u4] = c + u4 < nt ? tlist[wid][c + u4] * kTile + lane : -1;
+                    const int k = kk[u4] >= 0 ? kk[u4] : 0;
+                    in[u4] = __float_as_int(ldg_f32(&tg.p4[k].w));
+                    tx[u4] = ldg_f64(t64 + 3 * (size_t)k);
+                    ty[u4] = ldg_f64(t64 + 3 * (size_t)k + 1);
+                    tz[u4] = ldg_f64(t64 + 3 * (size_t)k + 2);
                 }
-                nt = 0;
-            };
-            for (int sb = 0; sb < tg.nsuper; sb += 64) {
-                const int u = sb + lane;
-                const bool su_ok = u < tg.nsuper && box_d2_plain(x, y, z, tg.slo[u], tg.shi[u]) <= Tb;
-                unsigned long long sm = __ballot(su_ok);
-                while (sm) {
-                    int su4[4];
-                    bool ok[4];
 #pragma unroll
-                    for (int u4 = 0; u4 < 4; ++u4) {
-                        su4[u4] = sm ? sb + __builtin_ctzll(sm) : -1;
-                        sm &= sm - 1;
-                        const int t = su4[u4] * kSuper + lane;
-                        ok[u4] = su4[u4] >= 0 && t < tg.ntiles;
-                        const float4 lo = ok[u4] ? tg.tlo[t] : make_float4(0.f, 0.f, 0.f, 0.f);
-                        const float4 hi = ok[u4] ? tg.thi[t] : lo;
-                        ok[u4] = ok[u4] && box_d2_plain(x, y, z, lo, hi) <= Tb;
+                for (int u4 = 0; u4 < 4; ++u4) {
+                    if (kk[u4] < 0 || in[u4] < 0) continue;  // past the list / padding
+                    const double tp[3] = {tx[u4], ty[u4], tz[u4]};
+                    const double D = d2_oracle(q, tp);
+                    if (D < bD || (D == bD && in[u4] < bI)) {
+                        bD = D;
+                        bI = in[u4];
+                        bM = kk[u4];
                     }
-#pragma unroll
-                    for (int u4 = 0; u4 < 4; ++u4) {
-                        unsigned long long tm = __ballot(ok[u4]);
-                        const int cnt = __builtin_popcountll(tm);
-                        if (nt + cnt > kExactList) scan_listed();  // the list is full: scan it first
-                        const int pos = nt + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(tm >> 32),
-                                                                         __builtin_amdgcn_mbcnt_lo((unsigned)tm, 0));
-                        if (ok[u4]) tlist[wid][pos] = su4[u4] * kSuper + lane;
-                        nt += cnt;
-                    }
-                    __builtin_amdgcn_wave_barrier();
                 }
             }
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-            scan_listed();
-#pragma unroll
-            for (int o = 32; o >= 1; o >>= 1) {  // lexicographic (d^2, input index) over the wave
-                const double oD = __shfl_xor(bD, o);
-                const int oI = __shfl_xor(bI, o), oM = __shfl_xor(bM, o);
-                if (oD < bD || (oD == bD && oI < bI)) {
-                    bD = oD;
-                    bI = oI;
-                    bM = oM;
-                }
+            nt = 0;
+        };
+        // candidate tiles: their boxes are tested four surviving super-tiles
+        // at a time and the survivors listed in LDS
+        const unsigned long long sm0 = __ballot(lane < nsuper && box_d2_plain(x, y, z, s0lo, s0hi) <= Tb);
+        for (int sb = 0; sb < nsuper; sb += 64) {
+            const int u = sb + lane;
+            unsigned long long sm = sm0;
+            if (sb > 0) {
+                const int uu = u < nsuper ? u : 0;
+                sm = __ballot(u < nsuper && box_d2_plain(x, y, z, ldg_f4(tg.slo + uu), ldg_f4(tg.shi + uu)) <= Tb);
             }
-            if (lane == 0) *bp = (bv & 0xFFFFFFFF00000000ull) | (unsigned)bM;
+            while (sm) {
+                int su4[4];
+                bool ok[4];
+#pragma unroll
+                for (int u4 = 0; u4 < 4; ++u4) {
+                    su4[u4] = sm ? sb + __builtin_ctzll(sm) : -1;
+                    sm &= sm - 1;
+                    const int t = su4[u4] * kSuper + lane;
+                    ok[u4] = su4[u4] >= 0 && t < tg.ntiles;
+                    const int tt = ok[u4] ? t : 0;
+                    const float4 lo = ldg_f4(tg.tlo + tt), hi = ldg_f4(tg.thi + tt);
+                    ok[u4] = ok[u4] && box_d2_plain(x, y, z, lo, hi) <= Tb;
+                }
+#pragma unroll
+                for (int u4 = 0; u4 < 4; ++u4) {
+                    unsigned long long tm = __ballot(ok[u4]);
+                    const int cnt = __builtin_popcountll(tm);
+                    if (nt + cnt > kExactList) scan_listed();  // the list is full: scan it first
+                    const int pos = nt + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(tm >> 32),
+                                                                     __builtin_amdgcn_mbcnt_lo((unsigned)tm, 0));
+                    if (ok[u4]) tlist[wid][pos] = su4[u4] * kSuper + lane;
+                    nt += cnt;
+                }
+                __builtin_amdgcn_wave_barrier();
+            }
         }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        scan_listed();
+#pragma unroll
+        for (int o = 32; o >= 1; o >>= 1) {  // lexicographic (d^2, input index) over the wave
+            const double oD = __shfl_xor(bD, o);
+            const int oI = __shfl_xor(bI, o), oM = __shfl_xor(bM, o);
+            if (oD < bD || (oD == bD && oI < bI)) {
+                bD = oD;
+                bI = oI;
+                bM = oM;
+            }
+        }
+        if (lane == 0) best[qi] = (bv & 0xFFFFFFFF00000000ull) | (unsigned)bM;
+        // the next entry's list writes follow this entry's reads of tlist
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     }
+    if (lane == 0 && filed) atomicAdd(ex.total, (unsigned long long)filed);
 }
 
 

@@ -322,8 +322,8 @@ struct orpcd_ctx {
                                   // oracle's lexicographic (d^2, input index) minimum): fp32 search +
                                   // runner-up band test + fp64 re-search of the uncertified queries;
                                   // 0: the fp32 search's answer (ties within 2^-17 relative by position)
-        int exact_blocks = 256;   // grid of the fp64 re-search (256-thread blocks; 64 listed queries per wave
-                                  // and round)
+        int exact_blocks = 256;   // grid of the fp64 re-search (256-thread blocks, one listed query per wave
+                                  // at a time)
     } opt;
     std::vector<hipEvent_t> ev_pool;
     orpcd::KernelStats stats;

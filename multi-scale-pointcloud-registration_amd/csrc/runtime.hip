@@ -386,7 +386,9 @@ int batch_setup(orpcd_ctx* c, const double* R0, const double* t0, int B, const o
     if (c->exact_live) {
         CTX_CHECK(c, c->xsec.ensure((size_t)B * N));
         CTX_CHECK(c, c->xtotal.ensure(1));
-        CTX_CHECK(c, c->xlist.ensure((size_t)B * N));
+        // at least one entry per wave of the re-search grid (each wave reads its
+        // first entry before the count)
+        CTX_CHECK(c, c->xlist.ensure(std::max<size_t>((size_t)B * N, (size_t)4 * 65536)));
         CTX_CHECK(c, c->xcnt.ensure(2));
         CTX_CHECK(c, hipMemsetAsync(c->xcnt.p, 0, 8, c->stream));
         CTX_CHECK(c, hipMemsetAsync(c->xtotal.p, 0, 8, c->stream));

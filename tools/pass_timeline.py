@@ -2,6 +2,7 @@
 for every ICP pass, the duration of each kernel and the gaps between them.
 
     python tools/pass_timeline.py gpurun_out/kt/run_results.db [--every 10]
+    python tools/pass_timeline.py gpurun_out/kt/<host>/<pid>_kernel_trace.csv [--every 10]
 
 A pass starts at an xform_queries_kernel launch.  Prints, per pass, the
 wall time from that launch to the next pass's, and the kernel durations
@@ -18,9 +19,15 @@ def short(n):
 
 
 def main():
-    db = sqlite3.connect(sys.argv[1])
     every = int(sys.argv[sys.argv.index("--every") + 1]) if "--every" in sys.argv else 10
-    rows = db.execute("select name, start, end from kernels order by start").fetchall()
+    if sys.argv[1].endswith(".csv"):  # rocprofv3 --output-format csv kernel trace
+        import csv
+        rows = sorted((r["Kernel_Name"], int(r["Start_Timestamp"]), int(r["End_Timestamp"]))
+                      for r in csv.DictReader(open(sys.argv[1])))
+        rows.sort(key=lambda r: r[1])
+    else:
+        db = sqlite3.connect(sys.argv[1])
+        rows = db.execute("select name, start, end from kernels order by start").fetchall()
     starts = [i for i, r in enumerate(rows) if "xform_queries_kernel" in r[0]]
     # the last batch: passes after the last large gap (> 2 ms) between passes
     last = 0
