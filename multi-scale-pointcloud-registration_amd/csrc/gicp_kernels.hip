@@ -128,9 +128,12 @@ __device__ __forceinline__ float ldg_f32(const float* p) {
 // the key truncation (2^-17 relative on the winner's d^2) and 2^-19 for its
 // own fp32 rounding.
 // ---------------------------------------------------------------------------
-// exact mode's search: 4 waves/SIMD, fully unrolled scan (measured at C2, 8 / 30
-// starts: 9.78 / 21.45 ms; 5 waves with the scan unrolled by 2 or 4, which fit
-// without spills: 9.74-9.94 / 21.98-22.29 ms; re-search grid 1024 blocks: 22.53)
+// exact mode's search: 5 waves/SIMD with the pipelined scan (ORPCD_PIPE_EXACT:
+// one pair read ahead, no deeper hoisting; 94 VGPRs).  C2 batches of 30 / 8
+// starts: 19.79 / 8.70 ms at 4 waves/SIMD with the compiler's scan schedule
+// (116 VGPRs; at 5 waves it spilled 17), 19.52 / 8.49 ms like this (hashes
+// equal).  The fast search gains nothing from it (14.9 / 4.5 ms either way,
+// also at 6 waves).
 #ifndef ORPCD_SCAN_UNROLL_EXACT
 #define ORPCD_SCAN_UNROLL_EXACT 8
 #endif
@@ -138,7 +141,16 @@ __device__ __forceinline__ float ldg_f32(const float* p) {
 #define ORPCD_SCAN_UNROLL_FAST 8
 #endif
 #ifndef ORPCD_EXACT_WAVES
-#define ORPCD_EXACT_WAVES 4
+#define ORPCD_EXACT_WAVES 5
+#endif
+#ifndef ORPCD_FAST_WAVES
+#define ORPCD_FAST_WAVES 5
+#endif
+#ifndef ORPCD_PIPE_EXACT
+#define ORPCD_PIPE_EXACT 1
+#endif
+#ifndef ORPCD_PIPE_FAST
+#define ORPCD_PIPE_FAST 0
 #endif
 constexpr float kU = 5.9604645e-08f;  // 2^-24
 __device__ __forceinline__ float exact_band_hi(float x, float A) {
@@ -192,6 +204,11 @@ __device__ __forceinline__ int culled_search(float4* stage, const float4* __rest
                                              unsigned long long* phase_cull_out = nullptr,
                                              unsigned* sk = nullptr) {
     constexpr int kScanUnroll = kExact ? ORPCD_SCAN_UNROLL_EXACT : ORPCD_SCAN_UNROLL_FAST;
+    // kPipe: the scan reads each target pair one iteration ahead and the
+    // compiler may not hoist more (a scheduling barrier per iteration): left
+    // to itself it issues a whole quarter's LDS reads up front, which holds
+    // ~20 more VGPRs than the scan needs
+    constexpr bool kPipe = kExact ? ORPCD_PIPE_EXACT : ORPCD_PIPE_FAST;
     const int lane = threadIdx.x & 63;
 #if ORPCD_CULL_PRIO > 0
     __builtin_amdgcn_s_setprio(ORPCD_CULL_PRIO);  // culling at raised issue priority
@@ -213,8 +230,10 @@ __device__ __forceinline__ int culled_search(float4* stage, const float4* __rest
     float e0 = kExact && v0 ? bound[0] : 0.0f, e1 = kExact && v1 ? bound[1] : 0.0f;
     if constexpr (kGBox) {
         const float4 g0 = gbox[0], g1 = gbox[1];
-        Wk = __float_as_uint(g0.w) & kKeyMask;
-        lox = g0.x, loy = g0.y, loz = g0.z, hix = g1.x, hiy = g1.y, hiz = g1.z;
+        // wave-uniform: scalar registers (the record is one address for every lane)
+        auto sc = [](float f) { return __uint_as_float(__builtin_amdgcn_readfirstlane(__float_as_uint(f))); };
+        Wk = __builtin_amdgcn_readfirstlane(__float_as_uint(g0.w)) & kKeyMask;
+        lox = sc(g0.x), loy = sc(g0.y), loz = sc(g0.z), hix = sc(g1.x), hiy = sc(g1.y), hiz = sc(g1.z);
     } else {
         static_assert(kGBox || !kExact, "exact mode needs the transform's wave boxes");
         Wk = wave_umax((k0 > k1 ? k0 : k1) & kKeyMask);
@@ -415,11 +434,27 @@ __device__ __forceinline__ int culled_search(float4* stage, const float4* __rest
             const bool need = qd2.x * kQuarterSlack < b0 || qd2.y * kQuarterSlack < b1;
             if (!__any(need)) continue;
             ++visited;
+            f2 ntx, nty, ntz;
+            if constexpr (kPipe) {
+                ntx = *reinterpret_cast<const f2*>(sx + qd * kQuarter);
+                nty = *reinterpret_cast<const f2*>(sx + 64 + qd * kQuarter);
+                ntz = *reinterpret_cast<const f2*>(sx + 128 + qd * kQuarter);
+            }
 #pragma unroll kScanUnroll
             for (int kk = qd * kQuarter; kk < (qd + 1) * kQuarter; kk += 2) {
-                const f2 tx = *reinterpret_cast<const f2*>(sx + kk);
-                const f2 ty = *reinterpret_cast<const f2*>(sx + 64 + kk);
-                const f2 tz = *reinterpret_cast<const f2*>(sx + 128 + kk);
+                f2 tx, ty, tz;
+                if constexpr (kPipe) {  // this pair's coordinates were read one iteration ahead
+                    tx = ntx, ty = nty, tz = ntz;
+                    if (kk + 2 < (qd + 1) * kQuarter) {
+                        ntx = *reinterpret_cast<const f2*>(sx + kk + 2);
+                        nty = *reinterpret_cast<const f2*>(sx + 64 + kk + 2);
+                        ntz = *reinterpret_cast<const f2*>(sx + 128 + kk + 2);
+                    }
+                } else {
+                    tx = *reinterpret_cast<const f2*>(sx + kk);
+                    ty = *reinterpret_cast<const f2*>(sx + 64 + kk);
+                    tz = *reinterpret_cast<const f2*>(sx + 128 + kk);
+                }
                 f2 dx = qx0 - tx, dy = qy0 - ty, dz = qz0 - tz;  // query 0 vs targets kk, kk+1
                 f2 d0 = dx * dx;
                 d0 = pk_fma(dy, dy, d0);
@@ -448,6 +483,7 @@ __device__ __forceinline__ int culled_search(float4* stage, const float4* __rest
                     m0 = min(m0, min(a0, c0));
                     m1 = min(m1, min(a1, c1));
                 }
+                if constexpr (kPipe) __builtin_amdgcn_sched_barrier(0);
             }
         }
         asm volatile("" ::: "memory");  // all reads of this tile precede the next stage write
@@ -918,7 +954,7 @@ __device__ __forceinline__ void nn_search_body(
 // class-major list, heaviest class first; the wave's duration is added to its
 // group's cost and to the pass total for the next pass's schedule.
 template <bool kExact>
-__global__ __launch_bounds__(kCBlock) __attribute__((amdgpu_waves_per_eu(kExact ? ORPCD_EXACT_WAVES : 5, 8))) void nn_search_sched_kernel(
+__global__ __launch_bounds__(kCBlock) __attribute__((amdgpu_waves_per_eu(kExact ? ORPCD_EXACT_WAVES : ORPCD_FAST_WAVES, 8))) void nn_search_sched_kernel(
     const float4* __restrict__ q32, int N, const TargetDesc* __restrict__ tdesc, int super_cull,
     unsigned long long* __restrict__ best, unsigned long long* __restrict__ counters,
     const float4* __restrict__ gbox, SchedS sa, ExactArgs ex) {
@@ -987,7 +1023,7 @@ __global__ __launch_bounds__(kCBlock) __attribute__((amdgpu_waves_per_eu(kExact 
 // Uniform-split search: grid = (sblk * S, running starts), 4 waves/block;
 // block (bx, by) is split bx % S of query block bx / S of launch row by.
 template <bool kExact>
-__global__ __launch_bounds__(kCBlock) __attribute__((amdgpu_waves_per_eu(kExact ? ORPCD_EXACT_WAVES : 5, 8))) void nn_search_kernel(
+__global__ __launch_bounds__(kCBlock) __attribute__((amdgpu_waves_per_eu(kExact ? ORPCD_EXACT_WAVES : ORPCD_FAST_WAVES, 8))) void nn_search_kernel(
     const float4* __restrict__ q32, int N, const TargetDesc* __restrict__ tdesc, TgtBounds tb, int super_cull,
     const int32_t* __restrict__ active, const int32_t* __restrict__ done, int S, unsigned long long* __restrict__ best,
     unsigned long long* __restrict__ counters, const float4* __restrict__ gbox, ExactArgs ex) {
@@ -1033,15 +1069,142 @@ __device__ __forceinline__ float box_d2_plain(float x, float y, float z, float4 
 
 constexpr int kExactList = 512;  // candidate tiles listed per wave before a scan
 
-__global__ __launch_bounds__(256) void nn_exact_kernel(const double* __restrict__ src, int N,
-                                                       const double* __restrict__ Qm,
-                                                       const TargetDesc* __restrict__ tdesc,
-                                                       const float4* __restrict__ q32, ExactArgs ex,
-                                                       unsigned long long* __restrict__ best) {
+// fused mode: a listed query's winner in best[] carries this bit in its index
+// word once its entry is done (Morton indices are < 2^27; kNone has it too)
+constexpr unsigned long long kResolvedBit = 1ull << 31;
+
+// One list entry (slot << 40 | target << 32 | query): the band test and, if
+// filed, the re-search.  Every lane of the wave calls it with the same entry;
+// returns the new winner's Morton index, or -1 when the fp32 winner stands.
+// bv: the winner as read here (for the caller's store).
+__device__ __forceinline__ int exact_entry(unsigned long long ent, const double* __restrict__ src, int N,
+                                           const double* __restrict__ Qm, const TargetDesc* __restrict__ tdesc,
+                                           const float4* __restrict__ q32, const ExactArgs& ex,
+                                           const unsigned long long* __restrict__ best, int* __restrict__ tl,
+                                           unsigned long long& bv, unsigned& filed) {
 #pragma clang fp contract(off)
-    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    __shared__ int tlist[4][kExactList];  // a wave's listed candidate tiles
-    const unsigned gw = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6), nw = gridDim.x * (blockDim.x >> 6);
+    const int lane = threadIdx.x & 63;
+    const int slot = (int)(ent >> 40), tk = (int)((ent >> 32) & 0xFFu), i = (int)(unsigned)ent;
+    const size_t qi = (size_t)slot * N + i;
+    const TargetDesc& tg = tdesc[tk];
+    // the entry's independent loads, one round
+    bv = best[qi];
+    const float4 qq = q32[qi];
+    const unsigned sk = ex.sec[qi];
+    double Q[12];
+#pragma unroll
+    for (int t = 0; t < 12; ++t) Q[t] = Qm[12 * slot + t];
+    const double p[3] = {src[3 * i], src[3 * i + 1], src[3 * i + 2]};
+    const int nsuper = tg.nsuper;
+    float4 s0lo, s0hi;
+    load_super0(search_tgt(tg), s0lo, s0hi);
+    double q[3];
+    xform(Q, p, q);
+    // one round trip for all of it: left alone, the compiler sinks the
+    // pose, source and box loads past the band test (a second round trip)
+    asm volatile("" ::"v"(bv), "v"(qq.x), "v"(qq.y), "v"(qq.z), "v"(sk), "v"(q[0]), "v"(q[1]), "v"(q[2]),
+                 "v"(s0lo.x), "v"(s0lo.y), "v"(s0lo.z), "v"(s0hi.x), "v"(s0hi.y), "v"(s0hi.z));
+    if (bv == kNone) return -1;
+    // the band test against the final winner; its band is also the culling bound
+    const float band = exact_band_hi(__uint_as_float((unsigned)(bv >> 32)), qnorm(qq.x, qq.y, qq.z));
+    if (!(__uint_as_float(sk & kKeyMask) <= band)) return -1;
+    ++filed;
+    const float Tb = band * 1.0001f;
+    const float x = qq.x, y = qq.y, z = qq.z;  // the search's fp32 query: (float)(Q p - origin)
+    const double* __restrict__ t64 = tg.xyz64;
+    double bD = 3.0e300;
+    int bI = 0x7FFFFFFF, bM = (int)(unsigned)bv;
+    int nt = 0;  // listed tiles (wave-uniform)
+    auto scan_listed = [&]() {  // four tiles at a time: every lane's four loads in flight together
+        for (int c = 0; c < nt; c += 4) {
+            int kk[4], in[4];
+            double tx[4], ty[4], tz[4];
+#pragma unroll
+            for (int u4 = 0; u4 < 4; ++u4) {
+                kk[u4] = c + u4 < nt ? tl[c + u4] * kTile + lane : -1;
+                const int k = kk[u4] >= 0 ? kk[u4] : 0;
+                in[u4] = __float_as_int(ldg_f32(&tg.p4[k].w));
+                tx[u4] = ldg_f64(t64 + 3 * (size_t)k);
+                ty[u4] = ldg_f64(t64 + 3 * (size_t)k + 1);
+                tz[u4] = ldg_f64(t64 + 3 * (size_t)k + 2);
+            }
+#pragma unroll
+            for (int u4 = 0; u4 < 4; ++u4) {
+                if (kk[u4] < 0 || in[u4] < 0) continue;  // past the list / padding
+                const double tp[3] = {tx[u4], ty[u4], tz[u4]};
+                const double D = d2_oracle(q, tp);
+                if (D < bD || (D == bD && in[u4] < bI)) {
+                    bD = D;
+                    bI = in[u4];
+                    bM = kk[u4];
+                }
+            }
+        }
+        nt = 0;
+    };
+    // candidate tiles: their boxes are tested four surviving super-tiles
+    // at a time and the survivors listed in LDS
+    const unsigned long long sm0 = __ballot(lane < nsuper && box_d2_plain(x, y, z, s0lo, s0hi) <= Tb);
+    for (int sb = 0; sb < nsuper; sb += 64) {
+        const int u = sb + lane;
+        unsigned long long sm = sm0;
+        if (sb > 0) {
+            const int uu = u < nsuper ? u : 0;
+            sm = __ballot(u < nsuper && box_d2_plain(x, y, z, ldg_f4(tg.slo + uu), ldg_f4(tg.shi + uu)) <= Tb);
+        }
+        while (sm) {
+            int su4[4];
+            bool ok[4];
+#pragma unroll
+            for (int u4 = 0; u4 < 4; ++u4) {
+                su4[u4] = sm ? sb + __builtin_ctzll(sm) : -1;
+                sm &= sm - 1;
+                const int t = su4[u4] * kSuper + lane;
+                ok[u4] = su4[u4] >= 0 && t < tg.ntiles;
+                const int tt = ok[u4] ? t : 0;
+                const float4 lo = ldg_f4(tg.tlo + tt), hi = ldg_f4(tg.thi + tt);
+                ok[u4] = ok[u4] && box_d2_plain(x, y, z, lo, hi) <= Tb;
+            }
+#pragma unroll
+            for (int u4 = 0; u4 < 4; ++u4) {
+                unsigned long long tm = __ballot(ok[u4]);
+                const int cnt = __builtin_popcountll(tm);
+                if (nt + cnt > kExactList) scan_listed();  // the list is full: scan it first
+                const int pos = nt + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(tm >> 32),
+                                                                 __builtin_amdgcn_mbcnt_lo((unsigned)tm, 0));
+                if (ok[u4]) tl[pos] = su4[u4] * kSuper + lane;
+                nt += cnt;
+            }
+            __builtin_amdgcn_wave_barrier();
+        }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    scan_listed();
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) {  // lexicographic (d^2, input index) over the wave
+        const double oD = __shfl_xor(bD, o);
+        const int oI = __shfl_xor(bI, o), oM = __shfl_xor(bM, o);
+        if (oD < bD || (oD == bD && oI < bI)) {
+            bD = oD;
+            bI = oI;
+            bM = oM;
+        }
+    }
+    return bM;
+}
+
+// The entries of this pass's list, one per wave at a time (entries gw, gw + nw,
+// ...).  kMark: every entry's final winner is stored with kResolvedBit, one
+// 64-bit agent-scope atomic store (no fence: the flag and the answer are one
+// word), for the fused accumulation's waiting threads.
+template <bool kMark>
+__device__ __forceinline__ void exact_entries(unsigned gw, unsigned nw, const double* __restrict__ src, int N,
+                                              const double* __restrict__ Qm, const TargetDesc* __restrict__ tdesc,
+                                              const float4* __restrict__ q32, const ExactArgs& ex,
+                                              unsigned long long* __restrict__ best, int* __restrict__ tl) {
+    const int lane = threadIdx.x & 63;
     // the first entry is read beside the count (the list holds at least one
     // entry per wave of the grid; an entry past the count is ignored)
     unsigned long long ent0 = ex.list[gw];
@@ -1053,121 +1216,32 @@ __global__ __launch_bounds__(256) void nn_exact_kernel(const double* __restrict_
         const unsigned long long ent =
             ((unsigned long long)(unsigned)__builtin_amdgcn_readfirstlane((unsigned)(ent0 >> 32)) << 32) |
             (unsigned)__builtin_amdgcn_readfirstlane((unsigned)ent0);
-        const int slot = (int)(ent >> 40), tk = (int)((ent >> 32) & 0xFFu), i = (int)(unsigned)ent;
-        const size_t qi = (size_t)slot * N + i;
-        const TargetDesc& tg = tdesc[tk];
-        // the entry's independent loads, one round
-        const unsigned long long bv = best[qi];
-        const float4 qq = q32[qi];
-        const unsigned sk = ex.sec[qi];
-        double Q[12];
-#pragma unroll
-        for (int t = 0; t < 12; ++t) Q[t] = Qm[12 * slot + t];
-        const double p[3] = {src[3 * i], src[3 * i + 1], src[3 * i + 2]};
-        const int nsuper = tg.nsuper;
-        float4 s0lo, s0hi;
-        load_super0(search_tgt(tg), s0lo, s0hi);
-        double q[3];
-        xform(Q, p, q);
-        // one round trip for all of it: left alone, the compiler sinks the
-        // pose, source and box loads past the band test (a second round trip)
-        asm volatile("" ::"v"(bv), "v"(qq.x), "v"(qq.y), "v"(qq.z), "v"(sk), "v"(q[0]), "v"(q[1]), "v"(q[2]),
-                     "v"(s0lo.x), "v"(s0lo.y), "v"(s0lo.z), "v"(s0hi.x), "v"(s0hi.y), "v"(s0hi.z));
-        if (bv == kNone) continue;
-        // the band test against the final winner; its band is also the culling bound
-        const float band = exact_band_hi(__uint_as_float((unsigned)(bv >> 32)), qnorm(qq.x, qq.y, qq.z));
-        if (!(__uint_as_float(sk & kKeyMask) <= band)) continue;
-        ++filed;
-        const float Tb = band * 1.0001f;
-        const float x = qq.x, y = qq.y, z = qq.z;  // the search's fp32 query: (float)(Q p - origin)
-        const double* __restrict__ t64 = tg.xyz64;
-        double bD = 3.0e300;
-        int bI = 0x7FFFFFFF, bM = (int)(unsigned)bv;
-        int nt = 0;  // listed tiles (wave-uniform)
-        auto scan_listed = [&]() {  // four tiles at a time: every lane's four loads in flight together
-            for (int c = 0; c < nt; c += 4) {
-                int kk[4], in[4];
-                double tx[4], ty[4], tz[4];
-#pragma unroll
-                for (int u4 = 0; u4 < 4; ++u4) {
-                    kk[u4] = c + u4 < nt ? tlist[wid][c + u4] * kTile + lane : -1;
-                    const int k = kk[u4] >= 0 ? kk[u4] : 0;
-                    in[u4] = __float_as_int(ldg_f32(&tg.p4[k].w));
-                    tx[u4] = ldg_f64(t64 + 3 * (size_t)k);
-                    ty[u4] = ldg_f64(t64 + 3 * (size_t)k + 1);
-                    tz[u4] = ldg_f64(t64 + 3 * (size_t)k + 2);
-                }
-#pragma unroll
-                for (int u4 = 0; u4 < 4; ++u4) {
-                    if (kk[u4] < 0 || in[u4] < 0) continue;  // past the list / padding
-                    const double tp[3] = {tx[u4], ty[u4], tz[u4]};
-                    const double D = d2_oracle(q, tp);
-                    if (D < bD || (D == bD && in[u4] < bI)) {
-                        bD = D;
-                        bI = in[u4];
-                        bM = kk[u4];
-                    }
-                }
-            }
-            nt = 0;
-        };
-        // candidate tiles: their boxes are tested four surviving super-tiles
-        // at a time and the survivors listed in LDS
-        const unsigned long long sm0 = __ballot(lane < nsuper && box_d2_plain(x, y, z, s0lo, s0hi) <= Tb);
-        for (int sb = 0; sb < nsuper; sb += 64) {
-            const int u = sb + lane;
-            unsigned long long sm = sm0;
-            if (sb > 0) {
-                const int uu = u < nsuper ? u : 0;
-                sm = __ballot(u < nsuper && box_d2_plain(x, y, z, ldg_f4(tg.slo + uu), ldg_f4(tg.shi + uu)) <= Tb);
-            }
-            while (sm) {
-                int su4[4];
-                bool ok[4];
-#pragma unroll
-                for (int u4 = 0; u4 < 4; ++u4) {
-                    su4[u4] = sm ? sb + __builtin_ctzll(sm) : -1;
-                    sm &= sm - 1;
-                    const int t = su4[u4] * kSuper + lane;
-                    ok[u4] = su4[u4] >= 0 && t < tg.ntiles;
-                    const int tt = ok[u4] ? t : 0;
-                    const float4 lo = ldg_f4(tg.tlo + tt), hi = ldg_f4(tg.thi + tt);
-                    ok[u4] = ok[u4] && box_d2_plain(x, y, z, lo, hi) <= Tb;
-                }
-#pragma unroll
-                for (int u4 = 0; u4 < 4; ++u4) {
-                    unsigned long long tm = __ballot(ok[u4]);
-                    const int cnt = __builtin_popcountll(tm);
-                    if (nt + cnt > kExactList) scan_listed();  // the list is full: scan it first
-                    const int pos = nt + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(tm >> 32),
-                                                                     __builtin_amdgcn_mbcnt_lo((unsigned)tm, 0));
-                    if (ok[u4]) tlist[wid][pos] = su4[u4] * kSuper + lane;
-                    nt += cnt;
-                }
-                __builtin_amdgcn_wave_barrier();
-            }
+        unsigned long long bv = kNone;
+        const int m = exact_entry(ent, src, N, Qm, tdesc, q32, ex, best, tl, bv, filed);
+        const size_t qi = (size_t)(ent >> 40) * N + (unsigned)ent;
+        if (lane == 0) {
+            const unsigned long long fin = m >= 0 ? (bv & 0xFFFFFFFF00000000ull) | (unsigned)m : bv;
+            if constexpr (kMark)
+                __hip_atomic_store(best + qi, fin | kResolvedBit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            else if (m >= 0)
+                best[qi] = fin;
         }
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        scan_listed();
-#pragma unroll
-        for (int o = 32; o >= 1; o >>= 1) {  // lexicographic (d^2, input index) over the wave
-            const double oD = __shfl_xor(bD, o);
-            const int oI = __shfl_xor(bI, o), oM = __shfl_xor(bM, o);
-            if (oD < bD || (oD == bD && oI < bI)) {
-                bD = oD;
-                bI = oI;
-                bM = oM;
-            }
-        }
-        if (lane == 0) best[qi] = (bv & 0xFFFFFFFF00000000ull) | (unsigned)bM;
-        // the next entry's list writes follow this entry's reads of tlist
+        // the next entry's list writes follow this entry's reads of tl
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     }
     if (lane == 0 && filed) atomicAdd(ex.total, (unsigned long long)filed);
+}
+
+__global__ __launch_bounds__(256) void nn_exact_kernel(const double* __restrict__ src, int N,
+                                                       const double* __restrict__ Qm,
+                                                       const TargetDesc* __restrict__ tdesc,
+                                                       const float4* __restrict__ q32, ExactArgs ex,
+                                                       unsigned long long* __restrict__ best) {
+    __shared__ int tlist[4][kExactList];  // a wave's listed candidate tiles
+    const unsigned gw = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6), nw = gridDim.x * (blockDim.x >> 6);
+    exact_entries<false>(gw, nw, src, N, Qm, tdesc, q32, ex, best, tlist[threadIdx.x >> 6]);
 }
 
 
@@ -1418,13 +1492,17 @@ hipError_t launch_solve6_test(const double* sums, int n, double* out_serial, dou
 
 // The GICP normal-equation terms of accumulation block `ablk` of start
 // `slot` (queries (ablk * qpt + k) * 256 + threadIdx.x): this thread's sums,
-// in query order k.  Writes the next pass's seed (prevnn).
+// in query order k.  Writes the next pass's seed (prevnn).  sec != null (the
+// fused exact mode): a query listed for the re-search (sec[] set) waits until
+// its entry is resolved and reads its final winner then.
 __device__ __forceinline__ void gicp_block_terms(int slot, int ablk, const double* __restrict__ src,
                                                  const double* __restrict__ scov, int N,
                                                  const double* __restrict__ tgt64, const double* __restrict__ tcov,
                                                  const double* __restrict__ Qm, const double* __restrict__ Rm,
                                                  double r2, unsigned long long* __restrict__ best,
-                                                 int32_t* __restrict__ prevnn, double acc[kNacc]) {
+                                                 int32_t* __restrict__ prevnn, double acc[kNacc],
+                                                 unsigned* __restrict__ sec = nullptr,
+                                                 unsigned long long* __restrict__ total = nullptr) {
 #pragma clang fp contract(off)  // no fused multiply-add: the same rounding in every caller
 #pragma unroll
     for (int v = 0; v < kNacc; ++v) acc[v] = 0.0;
@@ -1439,17 +1517,36 @@ __device__ __forceinline__ void gicp_block_terms(int slot, int ablk, const doubl
     // query order exactly as before.  Loads of a missing match read index 0.
     constexpr int kQ = accum_qpt(0);
     unsigned long long bv[kQ];
+    unsigned sk[kQ];
     double p[kQ][3], cs[kQ][6], t3[kQ][3], ct[kQ][6];
 #pragma unroll
     for (int k = 0; k < kQ; ++k) {
         const int i = (ablk * kQ + k) * 256 + threadIdx.x;
         const int ii = i < N ? i : 0;
         bv[k] = i < N ? best[(size_t)slot * N + i] : kNone;
+        sk[k] = sec && i < N ? sec[(size_t)slot * N + i] : 0xFFFFFFFFu;
 #pragma unroll
         for (int c = 0; c < 3; ++c) p[k][c] = src[3 * ii + c];
         const double* cs6 = scov + ((size_t)slot * N + ii) * 6;
 #pragma unroll
         for (int c = 0; c < 6; ++c) cs[k][c] = cs6[c];
+    }
+    if (sec) {
+#pragma unroll
+        for (int k = 0; k < kQ; ++k) {
+            if (sk[k] == 0xFFFFFFFFu) continue;  // not listed: the search's winner is final
+            const size_t qi = (size_t)slot * N + (ablk * kQ + k) * 256 + threadIdx.x;
+            // bounded: a wave never waits forever (2^22 polls); a time-out keeps
+            // the search's winner and counts in stats (exact_filed >= 2^40)
+            unsigned polls = 0;
+            unsigned long long v = bv[k];
+            while (!(v & kResolvedBit) && ++polls < (1u << 22)) {
+                __builtin_amdgcn_s_sleep(1);
+                v = __hip_atomic_load(best + qi, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+            if (!(v & kResolvedBit) && total) atomicAdd(total, 1ull << 40);
+            bv[k] = v == kNone ? kNone : v & ~kResolvedBit;
+        }
     }
 #pragma unroll
     for (int k = 0; k < kQ; ++k) {
@@ -1538,6 +1635,38 @@ __global__ __launch_bounds__(256) ORPCD_ACCUM_ATTR void gicp_accum_kernel(
     double acc[kNacc];
     gicp_block_terms(slot, blockIdx.x, src, scov, N, tg.xyz64, tg.tcov, Qm, Rm, r2, best, prevnn, acc);
     block_partial<kNacc>(acc, red, [](int v) { return v; }, partial + ((size_t)slot * nblk + blockIdx.x) * kPartialStride);
+}
+
+// Exact mode, fused: the re-search of the listed queries and the
+// accumulation in one launch (1-D grid).  Blocks [0, nexact) work the list one
+// entry per wave and publish each entry's final winner (with kResolvedBit);
+// the accumulation blocks after them ((row, block) = divmod(b -
+// nexact, nblk)) wait only for their own listed queries (~0.2%), so the
+// re-search's chain of round trips overlaps the accumulation instead of
+// preceding it (round 2: a kernel of its own, 13-23 us per pass at C2).  No
+// deadlock: a block waits only for blocks of lower index, which the
+// dispatcher placed before it (each XCD dispatches its blocks in order), and
+// those never wait.
+__global__ __launch_bounds__(256) ORPCD_ACCUM_ATTR void gicp_accum_exact_kernel(
+    const double* __restrict__ src, const double* __restrict__ scov, int N, const TargetDesc* __restrict__ tdesc,
+    TgtBounds tb, const int32_t* __restrict__ active, const double* __restrict__ Qm,
+    const double* __restrict__ Rm, const int32_t* __restrict__ done, double r2,
+    unsigned long long* __restrict__ best, int32_t* __restrict__ prevnn, double* __restrict__ partial,
+    int nblk, int nexact, const float4* __restrict__ q32, ExactArgs ex) {
+    __shared__ double red[4][kNacc];
+    __shared__ int tlist[4][kExactList];
+    if ((int)blockIdx.x < nexact) {
+        exact_entries<true>(blockIdx.x * 4 + (threadIdx.x >> 6), (unsigned)nexact * 4, src, N, Qm, tdesc, q32, ex,
+                            best, tlist[threadIdx.x >> 6]);
+        return;
+    }
+    const int b = (int)blockIdx.x - nexact, row = b / nblk, bx = b - row * nblk;
+    const int slot = active[row];
+    if (done[slot]) return;
+    const TargetDesc& tg = tdesc[target_of_row(tb, row)];
+    double acc[kNacc];
+    gicp_block_terms(slot, bx, src, scov, N, tg.xyz64, tg.tcov, Qm, Rm, r2, best, prevnn, acc, ex.sec, ex.total);
+    block_partial<kNacc>(acc, red, [](int v) { return v; }, partial + ((size_t)slot * nblk + bx) * kPartialStride);
 }
 
 // PointToPoint accumulation (TransformationEstimationPointToPoint, Eigen::
@@ -1879,13 +2008,22 @@ hipError_t launch_gicp_pass(const orpcd_ctx* c, int nact, int pass, double r2, h
 #endif
     }
     if ((e = hipGetLastError()) != hipSuccess) return e;
-    if (c->exact_live) {  // fp64 re-search of the queries the search could not certify
+    const int ablk = accum_blocks(N);
+    const bool fused = c->exact_live && c->est != kEstP2P && c->opt.exact_fused;
+    if (c->exact_live && !fused) {  // fp64 re-search of the queries the search could not certify
         nn_exact_kernel<<<(unsigned)c->opt.exact_blocks, 256, 0, s>>>(c->src.xyz64.p, N, c->Q.p, c->tdesc.p, c->q32.p,
                                                      exact_args(c, pass), c->best.p);
         if ((e = hipGetLastError()) != hipSuccess) return e;
     }
     if (mid && (e = hipEventRecord(mid, s)) != hipSuccess) return e;
-    const int ablk = accum_blocks(N);
+    if (fused) {
+        // re-search blocks: exact_fused per running start, at most exact_blocks
+        const int nexact = std::max(8, std::min(c->opt.exact_blocks, c->opt.exact_fused * nact));
+        gicp_accum_exact_kernel<<<(unsigned)(nexact + ablk * nact), 256, 0, s>>>(
+            c->src.xyz64.p, c->scov.p, N, c->tdesc.p, tb, c->active.p, c->Q.p, c->R.p, c->done.p, r2, c->best.p,
+            c->prevnn.p, c->partial.p, ablk, nexact, c->q32.p, exact_args(c, pass));
+        return hipGetLastError();
+    }
     if (c->est == kEstP2P) {
         p2p_accum_kernel<<<dim3((unsigned)ablk, (unsigned)nact), 256, 0, s>>>(
             c->src.xyz64.p, N, c->tdesc.p, tb, c->active.p, c->Q.p, c->done.p, r2, c->best.p, c->prevnn.p,

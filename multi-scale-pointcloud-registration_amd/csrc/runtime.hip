@@ -860,6 +860,10 @@ int run_passes(orpcd_ctx* c, int B, const orpcd_gicp_params* p, double* T_out, d
     if (c->exact_live) {  // entries re-searched over the batch (nn_exact_kernel adds each pass's count)
         unsigned long long tot = 0;
         CTX_CHECK(c, hipMemcpy(&tot, c->xtotal.p, 8, hipMemcpyDeviceToHost));
+        if (tot >> 40) {  // a fused accumulation thread stopped waiting for its re-search (never expected)
+            c->err = "exact_nn: a re-search result was not published in time";
+            return ORPCD_EDEVICE;
+        }
         c->stats.exact_filed += (double)tot;
     }
     return read_outputs(c, B, tiles_before, T_out, rmse_out, fitness_out, iters_out, ncorr_out);
@@ -1331,6 +1335,7 @@ int orpcd_set_option(orpcd_ctx* c, const char* key, double value) {
     else if (k == "sched_min_starts" && v >= 1) c->opt.sched_min_starts = v;
     else if (k == "exact_nn" && (v == 0 || v == 1)) c->opt.exact_nn = v;
     else if (k == "exact_blocks" && v >= 1 && v <= 65536) c->opt.exact_blocks = v;
+    else if (k == "exact_fused" && v >= 0 && v <= 4096) c->opt.exact_fused = v;
     else {
         c->err = "set_option: unknown key or bad value: " + k;
         return ORPCD_EINVAL;
