@@ -127,7 +127,8 @@ def main():
     # the search kernel that ran: the ordered dispatch for batches of >= 16
     # starts (option sched_min_starts), else the uniform-split kernel
     kname = "nn_search_sched_kernel" if st["sched_launches"] * 2 > st["launches"] else "nn_search_kernel"
-    traffic, traffic_src = pmc_traffic("orpcd::" + kname)
+    # the instantiation that ran: <true> in exact mode (the default), <false> otherwise
+    traffic, traffic_src = pmc_traffic("orpcd::" + kname, bool(getattr(opt, "_exact_nn", True)))
     avg_ms = st["ms"] / max(st["launches"], 1)
     flops_per_launch = st["pairs"] / max(st["launches"], 1) * FLOP_PER_PAIR
     achieved = flops_per_launch / (avg_ms * 1e-3) / 1e12 if avg_ms > 0 else 0.0
@@ -283,7 +284,7 @@ def align_vs_fixture(T, metric, sf, errors, gpu_seconds):
     return out
 
 
-def pmc_traffic(kernel):
+def pmc_traffic(kernel, exact=True):
     """HBM bytes per launch of `kernel` from the newest committed PMC summary
     (profiles/rNN_hbm.json: FETCH_SIZE x2 + WRITE_SIZE, MI355X_MICROARCH.md
     §HBM), collected by rocprofv3 --pmc on this same bench command."""
@@ -292,8 +293,9 @@ def pmc_traffic(kernel):
     if not files:
         return None, None
     d = json.load(open(files[-1]))
-    # the default (non-exact) instantiation of a templated kernel: "name<false>"
-    key = kernel if kernel in d else next((k for k in sorted(d) if k.startswith(kernel + "<false")), None)
+    # the instantiation of the templated search kernel that ran: "name<true>" (exact_nn) or "name<false>"
+    inst = kernel + ("<true" if exact else "<false")
+    key = kernel if kernel in d else next((k for k in sorted(d) if k.startswith(inst)), None)
     if key is None:
         return None, None
     return d[key]["hbm_bytes_per_launch_corrected"], os.path.basename(files[-1])

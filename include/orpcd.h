@@ -48,6 +48,9 @@
  *   orpcd_rng_draw_attempts
  *       the np.random draws of initialize_rotation, attempt after attempt
  *                                          Aligner/Aligner.py:125-162, 178-186
+ *   orpcd_rigid_residual
+ *       recognising the posed copy source @ R0 + t0 of a cached cloud
+ *                                          Aligner/Aligner.py:183-190
  */
 #ifndef ORPCD_H
 #define ORPCD_H
@@ -276,6 +279,15 @@ int orpcd_gicp_correspondences(orpcd_ctx* ctx, int32_t B, int32_t* idx_out);
  * cached gaussian; it is advanced in place.  Host code only (no device).   */
 int orpcd_rng_draw_attempts(uint32_t* key, int32_t* pos, int32_t* has_gauss, double* gauss, int64_t n,
                             double low, double high, double* theta, double* normal);
+
+/* ------------------------------------------------- drop-in rigid-image check
+ * out[0] = max |src - (base R + t)| over the n points and 3 axes (row
+ * vectors: src_i = base_i R + t, R row-major), out[1] = max |src|.  The
+ * drop-in GeneralizedICP.optimize (the reference's Aligner passing
+ * source @ R0 + t0 per attempt, Aligner.py:183-190) runs a call on its cached
+ * cloud only when out[0] <= 1e-12 (1 + out[1]).  Host code only.            */
+int orpcd_rigid_residual(const double* base, const double* src, int64_t n, const double* R, const double* t,
+                         double* out);
 
 /* ------------------------------------------------------------ measurement
  * Live kernel timing (hipEvents on the context's stream).  When enabled,

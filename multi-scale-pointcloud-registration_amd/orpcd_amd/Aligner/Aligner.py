@@ -49,6 +49,45 @@ from ..utils.constants import (
 from ..utils.logger_factory import LoggerFactory
 
 
+def draw_block(n: int, deg: float, mu: float, std: float, rs=None):
+    """n consecutive initialize_rotation() draws (Aligner.py:125-162) of an
+    Aligner with (deg, mu, std), bit for bit: the same stream consumption
+    (three uniform, then randn(3), per attempt) and the same translation
+    expression; the cos / sin of all 3n
+    angles by one ufunc call each and the n products r_1 (r_2 r_3) by one
+    stacked matmul, which give the scalar calls' and np.dot's values
+    (checked against the sequential draws in
+    tests/test_host.py::test_draw_block_matches_initialize_rotation).
+    rs: the global legacy RandomState (default; advanced through numpy's
+    API), another RandomState, or a _native.LegacyDraws (the same stream
+    replayed in C++, ~25 ns instead of ~4.6 us per attempt)."""
+    if isinstance(rs, _native.LegacyDraws):
+        th, g = rs.draw(n, -deg, deg)
+    else:
+        rs = np.random if rs is None else rs
+        uni, randn = rs.uniform, rs.randn
+        th = np.empty((n, 3))
+        g = np.empty((n, 3))
+        for k in range(n):
+            # uniform(size=3) consumes the stream as three scalar uniform()
+            # calls and returns the same values (low + (high - low) * double);
+            # the Gaussians stay one randn(3) per attempt (its cached second
+            # deviate makes the order matter)
+            th[k] = uni(-deg, deg, 3)
+            g[k] = randn(3)
+    t0s = list(mu + g * std)  # elementwise, as per attempt
+    c, s = np.cos(th), np.sin(th)
+    r = np.zeros((3, n, 3, 3))
+    r[0, :, 0, 0] = 1.0
+    r[0, :, 1, 1], r[0, :, 1, 2], r[0, :, 2, 1], r[0, :, 2, 2] = c[:, 0], -s[:, 0], s[:, 0], c[:, 0]
+    r[1, :, 1, 1] = 1.0
+    r[1, :, 0, 0], r[1, :, 0, 2], r[1, :, 2, 0], r[1, :, 2, 2] = c[:, 1], s[:, 1], -s[:, 1], c[:, 1]
+    r[2, :, 2, 2] = 1.0
+    r[2, :, 0, 0], r[2, :, 0, 1], r[2, :, 1, 0], r[2, :, 1, 1] = c[:, 2], -s[:, 2], s[:, 2], c[:, 2]
+    R = np.matmul(r[0], np.matmul(r[1], r[2]))
+    return list(R), t0s
+
+
 class Aligner:
     transfromation: np.ndarray = np.eye(4)
     scale_factors: np.ndarray = np.ones((1, 3))
@@ -138,42 +177,8 @@ class Aligner:
         return T
 
     def _draw_block(self, n: int, rs=None):
-        """n consecutive initialize_rotation() draws (Aligner.py:125-162), bit for
-        bit: the same stream consumption (three uniform, then randn(3), per
-        attempt) and the same translation expression; the cos / sin of all 3n
-        angles by one ufunc call each and the n products r_1 (r_2 r_3) by one
-        stacked matmul, which give the scalar calls' and np.dot's values
-        (checked against the sequential draws in
-        tests/test_host.py::test_draw_block_matches_initialize_rotation).
-        rs: the global legacy RandomState (default; advanced through numpy's
-        API), another RandomState, or a _native.LegacyDraws (the same stream
-        replayed in C++, ~25 ns instead of ~4.6 us per attempt)."""
-        deg = self._deg
-        if isinstance(rs, _native.LegacyDraws):
-            th, g = rs.draw(n, -deg, deg)
-        else:
-            rs = np.random if rs is None else rs
-            uni, randn = rs.uniform, rs.randn
-            th = np.empty((n, 3))
-            g = np.empty((n, 3))
-            for k in range(n):
-                # uniform(size=3) consumes the stream as three scalar uniform()
-                # calls and returns the same values (low + (high - low) * double);
-                # the Gaussians stay one randn(3) per attempt (its cached second
-                # deviate makes the order matter)
-                th[k] = uni(-deg, deg, 3)
-                g[k] = randn(3)
-        t0s = list(self._mu + g * self._std)  # elementwise, as per attempt
-        c, s = np.cos(th), np.sin(th)
-        r = np.zeros((3, n, 3, 3))
-        r[0, :, 0, 0] = 1.0
-        r[0, :, 1, 1], r[0, :, 1, 2], r[0, :, 2, 1], r[0, :, 2, 2] = c[:, 0], -s[:, 0], s[:, 0], c[:, 0]
-        r[1, :, 1, 1] = 1.0
-        r[1, :, 0, 0], r[1, :, 0, 2], r[1, :, 2, 0], r[1, :, 2, 2] = c[:, 1], s[:, 1], -s[:, 1], c[:, 1]
-        r[2, :, 2, 2] = 1.0
-        r[2, :, 0, 0], r[2, :, 0, 1], r[2, :, 1, 0], r[2, :, 1, 1] = c[:, 2], -s[:, 2], s[:, 2], c[:, 2]
-        R = np.matmul(r[0], np.matmul(r[1], r[2]))
-        return list(R), t0s
+        """n consecutive initialize_rotation() draws of this Aligner (draw_block)."""
+        return draw_block(n, self._deg, self._mu, self._std, rs)
 
     class _BlockStates:
         """The RNG state after attempt n of a drawn block, rebuilt on demand:

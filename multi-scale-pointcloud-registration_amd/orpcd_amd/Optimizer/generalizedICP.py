@@ -16,6 +16,9 @@ import numpy as np
 
 from .. import _native
 from ..utils.constants import (
+    __ALIGNER_DEG__,
+    __ALIGNER_MU__,
+    __ALIGNER_STD__,
     __GICP_EPSILON__,
     __ICP_RELATIVE_FITNESS__,
     __ICP_RELATIVE_RMSE__,
@@ -41,6 +44,8 @@ class GeneralizedICP(IOptimizer):
         device: Optional[int] = None,
         exact_nn: bool = True,
         rigid_cache: bool = True,
+        speculate: int = 29,
+        draw_model: Tuple[float, float, float] = (__ALIGNER_DEG__, __ALIGNER_MU__, __ALIGNER_STD__),
     ):
         self._LOG = LoggerFactory.get_logger(log_name=self.__class__.__name__)
         if max_correspondence_distance <= 0:
@@ -67,6 +72,17 @@ class GeneralizedICP(IOptimizer):
         # Aligner calls it): recognise a rigid image of the last cloud and
         # reuse its device layout and covariances (_rigid_image)
         self._rigid_cache = bool(rigid_cache)
+        # ... and run the caller's next attempts ahead as one batch (at most
+        # `speculate` of them; _speculate_next; 0: off).  draw_model: the (deg, mu, std) of the
+        # Aligner whose initialize_rotation draws are predicted.
+        self._speculate = max(0, int(speculate)) if rigid_cache else 0
+        self._draw_model = tuple(float(x) for x in draw_model)
+        self._spec = None  # predicted attempts: dict(base, target key, rows)
+        self._spec_prev = None  # the RNG state after the last optimize() call's draw
+        self._chain = None  # consecutive calls whose draws the model predicts (_speculate_next)
+        self._learned = None  # the length of the last chain: the caller's attempts per multistart
+        self._ended = None  # how the last confirmed chain ended: "switch" (new cloud / target) or "miss"
+        self.spec_stats = dict(served=0, batches=0, missed=0)
         self._base = None
         self._ctx = None
         self.last_result = None
@@ -107,8 +123,8 @@ class GeneralizedICP(IOptimizer):
         R, t = M[:3], M[3]
         if not np.all(np.isfinite(M)) or np.abs(R.T @ R - np.eye(3)).max() > 1e-12:
             return None
-        scale = 1.0 + float(np.abs(source).max())
-        if np.abs(source - (base @ R + t)).max() > 1e-12 * scale:
+        res, mag = _native.rigid_residual(base, source, R, t)  # every point, one native pass
+        if not res <= 1e-12 * (1.0 + mag):
             return None
         return R, t
 
@@ -116,22 +132,122 @@ class GeneralizedICP(IOptimizer):
         ctx = self.context
         ctx.set_target(target, self._epsilon)
         src = np.ascontiguousarray(source, dtype=np.float64)
-        pose = self._rigid_image(src) if self._rigid_cache else None
-        if pose is None:  # a new cloud: it becomes the base (layout and KNN-20 covariances once)
-            self._base = src.copy()
-            ctx.set_source(self._base)
-            pose = (np.eye(3), np.zeros(3))
+        state = np.random.get_state() if self._speculate else None  # after this attempt's draw
+        # a predicted attempt (checked on every point) needs no device work
+        row = self._speculated(src, ctx._target_key) if self._spec is not None else None
+        if row is None:
+            pose = self._rigid_image(src) if self._rigid_cache else None
+            if pose is None:  # a new cloud: it becomes the base (layout and KNN-20 covariances once)
+                self._base = src.copy()
+                ctx.set_source(self._base)
+                pose = (np.eye(3), np.zeros(3))
+            else:
+                ctx.set_source(self._base)  # cached on the device (content key)
+            if self._speculate:
+                row = self._speculate_next(ctx, pose, state)
+        self._spec_prev = state
+        if row is None:
+            r = ctx.gicp_batch(pose[0][None], pose[1][None], **self._params())
+            self.last_result = r
+            T, rmse = r["T"][0], float(r["rmse"][0])
         else:
-            ctx.set_source(self._base)  # cached on the device (content key)
-        r = ctx.gicp_batch(pose[0][None], pose[1][None], **self._params())
-        self.last_result = r
-        roto_translation = np.copy(r["T"][0])
+            T, rmse = row
+        roto_translation = np.copy(T)
         roto_translation[:3, :3] = roto_translation[:3, :3].T
-        rmse = float(r["rmse"][0])
         if rmse == 0:
             self._LOG.error(_ZERO_RMSE_MSG)
             raise ValueError(_ZERO_RMSE_MSG)
         return roto_translation, rmse
+
+    # ------------------------------------------------------------------
+    # Speculative attempts on the drop-in path.  The reference's Aligner calls
+    # optimize() once per attempt with source_initialized = source @ R0 + t0,
+    # (R0, t0) = initialize_rotation() drawn from np.random just before the
+    # call (Aligner.py:178-190).  The draw of a call is predicted from the RNG
+    # state seen by the previous call (read, never advanced: a private replay
+    # of the legacy MT19937 stream, draw_block); with the call's pose (R, t)
+    # relative to the cached base (base = S Rb + tb, source = S R0 + t0 =
+    # base R + t) it fixes the base's own pose Rb = R0 R^T, tb = (t0 - t) R^T.
+    # Two consecutive calls that agree on (Rb, tb) confirm the model (a
+    # chain); the next call's draws are then predicted and this call's start
+    # and the predicted ones run as ONE device batch.  A predicted result is
+    # returned only for a call whose source IS that predicted pose of the base
+    # (every point checked to 1e-12 of the extent, as _rigid_image), so a
+    # wrong prediction costs wasted device work, never a different answer;
+    # each start's result does not depend on its batch mates
+    # (tests/test_gpu_sched.py).  The batch covers the rest of the caller's
+    # multistart as learned from the previous chain's length (a multistart's
+    # attempts; `speculate` ahead until one has been seen).
+    # ------------------------------------------------------------------
+    def _speculated(self, src: np.ndarray, tkey):
+        sp, ch = self._spec, self._chain
+        if sp["base"] is not self._base or sp["tkey"] != tkey or not sp["rows"]:
+            self._spec = None
+            return None
+        R, t, T, rmse = sp["rows"].pop(0)
+        res, mag = _native.rigid_residual(self._base, src, R, t) if src.shape == self._base.shape else (1.0, 0.0)
+        if not res <= 1e-12 * (1.0 + mag):
+            # not the predicted attempt (the caller re-seeded, or draws
+            # differently): the chain ends here
+            self._spec = None
+            if self._rigid_image(src) is None:  # another cloud (the next multistart's): not a miss
+                self._end_chain("switch")
+            else:
+                self._end_chain("miss")
+                self.spec_stats["missed"] += 1
+            return None
+        ch["n"] += 1
+        self.spec_stats["served"] += 1
+        return T, rmse
+
+    def _end_chain(self, why):
+        ch = self._chain
+        if ch is None:
+            return
+        if ch["n"] >= 2:
+            self._learned = ch["n"]
+        self._ended = why if ch["n"] >= 2 else None
+        self._chain = None
+
+    def _speculate_next(self, ctx, pose, state):
+        """Extend or start the chain with this call; once confirmed, run this
+        call's start plus the predicted next attempts as one batch and return
+        this call's (T, rmse)."""
+        from ..Aligner.Aligner import draw_block
+
+        if self._spec_prev is None:
+            return None
+        deg, mu, std = self._draw_model
+        (R0,), (t0,) = draw_block(1, deg, mu, std, _native.LegacyDraws(self._spec_prev))
+        R, t = pose
+        Rb, tb = R0 @ R.T, (t0 - t) @ R.T
+        ch = self._chain
+        same = ch is not None and ch["base"] is self._base and ch["tkey"] == ctx._target_key
+        if same and np.abs(ch["Rb"] - Rb).max() <= 1e-9 and np.abs(ch["tb"] - tb).max() <= 1e-9:
+            ch["n"] += 1
+        else:
+            # a confirmed chain that ended on a new cloud or target (the next
+            # multistart of an align(): its draws continue the same stream) is
+            # followed at once; after a re-seed (a miss) or a disagreement,
+            # the new chain waits for a second call's confirmation
+            self._end_chain("switch" if ch is not None and not same else "miss")
+            self._chain = ch = dict(base=self._base, tkey=ctx._target_key, Rb=Rb, tb=tb, n=1)
+            if self._ended != "switch":
+                return None
+            self._ended = None
+        ahead = self._speculate if self._learned is None else min(self._speculate, self._learned - ch["n"])
+        if ahead < 1:
+            return None
+        Rb, tb = ch["Rb"], ch["tb"]
+        Rn, tn = draw_block(ahead, deg, mu, std, _native.LegacyDraws(state))
+        Rs = [R] + [Rb.T @ Rk for Rk in Rn]
+        ts = [t] + [tk - tb @ Rr for tk, Rr in zip(tn, Rs[1:])]
+        r = ctx.gicp_batch(np.array(Rs), np.array(ts), **self._params())
+        self.last_result = r
+        self.spec_stats["batches"] += 1
+        self._spec = dict(base=self._base, tkey=ctx._target_key,
+                          rows=[(Rs[k], ts[k], r["T"][k], float(r["rmse"][k])) for k in range(1, len(Rs))])
+        return r["T"][0], float(r["rmse"][0])
 
     def optimize_batch(self, source: np.ndarray, target: np.ndarray, R0: np.ndarray, t0: np.ndarray) -> dict:
         """GICP for every start ``source @ R0[b] + t0[b]`` (Aligner.py:183-190).

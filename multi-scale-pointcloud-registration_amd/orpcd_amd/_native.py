@@ -61,7 +61,7 @@ EXPORTED = ("orpcd_abi_version", "orpcd_device_count", "orpcd_ctx_create", "orpc
             "orpcd_sor", "orpcd_voxel_down_sample", "orpcd_farthest_downsample",
             "orpcd_set_option", "orpcd_set_targets", "orpcd_gicp_batch_targets", "orpcd_test_solve6",
             "orpcd_gicp_correspondences",
-            "orpcd_profiling", "orpcd_stats", "orpcd_reset_stats", "orpcd_rng_draw_attempts")
+            "orpcd_profiling", "orpcd_stats", "orpcd_reset_stats", "orpcd_rng_draw_attempts", "orpcd_rigid_residual")
 
 
 class LegacyDraws:
@@ -148,10 +148,21 @@ def load_library():
         L.orpcd_reset_stats.argtypes = [vp]
         L.orpcd_rng_draw_attempts.argtypes = [np.ctypeslib.ndpointer(dtype=np.uint32, flags="C_CONTIGUOUS"),
                                               _i32p, _i32p, _f64p, c_i64, c_dbl, c_dbl, _f64p, _f64p]
+        L.orpcd_rigid_residual.argtypes = [_f64p, _f64p, c_i64, _f64p, _f64p, _f64p]
         if L.orpcd_abi_version() != 1:
             raise NativeError("liborpcd_hip.so ABI mismatch")
         _lib = L
         return L
+
+
+def rigid_residual(base: np.ndarray, src: np.ndarray, R: np.ndarray, t: np.ndarray):
+    """(max |src - (base R + t)|, max |src|) for (n, 3) float64 clouds (host only)."""
+    out = np.zeros(2)
+    rc = load_library().orpcd_rigid_residual(base, src, len(src), np.ascontiguousarray(R, dtype=np.float64),
+                                             np.ascontiguousarray(t, dtype=np.float64), out)
+    if rc != ORPCD_OK:
+        raise NativeError(f"orpcd_rigid_residual failed (status {rc})")
+    return float(out[0]), float(out[1])
 
 
 def device_count() -> int:

@@ -314,8 +314,9 @@ def test_generalized_icp_drop_in_reuses_rigid_images():
             return dict(T=np.eye(4)[None], rmse=np.array([0.5]))
 
     src, tgt = small_pair(500, seed=3)
-    opt = GeneralizedICP()
+    opt = GeneralizedICP(speculate=0)
     fake = opt._ctx = FakeCtx()
+    fake._target_key = None
     opt.optimize(src, tgt)
     R0, t0 = rot_xyz(30, -40, 70), np.array([0.1, -0.2, 0.05])
     posed = np.dot(src.copy(), R0) + t0                # Aligner.py:183-185
@@ -332,6 +333,86 @@ def test_generalized_icp_drop_in_reuses_rigid_images():
     assert np.array_equal(fake.poses[3][0], np.eye(3))
     off = GeneralizedICP(rigid_cache=False)
     fake2 = off._ctx = FakeCtx()
+    fake2._target_key = None
     off.optimize(src, tgt)
     off.optimize(posed, tgt)
     assert np.array_equal(fake2.sources[1], posed) and np.array_equal(fake2.poses[1][0], np.eye(3))
+
+
+def test_generalized_icp_drop_in_speculates_the_callers_draws():
+    """The drop-in path over the reference-shaped Aligner (one optimize() per
+    attempt): from the second call on, the plugin predicts the caller's next
+    draws from np.random's state (without advancing it) and runs them as one
+    batch; every later call is served from that batch only after its source
+    is verified to be the predicted pose.  The results per call are those of
+    the call's own pose; np.random ends where the reference leaves it.  With
+    draws the model does not predict (deg pi/3) no chain is ever confirmed,
+    so nothing runs ahead."""
+    import math
+
+    from orpcd_amd import Aligner, GeneralizedICP, Preprocessor
+    from workloads import small_pair
+
+    class FakeCtx:  # rmse = a function of the start's posed cloud
+        def __init__(self):
+            self.batches = []
+            self._target_key = None
+
+        def set_option(self, key, value):
+            pass
+
+        def set_target(self, xyz, eps):
+            self._target_key = (xyz.shape, float(xyz.sum()))
+
+        def set_source(self, xyz):
+            self.base = xyz
+
+        def gicp_batch(self, R0, t0, **kw):
+            self.batches.append(len(R0))
+            rm = np.array([0.1 + float(np.abs(self.base @ R + t).sum()) * 1e-6 for R, t in zip(R0, t0)])
+            return dict(T=np.repeat(np.eye(4)[None], len(R0), 0), rmse=rm)
+
+    class OnlyOptimize:
+        def __init__(self, inner):
+            self.inner, self.rmse, self.expect = inner, [], []
+
+        def optimize(self, source, target, **kw):
+            T, m = self.inner.optimize(source, target, **kw)
+            self.rmse.append(m)
+            self.expect.append(0.1 + float(np.abs(source).sum()) * 1e-6)  # the call's own pose
+            return T, m
+
+    src, tgt = small_pair(400, seed=5)
+    # deg pi/2: the model's draws; two multistarts re-seeded between them (the
+    # second's first call is unpredictable: the leftover predictions of the
+    # first are checked, found wrong and dropped).  deg pi/3: never confirmed.
+    for deg, batches, served, missed in ((math.pi / 2, [1, 1, 30, 1, 1, 28], 27 + 27, 1),
+                                         (math.pi / 3, [1] * 60, 0, 0)):
+        opt = GeneralizedICP()
+        fake = opt._ctx = FakeCtx()
+        plug = OnlyOptimize(opt)
+        al = Aligner(Preprocessor([]), Preprocessor([]), plug, attempts=30, deg=deg)
+        for seed in (7, 8):
+            np.random.seed(seed)
+            al.multistart_registration(src, tgt)
+            after = np.random.get_state()
+            np.random.seed(seed)
+            for _ in range(30):
+                al.initialize_rotation()
+            ref = np.random.get_state()
+            assert np.array_equal(after[1], ref[1]) and after[2:] == ref[2:]  # the stream is not advanced
+        assert opt.spec_stats["served"] == served and opt.spec_stats["missed"] == missed, opt.spec_stats
+        assert fake.batches == batches, fake.batches
+        assert np.allclose(plug.rmse, plug.expect, rtol=0, atol=1e-12)
+    # an align()-like sequence: each multistart on a new (scaled) cloud, the
+    # stream never re-seeded -- a confirmed chain that ends on a new cloud is
+    # followed at once (its first call already runs the batch)
+    opt = GeneralizedICP()
+    fake = opt._ctx = FakeCtx()
+    plug = OnlyOptimize(opt)
+    al = Aligner(Preprocessor([]), Preprocessor([]), plug, attempts=30)
+    np.random.seed(9)
+    for k in range(3):
+        al.multistart_registration(src * (1.0 + 0.1 * k), tgt)
+    assert fake.batches == [1, 1, 30, 29, 1, 30], fake.batches
+    assert opt.spec_stats["missed"] == 0 and np.allclose(plug.rmse, plug.expect, rtol=0, atol=1e-12)

@@ -5,15 +5,23 @@ the reference's own Aligner calls the plugin) against the batched multistart
 
     python tools/bench_dropin.py [--reps 3] [--out profiles/r03_dropin.json]
 
-Three legs, same seeds (np.random.seed(1000 + k)), 30 attempts each:
+Multistart legs: np.random.seed(1000) once, then `reps` consecutive
+multistarts (the stream continues, as between the multistarts of an
+align()), 30 attempts each, timed per multistart (median):
   batched      Aligner -> GeneralizedICP.optimize_batch
   dropin       Aligner over a plugin exposing only optimize(): every call
                hands over source @ R0 + t0; the plugin recognises the rigid
-               image of its cached cloud (GeneralizedICP._rigid_image) and runs
-               the start on the cached layout / covariances
+               image of its cached cloud (GeneralizedICP._rigid_image), runs
+               the start on the cached layout / covariances, and from the
+               second call on runs the predicted next attempts ahead as one
+               batch (GeneralizedICP speculate=29, the default)
+  dropin_nospec  the same with speculate=0: one device batch per call
   dropin_cold  the same with rigid_cache=False: every posed copy uploaded,
                laid out and its KNN-20 covariances recomputed, as Open3D does
 Per-start results of the drop-in legs are compared with the batched table.
+align legs: the complete C2 align() (refine off, np.random.seed(0)) through
+the batched Aligner and through the reference-shaped sequential Aligner over
+the drop-in plugin (second of two runs each).
 """
 import argparse
 import json
@@ -57,10 +65,10 @@ def main():
         np.random.seed(999)
         al.multistart_registration(s, t)  # warm-up
         times, rmse = [], []
+        np.random.seed(1000)
         for k in range(a.reps):
             if isinstance(opt, OnlyOptimize):
                 opt.rmse = []
-            np.random.seed(1000 + k)
             t0 = time.perf_counter()
             al.multistart_registration(s, t)
             times.append(time.perf_counter() - t0)
@@ -69,14 +77,37 @@ def main():
         return float(np.median(times)), rmse
 
     tb, rb = leg(GeneralizedICP(), "batched")
-    td, rd = leg(OnlyOptimize(GeneralizedICP()), "dropin")
+    spec = GeneralizedICP()
+    td, rd = leg(OnlyOptimize(spec), "dropin")
+    tn, rn = leg(OnlyOptimize(GeneralizedICP(speculate=0)), "dropin_nospec")
     tc, rc = leg(OnlyOptimize(GeneralizedICP(rigid_cache=False)), "dropin_cold")
+    from workloads import c2_pair as pair
+
+    def align_leg(opt, name):
+        src_raw, tgt_raw = pair(50_000)
+        for _ in range(2):
+            np.random.seed(0)
+            al = Aligner(Preprocessor([]), Preprocessor([]), opt, attempts=a.attempts)
+            t0 = time.perf_counter()
+            T, m, sf, err = al.align(src_raw.copy(), tgt_raw.copy(), refine_registration=False)
+            dt = time.perf_counter() - t0
+        print(f"{name} align: {dt:.3f} s, rmse {m:.12g}", file=sys.stderr, flush=True)
+        return dt, float(m)
+
+    ta_b, ma_b = align_leg(GeneralizedICP(), "batched")
+    spec_al = GeneralizedICP()
+    ta_d, ma_d = align_leg(OnlyOptimize(spec_al), "dropin")
     d_warm = max(float(np.abs(x - y).max()) for x, y in zip(rd, rb))
     d_cold = max(float(np.abs(x - y).max()) for x, y in zip(rc, rb))
+    d_nospec = max(float(np.abs(x - y).max()) for x, y in zip(rn, rb))
     res = {"metric": "multistart wall-clock at C2 (30 starts), drop-in sequential vs batched", "unit": "ms",
            "batched_ms": round(tb * 1e3, 2), "dropin_ms": round(td * 1e3, 2), "dropin_cold_ms": round(tc * 1e3, 2),
+           "dropin_nospec_ms": round(tn * 1e3, 2), "speculation": spec.spec_stats,
            "dropin_over_batched": round(td / tb, 2), "dropin_cold_over_batched": round(tc / tb, 2),
-           "max_abs_d_rmse_vs_batched": {"dropin": d_warm, "dropin_cold": d_cold},
+           "max_abs_d_rmse_vs_batched": {"dropin": d_warm, "dropin_nospec": d_nospec, "dropin_cold": d_cold},
+           "align": {"batched_s": round(ta_b, 4), "dropin_s": round(ta_d, 4),
+                     "dropin_over_batched": round(ta_d / ta_b, 2), "d_rmse": abs(ma_d - ma_b),
+                     "speculation": spec_al.spec_stats},
            "reps": a.reps, "attempts": a.attempts}
     line = json.dumps(res)
     print(line)

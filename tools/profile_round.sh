@@ -14,3 +14,4 @@ timeout -k 10 400 python3 tools/bench_c4_align.py --out gpurun_out/c4_align.json
 timeout -k 10 300 python3 tools/bench_fgr.py --out gpurun_out/fgr_c3.json > gpurun_out/fgr.log 2>&1
 timeout -k 10 400 python3 tools/bench_c5.py --out gpurun_out/c5.json > gpurun_out/c5.log 2>&1
 timeout -k 10 300 python3 tools/bench_prep.py --out gpurun_out/prep.json > gpurun_out/prep.log 2>&1
+timeout -k 10 300 python3 tools/bench_dropin.py --reps 3 --out gpurun_out/dropin.json > gpurun_out/dropin.log 2>&1
