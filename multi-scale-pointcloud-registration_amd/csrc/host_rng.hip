@@ -23,6 +23,7 @@
 // block sizes, including odd attempt counts (a cached gaussian across blocks).
 #include <cmath>
 #include <cstdint>
+#include <limits>
 
 #include "orpcd_internal.h"
 
@@ -111,16 +112,22 @@ extern "C" int orpcd_rigid_residual(const double* base, const double* src, int64
                                     const double* t, double* out) {
     if (!base || !src || !R || !t || !out || n < 0) return ORPCD_EINVAL;
     double res = 0.0, mag = 0.0;
-    for (int64_t i = 0; i < n; ++i) {
+    bool nan = false;
+    const double R0 = R[0], R1 = R[1], R2 = R[2], R3 = R[3], R4 = R[4], R5 = R[5], R6 = R[6], R7 = R[7], R8 = R[8];
+    for (int64_t i = 0; i < n; ++i) {  // plain compares (vectorisable; fmax's NaN rules are not)
         const double* b = base + 3 * i;
         const double* s = src + 3 * i;
-        for (int c = 0; c < 3; ++c) {
-            const double v = b[0] * R[c] + b[1] * R[3 + c] + b[2] * R[6 + c] + t[c];
-            res = std::fmax(res, std::fabs(s[c] - v));
-            mag = std::fmax(mag, std::fabs(s[c]));
-        }
-        if (res != res) break;  // NaN: not an image
+        const double d0 = std::fabs(s[0] - (b[0] * R0 + b[1] * R3 + b[2] * R6 + t[0]));
+        const double d1 = std::fabs(s[1] - (b[0] * R1 + b[1] * R4 + b[2] * R7 + t[1]));
+        const double d2 = std::fabs(s[2] - (b[0] * R2 + b[1] * R5 + b[2] * R8 + t[2]));
+        const double dm = d0 > d1 ? (d0 > d2 ? d0 : d2) : (d1 > d2 ? d1 : d2);
+        const double a0 = std::fabs(s[0]), a1 = std::fabs(s[1]), a2 = std::fabs(s[2]);
+        const double am = a0 > a1 ? (a0 > a2 ? a0 : a2) : (a1 > a2 ? a1 : a2);
+        res = dm > res ? dm : res;
+        mag = am > mag ? am : mag;
+        nan |= (d0 != d0) | (d1 != d1) | (d2 != d2);
     }
+    if (nan) res = std::numeric_limits<double>::infinity();  // not an image
     out[0] = res;
     out[1] = mag;
     return ORPCD_OK;

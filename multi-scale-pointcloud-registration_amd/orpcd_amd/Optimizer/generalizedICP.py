@@ -10,6 +10,7 @@ comes back with R transposed (row-vector convention, :72-74) and a
 multistart attempts of one target scale run as ONE device batch
 (``orpcd_gicp_batch``) instead of ``attempts`` sequential calls.
 """
+import time
 from typing import Optional, Tuple
 
 import numpy as np
@@ -80,9 +81,10 @@ class GeneralizedICP(IOptimizer):
         self._spec = None  # predicted attempts: dict(base, target key, rows)
         self._spec_prev = None  # the RNG state after the last optimize() call's draw
         self._chain = None  # consecutive calls whose draws the model predicts (_speculate_next)
-        self._learned = None  # the length of the last chain: the caller's attempts per multistart
+        self._learned = None  # the caller's attempts per multistart, once seen (_count_call)
+        self._calls_key, self._calls, self._calls_ok = None, 0, False
         self._ended = None  # how the last confirmed chain ended: "switch" (new cloud / target) or "miss"
-        self.spec_stats = dict(served=0, batches=0, missed=0)
+        self.spec_stats = dict(served=0, batches=0, missed=0, batch_s=0.0, serve_s=0.0)
         self._base = None
         self._ctx = None
         self.last_result = None
@@ -145,6 +147,8 @@ class GeneralizedICP(IOptimizer):
                 ctx.set_source(self._base)  # cached on the device (content key)
             if self._speculate:
                 row = self._speculate_next(ctx, pose, state)
+        else:
+            self._count_call(ctx._target_key)
         self._spec_prev = state
         if row is None:
             r = ctx.gicp_batch(pose[0][None], pose[1][None], **self._params())
@@ -176,10 +180,17 @@ class GeneralizedICP(IOptimizer):
     # wrong prediction costs wasted device work, never a different answer;
     # each start's result does not depend on its batch mates
     # (tests/test_gpu_sched.py).  The batch covers the rest of the caller's
-    # multistart as learned from the previous chain's length (a multistart's
-    # attempts; `speculate` ahead until one has been seen).
+    # multistart as learned from a chain that ended on a new cloud (a
+    # multistart's attempts; `speculate` ahead until one has been seen).
     # ------------------------------------------------------------------
     def _speculated(self, src: np.ndarray, tkey):
+        t_0 = time.perf_counter()
+        r = self._speculated_row(src, tkey)
+        if r is not None:
+            self.spec_stats["serve_s"] += time.perf_counter() - t_0
+        return r
+
+    def _speculated_row(self, src: np.ndarray, tkey):
         sp, ch = self._spec, self._chain
         if sp["base"] is not self._base or sp["tkey"] != tkey or not sp["rows"]:
             self._spec = None
@@ -204,10 +215,20 @@ class GeneralizedICP(IOptimizer):
         ch = self._chain
         if ch is None:
             return
-        if ch["n"] >= 2:
-            self._learned = ch["n"]
         self._ended = why if ch["n"] >= 2 else None
         self._chain = None
+
+    def _count_call(self, tkey):
+        """Calls on the current (cloud, target): a confirmed run of them that
+        ends on a new cloud or target is one multistart of the caller, whose
+        length (its attempts) sizes later speculation."""
+        key = (id(self._base), tkey)
+        if key != self._calls_key:
+            if self._calls_key is not None and self._calls_ok and self._calls >= 2:
+                self._learned = self._calls
+            self._calls_key, self._calls, self._calls_ok = key, 0, False
+        self._calls += 1
+        return self._calls
 
     def _speculate_next(self, ctx, pose, state):
         """Extend or start the chain with this call; once confirmed, run this
@@ -215,6 +236,7 @@ class GeneralizedICP(IOptimizer):
         this call's (T, rmse)."""
         from ..Aligner.Aligner import draw_block
 
+        c = self._count_call(ctx._target_key)  # this call's position on its cloud and target
         if self._spec_prev is None:
             return None
         deg, mu, std = self._draw_model
@@ -235,14 +257,22 @@ class GeneralizedICP(IOptimizer):
             if self._ended != "switch":
                 return None
             self._ended = None
-        ahead = self._speculate if self._learned is None else min(self._speculate, self._learned - ch["n"])
+        # the rest of the caller's multistart when its length is known (a
+        # chain that ended on a new cloud or target: an align()'s multistarts),
+        # else `speculate` ahead; predictions left over past a multistart's end
+        # stay valid while the stream continues on the same cloud and target
+        self._calls_ok = True
+        A = self._learned
+        ahead = self._speculate if A is None else min(self._speculate, (A - c % A) % A)
         if ahead < 1:
             return None
         Rb, tb = ch["Rb"], ch["tb"]
         Rn, tn = draw_block(ahead, deg, mu, std, _native.LegacyDraws(state))
         Rs = [R] + [Rb.T @ Rk for Rk in Rn]
         ts = [t] + [tk - tb @ Rr for tk, Rr in zip(tn, Rs[1:])]
+        t_0 = time.perf_counter()
         r = ctx.gicp_batch(np.array(Rs), np.array(ts), **self._params())
+        self.spec_stats["batch_s"] += time.perf_counter() - t_0
         self.last_result = r
         self.spec_stats["batches"] += 1
         self._spec = dict(base=self._base, tkey=ctx._target_key,

@@ -42,11 +42,22 @@ class OnlyOptimize:
     def __init__(self, inner):
         self.inner = inner
         self.rmse = []
+        self.inside = 0.0  # seconds inside the plugin's optimize()
 
     def optimize(self, source, target, **kw):
+        t0 = time.perf_counter()
         T, m = self.inner.optimize(source, target, **kw)
+        self.inside += time.perf_counter() - t0
         self.rmse.append(m)
         return T, m
+
+
+class Constant:
+    """A plugin that returns at once: the reference loop's own cost per
+    multistart (deepcopy, initialize_rotation, np.dot per attempt)."""
+
+    def optimize(self, source, target, **kw):
+        return np.eye(4), 1.0
 
 
 def main():
@@ -64,18 +75,27 @@ def main():
         al = Aligner(Preprocessor([]), Preprocessor([]), opt, attempts=a.attempts)
         np.random.seed(999)
         al.multistart_registration(s, t)  # warm-up
-        times, rmse = [], []
+        times, rmse, inside = [], [], []
         np.random.seed(1000)
         for k in range(a.reps):
             if isinstance(opt, OnlyOptimize):
                 opt.rmse = []
+                opt.inside = 0.0
             t0 = time.perf_counter()
             al.multistart_registration(s, t)
             times.append(time.perf_counter() - t0)
-            rmse.append(np.array(opt.rmse) if isinstance(opt, OnlyOptimize) else al.history[-1]["rmse"])
-        print(f"{name}: {np.median(times) * 1e3:.1f} ms per multistart", file=sys.stderr, flush=True)
+            if isinstance(opt, OnlyOptimize):
+                inside.append(opt.inside)
+            rmse.append(np.array(opt.rmse) if isinstance(opt, OnlyOptimize) else
+                        al.history[-1]["rmse"] if hasattr(al, "history") and al.history else None)
+        print(f"{name}: {np.median(times) * 1e3:.1f} ms per multistart"
+              + (f" ({np.median(inside) * 1e3:.1f} ms inside optimize())" if inside else ""), file=sys.stderr, flush=True)
+        leg.inside[name] = round(float(np.median(inside)) * 1e3, 2) if inside else None
         return float(np.median(times)), rmse
 
+    leg.inside = {}
+
+    tk, _ = leg(Constant(), "caller_only")
     tb, rb = leg(GeneralizedICP(), "batched")
     spec = GeneralizedICP()
     td, rd = leg(OnlyOptimize(spec), "dropin")
@@ -103,6 +123,7 @@ def main():
     res = {"metric": "multistart wall-clock at C2 (30 starts), drop-in sequential vs batched", "unit": "ms",
            "batched_ms": round(tb * 1e3, 2), "dropin_ms": round(td * 1e3, 2), "dropin_cold_ms": round(tc * 1e3, 2),
            "dropin_nospec_ms": round(tn * 1e3, 2), "speculation": spec.spec_stats,
+           "caller_only_ms": round(tk * 1e3, 2), "inside_optimize_ms": leg.inside,
            "dropin_over_batched": round(td / tb, 2), "dropin_cold_over_batched": round(tc / tb, 2),
            "max_abs_d_rmse_vs_batched": {"dropin": d_warm, "dropin_nospec": d_nospec, "dropin_cold": d_cold},
            "align": {"batched_s": round(ta_b, 4), "dropin_s": round(ta_d, 4),
