@@ -98,7 +98,7 @@ def main():
     if st["launches"] > 0:
         avg_ms = st["ms"] / st["launches"]
         achieved = st["pairs"] / st["launches"] * 8 / (avg_ms * 1e-3) / 1e12
-        line["roofline"] = {"bound": "mfma", "kernel": "nn_search_kernel", "achieved": round(achieved, 3),
+        line["roofline"] = {"bound": "valu_fp32", "kernel": "nn_search_kernel", "achieved": round(achieved, 3),
                             "peak": FP32_PEAK_TF, "unit": "TFLOP/s", "frac": round(achieved / FP32_PEAK_TF, 4),
                             "avg_launch_ms": round(avg_ms, 4),
                             "pairs_vs_bruteforce": round(st["pairs"] / st["launches"] / (hi - lo) / len(tgt), 6)}
