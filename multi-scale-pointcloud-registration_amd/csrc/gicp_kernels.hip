@@ -741,9 +741,19 @@ __global__ __launch_bounds__(256) void xform_queries_kernel(const double* __rest
         x = (float)(q[0] - tg.ox), y = (float)(q[1] - tg.oy), z = (float)(q[2] - tg.oz);
         bound = r2s;
         const int jp = prevnn[(size_t)slot * N + i];
-        if (jp >= 0) {
-            bound = fminf(bound, seed_bound(d2f(x, y, z, p4[jp])));
-        } else if (jp == kNoSeed || reseed) {
+        if (jp >= 0) bound = fminf(bound, seed_bound(d2f(x, y, z, p4[jp])));
+        if (tg.sgrid) {
+            // the target nearest to the centre of the query's seed-grid cell
+            // (clamped to the grid): early passes move the poses far, so the
+            // previous correspondence alone is a loose bound (CPU study: a
+            // median 1.8x the nearest distance in pass 1, 1.007x with this
+            // seed beside it), and pass 0 needs no strided representatives
+            const int cx = min(kSeedGrid - 1, max(0, (int)((x - tg.sg_lo[0]) * tg.sg_inv[0])));
+            const int cy = min(kSeedGrid - 1, max(0, (int)((y - tg.sg_lo[1]) * tg.sg_inv[1])));
+            const int cz = min(kSeedGrid - 1, max(0, (int)((z - tg.sg_lo[2]) * tg.sg_inv[2])));
+            const int g = tg.sgrid[(cx * kSeedGrid + cy) * kSeedGrid + cz];
+            bound = fminf(bound, seed_bound(d2f(x, y, z, p4[g])));
+        } else if (jp < 0 && (jp == kNoSeed || reseed)) {
             for (int t = 0; t < tg.ntiles; t += tg.seed_stride)
                 bound = fminf(bound, seed_bound(d2f(x, y, z, p4[t * kTile])));
         }
@@ -1768,6 +1778,69 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 2))) void
     solve_start<kEst>(slot, s, N, pass, max_iter, rel_fit, rel_rmse, a, pin);
 }
 
+int seed_stride_for(int64_t ntiles, int reps = 512);
+
+// The seed grid of a target (CloudLayout::sgrid): cell i of kSeedGrid^3 over
+// the target's bounding box holds the Morton index of the target nearest to
+// its centre (fp32 culled search as nn1_kernel's, strided representative
+// seeds).  Only a bound seed: any target would do, the nearest is the best.
+__global__ __launch_bounds__(kCBlock) void seed_grid_kernel(const float4* __restrict__ p4,
+                                                            const float4* __restrict__ tlo,
+                                                            const float4* __restrict__ thi,
+                                                            const float4* __restrict__ qbox, int ntiles,
+                                                            const float4* __restrict__ slo,
+                                                            const float4* __restrict__ shi, int nsuper,
+                                                            int seed_stride, float lx, float ly, float lz, float cxs,
+                                                            float cys, float czs, int32_t* __restrict__ grid) {
+    __shared__ float4 stage[kCWaves][kTile];
+    constexpr int nq = kSeedGrid * kSeedGrid * kSeedGrid;
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const int i0 = blockIdx.x * kCBlockQ + wid * (64 * kCQPT) + lane;
+    float qx[kCQPT], qy[kCQPT], qz[kCQPT], bound[kCQPT], bd[kCQPT];
+    int bj[kCQPT];
+#pragma unroll
+    for (int k = 0; k < kCQPT; ++k) {
+        const int i = i0 + 64 * k;
+        const bool valid = i < nq;
+        qx[k] = lx + ((float)(i / (kSeedGrid * kSeedGrid)) + 0.5f) * cxs;
+        qy[k] = ly + ((float)((i / kSeedGrid) % kSeedGrid) + 0.5f) * cys;
+        qz[k] = lz + ((float)(i % kSeedGrid) + 0.5f) * czs;
+        float b = valid ? 3.0e38f : 0.0f;
+        if (valid)
+            for (int t = 0; t < ntiles; t += seed_stride)
+                b = fminf(b, seed_bound(d2f(qx[k], qy[k], qz[k], p4[t * kTile])));
+        bound[k] = b;
+    }
+    culled_search<false>(stage[wid], p4, tlo, thi, qbox, ntiles, slo, shi, nsuper, 1, 1, 0, qx, qy, qz, bound, bd, bj,
+                         lane < nsuper ? slo[lane] : make_float4(0.f, 0.f, 0.f, 0.f),
+                         lane < nsuper ? shi[lane] : make_float4(0.f, 0.f, 0.f, 0.f));
+#pragma unroll
+    for (int k = 0; k < kCQPT; ++k) {
+        const int i = i0 + 64 * k;
+        if (i < nq) grid[i] = bj[k] >= 0 ? bj[k] : 0;
+    }
+}
+
+hipError_t launch_seed_grid(CloudLayout& L, hipStream_t s) {
+    constexpr int nq = kSeedGrid * kSeedGrid * kSeedGrid;
+    hipError_t e = L.sgrid.ensure(nq);
+    if (e != hipSuccess) return e;
+    float cs[3];
+    for (int a = 0; a < 3; ++a) {
+        // the grid in the fp32 frame, a hair larger than the box; a
+        // degenerate axis gets a tiny cell (every query clamps into a cell)
+        const double ext = std::max(L.hi[a] - L.lo[a], 1e-30);
+        const double cell = ext * (1.0 + 1e-6) / kSeedGrid;
+        L.sg_lo[a] = (float)(L.lo[a] - L.org[a] - 1e-7 * ext);
+        cs[a] = (float)cell;
+        L.sg_inv[a] = (float)(1.0 / cell);
+    }
+    seed_grid_kernel<<<(unsigned)((nq + kCBlockQ - 1) / kCBlockQ), kCBlock, 0, s>>>(
+        L.p4.p, L.tlo.p, L.thi.p, L.qbox.p, (int)L.ntiles, L.slo.p, L.shi.p, (int)L.nsuper,
+        seed_stride_for(L.ntiles, 512), L.sg_lo[0], L.sg_lo[1], L.sg_lo[2], cs[0], cs[1], cs[2], L.sgrid.p);
+    return hipGetLastError();
+}
+
 // Kernel-level 1-NN (orpcd_nn1_radius): the same culled search on Morton-
 // ordered targets (representative seed, S = 1), fp64 re-check, no
 // accumulation.  Queries in input order.
@@ -1819,7 +1892,7 @@ __global__ __launch_bounds__(kCBlock) void nn1_kernel(const double* __restrict__
     }
 }
 
-int seed_stride_for(int64_t ntiles, int reps = 512) {  // at most ~reps representatives per query
+int seed_stride_for(int64_t ntiles, int reps) {  // at most ~reps representatives per query
     return (int)std::max<int64_t>(1, (ntiles + reps - 1) / reps);
 }
 
@@ -1930,6 +2003,11 @@ void write_target_desc(const CloudLayout& L, const double* tcov, int seed_reps, 
     d.ox = L.org[0];
     d.oy = L.org[1];
     d.oz = L.org[2];
+    d.sgrid = L.sgrid.n ? L.sgrid.p : nullptr;
+    for (int a = 0; a < 3; ++a) {
+        d.sg_lo[a] = L.sg_lo[a];
+        d.sg_inv[a] = L.sg_inv[a];
+    }
 }
 
 static SolveArgs solve_args(const orpcd_ctx* c) {

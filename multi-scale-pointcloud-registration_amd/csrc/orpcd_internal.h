@@ -88,6 +88,11 @@ struct CloudLayout {
     DevBuf<float4> tlo, thi;  // per 64-point tile AABB
     DevBuf<float4> qbox;      // per tile: its four 16-point quarters' AABBs (lo x4, hi x4)
     DevBuf<float4> slo, shi;  // per super-tile (64 tiles) AABB
+    double lo[3] = {0.0, 0.0, 0.0}, hi[3] = {0.0, 0.0, 0.0};  // bounding box (absolute)
+    // seed grid (targets): kSeedGrid^3 cells over the bounding box, per cell the
+    // Morton index of the target nearest to its centre (a search bound seed)
+    DevBuf<int32_t> sgrid;
+    float sg_lo[3] = {0.f, 0.f, 0.f}, sg_inv[3] = {0.f, 0.f, 0.f};  // fp32 frame: cell = (x - lo) * inv
     DevBuf<uint32_t> codes;   // scratch (2n)
     DevBuf<int32_t> ids;      // scratch
     DevBuf<unsigned char> sort_tmp;
@@ -100,6 +105,7 @@ struct CloudLayout {
         qbox.release();
         slo.release();
         shi.release();
+        sgrid.release();
         codes.release();
         ids.release();
         sort_tmp.release();
@@ -181,6 +187,8 @@ struct TargetDesc {
     const double *xyz64, *tcov;                        // fp64 points and GICP covariances (Morton order)
     int ntiles, nsuper, seed_stride, pad;
     double ox, oy, oz;                                 // fp32 frame origin (CloudLayout::org)
+    const int32_t* sgrid;                              // seed grid (CloudLayout::sgrid) or null
+    float sg_lo[3], sg_inv[3];
 };
 
 struct TgtBounds {
@@ -345,6 +353,12 @@ namespace orpcd {
 hipError_t launch_gather_rows(const double* in, const int32_t* idx, int64_t offset, int64_t n, int w, double* out,
                               hipStream_t s);
 // origin: the fp32 frame origin stored in L.org (the bbox centre)
+// gicp_kernels.hip: the target's seed grid (CloudLayout::sgrid)
+#ifndef ORPCD_SEED_GRID
+#define ORPCD_SEED_GRID 64
+#endif
+constexpr int kSeedGrid = ORPCD_SEED_GRID;  // cells per axis
+hipError_t launch_seed_grid(CloudLayout& L, hipStream_t s);
 hipError_t build_layout(const double* dev_in64, int64_t n, const double bbox_lo[3], double bbox_ext,
                         const double origin[3], CloudLayout& L, bool with_tiles, hipStream_t s);
 

@@ -68,7 +68,11 @@ int layout_from_device(orpcd_ctx* c, const double* host_xyz, const double* dev_x
                        bool tiles, double* margin = nullptr) {
     double lo[3], hi[3], org[3], ext;
     host_bbox(host_xyz, n, lo, hi, &ext);
-    for (int a = 0; a < 3; ++a) org[a] = 0.5 * (lo[a] + hi[a]);
+    for (int a = 0; a < 3; ++a) {
+        org[a] = 0.5 * (lo[a] + hi[a]);
+        L.lo[a] = lo[a];
+        L.hi[a] = hi[a];
+    }
     if (margin) *margin = coord_margin(lo, hi, org);
     CTX_CHECK(c, build_layout(dev_xyz, n, lo, ext, org, L, tiles, c->stream));
     return ORPCD_OK;
@@ -88,6 +92,7 @@ int upload_target_k(orpcd_ctx* c, int k, const double* xyz, int64_t m, double ep
     double margin = 0.0;
     int rc = upload_layout(c, xyz, m, c->tgts[k], true, &margin);
     if (rc) return rc;
+    CTX_CHECK(c, launch_seed_grid(c->tgts[k], c->stream));
     CTX_CHECK(c, c->tcovs[k].ensure((size_t)m * 6));
     CTX_CHECK(c, c->scratch64b.ensure((size_t)m * 6));
     if (eps >= 0.0) {
