@@ -355,7 +355,7 @@ hipError_t launch_gather_rows(const double* in, const int32_t* idx, int64_t offs
 // origin: the fp32 frame origin stored in L.org (the bbox centre)
 // gicp_kernels.hip: the target's seed grid (CloudLayout::sgrid)
 #ifndef ORPCD_SEED_GRID
-#define ORPCD_SEED_GRID 64
+#define ORPCD_SEED_GRID 48
 #endif
 constexpr int kSeedGrid = ORPCD_SEED_GRID;  // cells per axis
 hipError_t launch_seed_grid(CloudLayout& L, hipStream_t s);
