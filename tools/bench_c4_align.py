@@ -48,6 +48,7 @@ def main():
     ap.add_argument("--out", default=None)
     ap.add_argument("--depth", type=int, default=None, help="speculative_depth of the ranks (default: auto)")
     ap.add_argument("--interleave", action="store_true", help="ranks shard the flat start list attempt-major")
+    ap.add_argument("--profile-rank", type=int, default=None, help="cProfile this rank's align() (host time)")
     a = ap.parse_args()
     from orpcd_amd import Aligner, GeneralizedICP, Preprocessor, parallel
     from workloads import c2_pair
@@ -124,7 +125,15 @@ def main():
 
         parallel.world = lambda r=r: (r, a.ranks)
         parallel.allgather_records = replay
+        if a.profile_rank == r:
+            import cProfile
+            import pstats
+            pr = cProfile.Profile()
+            pr.enable()
         w, c, res, _ = align_once(a.depth)
+        if a.profile_rank == r:
+            pr.disable()
+            pstats.Stats(pr, stream=sys.stderr).sort_stats("tottime").print_stats(25)
         assert res["sf"] == res1["sf"] and res["metric"] == res1["metric"], (r, res, res1)
         rank_wall.append(w)
         rank_calls.append(c)
