@@ -4,6 +4,7 @@
 set -e
 mkdir -p gpurun_out
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
+rm -rf gpurun_out/kt gpurun_out/fetch gpurun_out/write gpurun_out/sq
 timeout -k 10 400 python3 bench.py > gpurun_out/bench.json 2> gpurun_out/bench.err
 B="python3 bench.py --cpu-seconds 0 --align 0"  # default steps/warmup: the same kernel mix as the bench line
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/kt -- $B > gpurun_out/kt.log 2>&1
@@ -14,4 +15,4 @@ timeout -k 10 400 python3 tools/bench_c4_align.py --out gpurun_out/c4_align.json
 timeout -k 10 300 python3 tools/bench_fgr.py --out gpurun_out/fgr_c3.json > gpurun_out/fgr.log 2>&1
 timeout -k 10 400 python3 tools/bench_c5.py --out gpurun_out/c5.json > gpurun_out/c5.log 2>&1
 timeout -k 10 300 python3 tools/bench_prep.py --out gpurun_out/prep.json > gpurun_out/prep.log 2>&1
-timeout -k 10 300 python3 tools/bench_dropin.py --reps 3 --out gpurun_out/dropin.json > gpurun_out/dropin.log 2>&1
+timeout -k 10 300 python3 tools/bench_dropin.py --reps 5 --out gpurun_out/dropin.json > gpurun_out/dropin.log 2>&1
