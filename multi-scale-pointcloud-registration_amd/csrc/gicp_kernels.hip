@@ -1784,16 +1784,17 @@ int seed_stride_for(int64_t ntiles, int reps = 512);
 // the target's bounding box holds the Morton index of the target nearest to
 // its centre (fp32 culled search as nn1_kernel's, strided representative
 // seeds).  Only a bound seed: any target would do, the nearest is the best.
-__global__ __launch_bounds__(kCBlock) void seed_grid_kernel(const float4* __restrict__ p4,
-                                                            const float4* __restrict__ tlo,
-                                                            const float4* __restrict__ thi,
-                                                            const float4* __restrict__ qbox, int ntiles,
-                                                            const float4* __restrict__ slo,
-                                                            const float4* __restrict__ shi, int nsuper,
-                                                            int seed_stride, float lx, float ly, float lz, float cxs,
-                                                            float cys, float czs, int32_t* __restrict__ grid) {
+// One launch builds the grids of several targets (grid.y = target, layouts
+// from their TargetDesc): a single grid is a latency-bound launch of ~860
+// waves (~0.4 ms), so six of them in sequence cost 2.4 ms per set_targets.
+__global__ __launch_bounds__(kCBlock) void seed_grid_kernel(const TargetDesc* __restrict__ tdesc, int first) {
     __shared__ float4 stage[kCWaves][kTile];
     constexpr int nq = kSeedGrid * kSeedGrid * kSeedGrid;
+    const TargetDesc& tg = tdesc[first + blockIdx.y];
+    const float4* __restrict__ p4 = tg.p4;
+    const int ntiles = tg.ntiles, nsuper = tg.nsuper;
+    const int seed_stride = max(1, (ntiles + 511) / 512);  // ~512 representatives
+    const float cxs = 1.0f / tg.sg_inv[0], cys = 1.0f / tg.sg_inv[1], czs = 1.0f / tg.sg_inv[2];
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     const int i0 = blockIdx.x * kCBlockQ + wid * (64 * kCQPT) + lane;
     float qx[kCQPT], qy[kCQPT], qz[kCQPT], bound[kCQPT], bd[kCQPT];
@@ -1802,18 +1803,19 @@ __global__ __launch_bounds__(kCBlock) void seed_grid_kernel(const float4* __rest
     for (int k = 0; k < kCQPT; ++k) {
         const int i = i0 + 64 * k;
         const bool valid = i < nq;
-        qx[k] = lx + ((float)(i / (kSeedGrid * kSeedGrid)) + 0.5f) * cxs;
-        qy[k] = ly + ((float)((i / kSeedGrid) % kSeedGrid) + 0.5f) * cys;
-        qz[k] = lz + ((float)(i % kSeedGrid) + 0.5f) * czs;
+        qx[k] = tg.sg_lo[0] + ((float)(i / (kSeedGrid * kSeedGrid)) + 0.5f) * cxs;
+        qy[k] = tg.sg_lo[1] + ((float)((i / kSeedGrid) % kSeedGrid) + 0.5f) * cys;
+        qz[k] = tg.sg_lo[2] + ((float)(i % kSeedGrid) + 0.5f) * czs;
         float b = valid ? 3.0e38f : 0.0f;
         if (valid)
             for (int t = 0; t < ntiles; t += seed_stride)
                 b = fminf(b, seed_bound(d2f(qx[k], qy[k], qz[k], p4[t * kTile])));
         bound[k] = b;
     }
-    culled_search<false>(stage[wid], p4, tlo, thi, qbox, ntiles, slo, shi, nsuper, 1, 1, 0, qx, qy, qz, bound, bd, bj,
-                         lane < nsuper ? slo[lane] : make_float4(0.f, 0.f, 0.f, 0.f),
-                         lane < nsuper ? shi[lane] : make_float4(0.f, 0.f, 0.f, 0.f));
+    culled_search<false>(stage[wid], p4, tg.tlo, tg.thi, tg.qbox, ntiles, tg.slo, tg.shi, nsuper, 1, 1, 0, qx, qy, qz,
+                         bound, bd, bj, lane < nsuper ? tg.slo[lane] : make_float4(0.f, 0.f, 0.f, 0.f),
+                         lane < nsuper ? tg.shi[lane] : make_float4(0.f, 0.f, 0.f, 0.f));
+    int32_t* grid = const_cast<int32_t*>(tg.sgrid);
 #pragma unroll
     for (int k = 0; k < kCQPT; ++k) {
         const int i = i0 + 64 * k;
@@ -1821,23 +1823,27 @@ __global__ __launch_bounds__(kCBlock) void seed_grid_kernel(const float4* __rest
     }
 }
 
-hipError_t launch_seed_grid(CloudLayout& L, hipStream_t s) {
+// The grid's buffer and frame (host side; the build is launch_seed_grids).
+hipError_t prepare_seed_grid(CloudLayout& L) {
     constexpr int nq = kSeedGrid * kSeedGrid * kSeedGrid;
     hipError_t e = L.sgrid.ensure(nq);
     if (e != hipSuccess) return e;
-    float cs[3];
     for (int a = 0; a < 3; ++a) {
         // the grid in the fp32 frame, a hair larger than the box; a
         // degenerate axis gets a tiny cell (every query clamps into a cell)
         const double ext = std::max(L.hi[a] - L.lo[a], 1e-30);
         const double cell = ext * (1.0 + 1e-6) / kSeedGrid;
         L.sg_lo[a] = (float)(L.lo[a] - L.org[a] - 1e-7 * ext);
-        cs[a] = (float)cell;
         L.sg_inv[a] = (float)(1.0 / cell);
     }
-    seed_grid_kernel<<<(unsigned)((nq + kCBlockQ - 1) / kCBlockQ), kCBlock, 0, s>>>(
-        L.p4.p, L.tlo.p, L.thi.p, L.qbox.p, (int)L.ntiles, L.slo.p, L.shi.p, (int)L.nsuper,
-        seed_stride_for(L.ntiles, 512), L.sg_lo[0], L.sg_lo[1], L.sg_lo[2], cs[0], cs[1], cs[2], L.sgrid.p);
+    return hipSuccess;
+}
+
+// The grids of targets [first, first + count) (their descriptors uploaded).
+hipError_t launch_seed_grids(const TargetDesc* tdesc, int first, int count, hipStream_t s) {
+    constexpr int nq = kSeedGrid * kSeedGrid * kSeedGrid;
+    seed_grid_kernel<<<dim3((unsigned)((nq + kCBlockQ - 1) / kCBlockQ), (unsigned)count), kCBlock, 0, s>>>(tdesc,
+                                                                                                         first);
     return hipGetLastError();
 }
 

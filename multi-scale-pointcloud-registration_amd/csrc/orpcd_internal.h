@@ -358,7 +358,8 @@ hipError_t launch_gather_rows(const double* in, const int32_t* idx, int64_t offs
 #define ORPCD_SEED_GRID 48
 #endif
 constexpr int kSeedGrid = ORPCD_SEED_GRID;  // cells per axis
-hipError_t launch_seed_grid(CloudLayout& L, hipStream_t s);
+hipError_t prepare_seed_grid(CloudLayout& L);
+hipError_t launch_seed_grids(const TargetDesc* tdesc, int first, int count, hipStream_t s);
 hipError_t build_layout(const double* dev_in64, int64_t n, const double bbox_lo[3], double bbox_ext,
                         const double origin[3], CloudLayout& L, bool with_tiles, hipStream_t s);
 

@@ -92,7 +92,7 @@ int upload_target_k(orpcd_ctx* c, int k, const double* xyz, int64_t m, double ep
     double margin = 0.0;
     int rc = upload_layout(c, xyz, m, c->tgts[k], true, &margin);
     if (rc) return rc;
-    CTX_CHECK(c, launch_seed_grid(c->tgts[k], c->stream));
+    CTX_CHECK(c, prepare_seed_grid(c->tgts[k]));  // built by launch_seed_grids once the descriptor is up
     CTX_CHECK(c, c->tcovs[k].ensure((size_t)m * 6));
     CTX_CHECK(c, c->scratch64b.ensure((size_t)m * 6));
     if (eps >= 0.0) {
@@ -110,7 +110,10 @@ int upload_target_k(orpcd_ctx* c, int k, const double* xyz, int64_t m, double ep
 }
 
 int upload_target(orpcd_ctx* c, const double* xyz, int64_t m, double eps) {
-    return upload_target_k(c, 0, xyz, m, eps);
+    int rc = upload_target_k(c, 0, xyz, m, eps);
+    if (rc) return rc;
+    CTX_CHECK(c, launch_seed_grids(c->tdesc.p, 0, 1, c->stream));
+    return ORPCD_OK;
 }
 
 // every target of the batch with covariances for `eps` (they depend on it)
@@ -120,6 +123,7 @@ int targets_for_epsilon(orpcd_ctx* c, int ntgt, double eps) {
         std::vector<double> host = c->tgt_host[k];
         int rc = upload_target_k(c, k, host.data(), c->tgts[k].n, eps);
         if (rc) return rc;
+        CTX_CHECK(c, launch_seed_grids(c->tdesc.p, k, 1, c->stream));
     }
     return ORPCD_OK;
 }
@@ -594,6 +598,7 @@ int orpcd_set_targets(orpcd_ctx* c, const double* xyz, const int64_t* m, int32_t
         if (rc) return rc;
         off += m[k];
     }
+    CTX_CHECK(c, launch_seed_grids(c->tdesc.p, 0, ntargets, c->stream));  // every target's grid, one launch
     CTX_CHECK(c, hipStreamSynchronize(c->stream));
     c->ntgt = ntargets;
     return ORPCD_OK;
