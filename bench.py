@@ -42,6 +42,10 @@ sys.path.insert(0, os.path.join(REPO, "multi-scale-pointcloud-registration_amd")
 sys.path.insert(0, REPO)
 
 FP32_PEAK_TFLOPS = 157.3    # MI355X FP32 VALU (packed v_pk_* math), MI355X_MICROARCH.md
+# VALU issue roof: 1024 SIMDs (256 CUs x 4) x 2.4 GHz (MI355X_MICROARCH.md max clock), one wave64
+# VALU instruction per SIMD every 4 cycles (16 lanes; 157.3 TF = 1024 x 16 lanes x 2 (FMA) x 2 (packed)
+# x 2.4 GHz)
+VALU_ISSUE_PEAK_GINST = 1024 * 2.4 / 4  # G wave-instructions/s
 FLOP_PER_PAIR = 8           # 3 sub + 3 mul/fma(=5) per query-target distance
 
 
@@ -129,6 +133,7 @@ def main():
     kname = "nn_search_sched_kernel" if st["sched_launches"] * 2 > st["launches"] else "nn_search_kernel"
     # the instantiation that ran: <true> in exact mode (the default), <false> otherwise
     traffic, traffic_src = pmc_traffic("orpcd::" + kname, bool(getattr(opt, "_exact_nn", True)))
+    valu_insts = pmc_counter("orpcd::" + kname, bool(getattr(opt, "_exact_nn", True)), "SQ_INSTS_VALU")
     avg_ms = st["ms"] / max(st["launches"], 1)
     flops_per_launch = st["pairs"] / max(st["launches"], 1) * FLOP_PER_PAIR
     achieved = flops_per_launch / (avg_ms * 1e-3) / 1e12 if avg_ms > 0 else 0.0
@@ -193,6 +198,14 @@ def main():
             "roofline": {"bound": "valu_fp32", "achieved": round(achieved, 3), "peak": FP32_PEAK_TFLOPS,
                          "unit": "TFLOP/s", "frac": round(achieved / FP32_PEAK_TFLOPS, 4), "traffic": traffic,
                          "traffic_source": traffic_src,
+                         # the binding resource: VALU instructions issued per launch (committed SQ_INSTS_VALU,
+                         # same command) over the live launch time, against the VALU issue roof -- most
+                         # issued instructions are culling and bookkeeping, not pair FLOPs
+                         "valu_issue": None if not valu_insts or avg_ms <= 0 else {
+                             "insts_per_launch": round(valu_insts),
+                             "achieved_ginst_s": round(valu_insts / (avg_ms * 1e-3) / 1e9, 1),
+                             "peak_ginst_s": VALU_ISSUE_PEAK_GINST,
+                             "frac": round(valu_insts / (avg_ms * 1e-3) / 1e9 / VALU_ISSUE_PEAK_GINST, 3)},
                          "kernel": kname, "avg_launch_ms": round(avg_ms, 4),
                          "search_kernel_ms_total": round(st["ms"], 3),
                          "launches": int(st["launches"]), "flop_per_pair": FLOP_PER_PAIR,
@@ -282,6 +295,19 @@ def align_vs_fixture(T, metric, sf, errors, gpu_seconds):
                                  "r02_gpu_box_seconds": 252.6}}
     out["speedup_vs_cpu_measured"] = round(meta["seconds"] / gpu_seconds, 1)
     return out
+
+
+def pmc_counter(kernel, exact, counter):
+    """Per-launch value of an SQ counter for `kernel` from the newest committed
+    profiles/rNN_pmc.json (rocprofv3 --pmc on this same bench command)."""
+    import glob
+    files = sorted(glob.glob(os.path.join(REPO, "profiles", "r*_pmc.json")))
+    if not files:
+        return None
+    d = json.load(open(files[-1]))
+    inst = kernel + ("<true" if exact else "<false")
+    key = kernel if kernel in d else next((k for k in sorted(d) if k.startswith(inst)), None)
+    return None if key is None else d[key].get(counter)
 
 
 def pmc_traffic(kernel, exact=True):
