@@ -242,8 +242,15 @@ int orpcd_fgr_optimize(orpcd_ctx* ctx, const double* src, int64_t n, const doubl
  *                   previous pass's measured cost (ordered dispatch)
  *   "sched_items", "sched_min_starts"  its split granularity, and the batch
  *                   size from which it is used
- *   "seed_reps"     pass-0 search bound: nearest of ~this many tile
- *                   representatives per query
+ *   "seed_grid"     1 (default) / 0: every query's search bound is also
+ *                   seeded by the target nearest its cell of the target's
+ *                   48^3 seed grid (built at set_target / set_targets)
+ *   "seed_reps"     pass-0 search bound without the seed grid: nearest of
+ *                   ~this many tile representatives per query
+ *   "exact_blocks", "exact_fused"  the fp64 re-search's grid in exact mode:
+ *                   at most exact_blocks blocks, exact_fused per running
+ *                   start inside the accumulation launch (0: a launch of
+ *                   its own before the accumulation)
  *   "exact_nn"      1 (default): every correspondence is the fp64 nearest
  *                   target (the oracle's lexicographic (d^2, input index)
  *                   minimum, i.e. Open3D's KD-tree answer); 0: the fp32

@@ -742,7 +742,7 @@ __global__ __launch_bounds__(256) void xform_queries_kernel(const double* __rest
         bound = r2s;
         const int jp = prevnn[(size_t)slot * N + i];
         if (jp >= 0) bound = fminf(bound, seed_bound(d2f(x, y, z, p4[jp])));
-        if (tg.sgrid) {
+        if (tg.sgrid && tg.sg_on) {
             // the target nearest to the centre of the query's seed-grid cell
             // (clamped to the grid): early passes move the poses far, so the
             // previous correspondence alone is a loose bound (CPU study: a
@@ -1993,7 +1993,7 @@ TgtBounds target_bounds(const orpcd_ctx* c, const int32_t* act, int nact) {
     return tb;
 }
 
-void write_target_desc(const CloudLayout& L, const double* tcov, int seed_reps, TargetDesc& d) {
+void write_target_desc(const CloudLayout& L, const double* tcov, int seed_reps, bool seed_grid, TargetDesc& d) {
     d.p4 = L.p4.p;
     d.tlo = L.tlo.p;
     d.thi = L.thi.p;
@@ -2005,7 +2005,7 @@ void write_target_desc(const CloudLayout& L, const double* tcov, int seed_reps, 
     d.ntiles = (int)L.ntiles;
     d.nsuper = (int)L.nsuper;
     d.seed_stride = seed_stride_for(L.ntiles, seed_reps);
-    d.pad = 0;
+    d.sg_on = seed_grid ? 1 : 0;
     d.ox = L.org[0];
     d.oy = L.org[1];
     d.oz = L.org[2];

@@ -185,9 +185,9 @@ constexpr int kMaxTargets = 16;
 struct TargetDesc {
     const float4 *p4, *tlo, *thi, *qbox, *slo, *shi;  // fp32 search layout (CloudLayout)
     const double *xyz64, *tcov;                        // fp64 points and GICP covariances (Morton order)
-    int ntiles, nsuper, seed_stride, pad;
+    int ntiles, nsuper, seed_stride, sg_on;            // sg_on: queries seeded by the seed grid (opt.seed_grid)
     double ox, oy, oz;                                 // fp32 frame origin (CloudLayout::org)
-    const int32_t* sgrid;                              // seed grid (CloudLayout::sgrid) or null
+    const int32_t* sgrid;                              // seed grid (CloudLayout::sgrid; built with the target)
     float sg_lo[3], sg_inv[3];
 };
 
@@ -319,7 +319,8 @@ struct orpcd_ctx {
         int sync_every = 8;       // passes between host checks of the done flags (C2 sweep: 4 17.6 ms, 8-16 17.3)
         int super_cull = 1;       // first culling level over 64-tile super-tiles
         int reseed = 0;           // representative seeding also after pass 0
-        int seed_reps = 64;       // pass-0 seed: nearest of ~this many tile representatives per query
+        int seed_reps = 64;       // pass-0 seed without a seed grid: nearest of ~this many tile representatives
+        int seed_grid = 1;        // 1: every query also seeded by its seed-grid cell's target (CloudLayout::sgrid)
                                   // (C2 sweep 8..512: equal within noise; 64 keeps the transform cheap)
         int sched = 1;            // 1: search waves dispatched heaviest first, heavy query groups split
                                   // further (costs measured in the previous pass); 0: uniform splits
@@ -388,7 +389,7 @@ int sched_capacity(const orpcd_ctx* c, int B);
 TgtBounds one_target();
 // bounds of the launch rows act[0..nact) (increasing slots) over the batch's targets
 TgtBounds target_bounds(const orpcd_ctx* c, const int32_t* act, int nact);
-void write_target_desc(const CloudLayout& L, const double* tcov, int seed_reps, TargetDesc& d);
+void write_target_desc(const CloudLayout& L, const double* tcov, int seed_reps, bool seed_grid, TargetDesc& d);
 hipError_t launch_gicp_pass(const orpcd_ctx* c, int nact, int pass, double r2, hipStream_t s, hipEvent_t mid,
                             const TgtBounds& tb);
 hipError_t launch_gicp_solve(const orpcd_ctx* c, int nact, int pass, const orpcd_gicp_params& p, hipStream_t s,

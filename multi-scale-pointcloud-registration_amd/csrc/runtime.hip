@@ -103,7 +103,7 @@ int upload_target_k(orpcd_ctx* c, int k, const double* xyz, int64_t m, double ep
     c->tgt_eps[k] = eps;
     c->tgt_host[k].assign(xyz, xyz + 3 * m);
     CTX_CHECK(c, c->tdesc.ensure(kMaxTargets));
-    write_target_desc(c->tgts[k], c->tcovs[k].p, c->opt.seed_reps, c->tdesc_h[k]);
+    write_target_desc(c->tgts[k], c->tcovs[k].p, c->opt.seed_reps, c->opt.seed_grid != 0, c->tdesc_h[k]);
     CTX_CHECK(c, hipMemcpyAsync(c->tdesc.p + k, &c->tdesc_h[k], sizeof(TargetDesc), hipMemcpyHostToDevice,
                                 c->stream));
     return ORPCD_OK;
@@ -1329,12 +1329,15 @@ int orpcd_set_option(orpcd_ctx* c, const char* key, double value) {
     else if (k == "super_cull" && (v == 0 || v == 1)) c->opt.super_cull = v;
     else if (k == "small_batch" && v >= 0) c->opt.small_batch = v;
     else if (k == "reseed" && (v == 0 || v == 1)) c->opt.reseed = v;
-    else if (k == "seed_reps" && v >= 1) {
-        c->opt.seed_reps = v;
-        // the seed stride lives in the targets' descriptors: rewrite them
+    else if ((k == "seed_reps" && v >= 1) || (k == "seed_grid" && (v == 0 || v == 1))) {
+        if (k == "seed_reps")
+            c->opt.seed_reps = v;
+        else
+            c->opt.seed_grid = v;
+        // both live in the targets' descriptors: rewrite them
         CTX_CHECK(c, hipSetDevice(c->device));
         for (int t = 0; t < c->ntgt; ++t) {
-            write_target_desc(c->tgts[t], c->tcovs[t].p, v, c->tdesc_h[t]);
+            write_target_desc(c->tgts[t], c->tcovs[t].p, c->opt.seed_reps, c->opt.seed_grid != 0, c->tdesc_h[t]);
             CTX_CHECK(c, hipMemcpyAsync(c->tdesc.p + t, &c->tdesc_h[t], sizeof(TargetDesc), hipMemcpyHostToDevice,
                                         c->stream));
         }
