@@ -1834,7 +1834,7 @@ hipError_t prepare_seed_grid(CloudLayout& L) {
         const double ext = std::max(L.hi[a] - L.lo[a], 1e-30);
         const double cell = ext * (1.0 + 1e-6) / kSeedGrid;
         L.sg_lo[a] = (float)(L.lo[a] - L.org[a] - 1e-7 * ext);
-        L.sg_inv[a] = (float)(1.0 / cell);
+        L.sg_inv[a] = (float)std::min(1.0 / cell, 1e30);  // finite: (x - lo) * inv never meets 0 * inf
     }
     return hipSuccess;
 }
