@@ -333,6 +333,8 @@ struct orpcd_ctx {
                                   // 0: the fp32 search's answer (ties within 2^-17 relative by position)
         int exact_blocks = 256;   // grid of the fp64 re-search (256-thread blocks, one listed query per wave
                                   // at a time)
+        int count_tiles = 1;      // profiling: the search also counts the quarters it scans (stats "tiles",
+                                  // "pairs"); 0: hipEvent timing only
         int exact_fused = 64;     // > 0: the re-search runs in the accumulation's launch (GICP), this many
                                   // blocks per running start (at most exact_blocks); 0: a launch of its own
     } opt;

@@ -759,8 +759,8 @@ int read_outputs(orpcd_ctx* c, int B, unsigned long long tiles_before, double* T
     CTX_CHECK(c, hipMemcpyAsync(nc.data(), c->out_ncorr.p, (size_t)B * 8, hipMemcpyDeviceToHost, s));
     CTX_CHECK(c, hipStreamSynchronize(s));
     unsigned long long tiles_after = 0;
-    if (c->profiling) CTX_CHECK(c, read_counters(c, tiles_after, unused, false));
-    if (c->profiling) {
+    if (c->count_tiles) CTX_CHECK(c, read_counters(c, tiles_after, unused, false));
+    if (c->count_tiles) {
         const double t = (double)(tiles_after - tiles_before);
         c->stats.tiles += t;
         c->stats.pairs += t * kQuarter * (64.0 * kCQPT);  // pairs evaluated by the scan (t in quarters)
@@ -793,12 +793,12 @@ int run_passes(orpcd_ctx* c, int B, const orpcd_gicp_params* p, double* T_out, d
     hipStream_t s = c->stream;
     const double r2 = p->max_correspondence_distance * p->max_correspondence_distance;
     unsigned long long tiles_before = 0, unused = 0;
-    if (c->profiling) CTX_CHECK(c, read_counters(c, tiles_before, unused, false));
+    if (c->profiling && c->opt.count_tiles) CTX_CHECK(c, read_counters(c, tiles_before, unused, false));
     int nact = B;
     static const bool trace = getenv("ORPCD_TRACE") != nullptr;
     const bool timed = c->profiling || trace;
     const int every = trace ? 1 : std::max(1, c->opt.sync_every);
-    c->count_tiles = timed;
+    c->count_tiles = timed && c->opt.count_tiles;
     if (timed) {
         while ((int)c->ev_pool.size() < 3 * every) {
             hipEvent_t e;
@@ -1052,7 +1052,7 @@ int orpcd_gicp_shard_pass(orpcd_ctx* c, double* sums_out, int32_t* active) {
     if (done) return ORPCD_OK;
     const double r2 = c->shard.p.max_correspondence_distance * c->shard.p.max_correspondence_distance;
     const bool timed = c->profiling;
-    c->count_tiles = timed;
+    c->count_tiles = timed && c->opt.count_tiles;
     unsigned long long tiles0 = 0, tiles1 = 0, unused = 0;
     if (timed) {
         while (c->ev_pool.size() < 3) {
@@ -1349,6 +1349,7 @@ int orpcd_set_option(orpcd_ctx* c, const char* key, double value) {
     else if (k == "exact_nn" && (v == 0 || v == 1)) c->opt.exact_nn = v;
     else if (k == "exact_blocks" && v >= 1 && v <= 65536) c->opt.exact_blocks = v;
     else if (k == "exact_fused" && v >= 0 && v <= 4096) c->opt.exact_fused = v;
+    else if (k == "count_tiles" && (v == 0 || v == 1)) c->opt.count_tiles = v;
     else {
         c->err = "set_option: unknown key or bad value: " + k;
         return ORPCD_EINVAL;

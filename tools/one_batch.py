@@ -44,6 +44,8 @@ def main():
     if st["exact_queries"] > 0:
         print(f"exact_nn: {st['exact_filed'] / reps:.0f} queries re-searched per batch of "
               f"{st['exact_queries'] / reps:.0f} ({100 * st['exact_filed'] / st['exact_queries']:.3f}%)")
+    if st.get("tiles", 0) > 0:  # {"profiling": 1}: quarters scanned by the search
+        print(f"quarters scanned per batch {st['tiles'] / reps:.4g}, search {st.get('ms', 0) / reps:.2f} ms")
     ctx.close()
 
 
