@@ -3,6 +3,7 @@
 // the hot path runs in the kernels of knn_kernels.hip / gicp_kernels.hip.
 #include <algorithm>
 #include <cmath>
+#include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -209,6 +210,24 @@ int features_device(orpcd_ctx* c, const double* host_xyz, int k, int64_t n, doub
 
 double norm3(const double* a) { return std::sqrt(a[0] * a[0] + a[1] * a[1] + a[2] * a[2]); }
 
+// ORPCD_FGR_TRACE=1: the FGR path's phases on stderr (each mark drains the
+// stream first, so the phases' own times, not their overlap)
+struct FgrTrace {
+    bool on = getenv("ORPCD_FGR_TRACE") != nullptr;
+    std::chrono::steady_clock::time_point t0 = std::chrono::steady_clock::now();
+    void mark(hipStream_t s, const char* what) {
+        if (!on) return;
+        (void)hipStreamSynchronize(s);
+        const auto t = std::chrono::steady_clock::now();
+        fprintf(stderr, "[orpcd fgr] %-28s %8.3f ms\n", what, std::chrono::duration<double, std::milli>(t - t0).count());
+        t0 = t;
+    }
+};
+thread_local FgrTrace* g_fgr_trace = nullptr;
+static void fgr_mark(hipStream_t s, const char* what) {
+    if (g_fgr_trace) g_fgr_trace->mark(s, what);
+}
+
 // O3D FastGlobalRegistration.cpp: NormalizePointCloud, AdvancedMatching,
 // OptimizePairwiseRegistration, GetInvTransformationOriginalScale and
 // EvaluateRegistration, with points and padded features already on device
@@ -246,6 +265,7 @@ int fgr_device(orpcd_ctx* c, const double* src, int64_t n, const double* tgt, in
     auto normalised = [&](int k, int64_t i, double out[3]) {
         for (int a = 0; a < 3; ++a) out[a] = (host[k][3 * i + a] - mean[k][a]) / scale;
     };
+    fgr_mark(s, "normalisation");
     // --- initial matching on the matrix cores, both directions
     int fi = 0, fj = 1;
     if (np[1] > np[0]) std::swap(fi, fj);
@@ -263,6 +283,7 @@ int fgr_device(orpcd_ctx* c, const double* src, int64_t n, const double* tgt, in
     CTX_CHECK(c, dedup_rows(F.feat[fj].p, F.fn2[fj].p, nPtj, F.dedup, &nu, s));
     CTX_CHECK(c, launch_feat_nn(F.feat[fi].p, F.fn2[fi].p, nPti, F.dedup.Fu.p, F.dedup.n2u.p, nu, F.dedup.uidx.p, 33,
                                 F.fnn, F.nn[1].p, s));
+    fgr_mark(s, "feature matching");
     std::vector<int32_t> j_to_i((size_t)nPtj), i_to_j((size_t)nPti);
     CTX_CHECK(c, hipMemcpyAsync(j_to_i.data(), F.nn[0].p, (size_t)nPtj * 4, hipMemcpyDeviceToHost, s));
     CTX_CHECK(c, hipMemcpyAsync(i_to_j.data(), F.nn[1].p, (size_t)nPti * 4, hipMemcpyDeviceToHost, s));
@@ -305,6 +326,7 @@ int fgr_device(orpcd_ctx* c, const double* src, int64_t n, const double* tgt, in
             if (cnt >= p.maximum_tuple_count) break;
         }
     }
+    fgr_mark(s, "cross check + tuple test");
     // pairs back to (source, target)
     const int K = (int)tup.size();
     std::vector<double> pq((size_t)std::max(K, 1) * 6);
@@ -323,6 +345,7 @@ int fgr_device(orpcd_ctx* c, const double* src, int64_t n, const double* tgt, in
     double Tn[16];
     CTX_CHECK(c, hipMemcpyAsync(Tn, F.Tn.p, sizeof(Tn), hipMemcpyDeviceToHost, s));
     CTX_CHECK(c, hipStreamSynchronize(s));
+    fgr_mark(s, "irls");
     // --- GetInvTransformationOriginalScale (4x4 algebra)
     double T[16] = {0};
     double inner[3];
@@ -357,6 +380,7 @@ int fgr_device(orpcd_ctx* c, const double* src, int64_t n, const double* tgt, in
         cnt += part[(size_t)2 * b];
         err2 += part[(size_t)2 * b + 1];
     }
+    fgr_mark(s, "evaluation");
     std::memcpy(T_out, T, sizeof(T));
     if (fitness_out) *fitness_out = cnt > 0 ? cnt / (double)n : 0.0;
     if (rmse_out) *rmse_out = cnt > 0 ? std::sqrt(err2 / cnt) : 0.0;
@@ -1301,14 +1325,21 @@ int orpcd_fgr_optimize(orpcd_ctx* c, const double* src, int64_t n, const double*
                 "(fastGlobalOptimizer.py:137-142 would index past the source's features)");
     CTX_REQUIRE(c, finite_cloud(src, n) && finite_cloud(tgt, m), "fgr_optimize: non-finite coordinates");
     CTX_CHECK(c, hipSetDevice(c->device));
+    FgrTrace tr;
+    g_fgr_trace = &tr;
+    struct Reset {
+        ~Reset() { g_fgr_trace = nullptr; }
+    } reset;
     const double* xyz[2] = {src, tgt};
     const int64_t np[2] = {n, m};
     for (int k = 0; k < 2; ++k) {
         CTX_CHECK(c, c->fgr.xyz[k].ensure((size_t)np[k] * 3));
         CTX_CHECK(c, hipMemcpyAsync(c->fgr.xyz[k].p, xyz[k], (size_t)np[k] * 24, hipMemcpyHostToDevice, c->stream));
     }
+    fgr_mark(c->stream, "upload");
     rc = fpfh_device(c, src, 0, n, normal_radius, normal_knn, fpfh_radius, fpfh_knn);
     if (rc) return rc;
+    fgr_mark(c->stream, "source normals + fpfh");
     CTX_CHECK(c, c->fgr.feat[1].ensure((size_t)m * kFeatDim));
     if (target_features_from_source) {
         CTX_CHECK(c, hipMemcpyAsync(c->fgr.feat[1].p, c->fgr.feat[0].p, (size_t)m * kFeatDim * 8,
@@ -1317,6 +1348,7 @@ int orpcd_fgr_optimize(orpcd_ctx* c, const double* src, int64_t n, const double*
         rc = fpfh_device(c, tgt, 1, m, normal_radius, normal_knn, fpfh_radius, fpfh_knn);
         if (rc) return rc;
     }
+    fgr_mark(c->stream, "target normals + fpfh");
     return fgr_device(c, src, n, tgt, m, *p, T_out, fitness_out, rmse_out, ncorr_out, n_mutual_out);
 }
 
