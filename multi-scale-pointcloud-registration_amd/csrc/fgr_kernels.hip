@@ -210,15 +210,18 @@ __device__ __forceinline__ void merge_lex(double& d, int& i, double od, int oi) 
 // EXACT: qidx / nsel / thr give the compacted flagged queries and their
 // pass-1 thresholds; out_s is unused.
 template <bool EXACT>
-__global__ __launch_bounds__(256) void feat_nn_kernel(const double* __restrict__ Fq, const double* __restrict__ nq2,
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void feat_nn_kernel(const double* __restrict__ Fq, const double* __restrict__ nq2,
                                                       int nq, const int32_t* __restrict__ qidx,
                                                       const int32_t* __restrict__ nsel,
                                                       const double* __restrict__ thr, const double* __restrict__ Ft,
                                                       const double* __restrict__ nt2, int nt, int part_len, int dim,
                                                       double* __restrict__ out_d, double* __restrict__ out_s,
                                                       int32_t* __restrict__ out_i) {
-    __shared__ double sT[kFT][kFD + 1];
-    __shared__ double sN[kFT];
+    // double-buffered stage: the next 64 targets are loaded into registers
+    // while the current ones are multiplied, then written to the other buffer
+    // (one barrier per stage)
+    __shared__ double sT2[2][kFT][kFD + 1];
+    __shared__ double sN2[2][kFT];
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     const int nrow = EXACT ? *nsel : nq;  // queries (rows of the compact list in EXACT mode)
     if ((int)blockIdx.x * 256 >= nrow) return;  // block-uniform
@@ -239,14 +242,35 @@ __global__ __launch_bounds__(256) void feat_nn_kernel(const double* __restrict__
     const double inf = __builtin_huge_val();
     double bd[4] = {inf, inf, inf, inf}, b2[4] = {inf, inf, inf, inf};
     int bi[4] = {-1, -1, -1, -1};
-    for (int t0 = t_begin; t0 < t_end; t0 += kFT) {
-        __syncthreads();
-        for (int e = threadIdx.x; e < kFT * kFD; e += 256) {
-            const int r = e / kFD, col = e - r * kFD;
-            sT[r][col] = (t0 + r < t_end) ? Ft[(size_t)(t0 + r) * kFD + col] : 0.0;
+    constexpr int kPer = kFT * kFD / 256;  // staged doubles per thread
+    static_assert(kFT * kFD % 256 == 0, "stage split");
+    double pre[kPer], preN = inf;
+    auto load_stage = [&](int t0) {
+#pragma unroll
+        for (int u = 0; u < kPer; ++u) {
+            const int e = threadIdx.x + 256 * u, r = e / kFD, col = e - r * kFD;
+            pre[u] = (t0 + r < t_end) ? Ft[(size_t)(t0 + r) * kFD + col] : 0.0;
         }
-        if (threadIdx.x < kFT) sN[threadIdx.x] = (t0 + threadIdx.x < t_end) ? nt2[t0 + threadIdx.x] : inf;
-        __syncthreads();
+        if (threadIdx.x < kFT) preN = (t0 + threadIdx.x < t_end) ? nt2[t0 + threadIdx.x] : inf;
+    };
+    auto store_stage = [&](int buf) {
+#pragma unroll
+        for (int u = 0; u < kPer; ++u) {
+            const int e = threadIdx.x + 256 * u, r = e / kFD, col = e - r * kFD;
+            sT2[buf][r][col] = pre[u];
+        }
+        if (threadIdx.x < kFT) sN2[buf][threadIdx.x] = preN;
+    };
+    if (t_begin < t_end) {
+        load_stage(t_begin);
+        store_stage(0);
+    }
+    __syncthreads();
+    for (int t0 = t_begin, buf = 0; t0 < t_end; t0 += kFT, buf ^= 1) {
+        const bool more = t0 + kFT < t_end;
+        if (more && !EXACT) load_stage(t0 + kFT);  // pass 2 holds too many registers to keep a stage in flight
+        double(*sT)[kFD + 1] = sT2[buf];
+        const double* sN = sN2[buf];
 #pragma unroll
         for (int sub = 0; sub < kFT / 16; ++sub) {
             d4 acc[4];
@@ -290,6 +314,21 @@ __global__ __launch_bounds__(256) void feat_nn_kernel(const double* __restrict__
                 }
             }
         }
+        // the other buffer was last read in the previous stage, before the
+        // barrier that ended it
+        if (more) {
+            if constexpr (EXACT) {  // straight into the other buffer
+                const int t1 = t0 + kFT;
+                for (int e = threadIdx.x; e < kFT * kFD; e += 256) {
+                    const int r = e / kFD, col = e - r * kFD;
+                    sT2[buf ^ 1][r][col] = (t1 + r < t_end) ? Ft[(size_t)(t1 + r) * kFD + col] : 0.0;
+                }
+                if (threadIdx.x < kFT) sN2[buf ^ 1][threadIdx.x] = (t1 + threadIdx.x < t_end) ? nt2[t1 + threadIdx.x] : inf;
+            } else {
+                store_stage(buf ^ 1);
+            }
+        }
+        __syncthreads();
     }
     // merge the 4 lane groups (l>>4) holding the same query column
 #pragma unroll
