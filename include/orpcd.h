@@ -251,6 +251,10 @@ int orpcd_fgr_optimize(orpcd_ctx* ctx, const double* src, int64_t n, const doubl
  *                   at most exact_blocks blocks, exact_fused per running
  *                   start inside the accumulation launch (0: a launch of
  *                   its own before the accumulation)
+ *   "count_tiles"   1 (default) / 0: while profiling (orpcd_profiling), the
+ *                   search also counts the quarters it scans (stats [2], [5]);
+ *                   0 keeps only the hipEvent timing (the counters' atomics
+ *                   cost 7-14% of a multistart)
  *   "exact_nn"      1 (default): every correspondence is the fp64 nearest
  *                   target (the oracle's lexicographic (d^2, input index)
  *                   minimum, i.e. Open3D's KD-tree answer); 0: the fp32
