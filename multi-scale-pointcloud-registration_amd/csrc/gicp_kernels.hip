@@ -155,14 +155,16 @@ __device__ __forceinline__ float ldg_f32(const float* p) {
 constexpr float kU = 5.9604645e-08f;  // 2^-24
 __device__ __forceinline__ float exact_band_hi(float x, float A) {
 #pragma clang fp contract(off)  // identical rounding in the query transform and the search
-    const float d = __builtin_sqrtf(x * 1.0000080f);  // x (1 + 2^-17 + margin): the masked key's upper end
+    // v_sqrt_f32 (1 ulp), not the correctly rounded expansion (~20 VALU): the
+    // final 2^-19 margin covers this function's rounding (~7 ulp with it)
+    const float d = __builtin_amdgcn_sqrtf(x * 1.0000080f);  // x (1 + 2^-17 + margin): the masked key's upper end
     const float dl = kU * (4.04f * A + 7.07f * d);      // 2 delta (+1%)
     const float r = d + dl;
     return r * r * 1.0000020f;  // (1 + 2^-19): this function's own fp32 rounding
 }
 __device__ __forceinline__ float qnorm(float x, float y, float z) {
 #pragma clang fp contract(off)
-    return __builtin_sqrtf(x * x + y * y + z * z) * 1.0000005f;
+    return __builtin_amdgcn_sqrtf(x * x + y * y + z * z) * 1.0000005f;  // 1-ulp sqrt inside the 8-ulp margin
 }
 // sentinel bound of a query in exact mode: strictly above band_hi of every
 // key below the plain bound, so a runner-up can never be the sentinel
@@ -274,6 +276,9 @@ __device__ __forceinline__ int culled_search(float4* stage, const float4* __rest
     // (S = 1: one super-tile, one tile per lane).  Lanes follow increasing
     // tile order, so candidates are visited in the same order as before.
     const int per = S == 1 ? kSuper : (kSuper - s + S - 1) / S;
+    // k / per for k < 64 as (k * perM) >> 16, exact for per <= 64: scalar
+    // integer ops per candidate instead of the VALU division expansion
+    const unsigned perM = __builtin_amdgcn_readfirstlane((65536u + (unsigned)per - 1u) / (unsigned)per);
     const int P = kSuper / per;
     bool haven = false;  // a prefetched round exists
     // the prefetched round's super-tile base and surviving mask before it was
@@ -282,7 +287,7 @@ __device__ __forceinline__ int culled_search(float4* stage, const float4* __rest
     int nsb = 0;
     unsigned long long nmask = 0;
     auto lane_tile = [&](int base, unsigned long long m) -> int {
-        const int lr = lane / per, lm = lane - lr * per;  // lane -> (super-tile of the round, tile of it)
+        const int lr = (int)(((unsigned)lane * perM) >> 16), lm = lane - lr * per;  // lane -> (super-tile of the round, tile of it)
         int su = -1;
         for (int r = 0; r < P && m; ++r) {  // the next P surviving super-tiles (scalar)
             const int st = base + __builtin_ctzll(m);
@@ -375,7 +380,7 @@ __device__ __forceinline__ int culled_search(float4* stage, const float4* __rest
             }
 #endif
             if (__any(need0 || need1)) {  // lane k's tile, from the round's scalar state
-                const int r = k / per, m = k - r * per;
+                const int r = (int)(((unsigned)k * perM) >> 16), m = k - r * per;
                 unsigned long long cm = cmask;
                 for (int i = 0; i < r; ++i) cm &= cm - 1;
                 return (csb + __builtin_ctzll(cm)) * kSuper + (S == 1 ? m : s + S * m);
