@@ -22,9 +22,22 @@ def short(name):
     return name.split("(")[0].replace("void ", "").strip()
 
 
+def newest_run(paths):
+    """The files of the newest rocprofv3 run among `paths` (gpurun merges each
+    call's outputs into the same local directory, so older runs accumulate):
+    the run is the file name's process-id prefix."""
+    if not paths:
+        return []
+    runs = {}
+    for p in paths:
+        runs.setdefault(os.path.basename(p).split("_")[0], []).append(p)
+    last = max(runs, key=lambda r: max(os.path.getmtime(p) for p in runs[r]))
+    return runs[last]
+
+
 def counters(d):
     out = {}
-    for path in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
+    for path in newest_run(glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)):
         for r in csv.DictReader(open(path)):
             k = (short(r["Kernel_Name"]), r["Counter_Name"])
             n, s = out.get(k, (0, 0.0))
@@ -42,7 +55,7 @@ def main():
     a = ap.parse_args()
     prof = os.path.join(REPO, "profiles")
     os.makedirs(prof, exist_ok=True)
-    stats = glob.glob(os.path.join(a.kt, "**", "*kernel_stats.csv"), recursive=True)[0]
+    stats = newest_run(glob.glob(os.path.join(a.kt, "**", "*kernel_stats.csv"), recursive=True))[0]
     shutil.copy(stats, os.path.join(prof, f"{a.round}_kernel_stats.csv"))
     rows = list(csv.DictReader(open(stats)))
     hbm = {}
