@@ -499,9 +499,9 @@ __device__ __forceinline__ int culled_search(float4* stage, const float4* __rest
                     }
                     m0 = umin3(m0, a0, c0);
                     m1 = umin3(m1, a1, c1);
-                } else {  // (left to the compiler: the v_min3 asm measured 1% slower here)
-                    m0 = min(m0, min(a0, c0));
-                    m1 = min(m1, min(a1, c1));
+                } else {  // min(min(m, a), c): the compiler forms v_min3_u32 for this association (asm measured slower)
+                    m0 = min(min(m0, a0), c0);
+                    m1 = min(min(m1, a1), c1);
                 }
                 if constexpr (kPipe) __builtin_amdgcn_sched_barrier(0);
             }
