@@ -405,7 +405,7 @@ __device__ __forceinline__ int culled_search(float4* stage, const float4* __rest
     float4 pre = make_float4(0.f, 0.f, 0.f, 0.f), preq = pre;
     if (nxt >= 0) {
         pre = p4[nxt * kTile + lane];
-        if (lane < 8) preq = qbox[nxt * 8 + lane];
+        if (lane < 2 * kNQ) preq = qbox[nxt * 2 * kNQ + lane];
     }
     while (nxt >= 0) {
         const int tile = __builtin_amdgcn_readfirstlane(nxt);
@@ -416,12 +416,12 @@ __device__ __forceinline__ int culled_search(float4* stage, const float4* __rest
         sx[lane] = pre.x;
         sx[64 + lane] = pre.y;
         sx[128 + lane] = pre.z;
-        if (lane < 8) reinterpret_cast<float4*>(sx + 192)[lane] = preq;
+        if (lane < 2 * kNQ) reinterpret_cast<float4*>(sx + 192)[lane] = preq;
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         nxt = next_candidate(lbn);
         if (nxt >= 0) {
             pre = p4[nxt * kTile + lane];
-            if (lane < 8) preq = qbox[nxt * 8 + lane];
+            if (lane < 2 * kNQ) preq = qbox[nxt * 2 * kNQ + lane];
         }
 #if ORPCD_CULL_PRIO > 0
         __builtin_amdgcn_s_setprio(0);  // the scan yields issue slots to waves in their culling chain
@@ -437,7 +437,7 @@ __device__ __forceinline__ int culled_search(float4* stage, const float4* __rest
             // below that query's bound (including this tile's earlier
             // quarters); the 2^-20 slack keeps the test conservative against
             // the scan's own fp32 rounding
-            const float4 lo = qb[qd], hi = qb[4 + qd];
+            const float4 lo = qb[qd], hi = qb[kNQ + qd];
             const float b0 = kExact ? e0 : __uint_as_float((k0 < m0 ? k0 : m0) & kKeyMask);
             const float b1 = kExact ? e1 : __uint_as_float((k1 < m1 ? k1 : m1) & kKeyMask);
             const f2 qd2 = box_d2_2q(f2{qx[0], qx[1]}, f2{qy[0], qy[1]}, f2{qz[0], qz[1]}, lo.x, lo.y, lo.z, hi.x,
@@ -546,7 +546,7 @@ __device__ __forceinline__ int culled_search(float4* stage, const float4* __rest
             nxt = next_candidate(lbn);
             if (nxt >= 0) {
                 pre = p4[nxt * kTile + lane];
-                if (lane < 8) preq = qbox[nxt * 8 + lane];
+                if (lane < 2 * kNQ) preq = qbox[nxt * 2 * kNQ + lane];
             }
         }
     }

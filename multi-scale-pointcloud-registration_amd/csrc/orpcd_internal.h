@@ -14,7 +14,12 @@ namespace orpcd {
 // ------------------------------------------------------------- geometry
 constexpr int kTile = 64;                      // targets per culling tile (one wave-wide load)
 constexpr int kSuper = 64;                     // tiles per super-tile (first culling level)
-constexpr int kQuarter = 16;                   // targets per tile quarter (per-query test inside a staged tile)
+#ifndef ORPCD_QUARTER
+#define ORPCD_QUARTER 16
+#endif
+constexpr int kQuarter = ORPCD_QUARTER;        // targets per tile quarter (per-query test inside a staged tile)
+constexpr int kNQ = kTile / kQuarter;          // quarters per tile (their boxes: qbox[2 kNQ t + k] lo, [.. + kNQ + k] hi)
+static_assert(kNQ * kQuarter == kTile && 2 * kNQ <= 16, "quarter boxes fit the stage after x|y|z (64 floats)");
 constexpr int kCQPT = 2;                       // queries per lane in the culled search
 constexpr int kCWaves = 4;                     // waves per block
 constexpr int kCBlock = 64 * kCWaves;          // threads per block

@@ -56,14 +56,14 @@ __global__ void gather_points_kernel(const double* __restrict__ in64, const int3
 }
 
 // One thread per 64-point tile: fp32 AABB over the tile's real points, and
-// the AABBs of its four 16-point quarters (qbox[8t + k] = lo of quarter k,
-// qbox[8t + 4 + k] = hi; a quarter without real points gets an empty box).
+// the AABBs of its kNQ kQuarter-point quarters (qbox[2 kNQ t + k] = lo of quarter k,
+// qbox[2 kNQ t + kNQ + k] = hi; a quarter without real points gets an empty box).
 __global__ void tile_aabb_kernel(const float4* __restrict__ p4, int n, int ntiles, float4* __restrict__ lo,
                                  float4* __restrict__ hi, float4* __restrict__ qbox) {
     const int t = blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= ntiles) return;
     float mnx = 3.0e38f, mny = 3.0e38f, mnz = 3.0e38f, mxx = -3.0e38f, mxy = -3.0e38f, mxz = -3.0e38f;
-    for (int q = 0; q < 4; ++q) {
+    for (int q = 0; q < kNQ; ++q) {
         float ax = 3.0e38f, ay = 3.0e38f, az = 3.0e38f, bx = -3.0e38f, by = -3.0e38f, bz = -3.0e38f;
         const int beg = t * kTile + q * kQuarter, end = min(n, beg + kQuarter);
         for (int k = beg; k < end; ++k) {
@@ -75,8 +75,8 @@ __global__ void tile_aabb_kernel(const float4* __restrict__ p4, int n, int ntile
             by = fmaxf(by, p.y);
             bz = fmaxf(bz, p.z);
         }
-        qbox[8 * (size_t)t + q] = make_float4(ax, ay, az, 0.f);
-        qbox[8 * (size_t)t + 4 + q] = make_float4(bx, by, bz, 0.f);
+        qbox[2 * kNQ * (size_t)t + q] = make_float4(ax, ay, az, 0.f);
+        qbox[2 * kNQ * (size_t)t + kNQ + q] = make_float4(bx, by, bz, 0.f);
         mnx = fminf(mnx, ax);
         mny = fminf(mny, ay);
         mnz = fminf(mnz, az);
@@ -139,7 +139,7 @@ hipError_t build_layout(const double* dev_in64, int64_t n, const double bbox_lo[
         if ((e = L.p4.ensure((size_t)L.npad)) != hipSuccess) return e;
         if ((e = L.tlo.ensure((size_t)L.ntiles)) != hipSuccess) return e;
         if ((e = L.thi.ensure((size_t)L.ntiles)) != hipSuccess) return e;
-        if ((e = L.qbox.ensure((size_t)L.ntiles * 8)) != hipSuccess) return e;
+        if ((e = L.qbox.ensure((size_t)L.ntiles * 2 * kNQ)) != hipSuccess) return e;
         L.nsuper = (L.ntiles + kSuper - 1) / kSuper;
         if ((e = L.slo.ensure((size_t)L.nsuper)) != hipSuccess) return e;
         if ((e = L.shi.ensure((size_t)L.nsuper)) != hipSuccess) return e;
