@@ -58,6 +58,10 @@ def parse():
     ap.add_argument("--attempts", type=int, default=30, help="multistart starts per GPU")
     ap.add_argument("--cpu-seconds", type=float, default=20.0, help="CPU baseline sample budget (0 = skip)")
     ap.add_argument("--align", type=int, default=1, help="also time one full align() on rank 0 (N=1)")
+    ap.add_argument("--c4", type=int, default=1,
+                    help="also time C4 at every N: align() with --c4-attempts starts per multistart, sharded over "
+                         "the N ranks (strong scaling: the same total work at every N)")
+    ap.add_argument("--c4-attempts", type=int, default=64)
     return ap.parse_args()
 
 
@@ -194,6 +198,8 @@ def main():
                            speculative_extra_multistarts=len(al.speculative_history))
             align_s.update(align_vs_fixture(T, metric, sf, errors, align_s["seconds"]))
 
+    c4 = c4_run(opt, src_raw, tgt_raw, args, barrier, dist) if args.c4 else None
+
     if rank == 0:
         line = {
             "metric": "GICP iters/sec (Aligner multistart, 50k<->50k)",
@@ -242,7 +248,18 @@ def main():
             "fast_mode": fast,
             "gicp_iterations": int(iters),
             "align": align_s,
+            "c4": c4,
         }
+        fixture_iters = align_s.pop("_fixture_iterations", 0) if align_s is not None else 0
+        if align_s is not None and cpu is not None and cpu.get("seconds_per_iteration"):
+            # the CPU align() on THIS host: the oracle's measured seconds per GICP iteration (the step-0
+            # sample above, per-call set-up included) times the complete align()'s iterations (fixture)
+            est = cpu["seconds_per_iteration"] * fixture_iters
+            if est > 0:
+                align_s["cpu_seconds_same_host_extrapolated"] = round(est, 1)
+                align_s["speedup_vs_cpu_same_host"] = round(est / align_s["seconds"], 1)
+        if cpu is not None:
+            cpu["seconds_per_iteration"] = round(cpu["seconds_per_iteration"], 6)
         print(json.dumps(line))
     if dist is not None:
         dist.destroy_process_group()
@@ -309,10 +326,65 @@ def align_vs_fixture(T, metric, sf, errors, gpu_seconds):
         "d_rmse": abs(float(metric) - float(z["metric"])), "max_abs_dT": float(np.abs(np.asarray(T) - z["T"]).max()),
         "compass_errors_max_abs_diff": float(np.abs(e - z["errors"]).max()) if len(e) == len(z["errors"]) else None,
         "oracle_rmse": float(z["metric"]), "fixture": "tests/golden/g7_align_c2.npz"},
-        "cpu_seconds_measured": {"value": meta["seconds"], "cores": meta["cores"],
-                                 "where": "the complete oracle align() run that made the fixture (builder container)",
-                                 "r02_gpu_box_seconds": 252.6}}
-    out["speedup_vs_cpu_measured"] = round(meta["seconds"] / gpu_seconds, 1)
+        "_fixture_iterations": int(z["call_iters"].sum())}
+    return out
+
+
+def c4_run(opt, src_raw, tgt_raw, args, barrier, dist):
+    """C4 (BASELINE.json configs[3], the north_star's strong-scaling case): one
+    complete Aligner.align() (Aligner.py:228-317, refine off) on the C2 pair
+    with --c4-attempts (64) starts per multistart, the starts of every device
+    batch sharded over the N ranks (one all-gather per batch).  The total work
+    is the same at every N, so T1 / TN is the strong-scaling speedup.  One
+    cold run (device buffers grown), then the timed run; the wall-clock is the
+    max over ranks between barriers.  The result is checked against the
+    committed complete-oracle C4 align() (tests/golden/g7_align_c4.npz)
+    when present."""
+    from orpcd_amd import Aligner, Preprocessor
+
+    world = dist.get_world_size() if dist is not None else 1
+    out = None
+    for timed in (False, True):
+        np.random.seed(0)
+        al = Aligner(Preprocessor([]), Preprocessor([]), opt, attempts=args.c4_attempts)
+        barrier()
+        t0 = time.perf_counter()
+        T, metric, sf, errors = al.align(src_raw, tgt_raw, refine_registration=False)
+        barrier()
+        el = time.perf_counter() - t0
+        if timed:
+            mine = el
+            if dist is not None:
+                import torch
+                dev = "cuda" if dist.get_backend() == "nccl" else "cpu"
+                t = torch.tensor([el], dtype=torch.float64, device=dev)
+                dist.all_reduce(t, op=dist.ReduceOp.MAX)
+                el = float(t.item())
+            iters = int(sum(h["iters"] for h in al.history))
+            spec = int(sum(h["iters"] for h in al.speculative_history))
+            out = {"workload": f"C4: Aligner.align() on the C2 pair, {args.c4_attempts} starts per multistart, "
+                               f"starts sharded over {world} GPU(s) (strong scaling)",
+                   "seconds": round(el, 4), "seconds_rank0": round(mine, 4), "n_gpus": world,
+                   "attempts": args.c4_attempts, "multistarts": len(al.history),
+                   "gicp_iterations": iters, "gicp_iterations_per_s": round(iters / el, 1),
+                   "speculative_gicp_iterations": spec,
+                   "rmse": float(metric), "scale_factors": [float(x) for x in np.asarray(sf).ravel()]}
+            path = os.path.join(REPO, "tests", "golden", "g7_align_c4.npz")
+            if os.path.exists(path):
+                z = np.load(path)
+                e = np.asarray(errors, dtype=np.float64)
+                rmse = np.concatenate([h["rmse"] for h in al.history])
+                its = np.concatenate([h["iters_per_start"] for h in al.history])
+                same = len(rmse) == len(z["call_rmse"])
+                out["parity_vs_oracle"] = {
+                    "fixture": "tests/golden/g7_align_c4.npz",
+                    "scale_factors_identical": bool(np.array_equal(np.asarray(sf).reshape(1, 3), z["sf"])),
+                    "d_rmse": abs(float(metric) - float(z["metric"])),
+                    "max_abs_dT": float(np.abs(np.asarray(T) - z["T"]).max()),
+                    "compass_errors_identical_count": bool(len(e) == len(z["errors"])),
+                    "starts": int(len(rmse)), "starts_oracle": int(len(z["call_rmse"])),
+                    "iterations_identical": int((its == z["call_iters"]).sum()) if same else None,
+                    "max_abs_d_rmse_per_start": float(np.abs(rmse - z["call_rmse"]).max()) if same else None}
     return out
 
 
@@ -371,7 +443,7 @@ def cpu_baseline(source, target, args):
             break
     el = time.perf_counter() - t0
     return {"oracle_rmse": oracle_rmse, "oracle_iters": oracle_iters, "value": round(iters / el, 3),
-            "unit": "GICP iterations/s",
+            "unit": "GICP iterations/s", "seconds_per_iteration": el / max(iters, 1),
             "cores": O.num_threads(),
             "cpu_model": cpu_model(),
             "kind": "port",

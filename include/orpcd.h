@@ -121,6 +121,35 @@ int orpcd_gicp_batch_targets(orpcd_ctx* ctx, const double* R0, const double* t0,
                              int32_t B, const orpcd_gicp_params* params, double* T_out, double* rmse_out,
                              double* fitness_out, int32_t* iters_out, int64_t* ncorr_out);
 
+/* ------------------------------------ source KNN-20 boundary ties (per pose)
+ * Open3D recomputes the source's KNN-20 covariances on every posed copy
+ * source_initialized = source @ R0 + t0 (Aligner.py:183-185; the PointCloud
+ * rebuilt in generalizedICP.py:54-70).  The batch rotates the unposed cloud's
+ * covariances, equal up to rounding except at points whose 20th and 21st
+ * neighbours are within the posing rounding of each other ("ties"):
+ * orpcd_set_source / orpcd_set_source_rows list them with every candidate
+ * neighbour, and each batch re-decides them per start from the posed
+ * coordinates numpy forms, np.dot(source, R0) + t0 (fma(a2, b2, fma(a1, b1,
+ * a0 * b0)) + t per coordinate).
+ * orpcd_source_ties: *n_ties listed points, *n_rows the input indices of
+ *   every point involved (ties and candidates, increasing; rows_out, nullable,
+ *   n_rows capacity), *complete 0 when more ties existed than were listed.
+ * orpcd_set_posed_tie_rows: the posed coordinates of those rows for each of
+ *   the next batch's B starts (B x n_rows x 3, caller order; a start whose
+ *   block begins with NaN uses numpy's product); consumed by that batch, which
+ *   must have B starts.  B <= 0 clears.  The drop-in path passes the rows of
+ *   the cloud it was actually given.
+ * orpcd_tie_sets: every tie's 20 neighbours (input indices, (d^2, index)
+ *   order; n_ties x 20): from posed_rows (n_rows x 3) when not NULL, else
+ *   those start b of the last batch used.                                   */
+int orpcd_source_ties(orpcd_ctx* ctx, int64_t* n_ties, int64_t* n_rows, int32_t* complete, int64_t* rows_out);
+int orpcd_set_posed_tie_rows(orpcd_ctx* ctx, int32_t B, const double* xyz);
+int orpcd_tie_sets(orpcd_ctx* ctx, int32_t b, const double* posed_rows, int32_t* sets_out);
+/* The posing the batch applies: out[i] = xyz[idx[i]] @ R + t (R row-major,
+ * idx NULL = rows 0..n-1) as numpy's np.dot + broadcast add forms it.  Host
+ * code only.                                                                */
+int orpcd_pose_rows(const double* xyz, const int64_t* idx, int64_t n, const double* R, const double* t, double* out);
+
 /* --------------------------------------- PointToPoint ICP refinement (§8f)
  * Aligner.refine_registration (Aligner.py:319-364, icp_type="PointToPoint")
  * -> o3d registration_icp(source, target, distance_threshold, init,

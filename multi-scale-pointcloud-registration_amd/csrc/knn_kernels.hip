@@ -318,7 +318,7 @@ __global__ __launch_bounds__(256) void knn_wave_kernel(
     const float4* __restrict__ thi, int ntiles, const float4* __restrict__ slo, const float4* __restrict__ shi,
     int nsuper, const double* __restrict__ in64, double r2, float margin, double ox, double oy, double oz, int K,
     int out_input_order, double* __restrict__ rawcov6, int32_t* __restrict__ nbr_idx, double* __restrict__ nbr_d2,
-    int32_t* __restrict__ nbr_cnt, double* __restrict__ mean_dist) {
+    int32_t* __restrict__ nbr_cnt, double* __restrict__ mean_dist, int KC, KnnTieOut ties) {
 #pragma clang fp contract(off)
     const int lane = threadIdx.x & 63;
     const int q = blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -398,11 +398,40 @@ __global__ __launch_bounds__(256) void knn_wave_kernel(
             }
         }
     }
-    // outputs (kept pairs beyond the count are (INF, max) and written as -1 / 0)
-    const int c = __popcll(__ballot(lane < K && Ld < INF));
+    // outputs: the first KC (<= K) kept pairs (beyond the count they are
+    // (INF, max) and written as -1 / 0)
+    const int c = __popcll(__ballot(lane < KC && Ld < INF));
     const int o = out_input_order ? perm[q] : q;
-    if (nbr_idx && lane < K) nbr_idx[(size_t)o * K + lane] = lane < c ? Li : -1;
-    if (nbr_d2 && lane < K) nbr_d2[(size_t)o * K + lane] = lane < c ? Ld : 0.0;
+    if (ties.cnt && KC < K) {
+        // boundary tie: the (KC+1)-th neighbour within the band of the KC-th, so
+        // a rigidly posed copy's rounding may swap them (a point the caller
+        // re-decides per pose from the listed K nearest, runtime.hip SourceTies)
+        const long long bk = __double_as_longlong(Ld);
+        auto lane_d = [&](int l) {  // lane l's kept distance (both halves zero-extended)
+            const unsigned hi = __builtin_amdgcn_readlane((unsigned)(bk >> 32), l);
+            const unsigned lo = __builtin_amdgcn_readlane((unsigned)bk, l);
+            return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
+        };
+        const double dk = lane_d(KC), dk1 = lane_d(KC - 1);
+        if (dk < INF && dk - dk1 <= ties.rel * dk + ties.abs_coef * sqrt(dk)) {
+            int e = 0;
+            if (lane == 0) e = atomicAdd(ties.cnt, 1);
+            e = __builtin_amdgcn_readfirstlane(e);
+            if (e < ties.cap) {
+                int32_t* row = ties.rows + (size_t)e * (K + 2);
+                if (lane == 0) {
+                    row[0] = q;
+                    row[1] = perm[q];
+                }
+                if (lane < K) {
+                    row[2 + lane] = Ld < INF ? Li : -1;
+                    ties.d2[(size_t)e * K + lane] = Ld;
+                }
+            }
+        }
+    }
+    if (nbr_idx && lane < KC) nbr_idx[(size_t)o * KC + lane] = lane < c ? Li : -1;
+    if (nbr_d2 && lane < KC) nbr_d2[(size_t)o * KC + lane] = lane < c ? Ld : 0.0;
     if (nbr_cnt && lane == 0) nbr_cnt[o] = c;
     if (mean_dist) {  // SOR: mean of sqrt(d^2) over the neighbours in list order (-1: empty search)
         const double sq = lane < c ? sqrt(Ld) : 0.0;
@@ -465,7 +494,7 @@ hipError_t launch_knn_tiles(const CloudLayout& L, const double* in64, int k, dou
         knn_wave_kernel<<<(unsigned)((L.n + 3) / 4), 256, 0, s>>>(
             L.xyz64.p, L.perm.p, (int)L.n, L.tlo.p, L.thi.p, (int)L.ntiles, L.slo.p, L.shi.p, (int)L.nsuper, in64, r2,
             (float)margin, L.org[0], L.org[1], L.org[2], k, out_input_order ? 1 : 0, rawcov6, nbr_idx, nbr_d2, nbr_cnt,
-            mean_dist);
+            mean_dist, k, KnnTieOut{});
         return hipGetLastError();
     }
     const dim3 grid((unsigned)((L.ntiles + 3) / 4));
@@ -485,6 +514,51 @@ hipError_t launch_knn_tiles(const CloudLayout& L, const double* in64, int k, dou
     else
         return hipErrorInvalidValue;
 #undef ORPCD_KNN_TILES
+    return hipGetLastError();
+}
+
+hipError_t launch_knn_cov_ties(const CloudLayout& L, const double* in64, int kcov, double margin, bool out_input_order,
+                               double* rawcov6, const KnnTieOut& ties, hipStream_t s) {
+    if (L.n <= 0) return hipSuccess;
+    const int K = kcov + kTieExtra;
+    if (kcov < 1 || K > 64) return hipErrorInvalidValue;
+    knn_wave_kernel<<<(unsigned)((L.n + 3) / 4), 256, 0, s>>>(
+        L.xyz64.p, L.perm.p, (int)L.n, L.tlo.p, L.thi.p, (int)L.ntiles, L.slo.p, L.shi.p, (int)L.nsuper, in64,
+        __builtin_huge_val(), (float)margin, L.org[0], L.org[1], L.org[2], K, out_input_order ? 1 : 0, rawcov6, nullptr,
+        nullptr, nullptr, nullptr, kcov, ties);
+    return hipGetLastError();
+}
+
+// Overrides of single (slot, point) source covariances: the raw neighbourhood
+// covariance of a boundary-tie point as its posed copy decides it (host,
+// runtime.hip SourceTies), already in the posed frame (no rotation).
+__global__ __launch_bounds__(64) void cov_override_kernel(const double* __restrict__ ent, int count, int n,
+                                                          double eps, double* __restrict__ cov6) {
+    const int e = blockIdx.x * 64 + threadIdx.x;
+    if (e >= count) return;
+    const double* r = ent + (size_t)e * 8;  // slot, Morton position, raw covariance (6)
+    const int64_t slot = (int64_t)r[0], pos = (int64_t)r[1];
+    Sym3 S{r[2], r[3], r[4], r[5], r[6], r[7]};
+    double nrm[3];
+    fast_eigen3x3(S, nrm);
+    if (nrm[0] * nrm[0] + nrm[1] * nrm[1] + nrm[2] * nrm[2] == 0.0) {
+        nrm[0] = 0.0;
+        nrm[1] = 0.0;
+        nrm[2] = 1.0;
+    }
+    Sym3 C = gicp_cov_from_normal(nrm, eps);
+    double* o = cov6 + ((size_t)slot * n + pos) * 6;
+    o[0] = C.xx;
+    o[1] = C.xy;
+    o[2] = C.xz;
+    o[3] = C.yy;
+    o[4] = C.yz;
+    o[5] = C.zz;
+}
+
+hipError_t launch_cov_override(const double* ent, int count, int64_t n, double eps, double* cov6, hipStream_t s) {
+    if (count <= 0) return hipSuccess;
+    cov_override_kernel<<<(unsigned)((count + 63) / 64), 64, 0, s>>>(ent, count, (int)n, eps, cov6);
     return hipGetLastError();
 }
 

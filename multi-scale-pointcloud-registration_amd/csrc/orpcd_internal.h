@@ -176,6 +176,20 @@ struct KernelStats {
     double exact_queries = 0;   // exact_nn: queries searched, every pass
 };
 
+// Boundary ties of a KNN covariance pass (launch_knn_cov_ties): points whose
+// (kcov+1)-th neighbour lies within rel * d2 + abs_coef * sqrt(d2) of the
+// kcov-th.  Entry e: rows[e * (K + 2)] = Morton position, [+1] = input index,
+// [+2 ..] the K = kcov + kTieExtra nearest input indices, d2[e * K ..] their
+// squared distances (ascending (d2, index)); cnt counts every tie (entries
+// past cap are dropped: the caller sees cnt > cap).
+struct KnnTieOut {
+    int* cnt = nullptr;
+    int32_t* rows = nullptr;
+    double* d2 = nullptr;
+    int cap = 0;
+    double rel = 0.0, abs_coef = 0.0;
+};
+
 // ------------------------------------------------- several targets per batch
 // A batch may hold starts against up to kMaxTargets targets (the six scale
 // candidates of one speculative compass iteration, Aligner.py:263-298, run
@@ -236,6 +250,49 @@ struct orpcd_ctx {
     orpcd::DevBuf<double> sraw;     // N*6 raw KNN-20 neighbourhood covariance
     bool src_cov = false;           // sraw holds the source's covariances (orpcd_set_source)
     int est = orpcd::kEstGICP;      // estimation of the running batch (GICP / PointToPoint)
+
+    // boundary ties of the source's KNN-20 neighbourhoods (SourceTies,
+    // runtime.hip): points whose 20th and 21st neighbours are so close that a
+    // posed copy's rounding decides which one enters the covariance.  Open3D
+    // (inside the reference) recomputes the covariances on every posed copy
+    // source @ R0 + t0 (Aligner.py:183-185, generalizedICP.py:54-70); the
+    // batch re-decides these points per start from the posed coordinates.
+    struct SourceTies {
+        bool on = false;           // a table for the current source (set_source / set_source_rows)
+        bool complete = true;      // every tie is in the table (false: the surplus keeps the rotated covariance)
+        int kcov = 20;
+        std::vector<double> xyz;   // the full source cloud, input order (posing)
+        std::vector<int32_t> pt;   // per tie: input index
+        std::vector<int32_t> pos;  // per tie: Morton position in the device source layout (-1: not on this rank)
+        std::vector<int32_t> off;  // per tie: its candidates cand[off[f] .. off[f+1]) (unposed (d2, index) order)
+        std::vector<int32_t> cand;
+        std::vector<int32_t> rows;      // sorted input indices of every tie point and candidate (the posed rows)
+        std::vector<int32_t> pt_row;    // per tie: its row in `rows`
+        std::vector<int32_t> cand_row;  // per candidate: its row in `rows`
+        std::vector<double> posed;      // caller-provided posed rows for the next batch (B x rows x 3, caller order)
+        int posed_B = 0;
+        std::vector<double> posed_slot;  // the same in slot order (batch_setup)
+        std::vector<int32_t> last_sets;  // the last batch: per slot, per tie, its kcov neighbours
+        void clear() {
+            on = false;
+            complete = true;
+            pt.clear();
+            pos.clear();
+            off.assign(1, 0);
+            cand.clear();
+            rows.clear();
+            pt_row.clear();
+            cand_row.clear();
+            posed.clear();
+            posed_B = 0;
+            posed_slot.clear();
+            last_sets.clear();
+        }
+    } ties;
+    orpcd::DevBuf<double> tie_ent;    // per batch: override entries {slot, position, raw covariance (6)}
+    orpcd::DevBuf<int32_t> tie_rows;  // knn tie table (KnnTieOut)
+    orpcd::DevBuf<double> tie_d2;
+    orpcd::DevBuf<int> tie_cnt;
 
     // batch state (per start slot)
     orpcd::DevBuf<double> scov;     // B*N*6 posed-frame source covariance
@@ -377,6 +434,14 @@ hipError_t launch_knn_tiles(const CloudLayout& L, const double* in64, int k, dou
                             int32_t* nbr_cnt, hipStream_t s, double* mean_dist = nullptr);
 hipError_t launch_normals_cov(const double* rawcov6, int64_t n, const double* Rc9, int nslots, double eps,
                               double* normals3, double* cov6, hipStream_t s);
+// KNN-kcov covariances (pure KNN, as launch_knn_tiles) whose search also keeps
+// kcov + kTieExtra neighbours and lists every boundary tie into `ties`
+// (SourceTies in runtime.hip); cov_override: entries {slot, Morton position,
+// raw covariance (6)} -> GICP covariance of that slot's point
+constexpr int kTieExtra = 4;
+hipError_t launch_knn_cov_ties(const CloudLayout& L, const double* in64, int kcov, double margin, bool out_input_order,
+                               double* rawcov6, const KnnTieOut& ties, hipStream_t s);
+hipError_t launch_cov_override(const double* ent, int count, int64_t n, double eps, double* cov6, hipStream_t s);
 
 // prep_kernels.hip
 hipError_t launch_sor_select(const double* avg, int64_t n, double std_ratio, double* stats, unsigned char* flag,

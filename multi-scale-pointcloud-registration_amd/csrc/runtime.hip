@@ -392,6 +392,216 @@ int fgr_device(orpcd_ctx* c, const double* src, int64_t n, const double* tgt, in
     return ORPCD_OK;
 }
 
+// ------------------------------------------------------------- SourceTies
+// Open3D recomputes the source's KNN-20 covariances on every posed copy
+// source_initialized = np.dot(source, R0) + t0 (Aligner.py:183-185; the
+// PointCloud rebuilt in generalizedICP.py:54-70); the batch rotates the
+// unposed cloud's covariances instead, which is the same up to rounding
+// EXCEPT where a point's 20th and 21st neighbours are so close that the posed
+// copy's rounding decides which one enters.  Those points are listed once per
+// source (source_ties_detect) with every candidate that could enter, and
+// re-decided per start from the posed coordinates numpy forms
+// (source_ties_apply): the oracle's distance expression, (d2, index) order,
+// ComputeCovariance's one-pass cumulants on the posed points.  Clouds without
+// such ties (C2) pay one 24- instead of 20-neighbour search at set_source.
+constexpr double kTieRel = 1e-8;     // tie band: relative part (posing rounding: ~1e-13 relative)
+constexpr double kTieAbs = 1e-12;    // ... and abs_coef = kTieAbs * (1 + max |coordinate|) times |d|
+constexpr int kTieCap = 4096;        // ties listed per cloud (the surplus keeps the rotated covariance)
+constexpr double kTieBruteBudget = 4e8;  // host pairs for ties whose candidates overflow the K-list
+
+// np.dot(p, R0) + t0 for one row as numpy computes it: OpenBLAS dgemm with
+// k = 3 accumulates fma(a2, b2, fma(a1, b1, a0 * b0)), then the broadcast add
+// (bit-identical to numpy: tests/test_host.py::test_posed_rows_match_numpy)
+void pose_row(const double* p, const double* R, const double* t, double* out) {
+#pragma clang fp contract(off)
+    for (int k = 0; k < 3; ++k) out[k] = std::fma(p[2], R[6 + k], std::fma(p[1], R[3 + k], p[0] * R[k])) + t[k];
+}
+
+// the oracle's / Open3D's point distance (KDTree::pt_d2: s = 0; s += d * d)
+double tie_d2(const double* a, const double* b) {
+#pragma clang fp contract(off)
+    double s = 0.0;
+    for (int k = 0; k < 3; ++k) {
+        const double d = a[k] - b[k];
+        s += d * d;
+    }
+    return s;
+}
+
+int source_ties_detect(orpcd_ctx* c, const CloudLayout& L, const double* dev_in64, const double* host_xyz, int64_t n,
+                       double margin, bool input_order, double* rawcov6) {
+    auto& T = c->ties;
+    T.clear();
+    const int kcov = T.kcov, K = kcov + kTieExtra;
+    double A = 0.0;
+    for (int a = 0; a < 3; ++a) A = std::max(A, std::max(std::fabs(L.lo[a]), std::fabs(L.hi[a])));
+    const double abs_coef = kTieAbs * (1.0 + A);
+    CTX_CHECK(c, c->tie_cnt.ensure(1));
+    CTX_CHECK(c, c->tie_rows.ensure((size_t)kTieCap * (K + 2)));
+    CTX_CHECK(c, c->tie_d2.ensure((size_t)kTieCap * K));
+    CTX_CHECK(c, hipMemsetAsync(c->tie_cnt.p, 0, 4, c->stream));
+    KnnTieOut to;
+    to.cnt = c->tie_cnt.p;
+    to.rows = c->tie_rows.p;
+    to.d2 = c->tie_d2.p;
+    to.cap = kTieCap;
+    to.rel = kTieRel;
+    to.abs_coef = abs_coef;
+    CTX_CHECK(c, launch_knn_cov_ties(L, dev_in64, kcov, margin, input_order, rawcov6, to, c->stream));
+    int cnt = 0;
+    CTX_CHECK(c, hipMemcpyAsync(&cnt, c->tie_cnt.p, 4, hipMemcpyDeviceToHost, c->stream));
+    CTX_CHECK(c, hipStreamSynchronize(c->stream));
+    T.on = true;
+    if (cnt == 0) return ORPCD_OK;
+    const int m = std::min(cnt, kTieCap);
+    T.complete = cnt <= kTieCap;
+    std::vector<int32_t> rows((size_t)m * (K + 2));
+    std::vector<double> d2((size_t)m * K);
+    CTX_CHECK(c, hipMemcpyAsync(rows.data(), c->tie_rows.p, rows.size() * 4, hipMemcpyDeviceToHost, c->stream));
+    CTX_CHECK(c, hipMemcpyAsync(d2.data(), c->tie_d2.p, d2.size() * 8, hipMemcpyDeviceToHost, c->stream));
+    CTX_CHECK(c, hipStreamSynchronize(c->stream));
+    T.xyz.assign(host_xyz, host_xyz + 3 * n);
+    // deterministic order (the atomic list order is not): by input index
+    std::vector<int> order((size_t)m);
+    for (int e = 0; e < m; ++e) order[e] = e;
+    std::sort(order.begin(), order.end(), [&](int a, int b) { return rows[(size_t)a * (K + 2) + 1] < rows[(size_t)b * (K + 2) + 1]; });
+    double budget = kTieBruteBudget;
+    std::vector<std::pair<double, int32_t>> bf;
+    for (int e : order) {
+        const int32_t* r = &rows[(size_t)e * (K + 2)];
+        const double* d = &d2[(size_t)e * K];
+        const double dk = d[kcov];  // the (kcov+1)-th neighbour
+        const double thr = dk + kTieRel * dk + abs_coef * std::sqrt(dk);
+        const size_t start = T.cand.size();
+        if (r[2 + K - 1] >= 0 && d[K - 1] <= thr) {
+            // more candidates than the list holds: all of them, by brute force
+            if (budget < (double)n) {
+                T.complete = false;
+                continue;
+            }
+            budget -= (double)n;
+            bf.clear();
+            const double* q = &host_xyz[3 * (size_t)r[1]];
+            for (int64_t j = 0; j < n; ++j) {
+                const double dd = tie_d2(q, &host_xyz[3 * j]);
+                if (dd <= thr) bf.push_back({dd, (int32_t)j});
+            }
+            std::sort(bf.begin(), bf.end());
+            for (auto& x : bf) T.cand.push_back(x.second);
+        } else {
+            for (int s2 = 0; s2 < K; ++s2)
+                if (r[2 + s2] >= 0 && d[s2] <= thr) T.cand.push_back(r[2 + s2]);
+        }
+        if ((int)(T.cand.size() - start) <= kcov) {  // nothing to decide (cannot happen for a listed tie)
+            T.cand.resize(start);
+            continue;
+        }
+        T.pt.push_back(r[1]);
+        T.pos.push_back(input_order ? -1 : r[0]);
+        T.off.push_back((int32_t)T.cand.size());
+    }
+    T.rows.assign(T.pt.begin(), T.pt.end());
+    T.rows.insert(T.rows.end(), T.cand.begin(), T.cand.end());
+    std::sort(T.rows.begin(), T.rows.end());
+    T.rows.erase(std::unique(T.rows.begin(), T.rows.end()), T.rows.end());
+    auto row_of = [&](int32_t i) { return (int32_t)(std::lower_bound(T.rows.begin(), T.rows.end(), i) - T.rows.begin()); };
+    T.pt_row.resize(T.pt.size());
+    for (size_t f = 0; f < T.pt.size(); ++f) T.pt_row[f] = row_of(T.pt[f]);
+    T.cand_row.resize(T.cand.size());
+    for (size_t k = 0; k < T.cand.size(); ++k) T.cand_row[k] = row_of(T.cand[k]);
+    return ORPCD_OK;
+}
+
+// Tie f's kcov neighbours (input indices, (d2, index) order) among its
+// candidates at posed rows P (rows x 3), and ComputeCovariance of them on the
+// posed points (O3D utility/Eigen.cpp: one-pass cumulants, 1/n).
+void tie_decide(const orpcd_ctx::SourceTies& T, size_t f, const double* P, int32_t* set_out, double cov6[6]) {
+#pragma clang fp contract(off)
+    const double* q = &P[3 * (size_t)T.pt_row[f]];
+    std::pair<double, int32_t> cd[256];
+    std::vector<std::pair<double, int32_t>> big;
+    const int nc = T.off[f + 1] - T.off[f];
+    std::pair<double, int32_t>* v = cd;
+    if (nc > 256) {
+        big.resize((size_t)nc);
+        v = big.data();
+    }
+    for (int k = 0; k < nc; ++k) {
+        const int32_t ck = T.off[f] + k;
+        v[k] = {tie_d2(q, &P[3 * (size_t)T.cand_row[ck]]), T.cand[ck]};
+    }
+    const int kc = T.kcov;
+    std::partial_sort(v, v + kc, v + nc);
+    double cu[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+    for (int s = 0; s < kc; ++s) {
+        set_out[s] = v[s].second;
+        const int32_t row = (int32_t)(std::lower_bound(T.rows.begin(), T.rows.end(), v[s].second) - T.rows.begin());
+        const double* p = &P[3 * (size_t)row];
+        cu[0] += p[0];
+        cu[1] += p[1];
+        cu[2] += p[2];
+        cu[3] += p[0] * p[0];
+        cu[4] += p[0] * p[1];
+        cu[5] += p[0] * p[2];
+        cu[6] += p[1] * p[1];
+        cu[7] += p[1] * p[2];
+        cu[8] += p[2] * p[2];
+    }
+    for (double& x : cu) x /= (double)kc;
+    cov6[0] = cu[3] - cu[0] * cu[0];
+    cov6[1] = cu[4] - cu[0] * cu[1];
+    cov6[2] = cu[5] - cu[0] * cu[2];
+    cov6[3] = cu[6] - cu[1] * cu[1];
+    cov6[4] = cu[7] - cu[1] * cu[2];
+    cov6[5] = cu[8] - cu[2] * cu[2];
+}
+
+// posed rows of start b: the caller's (orpcd_set_posed_tie_rows), or numpy's
+// np.dot(source, R0) + t0 of the source's own rows
+void tie_posed_rows(const orpcd_ctx::SourceTies& T, int b, const double* R0, const double* t0, double* P) {
+    const size_t nr = T.rows.size();
+    if (!T.posed_slot.empty() && std::isfinite(T.posed_slot[(size_t)b * nr * 3])) {
+        std::memcpy(P, &T.posed_slot[(size_t)b * nr * 3], nr * 3 * sizeof(double));
+        return;
+    }
+    for (size_t r = 0; r < nr; ++r) pose_row(&T.xyz[3 * (size_t)T.rows[r]], R0 + 9 * b, t0 + 3 * b, &P[3 * r]);
+}
+
+// Slot-ordered starts (R0 row-major: source @ R0 + t0): every tie's
+// covariance re-decided per start, written over the rotated one in c->scov.
+int source_ties_apply(orpcd_ctx* c, const double* R0, const double* t0, int B, double eps) {
+    auto& T = c->ties;
+    T.last_sets.clear();
+    if (!T.on || T.pt.empty()) {
+        T.posed_slot.clear();
+        return ORPCD_OK;
+    }
+    const size_t nt = T.pt.size(), nr = T.rows.size();
+    const int kc = T.kcov;
+    std::vector<double> P(nr * 3);
+    T.last_sets.assign((size_t)B * nt * kc, -1);
+    std::vector<double> ent;
+    ent.reserve((size_t)B * nt * 8);
+    for (int b = 0; b < B; ++b) {
+        tie_posed_rows(T, b, R0, t0, P.data());
+        for (size_t f = 0; f < nt; ++f) {
+            double cov[6];
+            tie_decide(T, f, P.data(), &T.last_sets[((size_t)b * nt + f) * kc], cov);
+            if (T.pos[f] < 0) continue;  // not on this rank's rows
+            ent.push_back((double)b);
+            ent.push_back((double)T.pos[f]);
+            for (double x : cov) ent.push_back(x);
+        }
+    }
+    T.posed_slot.clear();
+    const int count = (int)(ent.size() / 8);
+    if (count == 0) return ORPCD_OK;
+    CTX_CHECK(c, c->tie_ent.ensure(ent.size()));
+    CTX_CHECK(c, hipMemcpy(c->tie_ent.p, ent.data(), ent.size() * 8, hipMemcpyHostToDevice));
+    CTX_CHECK(c, launch_cov_override(c->tie_ent.p, count, c->src.n, eps, c->scov.p, c->stream));
+    return ORPCD_OK;
+}
+
 // Device state of a batch of B starts (pose = source @ R0_b + t0_b) before
 // pass 0: base poses, identity T, posed-frame source covariances, first
 // queries.  Host staging in c->h64 / c->h32 (layout used by gicp_batch).
@@ -498,7 +708,11 @@ int batch_setup(orpcd_ctx* c, const double* R0, const double* t0, int B, const o
     c->last_B = B;
     // posed-frame source covariances for every start (rigid equivariance)
     c->est = init16 ? kEstP2P : kEstGICP;
-    if (!init16) CTX_CHECK(c, launch_normals_cov(c->sraw.p, N, c->scratch64c.p, B, p->epsilon, nullptr, c->scov.p, s));
+    if (!init16) {
+        CTX_CHECK(c, launch_normals_cov(c->sraw.p, N, c->scratch64c.p, B, p->epsilon, nullptr, c->scov.p, s));
+        int rc = source_ties_apply(c, R0, t0, B, p->epsilon);  // boundary ties decided on the posed copies
+        if (rc) return rc;
+    }
     CTX_CHECK(c, launch_xform(c, B, 0, p->max_correspondence_distance * p->max_correspondence_distance, s,
                               target_bounds(c, hAct, B)));
     return ORPCD_OK;
@@ -640,8 +854,8 @@ int orpcd_set_source(orpcd_ctx* c, const double* xyz, int64_t n) {
     int rc = upload_layout(c, xyz, n, c->src, true, &margin);
     if (rc) return rc;
     CTX_CHECK(c, c->sraw.ensure((size_t)n * 6));
-    CTX_CHECK(c, launch_knn_tiles(c->src, c->scratch64a.p, 20, -1.0, margin, false, c->sraw.p, nullptr, nullptr,
-                                  nullptr, c->stream));
+    rc = source_ties_detect(c, c->src, c->scratch64a.p, xyz, n, margin, false, c->sraw.p);
+    if (rc) return rc;
     CTX_CHECK(c, hipStreamSynchronize(c->stream));
     c->src_cov = true;
     return ORPCD_OK;
@@ -684,6 +898,17 @@ int orpcd_gicp_batch_targets(orpcd_ctx* c, const double* R0, const double* t0, c
         for (int b = 0; b < B; ++b) pos[b] = b;
     }
     CTX_CHECK(c, hipSetDevice(c->device));
+    auto& TS = c->ties;
+    TS.posed_slot.clear();
+    if (TS.posed_B) {  // orpcd_set_posed_tie_rows: caller order -> slot order
+        const int pb = TS.posed_B;
+        TS.posed_B = 0;
+        CTX_REQUIRE(c, pb == B, "gicp_batch: posed tie rows were set for a different number of starts");
+        const size_t w = TS.rows.size() * 3;
+        TS.posed_slot.resize((size_t)B * w);
+        for (int b = 0; b < B; ++b) std::memcpy(&TS.posed_slot[(size_t)pos[b] * w], &TS.posed[(size_t)b * w], w * 8);
+        TS.posed.clear();
+    }
     int rc = targets_for_epsilon(c, ntg, p->epsilon);  // target covariances depend on epsilon
     if (rc) return rc;
     c->batch_ntgt = ntg;
@@ -717,6 +942,54 @@ int orpcd_gicp_batch_targets(orpcd_ctx* c, const double* R0, const double* t0, c
     return ORPCD_OK;
 }
 
+int orpcd_source_ties(orpcd_ctx* c, int64_t* n_ties, int64_t* n_rows, int32_t* complete, int64_t* rows_out) {
+    if (!c) return ORPCD_EINVAL;
+    CTX_REQUIRE(c, n_ties && n_rows, "source_ties: null argument");
+    const auto& T = c->ties;
+    *n_ties = (int64_t)T.pt.size();
+    *n_rows = (int64_t)T.rows.size();
+    if (complete) *complete = T.complete ? 1 : 0;
+    if (rows_out)
+        for (size_t r = 0; r < T.rows.size(); ++r) rows_out[r] = T.rows[r];
+    return ORPCD_OK;
+}
+
+int orpcd_pose_rows(const double* xyz, const int64_t* idx, int64_t n, const double* R, const double* t, double* out) {
+    if (!xyz || !R || !t || !out || n < 0) return ORPCD_EINVAL;
+    for (int64_t i = 0; i < n; ++i) pose_row(xyz + 3 * (idx ? idx[i] : i), R, t, out + 3 * i);
+    return ORPCD_OK;
+}
+
+int orpcd_set_posed_tie_rows(orpcd_ctx* c, int32_t B, const double* xyz) {
+    if (!c) return ORPCD_EINVAL;
+    auto& T = c->ties;
+    if (B <= 0 || !xyz) {  // clear
+        T.posed.clear();
+        T.posed_B = 0;
+        return ORPCD_OK;
+    }
+    T.posed.assign(xyz, xyz + (size_t)B * T.rows.size() * 3);
+    T.posed_B = B;
+    return ORPCD_OK;
+}
+
+int orpcd_tie_sets(orpcd_ctx* c, int32_t b, const double* posed_rows, int32_t* sets_out) {
+    if (!c) return ORPCD_EINVAL;
+    CTX_REQUIRE(c, sets_out, "tie_sets: null argument");
+    const auto& T = c->ties;
+    const size_t nt = T.pt.size(), kc = (size_t)T.kcov;
+    if (nt == 0) return ORPCD_OK;
+    if (posed_rows) {
+        double cov[6];
+        for (size_t f = 0; f < nt; ++f) tie_decide(T, f, posed_rows, sets_out + f * kc, cov);
+        return ORPCD_OK;
+    }
+    CTX_REQUIRE(c, b >= 0 && b < (int32_t)c->last_slot.size() && !T.last_sets.empty(),
+                "tie_sets: no such start in the last batch");
+    std::memcpy(sets_out, &T.last_sets[(size_t)c->last_slot[b] * nt * kc], nt * kc * 4);
+    return ORPCD_OK;
+}
+
 int orpcd_set_source_points(orpcd_ctx* c, const double* xyz, int64_t n) {
     if (!c) return ORPCD_EINVAL;
     CTX_REQUIRE(c, xyz && n > 0, "set_source_points: empty source cloud");
@@ -725,6 +998,7 @@ int orpcd_set_source_points(orpcd_ctx* c, const double* xyz, int64_t n) {
     CTX_CHECK(c, hipSetDevice(c->device));
     c->src_cov = false;
     c->last_B = 0;
+    c->ties.clear();
     int rc = upload_layout(c, xyz, n, c->src, true);
     if (rc) return rc;
     CTX_CHECK(c, hipStreamSynchronize(c->stream));
@@ -1028,14 +1302,24 @@ int orpcd_set_source_rows(orpcd_ctx* c, const double* xyz, int64_t n, int64_t ro
     int rc = upload_layout(c, xyz, n, c->aux, true, &margin);
     if (rc) return rc;
     CTX_CHECK(c, c->scratch64b.ensure((size_t)n * 6));
-    CTX_CHECK(c, launch_knn_tiles(c->aux, c->scratch64a.p, 20, -1.0, margin, true, c->scratch64b.p, nullptr, nullptr,
-                                  nullptr, c->stream));
+    rc = source_ties_detect(c, c->aux, c->scratch64a.p, xyz, n, margin, true, c->scratch64b.p);
+    if (rc) return rc;
     // the shard's rows in their own Morton layout, covariances gathered to it
     const int64_t ns = row_end - row_begin;
     rc = upload_layout(c, xyz + 3 * row_begin, ns, c->src, true);
     if (rc) return rc;
     CTX_CHECK(c, c->sraw.ensure((size_t)ns * 6));
     CTX_CHECK(c, launch_gather_rows(c->scratch64b.p, c->src.perm.p, row_begin, ns, 6, c->sraw.p, c->stream));
+    if (!c->ties.pt.empty()) {  // the ties on this rank's rows: their Morton positions
+        std::vector<int32_t> perm((size_t)ns), inv((size_t)ns);
+        CTX_CHECK(c, hipMemcpyAsync(perm.data(), c->src.perm.p, (size_t)ns * 4, hipMemcpyDeviceToHost, c->stream));
+        CTX_CHECK(c, hipStreamSynchronize(c->stream));
+        for (int64_t k = 0; k < ns; ++k) inv[(size_t)perm[k]] = (int32_t)k;
+        for (size_t f = 0; f < c->ties.pt.size(); ++f) {
+            const int64_t i = c->ties.pt[f];
+            c->ties.pos[f] = (i >= row_begin && i < row_end) ? inv[(size_t)(i - row_begin)] : -1;
+        }
+    }
     CTX_CHECK(c, hipStreamSynchronize(c->stream));
     c->src_cov = true;
     return ORPCD_OK;

@@ -84,8 +84,9 @@ class GeneralizedICP(IOptimizer):
         self._learned = None  # the caller's attempts per multistart, once seen (_count_call)
         self._calls_key, self._calls, self._calls_ok = None, 0, False
         self._ended = None  # how the last confirmed chain ended: "switch" (new cloud / target) or "miss"
-        self.spec_stats = dict(served=0, batches=0, missed=0, batch_s=0.0, serve_s=0.0)
+        self.spec_stats = dict(served=0, batches=0, missed=0, batch_s=0.0, serve_s=0.0, tie_reruns=0)
         self._base = None
+        self._tie_rows = None  # (base, rows of its KNN-20 boundary ties or None): _base_ties
         self._ctx = None
         self.last_result = None
 
@@ -130,6 +131,27 @@ class GeneralizedICP(IOptimizer):
             return None
         return R, t
 
+    def _base_ties(self, ctx):
+        """Rows of the base cloud's KNN-20 boundary ties (orpcd_source_ties;
+        None when it has none).  The device re-decides those points' neighbour
+        sets per start from posed coordinates; on this path a call's own
+        coordinates are the ones Open3D would use (the posed copy the caller
+        formed), so they are handed over (orpcd_set_posed_tie_rows)."""
+        if self._tie_rows is None or self._tie_rows[0] is not self._base:
+            t = ctx.source_ties()
+            self._tie_rows = (self._base, t["rows"] if t["n_ties"] else None)
+        return self._tie_rows[1]
+
+    def _run_alone(self, ctx, src, pose):
+        """One start on the cached base with pose (R, t), the call's own
+        posed coordinates deciding the boundary ties."""
+        rows = self._base_ties(ctx)
+        if rows is not None:
+            ctx.set_posed_tie_rows(src[rows][None])
+        r = ctx.gicp_batch(pose[0][None], pose[1][None], **self._params())
+        self.last_result = r
+        return r["T"][0], float(r["rmse"][0])
+
     def optimize(self, source: np.ndarray, target: np.ndarray, **kwargs) -> Tuple[np.ndarray, float]:
         ctx = self.context
         ctx.set_target(target, self._epsilon)
@@ -146,14 +168,12 @@ class GeneralizedICP(IOptimizer):
             else:
                 ctx.set_source(self._base)  # cached on the device (content key)
             if self._speculate:
-                row = self._speculate_next(ctx, pose, state)
+                row = self._speculate_next(ctx, pose, state, src)
         else:
             self._count_call(ctx._target_key)
         self._spec_prev = state
         if row is None:
-            r = ctx.gicp_batch(pose[0][None], pose[1][None], **self._params())
-            self.last_result = r
-            T, rmse = r["T"][0], float(r["rmse"][0])
+            T, rmse = self._run_alone(ctx, src, pose)
         else:
             T, rmse = row
         roto_translation = np.copy(T)
@@ -195,7 +215,7 @@ class GeneralizedICP(IOptimizer):
         if sp["base"] is not self._base or sp["tkey"] != tkey or not sp["rows"]:
             self._spec = None
             return None
-        R, t, T, rmse = sp["rows"].pop(0)
+        R, t, T, rmse, sets = sp["rows"].pop(0)
         res, mag = _native.rigid_residual(self._base, src, R, t) if src.shape == self._base.shape else (1.0, 0.0)
         if not res <= 1e-12 * (1.0 + mag):
             # not the predicted attempt (the caller re-seeded, or draws
@@ -208,6 +228,17 @@ class GeneralizedICP(IOptimizer):
                 self.spec_stats["missed"] += 1
             return None
         ch["n"] += 1
+        ctx = self.context
+        rows = self._base_ties(ctx)
+        if rows is not None:
+            ctx.set_source(self._base)  # the tie table is the device source's (cached: no upload)
+        if rows is not None and not np.array_equal(np.sort(sets, axis=1),
+                                                   np.sort(ctx.tie_sets(posed_rows=src[rows]), axis=1)):
+            # the predicted start decided a boundary tie from the base's posing,
+            # the caller's own posed copy decides it otherwise: this call alone
+            # (the order within a set only rounds the covariance's sums differently)
+            self.spec_stats["tie_reruns"] += 1
+            return self._run_alone(ctx, src, (R, t))
         self.spec_stats["served"] += 1
         return T, rmse
 
@@ -230,7 +261,7 @@ class GeneralizedICP(IOptimizer):
         self._calls += 1
         return self._calls
 
-    def _speculate_next(self, ctx, pose, state):
+    def _speculate_next(self, ctx, pose, state, src):
         """Extend or start the chain with this call; once confirmed, run this
         call's start plus the predicted next attempts as one batch and return
         this call's (T, rmse)."""
@@ -271,12 +302,18 @@ class GeneralizedICP(IOptimizer):
         Rs = [R] + [Rb.T @ Rk for Rk in Rn]
         ts = [t] + [tk - tb @ Rr for tk, Rr in zip(tn, Rs[1:])]
         t_0 = time.perf_counter()
+        rows = self._base_ties(ctx)
+        if rows is not None:  # this call's own posed rows; the predicted ones are posed from the base
+            posed = np.full((len(Rs), len(rows), 3), np.nan)
+            posed[0] = src[rows]
+            ctx.set_posed_tie_rows(posed)
         r = ctx.gicp_batch(np.array(Rs), np.array(ts), **self._params())
+        sets = [None if rows is None else ctx.tie_sets(k) for k in range(len(Rs))]
         self.spec_stats["batch_s"] += time.perf_counter() - t_0
         self.last_result = r
         self.spec_stats["batches"] += 1
         self._spec = dict(base=self._base, tkey=ctx._target_key,
-                          rows=[(Rs[k], ts[k], r["T"][k], float(r["rmse"][k])) for k in range(1, len(Rs))])
+                          rows=[(Rs[k], ts[k], r["T"][k], float(r["rmse"][k]), sets[k]) for k in range(1, len(Rs))])
         return r["T"][0], float(r["rmse"][0])
 
     def optimize_batch(self, source: np.ndarray, target: np.ndarray, R0: np.ndarray, t0: np.ndarray) -> dict:

@@ -61,7 +61,8 @@ EXPORTED = ("orpcd_abi_version", "orpcd_device_count", "orpcd_ctx_create", "orpc
             "orpcd_sor", "orpcd_voxel_down_sample", "orpcd_farthest_downsample",
             "orpcd_set_option", "orpcd_set_targets", "orpcd_gicp_batch_targets", "orpcd_test_solve6",
             "orpcd_gicp_correspondences",
-            "orpcd_profiling", "orpcd_stats", "orpcd_reset_stats", "orpcd_rng_draw_attempts", "orpcd_rigid_residual")
+            "orpcd_profiling", "orpcd_stats", "orpcd_reset_stats", "orpcd_rng_draw_attempts", "orpcd_rigid_residual",
+            "orpcd_source_ties", "orpcd_set_posed_tie_rows", "orpcd_tie_sets", "orpcd_pose_rows")
 
 
 class LegacyDraws:
@@ -149,6 +150,11 @@ def load_library():
         L.orpcd_rng_draw_attempts.argtypes = [np.ctypeslib.ndpointer(dtype=np.uint32, flags="C_CONTIGUOUS"),
                                               _i32p, _i32p, _f64p, c_i64, c_dbl, c_dbl, _f64p, _f64p]
         L.orpcd_rigid_residual.argtypes = [_f64p, _f64p, c_i64, _f64p, _f64p, _f64p]
+        L.orpcd_source_ties.argtypes = [vp, ctypes.POINTER(c_i64), ctypes.POINTER(c_i64), ctypes.POINTER(ctypes.c_int32),
+                                        vp]
+        L.orpcd_set_posed_tie_rows.argtypes = [vp, ctypes.c_int32, vp]
+        L.orpcd_tie_sets.argtypes = [vp, ctypes.c_int32, vp, _i32p]
+        L.orpcd_pose_rows.argtypes = [_f64p, vp, c_i64, _f64p, _f64p, _f64p]
         if L.orpcd_abi_version() != 1:
             raise NativeError("liborpcd_hip.so ABI mismatch")
         _lib = L
@@ -163,6 +169,20 @@ def rigid_residual(base: np.ndarray, src: np.ndarray, R: np.ndarray, t: np.ndarr
     if rc != ORPCD_OK:
         raise NativeError(f"orpcd_rigid_residual failed (status {rc})")
     return float(out[0]), float(out[1])
+
+
+def pose_rows(xyz: np.ndarray, R: np.ndarray, t: np.ndarray, idx=None) -> np.ndarray:
+    """xyz[idx] @ R + t as numpy's np.dot + add forms it (orpcd_pose_rows, host only)."""
+    xyz = np.ascontiguousarray(xyz, dtype=np.float64)
+    ix = None if idx is None else np.ascontiguousarray(idx, dtype=np.int64)
+    n = len(xyz) if ix is None else len(ix)
+    out = np.zeros((n, 3))
+    rc = load_library().orpcd_pose_rows(xyz, None if ix is None else ix.ctypes.data, n,
+                                        np.ascontiguousarray(R, dtype=np.float64),
+                                        np.ascontiguousarray(t, dtype=np.float64), out)
+    if rc != ORPCD_OK:
+        raise NativeError(f"orpcd_pose_rows failed (status {rc})")
+    return out
 
 
 def device_count() -> int:
@@ -285,6 +305,43 @@ class Context:
         self._source_key = None
         self._check(self._L.orpcd_set_source_points(self._h, xyz, len(xyz)), "orpcd_set_source_points")
         self._source_key = key
+
+    # ------------------------------------------------ source boundary ties
+    def source_ties(self) -> dict:
+        """The current source's KNN-20 boundary ties (orpcd_source_ties): the
+        number of listed points, the input indices of every row involved
+        (`rows`), and whether every tie was listed."""
+        nt, nr, comp = ctypes.c_int64(0), ctypes.c_int64(0), ctypes.c_int32(1)
+        self._check(self._L.orpcd_source_ties(self._h, ctypes.byref(nt), ctypes.byref(nr), ctypes.byref(comp), None),
+                    "orpcd_source_ties")
+        rows = np.zeros(nr.value, np.int64)
+        if nr.value:
+            self._check(self._L.orpcd_source_ties(self._h, ctypes.byref(nt), ctypes.byref(nr), ctypes.byref(comp),
+                                                  rows.ctypes.data), "orpcd_source_ties")
+        return dict(n_ties=int(nt.value), rows=rows, complete=bool(comp.value))
+
+    def set_posed_tie_rows(self, xyz):
+        """Posed coordinates of the tie rows for each start of the next batch
+        ((B, n_rows, 3); a start whose block is NaN uses numpy's product).
+        None clears."""
+        if xyz is None:
+            self._check(self._L.orpcd_set_posed_tie_rows(self._h, 0, None), "orpcd_set_posed_tie_rows")
+            return
+        xyz = np.ascontiguousarray(xyz, dtype=np.float64)
+        self._posed_keep = xyz
+        self._check(self._L.orpcd_set_posed_tie_rows(self._h, xyz.shape[0], xyz.ctypes.data), "orpcd_set_posed_tie_rows")
+
+    def tie_sets(self, b: int = -1, posed_rows=None, n_ties: Optional[int] = None) -> np.ndarray:
+        """(n_ties, 20) neighbour sets of the ties: from posed_rows ((n_rows, 3))
+        if given, else those start b of the last batch used."""
+        n = self.source_ties()["n_ties"] if n_ties is None else int(n_ties)
+        out = np.zeros((n, 20), np.int32)
+        if n == 0:
+            return out
+        pr = None if posed_rows is None else np.ascontiguousarray(posed_rows, dtype=np.float64)
+        self._check(self._L.orpcd_tie_sets(self._h, int(b), None if pr is None else pr.ctypes.data, out),
+                    "orpcd_tie_sets")
+        return out
 
     # --------------------------------------------------------------- GICP
     def gicp_batch(self, R0: np.ndarray, t0: np.ndarray, max_correspondence_distance=0.5, max_iteration=100,

@@ -11,7 +11,9 @@ C++/OpenMP restatement of Open3D 0.18, oracle/orpcd_oracle.cpp) on:
   refine off (BASELINE.json configs[0]);
 * C2: the same scans densified to 50k points each (workloads.c2_pair),
   Preprocessor([]) (RadiusScaler only), np.random.seed(0), 30 attempts, refine
-  off (configs[1]).
+  off (configs[1]);
+* C4: C2 with 64 attempts per multistart (configs[3]: the north_star's
+  64-start pattern search that bench.py --gpus N times at every N).
 
 Stored per config (g7_align_<cfg>.npz): the final T, metric, scale factors and
 compass errors, and for every optimize call in call order its (R0, t0), the
@@ -64,9 +66,10 @@ def run(cfg):
     else:
         src, tgt = c2_pair(50_000)
         pre = None
+    attempts = 64 if cfg == "c4" else 30
     opt = RecordingGICP(O)
     np.random.seed(0)
-    al = O.OracleAligner(opt, attempts=30, preprocess=pre)
+    al = O.OracleAligner(opt, attempts=attempts, preprocess=pre)
     t0 = time.perf_counter()
     T, metric, sf, errors = al.align(src, tgt)
     el = time.perf_counter() - t0
@@ -78,7 +81,8 @@ def run(cfg):
         call_T=np.array([r[0] for r in opt.rec]), call_rmse=np.array([r[1] for r in opt.rec]),
         call_fitness=np.array([r[2] for r in opt.rec]), call_iters=np.array([r[3] for r in opt.rec], np.int32))
     np.savez_compressed(os.path.join(HERE, f"g7_align_{cfg}.npz"), **out)
-    meta = {"config": cfg, "seconds": round(el, 1), "cores": O.num_threads(), "optimize_calls": len(calls),
+    meta = {"config": cfg, "attempts": attempts, "seconds": round(el, 1), "cores": O.num_threads(),
+            "optimize_calls": len(calls),
             "gicp_iterations": int(out["call_iters"].sum()), "metric": float(metric),
             "scale_factors": out["sf"].ravel().tolist()}
     with open(os.path.join(HERE, f"g7_align_{cfg}.json"), "w") as f:

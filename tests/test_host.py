@@ -309,6 +309,9 @@ def test_generalized_icp_drop_in_reuses_rigid_images():
         def set_source(self, xyz):
             self.sources.append(xyz)
 
+        def source_ties(self):
+            return dict(n_ties=0, rows=np.zeros(0, np.int64), complete=True)
+
         def gicp_batch(self, R0, t0, **kw):
             self.poses.append((R0[0].copy(), t0[0].copy()))
             return dict(T=np.eye(4)[None], rmse=np.array([0.5]))
@@ -367,6 +370,9 @@ def test_generalized_icp_drop_in_speculates_the_callers_draws():
         def set_source(self, xyz):
             self.base = xyz
 
+        def source_ties(self):
+            return dict(n_ties=0, rows=np.zeros(0, np.int64), complete=True)
+
         def gicp_batch(self, R0, t0, **kw):
             self.batches.append(len(R0))
             rm = np.array([0.1 + float(np.abs(self.base @ R + t).sum()) * 1e-6 for R, t in zip(R0, t0)])
@@ -417,3 +423,100 @@ def test_generalized_icp_drop_in_speculates_the_callers_draws():
         al.multistart_registration(src * (1.0 + 0.1 * k), tgt)
     assert fake.batches == [1, 1, 30, 30, 30], fake.batches  # the attempts learned from the first switch
     assert opt.spec_stats["missed"] == 0 and np.allclose(plug.rmse, plug.expect, rtol=0, atol=1e-12)
+
+
+def test_posed_rows_match_numpy():
+    """orpcd_pose_rows (the posing the batch applies to boundary-tie rows) is
+    numpy's np.dot(source, R0) + t0 bit for bit (Aligner.py:183-185): the
+    oracle fixtures' inputs were formed by numpy, so the tie decisions see the
+    same coordinates.  All 870 starts of the complete C1 align() fixture, on
+    the C1-like cloud and a cloud far from the origin; and row subsets."""
+    from orpcd_amd import _native
+    z = np.load(f"{GOLDEN}/g7_align_c1.npz")
+    rng = np.random.default_rng(11)
+    for cloud in (rng.standard_normal((3000, 3)) * 0.3, rng.standard_normal((500, 3)) * 50.0 + 1e3):
+        for R, t in zip(z["R0"], z["t0"]):
+            assert np.array_equal(_native.pose_rows(cloud, R, t), np.dot(cloud, R) + t)
+        idx = rng.integers(0, len(cloud), 37)
+        assert np.array_equal(_native.pose_rows(cloud, z["R0"][5], z["t0"][5], idx),
+                              (np.dot(cloud, z["R0"][5]) + z["t0"][5])[idx])
+
+
+def test_generalized_icp_drop_in_hands_over_posed_tie_rows():
+    """With KNN-20 boundary ties on the source (orpcd_source_ties), the
+    drop-in path hands the device each call's OWN posed coordinates of the tie
+    rows (the copy Open3D would re-estimate the covariances on,
+    generalizedICP.py:54-70); a predicted start (posed from the cached base)
+    is served only if its tie decisions equal the ones the call's own
+    coordinates give, else the call runs alone with its rows."""
+    from orpcd_amd import Aligner, GeneralizedICP, Preprocessor
+    from workloads import small_pair
+
+    rows = np.array([3, 17, 40, 41, 99])
+
+    def decide(P):  # a tie decision that flips on the last bits of the posed rows
+        return np.array([[int(np.ascontiguousarray(P).view(np.int64).sum() & 3)] * 20], np.int32)
+
+    class FakeCtx:
+        def __init__(self):
+            self.batches, self.given, self.last = [], [], []
+            self._target_key = None
+            self.posed = None
+
+        def set_option(self, key, value):
+            pass
+
+        def set_target(self, xyz, eps):
+            self._target_key = (xyz.shape, float(xyz.sum()))
+
+        def set_source(self, xyz):
+            self.base = xyz
+
+        def source_ties(self):
+            return dict(n_ties=1, rows=rows, complete=True)
+
+        def set_posed_tie_rows(self, xyz):
+            self.posed = None if xyz is None else np.array(xyz)
+
+        def gicp_batch(self, R0, t0, **kw):
+            B = len(R0)
+            P = self.posed if self.posed is not None else np.full((B, len(rows), 3), np.nan)
+            assert len(P) == B
+            self.posed = None
+            self.last = []
+            for b in range(B):
+                pb = P[b] if np.isfinite(P[b, 0, 0]) else np.dot(self.base[rows], R0[b]) + t0[b]
+                self.last.append(decide(pb))
+            self.given.append(P)
+            self.batches.append(B)
+            # rmse: the start's pose and its tie decision
+            rm = np.array([0.1 + float(np.abs(self.base @ R + t).sum()) * 1e-6 + 1e-3 * self.last[b][0, 0]
+                           for b, (R, t) in enumerate(zip(R0, t0))])
+            return dict(T=np.repeat(np.eye(4)[None], B, 0), rmse=rm)
+
+        def tie_sets(self, b=-1, posed_rows=None, n_ties=None):
+            return decide(posed_rows) if posed_rows is not None else self.last[b]
+
+    class OnlyOptimize:
+        def __init__(self, inner):
+            self.inner, self.rmse, self.expect = inner, [], []
+
+        def optimize(self, source, target, **kw):
+            T, m = self.inner.optimize(source, target, **kw)
+            self.rmse.append(m)
+            self.expect.append(0.1 + float(np.abs(source).sum()) * 1e-6 + 1e-3 * decide(source[rows])[0, 0])
+            return T, m
+
+    src, tgt = small_pair(400, seed=5)
+    opt = GeneralizedICP()
+    fake = opt._ctx = FakeCtx()
+    plug = OnlyOptimize(opt)
+    al = Aligner(Preprocessor([]), Preprocessor([]), plug, attempts=30)
+    np.random.seed(7)
+    al.multistart_registration(src, tgt)
+    st = opt.spec_stats
+    assert st["served"] + st["tie_reruns"] == 27 and st["tie_reruns"] > 0, st
+    # every call got its own coordinates' decision, served or re-run
+    assert np.allclose(plug.rmse, plug.expect, rtol=0, atol=1e-12)
+    # direct calls (and re-runs) handed over exactly their own rows
+    assert all(np.isfinite(g[0]).all() for g in fake.given)
