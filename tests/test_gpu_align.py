@@ -12,6 +12,8 @@ Gates:
   summation order differs).
   In the fp32-answer mode (exact_nn=False): scale factors identical, final
   RMSE within 1e-5 (north_star), T within 1e-4.
+* C4 (C2 with 64 starts per multistart, configs[3]; the one-GPU run of the
+  strong-scaling case bench.py times at every N): the same gates as C2.
 * C1 (Armadillo 330->0, Random(5000) + SOR, configs[0]): the same gates as
   C2.  The build computes the source's KNN-20 covariances once and rotates
   them per start, while the oracle (like Open3D in the reference) recomputes
@@ -93,3 +95,22 @@ def test_c1_align_matches_complete_oracle_align():
     assert np.array_equal(iters, z["call_iters"])
     assert np.abs(rmse - z["call_rmse"]).max() <= 1e-10
     assert abs(m - float(z["metric"])) <= 1e-12 and np.abs(T - z["T"]).max() <= 1e-9
+
+
+def test_c4_align_matches_complete_oracle_align():
+    from orpcd_amd import Aligner, GeneralizedICP, Preprocessor
+    from workloads import c2_pair
+    z = _fixture("c4")
+    src, tgt = c2_pair(50_000)
+    np.random.seed(0)
+    al = Aligner(Preprocessor([]), Preprocessor([]), GeneralizedICP(), attempts=64)
+    T, m, sf, errors = al.align(src, tgt, refine_registration=False)
+    assert np.array_equal(np.asarray(sf).reshape(1, 3), z["sf"]), (sf, z["sf"])
+    assert len(errors) == len(z["errors"]) and np.abs(np.asarray(errors) - z["errors"]).max() <= 1e-12
+    rmse, iters = _per_start(al.history)
+    assert len(rmse) == len(z["call_rmse"])
+    assert np.array_equal(iters, z["call_iters"])
+    assert np.abs(rmse - z["call_rmse"]).max() <= 1e-10
+    assert abs(m - float(z["metric"])) <= 1e-12 and np.abs(T - z["T"]).max() <= 1e-9
+    print(f"C4 align: {len(rmse)} starts, |d rmse| {abs(m - float(z['metric'])):.1e} "
+          f"|dT| {np.abs(T - z['T']).max():.1e}, worst per-start {np.abs(rmse - z['call_rmse']).max():.1e}")

@@ -65,16 +65,23 @@ def main():
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--attempts", type=int, default=30)
     ap.add_argument("--out", default=None)
+    ap.add_argument("--legs", default="caller_only,batched,dropin,dropin_nospec,dropin_cold,align",
+                    help="comma-separated subset of the legs to run")
     a = ap.parse_args()
+    legs = set(a.legs.split(","))
     from orpcd_amd import Aligner, GeneralizedICP, Preprocessor
     from workloads import c2_pair
     s, t = c2_pair(50_000)
     s, t = Preprocessor([]).preprocess(s), Preprocessor([]).preprocess(t)
 
+    from orpcd_amd import _native
+    ctx = _native.default_context(None)
+
     def leg(opt, name):
         al = Aligner(Preprocessor([]), Preprocessor([]), opt, attempts=a.attempts)
         np.random.seed(999)
         al.multistart_registration(s, t)  # warm-up
+        ctx.reset_stats()
         times, rmse, inside = [], [], []
         np.random.seed(1000)
         for k in range(a.reps):
@@ -91,16 +98,23 @@ def main():
         print(f"{name}: {np.median(times) * 1e3:.1f} ms per multistart"
               + (f" ({np.median(inside) * 1e3:.1f} ms inside optimize())" if inside else ""), file=sys.stderr, flush=True)
         leg.inside[name] = round(float(np.median(inside)) * 1e3, 2) if inside else None
+        st = ctx.stats()
+        nb = max(st["host_batches"], 1)
+        leg.host[name] = {k: round(st[k] / nb, 3) for k in ("host_batch_ms", "host_launch_ms", "host_sync_ms")}
+        leg.host[name]["batches"] = int(st["host_batches"])
+        print(f"  {name} per batch: {leg.host[name]}", file=sys.stderr, flush=True)
         return float(np.median(times)), rmse
 
     leg.inside = {}
+    leg.host = {}
 
-    tk, _ = leg(Constant(), "caller_only")
-    tb, rb = leg(GeneralizedICP(), "batched")
+    nan = (float("nan"), None)
+    tk, _ = leg(Constant(), "caller_only") if "caller_only" in legs else nan
+    tb, rb = leg(GeneralizedICP(), "batched") if "batched" in legs else nan
     spec = GeneralizedICP()
-    td, rd = leg(OnlyOptimize(spec), "dropin")
-    tn, rn = leg(OnlyOptimize(GeneralizedICP(speculate=0)), "dropin_nospec")
-    tc, rc = leg(OnlyOptimize(GeneralizedICP(rigid_cache=False)), "dropin_cold")
+    td, rd = leg(OnlyOptimize(spec), "dropin") if "dropin" in legs else nan
+    tn, rn = leg(OnlyOptimize(GeneralizedICP(speculate=0)), "dropin_nospec") if "dropin_nospec" in legs else nan
+    tc, rc = leg(OnlyOptimize(GeneralizedICP(rigid_cache=False)), "dropin_cold") if "dropin_cold" in legs else nan
     from workloads import c2_pair as pair
 
     def align_leg(opt, name):
@@ -114,16 +128,20 @@ def main():
         print(f"{name} align: {dt:.3f} s, rmse {m:.12g}", file=sys.stderr, flush=True)
         return dt, float(m)
 
-    ta_b, ma_b = align_leg(GeneralizedICP(), "batched")
     spec_al = GeneralizedICP()
-    ta_d, ma_d = align_leg(OnlyOptimize(spec_al), "dropin")
-    d_warm = max(float(np.abs(x - y).max()) for x, y in zip(rd, rb))
-    d_cold = max(float(np.abs(x - y).max()) for x, y in zip(rc, rb))
-    d_nospec = max(float(np.abs(x - y).max()) for x, y in zip(rn, rb))
+    if "align" in legs:
+        ta_b, ma_b = align_leg(GeneralizedICP(), "batched")
+        ta_d, ma_d = align_leg(OnlyOptimize(spec_al), "dropin")
+    else:
+        ta_b = ma_b = ta_d = ma_d = float("nan")
+
+    def dmax(r):
+        return max(float(np.abs(x - y).max()) for x, y in zip(r, rb)) if r is not None and rb is not None else None
+    d_warm, d_cold, d_nospec = dmax(rd), dmax(rc), dmax(rn)
     res = {"metric": "multistart wall-clock at C2 (30 starts), drop-in sequential vs batched", "unit": "ms",
            "batched_ms": round(tb * 1e3, 2), "dropin_ms": round(td * 1e3, 2), "dropin_cold_ms": round(tc * 1e3, 2),
            "dropin_nospec_ms": round(tn * 1e3, 2), "speculation": spec.spec_stats,
-           "caller_only_ms": round(tk * 1e3, 2), "inside_optimize_ms": leg.inside,
+           "caller_only_ms": round(tk * 1e3, 2), "inside_optimize_ms": leg.inside, "host_per_batch": leg.host,
            "dropin_over_batched": round(td / tb, 2), "dropin_cold_over_batched": round(tc / tb, 2),
            "max_abs_d_rmse_vs_batched": {"dropin": d_warm, "dropin_nospec": d_nospec, "dropin_cold": d_cold},
            "align": {"batched_s": round(ta_b, 4), "dropin_s": round(ta_d, 4),
