@@ -170,7 +170,7 @@ int orpcd_icp_p2p_batch(orpcd_ctx* ctx, const double* init, int32_t B, const orp
  * orpcd_sor: SOR.process (Preprocessor/Outliers/sor.py:51-79) -> o3d
  *   remove_statistical_outlier(nb_neighbors, std_ratio): kept input indices
  *   (increasing) in idx_out (n capacity), their count in *n_out; avg_out (n,
- *   nullable) the per-point mean KNN distance.  nb_neighbors <= 64.
+ *   nullable) the per-point mean KNN distance.  nb_neighbors <= 1024.
  * orpcd_voxel_down_sample: VoxelDownsampler (Downsamplers/voxelDownsampler.py:
  *   77-126) -> o3d voxel_down_sample(voxel_size): averaged points (n*3
  *   capacity, nullable = count only), voxels in lexicographic (ix, iy, iz)
@@ -339,7 +339,11 @@ int orpcd_rigid_residual(const double* base, const double* src, int64_t n, const
  * ran the ordered-dispatch search (nn_search_sched_kernel; the rest ran
  * nn_search_kernel), [8] = queries re-searched in fp64 (exact_nn), [9] =
  * queries searched while exact_nn was on.  [1] times the search kernel (and,
- * in exact mode, the fp64 re-search that follows it) only.                 */
+ * in exact mode, the fp64 re-search that follows it) only.
+ * Always counted (host wall-clock, whether profiling or not): [10] ms inside
+ * GICP batch calls (set-up to outputs), [11] ms of it in the pass launch
+ * calls, [12] ms of it waiting for the device (the every-sync_every-passes
+ * synchronisation), [13] GICP batches.                                      */
 int orpcd_profiling(orpcd_ctx* ctx, int32_t enable);
 int orpcd_stats(orpcd_ctx* ctx, double* stats_out, int32_t n);
 int orpcd_reset_stats(orpcd_ctx* ctx);

@@ -484,6 +484,211 @@ __global__ __launch_bounds__(256) void knn_wave_kernel(
     }
 }
 
+// ---------------------------------------------------------------------------
+// K > 64 (the reference accepts any positive neighbourhood size, e.g.
+// FastGlobalOptimizer(fpfh_knn=100), fastGlobalOptimizer.py:86-105): one wave
+// per query holds its K <= 64 P best (d^2, input index) SORTED over P chunks
+// of 64 (chunk j, lane s = the (64 j + s)-th nearest).  A candidate tile is
+// sorted across the lanes (bitonic), merged with the last chunk (its 64
+// smallest, as in knn_wave_kernel), and the result cascades forward through
+// the earlier chunks (each a sorted 64 + 64 merge: lane-wise min / max against
+// the reversed carry, two half-cleaner sorts).  Every element of the chunks
+// before the last ranks at most 64 (P - 1) + 64 among kept + new, so the K
+// nearest are always kept.  Same exact fp64 distances, tie order, culling and
+// outputs as knn_wave_kernel.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ void half_clean_sort(double& d, int& i, int lane) {  // bitonic 64 -> ascending
+#pragma unroll
+    for (int j = 32; j > 0; j >>= 1) xchg(d, i, j, (lane & j) == 0);
+}
+
+__device__ __forceinline__ double lane_dbl(double v, int l) {
+    const long long b = __double_as_longlong(v);
+    const unsigned lo = __builtin_amdgcn_readlane((unsigned)b, l);
+    const unsigned hi = __builtin_amdgcn_readlane((unsigned)(b >> 32), l);
+    return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
+}
+
+template <int P>
+__global__ __launch_bounds__(256) void knn_wave_multi_kernel(
+    const double* __restrict__ xyz64, const int32_t* __restrict__ perm, int n, const float4* __restrict__ tlo,
+    const float4* __restrict__ thi, int ntiles, const float4* __restrict__ slo, const float4* __restrict__ shi,
+    int nsuper, const double* __restrict__ in64, double r2, float margin, double ox, double oy, double oz, int K,
+    int out_input_order, double* __restrict__ rawcov6, int32_t* __restrict__ nbr_idx, double* __restrict__ nbr_d2,
+    int32_t* __restrict__ nbr_cnt, double* __restrict__ mean_dist) {
+#pragma clang fp contract(off)
+    const int lane = threadIdx.x & 63;
+    const int q = blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    if (q >= n) return;  // wave-uniform
+    const double qx = xyz64[3 * q], qy = xyz64[3 * q + 1], qz = xyz64[3 * q + 2];
+    const float fx = (float)(qx - ox), fy = (float)(qy - oy), fz = (float)(qz - oz);
+    const double INF = __builtin_huge_val();
+    double Ld[P];
+    int Li[P];
+#pragma unroll
+    for (int j = 0; j < P; ++j) {
+        Ld[j] = INF;
+        Li[j] = 0x7fffffff;
+    }
+    const int kc = (K - 1) >> 6, kl = (K - 1) & 63;  // the K-th kept pair: chunk kc, lane kl (uniform)
+    auto kth = [&](double& kd, int& ki) {
+#pragma unroll
+        for (int j = 0; j < P; ++j)
+            if (j == kc) {
+                kd = lane_dbl(Ld[j], kl);
+                ki = __builtin_amdgcn_readlane(Li[j], kl);
+            }
+    };
+    auto bound_f = [&]() -> float {
+        double kd;
+        int ki;
+        kth(kd, ki);
+        const double b = fmin(kd, r2);
+        return b >= 3.0e38 ? 3.0e38f : (float)b * 1.0000003f + 1e-37f;
+    };
+    const int own = q / kTile;
+    auto scan_tile = [&](int t) {
+        const int k = t * kTile + lane;
+        double d = INF;
+        int id = 0x7fffffff;
+        if (k < n) {
+            const double dx = qx - xyz64[3 * k], dy = qy - xyz64[3 * k + 1], dz = qz - xyz64[3 * k + 2];
+            const double dd = dx * dx + dy * dy + dz * dz;
+            if (dd < r2) {
+                d = dd;
+                id = perm[k];
+            }
+        }
+        double kd;
+        int ki;
+        kth(kd, ki);
+        if (!__any(pair_less(d, id, kd, ki))) return;
+        bitonic_sort64(d, id, lane);
+        // the 64 smallest of (last chunk, new), sorted: the carry
+        double cd = __shfl(d, 63 - lane, 64);
+        int ci = __shfl(id, 63 - lane, 64);
+        if (!pair_less(cd, ci, Ld[P - 1], Li[P - 1])) {
+            cd = Ld[P - 1];
+            ci = Li[P - 1];
+        }
+        half_clean_sort(cd, ci, lane);
+        // cascade: chunk j and the carry -> chunk j = their 64 smallest, carry = the rest
+#pragma unroll
+        for (int j = 0; j < P - 1; ++j) {
+            const double c0 = lane_dbl(cd, 0), lj = lane_dbl(Ld[j], 63);
+            const int c0i = __builtin_amdgcn_readlane(ci, 0), lji = __builtin_amdgcn_readlane(Li[j], 63);
+            if (!pair_less(c0, c0i, lj, lji)) continue;  // the carry lies wholly above chunk j (uniform)
+            const double rd = __shfl(cd, 63 - lane, 64);
+            const int ri = __shfl(ci, 63 - lane, 64);
+            const bool take = pair_less(rd, ri, Ld[j], Li[j]);
+            const double lo_d = take ? rd : Ld[j], hi_d = take ? Ld[j] : rd;
+            const int lo_i = take ? ri : Li[j], hi_i = take ? Li[j] : ri;
+            Ld[j] = lo_d;
+            Li[j] = lo_i;
+            cd = hi_d;
+            ci = hi_i;
+            half_clean_sort(Ld[j], Li[j], lane);
+            half_clean_sort(cd, ci, lane);
+        }
+        Ld[P - 1] = cd;
+        Li[P - 1] = ci;
+    };
+    constexpr int kWin = 2;
+    scan_tile(own);
+    for (int dt = 1; dt <= kWin; ++dt) {
+        if (own - dt >= 0) scan_tile(own - dt);
+        if (own + dt < ntiles) scan_tile(own + dt);
+    }
+    auto gap = [&](float4 a, float4 b) {
+        const float gx = fmaxf(0.0f, fmaxf(a.x - fx, fx - b.x) - margin);
+        const float gy = fmaxf(0.0f, fmaxf(a.y - fy, fy - b.y) - margin);
+        const float gz = fmaxf(0.0f, fmaxf(a.z - fz, fz - b.z) - margin);
+        return gx * gx + gy * gy + gz * gz;
+    };
+    for (int sb = 0; sb < nsuper; sb += 64) {
+        const int u = sb + lane;
+        const float sl = u < nsuper ? gap(slo[u], shi[u]) : 3.0e38f;
+        unsigned long long smask = __ballot(sl < bound_f());
+        while (smask) {
+            const int su = sb + __builtin_ctzll(smask);
+            smask &= smask - 1;
+            const int t = su * kSuper + lane;
+            const float lb = (t < ntiles && (t < own - kWin || t > own + kWin)) ? gap(tlo[t], thi[t]) : 3.0e38f;
+            unsigned long long tm = __ballot(lb < bound_f());
+            while (tm) {
+                const int k = __builtin_ctzll(tm);
+                tm &= tm - 1;
+                const float lbk = __uint_as_float(__builtin_amdgcn_readlane(__float_as_uint(lb), k));
+                if (!(lbk < bound_f())) continue;
+                scan_tile(su * kSuper + k);
+            }
+        }
+    }
+    // outputs: the first K kept pairs in list order
+    int c = 0;
+#pragma unroll
+    for (int j = 0; j < P; ++j) c += __popcll(__ballot(64 * j + lane < K && Ld[j] < INF));
+    const int o = out_input_order ? perm[q] : q;
+#pragma unroll
+    for (int j = 0; j < P; ++j) {
+        const int e = 64 * j + lane;
+        if (e < K) {
+            if (nbr_idx) nbr_idx[(size_t)o * K + e] = e < c ? Li[j] : -1;
+            if (nbr_d2) nbr_d2[(size_t)o * K + e] = e < c ? Ld[j] : 0.0;
+        }
+    }
+    if (nbr_cnt && lane == 0) nbr_cnt[o] = c;
+    if (mean_dist) {  // SOR: mean of sqrt(d^2) over the neighbours in list order (-1: empty search)
+        double sd = 0.0;
+#pragma unroll
+        for (int j = 0; j < P; ++j) {
+            const double sq = Ld[j] < INF ? sqrt(Ld[j]) : 0.0;
+            for (int s2 = 0; s2 < 64 && 64 * j + s2 < c; ++s2) sd += lane_dbl(sq, s2);
+        }
+        if (lane == 0) mean_dist[o] = c > 0 ? sd / (double)c : -1.0;
+    }
+    if (!rawcov6) return;
+    Sym3 C;
+    if (c >= 3) {  // O3D ComputeCovariance: one-pass cumulants in list order, 1/n
+        double cu[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll
+        for (int j = 0; j < P; ++j)
+            for (int s2 = 0; s2 < 64 && 64 * j + s2 < c; ++s2) {
+                const int jj = __builtin_amdgcn_readlane(Li[j], s2);
+                const double px = in64[3 * jj], py = in64[3 * jj + 1], pz = in64[3 * jj + 2];
+                cu[0] += px;
+                cu[1] += py;
+                cu[2] += pz;
+                cu[3] += px * px;
+                cu[4] += px * py;
+                cu[5] += px * pz;
+                cu[6] += py * py;
+                cu[7] += py * pz;
+                cu[8] += pz * pz;
+            }
+        const double cn = (double)c;
+#pragma unroll
+        for (int t = 0; t < 9; ++t) cu[t] /= cn;
+        C.xx = cu[3] - cu[0] * cu[0];
+        C.yy = cu[6] - cu[1] * cu[1];
+        C.zz = cu[8] - cu[2] * cu[2];
+        C.xy = cu[4] - cu[0] * cu[1];
+        C.xz = cu[5] - cu[0] * cu[2];
+        C.yz = cu[7] - cu[1] * cu[2];
+    } else {
+        C = Sym3{1.0, 0.0, 0.0, 1.0, 0.0, 1.0};
+    }
+    if (lane == 0) {
+        double* out = rawcov6 + (size_t)o * 6;
+        out[0] = C.xx;
+        out[1] = C.xy;
+        out[2] = C.xz;
+        out[3] = C.yy;
+        out[4] = C.yz;
+        out[5] = C.zz;
+    }
+}
+
 hipError_t launch_knn_tiles(const CloudLayout& L, const double* in64, int k, double radius, double margin,
                             bool out_input_order, double* rawcov6, int32_t* nbr_idx, double* nbr_d2,
                             int32_t* nbr_cnt, hipStream_t s, double* mean_dist) {
@@ -495,6 +700,25 @@ hipError_t launch_knn_tiles(const CloudLayout& L, const double* in64, int k, dou
             L.xyz64.p, L.perm.p, (int)L.n, L.tlo.p, L.thi.p, (int)L.ntiles, L.slo.p, L.shi.p, (int)L.nsuper, in64, r2,
             (float)margin, L.org[0], L.org[1], L.org[2], k, out_input_order ? 1 : 0, rawcov6, nbr_idx, nbr_d2, nbr_cnt,
             mean_dist, k, KnnTieOut{});
+        return hipGetLastError();
+    }
+    if (k > 64) {  // chunked sorted lists (knn_wave_multi_kernel), K <= kMaxKnn
+#define ORPCD_KNN_MULTI(PP)                                                                                       \
+    knn_wave_multi_kernel<PP><<<(unsigned)((L.n + 3) / 4), 256, 0, s>>>(                                          \
+        L.xyz64.p, L.perm.p, (int)L.n, L.tlo.p, L.thi.p, (int)L.ntiles, L.slo.p, L.shi.p, (int)L.nsuper, in64, r2, \
+        (float)margin, L.org[0], L.org[1], L.org[2], k, out_input_order ? 1 : 0, rawcov6, nbr_idx, nbr_d2, nbr_cnt, \
+        mean_dist)
+        if (k <= 128)
+            ORPCD_KNN_MULTI(2);
+        else if (k <= 256)
+            ORPCD_KNN_MULTI(4);
+        else if (k <= 512)
+            ORPCD_KNN_MULTI(8);
+        else if (k <= kMaxKnn)
+            ORPCD_KNN_MULTI(16);
+        else
+            return hipErrorInvalidValue;
+#undef ORPCD_KNN_MULTI
         return hipGetLastError();
     }
     const dim3 grid((unsigned)((L.ntiles + 3) / 4));

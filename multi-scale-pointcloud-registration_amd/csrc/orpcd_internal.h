@@ -174,6 +174,9 @@ struct KernelStats {
     double sched_launches = 0;  // timed launches of the ordered-dispatch search (nn_search_sched_kernel)
     double exact_filed = 0;     // exact_nn: queries re-searched in fp64 (nn_exact_kernel), every pass
     double exact_queries = 0;   // exact_nn: queries searched, every pass
+    // host wall-clock of the batches (always on; steady_clock): the whole
+    // gicp batch call, its launch calls, and its waits for the device
+    double host_batch_ms = 0, host_launch_ms = 0, host_sync_ms = 0, host_batches = 0;
 };
 
 // Boundary ties of a KNN covariance pass (launch_knn_cov_ties): points whose
@@ -397,6 +400,8 @@ struct orpcd_ctx {
                                   // at a time)
         int count_tiles = 1;      // profiling: the search also counts the quarters it scans (stats "tiles",
                                   // "pairs"); 0: hipEvent timing only
+        int sync_poll = 0;        // 1: the pass loop's device waits poll hipStreamQuery instead of blocking in
+                                  // hipStreamSynchronize
         int exact_fused = 64;     // > 0: the re-search runs in the accumulation's launch (GICP), this many
                                   // blocks per running start (at most exact_blocks); 0: a launch of its own
     } opt;
@@ -429,6 +434,7 @@ hipError_t build_layout(const double* dev_in64, int64_t n, const double bbox_lo[
                         const double origin[3], CloudLayout& L, bool with_tiles, hipStream_t s);
 
 // knn_kernels.hip
+constexpr int kMaxKnn = 1024;  // largest neighbourhood the device KNN keeps (16 sorted chunks of 64 per wave)
 hipError_t launch_knn_tiles(const CloudLayout& L, const double* in64, int k, double radius, double margin,
                             bool out_input_order, double* rawcov6, int32_t* nbr_idx, double* nbr_d2,
                             int32_t* nbr_cnt, hipStream_t s, double* mean_dist = nullptr);

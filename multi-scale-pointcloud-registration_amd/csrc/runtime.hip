@@ -176,8 +176,8 @@ int fpfh_buffers(orpcd_ctx* c, int k, int64_t n, int fpfh_knn) {
 
 int fpfh_device(orpcd_ctx* c, const double* host_xyz, int k, int64_t n, double normal_radius, int normal_knn,
                 double fpfh_radius, int fpfh_knn) {
-    CTX_REQUIRE(c, normal_knn > 0 && normal_knn <= 64 && fpfh_knn > 0 && fpfh_knn <= 64,
-                "fpfh: knn must be in [1, 64]");
+    CTX_REQUIRE(c, normal_knn > 0 && normal_knn <= kMaxKnn && fpfh_knn > 0 && fpfh_knn <= kMaxKnn,
+                "fpfh: knn must be in [1, 1024]");
     CTX_REQUIRE(c, normal_radius > 0 && fpfh_radius > 0, "fpfh: radii must be > 0");
     int rc = fpfh_buffers(c, k, n, fpfh_knn);
     if (rc) return rc;
@@ -918,6 +918,7 @@ int orpcd_gicp_batch_targets(orpcd_ctx* c, const double* R0, const double* t0, c
         std::memcpy(&sR[(size_t)pos[b] * 9], R0 + 9 * b, 9 * sizeof(double));
         std::memcpy(&st[(size_t)pos[b] * 3], t0 + 3 * b, 3 * sizeof(double));
     }
+    const auto t_batch = std::chrono::steady_clock::now();
     rc = batch_setup(c, sR.data(), st.data(), B, p);
     if (rc) return rc;
     std::vector<double> oT((size_t)B * 16), orm((size_t)B), ofit((size_t)B);
@@ -927,6 +928,8 @@ int orpcd_gicp_batch_targets(orpcd_ctx* c, const double* R0, const double* t0, c
     c->batch_ntgt = 1;
     c->batch_first[1] = 0;
     if (rc) return rc;
+    c->stats.host_batch_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_batch).count();
+    c->stats.host_batches += 1;
     c->last_slot = pos;
     c->last_slot_tgt.assign((size_t)B, 0);
     for (int k = 0; k < ntg; ++k)
@@ -1105,13 +1108,33 @@ int run_passes(orpcd_ctx* c, int B, const orpcd_gicp_params* p, double* T_out, d
         }
     }
     int pending = 0;  // timed passes since the last host sync
+    // ORPCD_GAPS=1: GPU-side anatomy of every pass (events before the pass,
+    // after the search, after the accumulation, after solve + next queries),
+    // summed per batch and printed: where a batch's device time goes,
+    // including idle gaps between kernels and around the host syncs
+    static const bool gaps = getenv("ORPCD_GAPS") != nullptr;
+    std::vector<hipEvent_t> gev;
+    double g_search = 0, g_accum = 0, g_solve = 0, g_between = 0;
+    hipEvent_t g_last = nullptr;
+    if (gaps) {
+        gev.resize((size_t)4 * (p->max_iteration + 2));
+        for (auto& e : gev) CTX_CHECK(c, hipEventCreateWithFlags(&e, hipEventDisableSystemFence));
+    }
+    using clk = std::chrono::steady_clock;
+    auto ms_since = [](clk::time_point a) { return std::chrono::duration<double, std::milli>(clk::now() - a).count(); };
     for (int pass = 0; pass <= p->max_iteration && nact > 0; ++pass) {
         hipEvent_t* ev = timed ? &c->ev_pool[3 * pending] : nullptr;
+        const auto tl = clk::now();
+        hipEvent_t* ge = gaps ? &gev[(size_t)4 * pass] : nullptr;
         if (timed) CTX_CHECK(c, hipEventRecord(ev[0], s));
+        if (gaps) CTX_CHECK(c, hipEventRecord(ge[0], s));
         const TgtBounds tb = target_bounds(c, hAct, nact);
-        CTX_CHECK(c, launch_gicp_pass(c, nact, pass, r2, s, timed ? ev[1] : nullptr, tb));
+        CTX_CHECK(c, launch_gicp_pass(c, nact, pass, r2, s, timed ? ev[1] : (gaps ? ge[1] : nullptr), tb));
         if (trace) CTX_CHECK(c, hipEventRecord(ev[2], s));  // accumulation time: traced runs only
+        if (gaps) CTX_CHECK(c, hipEventRecord(ge[2], s));
         CTX_CHECK(c, launch_gicp_solve(c, nact, pass, *p, s, tb));
+        if (gaps) CTX_CHECK(c, hipEventRecord(ge[3], s));
+        c->stats.host_launch_ms += ms_since(tl);
         ++pending;
         c->stats.passes += nact;
         if (c->exact_live) c->stats.exact_queries += (double)nact * (double)c->src.n;
@@ -1122,7 +1145,35 @@ int run_passes(orpcd_ctx* c, int B, const orpcd_gicp_params* p, double* T_out, d
         CTX_CHECK(c, hipMemcpyAsync(hDone, c->done.p, (size_t)B * 4, hipMemcpyDeviceToHost, s));
         unsigned long long tiles_now[2] = {0, 0};
         if (trace) CTX_CHECK(c, read_counters(c, tiles_now[0], tiles_now[1], true));
-        CTX_CHECK(c, hipStreamSynchronize(s));
+        const auto tw = clk::now();
+        if (c->opt.sync_poll) {
+            hipError_t e;
+            while ((e = hipStreamQuery(s)) == hipErrorNotReady) {
+                if (ms_since(tw) > 120e3) {
+                    c->err = "gicp: the device did not finish a pass interval within 120 s";
+                    return ORPCD_EDEVICE;
+                }
+            }
+            CTX_CHECK(c, e);
+        } else {
+            CTX_CHECK(c, hipStreamSynchronize(s));
+        }
+        c->stats.host_sync_ms += ms_since(tw);
+        if (gaps) {
+            for (int q = pass - pending + 1; q <= pass; ++q) {
+                hipEvent_t* g = &gev[(size_t)4 * q];
+                float a = 0, b = 0, d = 0, e = 0;
+                if (!timed) CTX_CHECK(c, hipEventElapsedTime(&a, g[0], g[1]));
+                CTX_CHECK(c, hipEventElapsedTime(&b, g[1], g[2]));
+                CTX_CHECK(c, hipEventElapsedTime(&d, g[2], g[3]));
+                if (g_last) CTX_CHECK(c, hipEventElapsedTime(&e, g_last, g[0]));
+                g_search += a;
+                g_accum += b;
+                g_solve += d;
+                g_between += e;
+                g_last = g[3];
+            }
+        }
         if (timed) {
             for (int q = 0; q < pending; ++q) {
                 float ms = 0.f, ms2 = 0.f;
@@ -1165,6 +1216,13 @@ int run_passes(orpcd_ctx* c, int B, const orpcd_gicp_params* p, double* T_out, d
         if (k != nact && k > 0) CTX_CHECK(c, hipMemcpyAsync(c->active.p, hAct, (size_t)k * 4, hipMemcpyHostToDevice, s));
         nact = k;
     }
+    if (gaps) {
+        float span = 0;
+        if (g_last) CTX_CHECK(c, hipEventElapsedTime(&span, gev[0], g_last));
+        fprintf(stderr, "[orpcd gaps] B %d: device span %.3f ms = search %.3f + accumulation %.3f + solve/queries %.3f"
+                        " + between passes %.3f\n", B, span, g_search, g_accum, g_solve, g_between);
+        for (auto e : gev) (void)hipEventDestroy(e);
+    }
     if (c->exact_live) {  // entries re-searched over the batch (nn_exact_kernel adds each pass's count)
         unsigned long long tot = 0;
         CTX_CHECK(c, hipMemcpy(&tot, c->xtotal.p, 8, hipMemcpyDeviceToHost));
@@ -1188,7 +1246,7 @@ int orpcd_sor(orpcd_ctx* c, const double* xyz, int64_t n, int32_t nb_neighbors, 
     *n_out = 0;
     CTX_REQUIRE(c, nb_neighbors >= 1 && std_ratio > 0,
                 "Illegal input parameters, the number of neighbors and standard deviation ratio must be positive.");
-    CTX_REQUIRE(c, nb_neighbors <= 64, "sor: nb_neighbors > 64 is not supported by the device KNN");
+    CTX_REQUIRE(c, nb_neighbors <= kMaxKnn, "sor: nb_neighbors > 1024 is not supported by the device KNN");
     if (n == 0) return ORPCD_OK;
     CTX_REQUIRE(c, xyz && n > 0 && n < kMaxPoints, "sor: bad cloud size");
     CTX_REQUIRE(c, finite_cloud(xyz, n), "sor: non-finite coordinates");
@@ -1457,7 +1515,7 @@ int orpcd_estimate_normals(orpcd_ctx* c, const double* xyz, int64_t n, int32_t k
     if (!c) return ORPCD_EINVAL;
     CTX_REQUIRE(c, xyz && n > 0, "estimate_normals: empty cloud");
     CTX_REQUIRE(c, n < kMaxPoints, "estimate_normals: too many points");
-    CTX_REQUIRE(c, knn > 0 && knn <= 64, "estimate_normals: knn must be in [1, 64]");
+    CTX_REQUIRE(c, knn > 0 && knn <= kMaxKnn, "estimate_normals: knn must be in [1, 1024]");
     CTX_REQUIRE(c, finite_cloud(xyz, n), "estimate_normals: non-finite coordinates");
     CTX_CHECK(c, hipSetDevice(c->device));
     double margin = 0.0;
@@ -1521,7 +1579,7 @@ int orpcd_fpfh_from_normals(orpcd_ctx* c, const double* xyz, const double* norma
                             double fpfh_radius, int32_t fpfh_knn, double* feat_out) {
     if (!c) return ORPCD_EINVAL;
     CTX_REQUIRE(c, xyz && normals && n > 0 && feat_out && n < kMaxPoints, "fpfh_from_normals: bad arguments");
-    CTX_REQUIRE(c, fpfh_knn > 0 && fpfh_knn <= 64, "fpfh: knn must be in [1, 64]");
+    CTX_REQUIRE(c, fpfh_knn > 0 && fpfh_knn <= kMaxKnn, "fpfh: knn must be in [1, 1024]");
     CTX_REQUIRE(c, fpfh_radius > 0, "fpfh: radii must be > 0");
     CTX_REQUIRE(c, finite_cloud(xyz, n) && finite_cloud(normals, n), "fpfh_from_normals: non-finite values");
     CTX_CHECK(c, hipSetDevice(c->device));
@@ -1666,6 +1724,7 @@ int orpcd_set_option(orpcd_ctx* c, const char* key, double value) {
     else if (k == "exact_blocks" && v >= 1 && v <= 65536) c->opt.exact_blocks = v;
     else if (k == "exact_fused" && v >= 0 && v <= 4096) c->opt.exact_fused = v;
     else if (k == "count_tiles" && (v == 0 || v == 1)) c->opt.count_tiles = v;
+    else if (k == "sync_poll" && (v == 0 || v == 1)) c->opt.sync_poll = v;
     else {
         c->err = "set_option: unknown key or bad value: " + k;
         return ORPCD_EINVAL;
@@ -1726,10 +1785,11 @@ int orpcd_profiling(orpcd_ctx* c, int32_t enable) {
 
 int orpcd_stats(orpcd_ctx* c, double* out, int32_t n) {
     if (!c || !out) return ORPCD_EINVAL;
-    const double v[10] = {c->stats.launches, c->stats.ms,       c->stats.pairs,          c->stats.iterations,
+    const double v[14] = {c->stats.launches, c->stats.ms,       c->stats.pairs,          c->stats.iterations,
                           c->stats.passes,   c->stats.tiles,    c->stats.accum_ms,       c->stats.sched_launches,
-                          c->stats.exact_filed, c->stats.exact_queries};
-    for (int i = 0; i < n && i < 10; ++i) out[i] = v[i];
+                          c->stats.exact_filed, c->stats.exact_queries, c->stats.host_batch_ms,
+                          c->stats.host_launch_ms, c->stats.host_sync_ms, c->stats.host_batches};
+    for (int i = 0; i < n && i < 14; ++i) out[i] = v[i];
     return ORPCD_OK;
 }
 

@@ -89,8 +89,9 @@ class FastGlobalOptimizer(IOptimizer):
                                                 __NORMAL_ESTIMATE_RADIUS__, "normal estimate radius")
         self._normal_estimate_knn = positive(normal_estimate_knn, __NORMAL_ESTIMATE_KNN__,
                                              "normal estimate knn")
-        if not (1 <= int(self._fpfh_knn) <= 64 and 1 <= int(self._normal_estimate_knn) <= 64):
-            raise ValueError("this build supports neighbourhoods of at most 64 points (knn <= 64)")
+        if not (int(self._fpfh_knn) <= 1024 and int(self._normal_estimate_knn) <= 1024):
+            # the device KNN keeps up to 16 sorted chunks of 64 per query (knn_wave_multi_kernel)
+            raise ValueError("this build supports neighbourhoods of at most 1024 points (knn <= 1024)")
         self._target_features_from_source = bool(target_features_from_source)
         self._maximum_tuple_count = int(maximum_tuple_count)
         self._seed = int(seed)

@@ -70,7 +70,7 @@ def test_fpfh_edge_cases(ctx, oracle):
     on, of = oracle.fpfh(dup, 0.1, 10, 0.1, 10)
     assert np.allclose(gn, on, atol=1e-10) and np.allclose(gf, of, atol=1e-9)
     with pytest.raises(ValueError):
-        ctx.fpfh(dup, 0.1, 65, 0.1, 10)
+        ctx.fpfh(dup, 0.1, 1025, 0.1, 10)
 
 
 def _certify_feature_nn(q, t, got):

@@ -46,7 +46,7 @@ def test_sor_edges(ctx, oracle):
     with pytest.raises(ValueError):
         ctx.sor(small, 0, 2.0)
     with pytest.raises(ValueError):
-        ctx.sor(small, 65, 2.0)
+        ctx.sor(small, 1025, 2.0)
 
 
 def test_sor_block_and_c1_preprocessing(oracle):

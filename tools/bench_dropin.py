@@ -65,6 +65,8 @@ def main():
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--attempts", type=int, default=30)
     ap.add_argument("--out", default=None)
+    ap.add_argument("--opt", default="{}", help="runtime options (orpcd_set_option), JSON")
+    ap.add_argument("--events", type=int, default=0, help="time the search launches with hipEvents (stats ms)")
     ap.add_argument("--legs", default="caller_only,batched,dropin,dropin_nospec,dropin_cold,align",
                     help="comma-separated subset of the legs to run")
     a = ap.parse_args()
@@ -76,12 +78,17 @@ def main():
 
     from orpcd_amd import _native
     ctx = _native.default_context(None)
+    for k, v in json.loads(a.opt).items():
+        ctx.set_option(k, v)
 
     def leg(opt, name):
         al = Aligner(Preprocessor([]), Preprocessor([]), opt, attempts=a.attempts)
         np.random.seed(999)
         al.multistart_registration(s, t)  # warm-up
         ctx.reset_stats()
+        if a.events:
+            ctx.set_option("count_tiles", 0)
+            ctx.profiling(True)
         times, rmse, inside = [], [], []
         np.random.seed(1000)
         for k in range(a.reps):
@@ -98,9 +105,13 @@ def main():
         print(f"{name}: {np.median(times) * 1e3:.1f} ms per multistart"
               + (f" ({np.median(inside) * 1e3:.1f} ms inside optimize())" if inside else ""), file=sys.stderr, flush=True)
         leg.inside[name] = round(float(np.median(inside)) * 1e3, 2) if inside else None
+        ctx.profiling(False)
         st = ctx.stats()
         nb = max(st["host_batches"], 1)
         leg.host[name] = {k: round(st[k] / nb, 3) for k in ("host_batch_ms", "host_launch_ms", "host_sync_ms")}
+        if a.events:
+            leg.host[name]["search_ms_per_batch"] = round(st["ms"] / nb, 3)
+            leg.host[name]["search_launches_per_batch"] = round(st["launches"] / nb, 1)
         leg.host[name]["batches"] = int(st["host_batches"])
         print(f"  {name} per batch: {leg.host[name]}", file=sys.stderr, flush=True)
         return float(np.median(times)), rmse
