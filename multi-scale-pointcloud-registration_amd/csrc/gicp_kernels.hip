@@ -1530,7 +1530,7 @@ __device__ __forceinline__ void gicp_block_terms(int slot, int ablk, const doubl
                                                  const double* __restrict__ tgt64, const double* __restrict__ tcov,
                                                  const double* __restrict__ Qm, const double* __restrict__ Rm,
                                                  double r2, unsigned long long* __restrict__ best,
-                                                 int32_t* __restrict__ prevnn, double acc[kNacc],
+                                                 int32_t* __restrict__ prevnn, double acc[kNacc], double om,
                                                  unsigned* __restrict__ sec = nullptr,
                                                  unsigned long long* __restrict__ total = nullptr) {
 #pragma clang fp contract(off)  // no fused multiply-add: the same rounding in every caller
@@ -1548,7 +1548,7 @@ __device__ __forceinline__ void gicp_block_terms(int slot, int ablk, const doubl
     constexpr int kQ = accum_qpt(0);
     unsigned long long bv[kQ];
     unsigned sk[kQ];
-    double p[kQ][3], cs[kQ][6], t3[kQ][3], ct[kQ][6];
+    double p[kQ][3], cs[kQ][kCovW], t3[kQ][3], ct[kQ][kCovW];
 #pragma unroll
     for (int k = 0; k < kQ; ++k) {
         const int i = (ablk * kQ + k) * 256 + threadIdx.x;
@@ -1557,9 +1557,9 @@ __device__ __forceinline__ void gicp_block_terms(int slot, int ablk, const doubl
         sk[k] = sec && i < N ? sec[(size_t)slot * N + i] : 0xFFFFFFFFu;
 #pragma unroll
         for (int c = 0; c < 3; ++c) p[k][c] = src[3 * ii + c];
-        const double* cs6 = scov + ((size_t)slot * N + ii) * 6;
+        const double* cs6 = scov + ((size_t)slot * N + ii) * kCovW;
 #pragma unroll
-        for (int c = 0; c < 6; ++c) cs[k][c] = cs6[c];
+        for (int c = 0; c < kCovW; ++c) cs[k][c] = cs6[c];
     }
     if (sec) {
 #pragma unroll
@@ -1587,7 +1587,7 @@ __device__ __forceinline__ void gicp_block_terms(int slot, int ablk, const doubl
 #pragma unroll
         for (int c = 0; c < 3; ++c) t3[k][c] = ldg_f64(tgt64 + 3 * jj + c);
 #pragma unroll
-        for (int c = 0; c < 6; ++c) ct[k][c] = ldg_f64(tcov + (size_t)jj * 6 + c);
+        for (int c = 0; c < kCovW; ++c) ct[k][c] = ldg_f64(tcov + (size_t)jj * kCovW + c);
     }
 #pragma unroll
     for (int k = 0; k < kQ; ++k) {
@@ -1597,12 +1597,25 @@ __device__ __forceinline__ void gicp_block_terms(int slot, int ablk, const doubl
         const double d[3] = {q[0] - t3[k][0], q[1] - t3[k][1], q[2] - t3[k][2]};
         const double d2 = d[0] * d[0] + d[1] * d[1] + d[2] * d[2];
         if (!(d2 < r2)) continue;
+#if ORPCD_NORMAL_COV
+        // Cs + Ct = 2 I - (1 - eps) (a a^T + b b^T), a = R e_s (the source's
+        // effective normal in the current pose: R (I - (1-eps) e e^T) R^T), b = e_t
+        const double* es = cs[k];
+        const double* b = ct[k];
+        const double a[3] = {R[0] * es[0] + R[1] * es[1] + R[2] * es[2], R[3] * es[0] + R[4] * es[1] + R[5] * es[2],
+                             R[6] * es[0] + R[7] * es[1] + R[8] * es[2]};
+        const Sym3 Mm{2.0 - om * (a[0] * a[0] + b[0] * b[0]), -om * (a[0] * a[1] + b[0] * b[1]),
+                      -om * (a[0] * a[2] + b[0] * b[2]),      2.0 - om * (a[1] * a[1] + b[1] * b[1]),
+                      -om * (a[1] * a[2] + b[1] * b[2]),      2.0 - om * (a[2] * a[2] + b[2] * b[2])};
+#else
+        (void)om;
         const double* cs6 = cs[k];
         const double* ct6 = ct[k];
         Sym3 Cs{cs6[0], cs6[1], cs6[2], cs6[3], cs6[4], cs6[5]};
         Cs = rotate_sym(R, Cs);
         const Sym3 Mm{Cs.xx + ct6[0], Cs.xy + ct6[1], Cs.xz + ct6[2], Cs.yy + ct6[3], Cs.yz + ct6[4],
                       Cs.zz + ct6[5]};
+#endif
         const Sym3 P = sym3_inverse(Mm);
         const double Pm[3][3] = {{P.xx, P.xy, P.xz}, {P.xy, P.yy, P.yz}, {P.xz, P.yz, P.zz}};
         // g = P d ; JTr = [q x g ; g]
@@ -1657,13 +1670,13 @@ __global__ __launch_bounds__(256) ORPCD_ACCUM_ATTR void gicp_accum_kernel(
     TgtBounds tb, const int32_t* __restrict__ active, const double* __restrict__ Qm,
     const double* __restrict__ Rm, const int32_t* __restrict__ done, double r2,
     unsigned long long* __restrict__ best, int32_t* __restrict__ prevnn, double* __restrict__ partial,
-    int nblk) {
+    int nblk, double om) {
     const int slot = active[blockIdx.y];
     if (done[slot]) return;
     const TargetDesc& tg = tdesc[target_of_row(tb, blockIdx.y)];
     __shared__ double red[4][kNacc];
     double acc[kNacc];
-    gicp_block_terms(slot, blockIdx.x, src, scov, N, tg.xyz64, tg.tcov, Qm, Rm, r2, best, prevnn, acc);
+    gicp_block_terms(slot, blockIdx.x, src, scov, N, tg.xyz64, tg.tcov, Qm, Rm, r2, best, prevnn, acc, om);
     block_partial<kNacc>(acc, red, [](int v) { return v; }, partial + ((size_t)slot * nblk + blockIdx.x) * kPartialStride);
 }
 
@@ -1682,7 +1695,7 @@ __global__ __launch_bounds__(256) ORPCD_ACCUM_ATTR void gicp_accum_exact_kernel(
     TgtBounds tb, const int32_t* __restrict__ active, const double* __restrict__ Qm,
     const double* __restrict__ Rm, const int32_t* __restrict__ done, double r2,
     unsigned long long* __restrict__ best, int32_t* __restrict__ prevnn, double* __restrict__ partial,
-    int nblk, int nexact, const float4* __restrict__ q32, ExactArgs ex) {
+    int nblk, int nexact, const float4* __restrict__ q32, ExactArgs ex, double om) {
     __shared__ double red[4][kNacc];
     __shared__ int tlist[4][kExactList];
     if ((int)blockIdx.x < nexact) {
@@ -1695,7 +1708,7 @@ __global__ __launch_bounds__(256) ORPCD_ACCUM_ATTR void gicp_accum_exact_kernel(
     if (done[slot]) return;
     const TargetDesc& tg = tdesc[target_of_row(tb, row)];
     double acc[kNacc];
-    gicp_block_terms(slot, bx, src, scov, N, tg.xyz64, tg.tcov, Qm, Rm, r2, best, prevnn, acc, ex.sec, ex.total);
+    gicp_block_terms(slot, bx, src, scov, N, tg.xyz64, tg.tcov, Qm, Rm, r2, best, prevnn, acc, om, ex.sec, ex.total);
     block_partial<kNacc>(acc, red, [](int v) { return v; }, partial + ((size_t)slot * nblk + bx) * kPartialStride);
 }
 
@@ -2125,7 +2138,7 @@ hipError_t launch_gicp_pass(const orpcd_ctx* c, int nact, int pass, double r2, h
         const int nexact = std::max(8, std::min(c->opt.exact_blocks, c->opt.exact_fused * nact));
         gicp_accum_exact_kernel<<<(unsigned)(nexact + ablk * nact), 256, 0, s>>>(
             c->src.xyz64.p, c->scov.p, N, c->tdesc.p, tb, c->active.p, c->Q.p, c->R.p, c->done.p, r2, c->best.p,
-            c->prevnn.p, c->partial.p, ablk, nexact, c->q32.p, exact_args(c, pass));
+            c->prevnn.p, c->partial.p, ablk, nexact, c->q32.p, exact_args(c, pass), 1.0 - c->batch_eps);
         return hipGetLastError();
     }
     if (c->est == kEstP2P) {
@@ -2136,7 +2149,7 @@ hipError_t launch_gicp_pass(const orpcd_ctx* c, int nact, int pass, double r2, h
     }
     gicp_accum_kernel<<<dim3((unsigned)ablk, (unsigned)nact), 256, 0, s>>>(
         c->src.xyz64.p, c->scov.p, N, c->tdesc.p, tb, c->active.p, c->Q.p, c->R.p, c->done.p, r2, c->best.p,
-        c->prevnn.p, c->partial.p, ablk);
+        c->prevnn.p, c->partial.p, ablk, 1.0 - c->batch_eps);
     return hipGetLastError();
 }
 

@@ -25,7 +25,8 @@ namespace orpcd {
 __global__ __launch_bounds__(256) void normals_cov_kernel(const double* __restrict__ rawcov6, int n,
                                                           const double* __restrict__ Rc9, int nslots, double eps,
                                                           double* __restrict__ normals3,
-                                                          double* __restrict__ cov6) {
+                                                          double* __restrict__ cov6,
+                                                          double* __restrict__ enorm3) {
     const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (gid >= (int64_t)n * nslots) return;
     const int b = (int)(gid / n);
@@ -49,6 +50,12 @@ __global__ __launch_bounds__(256) void normals_cov_kernel(const double* __restri
         normals3[3 * gid] = nrm[0];
         normals3[3 * gid + 1] = nrm[1];
         normals3[3 * gid + 2] = nrm[2];
+    }
+    if (enorm3) {  // C = I - (1 - eps) e e^T: e = n, or e1 where GetRotationFromE1ToX takes R = I
+        const bool quirk = nrm[0] < -0.99;
+        enorm3[3 * gid] = quirk ? 1.0 : nrm[0];
+        enorm3[3 * gid + 1] = quirk ? 0.0 : nrm[1];
+        enorm3[3 * gid + 2] = quirk ? 0.0 : nrm[2];
     }
     if (cov6 && eps >= 0.0) {
         Sym3 C = gicp_cov_from_normal(nrm, eps);
@@ -770,6 +777,14 @@ __global__ __launch_bounds__(64) void cov_override_kernel(const double* __restri
         nrm[1] = 0.0;
         nrm[2] = 1.0;
     }
+#if ORPCD_NORMAL_COV
+    (void)eps;
+    const bool quirk = nrm[0] < -0.99;
+    double* o = cov6 + ((size_t)slot * n + pos) * 3;
+    o[0] = quirk ? 1.0 : nrm[0];
+    o[1] = quirk ? 0.0 : nrm[1];
+    o[2] = quirk ? 0.0 : nrm[2];
+#else
     Sym3 C = gicp_cov_from_normal(nrm, eps);
     double* o = cov6 + ((size_t)slot * n + pos) * 6;
     o[0] = C.xx;
@@ -778,6 +793,7 @@ __global__ __launch_bounds__(64) void cov_override_kernel(const double* __restri
     o[3] = C.yy;
     o[4] = C.yz;
     o[5] = C.zz;
+#endif
 }
 
 hipError_t launch_cov_override(const double* ent, int count, int64_t n, double eps, double* cov6, hipStream_t s) {
@@ -787,11 +803,11 @@ hipError_t launch_cov_override(const double* ent, int count, int64_t n, double e
 }
 
 hipError_t launch_normals_cov(const double* rawcov6, int64_t n, const double* Rc9, int nslots, double eps,
-                              double* normals3, double* cov6, hipStream_t s) {
+                              double* normals3, double* cov6, hipStream_t s, double* enorm3) {
     const int64_t total = n * (int64_t)nslots;
     if (total <= 0) return hipSuccess;
     normals_cov_kernel<<<(unsigned)((total + 255) / 256), 256, 0, s>>>(rawcov6, (int)n, Rc9, nslots, eps,
-                                                                       normals3, cov6);
+                                                                       normals3, cov6, enorm3);
     return hipGetLastError();
 }
 

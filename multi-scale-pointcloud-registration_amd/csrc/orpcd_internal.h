@@ -25,6 +25,14 @@ constexpr int kCWaves = 4;                     // waves per block
 constexpr int kCBlock = 64 * kCWaves;          // threads per block
 constexpr int kCBlockQ = kCBlock * kCQPT;      // queries per block (one start)
 constexpr int kNacc = 29;                      // JTJ(21) + JTr(6) + sum d2 + count
+// GICP covariances stored as their effective normal e (C = I - (1 - eps) e e^T,
+// 3 doubles per point; e = e1 where Open3D's GetRotationFromE1ToX takes R = I)
+// instead of the 6 entries of C: half the accumulation's covariance loads.
+// 0: the 6-entry form (A/B builds).
+#ifndef ORPCD_NORMAL_COV
+#define ORPCD_NORMAL_COV 1
+#endif
+constexpr int kCovW = ORPCD_NORMAL_COV ? 3 : 6;  // doubles per stored GICP covariance
 constexpr int kEstGICP = 0, kEstP2P = 1;       // transformation estimation of a batch
 constexpr int kPartialStride = 32;             // doubles per block partial
 constexpr float kFarCoord = 1.0e18f;           // padding coordinate
@@ -236,7 +244,7 @@ struct orpcd_ctx {
 
     // targets (set per scale candidate), Morton order; target 0 is `tgt`
     orpcd::CloudLayout tgts[orpcd::kMaxTargets];
-    orpcd::DevBuf<double> tcovs[orpcd::kMaxTargets];  // M*6 GICP covariance (Morton order)
+    orpcd::DevBuf<double> tcovs[orpcd::kMaxTargets];  // M*kCovW GICP covariance (Morton order)
     double tgt_eps[orpcd::kMaxTargets] = {-1.0, -1.0, -1.0, -1.0, -1.0, -1.0, -1.0, -1.0,
                                           -1.0, -1.0, -1.0, -1.0, -1.0, -1.0, -1.0, -1.0};
     std::vector<double> tgt_host[orpcd::kMaxTargets];  // input-order copies (epsilon re-derivation)
@@ -298,7 +306,10 @@ struct orpcd_ctx {
     orpcd::DevBuf<int> tie_cnt;
 
     // batch state (per start slot)
-    orpcd::DevBuf<double> scov;     // B*N*6 posed-frame source covariance
+    orpcd::DevBuf<double> scov;     // B*N*kCovW posed-frame source covariance
+    double batch_eps = 1e-3;        // GICP epsilon of the running batch (the covariances' e e^T weight)
+    hipEvent_t gaps_ev0 = nullptr;  // ORPCD_GAPS: recorded where a batch's set-up starts
+    double gaps_setup_ms = 0;       // ORPCD_GAPS: host time of the last batch's set-up
     orpcd::DevBuf<int32_t> prevnn;  // B*N previous correspondence (Morton target index)
     orpcd::DevBuf<unsigned long long> best;  // B*N packed (d^2 bits, target) of the current pass
     orpcd::DevBuf<float4> q32;      // B*N fp32 queries of the current pass (x,y,z,0)
@@ -439,7 +450,7 @@ hipError_t launch_knn_tiles(const CloudLayout& L, const double* in64, int k, dou
                             bool out_input_order, double* rawcov6, int32_t* nbr_idx, double* nbr_d2,
                             int32_t* nbr_cnt, hipStream_t s, double* mean_dist = nullptr);
 hipError_t launch_normals_cov(const double* rawcov6, int64_t n, const double* Rc9, int nslots, double eps,
-                              double* normals3, double* cov6, hipStream_t s);
+                              double* normals3, double* cov6, hipStream_t s, double* enorm3 = nullptr);
 // KNN-kcov covariances (pure KNN, as launch_knn_tiles) whose search also keeps
 // kcov + kTieExtra neighbours and lists every boundary tie into `ties`
 // (SourceTies in runtime.hip); cov_override: entries {slot, Morton position,

@@ -94,12 +94,14 @@ int upload_target_k(orpcd_ctx* c, int k, const double* xyz, int64_t m, double ep
     int rc = upload_layout(c, xyz, m, c->tgts[k], true, &margin);
     if (rc) return rc;
     CTX_CHECK(c, prepare_seed_grid(c->tgts[k]));  // built by launch_seed_grids once the descriptor is up
-    CTX_CHECK(c, c->tcovs[k].ensure((size_t)m * 6));
+    CTX_CHECK(c, c->tcovs[k].ensure((size_t)m * kCovW));
     CTX_CHECK(c, c->scratch64b.ensure((size_t)m * 6));
     if (eps >= 0.0) {
         CTX_CHECK(c, launch_knn_tiles(c->tgts[k], c->scratch64a.p, 20, -1.0, margin, false, c->scratch64b.p, nullptr,
                                       nullptr, nullptr, c->stream));
-        CTX_CHECK(c, launch_normals_cov(c->scratch64b.p, m, nullptr, 1, eps, nullptr, c->tcovs[k].p, c->stream));
+        CTX_CHECK(c, launch_normals_cov(c->scratch64b.p, m, nullptr, 1, eps, nullptr,
+                                        ORPCD_NORMAL_COV ? nullptr : c->tcovs[k].p, c->stream,
+                                        ORPCD_NORMAL_COV ? c->tcovs[k].p : nullptr));
     }
     c->tgt_eps[k] = eps;
     c->tgt_host[k].assign(xyz, xyz + 3 * m);
@@ -613,7 +615,14 @@ int batch_setup(orpcd_ctx* c, const double* R0, const double* t0, int B, const o
     const int nblk = accum_blocks(N);
     c->last_B = 0;  // set once the batch is set up
     c->last_slot.clear();
-    if (!init16) CTX_CHECK(c, c->scov.ensure((size_t)B * N * 6));
+    static const bool gaps = getenv("ORPCD_GAPS") != nullptr;
+    const auto t_setup = std::chrono::steady_clock::now();
+    if (gaps) {
+        if (!c->gaps_ev0) CTX_CHECK(c, hipEventCreateWithFlags(&c->gaps_ev0, hipEventDisableSystemFence));
+        CTX_CHECK(c, hipEventRecord(c->gaps_ev0, c->stream));
+    }
+    if (!init16) CTX_CHECK(c, c->scov.ensure((size_t)B * N * kCovW));
+    c->batch_eps = p->epsilon;
     CTX_CHECK(c, c->prevnn.ensure((size_t)B * N));
     CTX_CHECK(c, c->best.ensure((size_t)B * N));
     CTX_CHECK(c, c->q32.ensure((size_t)B * N));
@@ -709,12 +718,15 @@ int batch_setup(orpcd_ctx* c, const double* R0, const double* t0, int B, const o
     // posed-frame source covariances for every start (rigid equivariance)
     c->est = init16 ? kEstP2P : kEstGICP;
     if (!init16) {
-        CTX_CHECK(c, launch_normals_cov(c->sraw.p, N, c->scratch64c.p, B, p->epsilon, nullptr, c->scov.p, s));
+        CTX_CHECK(c, launch_normals_cov(c->sraw.p, N, c->scratch64c.p, B, p->epsilon, nullptr,
+                                        ORPCD_NORMAL_COV ? nullptr : c->scov.p, s,
+                                        ORPCD_NORMAL_COV ? c->scov.p : nullptr));
         int rc = source_ties_apply(c, R0, t0, B, p->epsilon);  // boundary ties decided on the posed copies
         if (rc) return rc;
     }
     CTX_CHECK(c, launch_xform(c, B, 0, p->max_correspondence_distance * p->max_correspondence_distance, s,
                               target_bounds(c, hAct, B)));
+    c->gaps_setup_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_setup).count();
     return ORPCD_OK;
 }
 
@@ -1217,10 +1229,12 @@ int run_passes(orpcd_ctx* c, int B, const orpcd_gicp_params* p, double* T_out, d
         nact = k;
     }
     if (gaps) {
-        float span = 0;
+        float span = 0, pre = 0;
         if (g_last) CTX_CHECK(c, hipEventElapsedTime(&span, gev[0], g_last));
-        fprintf(stderr, "[orpcd gaps] B %d: device span %.3f ms = search %.3f + accumulation %.3f + solve/queries %.3f"
-                        " + between passes %.3f\n", B, span, g_search, g_accum, g_solve, g_between);
+        if (c->gaps_ev0) CTX_CHECK(c, hipEventElapsedTime(&pre, c->gaps_ev0, gev[0]));
+        fprintf(stderr, "[orpcd gaps] B %d: set-up host %.3f ms, device %.3f ms before pass 0; device span %.3f ms ="
+                        " search %.3f + accumulation %.3f + solve/queries %.3f + between passes %.3f\n", B,
+                c->gaps_setup_ms, pre, span, g_search, g_accum, g_solve, g_between);
         for (auto e : gev) (void)hipEventDestroy(e);
     }
     if (c->exact_live) {  // entries re-searched over the batch (nn_exact_kernel adds each pass's count)
