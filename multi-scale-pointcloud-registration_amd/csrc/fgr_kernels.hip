@@ -636,7 +636,7 @@ hipError_t launch_feat_nn(const double* Fq, const double* nq2, int64_t nq, const
         return e;
     if (getenv("ORPCD_TRACE")) {
         int32_t h = 0;
-        if ((e = hipMemcpyAsync(&h, nsel, 4, hipMemcpyDeviceToHost, s)) != hipSuccess) return e;
+        if ((e = d2h(&h, nsel, 4, s)) != hipSuccess) return e;
         if ((e = hipStreamSynchronize(s)) != hipSuccess) return e;
         fprintf(stderr, "[orpcd] feat_nn: %lld queries, %lld targets, %d parts, %d flagged for the exact pass\n",
                 (long long)nq, (long long)nt, parts, h);
@@ -682,7 +682,7 @@ hipError_t dedup_rows(const double* F, const double* n2, int64_t n, DedupBufs& b
                                            b.uidx.p, nsel, (int)n, s)) != hipSuccess)
         return e;
     int32_t nu = 0;
-    if ((e = hipMemcpyAsync(&nu, nsel, 4, hipMemcpyDeviceToHost, s)) != hipSuccess) return e;
+    if ((e = d2h(&nu, nsel, 4, s)) != hipSuccess) return e;
     if ((e = hipStreamSynchronize(s)) != hipSuccess) return e;
     gather_rows_kernel<<<(unsigned)(((int64_t)nu * kFD + 255) / 256), 256, 0, s>>>(F, n2, b.uidx.p, nu, b.Fu.p,
                                                                                    b.n2u.p);

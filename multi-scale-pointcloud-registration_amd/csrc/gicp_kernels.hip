@@ -2065,7 +2065,7 @@ static hipError_t dump_wavetime(int pass, int nact, int S, unsigned n, hipStream
     std::vector<unsigned long long> h((size_t)3 * n), keep;
     void* dp = nullptr;
     if ((e = hipGetSymbolAddress(&dp, HIP_SYMBOL(g_wt))) != hipSuccess) return e;
-    if ((e = hipMemcpy(h.data(), dp, h.size() * 8, hipMemcpyDeviceToHost)) != hipSuccess) return e;
+    if ((e = d2h(h.data(), dp, h.size() * 8, s)) != hipSuccess) return e;
     if ((e = hipMemset(dp, 0, h.size() * 8)) != hipSuccess) return e;
     for (unsigned k = 0; k < n; ++k)  // waves that searched (others exited early)
         if (h[3 * k] != 0) keep.insert(keep.end(), h.begin() + 3 * k, h.begin() + 3 * k + 3);

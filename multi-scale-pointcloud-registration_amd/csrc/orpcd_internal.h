@@ -4,6 +4,7 @@
 #include <stdint.h>
 
 #include <algorithm>
+#include <cstring>
 #include <string>
 #include <vector>
 
@@ -85,6 +86,91 @@ struct HostBuf {  // pinned
         n = 0;
     }
 };
+
+// ------------------------------------------------ host <-> device copies
+// Every copy between the device and host memory the library does not own as
+// pinned (the caller's arrays, std::vector buffers, stack scalars) goes
+// through a pinned staging buffer of the calling thread, never through
+// hipMemcpy* on pageable memory.  Measured on MI355X ("drop-in
+// stalls"): HIP pins pageable host pages for its copies, and when the host
+// later returns such pages to the kernel (glibc trimming its heap after the
+// caller frees a large array) the driver stops every queue of the process
+// until the mapping is restored -- 10-30 ms during which already enqueued
+// passes do not start.  The reference-shaped drop-in loop (a 1.2 MB posed copy
+// allocated and freed per attempt) hit it in most processes: a 30-start batch
+// took 31-47 ms instead of 15.7 ms.  With staged copies no host page of the
+// caller is ever known to the GPU.
+struct Staging {
+    HostBuf<unsigned char> buf;
+    hipEvent_t ev = nullptr;  // recorded after the last staged host -> device copy
+    bool pending = false;     // that copy may still be reading buf
+};
+inline Staging& staging() {
+    thread_local Staging st;
+    return st;
+}
+inline hipError_t staging_reserve(Staging& st, size_t bytes) {
+    hipError_t e = hipSuccess;
+    if (st.pending) {  // the previous host -> device copy still reads the buffer
+        if ((e = hipEventSynchronize(st.ev)) != hipSuccess) return e;
+        st.pending = false;
+    }
+    if (bytes > st.buf.n) e = st.buf.ensure(std::max(bytes, 2 * st.buf.n));  // geometric: few re-pins
+    return e;
+}
+// host -> device, asynchronous on s (src may be reused as soon as this returns)
+inline hipError_t h2d(void* dst, const void* src, size_t bytes, hipStream_t s) {
+    if (bytes == 0) return hipSuccess;
+    Staging& st = staging();
+    hipError_t e = staging_reserve(st, bytes);
+    if (e != hipSuccess) return e;
+    std::memcpy(st.buf.p, src, bytes);
+    if ((e = hipMemcpyAsync(dst, st.buf.p, bytes, hipMemcpyHostToDevice, s)) != hipSuccess) return e;
+    if (!st.ev && (e = hipEventCreateWithFlags(&st.ev, hipEventDisableTiming)) != hipSuccess) return e;
+    if ((e = hipEventRecord(st.ev, s)) != hipSuccess) return e;
+    st.pending = true;
+    return hipSuccess;
+}
+// the same for a strided block: `rows` rows of `width` bytes, pitches in bytes
+inline hipError_t h2d_2d(void* dst, size_t dpitch, const void* src, size_t spitch, size_t width, size_t rows,
+                         hipStream_t s) {
+    if (width == 0 || rows == 0) return hipSuccess;
+    Staging& st = staging();
+    hipError_t e = staging_reserve(st, width * rows);
+    if (e != hipSuccess) return e;
+    for (size_t r = 0; r < rows; ++r)
+        std::memcpy(st.buf.p + r * width, static_cast<const unsigned char*>(src) + r * spitch, width);
+    e = hipMemcpy2DAsync(dst, dpitch, st.buf.p, width, width, rows, hipMemcpyHostToDevice, s);
+    if (e != hipSuccess) return e;
+    if (!st.ev && (e = hipEventCreateWithFlags(&st.ev, hipEventDisableTiming)) != hipSuccess) return e;
+    if ((e = hipEventRecord(st.ev, s)) != hipSuccess) return e;
+    st.pending = true;
+    return hipSuccess;
+}
+// device -> host after everything enqueued on s: returns with dst written
+inline hipError_t d2h(void* dst, const void* src, size_t bytes, hipStream_t s) {
+    if (bytes == 0) return hipSuccess;
+    Staging& st = staging();
+    hipError_t e = staging_reserve(st, bytes);
+    if (e != hipSuccess) return e;
+    if ((e = hipMemcpyAsync(st.buf.p, src, bytes, hipMemcpyDeviceToHost, s)) != hipSuccess) return e;
+    if ((e = hipStreamSynchronize(s)) != hipSuccess) return e;
+    std::memcpy(dst, st.buf.p, bytes);
+    return hipSuccess;
+}
+inline hipError_t d2h_2d(void* dst, size_t dpitch, const void* src, size_t spitch, size_t width, size_t rows,
+                         hipStream_t s) {
+    if (width == 0 || rows == 0) return hipSuccess;
+    Staging& st = staging();
+    hipError_t e = staging_reserve(st, width * rows);
+    if (e != hipSuccess) return e;
+    e = hipMemcpy2DAsync(st.buf.p, width, src, spitch, width, rows, hipMemcpyDeviceToHost, s);
+    if (e != hipSuccess) return e;
+    if ((e = hipStreamSynchronize(s)) != hipSuccess) return e;
+    for (size_t r = 0; r < rows; ++r)
+        std::memcpy(static_cast<unsigned char*>(dst) + r * dpitch, st.buf.p + r * width, width);
+    return hipSuccess;
+}
 
 // A cloud in device memory, in Morton order (sort_kernels.hip).
 // Every fp32 copy (p4, tile / quarter / super-tile boxes) is relative to

@@ -163,7 +163,7 @@ hipError_t launch_voxel_down_sample(const double* xyz, int64_t n, const double v
     if ((e = hipcub::DeviceRunLengthEncode::Encode(b.tmp.p, t2, k1, b.ukey.p, cnt, nrun, N, s)) != hipSuccess)
         return e;
     int32_t nv = 0;
-    if ((e = hipMemcpyAsync(&nv, nrun, 4, hipMemcpyDeviceToHost, s)) != hipSuccess) return e;
+    if ((e = d2h(&nv, nrun, 4, s)) != hipSuccess) return e;
     if ((e = hipStreamSynchronize(s)) != hipSuccess) return e;
     *nvox_out = nv;
     if (!out || nv == 0) return hipSuccess;

@@ -83,7 +83,7 @@ int layout_from_device(orpcd_ctx* c, const double* host_xyz, const double* dev_x
 // order on device.
 int upload_layout(orpcd_ctx* c, const double* xyz, int64_t n, CloudLayout& L, bool tiles, double* margin = nullptr) {
     CTX_CHECK(c, c->scratch64a.ensure((size_t)n * 3));
-    CTX_CHECK(c, hipMemcpyAsync(c->scratch64a.p, xyz, (size_t)n * 24, hipMemcpyHostToDevice, c->stream));
+    CTX_CHECK(c, h2d(c->scratch64a.p, xyz, (size_t)n * 24, c->stream));
     return layout_from_device(c, xyz, c->scratch64a.p, n, L, tiles, margin);
 }
 
@@ -107,8 +107,7 @@ int upload_target_k(orpcd_ctx* c, int k, const double* xyz, int64_t m, double ep
     c->tgt_host[k].assign(xyz, xyz + 3 * m);
     CTX_CHECK(c, c->tdesc.ensure(kMaxTargets));
     write_target_desc(c->tgts[k], c->tcovs[k].p, c->opt.seed_reps, c->opt.seed_grid != 0, c->tdesc_h[k]);
-    CTX_CHECK(c, hipMemcpyAsync(c->tdesc.p + k, &c->tdesc_h[k], sizeof(TargetDesc), hipMemcpyHostToDevice,
-                                c->stream));
+    CTX_CHECK(c, h2d(c->tdesc.p + k, &c->tdesc_h[k], sizeof(TargetDesc), c->stream));
     return ORPCD_OK;
 }
 
@@ -134,7 +133,7 @@ int targets_for_epsilon(orpcd_ctx* c, int ntgt, double eps) {
 // sum / max of the spread profiling counters (device -> host, synchronous on s)
 hipError_t read_counters(orpcd_ctx* c, unsigned long long& tiles, unsigned long long& maxw, bool reset_max) {
     std::vector<unsigned long long> h((size_t)kCounterSlots * kCounterStride);
-    hipError_t e = hipMemcpyAsync(h.data(), c->counters.p, h.size() * 8, hipMemcpyDeviceToHost, c->stream);
+    hipError_t e = d2h(h.data(), c->counters.p, h.size() * 8, c->stream);
     if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
     if (e != hipSuccess) return e;
     tiles = 0;
@@ -144,7 +143,7 @@ hipError_t read_counters(orpcd_ctx* c, unsigned long long& tiles, unsigned long 
         maxw = std::max(maxw, h[(size_t)i * kCounterStride + 1]);
         if (reset_max) h[(size_t)i * kCounterStride + 1] = 0;
     }
-    if (reset_max) e = hipMemcpyAsync(c->counters.p, h.data(), h.size() * 8, hipMemcpyHostToDevice, c->stream);
+    if (reset_max) e = h2d(c->counters.p, h.data(), h.size() * 8, c->stream);
     return e;
 }
 
@@ -250,14 +249,14 @@ int fgr_device(orpcd_ctx* c, const double* src, int64_t n, const double* tgt, in
         const int64_t nb = (np[k] + 255) / 256;
         std::vector<double> part((size_t)nb * 3);
         CTX_CHECK(c, launch_sum3(F.xyz[k].p, np[k], F.red.p, s));
-        CTX_CHECK(c, hipMemcpyAsync(part.data(), F.red.p, part.size() * 8, hipMemcpyDeviceToHost, s));
+        CTX_CHECK(c, d2h(part.data(), F.red.p, part.size() * 8, s));
         CTX_CHECK(c, hipStreamSynchronize(s));
         double sum[3] = {0.0, 0.0, 0.0};
         for (int64_t b = 0; b < nb; ++b)
             for (int a = 0; a < 3; ++a) sum[a] += part[(size_t)3 * b + a];
         for (int a = 0; a < 3; ++a) mean[k][a] = sum[a] / (double)np[k];
         CTX_CHECK(c, launch_maxnorm(F.xyz[k].p, np[k], mean[k], F.red.p, s));
-        CTX_CHECK(c, hipMemcpyAsync(part.data(), F.red.p, (size_t)nb * 8, hipMemcpyDeviceToHost, s));
+        CTX_CHECK(c, d2h(part.data(), F.red.p, (size_t)nb * 8, s));
         CTX_CHECK(c, hipStreamSynchronize(s));
         double mx = 0.0;
         for (int64_t b = 0; b < nb; ++b) mx = std::max(mx, part[(size_t)b]);
@@ -287,8 +286,8 @@ int fgr_device(orpcd_ctx* c, const double* src, int64_t n, const double* tgt, in
                                 F.fnn, F.nn[1].p, s));
     fgr_mark(s, "feature matching");
     std::vector<int32_t> j_to_i((size_t)nPtj), i_to_j((size_t)nPti);
-    CTX_CHECK(c, hipMemcpyAsync(j_to_i.data(), F.nn[0].p, (size_t)nPtj * 4, hipMemcpyDeviceToHost, s));
-    CTX_CHECK(c, hipMemcpyAsync(i_to_j.data(), F.nn[1].p, (size_t)nPti * 4, hipMemcpyDeviceToHost, s));
+    CTX_CHECK(c, d2h(j_to_i.data(), F.nn[0].p, (size_t)nPtj * 4, s));
+    CTX_CHECK(c, d2h(i_to_j.data(), F.nn[1].p, (size_t)nPti * 4, s));
     CTX_CHECK(c, hipStreamSynchronize(s));
     // --- cross check, in i order: (i, i_to_j[i]) with j_to_i[i_to_j[i]] == i
     std::vector<std::pair<int, int>> corres;
@@ -341,11 +340,11 @@ int fgr_device(orpcd_ctx* c, const double* src, int64_t n, const double* tgt, in
     // --- GNC / Geman-McClure IRLS in one workgroup (fp64)
     CTX_CHECK(c, F.pq.ensure(pq.size()));
     CTX_CHECK(c, F.Tn.ensure(16));
-    if (K > 0) CTX_CHECK(c, hipMemcpyAsync(F.pq.p, pq.data(), (size_t)K * 48, hipMemcpyHostToDevice, s));
+    if (K > 0) CTX_CHECK(c, h2d(F.pq.p, pq.data(), (size_t)K * 48, s));
     CTX_CHECK(c, launch_fgr_irls(F.pq.p, F.pq.p + (size_t)3 * K, K, 1.0, p.iteration_number, p.division_factor,
                                  p.maximum_correspondence_distance, p.decrease_mu ? 1 : 0, F.Tn.p, s));
     double Tn[16];
-    CTX_CHECK(c, hipMemcpyAsync(Tn, F.Tn.p, sizeof(Tn), hipMemcpyDeviceToHost, s));
+    CTX_CHECK(c, d2h(Tn, F.Tn.p, sizeof(Tn), s));
     CTX_CHECK(c, hipStreamSynchronize(s));
     fgr_mark(s, "irls");
     // --- GetInvTransformationOriginalScale (4x4 algebra)
@@ -367,7 +366,7 @@ int fgr_device(orpcd_ctx* c, const double* src, int64_t n, const double* tgt, in
     CTX_CHECK(c, c->scratch32.ensure((size_t)n));
     CTX_CHECK(c, c->scratch64c.ensure((size_t)n));
     double* dT = F.raw.p + (size_t)n * 3;
-    CTX_CHECK(c, hipMemcpyAsync(dT, T, sizeof(T), hipMemcpyHostToDevice, s));
+    CTX_CHECK(c, h2d(dT, T, sizeof(T), s));
     CTX_CHECK(c, launch_transform_points(F.xyz[0].p, n, dT, F.raw.p, s));
     const double r = p.maximum_correspondence_distance;
     CTX_CHECK(c, launch_nn1(F.raw.p, n, c->aux, r * r, c->scratch32.p, c->scratch64c.p, s));
@@ -375,7 +374,7 @@ int fgr_device(orpcd_ctx* c, const double* src, int64_t n, const double* tgt, in
     CTX_CHECK(c, F.red.ensure((size_t)nb * 2));
     CTX_CHECK(c, launch_corr_stats(c->scratch32.p, c->scratch64c.p, n, F.red.p, s));
     std::vector<double> part((size_t)nb * 2);
-    CTX_CHECK(c, hipMemcpyAsync(part.data(), F.red.p, part.size() * 8, hipMemcpyDeviceToHost, s));
+    CTX_CHECK(c, d2h(part.data(), F.red.p, part.size() * 8, s));
     CTX_CHECK(c, hipStreamSynchronize(s));
     double cnt = 0.0, err2 = 0.0;
     for (int64_t b = 0; b < nb; ++b) {
@@ -451,7 +450,7 @@ int source_ties_detect(orpcd_ctx* c, const CloudLayout& L, const double* dev_in6
     to.abs_coef = abs_coef;
     CTX_CHECK(c, launch_knn_cov_ties(L, dev_in64, kcov, margin, input_order, rawcov6, to, c->stream));
     int cnt = 0;
-    CTX_CHECK(c, hipMemcpyAsync(&cnt, c->tie_cnt.p, 4, hipMemcpyDeviceToHost, c->stream));
+    CTX_CHECK(c, d2h(&cnt, c->tie_cnt.p, 4, c->stream));
     CTX_CHECK(c, hipStreamSynchronize(c->stream));
     T.on = true;
     if (cnt == 0) return ORPCD_OK;
@@ -459,8 +458,8 @@ int source_ties_detect(orpcd_ctx* c, const CloudLayout& L, const double* dev_in6
     T.complete = cnt <= kTieCap;
     std::vector<int32_t> rows((size_t)m * (K + 2));
     std::vector<double> d2((size_t)m * K);
-    CTX_CHECK(c, hipMemcpyAsync(rows.data(), c->tie_rows.p, rows.size() * 4, hipMemcpyDeviceToHost, c->stream));
-    CTX_CHECK(c, hipMemcpyAsync(d2.data(), c->tie_d2.p, d2.size() * 8, hipMemcpyDeviceToHost, c->stream));
+    CTX_CHECK(c, d2h(rows.data(), c->tie_rows.p, rows.size() * 4, c->stream));
+    CTX_CHECK(c, d2h(d2.data(), c->tie_d2.p, d2.size() * 8, c->stream));
     CTX_CHECK(c, hipStreamSynchronize(c->stream));
     T.xyz.assign(host_xyz, host_xyz + 3 * n);
     // deterministic order (the atomic list order is not): by input index
@@ -599,7 +598,7 @@ int source_ties_apply(orpcd_ctx* c, const double* R0, const double* t0, int B, d
     const int count = (int)(ent.size() / 8);
     if (count == 0) return ORPCD_OK;
     CTX_CHECK(c, c->tie_ent.ensure(ent.size()));
-    CTX_CHECK(c, hipMemcpy(c->tie_ent.p, ent.data(), ent.size() * 8, hipMemcpyHostToDevice));
+    CTX_CHECK(c, h2d(c->tie_ent.p, ent.data(), ent.size() * 8, c->stream));
     CTX_CHECK(c, launch_cov_override(c->tie_ent.p, count, c->src.n, eps, c->scov.p, c->stream));
     return ORPCD_OK;
 }
@@ -1069,7 +1068,7 @@ int read_outputs(orpcd_ctx* c, int B, unsigned long long tiles_before, double* T
     CTX_CHECK(c, hipMemcpyAsync(hRmse, c->out_rmse.p, (size_t)B * 8, hipMemcpyDeviceToHost, s));
     CTX_CHECK(c, hipMemcpyAsync(hIters, c->out_iters.p, (size_t)B * 4, hipMemcpyDeviceToHost, s));
     std::vector<int64_t> nc((size_t)B);
-    CTX_CHECK(c, hipMemcpyAsync(nc.data(), c->out_ncorr.p, (size_t)B * 8, hipMemcpyDeviceToHost, s));
+    CTX_CHECK(c, d2h(nc.data(), c->out_ncorr.p, (size_t)B * 8, s));
     CTX_CHECK(c, hipStreamSynchronize(s));
     unsigned long long tiles_after = 0;
     if (c->count_tiles) CTX_CHECK(c, read_counters(c, tiles_after, unused, false));
@@ -1134,6 +1133,10 @@ int run_passes(orpcd_ctx* c, int B, const orpcd_gicp_params* p, double* T_out, d
     }
     using clk = std::chrono::steady_clock;
     auto ms_since = [](clk::time_point a) { return std::chrono::duration<double, std::milli>(clk::now() - a).count(); };
+    const auto t_run = clk::now();
+    const double sync_before = c->stats.host_sync_ms;
+    int nsync = 0;
+    double sync_max = 0.0;
     for (int pass = 0; pass <= p->max_iteration && nact > 0; ++pass) {
         hipEvent_t* ev = timed ? &c->ev_pool[3 * pending] : nullptr;
         const auto tl = clk::now();
@@ -1170,7 +1173,10 @@ int run_passes(orpcd_ctx* c, int B, const orpcd_gicp_params* p, double* T_out, d
         } else {
             CTX_CHECK(c, hipStreamSynchronize(s));
         }
-        c->stats.host_sync_ms += ms_since(tw);
+        const double waited = ms_since(tw);
+        c->stats.host_sync_ms += waited;
+        ++nsync;
+        sync_max = std::max(sync_max, waited);
         if (gaps) {
             for (int q = pass - pending + 1; q <= pass; ++q) {
                 hipEvent_t* g = &gev[(size_t)4 * q];
@@ -1204,14 +1210,14 @@ int run_passes(orpcd_ctx* c, int B, const orpcd_gicp_params* p, double* T_out, d
                     last = tiles_now[0];
                     if (getenv("ORPCD_PHASES")) {  // libraries built with -DORPCD_PHASES
                         std::vector<unsigned long long> h((size_t)kCounterSlots * kCounterStride);
-                        CTX_CHECK(c, hipMemcpy(h.data(), c->counters.p, h.size() * 8, hipMemcpyDeviceToHost));
+                        CTX_CHECK(c, d2h(h.data(), c->counters.p, h.size() * 8, c->stream));
                         unsigned long long ph[8] = {0, 0, 0, 0, 0, 0, 0, 0};
                         for (int q = 0; q < kCounterSlots; ++q)
                             for (int f = 0; f < 8; ++f) {
                                 ph[f] += h[(size_t)q * kCounterStride + 2 + f];
                                 h[(size_t)q * kCounterStride + 2 + f] = 0;
                             }
-                        CTX_CHECK(c, hipMemcpy(c->counters.p, h.data(), h.size() * 8, hipMemcpyHostToDevice));
+                        CTX_CHECK(c, h2d(c->counters.p, h.data(), h.size() * 8, c->stream));
                         const double w = ph[3] > 0 ? (double)ph[3] : 1.0;
                         fprintf(stderr, "[orpcd]   waves %llu cycles/wave: query load %.0f  search %.0f (culling %.0f)"
                                 "  per wave: AABB rounds %.2f candidate tests %.2f improving tiles %.2f"
@@ -1235,11 +1241,13 @@ int run_passes(orpcd_ctx* c, int B, const orpcd_gicp_params* p, double* T_out, d
         fprintf(stderr, "[orpcd gaps] B %d: set-up host %.3f ms, device %.3f ms before pass 0; device span %.3f ms ="
                         " search %.3f + accumulation %.3f + solve/queries %.3f + between passes %.3f\n", B,
                 c->gaps_setup_ms, pre, span, g_search, g_accum, g_solve, g_between);
+        fprintf(stderr, "[orpcd gaps]   host: passes %.3f ms, %d device waits %.3f ms (longest %.3f)\n", ms_since(t_run),
+                nsync, c->stats.host_sync_ms - sync_before, sync_max);
         for (auto e : gev) (void)hipEventDestroy(e);
     }
     if (c->exact_live) {  // entries re-searched over the batch (nn_exact_kernel adds each pass's count)
         unsigned long long tot = 0;
-        CTX_CHECK(c, hipMemcpy(&tot, c->xtotal.p, 8, hipMemcpyDeviceToHost));
+        CTX_CHECK(c, d2h(&tot, c->xtotal.p, 8, c->stream));
         if (tot >> 40) {  // a fused accumulation thread stopped waiting for its re-search (never expected)
             c->err = "exact_nn: a re-search result was not published in time";
             return ORPCD_EDEVICE;
@@ -1279,11 +1287,11 @@ int orpcd_sor(orpcd_ctx* c, const double* xyz, int64_t n, int32_t nb_neighbors, 
     CTX_CHECK(c, launch_sor_select(avg, n, std_ratio, c->scratch64c.p, c->vox.flag.p, c->scratch32.p,
                                    c->scratch32.p + n, c->vox.tmp, s));
     int32_t k = 0;
-    CTX_CHECK(c, hipMemcpyAsync(&k, c->scratch32.p + n, 4, hipMemcpyDeviceToHost, s));
+    CTX_CHECK(c, d2h(&k, c->scratch32.p + n, 4, s));
     CTX_CHECK(c, hipStreamSynchronize(s));
     std::vector<int32_t> kept((size_t)k);
-    if (k > 0) CTX_CHECK(c, hipMemcpyAsync(kept.data(), c->scratch32.p, (size_t)k * 4, hipMemcpyDeviceToHost, s));
-    if (avg_out) CTX_CHECK(c, hipMemcpyAsync(avg_out, avg, (size_t)n * 8, hipMemcpyDeviceToHost, s));
+    if (k > 0) CTX_CHECK(c, d2h(kept.data(), c->scratch32.p, (size_t)k * 4, s));
+    if (avg_out) CTX_CHECK(c, d2h(avg_out, avg, (size_t)n * 8, s));
     CTX_CHECK(c, hipStreamSynchronize(s));
     for (int32_t i = 0; i < k; ++i) idx_out[i] = kept[i];
     *n_out = k;
@@ -1318,12 +1326,12 @@ int orpcd_voxel_down_sample(orpcd_ctx* c, const double* xyz, int64_t n, double v
     hipStream_t s = c->stream;
     CTX_CHECK(c, c->vox.xyz.ensure((size_t)n * 3));
     if (out_xyz) CTX_CHECK(c, c->vox.out.ensure((size_t)n * 3));
-    CTX_CHECK(c, hipMemcpyAsync(c->vox.xyz.p, xyz, (size_t)n * 24, hipMemcpyHostToDevice, s));
+    CTX_CHECK(c, h2d(c->vox.xyz.p, xyz, (size_t)n * 24, s));
     int64_t nv = 0;
     CTX_CHECK(c, launch_voxel_down_sample(c->vox.xyz.p, n, vmin, voxel_size, c->vox, out_xyz ? c->vox.out.p : nullptr,
                                           &nv, s));
     if (out_xyz && nv > 0)
-        CTX_CHECK(c, hipMemcpyAsync(out_xyz, c->vox.out.p, (size_t)nv * 24, hipMemcpyDeviceToHost, s));
+        CTX_CHECK(c, d2h(out_xyz, c->vox.out.p, (size_t)nv * 24, s));
     CTX_CHECK(c, hipStreamSynchronize(s));
     *n_out = nv;
     return ORPCD_OK;
@@ -1347,13 +1355,13 @@ int orpcd_farthest_downsample(orpcd_ctx* c, const double* xyz, int64_t n, int32_
     CTX_CHECK(c, c->scratch64c.ensure((size_t)2 * c->fps_blocks));
     CTX_CHECK(c, c->vox.tag.ensure((size_t)2 * c->fps_blocks));
     CTX_CHECK(c, c->scratch32.ensure(2));
-    CTX_CHECK(c, hipMemcpyAsync(c->vox.xyz.p, xyz, (size_t)n * 24, hipMemcpyHostToDevice, s));
+    CTX_CHECK(c, h2d(c->vox.xyz.p, xyz, (size_t)n * 24, s));
     unsigned* err = reinterpret_cast<unsigned*>(c->scratch32.p);
     CTX_CHECK(c, launch_fps(c->vox.xyz.p, n, (int)first, sample_size, c->fps_blocks, c->vox.idx64.p,
                             c->scratch64c.p, c->vox.tag.p, err, s));
     unsigned herr = 0;
-    CTX_CHECK(c, hipMemcpyAsync(idx_out, c->vox.idx64.p, (size_t)sample_size * 8, hipMemcpyDeviceToHost, s));
-    CTX_CHECK(c, hipMemcpyAsync(&herr, err, 4, hipMemcpyDeviceToHost, s));
+    CTX_CHECK(c, d2h(idx_out, c->vox.idx64.p, (size_t)sample_size * 8, s));
+    CTX_CHECK(c, d2h(&herr, err, 4, s));
     CTX_CHECK(c, hipStreamSynchronize(s));
     if (herr) {
         c->err = "farthest_downsample: blocks of the cooperative launch were not co-resident";
@@ -1384,7 +1392,7 @@ int orpcd_set_source_rows(orpcd_ctx* c, const double* xyz, int64_t n, int64_t ro
     CTX_CHECK(c, launch_gather_rows(c->scratch64b.p, c->src.perm.p, row_begin, ns, 6, c->sraw.p, c->stream));
     if (!c->ties.pt.empty()) {  // the ties on this rank's rows: their Morton positions
         std::vector<int32_t> perm((size_t)ns), inv((size_t)ns);
-        CTX_CHECK(c, hipMemcpyAsync(perm.data(), c->src.perm.p, (size_t)ns * 4, hipMemcpyDeviceToHost, c->stream));
+        CTX_CHECK(c, d2h(perm.data(), c->src.perm.p, (size_t)ns * 4, c->stream));
         CTX_CHECK(c, hipStreamSynchronize(c->stream));
         for (int64_t k = 0; k < ns; ++k) inv[(size_t)perm[k]] = (int32_t)k;
         for (size_t f = 0; f < c->ties.pt.size(); ++f) {
@@ -1425,7 +1433,7 @@ int orpcd_gicp_shard_pass(orpcd_ctx* c, double* sums_out, int32_t* active) {
     CTX_REQUIRE(c, sums_out && active, "gicp_shard_pass: null argument");
     CTX_REQUIRE(c, c->shard.begun, "gicp_shard_pass: call orpcd_gicp_shard_begin first");
     int32_t done = 0;
-    CTX_CHECK(c, hipMemcpyAsync(&done, c->done.p, 4, hipMemcpyDeviceToHost, c->stream));
+    CTX_CHECK(c, d2h(&done, c->done.p, 4, c->stream));
     CTX_CHECK(c, hipStreamSynchronize(c->stream));
     *active = done ? 0 : 1;
     for (int v = 0; v < kNacc; ++v) sums_out[v] = 0.0;
@@ -1447,7 +1455,7 @@ int orpcd_gicp_shard_pass(orpcd_ctx* c, double* sums_out, int32_t* active) {
                                   one_target()));
     if (timed) CTX_CHECK(c, hipEventRecord(c->ev_pool[2], c->stream));
     CTX_CHECK(c, launch_reduce_partials(c, 0, c->scratch64c.p, c->stream));
-    CTX_CHECK(c, hipMemcpyAsync(sums_out, c->scratch64c.p, kNacc * 8, hipMemcpyDeviceToHost, c->stream));
+    CTX_CHECK(c, d2h(sums_out, c->scratch64c.p, kNacc * 8, c->stream));
     CTX_CHECK(c, hipStreamSynchronize(c->stream));
     if (timed) {
         float ms = 0.f, ms2 = 0.f;
@@ -1468,10 +1476,10 @@ int orpcd_gicp_shard_update(orpcd_ctx* c, const double* sums_in, int32_t* done_o
     if (!c) return ORPCD_EINVAL;
     CTX_REQUIRE(c, sums_in && done_out, "gicp_shard_update: null argument");
     CTX_REQUIRE(c, c->shard.begun, "gicp_shard_update: call orpcd_gicp_shard_begin first");
-    CTX_CHECK(c, hipMemcpyAsync(c->scratch64c.p, sums_in, kNacc * 8, hipMemcpyHostToDevice, c->stream));
+    CTX_CHECK(c, h2d(c->scratch64c.p, sums_in, kNacc * 8, c->stream));
     CTX_CHECK(c, launch_gicp_solve_sums(c, c->scratch64c.p, c->shard.n_total, c->shard.pass, c->shard.p, c->stream));
     int32_t done = 0;
-    CTX_CHECK(c, hipMemcpyAsync(&done, c->done.p, 4, hipMemcpyDeviceToHost, c->stream));
+    CTX_CHECK(c, d2h(&done, c->done.p, 4, c->stream));
     CTX_CHECK(c, hipStreamSynchronize(c->stream));
     c->shard.pass += 1;
     *done_out = done;
@@ -1487,12 +1495,12 @@ int orpcd_gicp_shard_result(orpcd_ctx* c, double* T_out, double* rmse_out, doubl
     double fit = 0.0;
     int64_t nc = 0;
     hipStream_t s = c->stream;
-    CTX_CHECK(c, hipMemcpyAsync(&done, c->done.p, 4, hipMemcpyDeviceToHost, s));
-    CTX_CHECK(c, hipMemcpyAsync(T_out, c->T.p, 16 * 8, hipMemcpyDeviceToHost, s));
-    CTX_CHECK(c, hipMemcpyAsync(rmse_out, c->out_rmse.p, 8, hipMemcpyDeviceToHost, s));
-    CTX_CHECK(c, hipMemcpyAsync(&fit, c->out_fit.p, 8, hipMemcpyDeviceToHost, s));
-    CTX_CHECK(c, hipMemcpyAsync(&iters, c->out_iters.p, 4, hipMemcpyDeviceToHost, s));
-    CTX_CHECK(c, hipMemcpyAsync(&nc, c->out_ncorr.p, 8, hipMemcpyDeviceToHost, s));
+    CTX_CHECK(c, d2h(&done, c->done.p, 4, s));
+    CTX_CHECK(c, d2h(T_out, c->T.p, 16 * 8, s));
+    CTX_CHECK(c, d2h(rmse_out, c->out_rmse.p, 8, s));
+    CTX_CHECK(c, d2h(&fit, c->out_fit.p, 8, s));
+    CTX_CHECK(c, d2h(&iters, c->out_iters.p, 4, s));
+    CTX_CHECK(c, d2h(&nc, c->out_ncorr.p, 8, s));
     CTX_CHECK(c, hipStreamSynchronize(s));
     CTX_REQUIRE(c, done, "gicp_shard_result: the start has not finished");
     if (fitness_out) *fitness_out = fit;
@@ -1516,10 +1524,10 @@ int orpcd_nn1_radius(orpcd_ctx* c, const double* q, int64_t nq, const double* t,
     CTX_CHECK(c, c->scratch64b.ensure((size_t)nq * 3));
     CTX_CHECK(c, c->scratch64c.ensure((size_t)nq));
     CTX_CHECK(c, c->scratch32.ensure((size_t)nq));
-    CTX_CHECK(c, hipMemcpyAsync(c->scratch64b.p, q, (size_t)nq * 24, hipMemcpyHostToDevice, c->stream));
+    CTX_CHECK(c, h2d(c->scratch64b.p, q, (size_t)nq * 24, c->stream));
     CTX_CHECK(c, launch_nn1(c->scratch64b.p, nq, c->aux, radius * radius, c->scratch32.p, c->scratch64c.p, c->stream));
-    CTX_CHECK(c, hipMemcpyAsync(idx_out, c->scratch32.p, (size_t)nq * 4, hipMemcpyDeviceToHost, c->stream));
-    CTX_CHECK(c, hipMemcpyAsync(d2_out, c->scratch64c.p, (size_t)nq * 8, hipMemcpyDeviceToHost, c->stream));
+    CTX_CHECK(c, d2h(idx_out, c->scratch32.p, (size_t)nq * 4, c->stream));
+    CTX_CHECK(c, d2h(d2_out, c->scratch64c.p, (size_t)nq * 8, c->stream));
     CTX_CHECK(c, hipStreamSynchronize(c->stream));
     return ORPCD_OK;
 }
@@ -1544,11 +1552,11 @@ int orpcd_estimate_normals(orpcd_ctx* c, const double* xyz, int64_t n, int32_t k
                                   c->stream));
     CTX_CHECK(c, launch_normals_cov(uraw, n, nullptr, 1, epsilon, unrm, epsilon >= 0 ? ucov : nullptr, c->stream));
     std::vector<double> raw6((size_t)n * 6), cov6;
-    CTX_CHECK(c, hipMemcpyAsync(raw6.data(), uraw, (size_t)n * 48, hipMemcpyDeviceToHost, c->stream));
-    if (normals_out) CTX_CHECK(c, hipMemcpyAsync(normals_out, unrm, (size_t)n * 24, hipMemcpyDeviceToHost, c->stream));
+    CTX_CHECK(c, d2h(raw6.data(), uraw, (size_t)n * 48, c->stream));
+    if (normals_out) CTX_CHECK(c, d2h(normals_out, unrm, (size_t)n * 24, c->stream));
     if (gicpcov_out && epsilon >= 0) {
         cov6.resize((size_t)n * 6);
-        CTX_CHECK(c, hipMemcpyAsync(cov6.data(), ucov, (size_t)n * 48, hipMemcpyDeviceToHost, c->stream));
+        CTX_CHECK(c, d2h(cov6.data(), ucov, (size_t)n * 48, c->stream));
     }
     CTX_CHECK(c, hipStreamSynchronize(c->stream));
     auto expand = [n](const std::vector<double>& s6, double* o9) {
@@ -1578,13 +1586,12 @@ int orpcd_fpfh(orpcd_ctx* c, const double* xyz, int64_t n, double normal_radius,
     CTX_REQUIRE(c, finite_cloud(xyz, n), "fpfh: non-finite coordinates");
     CTX_CHECK(c, hipSetDevice(c->device));
     CTX_CHECK(c, c->fgr.xyz[0].ensure((size_t)n * 3));
-    CTX_CHECK(c, hipMemcpyAsync(c->fgr.xyz[0].p, xyz, (size_t)n * 24, hipMemcpyHostToDevice, c->stream));
+    CTX_CHECK(c, h2d(c->fgr.xyz[0].p, xyz, (size_t)n * 24, c->stream));
     int rc = fpfh_device(c, xyz, 0, n, normal_radius, normal_knn, fpfh_radius, fpfh_knn);
     if (rc) return rc;
     if (normals_out)
-        CTX_CHECK(c, hipMemcpyAsync(normals_out, c->fgr.nrm.p, (size_t)n * 24, hipMemcpyDeviceToHost, c->stream));
-    CTX_CHECK(c, hipMemcpy2DAsync(feat_out, 33 * sizeof(double), c->fgr.feat[0].p, kFeatDim * sizeof(double),
-                                  33 * sizeof(double), (size_t)n, hipMemcpyDeviceToHost, c->stream));
+        CTX_CHECK(c, d2h(normals_out, c->fgr.nrm.p, (size_t)n * 24, c->stream));
+    CTX_CHECK(c, d2h_2d(feat_out, 33 * sizeof(double), c->fgr.feat[0].p, kFeatDim * sizeof(double), 33 * sizeof(double), (size_t)n, c->stream));
     CTX_CHECK(c, hipStreamSynchronize(c->stream));
     return ORPCD_OK;
 }
@@ -1600,12 +1607,11 @@ int orpcd_fpfh_from_normals(orpcd_ctx* c, const double* xyz, const double* norma
     int rc = fpfh_buffers(c, 0, n, fpfh_knn);
     if (rc) return rc;
     CTX_CHECK(c, c->fgr.xyz[0].ensure((size_t)n * 3));
-    CTX_CHECK(c, hipMemcpyAsync(c->fgr.xyz[0].p, xyz, (size_t)n * 24, hipMemcpyHostToDevice, c->stream));
-    CTX_CHECK(c, hipMemcpyAsync(c->fgr.nrm.p, normals, (size_t)n * 24, hipMemcpyHostToDevice, c->stream));
+    CTX_CHECK(c, h2d(c->fgr.xyz[0].p, xyz, (size_t)n * 24, c->stream));
+    CTX_CHECK(c, h2d(c->fgr.nrm.p, normals, (size_t)n * 24, c->stream));
     rc = features_device(c, xyz, 0, n, fpfh_radius, fpfh_knn, 0.0);
     if (rc) return rc;
-    CTX_CHECK(c, hipMemcpy2DAsync(feat_out, 33 * sizeof(double), c->fgr.feat[0].p, kFeatDim * sizeof(double),
-                                  33 * sizeof(double), (size_t)n, hipMemcpyDeviceToHost, c->stream));
+    CTX_CHECK(c, d2h_2d(feat_out, 33 * sizeof(double), c->fgr.feat[0].p, kFeatDim * sizeof(double), 33 * sizeof(double), (size_t)n, c->stream));
     CTX_CHECK(c, hipStreamSynchronize(c->stream));
     return ORPCD_OK;
 }
@@ -1630,8 +1636,8 @@ int orpcd_fgr(orpcd_ctx* c, const double* src, int64_t n, const double* tgt, int
     for (int k = 0; k < 2; ++k) {
         CTX_CHECK(c, c->fgr.xyz[k].ensure((size_t)np[k] * 3));
         CTX_CHECK(c, c->fgr.feat[k].ensure((size_t)np[k] * kFeatDim));
-        CTX_CHECK(c, hipMemcpyAsync(c->fgr.xyz[k].p, xyz[k], (size_t)np[k] * 24, hipMemcpyHostToDevice, c->stream));
-        CTX_CHECK(c, hipMemcpyAsync(c->fgr.raw.p, feat[k], (size_t)np[k] * 33 * 8, hipMemcpyHostToDevice, c->stream));
+        CTX_CHECK(c, h2d(c->fgr.xyz[k].p, xyz[k], (size_t)np[k] * 24, c->stream));
+        CTX_CHECK(c, h2d(c->fgr.raw.p, feat[k], (size_t)np[k] * 33 * 8, c->stream));
         CTX_CHECK(c, launch_pad_features(c->fgr.raw.p, np[k], c->fgr.feat[k].p, c->stream));
     }
     return fgr_device(c, src, n, tgt, m, *p, T_out, fitness_out, rmse_out, ncorr_out, n_mutual_out);
@@ -1653,8 +1659,7 @@ int orpcd_feature_nn(orpcd_ctx* c, const double* q, int64_t nq, const double* t,
         CTX_CHECK(c, F.feat[k].ensure((size_t)np[k] * kFeatDim));
         CTX_CHECK(c, F.fn2[k].ensure((size_t)np[k]));
         CTX_CHECK(c, hipMemsetAsync(F.feat[k].p, 0, (size_t)np[k] * kFeatDim * 8, c->stream));
-        CTX_CHECK(c, hipMemcpy2DAsync(F.feat[k].p, kFeatDim * 8, in[k], (size_t)dim * 8, (size_t)dim * 8,
-                                      (size_t)np[k], hipMemcpyHostToDevice, c->stream));
+        CTX_CHECK(c, h2d_2d(F.feat[k].p, kFeatDim * 8, in[k], (size_t)dim * 8, (size_t)dim * 8, (size_t)np[k], c->stream));
         CTX_CHECK(c, launch_feat_norm(F.feat[k].p, np[k], F.fn2[k].p, c->stream));
     }
     CTX_CHECK(c, F.nn[0].ensure((size_t)nq));
@@ -1662,7 +1667,7 @@ int orpcd_feature_nn(orpcd_ctx* c, const double* q, int64_t nq, const double* t,
     CTX_CHECK(c, dedup_rows(F.feat[1].p, F.fn2[1].p, nt, F.dedup, &nu, c->stream));
     CTX_CHECK(c, launch_feat_nn(F.feat[0].p, F.fn2[0].p, nq, F.dedup.Fu.p, F.dedup.n2u.p, nu, F.dedup.uidx.p, dim,
                                 F.fnn, F.nn[0].p, c->stream));
-    CTX_CHECK(c, hipMemcpyAsync(idx_out, F.nn[0].p, (size_t)nq * 4, hipMemcpyDeviceToHost, c->stream));
+    CTX_CHECK(c, d2h(idx_out, F.nn[0].p, (size_t)nq * 4, c->stream));
     CTX_CHECK(c, hipStreamSynchronize(c->stream));
     return ORPCD_OK;
 }
@@ -1690,7 +1695,7 @@ int orpcd_fgr_optimize(orpcd_ctx* c, const double* src, int64_t n, const double*
     const int64_t np[2] = {n, m};
     for (int k = 0; k < 2; ++k) {
         CTX_CHECK(c, c->fgr.xyz[k].ensure((size_t)np[k] * 3));
-        CTX_CHECK(c, hipMemcpyAsync(c->fgr.xyz[k].p, xyz[k], (size_t)np[k] * 24, hipMemcpyHostToDevice, c->stream));
+        CTX_CHECK(c, h2d(c->fgr.xyz[k].p, xyz[k], (size_t)np[k] * 24, c->stream));
     }
     fgr_mark(c->stream, "upload");
     rc = fpfh_device(c, src, 0, n, normal_radius, normal_knn, fpfh_radius, fpfh_knn);
@@ -1726,8 +1731,7 @@ int orpcd_set_option(orpcd_ctx* c, const char* key, double value) {
         CTX_CHECK(c, hipSetDevice(c->device));
         for (int t = 0; t < c->ntgt; ++t) {
             write_target_desc(c->tgts[t], c->tcovs[t].p, c->opt.seed_reps, c->opt.seed_grid != 0, c->tdesc_h[t]);
-            CTX_CHECK(c, hipMemcpyAsync(c->tdesc.p + t, &c->tdesc_h[t], sizeof(TargetDesc), hipMemcpyHostToDevice,
-                                        c->stream));
+            CTX_CHECK(c, h2d(c->tdesc.p + t, &c->tdesc_h[t], sizeof(TargetDesc), c->stream));
         }
         CTX_CHECK(c, hipStreamSynchronize(c->stream));
     }
@@ -1756,15 +1760,15 @@ int orpcd_gicp_correspondences(orpcd_ctx* c, int32_t B, int32_t* idx_out) {
     CTX_CHECK(c, hipStreamSynchronize(c->stream));
     std::vector<int32_t> nn((size_t)B * N), sp((size_t)N);
     std::vector<std::vector<int32_t>> tp((size_t)kMaxTargets);
-    CTX_CHECK(c, hipMemcpy(nn.data(), c->prevnn.p, nn.size() * 4, hipMemcpyDeviceToHost));
-    CTX_CHECK(c, hipMemcpy(sp.data(), c->src.perm.p, sp.size() * 4, hipMemcpyDeviceToHost));
+    CTX_CHECK(c, d2h(nn.data(), c->prevnn.p, nn.size() * 4, c->stream));
+    CTX_CHECK(c, d2h(sp.data(), c->src.perm.p, sp.size() * 4, c->stream));
     for (int b = 0; b < B; ++b) {
         const int q = c->last_slot[b], k = c->last_slot_tgt[q];
         std::vector<int32_t>& perm = tp[k];
         const int64_t M = c->tgts[k].n;
         if (perm.empty()) {
             perm.resize((size_t)M);
-            CTX_CHECK(c, hipMemcpy(perm.data(), c->tgts[k].perm.p, (size_t)M * 4, hipMemcpyDeviceToHost));
+            CTX_CHECK(c, d2h(perm.data(), c->tgts[k].perm.p, (size_t)M * 4, c->stream));
         }
         for (int64_t i = 0; i < N; ++i) {  // Morton query i is source point sp[i]
             const int32_t j = nn[(size_t)q * N + i];
@@ -1783,10 +1787,10 @@ int orpcd_test_solve6(orpcd_ctx* c, const double* sums27, int32_t n, double* out
     double* dsum = c->scratch64c.p;
     double* dser = dsum + (size_t)n * 27;
     double* dwav = dser + (size_t)n * 23;
-    CTX_CHECK(c, hipMemcpyAsync(dsum, sums27, (size_t)n * 27 * 8, hipMemcpyHostToDevice, c->stream));
+    CTX_CHECK(c, h2d(dsum, sums27, (size_t)n * 27 * 8, c->stream));
     CTX_CHECK(c, launch_solve6_test(dsum, n, dser, dwav, c->stream));
-    CTX_CHECK(c, hipMemcpyAsync(out_serial, dser, (size_t)n * 23 * 8, hipMemcpyDeviceToHost, c->stream));
-    CTX_CHECK(c, hipMemcpyAsync(out_wave, dwav, (size_t)n * 23 * 8, hipMemcpyDeviceToHost, c->stream));
+    CTX_CHECK(c, d2h(out_serial, dser, (size_t)n * 23 * 8, c->stream));
+    CTX_CHECK(c, d2h(out_wave, dwav, (size_t)n * 23 * 8, c->stream));
     CTX_CHECK(c, hipStreamSynchronize(c->stream));
     return ORPCD_OK;
 }
