@@ -242,6 +242,18 @@ int main() {
             }
             hipMemcpy(v == 0 ? o1.data() : o2.data(), dout, o1.size() * 4, hipMemcpyDeviceToHost);
         }
+        if (getenv("SCAN_DUMP")) {  // inputs and both variants' keys for a CPU check
+            char fn[256];
+            snprintf(fn, sizeof fn, "%s_nq%d.bin", getenv("SCAN_DUMP"), nq);
+            if (FILE* f = fopen(fn, "wb")) {
+                fwrite(tg.data(), 16, tg.size(), f);
+                fwrite(cen.data(), 16, cen.size(), f);
+                fwrite(qs.data(), 16, qs.size(), f);
+                fwrite(o1.data(), 4, o1.size(), f);
+                fwrite(o2.data(), 4, o2.size(), f);
+                fclose(f);
+            }
+        }
         // same minimum keys (tile-local index bits) for most queries: the two
         // distance forms round differently, so a few near-ties may differ
         int same = 0, tot = 0;
