@@ -266,7 +266,7 @@ __device__ __forceinline__ int culled_search(float4* stage, const float4* __rest
     float lb = inf;
     float4 a = make_float4(0.f, 0.f, 0.f, 0.f), b = a;
 #ifdef ORPCD_PHASES
-    unsigned long long ph_cull = 0, ph_rounds = 0, ph_tests = 0, ph_impr = 0, ph_need = 0;
+    unsigned long long ph_cull = 0, ph_rounds = 0, ph_tests = 0, ph_impr = 0, ph_need = 0, ph_staged = 0;
 #endif
     // the tile AABBs of the NEXT round are loaded while the current round is
     // tested and scanned (one round of load latency hidden).  A round holds
@@ -409,6 +409,9 @@ __device__ __forceinline__ int culled_search(float4* stage, const float4* __rest
     }
     while (nxt >= 0) {
         const int tile = __builtin_amdgcn_readfirstlane(nxt);
+#ifdef ORPCD_PHASES
+        ++ph_staged;
+#endif
         // SoA stage: x[64] | y[64] | z[64] | quarter boxes (lo x4, hi x4); a
         // ds_read_b64 yields two targets' coordinate, already an aligned
         // register pair for v_pk_* math
@@ -569,6 +572,7 @@ __device__ __forceinline__ int culled_search(float4* stage, const float4* __rest
         phase_cull_out[2] = ph_tests;
         phase_cull_out[3] = ph_impr;
         phase_cull_out[4] = ph_need;
+        phase_cull_out[5] = ph_staged;
     }
 #endif
     return visited;
@@ -865,7 +869,7 @@ __device__ __forceinline__ int search_group(const float4* __restrict__ q32, int 
 #ifdef ORPCD_PHASES
     const float wq = __uint_as_float(wave_umax(__float_as_uint(qx[0] + qy[1])));  // the query loads have landed
     const unsigned long long ph_t1 = __builtin_readcyclecounter() + (wq == 1.2345f ? 1 : 0);
-    unsigned long long ph_cull[5] = {0, 0, 0, 0, 0};
+    unsigned long long ph_cull[6] = {0, 0, 0, 0, 0, 0};
     const int visited = culled_search<true>(stage_w, tg.p4, tg.tlo, tg.thi, tg.qbox, tg.ntiles, tg.slo, tg.shi,
                                             tg.nsuper, super_cull, S, split, qx, qy, qz, bound, bd, bj, s0lo, s0hi,
                                             gb, ph_cull);
@@ -888,6 +892,7 @@ __device__ __forceinline__ int search_group(const float4* __restrict__ q32, int 
         atomicAdd(cs + 5, 1ull);            // waves
         atomicAdd(cs + 8, ph_cull[3]);      // scanned tiles that improved some query of the wave
         atomicAdd(cs + 9, ph_cull[4]);      // queries whose own box test wanted the candidate tile
+        atomicAdd(cs + 10, ph_cull[5]);     // tiles staged (and their quarters tested)
 #endif
     }
     unsigned long long* out = best + (size_t)slot * N;

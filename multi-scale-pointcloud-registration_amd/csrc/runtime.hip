@@ -1211,9 +1211,9 @@ int run_passes(orpcd_ctx* c, int B, const orpcd_gicp_params* p, double* T_out, d
                     if (getenv("ORPCD_PHASES")) {  // libraries built with -DORPCD_PHASES
                         std::vector<unsigned long long> h((size_t)kCounterSlots * kCounterStride);
                         CTX_CHECK(c, d2h(h.data(), c->counters.p, h.size() * 8, c->stream));
-                        unsigned long long ph[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+                        unsigned long long ph[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
                         for (int q = 0; q < kCounterSlots; ++q)
-                            for (int f = 0; f < 8; ++f) {
+                            for (int f = 0; f < 9; ++f) {
                                 ph[f] += h[(size_t)q * kCounterStride + 2 + f];
                                 h[(size_t)q * kCounterStride + 2 + f] = 0;
                             }
@@ -1221,8 +1221,9 @@ int run_passes(orpcd_ctx* c, int B, const orpcd_gicp_params* p, double* T_out, d
                         const double w = ph[3] > 0 ? (double)ph[3] : 1.0;
                         fprintf(stderr, "[orpcd]   waves %llu cycles/wave: query load %.0f  search %.0f (culling %.0f)"
                                 "  per wave: AABB rounds %.2f candidate tests %.2f improving tiles %.2f"
-                                " queries wanting a returned candidate %.2f\n",
-                                ph[3], ph[0] / w, ph[2] / w, ph[1] / w, ph[4] / w, ph[5] / w, ph[6] / w, ph[7] / w);
+                                " queries wanting a returned candidate %.2f tiles staged %.2f\n",
+                                ph[3], ph[0] / w, ph[2] / w, ph[1] / w, ph[4] / w, ph[5] / w, ph[6] / w, ph[7] / w,
+                                ph[8] / w);
                     }
                 }
             }
