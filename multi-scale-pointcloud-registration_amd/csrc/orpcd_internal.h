@@ -15,8 +15,12 @@ namespace orpcd {
 // ------------------------------------------------------------- geometry
 constexpr int kTile = 64;                      // targets per culling tile (one wave-wide load)
 constexpr int kSuper = 64;                     // tiles per super-tile (first culling level)
+// 8-point in-tile boxes since round 4 (with the clamped box distance of
+// box_d2_2q): C2 exact 30 starts 16.13 -> 15.88 ms, fp32 mode 13.38 -> 13.21,
+// C5 search 0.216 ms either way with 23% fewer pairs scanned; identical
+// results (profiles/r04_box_med3_ab.log).  16: round 3's boxes.
 #ifndef ORPCD_QUARTER
-#define ORPCD_QUARTER 16
+#define ORPCD_QUARTER 8
 #endif
 constexpr int kQuarter = ORPCD_QUARTER;        // targets per tile quarter (per-query test inside a staged tile)
 constexpr int kNQ = kTile / kQuarter;          // quarters per tile (their boxes: qbox[2 kNQ t + k] lo, [.. + kNQ + k] hi)

@@ -57,7 +57,7 @@ __global__ void gather_points_kernel(const double* __restrict__ in64, const int3
 
 // One thread per 64-point tile: fp32 AABB over the tile's real points, and
 // the AABBs of its kNQ kQuarter-point quarters (qbox[2 kNQ t + k] = lo of quarter k,
-// qbox[2 kNQ t + kNQ + k] = hi; a quarter without real points gets an empty box).
+// qbox[2 kNQ t + kNQ + k] = hi; a quarter without real points gets a point box at 3e38).
 __global__ void tile_aabb_kernel(const float4* __restrict__ p4, int n, int ntiles, float4* __restrict__ lo,
                                  float4* __restrict__ hi, float4* __restrict__ qbox) {
     const int t = blockIdx.x * blockDim.x + threadIdx.x;
@@ -75,8 +75,11 @@ __global__ void tile_aabb_kernel(const float4* __restrict__ p4, int n, int ntile
             by = fmaxf(by, p.y);
             bz = fmaxf(bz, p.z);
         }
-        qbox[2 * kNQ * (size_t)t + q] = make_float4(ax, ay, az, 0.f);
-        qbox[2 * kNQ * (size_t)t + kNQ + q] = make_float4(bx, by, bz, 0.f);
+        // a quarter without points: the point box (3e38, 3e38, 3e38), whose
+        // clamped distance (box_d2_2q) overflows to inf for any query
+        const bool empty = end <= beg;
+        qbox[2 * kNQ * (size_t)t + q] = empty ? make_float4(3.0e38f, 3.0e38f, 3.0e38f, 0.f) : make_float4(ax, ay, az, 0.f);
+        qbox[2 * kNQ * (size_t)t + kNQ + q] = empty ? make_float4(3.0e38f, 3.0e38f, 3.0e38f, 0.f) : make_float4(bx, by, bz, 0.f);
         mnx = fminf(mnx, ax);
         mny = fminf(mny, ay);
         mnz = fminf(mnz, az);
