@@ -1,6 +1,6 @@
 """Summarise rocprofv3 CSV output into profiles/ (committed evidence).
 
-    python tools/summarize_profile.py --round r01 --kt DIR [--fetch DIR] [--write DIR] [--pmc DIR ...]
+    python tools/summarize_profile.py --round r01 --kt DIR [--fetch DIR] [--write DIR] [--pmc DIR ...] [--out-dir D]
 
 Writes profiles/<round>_kernel_stats.csv (rocprofv3 --kernel-trace --stats),
 profiles/<round>_hbm.json (per-kernel FETCH_SIZE / WRITE_SIZE per launch with
@@ -52,8 +52,10 @@ def main():
     ap.add_argument("--fetch")
     ap.add_argument("--write")
     ap.add_argument("--pmc", nargs="*", default=[])
+    ap.add_argument("--out-dir", default=os.path.join(REPO, "profiles"),
+                    help="where the summaries go (on the GPU box: under gpurun_out/, so they come back)")
     a = ap.parse_args()
-    prof = os.path.join(REPO, "profiles")
+    prof = a.out_dir
     os.makedirs(prof, exist_ok=True)
     stats = newest_run(glob.glob(os.path.join(a.kt, "**", "*kernel_stats.csv"), recursive=True))[0]
     shutil.copy(stats, os.path.join(prof, f"{a.round}_kernel_stats.csv"))
