@@ -97,7 +97,13 @@ constexpr unsigned long long kNone = ~0ull;
 constexpr int kNoSeed = -1;   // prevnn before the first pass (representative seed)
 constexpr int kNoMatch = -2;  // no target within the search radius last pass
 constexpr unsigned kKeyMask = 0xFFFFFFC0u;  // d^2 bits kept in a scan key (low 6 = tile-local index)
-constexpr float kQuarterSlack = 1.0f - 1.0f / 1048576.0f;  // quarter test: box d^2 x (1 - 2^-20) vs the bound
+// quarter test: box d^2 < bound x (1 + 2^-19), i.e. box d^2 x (1 - 2^-20) <
+// bound with the factor moved onto the bound (b (1 + 2^-19) rounded to fp32
+// is >= b / (1 - 2^-20), so every quarter the round-3 form scanned is still
+// scanned; a few more may be, which cannot change a result: their keys lie
+// above the bound).  Exact mode widens the band once per improving tile
+// instead of multiplying every box d^2.
+constexpr float kQuarterWiden = 1.0f + 1.0f / 524288.0f;
 
 // A load through a pointer the compiler cannot prove global (one read from a
 // TargetDesc): as a global load, not a flat one -- flat loads count against
@@ -240,6 +246,7 @@ __device__ __forceinline__ int culled_search(float4* stage, const float4* __rest
     // exact: each query's culling bound, band_hi of its best key (the sentinel
     // before it has one): every candidate within the band is scanned
     float e0 = kExact && v0 ? bound[0] : 0.0f, e1 = kExact && v1 ? bound[1] : 0.0f;
+    f2 ew = f2{e0, e1} * f2{kQuarterWiden, kQuarterWiden};  // exact: the quarter tests' bounds
     if constexpr (kGBox) {
         const float4 g0 = gbox[0], g1 = gbox[1];
         // wave-uniform: scalar registers (the record is one address for every lane)
@@ -442,14 +449,16 @@ __device__ __forceinline__ int culled_search(float4* stage, const float4* __rest
         for (int qd = 0; qd < kTile / kQuarter; ++qd) {
             // a quarter is scanned only if some query's box distance to it is
             // below that query's bound (including this tile's earlier
-            // quarters); the 2^-20 slack keeps the test conservative against
-            // the scan's own fp32 rounding
+            // quarters); the bound widened by 2^-19 (kQuarterWiden) keeps the
+            // test conservative against the scan's own fp32 rounding
             const float4 lo = qb[qd], hi = qb[kNQ + qd];
-            const float b0 = kExact ? e0 : __uint_as_float((k0 < m0 ? k0 : m0) & kKeyMask);
-            const float b1 = kExact ? e1 : __uint_as_float((k1 < m1 ? k1 : m1) & kKeyMask);
+            const f2 bw = kExact ? ew
+                                 : f2{__uint_as_float((k0 < m0 ? k0 : m0) & kKeyMask),
+                                      __uint_as_float((k1 < m1 ? k1 : m1) & kKeyMask)} *
+                                       f2{kQuarterWiden, kQuarterWiden};
             const f2 qd2 = box_d2_2q(f2{qx[0], qx[1]}, f2{qy[0], qy[1]}, f2{qz[0], qz[1]}, lo.x, lo.y, lo.z, hi.x,
                                      hi.y, hi.z);
-            const bool need = qd2.x * kQuarterSlack < b0 || qd2.y * kQuarterSlack < b1;
+            const bool need = qd2.x < bw.x || qd2.y < bw.y;
             if (!__any(need)) continue;
             ++visited;
             f2 ntx, nty, ntz;
@@ -532,6 +541,7 @@ __device__ __forceinline__ int culled_search(float4* stage, const float4* __rest
                 t1 = tile;
                 e1 = exact_band_hi(__uint_as_float(k1 & kKeyMask), qnorm(qx[1], qy[1], qz[1]));
             }
+            ew = f2{e0, e1} * f2{kQuarterWiden, kQuarterWiden};
         } else {
             if ((m0 & kKeyMask) < (k0 & kKeyMask)) {
                 k0 = m0;
