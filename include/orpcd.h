@@ -73,6 +73,11 @@ typedef enum {
 typedef struct orpcd_ctx orpcd_ctx;
 
 int orpcd_abi_version(void);
+/* sha256 (16 hex) of the sources the library was built from, and the extra
+ * compile flags of an instrumented variant ("" for the product build); the
+ * Python binding refuses a library whose id differs from the sources beside it */
+const char* orpcd_build_id(void);
+const char* orpcd_build_flags(void);
 int orpcd_device_count(int* count);
 int orpcd_ctx_create(int device, orpcd_ctx** out);
 int orpcd_ctx_destroy(orpcd_ctx* ctx);

@@ -9,6 +9,7 @@ The .so is git-ignored but travels to the GPU box with the snapshot.
 from __future__ import annotations
 
 import glob
+import hashlib
 import os
 import subprocess
 import sys
@@ -29,6 +30,41 @@ CXXFLAGS = EXTRA + ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-Wa
 
 def _headers():
     return glob.glob(os.path.join(CSRC, "*.h")) + glob.glob(os.path.join(REPO, "include", "*.h"))
+
+
+def source_id() -> str:
+    """sha256 (first 16 hex) over every source the library is built from
+    (csrc/*.hip, csrc/*.h, include/*.h, by name and content).  The library
+    embeds it (orpcd_build_id) and orpcd_amd._native refuses a library whose
+    id differs from the sources beside it: a stale prebuilt .so fails loudly."""
+    h = hashlib.sha256()
+    files = sorted(glob.glob(os.path.join(CSRC, "*.hip")) + glob.glob(os.path.join(CSRC, "*.h"))
+                   + glob.glob(os.path.join(REPO, "include", "*.h")))
+    for f in files:
+        h.update(os.path.basename(f).encode() + b"\0")
+        with open(f, "rb") as fh:
+            h.update(fh.read())
+        h.update(b"\0")
+    return h.hexdigest()[:16]
+
+
+def _build_id_object(force):
+    """A one-function host unit returning the source id and the extra flags."""
+    sid = source_id()
+    flags = " ".join(EXTRA)
+    src = os.path.join(OBJ_DIR, "build_id.cpp")
+    text = (f'extern "C" const char* orpcd_build_id(void) {{ return "{sid}"; }}\n'
+            f'extern "C" const char* orpcd_build_flags(void) {{ return "{flags}"; }}\n')
+    old = open(src).read() if os.path.exists(src) else None
+    if old != text:
+        with open(src, "w") as fh:
+            fh.write(text)
+    obj = src + ".o"
+    if force or _stale(obj, [src]):
+        r = subprocess.run([HIPCC, "-O2", "-fPIC", "-c", "-x", "c++", src, "-o", obj], capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError(f"hipcc failed on build_id.cpp:\n{r.stdout}\n{r.stderr}")
+    return obj
 
 
 def _stale(target, deps):
@@ -58,6 +94,7 @@ def build(force: bool = False, verbose: bool = False) -> str:
     srcs = sorted(glob.glob(os.path.join(CSRC, "*.hip")))
     with ThreadPoolExecutor(max_workers=min(8, len(srcs))) as ex:
         objs = list(ex.map(lambda s: _compile(s, force), srcs))
+    objs.append(_build_id_object(force))
     if force or _stale(LIB, objs):
         cmd = [HIPCC, "-shared", f"--offload-arch={ARCH}", "-fPIC", "-o", LIB] + objs
         r = subprocess.run(cmd, capture_output=True, text=True)

@@ -72,3 +72,32 @@ def test_product_package_never_imports_the_oracle():
             if f.endswith((".py", ".hip", ".h", ".cpp")):
                 text = open(os.path.join(root, f)).read()
                 assert "import oracle" not in text and "liborpcd_oracle" not in text, f
+
+
+def test_library_was_built_from_these_sources():
+    """The shipped .so embeds the sha256 of csrc/ + include/ (orpcd_build_id);
+    the binding compares it with the tree, so a stale prebuilt library cannot
+    run silently on the GPU box."""
+    import importlib.util
+    from orpcd_amd import _native
+    if "ORPCD_HIP_LIB" in os.environ:
+        pytest.skip("a variant library is selected")
+    spec = importlib.util.spec_from_file_location(
+        "bn", os.path.join(REPO, "multi-scale-pointcloud-registration_amd", "build_native.py"))
+    bn = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(bn)
+    sid, flags = _native.build_id()
+    assert sid == bn.source_id() and flags == ""
+
+
+def test_stale_library_is_refused(monkeypatch):
+    from orpcd_amd import _native
+
+    class Stale:
+        @staticmethod
+        def orpcd_build_id():
+            return b"0000000000000000"
+
+    monkeypatch.delenv("ORPCD_HIP_LIB", raising=False)
+    with pytest.raises(_native.NativeError, match="built from other sources"):
+        _native._check_build_id(Stale)
