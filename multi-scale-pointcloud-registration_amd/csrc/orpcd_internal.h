@@ -103,12 +103,14 @@ struct HostBuf {  // pinned
 // passes do not start.  The reference-shaped drop-in loop (a 1.2 MB posed copy
 // allocated and freed per attempt) hit it in most processes: a 30-start batch
 // took 31-47 ms instead of 15.7 ms.  With staged copies no host page of the
-// caller is ever known to the GPU.
+// caller is ever known to the GPU.  A thread pins at most kStageChunk bytes;
+// larger copies go through it in chunks.
 struct Staging {
     HostBuf<unsigned char> buf;
     hipEvent_t ev = nullptr;  // recorded after the last staged host -> device copy
     bool pending = false;     // that copy may still be reading buf
 };
+constexpr size_t kStageChunk = (size_t)32 << 20;  // pinned bytes per thread at most; larger copies go in chunks
 inline Staging& staging() {
     thread_local Staging st;
     return st;
@@ -119,60 +121,81 @@ inline hipError_t staging_reserve(Staging& st, size_t bytes) {
         if ((e = hipEventSynchronize(st.ev)) != hipSuccess) return e;
         st.pending = false;
     }
-    if (bytes > st.buf.n) e = st.buf.ensure(std::max(bytes, 2 * st.buf.n));  // geometric: few re-pins
+    if (bytes > st.buf.n) e = st.buf.ensure(std::min(kStageChunk, std::max(bytes, 2 * st.buf.n)));  // few re-pins
     return e;
 }
-// host -> device, asynchronous on s (src may be reused as soon as this returns)
-inline hipError_t h2d(void* dst, const void* src, size_t bytes, hipStream_t s) {
-    if (bytes == 0) return hipSuccess;
-    Staging& st = staging();
-    hipError_t e = staging_reserve(st, bytes);
-    if (e != hipSuccess) return e;
-    std::memcpy(st.buf.p, src, bytes);
-    if ((e = hipMemcpyAsync(dst, st.buf.p, bytes, hipMemcpyHostToDevice, s)) != hipSuccess) return e;
+inline hipError_t staging_mark(Staging& st, hipStream_t s) {
+    hipError_t e = hipSuccess;
     if (!st.ev && (e = hipEventCreateWithFlags(&st.ev, hipEventDisableTiming)) != hipSuccess) return e;
     if ((e = hipEventRecord(st.ev, s)) != hipSuccess) return e;
     st.pending = true;
+    return hipSuccess;
+}
+// host -> device, asynchronous on s (src may be reused as soon as this returns)
+inline hipError_t h2d(void* dst, const void* src, size_t bytes, hipStream_t s) {
+    Staging& st = staging();
+    for (size_t off = 0; off < bytes; off += kStageChunk) {
+        const size_t n = std::min(kStageChunk, bytes - off);
+        hipError_t e = staging_reserve(st, n);
+        if (e != hipSuccess) return e;
+        std::memcpy(st.buf.p, static_cast<const unsigned char*>(src) + off, n);
+        if ((e = hipMemcpyAsync(static_cast<unsigned char*>(dst) + off, st.buf.p, n, hipMemcpyHostToDevice, s)) !=
+            hipSuccess)
+            return e;
+        if ((e = staging_mark(st, s)) != hipSuccess) return e;
+    }
     return hipSuccess;
 }
 // the same for a strided block: `rows` rows of `width` bytes, pitches in bytes
 inline hipError_t h2d_2d(void* dst, size_t dpitch, const void* src, size_t spitch, size_t width, size_t rows,
                          hipStream_t s) {
-    if (width == 0 || rows == 0) return hipSuccess;
+    if (width == 0) return hipSuccess;
     Staging& st = staging();
-    hipError_t e = staging_reserve(st, width * rows);
-    if (e != hipSuccess) return e;
-    for (size_t r = 0; r < rows; ++r)
-        std::memcpy(st.buf.p + r * width, static_cast<const unsigned char*>(src) + r * spitch, width);
-    e = hipMemcpy2DAsync(dst, dpitch, st.buf.p, width, width, rows, hipMemcpyHostToDevice, s);
-    if (e != hipSuccess) return e;
-    if (!st.ev && (e = hipEventCreateWithFlags(&st.ev, hipEventDisableTiming)) != hipSuccess) return e;
-    if ((e = hipEventRecord(st.ev, s)) != hipSuccess) return e;
-    st.pending = true;
+    const size_t per = std::max<size_t>(1, kStageChunk / width);  // rows per chunk
+    for (size_t r0 = 0; r0 < rows; r0 += per) {
+        const size_t nr = std::min(per, rows - r0);
+        hipError_t e = staging_reserve(st, width * nr);
+        if (e != hipSuccess) return e;
+        for (size_t r = 0; r < nr; ++r)
+            std::memcpy(st.buf.p + r * width, static_cast<const unsigned char*>(src) + (r0 + r) * spitch, width);
+        e = hipMemcpy2DAsync(static_cast<unsigned char*>(dst) + r0 * dpitch, dpitch, st.buf.p, width, width, nr,
+                             hipMemcpyHostToDevice, s);
+        if (e != hipSuccess) return e;
+        if ((e = staging_mark(st, s)) != hipSuccess) return e;
+    }
     return hipSuccess;
 }
 // device -> host after everything enqueued on s: returns with dst written
 inline hipError_t d2h(void* dst, const void* src, size_t bytes, hipStream_t s) {
-    if (bytes == 0) return hipSuccess;
     Staging& st = staging();
-    hipError_t e = staging_reserve(st, bytes);
-    if (e != hipSuccess) return e;
-    if ((e = hipMemcpyAsync(st.buf.p, src, bytes, hipMemcpyDeviceToHost, s)) != hipSuccess) return e;
-    if ((e = hipStreamSynchronize(s)) != hipSuccess) return e;
-    std::memcpy(dst, st.buf.p, bytes);
+    for (size_t off = 0; off < bytes; off += kStageChunk) {
+        const size_t n = std::min(kStageChunk, bytes - off);
+        hipError_t e = staging_reserve(st, n);
+        if (e != hipSuccess) return e;
+        if ((e = hipMemcpyAsync(st.buf.p, static_cast<const unsigned char*>(src) + off, n, hipMemcpyDeviceToHost,
+                                s)) != hipSuccess)
+            return e;
+        if ((e = hipStreamSynchronize(s)) != hipSuccess) return e;
+        std::memcpy(static_cast<unsigned char*>(dst) + off, st.buf.p, n);
+    }
     return hipSuccess;
 }
 inline hipError_t d2h_2d(void* dst, size_t dpitch, const void* src, size_t spitch, size_t width, size_t rows,
                          hipStream_t s) {
-    if (width == 0 || rows == 0) return hipSuccess;
+    if (width == 0) return hipSuccess;
     Staging& st = staging();
-    hipError_t e = staging_reserve(st, width * rows);
-    if (e != hipSuccess) return e;
-    e = hipMemcpy2DAsync(st.buf.p, width, src, spitch, width, rows, hipMemcpyDeviceToHost, s);
-    if (e != hipSuccess) return e;
-    if ((e = hipStreamSynchronize(s)) != hipSuccess) return e;
-    for (size_t r = 0; r < rows; ++r)
-        std::memcpy(static_cast<unsigned char*>(dst) + r * dpitch, st.buf.p + r * width, width);
+    const size_t per = std::max<size_t>(1, kStageChunk / width);
+    for (size_t r0 = 0; r0 < rows; r0 += per) {
+        const size_t nr = std::min(per, rows - r0);
+        hipError_t e = staging_reserve(st, width * nr);
+        if (e != hipSuccess) return e;
+        e = hipMemcpy2DAsync(st.buf.p, width, static_cast<const unsigned char*>(src) + r0 * spitch, spitch, width, nr,
+                             hipMemcpyDeviceToHost, s);
+        if (e != hipSuccess) return e;
+        if ((e = hipStreamSynchronize(s)) != hipSuccess) return e;
+        for (size_t r = 0; r < nr; ++r)
+            std::memcpy(static_cast<unsigned char*>(dst) + (r0 + r) * dpitch, st.buf.p + r * width, width);
+    }
     return hipSuccess;
 }
 
