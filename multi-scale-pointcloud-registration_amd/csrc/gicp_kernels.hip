@@ -52,11 +52,6 @@
 #ifndef ORPCD_CULL_PRIO
 #define ORPCD_CULL_PRIO 3
 #endif
-// 1: the 6x6 LDLT solve is computed beside the determinant test instead of
-// after it (A/B variant; same results)
-#ifndef ORPCD_SOLVE_SPEC
-#define ORPCD_SOLVE_SPEC 0
-#endif
 
 namespace orpcd {
 
@@ -1464,20 +1459,8 @@ __device__ bool solve_start(int slot, const double s[kNacc], int64_t N, int pass
         double row[6], b[6];
         sym6_row(s, lane, row);
         for (int r = 0; r < 6; ++r) b[r] = -s[21 + r];
-#if ORPCD_SOLVE_SPEC
-        // the LDLT solve does not depend on the determinant: both chains in
-        // one basic block, the solution kept only if the determinant passes
-        double JTJs[36], xs[6];
-        for (int i = 0, k = 0; i < 6; ++i)
-            for (int j = i; j < 6; ++j, ++k) JTJs[6 * i + j] = JTJs[6 * j + i] = s[k];
-        ldlt_solve6(JTJs, b, xs);
-        const double det = det6_wave(row, lane);
-        if (!(fabs(det) < 1e-6 || isnan(det) || isinf(det))) vec6_to_m4_wave(xs, upd, lane);
-        if (false) {
-#else
         const double det = det6_wave(row, lane);
         if (!(fabs(det) < 1e-6 || isnan(det) || isinf(det))) {
-#endif
             // LDLT as the single-lane routine on every lane (uniform values):
             // 6.5k cycles against 8.7k for ldlt_solve6_wave, whose readlane
             // chains outweigh the row parallelism (tools/solve_bench.hip);
