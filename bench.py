@@ -229,6 +229,9 @@ def main():
                              "achieved_ginst_s": round(valu_insts / (avg_ms * 1e-3) / 1e9, 1),
                              "peak_ginst_s": VALU_ISSUE_PEAK_GINST,
                              "frac": round(valu_insts / (avg_ms * 1e-3) / 1e9 / VALU_ISSUE_PEAK_GINST, 3)},
+                         "note": "achieved = 8 FLOP x pairs the culled search evaluates; it falls whenever "
+                                 "culling improves (round 4's 8-point in-tile boxes: 39% fewer pairs per "
+                                 "launch in a 4% shorter launch), so valu_issue.frac is the binding roof",
                          "kernel": kname, "avg_launch_ms": round(avg_ms, 4),
                          "search_kernel_ms_total": round(st["ms"], 3),
                          "launches": int(st["launches"]), "flop_per_pair": FLOP_PER_PAIR,
