@@ -1,3 +1,5 @@
+# Historical: the sync_lag option this A/B drives was measured (profiles/r04_sync_lag_ab.log) and
+# removed from the library; DESIGN.md §5 (round 4) has the numbers.
 # Lagged host syncs (option sync_lag) against drained ones: C2 exact 30 / 8
 # starts and fp32 mode 30 starts, interleaved; result hashes must match.
 #   bash tools/lag_ab.sh [tag]   (on the GPU box)

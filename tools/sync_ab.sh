@@ -1,3 +1,5 @@
+# Historical: the sync_lag option this A/B drives was measured (profiles/r04_sync_lag_ab.log) and
+# removed from the library; DESIGN.md §5 (round 4) has the numbers.
 # Host-sync variants of the pass loop: the previous library (abl/base.so:
 # drained syncs with a done-flag copy per sync) against this tree drained
 # (sync_lag 0) and lagged (sync_lag 1), both with the mapped done flags.
