@@ -1,5 +1,5 @@
 # One round's GPU evidence: bench line, rocprofv3 kernel stats + HBM/SQ counter
-# passes of the bench command, and the side workloads (C3 FGR, C4 align(), C5, prep).
+# passes of the bench command, and the side workloads (C3 FGR, C4 align(), C5, prep, C1, drop-in).
 #   bash tools/profile_round.sh [round]   (on the GPU box; outputs under gpurun_out/)
 # The raw rocprofv3 CSVs are summarised on the box (tools/summarize_profile.py
 # --out-dir gpurun_out/summary) and then deleted: gpurun brings back at most
@@ -32,6 +32,8 @@ step c5
 timeout -k 10 400 python3 tools/bench_c5.py --out gpurun_out/c5.json > gpurun_out/c5.log 2>&1
 step prep
 timeout -k 10 300 python3 tools/bench_prep.py --out gpurun_out/prep.json > gpurun_out/prep.log 2>&1
+step c1
+timeout -k 10 300 python3 tools/bench_c1.py --out gpurun_out/c1.json > gpurun_out/c1.log 2>&1
 step dropin
 timeout -k 10 300 python3 tools/bench_dropin.py --reps 5 --out gpurun_out/dropin.json > gpurun_out/dropin.log 2>&1
 step done
