@@ -157,8 +157,11 @@ def load_library():
         L.orpcd_pose_rows.argtypes = [_f64p, vp, c_i64, _f64p, _f64p, _f64p]
         if L.orpcd_abi_version() != 1:
             raise NativeError("liborpcd_hip.so ABI mismatch")
-        L.orpcd_build_id.restype = ctypes.c_char_p
-        L.orpcd_build_flags.restype = ctypes.c_char_p
+        if hasattr(L, "orpcd_build_id"):
+            L.orpcd_build_id.restype = ctypes.c_char_p
+            L.orpcd_build_flags.restype = ctypes.c_char_p
+        elif "ORPCD_HIP_LIB" not in os.environ:  # a variant built from an older commit may predate it
+            raise NativeError(f"{LIB_PATH} has no orpcd_build_id: stale library; rebuild it")
         _check_build_id(L)
         _lib = L
         return L

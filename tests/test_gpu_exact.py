@@ -276,3 +276,32 @@ def test_exact_tiny_clouds_and_iteration_caps(exact, oracle):
     o = oracle.gicp(src, tgt[:7], 0.5, 5)
     assert r["iters"][0] == o["iters"] and np.abs(r["T"][0] - o["T"]).max() <= 1e-9
     assert abs(r["rmse"][0] - o["rmse"]) <= 1e-12
+
+
+@pytest.mark.parametrize("m", [1, 7, 8, 9, 63, 64, 65, 71, 127, 129, 4095, 4097])
+def test_exact_correspondences_ragged_target_sizes(exact, oracle, m):
+    """Every partial-tile shape of the in-tile boxes (8 points since round 4;
+    a box without points is stored as the point (3e38, 3e38, 3e38), see
+    tile_aabb_kernel): pass-0 correspondences index for index, exact and fp32
+    mode (the latter within its tie tolerance: the same d^2 to 2^-17)."""
+    rng = np.random.default_rng(m)
+    tgt = rng.normal(size=(m, 3)) * 0.3
+    src = rng.normal(size=(700, 3)) * 0.3
+    R0 = np.array([np.eye(3), rot_xyz(10, -20, 30)])
+    t0 = np.array([[0.0, 0.0, 0.0], [0.02, 0.01, -0.03]])
+    exact.set_target(tgt)
+    exact.set_source(src)
+    exact.gicp_batch(R0, t0, max_correspondence_distance=5.0, max_iteration=0)
+    _check_corr(exact, oracle, src, tgt, R0, t0, 5.0)
+    exact.set_option("exact_nn", 0)
+    try:
+        exact.gicp_batch(R0, t0, max_correspondence_distance=5.0, max_iteration=0)
+        g = exact.gicp_correspondences(2, len(src))
+        for b in range(2):
+            q = _posed(src, R0[b], t0[b])
+            oi, od2 = oracle.nn1_radius(q, tgt, 5.0)
+            assert np.all(g[b] >= 0)
+            d2 = ((q - tgt[g[b]]) ** 2).sum(1)
+            assert np.all(d2 <= od2 * (1 + 2e-5) + 1e-30)
+    finally:
+        exact.set_option("exact_nn", 1)
