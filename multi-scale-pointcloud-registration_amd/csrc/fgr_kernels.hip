@@ -177,12 +177,45 @@ __global__ void feat_norm_kernel(const double* __restrict__ F, int n, double* __
 // oracle gives, and the near-tie sets stay small.
 //
 // Tiling: one wave owns 64 queries as 4 column tiles of 16; the block stages
-// 64 targets x 36 in LDS.  D[i][j] = sum_k A[i][k] B[k][j] with A = 16 targets
-// (lane l supplies A[l&15][l>>4]) and B = 16 queries (lane l supplies
-// B[l>>4][l&15]); the f64 accumulator holds D[(l>>4) + 4r][l&15], r = 0..3.
-// blockIdx.y splits the targets into parts (merged by the merge kernels).
+// 64 targets x 36 in LDS.  D[i][j] = C[i][j] + sum_k A[i][k] B[k][j] with
+// A = 16 targets (lane l supplies A[l&15][l>>4]), B = -2 x 16 queries (lane l
+// supplies B[l>>4][l&15]; the scaling is exact) and C = |q_j|^2, so the f64
+// accumulator holds |q|^2 - 2 q.t at D[(l>>4) + 4r][l&15], r = 0..3, and a
+// distance costs one add.  blockIdx.y splits the targets into parts
+// (feat_nn_parts; merged by the merge kernels).  The accumulation order
+// differs from |t|^2 + |q|^2 - 2 q.t by rounding only, inside the flag bound.
 constexpr int kFT = 64;
-constexpr int kExactParts = 16;
+constexpr int kMaxParts = 32;  // target parts per launch (feat_nn_parts)
+// Padded target rows (past a part's end) carry this norm: their distances
+// are huge but finite, so a key built from one is never a NaN.
+constexpr double kPadNorm = 1e300;
+
+// Pass-1 key: the distance with its low `bits` mantissa bits replaced by the
+// target's index within the part (one v_bfi_b32).  Keys of distinct targets
+// differ, order as their distances up to 2^(bits-52) relative, and the
+// running best and runner-up become two minima and a maximum.
+__host__ __device__ inline int feat_key_bits(int part_len) {
+    int b = 1;
+    while ((1 << b) < part_len) ++b;
+    return b;
+}
+__device__ __forceinline__ double feat_key(double d, unsigned idx, unsigned mask) {
+    const unsigned lo = (unsigned)__double2loint(d);
+    return __hiloint2double(__double2hiint(d), (int)((lo & ~mask) | idx));
+}
+// v_min_f64 / v_max_f64 without the canonicalising moves the compiler adds for
+// fmin/fmax of values it cannot prove canonical (keys are built bitwise; no
+// operand is ever a NaN)
+__device__ __forceinline__ double vmin_f64(double a, double b) {
+    double r;
+    asm("v_min_f64 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
+__device__ __forceinline__ double vmax_f64(double a, double b) {
+    double r;
+    asm("v_max_f64 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
 
 // (d, i, s) <- merge with (od, oi, os): best distance, its lowest index, and
 // the runner-up distance (a tie at the best counts as a runner-up).
@@ -237,21 +270,24 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void f
         th[qt] = (EXACT && q >= 0) ? thr[q] : -1.0;
         qrow[qt] = Fq + (size_t)(q >= 0 ? q : 0) * kFD;
 #pragma unroll
-        for (int kb = 0; kb < 9; ++kb) b[qt][kb] = q >= 0 ? qrow[qt][4 * kb + (lane >> 4)] : 0.0;
+        for (int kb = 0; kb < 9; ++kb) b[qt][kb] = q >= 0 ? -2.0 * qrow[qt][4 * kb + (lane >> 4)] : 0.0;
     }
     const double inf = __builtin_huge_val();
     double bd[4] = {inf, inf, inf, inf}, b2[4] = {inf, inf, inf, inf};
     int bi[4] = {-1, -1, -1, -1};
     constexpr int kPer = kFT * kFD / 256;  // staged doubles per thread
     static_assert(kFT * kFD % 256 == 0, "stage split");
-    double pre[kPer], preN = inf;
+    double pre[kPer], preN = kPadNorm;
+    const unsigned kmask = (1u << feat_key_bits(part_len)) - 1u;
     auto load_stage = [&](int t0) {
 #pragma unroll
         for (int u = 0; u < kPer; ++u) {
+            // rows past the part's end re-read its last row (no branch per
+            // load): their distances are inf through sN, whatever the row
             const int e = threadIdx.x + 256 * u, r = e / kFD, col = e - r * kFD;
-            pre[u] = (t0 + r < t_end) ? Ft[(size_t)(t0 + r) * kFD + col] : 0.0;
+            pre[u] = Ft[(size_t)min(t0 + r, t_end - 1) * kFD + col];
         }
-        if (threadIdx.x < kFT) preN = (t0 + threadIdx.x < t_end) ? nt2[t0 + threadIdx.x] : inf;
+        if (threadIdx.x < kFT) preN = (t0 + threadIdx.x < t_end) ? nt2[t0 + threadIdx.x] : kPadNorm;
     };
     auto store_stage = [&](int buf) {
 #pragma unroll
@@ -268,14 +304,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void f
     __syncthreads();
     for (int t0 = t_begin, buf = 0; t0 < t_end; t0 += kFT, buf ^= 1) {
         const bool more = t0 + kFT < t_end;
-        if (more && !EXACT) load_stage(t0 + kFT);  // pass 2 holds too many registers to keep a stage in flight
+        if (more) load_stage(t0 + kFT);
         double(*sT)[kFD + 1] = sT2[buf];
         const double* sN = sN2[buf];
-#pragma unroll
+#pragma unroll 1
         for (int sub = 0; sub < kFT / 16; ++sub) {
             d4 acc[4];
 #pragma unroll
-            for (int qt = 0; qt < 4; ++qt) acc[qt] = d4{0.0, 0.0, 0.0, 0.0};
+            for (int qt = 0; qt < 4; ++qt) acc[qt] = d4{qn[qt], qn[qt], qn[qt], qn[qt]};
 #pragma unroll
             for (int kb = 0; kb < 9; ++kb) {
                 const double a = sT[sub * 16 + (lane & 15)][4 * kb + (lane >> 4)];
@@ -286,17 +322,17 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void f
             for (int r = 0; r < 4; ++r) {
                 const int row = sub * 16 + (lane >> 4) + 4 * r;
                 const double tn = sN[row];
+                const unsigned lidx = (unsigned)(t0 - t_begin + row);
 #pragma unroll
                 for (int qt = 0; qt < 4; ++qt) {
-                    const double d = tn + qn[qt] - 2.0 * acc[qt][r];
+                    const double d = tn + acc[qt][r];
                     if (!EXACT) {
-                        if (d < bd[qt]) {
-                            b2[qt] = bd[qt];
-                            bd[qt] = d;
-                            bi[qt] = t0 + row;
-                        } else if (d < b2[qt]) {
-                            b2[qt] = d;
-                        }
+                        // best and runner-up keys: five VALU per element, no
+                        // compare or select (the compare/select form cost 11
+                        // and held pass 1 at 9.3 ms against 8.2)
+                        const double key = feat_key(d, lidx, kmask);
+                        b2[qt] = vmin_f64(b2[qt], vmax_f64(bd[qt], key));
+                        bd[qt] = vmin_f64(bd[qt], key);
                     } else if (d <= th[qt]) {
                         double ex = 0.0;
                         {
@@ -316,19 +352,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void f
         }
         // the other buffer was last read in the previous stage, before the
         // barrier that ended it
-        if (more) {
-            if constexpr (EXACT) {  // straight into the other buffer
-                const int t1 = t0 + kFT;
-                for (int e = threadIdx.x; e < kFT * kFD; e += 256) {
-                    const int r = e / kFD, col = e - r * kFD;
-                    sT2[buf ^ 1][r][col] = (t1 + r < t_end) ? Ft[(size_t)(t1 + r) * kFD + col] : 0.0;
-                }
-                if (threadIdx.x < kFT) sN2[buf ^ 1][threadIdx.x] = (t1 + threadIdx.x < t_end) ? nt2[t1 + threadIdx.x] : inf;
-            } else {
-                store_stage(buf ^ 1);
-            }
-        }
+        if (more) store_stage(buf ^ 1);
         __syncthreads();
+    }
+    if (!EXACT) {
+#pragma unroll
+        for (int qt = 0; qt < 4; ++qt)
+            bi[qt] = bd[qt] < inf ? (int)((unsigned)__double2loint(bd[qt]) & kmask) + t_begin : -1;
     }
     // merge the 4 lane groups (l>>4) holding the same query column
 #pragma unroll
@@ -357,7 +387,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void f
 __global__ void merge_parts_kernel(const double* __restrict__ pd, const double* __restrict__ ps,
                                    const int32_t* __restrict__ pi, int nq, int nparts, const double* __restrict__ nq2,
                                    const double* __restrict__ nt2, const int32_t* __restrict__ tmap,
-                                   int32_t* __restrict__ out, int32_t* __restrict__ flag, double* __restrict__ thr) {
+                                   int32_t* __restrict__ out, int32_t* __restrict__ flag, double* __restrict__ thr,
+                                   double key_slack) {
     const int q = blockIdx.x * blockDim.x + threadIdx.x;
     if (q >= nq) return;
     double bd = pd[q], bs = ps[q];
@@ -365,7 +396,9 @@ __global__ void merge_parts_kernel(const double* __restrict__ pd, const double* 
     for (int p = 1; p < nparts; ++p)  // parts cover increasing target ranges
         merge_best(bd, bi, bs, pd[(size_t)p * nq + q], pi[(size_t)p * nq + q], ps[(size_t)p * nq + q]);
     out[q] = bi >= 0 && tmap ? tmap[bi] : bi;
-    const double tol = 2e-13 * (nq2[q] + (bi >= 0 ? nt2[bi] : 0.0) + fabs(bd));
+    // + the keys' perturbation (key_slack = 2^(bits-51): twice 2^(bits-52))
+    const double tol = 2e-13 * (nq2[q] + (bi >= 0 ? nt2[bi] : 0.0) + fabs(bd)) +
+                       key_slack * (fabs(bd) + (bs < __builtin_huge_val() ? fabs(bs) : 0.0));
     flag[q] = (bi >= 0 && bs - bd <= tol) ? 1 : 0;
     thr[q] = bd + 2.0 * tol;
 }
@@ -600,31 +633,57 @@ hipError_t launch_feat_norm(const double* F36, int64_t n, double* nrm2, hipStrea
     return hipGetLastError();
 }
 
-int feat_nn_parts(int64_t nq) {  // split targets so that ~8k waves run
-    const int64_t waves = (nq + 63) / 64;
-    return (int)std::min<int64_t>(16, std::max<int64_t>(1, 8192 / std::max<int64_t>(waves, 1)));
+// Target parts for a launch of `blocks` query blocks per part, in [1, maxp]
+// (at least 64 targets a part).  Every block of a launch runs the same number
+// of 64-target stages, so the launch takes ceil(parts * blocks / slots)
+// rounds of the device's resident block slots (2 four-wave blocks per CU at
+// the kernels' ~250 VGPRs), each of ceil(nt / parts / 64) stages plus about
+// two stages' worth of query loads and merges: the count minimising that
+// product wins (100k queries x 67k targets: 9 parts, 7 full rounds, where a
+// fixed 5 parts left the 4th of 4 rounds 18% idle).
+int feat_nn_parts(int64_t blocks, int64_t nt, int maxp) {
+    static int slots = 0;
+    if (slots == 0) {
+        int dev = 0, cus = 0;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+            cus = 256;
+        slots = 2 * cus;
+    }
+    const int64_t pmax = std::max<int64_t>(1, std::min<int64_t>(maxp, (nt + kFT - 1) / kFT));
+    int best = 1;
+    int64_t best_cost = INT64_MAX;
+    for (int64_t p = 1; p <= pmax; ++p) {
+        const int64_t rounds = (p * blocks + slots - 1) / slots;
+        const int64_t stages = ((nt + p - 1) / p + kFT - 1) / kFT + 2;
+        if (rounds * stages < best_cost) {
+            best_cost = rounds * stages;
+            best = (int)p;
+        }
+    }
+    return best;
 }
 
 hipError_t launch_feat_nn(const double* Fq, const double* nq2, int64_t nq, const double* Ft, const double* nt2,
                           int64_t nt, const int32_t* tmap, int dim, FeatNNBufs& b, int32_t* out, hipStream_t s) {
     if (nq <= 0) return hipSuccess;
     hipError_t e;
-    const int parts = feat_nn_parts(nq);
-    if ((e = b.part_d.ensure((size_t)2 * std::max(parts, kExactParts) * nq)) != hipSuccess) return e;
-    if ((e = b.part_i.ensure((size_t)std::max(parts, kExactParts) * nq)) != hipSuccess) return e;
+    const unsigned gq = (unsigned)((nq + 255) / 256);
+    const int parts = feat_nn_parts(gq, nt, kMaxParts);
+    if ((e = b.part_d.ensure((size_t)2 * kMaxParts * nq)) != hipSuccess) return e;
+    if ((e = b.part_i.ensure((size_t)kMaxParts * nq)) != hipSuccess) return e;
     if ((e = b.flag.ensure((size_t)nq)) != hipSuccess) return e;
     if ((e = b.qidx.ensure((size_t)nq + 1)) != hipSuccess) return e;
     if ((e = b.thr.ensure((size_t)nq)) != hipSuccess) return e;
-    double* part_s = b.part_d.p + (size_t)std::max(parts, kExactParts) * nq;
+    double* part_s = b.part_d.p + (size_t)kMaxParts * nq;
     int32_t* nsel = b.qidx.p + nq;
-    const unsigned gq = (unsigned)((nq + 255) / 256);
     const int len1 = (int)(((nt + parts - 1) / parts + kFT - 1) / kFT * kFT);
     feat_nn_kernel<false><<<dim3(gq, (unsigned)parts), 256, 0, s>>>(Fq, nq2, (int)nq, nullptr, nullptr, nullptr, Ft,
                                                                    nt2, (int)nt, len1, dim, b.part_d.p, part_s,
                                                                    b.part_i.p);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     merge_parts_kernel<<<gq, 256, 0, s>>>(b.part_d.p, part_s, b.part_i.p, (int)nq, parts, nq2, nt2, tmap, out,
-                                          b.flag.p, b.thr.p);
+                                          b.flag.p, b.thr.p, ldexp(1.0, feat_key_bits(len1) - 51));
     if ((e = hipGetLastError()) != hipSuccess) return e;
     size_t tmp = 0;
     if ((e = hipcub::DeviceSelect::Flagged(nullptr, tmp, hipcub::CountingInputIterator<int32_t>(0), b.flag.p,
@@ -634,19 +693,22 @@ hipError_t launch_feat_nn(const double* Fq, const double* nq2, int64_t nq, const
     if ((e = hipcub::DeviceSelect::Flagged(b.tmp.p, tmp, hipcub::CountingInputIterator<int32_t>(0), b.flag.p,
                                            b.qidx.p, nsel, (int)nq, s)) != hipSuccess)
         return e;
-    if (getenv("ORPCD_TRACE")) {
-        int32_t h = 0;
-        if ((e = d2h(&h, nsel, 4, s)) != hipSuccess) return e;
-        if ((e = hipStreamSynchronize(s)) != hipSuccess) return e;
-        fprintf(stderr, "[orpcd] feat_nn: %lld queries, %lld targets, %d parts, %d flagged for the exact pass\n",
-                (long long)nq, (long long)nt, parts, h);
-    }
-    const int len2 = (int)(((nt + kExactParts - 1) / kExactParts + kFT - 1) / kFT * kFT);
-    feat_nn_kernel<true><<<dim3(gq, (unsigned)kExactParts), 256, 0, s>>>(Fq, nq2, (int)nq, b.qidx.p, nsel, b.thr.p,
-                                                                        Ft, nt2, (int)nt, len2, dim, b.part_d.p,
-                                                                        nullptr, b.part_i.p);
+    // the flagged count sizes pass 2's grid and its parts (one 4-byte read;
+    // the stream drains here anyway before the caller reads the answers)
+    int32_t nflag = 0;
+    if ((e = d2h(&nflag, nsel, 4, s)) != hipSuccess) return e;
+    const unsigned g2 = (unsigned)((nflag + 255) / 256);
+    const int parts2 = nflag > 0 ? feat_nn_parts(g2, nt, kMaxParts) : 0;
+    if (getenv("ORPCD_TRACE"))
+        fprintf(stderr, "[orpcd] feat_nn: %lld queries, %lld targets, %d parts, %d flagged for the exact pass (%d parts)\n",
+                (long long)nq, (long long)nt, parts, nflag, parts2);
+    if (nflag == 0) return hipSuccess;
+    const int len2 = (int)(((nt + parts2 - 1) / parts2 + kFT - 1) / kFT * kFT);
+    feat_nn_kernel<true><<<dim3(g2, (unsigned)parts2), 256, 0, s>>>(Fq, nq2, (int)nq, b.qidx.p, nsel, b.thr.p, Ft,
+                                                                    nt2, (int)nt, len2, dim, b.part_d.p, nullptr,
+                                                                    b.part_i.p);
     if ((e = hipGetLastError()) != hipSuccess) return e;
-    merge_exact_kernel<<<gq, 256, 0, s>>>(b.part_d.p, b.part_i.p, (int)nq, kExactParts, b.qidx.p, nsel, tmap, out);
+    merge_exact_kernel<<<g2, 256, 0, s>>>(b.part_d.p, b.part_i.p, (int)nq, parts2, b.qidx.p, nsel, tmap, out);
     return hipGetLastError();
 }
 

@@ -609,7 +609,7 @@ hipError_t launch_fpfh(const double* pts, const double* nrm, int64_t n, const in
                        const int32_t* cnt, int k, double* spfh, double* feat36, hipStream_t s);
 hipError_t launch_pad_features(const double* in33, int64_t n, double* out36, hipStream_t s);
 hipError_t launch_feat_norm(const double* F36, int64_t n, double* nrm2, hipStream_t s);
-int feat_nn_parts(int64_t nq);
+int feat_nn_parts(int64_t blocks, int64_t nt, int maxp);
 // tmap (or null): target row -> reported index
 hipError_t launch_feat_nn(const double* Fq, const double* nq2, int64_t nq, const double* Ft, const double* nt2,
                           int64_t nt, const int32_t* tmap, int dim, FeatNNBufs& b, int32_t* out, hipStream_t s);
