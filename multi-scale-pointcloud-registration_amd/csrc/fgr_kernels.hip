@@ -241,8 +241,11 @@ __device__ __forceinline__ void merge_lex(double& d, int& i, double od, int oi) 
 }
 
 // EXACT: qidx / nsel / thr give the compacted flagged queries and their
-// pass-1 thresholds; out_s is unused.
-template <bool EXACT>
+// pass-1 thresholds; out_s is unused.  KB: MFMAs per 16x16 tile.  9 covers
+// all 36 columns; 8 (dim <= 33, the FPFH case) covers columns 0..31 and adds
+// column 32 with one VALU fma per element, skipping the zero padding's MFMA
+// (an eighth of the matrix work).
+template <bool EXACT, int KB>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void feat_nn_kernel(const double* __restrict__ Fq, const double* __restrict__ nq2,
                                                       int nq, const int32_t* __restrict__ qidx,
                                                       const int32_t* __restrict__ nsel,
@@ -260,7 +263,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void f
     if ((int)blockIdx.x * 256 >= nrow) return;  // block-uniform
     const int q0 = (blockIdx.x * 4 + wid) * 64;
     const int t_begin = blockIdx.y * part_len, t_end = min(nt, t_begin + part_len);
-    double b[4][9], qn[4], th[4];
+    static_assert(KB == 8 || KB == 9, "KB");
+    double b[4][9], qn[4], th[4], c32[4];
     const double* qrow[4];
 #pragma unroll
     for (int qt = 0; qt < 4; ++qt) {
@@ -270,7 +274,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void f
         th[qt] = (EXACT && q >= 0) ? thr[q] : -1.0;
         qrow[qt] = Fq + (size_t)(q >= 0 ? q : 0) * kFD;
 #pragma unroll
-        for (int kb = 0; kb < 9; ++kb) b[qt][kb] = q >= 0 ? -2.0 * qrow[qt][4 * kb + (lane >> 4)] : 0.0;
+        for (int kb = 0; kb < KB; ++kb) b[qt][kb] = q >= 0 ? -2.0 * qrow[qt][4 * kb + (lane >> 4)] : 0.0;
+        c32[qt] = (KB == 8 && q >= 0) ? -2.0 * qrow[qt][32] : 0.0;
     }
     const double inf = __builtin_huge_val();
     double bd[4] = {inf, inf, inf, inf}, b2[4] = {inf, inf, inf, inf};
@@ -313,7 +318,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void f
 #pragma unroll
             for (int qt = 0; qt < 4; ++qt) acc[qt] = d4{qn[qt], qn[qt], qn[qt], qn[qt]};
 #pragma unroll
-            for (int kb = 0; kb < 9; ++kb) {
+            for (int kb = 0; kb < KB; ++kb) {
                 const double a = sT[sub * 16 + (lane & 15)][4 * kb + (lane >> 4)];
 #pragma unroll
                 for (int qt = 0; qt < 4; ++qt) acc[qt] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b[qt][kb], acc[qt], 0, 0, 0);
@@ -322,10 +327,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void f
             for (int r = 0; r < 4; ++r) {
                 const int row = sub * 16 + (lane >> 4) + 4 * r;
                 const double tn = sN[row];
+                const double t32 = KB == 8 ? sT[row][32] : 0.0;
                 const unsigned lidx = (unsigned)(t0 - t_begin + row);
 #pragma unroll
                 for (int qt = 0; qt < 4; ++qt) {
-                    const double d = tn + acc[qt][r];
+                    const double d = KB == 8 ? tn + fma(c32[qt], t32, acc[qt][r]) : tn + acc[qt][r];
                     if (!EXACT) {
                         // best and runner-up keys: five VALU per element, no
                         // compare or select (the compare/select form cost 11
@@ -678,9 +684,9 @@ hipError_t launch_feat_nn(const double* Fq, const double* nq2, int64_t nq, const
     double* part_s = b.part_d.p + (size_t)kMaxParts * nq;
     int32_t* nsel = b.qidx.p + nq;
     const int len1 = (int)(((nt + parts - 1) / parts + kFT - 1) / kFT * kFT);
-    feat_nn_kernel<false><<<dim3(gq, (unsigned)parts), 256, 0, s>>>(Fq, nq2, (int)nq, nullptr, nullptr, nullptr, Ft,
-                                                                   nt2, (int)nt, len1, dim, b.part_d.p, part_s,
-                                                                   b.part_i.p);
+    auto pass1 = dim <= 33 ? feat_nn_kernel<false, 8> : feat_nn_kernel<false, 9>;
+    pass1<<<dim3(gq, (unsigned)parts), 256, 0, s>>>(Fq, nq2, (int)nq, nullptr, nullptr, nullptr, Ft, nt2, (int)nt, len1,
+                                                    dim, b.part_d.p, part_s, b.part_i.p);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     merge_parts_kernel<<<gq, 256, 0, s>>>(b.part_d.p, part_s, b.part_i.p, (int)nq, parts, nq2, nt2, tmap, out,
                                           b.flag.p, b.thr.p, ldexp(1.0, feat_key_bits(len1) - 51));
@@ -704,9 +710,9 @@ hipError_t launch_feat_nn(const double* Fq, const double* nq2, int64_t nq, const
                 (long long)nq, (long long)nt, parts, nflag, parts2);
     if (nflag == 0) return hipSuccess;
     const int len2 = (int)(((nt + parts2 - 1) / parts2 + kFT - 1) / kFT * kFT);
-    feat_nn_kernel<true><<<dim3(g2, (unsigned)parts2), 256, 0, s>>>(Fq, nq2, (int)nq, b.qidx.p, nsel, b.thr.p, Ft,
-                                                                    nt2, (int)nt, len2, dim, b.part_d.p, nullptr,
-                                                                    b.part_i.p);
+    auto pass2 = dim <= 33 ? feat_nn_kernel<true, 8> : feat_nn_kernel<true, 9>;
+    pass2<<<dim3(g2, (unsigned)parts2), 256, 0, s>>>(Fq, nq2, (int)nq, b.qidx.p, nsel, b.thr.p, Ft, nt2, (int)nt, len2,
+                                                     dim, b.part_d.p, nullptr, b.part_i.p);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     merge_exact_kernel<<<g2, 256, 0, s>>>(b.part_d.p, b.part_i.p, (int)nq, parts2, b.qidx.p, nsel, tmap, out);
     return hipGetLastError();

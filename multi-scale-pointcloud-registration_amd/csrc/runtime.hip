@@ -235,7 +235,8 @@ static void fgr_mark(hipStream_t s, const char* what) {
 // (fgr.xyz[0..1], fgr.feat[0..1]).  src / tgt are the host copies used by the
 // sequential tuple test.
 int fgr_device(orpcd_ctx* c, const double* src, int64_t n, const double* tgt, int64_t m, const orpcd_fgr_params& p,
-               double* T_out, double* fitness_out, double* rmse_out, int64_t* ncorr_out, int64_t* n_mutual_out) {
+               double* T_out, double* fitness_out, double* rmse_out, int64_t* ncorr_out, int64_t* n_mutual_out,
+               bool same_features) {
     auto& F = c->fgr;
     hipStream_t s = c->stream;
     const int64_t np[2] = {n, m};
@@ -281,9 +282,17 @@ int fgr_device(orpcd_ctx* c, const double* src, int64_t n, const double* tgt, in
     CTX_CHECK(c, dedup_rows(F.feat[fi].p, F.fn2[fi].p, nPti, F.dedup, &nu, s));
     CTX_CHECK(c, launch_feat_nn(F.feat[fj].p, F.fn2[fj].p, nPtj, F.dedup.Fu.p, F.dedup.n2u.p, nu, F.dedup.uidx.p, 33,
                                 F.fnn, F.nn[0].p, s));
-    CTX_CHECK(c, dedup_rows(F.feat[fj].p, F.fn2[fj].p, nPtj, F.dedup, &nu, s));
-    CTX_CHECK(c, launch_feat_nn(F.feat[fi].p, F.fn2[fi].p, nPti, F.dedup.Fu.p, F.dedup.n2u.p, nu, F.dedup.uidx.p, 33,
-                                F.fnn, F.nn[1].p, s));
+    if (same_features) {
+        // the two feature sets are the same rows (Q4 on equal-size clouds,
+        // fastGlobalOptimizer.py:137-142, or identical caller features): the
+        // second direction is the first one's problem input for input, so
+        // its answers are the first one's
+        CTX_CHECK(c, hipMemcpyAsync(F.nn[1].p, F.nn[0].p, (size_t)nPti * 4, hipMemcpyDeviceToDevice, s));
+    } else {
+        CTX_CHECK(c, dedup_rows(F.feat[fj].p, F.fn2[fj].p, nPtj, F.dedup, &nu, s));
+        CTX_CHECK(c, launch_feat_nn(F.feat[fi].p, F.fn2[fi].p, nPti, F.dedup.Fu.p, F.dedup.n2u.p, nu, F.dedup.uidx.p,
+                                    33, F.fnn, F.nn[1].p, s));
+    }
     fgr_mark(s, "feature matching");
     std::vector<int32_t> j_to_i((size_t)nPtj), i_to_j((size_t)nPti);
     CTX_CHECK(c, d2h(j_to_i.data(), F.nn[0].p, (size_t)nPtj * 4, s));
@@ -1641,7 +1650,8 @@ int orpcd_fgr(orpcd_ctx* c, const double* src, int64_t n, const double* tgt, int
         CTX_CHECK(c, h2d(c->fgr.raw.p, feat[k], (size_t)np[k] * 33 * 8, c->stream));
         CTX_CHECK(c, launch_pad_features(c->fgr.raw.p, np[k], c->fgr.feat[k].p, c->stream));
     }
-    return fgr_device(c, src, n, tgt, m, *p, T_out, fitness_out, rmse_out, ncorr_out, n_mutual_out);
+    const bool same = n == m && (src_feat == tgt_feat || std::memcmp(src_feat, tgt_feat, (size_t)n * 33 * 8) == 0);
+    return fgr_device(c, src, n, tgt, m, *p, T_out, fitness_out, rmse_out, ncorr_out, n_mutual_out, same);
 }
 
 int orpcd_feature_nn(orpcd_ctx* c, const double* q, int64_t nq, const double* t, int64_t nt, int32_t dim,
@@ -1711,7 +1721,8 @@ int orpcd_fgr_optimize(orpcd_ctx* c, const double* src, int64_t n, const double*
         if (rc) return rc;
     }
     fgr_mark(c->stream, "target normals + fpfh");
-    return fgr_device(c, src, n, tgt, m, *p, T_out, fitness_out, rmse_out, ncorr_out, n_mutual_out);
+    return fgr_device(c, src, n, tgt, m, *p, T_out, fitness_out, rmse_out, ncorr_out, n_mutual_out,
+                      target_features_from_source && m == n);
 }
 
 int orpcd_set_option(orpcd_ctx* c, const char* key, double value) {

@@ -20,3 +20,4 @@ for L in "$@"; do
 done
 unset ORPCD_HIP_LIB
 ORPCD_TRACE=1 timeout -k 10 180 python3 tools/fgr_ab.py --tag trace --reps 1 2>&1 | grep "feat_nn" | sort | uniq -c > gpurun_out/$T/flagged.txt || true
+ORPCD_FGR_TRACE=1 timeout -k 10 180 python3 tools/fgr_ab.py --tag phases --reps 2 > gpurun_out/$T/phases.txt 2>&1 || true
