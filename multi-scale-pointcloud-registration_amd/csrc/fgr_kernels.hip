@@ -469,6 +469,132 @@ __global__ void gather_rows_kernel(const double* __restrict__ F, const double* _
 // O3D FastGlobalRegistration.cpp OptimizePairwiseRegistration over the tuple
 // correspondences: p (normalised source) and q (normalised target, moved by
 // every update in place).
+// One correspondence's Geman-McClure weighted terms (21 JTJ + 6 JTr).
+__device__ __forceinline__ void irls_terms(const double pc[3], const double qc[3], double par, double acc[27]) {
+    const double qx = qc[0], qy = qc[1], qz = qc[2];
+    const double r[3] = {pc[0] - qx, pc[1] - qy, pc[2] - qz};
+    const double temp = par / (r[0] * r[0] + r[1] * r[1] + r[2] * r[2] + par);
+    const double s = temp * temp;
+    const double J[3][6] = {{0, -qz, qy, -1, 0, 0}, {qz, 0, -qx, 0, -1, 0}, {-qy, qx, 0, 0, 0, -1}};
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+        int e = 0;
+#pragma unroll
+        for (int u = 0; u < 6; ++u) {
+#pragma unroll
+            for (int v = u; v < 6; ++v) acc[e++] += J[a][u] * J[a][v] * s;
+            acc[21 + u] += J[a][u] * r[a] * s;
+        }
+    }
+}
+
+// The register-resident form (K <= kIrlsThreads * kIrlsPer, the default
+// maximum_tuple_count of 1000 gives K = 3000): 8 waves, each thread holding
+// its correspondences (c = thread + 512 k) in registers for all iterations;
+// per iteration 27 wave sums, a fixed-order sum over the waves, and the 6x6
+// solve on wave 0 (det6_wave / ldlt_solve6 / vec6_to_m4_wave, bit-identical to
+// the single-lane routines).  The one-block 256-thread form below re-read q
+// from memory and solved on one lane: 19 us per iteration against ~6.
+constexpr int kIrlsThreads = 512, kIrlsPer = 6;
+__global__ __launch_bounds__(kIrlsThreads) void fgr_irls_reg_kernel(const double* __restrict__ p,
+                                                                    double* __restrict__ q, int K, double par0,
+                                                                    int iters, double division_factor,
+                                                                    double max_corr, int decrease_mu,
+                                                                    double* __restrict__ T_out) {
+    constexpr int kW = kIrlsThreads / 64;
+    __shared__ double red[kW][27];
+    __shared__ double sums[27];
+    __shared__ double delta[16];
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    double trans[16];
+#pragma unroll
+    for (int t = 0; t < 16; ++t) trans[t] = (t % 5 == 0) ? 1.0 : 0.0;
+    if (K < 10) {  // O3D: fewer than 10 correspondences -> identity
+        if (threadIdx.x < 16) T_out[threadIdx.x] = trans[threadIdx.x];
+        return;
+    }
+    double pl[kIrlsPer][3], ql[kIrlsPer][3];
+#pragma unroll
+    for (int k = 0; k < kIrlsPer; ++k) {
+        const int c = threadIdx.x + kIrlsThreads * k;
+        const int cc = c < K ? c : 0;
+#pragma unroll
+        for (int a = 0; a < 3; ++a) {
+            pl[k][a] = p[3 * cc + a];
+            ql[k][a] = q[3 * cc + a];
+        }
+    }
+    double par = par0;
+    for (int itr = 0; itr < iters; ++itr) {
+        double acc[27];
+#pragma unroll
+        for (int v = 0; v < 27; ++v) acc[v] = 0.0;
+#pragma unroll
+        for (int k = 0; k < kIrlsPer; ++k)
+            if ((int)threadIdx.x + kIrlsThreads * k < K) irls_terms(pl[k], ql[k], par, acc);
+#pragma unroll
+        for (int v = 0; v < 27; ++v) {
+            const double sv = wave_sum(acc[v]);
+            if (lane == 0) red[wid][v] = sv;
+        }
+        __syncthreads();
+        if (threadIdx.x < 27) {
+            double t = red[0][threadIdx.x];
+            for (int w = 1; w < kW; ++w) t += red[w][threadIdx.x];
+            sums[threadIdx.x] = t;
+        }
+        __syncthreads();
+        if (wid == 0) {
+            double s[27];
+#pragma unroll
+            for (int v = 0; v < 27; ++v) s[v] = sums[v];
+            double neg[21], row[6], A[36], bvec[6], x[6] = {0, 0, 0, 0, 0, 0}, dl[16];
+#pragma unroll
+            for (int v = 0; v < 21; ++v) neg[v] = -s[v];
+            sym6_row(neg, lane, row);  // SolveLinearSystemPSD(-JTJ, JTr): check_det
+            for (int u = 0, e = 0; u < 6; ++u)
+                for (int v = u; v < 6; ++v, ++e) A[6 * u + v] = A[6 * v + u] = neg[e];
+#pragma unroll
+            for (int u = 0; u < 6; ++u) bvec[u] = s[21 + u];
+            const double det = det6_wave(row, lane);
+            if (!(fabs(det) < 1e-6 || isnan(det) || isinf(det))) ldlt_solve6(A, bvec, x);
+            vec6_to_m4_wave(x, dl, lane);
+            double tn[16];
+            m4_mul(dl, trans, tn);
+#pragma unroll
+            for (int t = 0; t < 16; ++t) trans[t] = tn[t];
+#pragma unroll
+            for (int t = 0; t < 16; ++t)
+                if (lane == t) delta[t] = dl[t];
+        }
+        __syncthreads();
+        double dm[12];
+#pragma unroll
+        for (int t = 0; t < 12; ++t) dm[t] = delta[t];
+#pragma unroll
+        for (int k = 0; k < kIrlsPer; ++k) {
+            const double x = ql[k][0], y = ql[k][1], z = ql[k][2];
+            ql[k][0] = dm[0] * x + dm[1] * y + dm[2] * z + dm[3];
+            ql[k][1] = dm[4] * x + dm[5] * y + dm[6] * z + dm[7];
+            ql[k][2] = dm[8] * x + dm[9] * y + dm[10] * z + dm[11];
+        }
+        if (decrease_mu && itr % 4 == 0 && par > max_corr) par /= division_factor;
+        // delta is rewritten only after the next iteration's first barrier
+    }
+#pragma unroll
+    for (int k = 0; k < kIrlsPer; ++k) {
+        const int c = threadIdx.x + kIrlsThreads * k;
+        if (c < K)
+#pragma unroll
+            for (int a = 0; a < 3; ++a) q[3 * c + a] = ql[k][a];
+    }
+    if (wid == 0 && lane < 16) {
+#pragma unroll
+        for (int t = 0; t < 16; ++t)
+            if (lane == t) T_out[t] = trans[t];
+    }
+}
+
 __global__ __launch_bounds__(256) void fgr_irls_kernel(const double* __restrict__ p, double* __restrict__ q, int K,
                                                        double par0, int iters, double division_factor,
                                                        double max_corr, int decrease_mu, double* __restrict__ T_out) {
@@ -488,21 +614,9 @@ __global__ __launch_bounds__(256) void fgr_irls_kernel(const double* __restrict_
 #pragma unroll
         for (int v = 0; v < 27; ++v) acc[v] = 0.0;
         for (int c = threadIdx.x; c < K; c += 256) {
-            const double qx = q[3 * c], qy = q[3 * c + 1], qz = q[3 * c + 2];
-            const double r[3] = {p[3 * c] - qx, p[3 * c + 1] - qy, p[3 * c + 2] - qz};
-            const double temp = par / (r[0] * r[0] + r[1] * r[1] + r[2] * r[2] + par);
-            const double s = temp * temp;
-            const double J[3][6] = {{0, -qz, qy, -1, 0, 0}, {qz, 0, -qx, 0, -1, 0}, {-qy, qx, 0, 0, 0, -1}};
-#pragma unroll
-            for (int a = 0; a < 3; ++a) {
-                int e = 0;
-#pragma unroll
-                for (int u = 0; u < 6; ++u) {
-#pragma unroll
-                    for (int v = u; v < 6; ++v) acc[e++] += J[a][u] * J[a][v] * s;
-                    acc[21 + u] += J[a][u] * r[a] * s;
-                }
-            }
+            const double pc[3] = {p[3 * c], p[3 * c + 1], p[3 * c + 2]};
+            const double qc[3] = {q[3 * c], q[3 * c + 1], q[3 * c + 2]};
+            irls_terms(pc, qc, par, acc);
         }
 #pragma unroll
         for (int v = 0; v < 27; ++v) {
@@ -760,7 +874,11 @@ hipError_t dedup_rows(const double* F, const double* n2, int64_t n, DedupBufs& b
 
 hipError_t launch_fgr_irls(const double* p, double* q, int K, double par0, int iters, double division_factor,
                            double max_corr, int decrease_mu, double* T_out, hipStream_t s) {
-    fgr_irls_kernel<<<1, 256, 0, s>>>(p, q, K, par0, iters, division_factor, max_corr, decrease_mu, T_out);
+    if (K <= kIrlsThreads * kIrlsPer)
+        fgr_irls_reg_kernel<<<1, kIrlsThreads, 0, s>>>(p, q, K, par0, iters, division_factor, max_corr, decrease_mu,
+                                                       T_out);
+    else
+        fgr_irls_kernel<<<1, 256, 0, s>>>(p, q, K, par0, iters, division_factor, max_corr, decrease_mu, T_out);
     return hipGetLastError();
 }
 

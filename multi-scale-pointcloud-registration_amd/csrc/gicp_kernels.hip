@@ -41,6 +41,8 @@
 #include <cstdlib>
 #include <vector>
 
+#include <hipcub/hipcub.hpp>
+
 #include "device_math.h"
 #include "orpcd_internal.h"
 #include "wave_ops.h"
@@ -1899,10 +1901,13 @@ hipError_t launch_seed_grids(const TargetDesc* tdesc, int first, int count, hipS
     return hipGetLastError();
 }
 
-// Kernel-level 1-NN (orpcd_nn1_radius): the same culled search on Morton-
-// ordered targets (representative seed, S = 1), fp64 re-check, no
-// accumulation.  Queries in input order.
-__global__ __launch_bounds__(kCBlock) void nn1_kernel(const double* __restrict__ q64, int nq,
+// Kernel-level 1-NN (orpcd_nn1_radius, FGR's EvaluateRegistration): the same
+// culled search on Morton-ordered targets (representative seed, S = 1), fp64
+// re-check, no accumulation.  order != null: query slot i serves input query
+// order[i] (the batch's Morton order, so that a wave's queries share a small
+// box and the culling works; results land at the input index).
+__global__ __launch_bounds__(kCBlock) void nn1_kernel(const int32_t* __restrict__ order,
+                                                      const double* __restrict__ q64, int nq,
                                                       const float4* __restrict__ p4, const float4* __restrict__ tlo,
                                                       const float4* __restrict__ thi, const float4* __restrict__ qbox, int ntiles,
                                                       const float4* __restrict__ slo, const float4* __restrict__ shi,
@@ -1916,8 +1921,9 @@ __global__ __launch_bounds__(kCBlock) void nn1_kernel(const double* __restrict__
     int bj[kCQPT];
 #pragma unroll
     for (int k = 0; k < kCQPT; ++k) {
-        const int i = i0 + 64 * k;
-        const bool valid = i < nq;
+        const int s = i0 + 64 * k;
+        const bool valid = s < nq;
+        const int i = valid && order ? order[s] : s;
         qx[k] = valid ? (float)(q64[3 * i] - org.x) : 0.f;
         qy[k] = valid ? (float)(q64[3 * i + 1] - org.y) : 0.f;
         qz[k] = valid ? (float)(q64[3 * i + 2] - org.z) : 0.f;
@@ -1932,8 +1938,9 @@ __global__ __launch_bounds__(kCBlock) void nn1_kernel(const double* __restrict__
                   lane < nsuper ? shi[lane] : make_float4(0.f, 0.f, 0.f, 0.f));
 #pragma unroll
     for (int k = 0; k < kCQPT; ++k) {
-        const int i = i0 + 64 * k;
-        if (i >= nq) continue;
+        const int s = i0 + 64 * k;
+        if (s >= nq) continue;
+        const int i = order ? order[s] : s;
         int j = bj[k];
         double dd = 0.0;
         if (j >= 0) {
@@ -2201,11 +2208,36 @@ hipError_t launch_gicp_solve_sums(const orpcd_ctx* c, const double* sums29, int6
     return launch_xform(c, 1, pass + 1, r2, s, one_target());
 }
 
+constexpr int64_t kNn1OrderMin = 4096;  // smaller batches search in input order
+
 hipError_t launch_nn1(const double* q, int64_t nq, const CloudLayout& t, double r2, int32_t* idx, double* d2,
-                      hipStream_t s) {
+                      QueryOrder& qo, hipStream_t s) {
     if (nq <= 0) return hipSuccess;
     const unsigned grid = (unsigned)((nq + kCBlockQ - 1) / kCBlockQ);
-    nn1_kernel<<<grid, kCBlock, 0, s>>>(q, (int)nq, t.p4.p, t.tlo.p, t.thi.p, t.qbox.p, (int)t.ntiles, t.slo.p, t.shi.p,
+    // a batch in arbitrary order is first put in Morton order over the
+    // target's box (30-bit codes, hipCUB radix sort): C3's evaluation, 100k
+    // queries in input order, 1.44 ms unordered
+    const int32_t* order = nullptr;
+    if (nq >= kNn1OrderMin) {
+        hipError_t e;
+        if ((e = qo.codes.ensure((size_t)nq * 2)) != hipSuccess) return e;
+        if ((e = qo.ids.ensure((size_t)nq)) != hipSuccess) return e;
+        if ((e = qo.order.ensure((size_t)nq)) != hipSuccess) return e;
+        double ext = 0.0;
+        for (int a = 0; a < 3; ++a) ext = std::max(ext, t.hi[a] - t.lo[a]);
+        const double scale = ext > 0 ? 1023.0 / ext : 0.0;
+        if ((e = launch_morton(q, nq, t.lo, scale, qo.codes.p, qo.ids.p, s)) != hipSuccess) return e;
+        size_t tmp = 0;
+        if ((e = hipcub::DeviceRadixSort::SortPairs(nullptr, tmp, qo.codes.p, qo.codes.p + nq, qo.ids.p, qo.order.p,
+                                                    (int)nq, 0, 30, s)) != hipSuccess)
+            return e;
+        if ((e = qo.tmp.ensure(tmp)) != hipSuccess) return e;
+        if ((e = hipcub::DeviceRadixSort::SortPairs(qo.tmp.p, tmp, qo.codes.p, qo.codes.p + nq, qo.ids.p, qo.order.p,
+                                                    (int)nq, 0, 30, s)) != hipSuccess)
+            return e;
+        order = qo.order.p;
+    }
+    nn1_kernel<<<grid, kCBlock, 0, s>>>(order, q, (int)nq, t.p4.p, t.tlo.p, t.thi.p, t.qbox.p, (int)t.ntiles, t.slo.p, t.shi.p,
                                         (int)t.nsuper, seed_stride_for(t.ntiles), t.xyz64.p, t.perm.p, r2,
                                         search_r2(r2), idx, d2, org_of(t));
     return hipGetLastError();

@@ -238,6 +238,14 @@ struct CloudLayout {
     }
 };
 
+// Morton order of a query batch (launch_nn1): codes, identity ids, the
+// sorted order and the sort's scratch.
+struct QueryOrder {
+    DevBuf<uint32_t> codes;
+    DevBuf<int32_t> ids, order;
+    DevBuf<unsigned char> tmp;
+};
+
 struct DedupBufs {
     DevBuf<unsigned long long> key;
     DevBuf<int32_t> val, head, uidx;
@@ -466,6 +474,7 @@ struct orpcd_ctx {
     orpcd::CloudLayout aux;
     orpcd::DevBuf<double> scratch64a, scratch64b, scratch64c;
     orpcd::DevBuf<int32_t> scratch32;
+    orpcd::QueryOrder qorder;  // launch_nn1's Morton order of the queries
 
     orpcd::HostBuf<double> h64;
     orpcd::HostBuf<int32_t> h32;
@@ -554,6 +563,8 @@ hipError_t launch_gather_rows(const double* in, const int32_t* idx, int64_t offs
 constexpr int kSeedGrid = ORPCD_SEED_GRID;  // cells per axis
 hipError_t prepare_seed_grid(CloudLayout& L);
 hipError_t launch_seed_grids(const TargetDesc* tdesc, int first, int count, hipStream_t s);
+hipError_t launch_morton(const double* xyz, int64_t n, const double lo[3], double scale, uint32_t* code,
+                         int32_t* idx, hipStream_t s);
 hipError_t build_layout(const double* dev_in64, int64_t n, const double bbox_lo[3], double bbox_ext,
                         const double origin[3], CloudLayout& L, bool with_tiles, hipStream_t s);
 
@@ -600,7 +611,7 @@ hipError_t launch_reduce_partials(const orpcd_ctx* c, int slot, double* sums29, 
 hipError_t launch_gicp_solve_sums(const orpcd_ctx* c, const double* sums29, int64_t n_total, int pass,
                                   const orpcd_gicp_params& p, hipStream_t s);
 hipError_t launch_nn1(const double* q, int64_t nq, const CloudLayout& t, double r2, int32_t* idx, double* d2,
-                      hipStream_t s);
+                      QueryOrder& qo, hipStream_t s);
 hipError_t launch_solve6_test(const double* sums, int n, double* out_serial, double* out_wave, hipStream_t s);
 
 // fgr_kernels.hip

@@ -378,7 +378,7 @@ int fgr_device(orpcd_ctx* c, const double* src, int64_t n, const double* tgt, in
     CTX_CHECK(c, h2d(dT, T, sizeof(T), s));
     CTX_CHECK(c, launch_transform_points(F.xyz[0].p, n, dT, F.raw.p, s));
     const double r = p.maximum_correspondence_distance;
-    CTX_CHECK(c, launch_nn1(F.raw.p, n, c->aux, r * r, c->scratch32.p, c->scratch64c.p, s));
+    CTX_CHECK(c, launch_nn1(F.raw.p, n, c->aux, r * r, c->scratch32.p, c->scratch64c.p, c->qorder, s));
     const int64_t nb = (n + 255) / 256;
     CTX_CHECK(c, F.red.ensure((size_t)nb * 2));
     CTX_CHECK(c, launch_corr_stats(c->scratch32.p, c->scratch64c.p, n, F.red.p, s));
@@ -1535,7 +1535,8 @@ int orpcd_nn1_radius(orpcd_ctx* c, const double* q, int64_t nq, const double* t,
     CTX_CHECK(c, c->scratch64c.ensure((size_t)nq));
     CTX_CHECK(c, c->scratch32.ensure((size_t)nq));
     CTX_CHECK(c, h2d(c->scratch64b.p, q, (size_t)nq * 24, c->stream));
-    CTX_CHECK(c, launch_nn1(c->scratch64b.p, nq, c->aux, radius * radius, c->scratch32.p, c->scratch64c.p, c->stream));
+    CTX_CHECK(c, launch_nn1(c->scratch64b.p, nq, c->aux, radius * radius, c->scratch32.p, c->scratch64c.p, c->qorder,
+                            c->stream));
     CTX_CHECK(c, d2h(idx_out, c->scratch32.p, (size_t)nq * 4, c->stream));
     CTX_CHECK(c, d2h(d2_out, c->scratch64c.p, (size_t)nq * 8, c->stream));
     CTX_CHECK(c, hipStreamSynchronize(c->stream));

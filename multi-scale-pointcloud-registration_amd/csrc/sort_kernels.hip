@@ -127,6 +127,13 @@ hipError_t launch_gather_rows(const double* in, const int32_t* idx, int64_t offs
     return hipGetLastError();
 }
 
+hipError_t launch_morton(const double* xyz, int64_t n, const double lo[3], double scale, uint32_t* code,
+                         int32_t* idx, hipStream_t s) {
+    if (n <= 0) return hipSuccess;
+    morton_kernel<<<(unsigned)((n + 255) / 256), 256, 0, s>>>(xyz, (int)n, lo[0], lo[1], lo[2], scale, code, idx);
+    return hipGetLastError();
+}
+
 hipError_t build_layout(const double* dev_in64, int64_t n, const double bbox_lo[3], double bbox_ext,
                         const double origin[3], CloudLayout& L, bool with_tiles, hipStream_t s) {
     L.n = n;
