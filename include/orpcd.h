@@ -348,7 +348,11 @@ int orpcd_rigid_residual(const double* base, const double* src, int64_t n, const
  * Always counted (host wall-clock, whether profiling or not): [10] ms inside
  * GICP batch calls (set-up to outputs), [11] ms of it in the pass launch
  * calls, [12] ms of it waiting for the device (the every-sync_every-passes
- * synchronisation), [13] GICP batches.                                      */
+ * synchronisation), [13] GICP batches.
+ * Feature nearest neighbour (orpcd_feature_nn, orpcd_fgr*; while profiling,
+ * hipEvents around each pass): [14] pass-1 ms, [15] pass-2 (exact
+ * re-measure) ms, [16] pass-1 query-target pairs (queries x distinct target
+ * rows), [17] pass-2 pairs (flagged queries x distinct rows), [18] calls.   */
 int orpcd_profiling(orpcd_ctx* ctx, int32_t enable);
 int orpcd_stats(orpcd_ctx* ctx, double* stats_out, int32_t n);
 int orpcd_reset_stats(orpcd_ctx* ctx);

@@ -785,9 +785,16 @@ int feat_nn_parts(int64_t blocks, int64_t nt, int maxp) {
 }
 
 hipError_t launch_feat_nn(const double* Fq, const double* nq2, int64_t nq, const double* Ft, const double* nt2,
-                          int64_t nt, const int32_t* tmap, int dim, FeatNNBufs& b, int32_t* out, hipStream_t s) {
+                          int64_t nt, const int32_t* tmap, int dim, FeatNNBufs& b, int32_t* out, hipStream_t s,
+                          double* timing) {
     if (nq <= 0) return hipSuccess;
     hipError_t e;
+    // timing (profiling): events around each pass; timing[0..4] += pass-1 ms,
+    // pass-2 ms, pass-1 pairs, pass-2 pairs, calls
+    if (timing)
+        for (auto& ev : b.ev)
+            if (!ev && (e = hipEventCreateWithFlags(&ev, hipEventDisableSystemFence)) != hipSuccess) return e;
+    if (timing && (e = hipEventRecord(b.ev[0], s)) != hipSuccess) return e;
     const unsigned gq = (unsigned)((nq + 255) / 256);
     const int parts = feat_nn_parts(gq, nt, kMaxParts);
     if ((e = b.part_d.ensure((size_t)2 * kMaxParts * nq)) != hipSuccess) return e;
@@ -802,6 +809,7 @@ hipError_t launch_feat_nn(const double* Fq, const double* nq2, int64_t nq, const
     pass1<<<dim3(gq, (unsigned)parts), 256, 0, s>>>(Fq, nq2, (int)nq, nullptr, nullptr, nullptr, Ft, nt2, (int)nt, len1,
                                                     dim, b.part_d.p, part_s, b.part_i.p);
     if ((e = hipGetLastError()) != hipSuccess) return e;
+    if (timing && (e = hipEventRecord(b.ev[1], s)) != hipSuccess) return e;
     merge_parts_kernel<<<gq, 256, 0, s>>>(b.part_d.p, part_s, b.part_i.p, (int)nq, parts, nq2, nt2, tmap, out,
                                           b.flag.p, b.thr.p, ldexp(1.0, feat_key_bits(len1) - 51));
     if ((e = hipGetLastError()) != hipSuccess) return e;
@@ -822,12 +830,27 @@ hipError_t launch_feat_nn(const double* Fq, const double* nq2, int64_t nq, const
     if (getenv("ORPCD_TRACE"))
         fprintf(stderr, "[orpcd] feat_nn: %lld queries, %lld targets, %d parts, %d flagged for the exact pass (%d parts)\n",
                 (long long)nq, (long long)nt, parts, nflag, parts2);
+    float ms1 = 0.f, ms2 = 0.f;
+    if (timing && (e = hipEventElapsedTime(&ms1, b.ev[0], b.ev[1])) != hipSuccess) return e;  // drained by d2h
+    if (timing) {
+        timing[0] += ms1;
+        timing[2] += (double)nq * (double)nt;
+        timing[3] += (double)nflag * (double)nt;
+        timing[4] += 1;
+    }
     if (nflag == 0) return hipSuccess;
+    if (timing && (e = hipEventRecord(b.ev[2], s)) != hipSuccess) return e;
     const int len2 = (int)(((nt + parts2 - 1) / parts2 + kFT - 1) / kFT * kFT);
     auto pass2 = dim <= 33 ? feat_nn_kernel<true, 8> : feat_nn_kernel<true, 9>;
     pass2<<<dim3(g2, (unsigned)parts2), 256, 0, s>>>(Fq, nq2, (int)nq, b.qidx.p, nsel, b.thr.p, Ft, nt2, (int)nt, len2,
                                                      dim, b.part_d.p, nullptr, b.part_i.p);
     if ((e = hipGetLastError()) != hipSuccess) return e;
+    if (timing) {
+        if ((e = hipEventRecord(b.ev[3], s)) != hipSuccess) return e;
+        if ((e = hipEventSynchronize(b.ev[3])) != hipSuccess) return e;
+        if ((e = hipEventElapsedTime(&ms2, b.ev[2], b.ev[3])) != hipSuccess) return e;
+        timing[1] += ms2;
+    }
     merge_exact_kernel<<<g2, 256, 0, s>>>(b.part_d.p, b.part_i.p, (int)nq, parts2, b.qidx.p, nsel, tmap, out);
     return hipGetLastError();
 }

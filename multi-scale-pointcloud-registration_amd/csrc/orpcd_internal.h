@@ -267,6 +267,7 @@ struct FeatNNBufs {
     DevBuf<double> part_d, thr;
     DevBuf<int32_t> part_i, flag, qidx;
     DevBuf<unsigned char> tmp;
+    hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};  // pass timing (created on first use)
     void release() {
         part_d.release();
         thr.release();
@@ -274,6 +275,10 @@ struct FeatNNBufs {
         flag.release();
         qidx.release();
         tmp.release();
+        for (auto& e : ev) {
+            if (e) (void)hipEventDestroy(e);
+            e = nullptr;
+        }
     }
 };
 
@@ -306,6 +311,9 @@ struct KernelStats {
     // host wall-clock of the batches (always on; steady_clock): the whole
     // gicp batch call, its launch calls, and its waits for the device
     double host_batch_ms = 0, host_launch_ms = 0, host_sync_ms = 0, host_batches = 0;
+    // feature nearest neighbour (launch_feat_nn, while profiling): pass-1 ms,
+    // pass-2 ms, pass-1 query-target pairs, pass-2 pairs, calls
+    double feat[5] = {0, 0, 0, 0, 0};
 };
 
 // Boundary ties of a KNN covariance pass (launch_knn_cov_ties): points whose
@@ -623,7 +631,8 @@ hipError_t launch_feat_norm(const double* F36, int64_t n, double* nrm2, hipStrea
 int feat_nn_parts(int64_t blocks, int64_t nt, int maxp);
 // tmap (or null): target row -> reported index
 hipError_t launch_feat_nn(const double* Fq, const double* nq2, int64_t nq, const double* Ft, const double* nt2,
-                          int64_t nt, const int32_t* tmap, int dim, FeatNNBufs& b, int32_t* out, hipStream_t s);
+                          int64_t nt, const int32_t* tmap, int dim, FeatNNBufs& b, int32_t* out, hipStream_t s,
+                          double* timing = nullptr);
 // Representatives (lowest index) of the distinct rows of F (n x 36): b.uidx
 // (increasing), b.Fu / b.n2u their rows and norms; *nu_out their count.
 hipError_t dedup_rows(const double* F, const double* n2, int64_t n, DedupBufs& b, int64_t* nu_out, hipStream_t s);

@@ -281,7 +281,7 @@ int fgr_device(orpcd_ctx* c, const double* src, int64_t n, const double* tgt, in
     int64_t nu = 0;
     CTX_CHECK(c, dedup_rows(F.feat[fi].p, F.fn2[fi].p, nPti, F.dedup, &nu, s));
     CTX_CHECK(c, launch_feat_nn(F.feat[fj].p, F.fn2[fj].p, nPtj, F.dedup.Fu.p, F.dedup.n2u.p, nu, F.dedup.uidx.p, 33,
-                                F.fnn, F.nn[0].p, s));
+                                F.fnn, F.nn[0].p, s, c->profiling ? c->stats.feat : nullptr));
     if (same_features) {
         // the two feature sets are the same rows (Q4 on equal-size clouds,
         // fastGlobalOptimizer.py:137-142, or identical caller features): the
@@ -291,7 +291,7 @@ int fgr_device(orpcd_ctx* c, const double* src, int64_t n, const double* tgt, in
     } else {
         CTX_CHECK(c, dedup_rows(F.feat[fj].p, F.fn2[fj].p, nPtj, F.dedup, &nu, s));
         CTX_CHECK(c, launch_feat_nn(F.feat[fi].p, F.fn2[fi].p, nPti, F.dedup.Fu.p, F.dedup.n2u.p, nu, F.dedup.uidx.p,
-                                    33, F.fnn, F.nn[1].p, s));
+                                    33, F.fnn, F.nn[1].p, s, c->profiling ? c->stats.feat : nullptr));
     }
     fgr_mark(s, "feature matching");
     std::vector<int32_t> j_to_i((size_t)nPtj), i_to_j((size_t)nPti);
@@ -1678,7 +1678,7 @@ int orpcd_feature_nn(orpcd_ctx* c, const double* q, int64_t nq, const double* t,
     int64_t nu = 0;
     CTX_CHECK(c, dedup_rows(F.feat[1].p, F.fn2[1].p, nt, F.dedup, &nu, c->stream));
     CTX_CHECK(c, launch_feat_nn(F.feat[0].p, F.fn2[0].p, nq, F.dedup.Fu.p, F.dedup.n2u.p, nu, F.dedup.uidx.p, dim,
-                                F.fnn, F.nn[0].p, c->stream));
+                                F.fnn, F.nn[0].p, c->stream, c->profiling ? c->stats.feat : nullptr));
     CTX_CHECK(c, d2h(idx_out, F.nn[0].p, (size_t)nq * 4, c->stream));
     CTX_CHECK(c, hipStreamSynchronize(c->stream));
     return ORPCD_OK;
@@ -1816,11 +1816,12 @@ int orpcd_profiling(orpcd_ctx* c, int32_t enable) {
 
 int orpcd_stats(orpcd_ctx* c, double* out, int32_t n) {
     if (!c || !out) return ORPCD_EINVAL;
-    const double v[14] = {c->stats.launches, c->stats.ms,       c->stats.pairs,          c->stats.iterations,
+    const double v[19] = {c->stats.launches, c->stats.ms,       c->stats.pairs,          c->stats.iterations,
                           c->stats.passes,   c->stats.tiles,    c->stats.accum_ms,       c->stats.sched_launches,
                           c->stats.exact_filed, c->stats.exact_queries, c->stats.host_batch_ms,
-                          c->stats.host_launch_ms, c->stats.host_sync_ms, c->stats.host_batches};
-    for (int i = 0; i < n && i < 14; ++i) out[i] = v[i];
+                          c->stats.host_launch_ms, c->stats.host_sync_ms, c->stats.host_batches,
+                          c->stats.feat[0], c->stats.feat[1], c->stats.feat[2], c->stats.feat[3], c->stats.feat[4]};
+    for (int i = 0; i < n && i < 19; ++i) out[i] = v[i];
     return ORPCD_OK;
 }
 

@@ -611,11 +611,13 @@ class Context:
         self._check(self._L.orpcd_profiling(self._h, int(bool(enable))), "orpcd_profiling")
 
     def stats(self) -> dict:
-        out = np.zeros(14)
-        self._check(self._L.orpcd_stats(self._h, out, 14), "orpcd_stats")
+        out = np.zeros(19)
+        self._check(self._L.orpcd_stats(self._h, out, 19), "orpcd_stats")
         return dict(launches=out[0], ms=out[1], pairs=out[2], iterations=out[3], passes=out[4], tiles=out[5],
                     accum_ms=out[6], sched_launches=out[7], exact_filed=out[8], exact_queries=out[9],
-                    host_batch_ms=out[10], host_launch_ms=out[11], host_sync_ms=out[12], host_batches=out[13])
+                    host_batch_ms=out[10], host_launch_ms=out[11], host_sync_ms=out[12], host_batches=out[13],
+                    feat_pass1_ms=out[14], feat_pass2_ms=out[15], feat_pass1_pairs=out[16],
+                    feat_pass2_pairs=out[17], feat_calls=out[18])
 
     def reset_stats(self):
         self._check(self._L.orpcd_reset_stats(self._h), "orpcd_reset_stats")

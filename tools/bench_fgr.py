@@ -5,9 +5,9 @@
 Times the build's plugin (FPFH of both clouds + fp64-MFMA mutual matching +
 tuple test + GNC IRLS + evaluation, one orpcd_fgr_optimize call) with inputs
 on the host, as the Aligner hands them over, and the feature-NN kernel alone
-with HIP events (orpcd_profiling) for its roofline: algorithmic work
-2*33*N*M FLOP per direction, priced against the fp64 matrix
-peak.  The CPU oracle (same seed, same Q4 choice) is timed once on the host
+with HIP events per pass (orpcd_profiling / orpcd_stats) for its roofline:
+2*33 FLOP per query-target pair over the pairs pass 1
+evaluates, priced against the fp64 matrix peak.  The CPU oracle (same seed, same Q4 choice) is timed once on the host
 cores as the baseline and its result compared.
 """
 import argparse
@@ -51,17 +51,25 @@ def main():
         times.append(time.perf_counter() - t0)
     r = opt.last_result
 
-    # feature-NN kernel alone (both directions), HIP-event timed
+    # feature-NN kernels alone (one direction: the source features against
+    # themselves, as Q4 pairs them), hipEvent-timed per pass (orpcd_stats)
     ctx = opt.context
     _, fs = ctx.fpfh(src, 0.1, 20, 0.1, 20)
     ctx.feature_nn(fs[:4096], fs)                       # warm-up
-    t0 = time.perf_counter()
     reps = 3
+    ctx.profiling(True)
+    ctx.reset_stats()
+    t0 = time.perf_counter()
     for _ in range(reps):
         ctx.feature_nn(fs, fs)
     nn_s = (time.perf_counter() - t0) / reps
+    st = ctx.stats()
+    ctx.profiling(False)
     n = len(src)
-    nn_flop = 2 * 33 * n * n                            # one direction, algorithmic
+    flop_pair = 2 * 33                                  # per query-target pair
+    p1_ms, p2_ms = st["feat_pass1_ms"] / reps, st["feat_pass2_ms"] / reps
+    p1_pairs, p2_pairs = st["feat_pass1_pairs"] / reps, st["feat_pass2_pairs"] / reps
+    achieved = flop_pair * p1_pairs / (p1_ms * 1e-3) / 1e12
     line = {
         "metric": "FastGlobalOptimizer.optimize wall-clock (C3, 100k<->100k)",
         "value": round(1e3 * float(np.median(times)), 3), "unit": "ms", "higher_is_better": False,
@@ -71,10 +79,16 @@ def main():
                    "points": n},
         "result": {"rmse": float(rmse), "fitness": r["fitness"], "n_mutual": r["n_mutual"],
                    "n_tuple_corr": r["n_tuple_corr"]},
-        "feature_nn": {"seconds_per_direction_incl_upload": round(nn_s, 5),
-                       "achieved_tflops": round(nn_flop / nn_s / 1e12, 3),
-                       "peak_tflops": FP64_MATRIX_PEAK_TF,
-                       "frac": round(nn_flop / nn_s / 1e12 / FP64_MATRIX_PEAK_TF, 4)},
+        "feature_nn": {
+            "kernel": "feat_nn_kernel (pass 1: every query; pass 2: flagged near-ties, exact re-measure)",
+            "pass1_ms": round(p1_ms, 4), "pass2_ms": round(p2_ms, 4),
+            "pass1_pairs": p1_pairs, "pass2_pairs": p2_pairs, "flop_per_pair": flop_pair,
+            "achieved_tflops": round(achieved, 3), "peak_tflops": FP64_MATRIX_PEAK_TF,
+            "frac": round(achieved / FP64_MATRIX_PEAK_TF, 4),
+            "pass2_achieved_tflops": round(flop_pair * p2_pairs / max(p2_ms * 1e-3, 1e-12) / 1e12, 3),
+            "seconds_per_direction_incl_upload": round(nn_s, 5),
+            "note": "pairs = queries x distinct target rows (exact duplicate rows are collapsed first); "
+                    "brute-force equivalent N x N = %.3g pairs" % (float(n) * n)},
     }
     if args.cpu:
         sys.path.insert(0, os.path.join(REPO, "oracle"))
