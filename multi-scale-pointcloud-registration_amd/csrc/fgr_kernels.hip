@@ -252,7 +252,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void f
                                                       const double* __restrict__ thr, const double* __restrict__ Ft,
                                                       const double* __restrict__ nt2, int nt, int part_len, int dim,
                                                       double* __restrict__ out_d, double* __restrict__ out_s,
-                                                      int32_t* __restrict__ out_i) {
+                                                      int32_t* __restrict__ out_i, const uint32_t* __restrict__ need,
+                                                      int len1) {
     // double-buffered stage: the next 64 targets are loaded into registers
     // while the current ones are multiplied, then written to the other buffer
     // (one barrier per stage)
@@ -264,6 +265,23 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void f
     const int q0 = (blockIdx.x * 4 + wid) * 64;
     const int t_begin = blockIdx.y * part_len, t_end = min(nt, t_begin + part_len);
     static_assert(KB == 8 || KB == 9, "KB");
+    if (EXACT && need) {
+        // pass 2 over a sub-part: skipped (empty results) when no row of the
+        // block can have a candidate in the pass-1 parts it overlaps
+        uint32_t range = 0;
+        if (t_begin < t_end) {
+            const int p_lo = t_begin / len1, p_hi = (t_end - 1) / len1;
+            range = (p_hi >= 31 ? 0xFFFFFFFFu : ((1u << (p_hi + 1)) - 1u)) & ~((1u << p_lo) - 1u);
+        }
+        const int j = (int)blockIdx.x * 256 + (int)threadIdx.x;
+        if (!__syncthreads_or(j < nrow && (need[j] & range) != 0)) {
+            if (j < nrow) {
+                out_d[(size_t)blockIdx.y * nq + j] = __builtin_huge_val();
+                out_i[(size_t)blockIdx.y * nq + j] = -1;
+            }
+            return;
+        }
+    }
     double b[4][9], qn[4], th[4], c32[4];
     const double* qrow[4];
 #pragma unroll
@@ -394,7 +412,7 @@ __global__ void merge_parts_kernel(const double* __restrict__ pd, const double* 
                                    const int32_t* __restrict__ pi, int nq, int nparts, const double* __restrict__ nq2,
                                    const double* __restrict__ nt2, const int32_t* __restrict__ tmap,
                                    int32_t* __restrict__ out, int32_t* __restrict__ flag, double* __restrict__ thr,
-                                   double key_slack) {
+                                   double key_slack, uint32_t* __restrict__ need) {
     const int q = blockIdx.x * blockDim.x + threadIdx.x;
     if (q >= nq) return;
     double bd = pd[q], bs = ps[q];
@@ -406,7 +424,24 @@ __global__ void merge_parts_kernel(const double* __restrict__ pd, const double* 
     const double tol = 2e-13 * (nq2[q] + (bi >= 0 ? nt2[bi] : 0.0) + fabs(bd)) +
                        key_slack * (fabs(bd) + (bs < __builtin_huge_val() ? fabs(bs) : 0.0));
     flag[q] = (bi >= 0 && bs - bd <= tol) ? 1 : 0;
-    thr[q] = bd + 2.0 * tol;
+    const double th = bd + 2.0 * tol;
+    thr[q] = th;
+    // the parts that can hold a pass-2 candidate: every target of part p
+    // has an expansion >= its best key - the key perturbation, and pass 2's
+    // expansions differ from pass 1's by less than tol
+    uint32_t m = 0;
+    for (int p = 0; p < nparts; ++p) {
+        const double kp = pd[(size_t)p * nq + q];
+        if (pi[(size_t)p * nq + q] >= 0 && kp <= th + tol + key_slack * (fabs(kp) + fabs(th))) m |= 1u << p;
+    }
+    need[q] = m;
+}
+
+// need[j] = need_q[qidx[j]] for the compact list (sort keys of pass 2's order)
+__global__ void gather_need_kernel(const int32_t* __restrict__ qidx, const int32_t* __restrict__ nsel,
+                                   const uint32_t* __restrict__ need_q, uint32_t* __restrict__ key) {
+    const int j = blockIdx.x * blockDim.x + threadIdx.x;
+    if (j < *nsel) key[j] = need_q[qidx[j]];
 }
 
 // Pass-2 merge (lexicographic on the exact distance) into the answers.
@@ -802,16 +837,19 @@ hipError_t launch_feat_nn(const double* Fq, const double* nq2, int64_t nq, const
     if ((e = b.flag.ensure((size_t)nq)) != hipSuccess) return e;
     if ((e = b.qidx.ensure((size_t)nq + 1)) != hipSuccess) return e;
     if ((e = b.thr.ensure((size_t)nq)) != hipSuccess) return e;
+    if ((e = b.need.ensure((size_t)nq)) != hipSuccess) return e;
+    if ((e = b.nkey.ensure((size_t)2 * nq)) != hipSuccess) return e;
+    if ((e = b.qsort.ensure((size_t)nq)) != hipSuccess) return e;
     double* part_s = b.part_d.p + (size_t)kMaxParts * nq;
     int32_t* nsel = b.qidx.p + nq;
     const int len1 = (int)(((nt + parts - 1) / parts + kFT - 1) / kFT * kFT);
     auto pass1 = dim <= 33 ? feat_nn_kernel<false, 8> : feat_nn_kernel<false, 9>;
     pass1<<<dim3(gq, (unsigned)parts), 256, 0, s>>>(Fq, nq2, (int)nq, nullptr, nullptr, nullptr, Ft, nt2, (int)nt, len1,
-                                                    dim, b.part_d.p, part_s, b.part_i.p);
+                                                    dim, b.part_d.p, part_s, b.part_i.p, nullptr, len1);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     if (timing && (e = hipEventRecord(b.ev[1], s)) != hipSuccess) return e;
     merge_parts_kernel<<<gq, 256, 0, s>>>(b.part_d.p, part_s, b.part_i.p, (int)nq, parts, nq2, nt2, tmap, out,
-                                          b.flag.p, b.thr.p, ldexp(1.0, feat_key_bits(len1) - 51));
+                                          b.flag.p, b.thr.p, ldexp(1.0, feat_key_bits(len1) - 51), b.need.p);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     size_t tmp = 0;
     if ((e = hipcub::DeviceSelect::Flagged(nullptr, tmp, hipcub::CountingInputIterator<int32_t>(0), b.flag.p,
@@ -825,8 +863,12 @@ hipError_t launch_feat_nn(const double* Fq, const double* nq2, int64_t nq, const
     // the stream drains here anyway before the caller reads the answers)
     int32_t nflag = 0;
     if ((e = d2h(&nflag, nsel, 4, s)) != hipSuccess) return e;
+    // Pass 2 runs over kMaxParts sub-parts, its flagged queries ordered by
+    // their need masks (the pass-1 parts that can hold a candidate; most
+    // near-tie clusters sit in one or two), and a block skips every sub-part
+    // none of its rows needs.
     const unsigned g2 = (unsigned)((nflag + 255) / 256);
-    const int parts2 = nflag > 0 ? feat_nn_parts(g2, nt, kMaxParts) : 0;
+    const int parts2 = nflag > 0 ? (int)std::max<int64_t>(1, std::min<int64_t>(kMaxParts, (nt + kFT - 1) / kFT)) : 0;
     if (getenv("ORPCD_TRACE"))
         fprintf(stderr, "[orpcd] feat_nn: %lld queries, %lld targets, %d parts, %d flagged for the exact pass (%d parts)\n",
                 (long long)nq, (long long)nt, parts, nflag, parts2);
@@ -840,10 +882,20 @@ hipError_t launch_feat_nn(const double* Fq, const double* nq2, int64_t nq, const
     }
     if (nflag == 0) return hipSuccess;
     if (timing && (e = hipEventRecord(b.ev[2], s)) != hipSuccess) return e;
+    gather_need_kernel<<<g2, 256, 0, s>>>(b.qidx.p, nsel, b.need.p, b.nkey.p);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    size_t tmp2 = 0;
+    if ((e = hipcub::DeviceRadixSort::SortPairs(nullptr, tmp2, b.nkey.p, b.nkey.p + nq, b.qidx.p, b.qsort.p, nflag, 0,
+                                                parts, s)) != hipSuccess)
+        return e;
+    if ((e = b.tmp.ensure(tmp2)) != hipSuccess) return e;
+    if ((e = hipcub::DeviceRadixSort::SortPairs(b.tmp.p, tmp2, b.nkey.p, b.nkey.p + nq, b.qidx.p, b.qsort.p, nflag, 0,
+                                                parts, s)) != hipSuccess)
+        return e;
     const int len2 = (int)(((nt + parts2 - 1) / parts2 + kFT - 1) / kFT * kFT);
     auto pass2 = dim <= 33 ? feat_nn_kernel<true, 8> : feat_nn_kernel<true, 9>;
-    pass2<<<dim3(g2, (unsigned)parts2), 256, 0, s>>>(Fq, nq2, (int)nq, b.qidx.p, nsel, b.thr.p, Ft, nt2, (int)nt, len2,
-                                                     dim, b.part_d.p, nullptr, b.part_i.p);
+    pass2<<<dim3(g2, (unsigned)parts2), 256, 0, s>>>(Fq, nq2, (int)nq, b.qsort.p, nsel, b.thr.p, Ft, nt2, (int)nt, len2,
+                                                     dim, b.part_d.p, nullptr, b.part_i.p, b.nkey.p + nq, len1);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     if (timing) {
         if ((e = hipEventRecord(b.ev[3], s)) != hipSuccess) return e;
@@ -851,7 +903,7 @@ hipError_t launch_feat_nn(const double* Fq, const double* nq2, int64_t nq, const
         if ((e = hipEventElapsedTime(&ms2, b.ev[2], b.ev[3])) != hipSuccess) return e;
         timing[1] += ms2;
     }
-    merge_exact_kernel<<<g2, 256, 0, s>>>(b.part_d.p, b.part_i.p, (int)nq, parts2, b.qidx.p, nsel, tmap, out);
+    merge_exact_kernel<<<g2, 256, 0, s>>>(b.part_d.p, b.part_i.p, (int)nq, parts2, b.qsort.p, nsel, tmap, out);
     return hipGetLastError();
 }
 

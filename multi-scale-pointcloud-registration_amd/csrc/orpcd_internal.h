@@ -265,7 +265,8 @@ struct DedupBufs {
 
 struct FeatNNBufs {
     DevBuf<double> part_d, thr;
-    DevBuf<int32_t> part_i, flag, qidx;
+    DevBuf<int32_t> part_i, flag, qidx, qsort;
+    DevBuf<uint32_t> need, nkey;  // per-query pass-1 part masks; pass 2's sort keys (2 x)
     DevBuf<unsigned char> tmp;
     hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};  // pass timing (created on first use)
     void release() {
@@ -274,6 +275,9 @@ struct FeatNNBufs {
         part_i.release();
         flag.release();
         qidx.release();
+        qsort.release();
+        need.release();
+        nkey.release();
         tmp.release();
         for (auto& e : ev) {
             if (e) (void)hipEventDestroy(e);
