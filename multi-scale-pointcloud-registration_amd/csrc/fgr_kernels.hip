@@ -907,6 +907,35 @@ hipError_t launch_feat_nn(const double* Fq, const double* nq2, int64_t nq, const
     return hipGetLastError();
 }
 
+// Answers of duplicate rows from their representatives' (dedup_rows' runs:
+// sorted position p holds row vs[p]; a row that is not its own
+// representative (uflag 0) equals the row at its run head).
+__global__ void unique_pos_kernel(const int32_t* __restrict__ uidx, int nu, int32_t* __restrict__ pos) {
+    const int k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k < nu) pos[uidx[k]] = k;
+}
+
+__global__ void expand_dup_kernel(const int32_t* __restrict__ vs, const int32_t* __restrict__ head,
+                                  const unsigned char* __restrict__ uflag, int n, const int32_t* __restrict__ pos,
+                                  const int32_t* __restrict__ out_u, int32_t* __restrict__ out) {
+    const int p = blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= n) return;
+    const int i = vs[p];
+    const int r = uflag[i] ? i : vs[head[p]];
+    out[i] = out_u[pos[r]];
+}
+
+hipError_t expand_dup_answers(const DedupBufs& b, int64_t n, int64_t nu, const int32_t* out_u, int32_t* pos,
+                              int32_t* out, hipStream_t s) {
+    if (n <= 0) return hipSuccess;
+    unique_pos_kernel<<<(unsigned)((nu + 255) / 256), 256, 0, s>>>(b.uidx.p, (int)nu, pos);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    expand_dup_kernel<<<(unsigned)((n + 255) / 256), 256, 0, s>>>(b.val.p + n, b.head.p, b.uflag.p, (int)n, pos,
+                                                                  out_u, out);
+    return hipGetLastError();
+}
+
 hipError_t dedup_rows(const double* F, const double* n2, int64_t n, DedupBufs& b, int64_t* nu_out, hipStream_t s) {
     hipError_t e;
     if ((e = b.key.ensure((size_t)n * 2)) != hipSuccess) return e;

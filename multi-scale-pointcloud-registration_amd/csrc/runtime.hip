@@ -280,15 +280,21 @@ int fgr_device(orpcd_ctx* c, const double* src, int64_t n, const double* tgt, in
     CTX_CHECK(c, F.nn[1].ensure((size_t)nPti));
     int64_t nu = 0;
     CTX_CHECK(c, dedup_rows(F.feat[fi].p, F.fn2[fi].p, nPti, F.dedup, &nu, s));
-    CTX_CHECK(c, launch_feat_nn(F.feat[fj].p, F.fn2[fj].p, nPtj, F.dedup.Fu.p, F.dedup.n2u.p, nu, F.dedup.uidx.p, 33,
-                                F.fnn, F.nn[0].p, s, c->profiling ? c->stats.feat : nullptr));
     if (same_features) {
-        // the two feature sets are the same rows (Q4 on equal-size clouds,
+        // The two feature sets are the same rows (Q4 on equal-size clouds,
         // fastGlobalOptimizer.py:137-142, or identical caller features): the
-        // second direction is the first one's problem input for input, so
-        // its answers are the first one's
+        // second direction is the first one's problem input for input, and
+        // identical query rows have identical answers, so one search runs,
+        // over the distinct rows against themselves (F.nn[1] as its output),
+        // and every row takes its representative's answer.
+        CTX_CHECK(c, F.dpos.ensure((size_t)nPti));
+        CTX_CHECK(c, launch_feat_nn(F.dedup.Fu.p, F.dedup.n2u.p, nu, F.dedup.Fu.p, F.dedup.n2u.p, nu, F.dedup.uidx.p,
+                                    33, F.fnn, F.nn[1].p, s, c->profiling ? c->stats.feat : nullptr));
+        CTX_CHECK(c, expand_dup_answers(F.dedup, nPti, nu, F.nn[1].p, F.dpos.p, F.nn[0].p, s));
         CTX_CHECK(c, hipMemcpyAsync(F.nn[1].p, F.nn[0].p, (size_t)nPti * 4, hipMemcpyDeviceToDevice, s));
     } else {
+        CTX_CHECK(c, launch_feat_nn(F.feat[fj].p, F.fn2[fj].p, nPtj, F.dedup.Fu.p, F.dedup.n2u.p, nu, F.dedup.uidx.p,
+                                    33, F.fnn, F.nn[0].p, s, c->profiling ? c->stats.feat : nullptr));
         CTX_CHECK(c, dedup_rows(F.feat[fj].p, F.fn2[fj].p, nPtj, F.dedup, &nu, s));
         CTX_CHECK(c, launch_feat_nn(F.feat[fi].p, F.fn2[fi].p, nPti, F.dedup.Fu.p, F.dedup.n2u.p, nu, F.dedup.uidx.p,
                                     33, F.fnn, F.nn[1].p, s, c->profiling ? c->stats.feat : nullptr));
