@@ -504,7 +504,50 @@ __global__ void gather_rows_kernel(const double* __restrict__ F, const double* _
 // O3D FastGlobalRegistration.cpp OptimizePairwiseRegistration over the tuple
 // correspondences: p (normalised source) and q (normalised target, moved by
 // every update in place).
-// One correspondence's Geman-McClure weighted terms (21 JTJ + 6 JTr).
+// One correspondence's Geman-McClure weighted terms (21 JTJ + 6 JTr), with
+// J = [[0, -z, y, -1, 0, 0], [z, 0, -x, 0, -1, 0], [-y, x, 0, 0, 0, -1]]
+// written out: the terms J's zeros contribute are exact no-ops of the
+// generic form (irls_terms), so only the nonzero ones are formed, in the
+// same row order a = 0, 1, 2 — 27 accumulations instead of 63 products
+// (the register-resident kernel runs on one CU, where its fp64 VALU work is
+// the iteration's longest stage).
+__device__ __forceinline__ void irls_terms_sparse(const double pc[3], const double qc[3], double par,
+                                                  double acc[27]) {
+    const double x = qc[0], y = qc[1], z = qc[2];
+    const double r0 = pc[0] - x, r1 = pc[1] - y, r2 = pc[2] - z;
+    const double temp = par / (r0 * r0 + r1 * r1 + r2 * r2 + par);
+    const double s = temp * temp;
+    const double my = -y, mz = -z, mx = -x;
+    acc[0] += (z * z) * s;  // (0,0): a = 1, 2
+    acc[0] += (my * my) * s;
+    acc[1] += (my * x) * s;   // (0,1): a = 2
+    acc[2] += (z * mx) * s;   // (0,2): a = 1
+    acc[4] += (z * -1.0) * s;   // (0,4): a = 1
+    acc[5] += (my * -1.0) * s;  // (0,5): a = 2
+    acc[6] += (mz * mz) * s;  // (1,1): a = 0, 2
+    acc[6] += (x * x) * s;
+    acc[7] += (mz * y) * s;     // (1,2): a = 0
+    acc[8] += (mz * -1.0) * s;  // (1,3): a = 0
+    acc[10] += (x * -1.0) * s;  // (1,5): a = 2
+    acc[11] += (y * y) * s;  // (2,2): a = 0, 1
+    acc[11] += (mx * mx) * s;
+    acc[12] += (y * -1.0) * s;   // (2,3): a = 0
+    acc[13] += (mx * -1.0) * s;  // (2,4): a = 1
+    acc[15] += s;  // (3,3): a = 0, (-1)(-1)
+    acc[18] += s;  // (4,4): a = 1
+    acc[20] += s;  // (5,5): a = 2
+    acc[21] += (z * r1) * s;  // JTr: u = 0 (a = 1, 2)
+    acc[21] += (my * r2) * s;
+    acc[22] += (mz * r0) * s;  // u = 1 (a = 0, 2)
+    acc[22] += (x * r2) * s;
+    acc[23] += (y * r0) * s;  // u = 2 (a = 0, 1)
+    acc[23] += (mx * r1) * s;
+    acc[24] += (-1.0 * r0) * s;  // u = 3..5
+    acc[25] += (-1.0 * r1) * s;
+    acc[26] += (-1.0 * r2) * s;
+}
+
+// One correspondence's terms, the generic form (the memory-resident kernel).
 __device__ __forceinline__ void irls_terms(const double pc[3], const double qc[3], double par, double acc[27]) {
     const double qx = qc[0], qy = qc[1], qz = qc[2];
     const double r[3] = {pc[0] - qx, pc[1] - qy, pc[2] - qz};
@@ -531,14 +574,44 @@ __device__ __forceinline__ void irls_terms(const double pc[3], const double qc[3
 // the single-lane routines).  The one-block 256-thread form below re-read q
 // from memory and solved on one lane: 19 us per iteration against ~6.
 constexpr int kIrlsThreads = 512, kIrlsPer = 6;
+
+#ifndef ORPCD_IRLS_DPP
+#define ORPCD_IRLS_DPP 1
+#endif
+// A double moved across lanes by one DPP pattern (both halves).
+template <int kCtrl>
+__device__ __forceinline__ double dpp_f64(double v) {
+    const unsigned long long b = (unsigned long long)__double_as_longlong(v);
+    const int lo = __builtin_amdgcn_mov_dpp((int)(unsigned)b, kCtrl, 0xF, 0xF, false);
+    const int hi = __builtin_amdgcn_mov_dpp((int)(unsigned)(b >> 32), kCtrl, 0xF, 0xF, false);
+    return __longlong_as_double(((long long)(unsigned)hi << 32) | (unsigned)lo);
+}
+// Wave sum for lane 0 on the VALU's DPP paths: quad swaps (xor 1, xor 2),
+// then the half-row and row mirrors (the other quad, the other half of the
+// row: every row of 16 ends uniform), then the four row sums by readlane —
+// instead of six ds_bpermute round trips per value (5.2 us of every IRLS
+// iteration for 27 sums).  A different tree than wave_sum's xor butterfly.
+__device__ __forceinline__ double wave_sum_dpp(double v) {
+    v += dpp_f64<0xB1>(v);   // quad_perm [1, 0, 3, 2]
+    v += dpp_f64<0x4E>(v);   // quad_perm [2, 3, 0, 1]
+    v += dpp_f64<0x141>(v);  // row_half_mirror
+    v += dpp_f64<0x140>(v);  // row_mirror
+    return (rl64(v, 0) + rl64(v, 16)) + (rl64(v, 32) + rl64(v, 48));
+}
 __global__ __launch_bounds__(kIrlsThreads) void fgr_irls_reg_kernel(const double* __restrict__ p,
                                                                     double* __restrict__ q, int K, double par0,
                                                                     int iters, double division_factor,
                                                                     double max_corr, int decrease_mu,
                                                                     double* __restrict__ T_out) {
     constexpr int kW = kIrlsThreads / 64;
-    __shared__ double red[kW][27];
-    __shared__ double sums[27];
+    // Of the 27 sums only 16 are distinct (irls_terms_sparse): (0,3), (1,4),
+    // (2,5), (3,4), (3,5), (4,5) are never added to, (3,3) = (4,4) = (5,5),
+    // and (1,3) = -(0,4), (2,3) = -(0,5), (2,4) = -(1,5) term by term, so
+    // bit for bit.  Only those 16 are reduced.
+    constexpr int kNd = 16;
+    constexpr int kDist[kNd] = {0, 1, 2, 4, 5, 6, 7, 10, 11, 15, 21, 22, 23, 24, 25, 26};
+    __shared__ double red[kW][kNd];
+    __shared__ double sums[kNd];
     __shared__ double delta[16];
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     double trans[16];
@@ -560,29 +633,49 @@ __global__ __launch_bounds__(kIrlsThreads) void fgr_irls_reg_kernel(const double
         }
     }
     double par = par0;
+#ifdef ORPCD_IRLS_TIME  // phase times of wave 0 (s_memrealtime, 10 ns ticks), printed at the end
+    unsigned long long ph[6] = {0, 0, 0, 0, 0, 0}, tq = __builtin_amdgcn_s_memrealtime(), tc0 = __builtin_amdgcn_s_memtime();
+#define IRLS_T(k)                                                  \
+    do {                                                           \
+        const unsigned long long tn_ = __builtin_amdgcn_s_memrealtime(); \
+        ph[k] += tn_ - tq;                                         \
+        tq = tn_;                                                  \
+    } while (0)
+#else
+#define IRLS_T(k) (void)0
+#endif
     for (int itr = 0; itr < iters; ++itr) {
         double acc[27];
 #pragma unroll
         for (int v = 0; v < 27; ++v) acc[v] = 0.0;
 #pragma unroll
         for (int k = 0; k < kIrlsPer; ++k)
-            if ((int)threadIdx.x + kIrlsThreads * k < K) irls_terms(pl[k], ql[k], par, acc);
+            if ((int)threadIdx.x + kIrlsThreads * k < K) irls_terms_sparse(pl[k], ql[k], par, acc);
+        IRLS_T(0);
 #pragma unroll
-        for (int v = 0; v < 27; ++v) {
-            const double sv = wave_sum(acc[v]);
+        for (int v = 0; v < kNd; ++v) {
+            const double sv = ORPCD_IRLS_DPP ? wave_sum_dpp(acc[kDist[v]]) : wave_sum(acc[kDist[v]]);
             if (lane == 0) red[wid][v] = sv;
         }
+        IRLS_T(1);
         __syncthreads();
-        if (threadIdx.x < 27) {
+        if (threadIdx.x < kNd) {
             double t = red[0][threadIdx.x];
             for (int w = 1; w < kW; ++w) t += red[w][threadIdx.x];
             sums[threadIdx.x] = t;
         }
         __syncthreads();
+        IRLS_T(2);
         if (wid == 0) {
             double s[27];
 #pragma unroll
-            for (int v = 0; v < 27; ++v) s[v] = sums[v];
+            for (int v = 0; v < 27; ++v) s[v] = 0.0;  // (0,3), (1,4), (2,5), (3,4), (3,5), (4,5)
+#pragma unroll
+            for (int v = 0; v < kNd; ++v) s[kDist[v]] = sums[v];
+            s[18] = s[20] = s[15];
+            s[8] = -s[4];
+            s[12] = -s[5];
+            s[13] = -s[10];
             double neg[21], row[6], A[36], bvec[6], x[6] = {0, 0, 0, 0, 0, 0}, dl[16];
 #pragma unroll
             for (int v = 0; v < 21; ++v) neg[v] = -s[v];
@@ -602,7 +695,9 @@ __global__ __launch_bounds__(kIrlsThreads) void fgr_irls_reg_kernel(const double
             for (int t = 0; t < 16; ++t)
                 if (lane == t) delta[t] = dl[t];
         }
+        IRLS_T(3);
         __syncthreads();
+        IRLS_T(4);
         double dm[12];
 #pragma unroll
         for (int t = 0; t < 12; ++t) dm[t] = delta[t];
@@ -615,7 +710,15 @@ __global__ __launch_bounds__(kIrlsThreads) void fgr_irls_reg_kernel(const double
         }
         if (decrease_mu && itr % 4 == 0 && par > max_corr) par /= division_factor;
         // delta is rewritten only after the next iteration's first barrier
+        IRLS_T(5);
     }
+#ifdef ORPCD_IRLS_TIME
+    if (threadIdx.x == 0)
+        printf("[irls] %d iters, K %d: accumulate %.2f, wave sums %.2f, block sums %.2f, solve %.2f, barrier %.2f, "
+               "update %.2f us total; shader cycles %llu\n", iters, K, ph[0] * 0.01, ph[1] * 0.01, ph[2] * 0.01,
+               ph[3] * 0.01, ph[4] * 0.01, ph[5] * 0.01, __builtin_amdgcn_s_memtime() - tc0);
+#endif
+#undef IRLS_T
 #pragma unroll
     for (int k = 0; k < kIrlsPer; ++k) {
         const int c = threadIdx.x + kIrlsThreads * k;

@@ -186,9 +186,19 @@ int fpfh_device(orpcd_ctx* c, const double* host_xyz, int k, int64_t n, double n
     double margin = 0.0;
     rc = layout_from_device(c, host_xyz, F.xyz[k].p, n, c->aux, true, &margin);
     if (rc) return rc;
-    CTX_CHECK(c, launch_knn_tiles(c->aux, F.xyz[k].p, normal_knn, normal_radius, margin, true, F.raw.p, nullptr,
-                                  nullptr, nullptr, c->stream));
+    // the normals' and the features' neighbourhoods are the same search when
+    // their (radius, knn) agree (the FGR defaults: 0.1, 20): one KNN pass
+    // then writes the covariances and the neighbour lists together
+    const bool shared = normal_knn == fpfh_knn && normal_radius == fpfh_radius;
+    CTX_CHECK(c, launch_knn_tiles(c->aux, F.xyz[k].p, normal_knn, normal_radius, margin, true, F.raw.p,
+                                  shared ? F.nbr.p : nullptr, shared ? F.nd2.p : nullptr, shared ? F.cnt.p : nullptr,
+                                  c->stream));
     CTX_CHECK(c, launch_normals_cov(F.raw.p, n, nullptr, 1, -1.0, F.nrm.p, nullptr, c->stream));
+    if (shared) {
+        CTX_CHECK(c, launch_fpfh(F.xyz[k].p, F.nrm.p, n, F.nbr.p, F.nd2.p, F.cnt.p, fpfh_knn, F.spfh.p, F.feat[k].p,
+                                 c->stream));
+        return ORPCD_OK;
+    }
     return features_device(c, nullptr, k, n, fpfh_radius, fpfh_knn, margin);
 }
 
