@@ -900,14 +900,13 @@ hipError_t launch_feat_norm(const double* F36, int64_t n, double* nrm2, hipStrea
 // product wins (100k queries x 67k targets: 9 parts, 7 full rounds, where a
 // fixed 5 parts left the 4th of 4 rounds 18% idle).
 int feat_nn_parts(int64_t blocks, int64_t nt, int maxp) {
-    static int slots = 0;
-    if (slots == 0) {
+    static const int slots = [] {  // thread-safe once-only initialisation
         int dev = 0, cus = 0;
         if (hipGetDevice(&dev) != hipSuccess ||
             hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
             cus = 256;
-        slots = 2 * cus;
-    }
+        return 2 * cus;
+    }();
     const int64_t pmax = std::max<int64_t>(1, std::min<int64_t>(maxp, (nt + kFT - 1) / kFT));
     int best = 1;
     int64_t best_cost = INT64_MAX;
