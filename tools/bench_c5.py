@@ -30,6 +30,10 @@ def main():
     ap.add_argument("--parity", type=int, default=1, help="also run the full oracle GICP and compare")
     ap.add_argument("--out", default=None)
     ap.add_argument("--opt", default="{}", help="runtime options (orpcd_set_option), JSON")
+    ap.add_argument("--path", choices=["auto", "rows", "batch"], default="auto",
+                    help="rows: the row-sharded pass API (a host all-reduce every pass); batch: orpcd_gicp_batch "
+                         "with one start (host sync every sync_every passes; bit-identical at one rank); "
+                         "auto: batch on one GPU, rows on several")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -47,24 +51,34 @@ def main():
         ctx.set_option(k, v)
     params = dict(max_correspondence_distance=0.5, max_iteration=args.iters)
 
+    path = args.path if args.path != "auto" else ("batch" if world == 1 else "rows")
+    if path == "batch" and world > 1:
+        raise SystemExit("--path batch runs one GPU")
     t0 = time.perf_counter()
     ctx.set_target(tgt, 1e-3, cache=False)
     lo, hi = parallel.shard(len(src), rank, world)
-    ctx.set_source_rows(src, lo, hi)
+    if path == "batch":
+        ctx.set_source(src, cache=False)
+    else:
+        ctx.set_source_rows(src, lo, hi)
     setup_s = time.perf_counter() - t0
-    # warm-up (code objects, allocations) on a short run
-    ctx.shard_begin(np.eye(3), np.zeros(3), n_total=len(src), **dict(params, max_iteration=1))
-    while True:
-        sums, act = ctx.shard_pass()
-        if not act or ctx.shard_update(parallel.allreduce_sum(sums)):
-            break
-    def run():
-        ctx.shard_begin(np.eye(3), np.zeros(3), n_total=len(src), **params)
+
+    def run_rows(prm):
+        ctx.shard_begin(np.eye(3), np.zeros(3), n_total=len(src), **prm)
         while True:
             sums, act = ctx.shard_pass()
             if not act or ctx.shard_update(parallel.allreduce_sum(sums)):
                 break
         return ctx.shard_result()
+
+    def run_batch(prm):
+        b = ctx.gicp_batch(np.eye(3)[None], np.zeros((1, 3)), **prm)
+        return {k: (v[0] if k == "T" else v[0].item()) for k, v in b.items()}
+
+    def run(prm=params):
+        return run_batch(prm) if path == "batch" else run_rows(prm)
+
+    run(dict(params, max_iteration=1))  # warm-up (code objects, allocations) on a short run
 
     if world > 1:
         dist.barrier()
@@ -90,7 +104,9 @@ def main():
         "n_gpus": world, "scaling": "strong", "dtype": "f32+f64",
         "data": "synthetic C5 (bumpy sphere, default_rng(5), target = R(10deg) x + 0.02 + N(0,1e-4))",
         "config": {"workload": "C5: GeneralizedICP max_iterations=30 from identity", "points": len(src),
-                   "parallelism": f"source rows over {world} GPU(s), all-reduce of 29 f64 per pass"},
+                   "parallelism": (f"source rows over {world} GPU(s), all-reduce of 29 f64 per pass" if path == "rows"
+                                   else "one start, orpcd_gicp_batch (bit-identical to the one-rank row path)"),
+                   "path": path},
         "ms_per_iteration": round(1e3 * elapsed / max(passes, 1), 3),
         "setup_s": round(setup_s, 3),
         "result": {"rmse": r["rmse"], "fitness": r["fitness"], "iters": r["iters"], "ncorr": r["ncorr"]},
