@@ -119,6 +119,36 @@ def test_feature_nn_near_duplicates_resolved_exactly(ctx):
     assert ctx.feature_nn(q3, t)[0] == 150                          # -> lowest index
 
 
+def _exact_lex_nn(q, t):
+    """The oracle's answer: squared distance summed column by column in order
+    (unfused), lexicographic (distance, index) minimum."""
+    out = np.empty(len(q), np.int64)
+    for i, row in enumerate(q):
+        d = np.zeros(len(t))
+        for k in range(t.shape[1]):
+            df = row[k] - t[:, k]
+            d = d + df * df
+        out[i] = int(np.flatnonzero(d == d.min())[0])
+    return out
+
+
+def test_feature_nn_near_ties_spread_over_target_parts(ctx):
+    """Near-duplicate and duplicate rows of one feature row placed in many
+    target parts: pass 1 flags the queries, and pass 2 may only skip the parts
+    whose best key rules them out (its need masks) — the answer must be the
+    exact lexicographic minimum, index for index."""
+    rng = np.random.default_rng(31)
+    t = rng.random((20000, 33)) * 50
+    r0 = t[17].copy()
+    for j, pos in enumerate((150, 4200, 9000, 13333, 16000, 19990)):
+        t[pos] = r0
+        if j % 2 == 0:  # every other copy differs in its last bits
+            t[pos, (5 * j) % 33] = np.nextafter(t[pos, (5 * j) % 33], np.inf if j % 4 else -np.inf)
+    q = np.vstack([r0 + rng.normal(0, 1e-9, 33) for _ in range(6)] + [r0, t[4200], t[9000]])
+    got = ctx.feature_nn(q, t)
+    assert np.array_equal(got, _exact_lex_nn(q, t))
+
+
 def test_feature_nn_large_splits(ctx):
     rng = np.random.default_rng(3)
     q = rng.random((600, 33)) * 50
