@@ -384,8 +384,9 @@ int fgr_device(orpcd_ctx* c, const double* src, int64_t n, const double* tgt, in
         T[4 * a + 3] = -(Tn[a] * inner[0] + Tn[4 + a] * inner[1] + Tn[8 + a] * inner[2]);
     }
     T[15] = 1.0;
-    // --- EvaluateRegistration(source, target, max_corr, T)
-    int rc = upload_layout(c, tgt, m, c->aux, true);
+    // --- EvaluateRegistration(source, target, max_corr, T); the target is
+    // already on the device (F.xyz[1])
+    int rc = layout_from_device(c, tgt, F.xyz[1].p, m, c->aux, true);
     if (rc) return rc;
     CTX_CHECK(c, F.raw.ensure((size_t)n * 3 + 16));
     CTX_CHECK(c, c->scratch32.ensure((size_t)n));
