@@ -42,10 +42,12 @@ sys.path.insert(0, os.path.join(REPO, "multi-scale-pointcloud-registration_amd")
 sys.path.insert(0, REPO)
 
 FP32_PEAK_TFLOPS = 157.3    # MI355X FP32 VALU (packed v_pk_* math), MI355X_MICROARCH.md
-# VALU issue roof: 1024 SIMDs (256 CUs x 4) x 2.4 GHz (MI355X_MICROARCH.md max clock), one wave64
-# VALU instruction per SIMD every 4 cycles (16 lanes; 157.3 TF = 1024 x 16 lanes x 2 (FMA) x 2 (packed)
-# x 2.4 GHz)
-VALU_ISSUE_PEAK_GINST = 1024 * 2.4 / 4  # G wave-instructions/s
+# VALU issue roof: 1024 SIMDs (256 CUs x 4) x 2.4 GHz (MI355X_MICROARCH.md max clock); gfx950's SIMDs
+# are SIMD-32 and issue a wave64 VALU instruction every 2 cycles at throughput (MI355X_MICROARCH.md
+# "Wave scheduling" and the v_fma_f32 row of its cycle constants; rounds 1-4 used the SIMD-16 figure
+# of 4 cycles, which halved this roof)
+VALU_ISSUE_PEAK_GINST = 1024 * 2.4 / 2  # G wave-instructions/s
+WAVE_SLOTS = 256 * 4 * 5    # search waves resident at most: 5 per SIMD (amdgpu_waves_per_eu(5), 94 VGPRs)
 FLOP_PER_PAIR = 8           # 3 sub + 3 mul/fma(=5) per query-target distance
 
 
@@ -229,9 +231,13 @@ def main():
                              "achieved_ginst_s": round(valu_insts / (avg_ms * 1e-3) / 1e9, 1),
                              "peak_ginst_s": VALU_ISSUE_PEAK_GINST,
                              "frac": round(valu_insts / (avg_ms * 1e-3) / 1e9 / VALU_ISSUE_PEAK_GINST, 3)},
+                         # where the search's wave-cycles go (committed SQ counters of the same command):
+                         # parked on memory / issue-stalled / issuing, and the average resident waves
+                         "stalls": pmc_stalls("orpcd::" + kname, bool(getattr(opt, "_exact_nn", True))),
                          "note": "achieved = 8 FLOP x pairs the culled search evaluates; it falls whenever "
                                  "culling improves (round 4's 8-point in-tile boxes: 39% fewer pairs per "
-                                 "launch in a 4% shorter launch), so valu_issue.frac is the binding roof",
+                                 "launch in a 4% shorter launch). Neither roof binds: the stall breakdown "
+                                 "(latency: waves parked on memory and dependency chains) does, DESIGN.md §6",
                          "kernel": kname, "avg_launch_ms": round(avg_ms, 4),
                          "search_kernel_ms_total": round(st["ms"], 3),
                          "launches": int(st["launches"]), "flop_per_pair": FLOP_PER_PAIR,
@@ -402,6 +408,50 @@ def pmc_counter(kernel, exact, counter):
     inst = kernel + ("<true" if exact else "<false")
     key = kernel if kernel in d else next((k for k in sorted(d) if k.startswith(inst)), None)
     return None if key is None else d[key].get(counter)
+
+
+def pmc_stalls(kernel, exact):
+    """Wave-cycle breakdown of `kernel` per launch from the newest committed
+    SQ counters (profiles/rNN_pmc.json) and the same round's kernel-trace
+    average duration (rNN_kernel_stats.csv): SQ_WAIT_ANY (parked: s_waitcnt on
+    memory / barrier), SQ_WAIT_INST_ANY (issue stalls: dependencies, pipe
+    busy), the rest (issuing), all over SQ_WAVE_CYCLES (quad-cycles,
+    MI355X_MICROARCH.md §rocprofv3 PMC slots), and the average resident waves
+    = wave-cycles / (launch duration x clock) against the 5120 slots the
+    kernel's register budget allows.  The clock is GRBM_GUI_ACTIVE / 8 / the
+    launch time when that counter was collected, else 2.4 GHz."""
+    import csv
+    import glob
+    files = sorted(glob.glob(os.path.join(REPO, "profiles", "r*_pmc.json")))
+    if not files:
+        return None
+    d = json.load(open(files[-1]))
+    inst = kernel + ("<true" if exact else "<false")
+    key = kernel if kernel in d else next((k for k in sorted(d) if k.startswith(inst)), None)
+    if key is None or "SQ_WAVE_CYCLES" not in d[key]:
+        return None
+    c = d[key]
+    rnd = os.path.basename(files[-1]).split("_")[0]
+    avg_ns = None
+    ks = os.path.join(REPO, "profiles", f"{rnd}_kernel_stats.csv")
+    if os.path.exists(ks):
+        for r in csv.DictReader(open(ks)):
+            if r["Name"].replace("void ", "").startswith(inst):
+                avg_ns = float(r["AverageNs"])
+    wc = c["SQ_WAVE_CYCLES"]
+    out = {"source": f"{os.path.basename(files[-1])} + {rnd}_kernel_stats.csv",
+           "wait_any_frac": round(c.get("SQ_WAIT_ANY", 0) / wc, 3),
+           "wait_inst_any_frac": round(c.get("SQ_WAIT_INST_ANY", 0) / wc, 3)}
+    if "SQ_ACTIVE_INST_ANY" in c:
+        out["active_inst_any_frac"] = round(c["SQ_ACTIVE_INST_ANY"] / wc, 3)
+    out["waves_per_launch"] = round(c.get("SQ_WAVES", 0))
+    if avg_ns:
+        ghz = c["GRBM_GUI_ACTIVE"] / 8 / avg_ns if "GRBM_GUI_ACTIVE" in c else 2.4
+        res = wc * 4 / (avg_ns * ghz)
+        out.update(avg_launch_us_profiled=round(avg_ns / 1e3, 2), clock_ghz=round(ghz, 3),
+                   avg_resident_waves=round(res), resident_frac_of_slots=round(res / WAVE_SLOTS, 3),
+                   avg_wave_us=round(wc * 4 / max(c.get("SQ_WAVES", 1), 1) / ghz / 1e3, 2))
+    return out
 
 
 def pmc_traffic(kernel, exact=True):

@@ -45,6 +45,9 @@
  *       the feature matching inside registration_fgr_based_on_feature_matching
  *   orpcd_fgr_optimize
  *       FastGlobalOptimizer.optimize       Optimizer/fastGlobalOptimizer.py:146-190
+ *   orpcd_fgr_optimize_batch
+ *       the B optimize() calls of one multistart (or of several scale
+ *       candidates)                        Aligner/Aligner.py:178-202, 263-298
  *   orpcd_rng_draw_attempts
  *       the np.random draws of initialize_rotation, attempt after attempt
  *                                          Aligner/Aligner.py:125-162, 178-186
@@ -264,6 +267,25 @@ int orpcd_fgr_optimize(orpcd_ctx* ctx, const double* src, int64_t n, const doubl
                        double* T_out, double* fitness_out, double* rmse_out, int64_t* ncorr_out,
                        int64_t* n_mutual_out);
 
+/* FastGlobalOptimizer.optimize for B posed copies of one source as ONE call
+ * (the multistart of Aligner.py:178-202 and the speculative compass's
+ * candidates, replacing B calls of orpcd_fgr_optimize): start b is
+ * optimize(src @ R0[b] + t0[b], target[target_of_start[b]]) (R0 row-major,
+ * posed as numpy rounds np.dot(src, R0) + t0), bit for bit what
+ * orpcd_fgr_optimize returns for that posed copy.  Up to 16 targets,
+ * concatenated in tgts (m[k] points each); target_of_start may be NULL
+ * (every start against target 0).  Per start: T_out[16 b] (column
+ * convention), fitness / rmse / ncorr [b], n_mutual_out[2 b .. 2 b + 1].
+ * The per-start normals, FPFH, normalisation and evaluation run queued on the
+ * device; the tuple tests run on host threads; the B IRLS problems run in one
+ * launch.                                                                   */
+int orpcd_fgr_optimize_batch(orpcd_ctx* ctx, const double* src, int64_t n, const double* tgts, const int64_t* m,
+                             int32_t ntgt, const double* R0, const double* t0, const int32_t* target_of_start,
+                             int32_t B, double normal_radius, int32_t normal_knn, double fpfh_radius,
+                             int32_t fpfh_knn, int32_t target_features_from_source, const orpcd_fgr_params* params,
+                             double* T_out, double* fitness_out, double* rmse_out, int64_t* ncorr_out,
+                             int64_t* n_mutual_out);
+
 /* Tuning knobs (defaults are the measured best on MI355X):
  *   "search_waves"  split a start's tiles over waves until ~this many run
  *   "sync_every"    passes between host checks of the per-start done flags
@@ -352,7 +374,10 @@ int orpcd_rigid_residual(const double* base, const double* src, int64_t n, const
  * Feature nearest neighbour (orpcd_feature_nn, orpcd_fgr*; while profiling,
  * hipEvents around each pass): [14] pass-1 ms, [15] pass-2 (exact
  * re-measure) ms, [16] pass-1 query-target pairs (queries x distinct target
- * rows), [17] pass-2 pairs (flagged queries x distinct rows), [18] calls.   */
+ * rows), [17] pass-2 pairs (flagged queries x distinct rows), [18] calls.
+ * Always counted: [19] GICP starts whose source KNN-20 boundary ties may not
+ * all have been re-decided from their posed copy (tie table overflowed, or
+ * the posed coordinates beyond the size the tie band was set for).          */
 int orpcd_profiling(orpcd_ctx* ctx, int32_t enable);
 int orpcd_stats(orpcd_ctx* ctx, double* stats_out, int32_t n);
 int orpcd_reset_stats(orpcd_ctx* ctx);

@@ -10,6 +10,7 @@ from __future__ import annotations
 
 import glob
 import hashlib
+import json
 import os
 import subprocess
 import sys
@@ -51,10 +52,10 @@ def source_id() -> str:
 def _build_id_object(force):
     """A one-function host unit returning the source id and the extra flags."""
     sid = source_id()
-    flags = " ".join(EXTRA)
+    flags = json.dumps(" ".join(EXTRA))  # a C string literal: quotes and backslashes escaped
     src = os.path.join(OBJ_DIR, "build_id.cpp")
     text = (f'extern "C" const char* orpcd_build_id(void) {{ return "{sid}"; }}\n'
-            f'extern "C" const char* orpcd_build_flags(void) {{ return "{flags}"; }}\n')
+            f'extern "C" const char* orpcd_build_flags(void) {{ return {flags}; }}\n')
     old = open(src).read() if os.path.exists(src) else None
     if old != text:
         with open(src, "w") as fh:

@@ -381,8 +381,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void f
     }
     if (!EXACT) {
 #pragma unroll
-        for (int qt = 0; qt < 4; ++qt)
-            bi[qt] = bd[qt] < inf ? (int)((unsigned)__double2loint(bd[qt]) & kmask) + t_begin : -1;
+        for (int qt = 0; qt < 4; ++qt) {
+            // a key's index is a row of this part; a padded row (past t_end)
+            // can only win if every real distance was a NaN key, which the
+            // entry points exclude (feature_rows_ok) -- dropped all the same
+            const int cand = (int)((unsigned)__double2loint(bd[qt]) & kmask) + t_begin;
+            bi[qt] = bd[qt] < inf && cand < t_end ? cand : -1;
+        }
     }
     // merge the 4 lane groups (l>>4) holding the same query column
 #pragma unroll
@@ -600,11 +605,32 @@ __device__ __forceinline__ double wave_sum_dpp(double v) {
     v += dpp_f64<0x140>(v);  // row_mirror
     return (rl64(v, 0) + rl64(v, 16)) + (rl64(v, 32) + rl64(v, 48));
 }
-__global__ __launch_bounds__(kIrlsThreads) void fgr_irls_reg_kernel(const double* __restrict__ p,
-                                                                    double* __restrict__ q, int K, double par0,
+// meta (batched FGR, orpcd_fgr_optimize_batch): block b solves the problem
+// meta[3b..3b+2] = {offset of its p rows (doubles), K, output slot}: p at
+// p + offset, q right after it (3K doubles), T at T_out + 16 slot.  Each block
+// runs the single problem's arithmetic unchanged, so a batched start's T is
+// bit-identical to its own launch.
+__device__ __forceinline__ void irls_problem(const int64_t* meta, const double*& p, double*& q, int& K,
+                                             double*& T_out) {
+    if (!meta) return;
+    const int64_t* m = meta + 3 * blockIdx.x;
+    K = (int)m[1];
+    q = const_cast<double*>(p) + m[0] + 3 * (int64_t)K;
+    p = p + m[0];
+    T_out = T_out + 16 * m[2];
+}
+
+__global__ __launch_bounds__(kIrlsThreads) void fgr_irls_reg_kernel(const double* __restrict__ p_,
+                                                                    double* __restrict__ q_, int K_, double par0,
                                                                     int iters, double division_factor,
                                                                     double max_corr, int decrease_mu,
-                                                                    double* __restrict__ T_out) {
+                                                                    double* __restrict__ T_out_,
+                                                                    const int64_t* __restrict__ meta) {
+    const double* p = p_;
+    double* q = q_;
+    int K = K_;
+    double* T_out = T_out_;
+    irls_problem(meta, p, q, K, T_out);
     constexpr int kW = kIrlsThreads / 64;
     // Of the 27 sums only 16 are distinct (irls_terms_sparse): (0,3), (1,4),
     // (2,5), (3,4), (3,5), (4,5) are never added to, (3,3) = (4,4) = (5,5),
@@ -735,9 +761,15 @@ __global__ __launch_bounds__(kIrlsThreads) void fgr_irls_reg_kernel(const double
     }
 }
 
-__global__ __launch_bounds__(256) void fgr_irls_kernel(const double* __restrict__ p, double* __restrict__ q, int K,
+__global__ __launch_bounds__(256) void fgr_irls_kernel(const double* __restrict__ p_, double* __restrict__ q_, int K_,
                                                        double par0, int iters, double division_factor,
-                                                       double max_corr, int decrease_mu, double* __restrict__ T_out) {
+                                                       double max_corr, int decrease_mu, double* __restrict__ T_out_,
+                                                       const int64_t* __restrict__ meta) {
+    const double* p = p_;
+    double* q = q_;
+    int K = K_;
+    double* T_out = T_out_;
+    irls_problem(meta, p, q, K, T_out);
     __shared__ double red[4][27];
     __shared__ double delta[16];
     __shared__ double trans[16];
@@ -1080,13 +1112,57 @@ hipError_t dedup_rows(const double* F, const double* n2, int64_t n, DedupBufs& b
     return hipGetLastError();
 }
 
+// dedup_rows' representative flags only (no count, no gather, no host
+// sync): uflag_out[i] = 1 iff row i is the lowest index of its exact-equal
+// rows.  Scratch in b (reused in stream order by the next call).
+hipError_t dedup_flags(const double* F, int64_t n, DedupBufs& b, unsigned char* uflag_out, hipStream_t s) {
+    hipError_t e;
+    if (n <= 0) return hipSuccess;
+    if ((e = b.key.ensure((size_t)n * 2)) != hipSuccess) return e;
+    if ((e = b.val.ensure((size_t)n * 2)) != hipSuccess) return e;
+    if ((e = b.head.ensure((size_t)n + 1)) != hipSuccess) return e;
+    const unsigned g = (unsigned)((n + 255) / 256);
+    unsigned long long *k0 = b.key.p, *k1 = b.key.p + n;
+    int32_t *v0 = b.val.p, *v1 = b.val.p + n;
+    row_hash_kernel<<<g, 256, 0, s>>>(F, (int)n, k0, v0);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    size_t t1 = 0, t2 = 0;
+    if ((e = hipcub::DeviceRadixSort::SortPairs(nullptr, t1, k0, k1, v0, v1, (int)n, 0, 64, s)) != hipSuccess) return e;
+    if ((e = hipcub::DeviceScan::InclusiveScan(nullptr, t2, v0, v0, hipcub::Max(), (int)n, s)) != hipSuccess) return e;
+    if ((e = b.tmp.ensure(std::max(t1, t2))) != hipSuccess) return e;
+    if ((e = hipcub::DeviceRadixSort::SortPairs(b.tmp.p, t1, k0, k1, v0, v1, (int)n, 0, 64, s)) != hipSuccess) return e;
+    run_start_kernel<<<g, 256, 0, s>>>(k1, (int)n, v0);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    if ((e = hipcub::DeviceScan::InclusiveScan(b.tmp.p, t2, v0, b.head.p, hipcub::Max(), (int)n, s)) != hipSuccess)
+        return e;
+    representative_kernel<<<g, 256, 0, s>>>(F, v1, b.head.p, (int)n, uflag_out);
+    return hipGetLastError();
+}
+
 hipError_t launch_fgr_irls(const double* p, double* q, int K, double par0, int iters, double division_factor,
                            double max_corr, int decrease_mu, double* T_out, hipStream_t s) {
     if (K <= kIrlsThreads * kIrlsPer)
         fgr_irls_reg_kernel<<<1, kIrlsThreads, 0, s>>>(p, q, K, par0, iters, division_factor, max_corr, decrease_mu,
-                                                       T_out);
+                                                       T_out, nullptr);
     else
-        fgr_irls_kernel<<<1, 256, 0, s>>>(p, q, K, par0, iters, division_factor, max_corr, decrease_mu, T_out);
+        fgr_irls_kernel<<<1, 256, 0, s>>>(p, q, K, par0, iters, division_factor, max_corr, decrease_mu, T_out,
+                                          nullptr);
+    return hipGetLastError();
+}
+
+hipError_t launch_fgr_irls_batch(const double* pq, const int64_t* meta_reg, int nreg, const int64_t* meta_mem,
+                                 int nmem, double par0, int iters, double division_factor, double max_corr,
+                                 int decrease_mu, double* T_out, hipStream_t s) {
+    // problems of <= 3072 correspondences: one register-resident 512-thread
+    // workgroup each, all of them in one launch (one CU per start); larger
+    // ones: the memory-resident form, likewise
+    if (nreg > 0)
+        fgr_irls_reg_kernel<<<(unsigned)nreg, kIrlsThreads, 0, s>>>(pq, nullptr, 0, par0, iters, division_factor,
+                                                                    max_corr, decrease_mu, T_out, meta_reg);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess || nmem <= 0) return e;
+    fgr_irls_kernel<<<(unsigned)nmem, 256, 0, s>>>(pq, nullptr, 0, par0, iters, division_factor, max_corr,
+                                                   decrease_mu, T_out, meta_mem);
     return hipGetLastError();
 }
 

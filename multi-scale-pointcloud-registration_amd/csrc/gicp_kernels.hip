@@ -1004,19 +1004,24 @@ __device__ __forceinline__ void nn_search_body(
 // Ordered dispatch (SchedS): wave k of the launch takes item k of the
 // class-major list, heaviest class first; the wave's duration is added to its
 // group's cost and to the pass total for the next pass's schedule.
+// Waves per workgroup of the ordered dispatch (A/B macro ORPCD_SCHED_WAVES).
+#ifndef ORPCD_SCHED_WAVES
+#define ORPCD_SCHED_WAVES 4
+#endif
+constexpr int kSWaves = ORPCD_SCHED_WAVES;
 template <bool kExact>
-__global__ __launch_bounds__(kCBlock) __attribute__((amdgpu_waves_per_eu(kExact ? ORPCD_EXACT_WAVES : ORPCD_FAST_WAVES, 8))) void nn_search_sched_kernel(
+__global__ __launch_bounds__(64 * kSWaves) __attribute__((amdgpu_waves_per_eu(kExact ? ORPCD_EXACT_WAVES : ORPCD_FAST_WAVES, 8))) void nn_search_sched_kernel(
     const float4* __restrict__ q32, int N, const TargetDesc* __restrict__ tdesc, int super_cull,
     unsigned long long* __restrict__ best, unsigned long long* __restrict__ counters,
     const float4* __restrict__ gbox, SchedS sa, ExactArgs ex) {
-    __shared__ float4 stage[kCWaves][kTile];
+    __shared__ float4 stage[kSWaves][kTile];
     const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
     const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
     if (blockIdx.x == 0 && wid == 0) {
         if (lane < kSchedClasses) sa.cnt_next[lane] = 0u;
         sa.wtot_next[lane] = 0ull;  // kSchedTot == 64
     }
-    const unsigned w = __builtin_amdgcn_readfirstlane(blockIdx.x * kCWaves + wid);
+    const unsigned w = __builtin_amdgcn_readfirstlane(blockIdx.x * kSWaves + wid);
     unsigned base = 0, off = 0;
     int cls = -1;
 #pragma unroll
@@ -2128,13 +2133,13 @@ hipError_t launch_gicp_pass(const orpcd_ctx* c, int nact, int pass, double r2, h
         sa.cap = c->sched_cap;
         sa.NG = (int)NG;
         sa.B = (int)B;
-        const int64_t grid = (std::min<int64_t>(items, c->sched_cap) + kCWaves - 1) / kCWaves;
+        const int64_t grid = (std::min<int64_t>(items, c->sched_cap) + kSWaves - 1) / kSWaves;
         auto kern = c->exact_live ? nn_search_sched_kernel<true> : nn_search_sched_kernel<false>;
-        kern<<<dim3((unsigned)grid), kCBlock, 0, s>>>(c->q32.p, N, c->tdesc.p, c->opt.super_cull, c->best.p,
+        kern<<<dim3((unsigned)grid), 64 * kSWaves, 0, s>>>(c->q32.p, N, c->tdesc.p, c->opt.super_cull, c->best.p,
                                                       c->count_tiles ? c->counters.p : nullptr, c->gbox.p, sa,
                                                       exact_args(c, pass));
 #ifdef ORPCD_WAVETIME
-        if ((e = dump_wavetime(pass, nact, 0, (unsigned)(grid * kCWaves), s)) != hipSuccess) return e;
+        if ((e = dump_wavetime(pass, nact, 0, (unsigned)(grid * kSWaves), s)) != hipSuccess) return e;
 #endif
     } else {
         // few running starts: half the wave target (8 starts: 16k waves 8.16 ms

@@ -107,8 +107,16 @@ struct HostBuf {  // pinned
 // larger copies go through it in chunks.
 struct Staging {
     HostBuf<unsigned char> buf;
-    hipEvent_t ev = nullptr;  // recorded after the last staged host -> device copy
-    bool pending = false;     // that copy may still be reading buf
+    // recorded after the last staged host -> device copy, one event per device
+    // (an event records only on streams of the device it was created on)
+    std::vector<hipEvent_t> ev;
+    int ev_dev = -1;        // device of the pending copy's event
+    bool pending = false;   // that copy may still be reading buf
+    ~Staging() {            // thread exit: the events and the pinned buffer go with the thread
+        for (hipEvent_t e : ev)
+            if (e) (void)hipEventDestroy(e);
+        buf.release();
+    }
 };
 constexpr size_t kStageChunk = (size_t)32 << 20;  // pinned bytes per thread at most; larger copies go in chunks
 inline Staging& staging() {
@@ -118,16 +126,20 @@ inline Staging& staging() {
 inline hipError_t staging_reserve(Staging& st, size_t bytes) {
     hipError_t e = hipSuccess;
     if (st.pending) {  // the previous host -> device copy still reads the buffer
-        if ((e = hipEventSynchronize(st.ev)) != hipSuccess) return e;
+        if ((e = hipEventSynchronize(st.ev[st.ev_dev])) != hipSuccess) return e;
         st.pending = false;
     }
     if (bytes > st.buf.n) e = st.buf.ensure(std::min(kStageChunk, std::max(bytes, 2 * st.buf.n)));  // few re-pins
     return e;
 }
 inline hipError_t staging_mark(Staging& st, hipStream_t s) {
-    hipError_t e = hipSuccess;
-    if (!st.ev && (e = hipEventCreateWithFlags(&st.ev, hipEventDisableTiming)) != hipSuccess) return e;
-    if ((e = hipEventRecord(st.ev, s)) != hipSuccess) return e;
+    int dev = 0;
+    hipError_t e = hipGetDevice(&dev);  // the copy's stream belongs to the current device (callers set it)
+    if (e != hipSuccess) return e;
+    if ((int)st.ev.size() <= dev) st.ev.resize((size_t)dev + 1, nullptr);
+    if (!st.ev[dev] && (e = hipEventCreateWithFlags(&st.ev[dev], hipEventDisableTiming)) != hipSuccess) return e;
+    if ((e = hipEventRecord(st.ev[dev], s)) != hipSuccess) return e;
+    st.ev_dev = dev;
     st.pending = true;
     return hipSuccess;
 }
@@ -318,6 +330,9 @@ struct KernelStats {
     // feature nearest neighbour (launch_feat_nn, while profiling): pass-1 ms,
     // pass-2 ms, pass-1 query-target pairs, pass-2 pairs, calls
     double feat[5] = {0, 0, 0, 0, 0};
+    // starts whose source boundary ties may not all have been re-decided
+    // (tie table overflowed, or posed coordinates beyond the band's assumption)
+    double tie_gaps = 0;
 };
 
 // Boundary ties of a KNN covariance pass (launch_knn_cov_ties): points whose
@@ -404,6 +419,7 @@ struct orpcd_ctx {
     struct SourceTies {
         bool on = false;           // a table for the current source (set_source / set_source_rows)
         bool complete = true;      // every tie is in the table (false: the surplus keeps the rotated covariance)
+        double band_A = 0.0;       // max |coordinate| of the cloud the band was sized for
         int kcov = 20;
         std::vector<double> xyz;   // the full source cloud, input order (posing)
         std::vector<int32_t> pt;   // per tie: input index
@@ -500,7 +516,28 @@ struct orpcd_ctx {
         orpcd::DevBuf<int32_t> nbr, cnt, nn[2], dpos;
         orpcd::DedupBufs dedup;
         orpcd::FeatNNBufs fnn;
+        // orpcd_fgr_optimize_batch: the batch's posed sources (B x n x 3) and
+        // their features (B x n x 36), per-target points / features /
+        // evaluation layouts, and the per-start reduction partials, tuples,
+        // IRLS problem table and transforms
+        struct Batch {
+            orpcd::DevBuf<double> X, FB, part, pq, Tn, T, Q, txyz[orpcd::kMaxTargets], tfeat[orpcd::kMaxTargets];
+            orpcd::DevBuf<int64_t> meta;
+            orpcd::DevBuf<unsigned char> uflag;
+            orpcd::CloudLayout tlay[orpcd::kMaxTargets];
+            void release() {
+                for (auto* b : {&X, &FB, &part, &pq, &Tn, &T, &Q}) b->release();
+                for (int k = 0; k < orpcd::kMaxTargets; ++k) {
+                    txyz[k].release();
+                    tfeat[k].release();
+                    tlay[k].release();
+                }
+                meta.release();
+                uflag.release();
+            }
+        } bt;
         void release() {
+            bt.release();
             for (int k = 0; k < 2; ++k) {
                 xyz[k].release();
                 feat[k].release();
@@ -646,6 +683,13 @@ hipError_t expand_dup_answers(const DedupBufs& b, int64_t n, int64_t nu, const i
                               int32_t* out, hipStream_t s);
 hipError_t launch_fgr_irls(const double* p, double* q, int K, double par0, int iters, double division_factor,
                            double max_corr, int decrease_mu, double* T_out, hipStream_t s);
+// several IRLS problems in one launch each for the register- and the
+// memory-resident form: meta = {offset of p in pq (doubles), K, output slot} per problem
+hipError_t launch_fgr_irls_batch(const double* pq, const int64_t* meta_reg, int nreg, const int64_t* meta_mem,
+                                 int nmem, double par0, int iters, double division_factor, double max_corr,
+                                 int decrease_mu, double* T_out, hipStream_t s);
+// representative flags of dedup_rows (uflag_out[i] = row i is the lowest index of its equal rows)
+hipError_t dedup_flags(const double* F, int64_t n, DedupBufs& b, unsigned char* uflag_out, hipStream_t s);
 hipError_t launch_sum3(const double* xyz, int64_t n, double* part, hipStream_t s);
 hipError_t launch_maxnorm(const double* xyz, int64_t n, const double mean[3], double* part, hipStream_t s);
 hipError_t launch_transform_points(const double* in, int64_t n, const double* T, double* out, hipStream_t s);

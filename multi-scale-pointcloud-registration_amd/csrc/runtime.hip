@@ -9,6 +9,7 @@
 #include <cstring>
 #include <new>
 #include <random>
+#include <thread>
 #include <utility>
 
 #include "orpcd_internal.h"
@@ -38,6 +39,24 @@ namespace {
 bool finite_cloud(const double* xyz, int64_t n) {
     for (int64_t i = 0; i < 3 * n; ++i)
         if (!std::isfinite(xyz[i])) return false;
+    return true;
+}
+
+// Feature rows the matrix-core search can order: finite entries and a squared
+// norm <= 1e150, so every expansion |q|^2 + |t|^2 - 2 q.t stays finite and far
+// below the padded rows' kPadNorm (1e300); a larger row would give an inf
+// distance whose index-carrying key is a NaN (FPFH rows are histograms
+// normalised to 100 per bin group: |f|^2 <= 3e4).
+bool feature_rows_ok(const double* f, int64_t rows, int dim) {
+    for (int64_t r = 0; r < rows; ++r) {
+        double n2 = 0.0;
+        for (int k = 0; k < dim; ++k) {
+            const double v = f[r * dim + k];
+            if (!std::isfinite(v)) return false;
+            n2 += v * v;
+        }
+        if (!(n2 <= 1e150)) return false;
+    }
     return true;
 }
 
@@ -175,6 +194,32 @@ int fpfh_buffers(orpcd_ctx* c, int k, int64_t n, int fpfh_knn) {
     return ORPCD_OK;
 }
 
+// Normals + FPFH of the device cloud `pts` (input order; host_xyz its host
+// copy for the bounding box) into feat_out (n x 36), with c->aux as the
+// layout and the fgr scratch buffers (sized by fpfh_buffers).  Stream-ordered
+// throughout: no host synchronisation, so a batch can queue one cloud after
+// another.
+int fpfh_at(orpcd_ctx* c, const double* host_xyz, const double* pts, int64_t n, double normal_radius, int normal_knn,
+            double fpfh_radius, int fpfh_knn, double* feat_out) {
+    auto& F = c->fgr;
+    double margin = 0.0;
+    int rc = layout_from_device(c, host_xyz, pts, n, c->aux, true, &margin);
+    if (rc) return rc;
+    // the normals' and the features' neighbourhoods are the same search when
+    // their (radius, knn) agree (the FGR defaults: 0.1, 20): one KNN pass
+    // then writes the covariances and the neighbour lists together
+    const bool shared = normal_knn == fpfh_knn && normal_radius == fpfh_radius;
+    CTX_CHECK(c, launch_knn_tiles(c->aux, pts, normal_knn, normal_radius, margin, true, F.raw.p,
+                                  shared ? F.nbr.p : nullptr, shared ? F.nd2.p : nullptr, shared ? F.cnt.p : nullptr,
+                                  c->stream));
+    CTX_CHECK(c, launch_normals_cov(F.raw.p, n, nullptr, 1, -1.0, F.nrm.p, nullptr, c->stream));
+    if (!shared)  // compute_fpfh_feature's own neighbourhoods
+        CTX_CHECK(c, launch_knn_tiles(c->aux, pts, fpfh_knn, fpfh_radius, margin, true, nullptr, F.nbr.p, F.nd2.p,
+                                      F.cnt.p, c->stream));
+    CTX_CHECK(c, launch_fpfh(pts, F.nrm.p, n, F.nbr.p, F.nd2.p, F.cnt.p, fpfh_knn, F.spfh.p, feat_out, c->stream));
+    return ORPCD_OK;
+}
+
 int fpfh_device(orpcd_ctx* c, const double* host_xyz, int k, int64_t n, double normal_radius, int normal_knn,
                 double fpfh_radius, int fpfh_knn) {
     CTX_REQUIRE(c, normal_knn > 0 && normal_knn <= kMaxKnn && fpfh_knn > 0 && fpfh_knn <= kMaxKnn,
@@ -183,23 +228,7 @@ int fpfh_device(orpcd_ctx* c, const double* host_xyz, int k, int64_t n, double n
     int rc = fpfh_buffers(c, k, n, fpfh_knn);
     if (rc) return rc;
     auto& F = c->fgr;
-    double margin = 0.0;
-    rc = layout_from_device(c, host_xyz, F.xyz[k].p, n, c->aux, true, &margin);
-    if (rc) return rc;
-    // the normals' and the features' neighbourhoods are the same search when
-    // their (radius, knn) agree (the FGR defaults: 0.1, 20): one KNN pass
-    // then writes the covariances and the neighbour lists together
-    const bool shared = normal_knn == fpfh_knn && normal_radius == fpfh_radius;
-    CTX_CHECK(c, launch_knn_tiles(c->aux, F.xyz[k].p, normal_knn, normal_radius, margin, true, F.raw.p,
-                                  shared ? F.nbr.p : nullptr, shared ? F.nd2.p : nullptr, shared ? F.cnt.p : nullptr,
-                                  c->stream));
-    CTX_CHECK(c, launch_normals_cov(F.raw.p, n, nullptr, 1, -1.0, F.nrm.p, nullptr, c->stream));
-    if (shared) {
-        CTX_CHECK(c, launch_fpfh(F.xyz[k].p, F.nrm.p, n, F.nbr.p, F.nd2.p, F.cnt.p, fpfh_knn, F.spfh.p, F.feat[k].p,
-                                 c->stream));
-        return ORPCD_OK;
-    }
-    return features_device(c, nullptr, k, n, fpfh_radius, fpfh_knn, margin);
+    return fpfh_at(c, host_xyz, F.xyz[k].p, n, normal_radius, normal_knn, fpfh_radius, fpfh_knn, F.feat[k].p);
 }
 
 // compute_fpfh_feature of fgr.xyz[k] with the normals in fgr.nrm.  host_xyz
@@ -221,6 +250,82 @@ int features_device(orpcd_ctx* c, const double* host_xyz, int k, int64_t n, doub
 
 double norm3(const double* a) { return std::sqrt(a[0] * a[0] + a[1] * a[1] + a[2] * a[2]); }
 
+// O3D FastGlobalRegistration.cpp NormalizePointCloud's result for one cloud:
+// (p - mean) / scale (scale: the larger of the two clouds' max |p - mean|).
+struct FgrCloud {
+    const double* xyz = nullptr;  // host, input order
+    double mean[3] = {0.0, 0.0, 0.0};
+    void at(int64_t i, double scale, double out[3]) const {
+        for (int a = 0; a < 3; ++a) out[a] = (xyz[3 * i + a] - mean[a]) / scale;
+    }
+};
+
+// AdvancedMatching's tuple test (Open3D's sequential mt19937 draws, seeded:
+// DESIGN.md §2) over the cross-checked pairs `corres` (i in cloud fi, j in
+// cloud fj), then the tuples as (source, target) rows, normalised: p[K x 3]
+// followed by q[K x 3] in pq.  Returns K.
+int fgr_tuples(const std::vector<std::pair<int, int>>& corres, const orpcd_fgr_params& p, const FgrCloud cl[2],
+               double scale, int fi, int fj, std::vector<double>& pq) {
+    const int ncorr = (int)corres.size();
+    std::vector<std::pair<int, int>> tup;
+    if (ncorr > 0) {
+        std::mt19937 gen((std::mt19937::result_type)p.seed);
+        std::uniform_int_distribution<int> dis(0, ncorr - 1);
+        const int64_t trials = (int64_t)ncorr * 100;
+        const double sc = p.tuple_scale;
+        int cnt = 0;
+        for (int64_t t = 0; t < trials; ++t) {
+            const int r[3] = {dis(gen), dis(gen), dis(gen)};
+            double pi[3][3], pj[3][3];
+            for (int e = 0; e < 3; ++e) {
+                cl[fi].at(corres[r[e]].first, scale, pi[e]);
+                cl[fj].at(corres[r[e]].second, scale, pj[e]);
+            }
+            double li[3], lj[3];
+            for (int e = 0; e < 3; ++e) {
+                const int f = (e + 1) % 3;
+                const double di[3] = {pi[e][0] - pi[f][0], pi[e][1] - pi[f][1], pi[e][2] - pi[f][2]};
+                const double dj[3] = {pj[e][0] - pj[f][0], pj[e][1] - pj[f][1], pj[e][2] - pj[f][2]};
+                li[e] = norm3(di);
+                lj[e] = norm3(dj);
+            }
+            if ((li[0] * sc < lj[0]) && (lj[0] < li[0] / sc) && (li[1] * sc < lj[1]) && (lj[1] < li[1] / sc) &&
+                (li[2] * sc < lj[2]) && (lj[2] < li[2] / sc)) {
+                for (int e = 0; e < 3; ++e) tup.push_back(corres[r[e]]);
+                ++cnt;
+            }
+            if (cnt >= p.maximum_tuple_count) break;
+        }
+    }
+    // pairs back to (source, target)
+    const int K = (int)tup.size();
+    pq.assign((size_t)std::max(K, 1) * 6, 0.0);
+    for (int e = 0; e < K; ++e) {
+        const int si = fi == 0 ? tup[e].first : tup[e].second;
+        const int ti = fi == 0 ? tup[e].second : tup[e].first;
+        cl[0].at(si, scale, &pq[(size_t)3 * e]);
+        cl[1].at(ti, scale, &pq[(size_t)3 * K + 3 * e]);
+    }
+    return K;
+}
+
+// GetInvTransformationOriginalScale: the normalised-frame Tn back to the
+// clouds' own frames (Open3D's column convention).
+void fgr_original_scale(const double Tn[16], const double mean_src[3], const double mean_tgt[3], double scale,
+                        double T[16]) {
+    double inner[3];
+    for (int a = 0; a < 3; ++a) {
+        const double mr = Tn[4 * a] * mean_tgt[0] + Tn[4 * a + 1] * mean_tgt[1] + Tn[4 * a + 2] * mean_tgt[2];
+        inner[a] = -mr + Tn[4 * a + 3] * scale + mean_src[a];
+    }
+    for (int a = 0; a < 16; ++a) T[a] = 0.0;
+    for (int a = 0; a < 3; ++a) {
+        for (int b = 0; b < 3; ++b) T[4 * a + b] = Tn[4 * b + a];
+        T[4 * a + 3] = -(Tn[a] * inner[0] + Tn[4 + a] * inner[1] + Tn[8 + a] * inner[2]);
+    }
+    T[15] = 1.0;
+}
+
 // ORPCD_FGR_TRACE=1: the FGR path's phases on stderr (each mark drains the
 // stream first, so the phases' own times, not their overlap)
 struct FgrTrace {
@@ -237,6 +342,61 @@ struct FgrTrace {
 thread_local FgrTrace* g_fgr_trace = nullptr;
 static void fgr_mark(hipStream_t s, const char* what) {
     if (g_fgr_trace) g_fgr_trace->mark(s, what);
+}
+
+// AdvancedMatching's initial matching and cross check over padded feature
+// rows on the device (source n rows, target m rows): nearest rows both ways
+// on the matrix cores (launch_feat_nn, exact), then (i, i_to_j[i]) with
+// j_to_i[i_to_j[i]] == i in i order, i over the larger set (fi; Open3D
+// swaps the roles when the target has more points).  same_features: the two
+// sets are the same rows (Q4 on equal-size clouds, fastGlobalOptimizer.py:
+// 137-142, or identical caller features).
+int fgr_match(orpcd_ctx* c, const double* fsrc, int64_t n, const double* ftgt, int64_t m, bool same_features,
+              std::vector<std::pair<int, int>>& corres) {
+    auto& F = c->fgr;
+    hipStream_t s = c->stream;
+    const int64_t np[2] = {n, m};
+    const double* feat[2] = {fsrc, ftgt};
+    int fi = 0, fj = 1;
+    if (np[1] > np[0]) std::swap(fi, fj);
+    const int64_t nPti = np[fi], nPtj = np[fj];
+    for (int k = 0; k < 2; ++k) {
+        CTX_CHECK(c, F.fn2[k].ensure((size_t)np[k]));
+        CTX_CHECK(c, launch_feat_norm(feat[k], np[k], F.fn2[k].p, s));
+    }
+    CTX_CHECK(c, F.nn[0].ensure((size_t)nPtj));
+    CTX_CHECK(c, F.nn[1].ensure((size_t)nPti));
+    int64_t nu = 0;
+    CTX_CHECK(c, dedup_rows(feat[fi], F.fn2[fi].p, nPti, F.dedup, &nu, s));
+    if (same_features) {
+        // the second direction is the first one's problem input for input,
+        // and identical query rows have identical answers, so one search
+        // runs, over the distinct rows against themselves (F.nn[1] as its
+        // output), and every row takes its representative's answer
+        CTX_CHECK(c, F.dpos.ensure((size_t)nPti));
+        CTX_CHECK(c, launch_feat_nn(F.dedup.Fu.p, F.dedup.n2u.p, nu, F.dedup.Fu.p, F.dedup.n2u.p, nu, F.dedup.uidx.p,
+                                    33, F.fnn, F.nn[1].p, s, c->profiling ? c->stats.feat : nullptr));
+        CTX_CHECK(c, expand_dup_answers(F.dedup, nPti, nu, F.nn[1].p, F.dpos.p, F.nn[0].p, s));
+        CTX_CHECK(c, hipMemcpyAsync(F.nn[1].p, F.nn[0].p, (size_t)nPti * 4, hipMemcpyDeviceToDevice, s));
+    } else {
+        CTX_CHECK(c, launch_feat_nn(feat[fj], F.fn2[fj].p, nPtj, F.dedup.Fu.p, F.dedup.n2u.p, nu, F.dedup.uidx.p, 33,
+                                    F.fnn, F.nn[0].p, s, c->profiling ? c->stats.feat : nullptr));
+        CTX_CHECK(c, dedup_rows(feat[fj], F.fn2[fj].p, nPtj, F.dedup, &nu, s));
+        CTX_CHECK(c, launch_feat_nn(feat[fi], F.fn2[fi].p, nPti, F.dedup.Fu.p, F.dedup.n2u.p, nu, F.dedup.uidx.p, 33,
+                                    F.fnn, F.nn[1].p, s, c->profiling ? c->stats.feat : nullptr));
+    }
+    fgr_mark(s, "feature matching");
+    std::vector<int32_t> j_to_i((size_t)nPtj), i_to_j((size_t)nPti);
+    CTX_CHECK(c, d2h(j_to_i.data(), F.nn[0].p, (size_t)nPtj * 4, s));
+    CTX_CHECK(c, d2h(i_to_j.data(), F.nn[1].p, (size_t)nPti * 4, s));
+    CTX_CHECK(c, hipStreamSynchronize(s));
+    // cross check, in i order: (i, i_to_j[i]) with j_to_i[i_to_j[i]] == i
+    corres.clear();
+    for (int64_t i = 0; i < nPti; ++i) {
+        const int j = i_to_j[i];
+        if (j >= 0 && j < nPtj && j_to_i[j] == i) corres.push_back({(int)i, j});
+    }
+    return ORPCD_OK;
 }
 
 // O3D FastGlobalRegistration.cpp: NormalizePointCloud, AdvancedMatching,
@@ -274,94 +434,23 @@ int fgr_device(orpcd_ctx* c, const double* src, int64_t n, const double* tgt, in
         scale = std::max(scale, mx);
     }
     CTX_REQUIRE(c, scale > 0.0, "fgr: degenerate clouds (all points at their mean)");
-    auto normalised = [&](int k, int64_t i, double out[3]) {
-        for (int a = 0; a < 3; ++a) out[a] = (host[k][3 * i + a] - mean[k][a]) / scale;
-    };
+    FgrCloud cl[2];
+    for (int k = 0; k < 2; ++k) {
+        cl[k].xyz = host[k];
+        for (int a = 0; a < 3; ++a) cl[k].mean[a] = mean[k][a];
+    }
     fgr_mark(s, "normalisation");
     // --- initial matching on the matrix cores, both directions
     int fi = 0, fj = 1;
     if (np[1] > np[0]) std::swap(fi, fj);
-    const int64_t nPti = np[fi], nPtj = np[fj];
-    for (int k = 0; k < 2; ++k) {
-        CTX_CHECK(c, F.fn2[k].ensure((size_t)np[k]));
-        CTX_CHECK(c, launch_feat_norm(F.feat[k].p, np[k], F.fn2[k].p, s));
-    }
-    CTX_CHECK(c, F.nn[0].ensure((size_t)nPtj));
-    CTX_CHECK(c, F.nn[1].ensure((size_t)nPti));
-    int64_t nu = 0;
-    CTX_CHECK(c, dedup_rows(F.feat[fi].p, F.fn2[fi].p, nPti, F.dedup, &nu, s));
-    if (same_features) {
-        // The two feature sets are the same rows (Q4 on equal-size clouds,
-        // fastGlobalOptimizer.py:137-142, or identical caller features): the
-        // second direction is the first one's problem input for input, and
-        // identical query rows have identical answers, so one search runs,
-        // over the distinct rows against themselves (F.nn[1] as its output),
-        // and every row takes its representative's answer.
-        CTX_CHECK(c, F.dpos.ensure((size_t)nPti));
-        CTX_CHECK(c, launch_feat_nn(F.dedup.Fu.p, F.dedup.n2u.p, nu, F.dedup.Fu.p, F.dedup.n2u.p, nu, F.dedup.uidx.p,
-                                    33, F.fnn, F.nn[1].p, s, c->profiling ? c->stats.feat : nullptr));
-        CTX_CHECK(c, expand_dup_answers(F.dedup, nPti, nu, F.nn[1].p, F.dpos.p, F.nn[0].p, s));
-        CTX_CHECK(c, hipMemcpyAsync(F.nn[1].p, F.nn[0].p, (size_t)nPti * 4, hipMemcpyDeviceToDevice, s));
-    } else {
-        CTX_CHECK(c, launch_feat_nn(F.feat[fj].p, F.fn2[fj].p, nPtj, F.dedup.Fu.p, F.dedup.n2u.p, nu, F.dedup.uidx.p,
-                                    33, F.fnn, F.nn[0].p, s, c->profiling ? c->stats.feat : nullptr));
-        CTX_CHECK(c, dedup_rows(F.feat[fj].p, F.fn2[fj].p, nPtj, F.dedup, &nu, s));
-        CTX_CHECK(c, launch_feat_nn(F.feat[fi].p, F.fn2[fi].p, nPti, F.dedup.Fu.p, F.dedup.n2u.p, nu, F.dedup.uidx.p,
-                                    33, F.fnn, F.nn[1].p, s, c->profiling ? c->stats.feat : nullptr));
-    }
-    fgr_mark(s, "feature matching");
-    std::vector<int32_t> j_to_i((size_t)nPtj), i_to_j((size_t)nPti);
-    CTX_CHECK(c, d2h(j_to_i.data(), F.nn[0].p, (size_t)nPtj * 4, s));
-    CTX_CHECK(c, d2h(i_to_j.data(), F.nn[1].p, (size_t)nPti * 4, s));
-    CTX_CHECK(c, hipStreamSynchronize(s));
-    // --- cross check, in i order: (i, i_to_j[i]) with j_to_i[i_to_j[i]] == i
     std::vector<std::pair<int, int>> corres;
-    for (int64_t i = 0; i < nPti; ++i) {
-        const int j = i_to_j[i];
-        if (j >= 0 && j < nPtj && j_to_i[j] == i) corres.push_back({(int)i, j});
-    }
+    int rc = fgr_match(c, F.feat[0].p, n, F.feat[1].p, m, same_features, corres);
+    if (rc) return rc;
     // --- tuple test: Open3D's sequential mt19937 draws (RNG-bound, host)
     const int ncorr = (int)corres.size();
-    std::vector<std::pair<int, int>> tup;
-    if (ncorr > 0) {
-        std::mt19937 gen((std::mt19937::result_type)p.seed);
-        std::uniform_int_distribution<int> dis(0, ncorr - 1);
-        const int64_t trials = (int64_t)ncorr * 100;
-        const double sc = p.tuple_scale;
-        int cnt = 0;
-        for (int64_t t = 0; t < trials; ++t) {
-            const int r[3] = {dis(gen), dis(gen), dis(gen)};
-            double pi[3][3], pj[3][3];
-            for (int e = 0; e < 3; ++e) {
-                normalised(fi, corres[r[e]].first, pi[e]);
-                normalised(fj, corres[r[e]].second, pj[e]);
-            }
-            double li[3], lj[3];
-            for (int e = 0; e < 3; ++e) {
-                const int f = (e + 1) % 3;
-                const double di[3] = {pi[e][0] - pi[f][0], pi[e][1] - pi[f][1], pi[e][2] - pi[f][2]};
-                const double dj[3] = {pj[e][0] - pj[f][0], pj[e][1] - pj[f][1], pj[e][2] - pj[f][2]};
-                li[e] = norm3(di);
-                lj[e] = norm3(dj);
-            }
-            if ((li[0] * sc < lj[0]) && (lj[0] < li[0] / sc) && (li[1] * sc < lj[1]) && (lj[1] < li[1] / sc) &&
-                (li[2] * sc < lj[2]) && (lj[2] < li[2] / sc)) {
-                for (int e = 0; e < 3; ++e) tup.push_back(corres[r[e]]);
-                ++cnt;
-            }
-            if (cnt >= p.maximum_tuple_count) break;
-        }
-    }
+    std::vector<double> pq;
+    const int K = fgr_tuples(corres, p, cl, scale, fi, fj, pq);
     fgr_mark(s, "cross check + tuple test");
-    // pairs back to (source, target)
-    const int K = (int)tup.size();
-    std::vector<double> pq((size_t)std::max(K, 1) * 6);
-    for (int e = 0; e < K; ++e) {
-        const int si = fi == 0 ? tup[e].first : tup[e].second;
-        const int ti = fi == 0 ? tup[e].second : tup[e].first;
-        normalised(0, si, &pq[(size_t)3 * e]);
-        normalised(1, ti, &pq[(size_t)3 * K + 3 * e]);
-    }
     // --- GNC / Geman-McClure IRLS in one workgroup (fp64)
     CTX_CHECK(c, F.pq.ensure(pq.size()));
     CTX_CHECK(c, F.Tn.ensure(16));
@@ -373,20 +462,11 @@ int fgr_device(orpcd_ctx* c, const double* src, int64_t n, const double* tgt, in
     CTX_CHECK(c, hipStreamSynchronize(s));
     fgr_mark(s, "irls");
     // --- GetInvTransformationOriginalScale (4x4 algebra)
-    double T[16] = {0};
-    double inner[3];
-    for (int a = 0; a < 3; ++a) {
-        const double mr = Tn[4 * a] * mean[1][0] + Tn[4 * a + 1] * mean[1][1] + Tn[4 * a + 2] * mean[1][2];
-        inner[a] = -mr + Tn[4 * a + 3] * scale + mean[0][a];
-    }
-    for (int a = 0; a < 3; ++a) {
-        for (int b = 0; b < 3; ++b) T[4 * a + b] = Tn[4 * b + a];
-        T[4 * a + 3] = -(Tn[a] * inner[0] + Tn[4 + a] * inner[1] + Tn[8 + a] * inner[2]);
-    }
-    T[15] = 1.0;
+    double T[16];
+    fgr_original_scale(Tn, mean[0], mean[1], scale, T);
     // --- EvaluateRegistration(source, target, max_corr, T); the target is
     // already on the device (F.xyz[1])
-    int rc = layout_from_device(c, tgt, F.xyz[1].p, m, c->aux, true);
+    rc = layout_from_device(c, tgt, F.xyz[1].p, m, c->aux, true);
     if (rc) return rc;
     CTX_CHECK(c, F.raw.ensure((size_t)n * 3 + 16));
     CTX_CHECK(c, c->scratch32.ensure((size_t)n));
@@ -463,6 +543,7 @@ int source_ties_detect(orpcd_ctx* c, const CloudLayout& L, const double* dev_in6
     double A = 0.0;
     for (int a = 0; a < 3; ++a) A = std::max(A, std::max(std::fabs(L.lo[a]), std::fabs(L.hi[a])));
     const double abs_coef = kTieAbs * (1.0 + A);
+    T.band_A = A;
     CTX_CHECK(c, c->tie_cnt.ensure(1));
     CTX_CHECK(c, c->tie_rows.ensure((size_t)kTieCap * (K + 2)));
     CTX_CHECK(c, c->tie_d2.ensure((size_t)kTieCap * K));
@@ -599,6 +680,19 @@ void tie_posed_rows(const orpcd_ctx::SourceTies& T, int b, const double* R0, con
 int source_ties_apply(orpcd_ctx* c, const double* R0, const double* t0, int B, double eps) {
     auto& T = c->ties;
     T.last_sets.clear();
+    if (T.on) {
+        // starts whose ties may not all be re-decided (statistics, surfaced
+        // as GeneralizedICP.spec_stats["tie_gaps"]): the table overflowed
+        // (kTieCap / the brute-force budget), or the posed copy's coordinates
+        // exceed what the band's absolute term assumes: posing rounds a
+        // coordinate by ~u |x R0 + t0| <= u (sqrt(3) A + |t0|), and kTieAbs
+        // (1 + A) holds ~2000x that for |x R0 + t0| <= 1000 (1 + A)
+        for (int b = 0; b < B; ++b) {
+            double tb = 0.0;
+            for (int k = 0; k < 3; ++k) tb = std::max(tb, std::fabs(t0[3 * b + k]));
+            if (!T.complete || std::sqrt(3.0) * T.band_A + tb > 1000.0 * (1.0 + T.band_A)) c->stats.tie_gaps += 1;
+        }
+    }
     if (!T.on || T.pt.empty()) {
         T.posed_slot.clear();
         return ORPCD_OK;
@@ -760,6 +854,23 @@ int run_passes(orpcd_ctx* c, int B, const orpcd_gicp_params* p, double* T_out, d
 int read_outputs(orpcd_ctx* c, int B, unsigned long long tiles_before, double* T_out, double* rmse_out,
                  double* fitness_out, int32_t* iters_out, int64_t* ncorr_out);
 
+// f(b) for b in [0, n) on up to 16 host threads (the GPU box grants 16 cores;
+// every b writes only its own outputs)
+template <typename Fn>
+void host_parallel(int n, Fn f) {
+    const int nt = std::max(1, std::min({n, 16, (int)std::max(1u, std::thread::hardware_concurrency())}));
+    if (nt <= 1) {
+        for (int b = 0; b < n; ++b) f(b);
+        return;
+    }
+    std::vector<std::thread> th;
+    for (int t = 0; t < nt; ++t)
+        th.emplace_back([&, t] {
+            for (int b = t; b < n; b += nt) f(b);
+        });
+    for (auto& x : th) x.join();
+}
+
 }  // namespace
 
 extern "C" {
@@ -907,6 +1018,15 @@ int orpcd_gicp_batch_targets(orpcd_ctx* c, const double* R0, const double* t0, c
                              int32_t B, const orpcd_gicp_params* p, double* T_out, double* rmse_out,
                              double* fitness_out, int32_t* iters_out, int64_t* ncorr_out) {
     if (!c) return ORPCD_EINVAL;
+    // the caller's posed tie rows (orpcd_set_posed_tie_rows) belong to this
+    // call only: taken before any validation, so a rejected batch never
+    // leaves them for the next one
+    auto& TS = c->ties;
+    std::vector<double> posed;
+    posed.swap(TS.posed);
+    const int posed_B = TS.posed_B;
+    TS.posed_B = 0;
+    TS.posed_slot.clear();
     CTX_REQUIRE(c, R0 && t0 && p && T_out && rmse_out, "gicp_batch: null argument");
     CTX_REQUIRE(c, B > 0, "gicp_batch: B must be > 0");
     CTX_REQUIRE(c, c->src.n > 0, "gicp_batch: no source (call orpcd_set_source)");
@@ -935,16 +1055,11 @@ int orpcd_gicp_batch_targets(orpcd_ctx* c, const double* R0, const double* t0, c
         for (int b = 0; b < B; ++b) pos[b] = b;
     }
     CTX_CHECK(c, hipSetDevice(c->device));
-    auto& TS = c->ties;
-    TS.posed_slot.clear();
-    if (TS.posed_B) {  // orpcd_set_posed_tie_rows: caller order -> slot order
-        const int pb = TS.posed_B;
-        TS.posed_B = 0;
-        CTX_REQUIRE(c, pb == B, "gicp_batch: posed tie rows were set for a different number of starts");
+    if (posed_B) {  // caller order -> slot order
+        CTX_REQUIRE(c, posed_B == B, "gicp_batch: posed tie rows were set for a different number of starts");
         const size_t w = TS.rows.size() * 3;
         TS.posed_slot.resize((size_t)B * w);
-        for (int b = 0; b < B; ++b) std::memcpy(&TS.posed_slot[(size_t)pos[b] * w], &TS.posed[(size_t)b * w], w * 8);
-        TS.posed.clear();
+        for (int b = 0; b < B; ++b) std::memcpy(&TS.posed_slot[(size_t)pos[b] * w], &posed[(size_t)b * w], w * 8);
     }
     int rc = targets_for_epsilon(c, ntg, p->epsilon);  // target covariances depend on epsilon
     if (rc) return rc;
@@ -1654,8 +1769,8 @@ int orpcd_fgr(orpcd_ctx* c, const double* src, int64_t n, const double* tgt, int
     int rc = check_fgr_params(c, p);
     if (rc) return rc;
     CTX_REQUIRE(c, finite_cloud(src, n) && finite_cloud(tgt, m), "fgr: non-finite coordinates");
-    for (int64_t i = 0; i < 33 * n; ++i) CTX_REQUIRE(c, std::isfinite(src_feat[i]), "fgr: non-finite feature");
-    for (int64_t i = 0; i < 33 * m; ++i) CTX_REQUIRE(c, std::isfinite(tgt_feat[i]), "fgr: non-finite feature");
+    CTX_REQUIRE(c, feature_rows_ok(src_feat, n, 33) && feature_rows_ok(tgt_feat, m, 33),
+                "fgr: non-finite feature, or a feature row with squared norm above 1e150");
     CTX_CHECK(c, hipSetDevice(c->device));
     const double* xyz[2] = {src, tgt};
     const double* feat[2] = {src_feat, tgt_feat};
@@ -1677,8 +1792,8 @@ int orpcd_feature_nn(orpcd_ctx* c, const double* q, int64_t nq, const double* t,
     if (!c) return ORPCD_EINVAL;
     CTX_REQUIRE(c, q && t && idx_out && nq >= 0 && nt > 0, "feature_nn: bad arguments");
     CTX_REQUIRE(c, dim > 0 && dim <= kFeatDim, "feature_nn: dim must be in [1, 36]");
-    for (int64_t i = 0; i < nq * dim; ++i) CTX_REQUIRE(c, std::isfinite(q[i]), "feature_nn: non-finite value");
-    for (int64_t i = 0; i < nt * dim; ++i) CTX_REQUIRE(c, std::isfinite(t[i]), "feature_nn: non-finite value");
+    CTX_REQUIRE(c, feature_rows_ok(q, nq, dim) && feature_rows_ok(t, nt, dim),
+                "feature_nn: non-finite value, or a row with squared norm above 1e150");
     if (nq == 0) return ORPCD_OK;
     CTX_CHECK(c, hipSetDevice(c->device));
     auto& F = c->fgr;
@@ -1741,6 +1856,203 @@ int orpcd_fgr_optimize(orpcd_ctx* c, const double* src, int64_t n, const double*
     fgr_mark(c->stream, "target normals + fpfh");
     return fgr_device(c, src, n, tgt, m, *p, T_out, fitness_out, rmse_out, ncorr_out, n_mutual_out,
                       target_features_from_source && m == n);
+}
+
+int orpcd_fgr_optimize_batch(orpcd_ctx* c, const double* src, int64_t n, const double* tgts, const int64_t* m,
+                             int32_t ntgt, const double* R0, const double* t0, const int32_t* target_of_start,
+                             int32_t B, double normal_radius, int32_t normal_knn, double fpfh_radius, int32_t fpfh_knn,
+                             int32_t target_features_from_source, const orpcd_fgr_params* p, double* T_out,
+                             double* fitness_out, double* rmse_out, int64_t* ncorr_out, int64_t* n_mutual_out) {
+    if (!c) return ORPCD_EINVAL;
+    CTX_REQUIRE(c, src && tgts && m && R0 && t0 && p && T_out && n > 0 && n < kMaxPoints && B > 0,
+                "fgr_optimize_batch: bad arguments");
+    CTX_REQUIRE(c, ntgt >= 1 && ntgt <= kMaxTargets, "fgr_optimize_batch: 1..16 targets");
+    int rc = check_fgr_params(c, p);
+    if (rc) return rc;
+    CTX_REQUIRE(c, normal_knn > 0 && normal_knn <= kMaxKnn && fpfh_knn > 0 && fpfh_knn <= kMaxKnn,
+                "fpfh: knn must be in [1, 1024]");
+    CTX_REQUIRE(c, normal_radius > 0 && fpfh_radius > 0, "fpfh: radii must be > 0");
+    const bool q4 = target_features_from_source != 0;
+    std::vector<int64_t> toff((size_t)ntgt + 1, 0);
+    for (int k = 0; k < ntgt; ++k) {
+        CTX_REQUIRE(c, m[k] > 0 && m[k] < kMaxPoints, "fgr_optimize_batch: bad target size");
+        CTX_REQUIRE(c, !q4 || m[k] <= n,
+                    "fgr_optimize_batch: target features taken from the source need m <= n "
+                    "(fastGlobalOptimizer.py:137-142 would index past the source's features)");
+        toff[k + 1] = toff[k] + m[k];
+    }
+    std::vector<int> tk((size_t)B, 0);
+    for (int b = 0; b < B; ++b) {
+        tk[b] = target_of_start ? target_of_start[b] : 0;
+        CTX_REQUIRE(c, tk[b] >= 0 && tk[b] < ntgt, "fgr_optimize_batch: target index out of range");
+    }
+    CTX_REQUIRE(c, finite_cloud(src, n) && finite_cloud(tgts, toff[ntgt]), "fgr_optimize_batch: non-finite coordinates");
+    for (int64_t i = 0; i < 9 * (int64_t)B; ++i) CTX_REQUIRE(c, std::isfinite(R0[i]), "fgr_optimize_batch: non-finite R0");
+    for (int64_t i = 0; i < 3 * (int64_t)B; ++i) CTX_REQUIRE(c, std::isfinite(t0[i]), "fgr_optimize_batch: non-finite t0");
+    CTX_CHECK(c, hipSetDevice(c->device));
+    auto& F = c->fgr;
+    auto& bt = F.bt;
+    hipStream_t s = c->stream;
+    // --- targets, once each: points, normalisation (mean, max |p - mean|),
+    // the evaluation's layout, and their own features unless Q4
+    std::vector<double> tmean((size_t)ntgt * 3), tmax((size_t)ntgt);
+    for (int k = 0; k < ntgt; ++k) {
+        const double* tg = tgts + 3 * toff[k];
+        const int64_t mk = m[k], nb = (mk + 255) / 256;
+        CTX_CHECK(c, bt.txyz[k].ensure((size_t)mk * 3));
+        CTX_CHECK(c, h2d(bt.txyz[k].p, tg, (size_t)mk * 24, s));
+        CTX_CHECK(c, F.red.ensure((size_t)nb * 3));
+        std::vector<double> part((size_t)nb * 3);
+        CTX_CHECK(c, launch_sum3(bt.txyz[k].p, mk, F.red.p, s));
+        CTX_CHECK(c, d2h(part.data(), F.red.p, part.size() * 8, s));
+        double sum[3] = {0.0, 0.0, 0.0};
+        for (int64_t q = 0; q < nb; ++q)
+            for (int a = 0; a < 3; ++a) sum[a] += part[(size_t)3 * q + a];
+        for (int a = 0; a < 3; ++a) tmean[3 * k + a] = sum[a] / (double)mk;
+        CTX_CHECK(c, launch_maxnorm(bt.txyz[k].p, mk, &tmean[3 * k], F.red.p, s));
+        CTX_CHECK(c, d2h(part.data(), F.red.p, (size_t)nb * 8, s));
+        double mx = 0.0;
+        for (int64_t q = 0; q < nb; ++q) mx = std::max(mx, part[(size_t)q]);
+        tmax[k] = mx;
+        if (!q4) {
+            rc = fpfh_buffers(c, 1, mk, fpfh_knn);
+            if (rc) return rc;
+            CTX_CHECK(c, bt.tfeat[k].ensure((size_t)mk * kFeatDim));
+            rc = fpfh_at(c, tg, bt.txyz[k].p, mk, normal_radius, normal_knn, fpfh_radius, fpfh_knn, bt.tfeat[k].p);
+            if (rc) return rc;
+        }
+        rc = layout_from_device(c, tg, bt.txyz[k].p, mk, bt.tlay[k], true);
+        if (rc) return rc;
+    }
+    // --- the posed sources source @ R0[b] + t0[b], rounded as numpy forms
+    // them (pose_row), and their normals + FPFH, queued start after start
+    std::vector<double> P((size_t)B * n * 3);
+    host_parallel(B, [&](int b) {
+        for (int64_t i = 0; i < n; ++i) pose_row(src + 3 * i, R0 + 9 * b, t0 + 3 * b, &P[((size_t)b * n + i) * 3]);
+    });
+    CTX_CHECK(c, bt.X.ensure((size_t)B * n * 3));
+    CTX_CHECK(c, bt.FB.ensure((size_t)B * n * kFeatDim));
+    CTX_CHECK(c, h2d(bt.X.p, P.data(), P.size() * 8, s));
+    rc = fpfh_buffers(c, 0, n, fpfh_knn);
+    if (rc) return rc;
+    for (int b = 0; b < B; ++b) {
+        rc = fpfh_at(c, &P[(size_t)b * n * 3], bt.X.p + (size_t)b * n * 3, n, normal_radius, normal_knn, fpfh_radius,
+                     fpfh_knn, bt.FB.p + (size_t)b * n * kFeatDim);
+        if (rc) return rc;
+    }
+    // --- normalisation of every posed source (fixed-order partials, one read-back per phase)
+    const int64_t nb = (n + 255) / 256;
+    CTX_CHECK(c, bt.part.ensure((size_t)B * nb * 3));
+    std::vector<double> part((size_t)B * nb * 3), smean((size_t)B * 3), scale((size_t)B);
+    for (int b = 0; b < B; ++b) CTX_CHECK(c, launch_sum3(bt.X.p + (size_t)b * n * 3, n, bt.part.p + (size_t)b * nb * 3, s));
+    CTX_CHECK(c, d2h(part.data(), bt.part.p, part.size() * 8, s));
+    for (int b = 0; b < B; ++b) {
+        double sum[3] = {0.0, 0.0, 0.0};
+        for (int64_t q = 0; q < nb; ++q)
+            for (int a = 0; a < 3; ++a) sum[a] += part[((size_t)b * nb + q) * 3 + a];
+        for (int a = 0; a < 3; ++a) smean[3 * b + a] = sum[a] / (double)n;
+        CTX_CHECK(c, launch_maxnorm(bt.X.p + (size_t)b * n * 3, n, &smean[3 * b], bt.part.p + (size_t)b * nb, s));
+    }
+    CTX_CHECK(c, d2h(part.data(), bt.part.p, (size_t)B * nb * 8, s));
+    for (int b = 0; b < B; ++b) {
+        double mx = 0.0;
+        for (int64_t q = 0; q < nb; ++q) mx = std::max(mx, part[(size_t)b * nb + q]);
+        scale[b] = std::max(std::max(0.0, mx), tmax[tk[b]]);
+        CTX_REQUIRE(c, scale[b] > 0.0, "fgr: degenerate clouds (all points at their mean)");
+    }
+    // --- initial matching + cross check per start
+    std::vector<std::vector<std::pair<int, int>>> corres((size_t)B);
+    if (q4) {
+        // Q4 (the target's features are the posed source's own first m rows):
+        // every row's nearest feature row is the lowest index of its exact
+        // duplicates (distance 0; any other row is strictly farther), in both
+        // directions, so the mutual pairs are (i, i) for the rows i < m that
+        // are their own representative -- what the per-call path's exact
+        // searches return (fgr_match; for i >= m the target-side answer
+        // rep(j) <= j < m <= i can never point back).  No search is needed.
+        CTX_CHECK(c, bt.uflag.ensure((size_t)B * n));
+        for (int b = 0; b < B; ++b)
+            CTX_CHECK(c, dedup_flags(bt.FB.p + (size_t)b * n * kFeatDim, n, F.dedup, bt.uflag.p + (size_t)b * n, s));
+        std::vector<unsigned char> fl((size_t)B * n);
+        CTX_CHECK(c, d2h(fl.data(), bt.uflag.p, fl.size(), s));
+        for (int b = 0; b < B; ++b)
+            for (int64_t i = 0; i < m[tk[b]]; ++i)
+                if (fl[(size_t)b * n + i]) corres[b].push_back({(int)i, (int)i});
+    } else {
+        for (int b = 0; b < B; ++b) {
+            rc = fgr_match(c, bt.FB.p + (size_t)b * n * kFeatDim, n, bt.tfeat[tk[b]].p, m[tk[b]], false, corres[b]);
+            if (rc) return rc;
+        }
+    }
+    // --- tuple tests (host, one mt19937 per start, in parallel)
+    std::vector<std::vector<double>> pqs((size_t)B);
+    std::vector<int> K((size_t)B);
+    host_parallel(B, [&](int b) {
+        FgrCloud cl[2];
+        cl[0].xyz = &P[(size_t)b * n * 3];
+        cl[1].xyz = tgts + 3 * toff[tk[b]];
+        for (int a = 0; a < 3; ++a) {
+            cl[0].mean[a] = smean[3 * b + a];
+            cl[1].mean[a] = tmean[3 * tk[b] + a];
+        }
+        const int fi = m[tk[b]] > n ? 1 : 0;
+        K[b] = fgr_tuples(corres[b], *p, cl, scale[b], fi, 1 - fi, pqs[b]);
+    });
+    // --- IRLS: every start's problem in one launch (one workgroup each)
+    std::vector<int64_t> meta_reg, meta_mem;
+    int64_t off = 0;
+    for (int b = 0; b < B; ++b) {
+        auto& mt = K[b] <= 512 * 6 ? meta_reg : meta_mem;  // kIrlsThreads x kIrlsPer: launch_fgr_irls's split
+        mt.insert(mt.end(), {off, (int64_t)K[b], (int64_t)b});
+        off += 6 * (int64_t)std::max(K[b], 1);
+    }
+    std::vector<double> pq((size_t)off);
+    for (int b = 0, o = 0; b < B; o += 6 * std::max(K[b], 1), ++b)
+        std::memcpy(&pq[(size_t)o], pqs[b].data(), (size_t)6 * std::max(K[b], 1) * 8);
+    std::vector<int64_t> meta(meta_reg);
+    meta.insert(meta.end(), meta_mem.begin(), meta_mem.end());
+    CTX_CHECK(c, bt.pq.ensure(pq.size()));
+    CTX_CHECK(c, bt.meta.ensure(meta.size()));
+    CTX_CHECK(c, bt.Tn.ensure((size_t)B * 16));
+    CTX_CHECK(c, h2d(bt.pq.p, pq.data(), pq.size() * 8, s));
+    CTX_CHECK(c, h2d(bt.meta.p, meta.data(), meta.size() * 8, s));
+    const int nreg = (int)meta_reg.size() / 3, nmem = (int)meta_mem.size() / 3;
+    CTX_CHECK(c, launch_fgr_irls_batch(bt.pq.p, bt.meta.p, nreg, bt.meta.p + 3 * (size_t)nreg, nmem, 1.0,
+                                       p->iteration_number, p->division_factor, p->maximum_correspondence_distance,
+                                       p->decrease_mu ? 1 : 0, bt.Tn.p, s));
+    std::vector<double> Tn((size_t)B * 16), T((size_t)B * 16);
+    CTX_CHECK(c, d2h(Tn.data(), bt.Tn.p, Tn.size() * 8, s));
+    for (int b = 0; b < B; ++b)
+        fgr_original_scale(&Tn[(size_t)b * 16], &smean[3 * b], &tmean[3 * tk[b]], scale[b], &T[(size_t)b * 16]);
+    // --- EvaluateRegistration per start against its target's layout
+    CTX_CHECK(c, bt.T.ensure((size_t)B * 16));
+    CTX_CHECK(c, bt.Q.ensure((size_t)n * 3));
+    CTX_CHECK(c, h2d(bt.T.p, T.data(), T.size() * 8, s));
+    CTX_CHECK(c, c->scratch32.ensure((size_t)n));
+    CTX_CHECK(c, c->scratch64c.ensure((size_t)n));
+    const double r = p->maximum_correspondence_distance;
+    for (int b = 0; b < B; ++b) {
+        CTX_CHECK(c, launch_transform_points(bt.X.p + (size_t)b * n * 3, n, bt.T.p + 16 * (size_t)b, bt.Q.p, s));
+        CTX_CHECK(c, launch_nn1(bt.Q.p, n, bt.tlay[tk[b]], r * r, c->scratch32.p, c->scratch64c.p, c->qorder, s));
+        CTX_CHECK(c, launch_corr_stats(c->scratch32.p, c->scratch64c.p, n, bt.part.p + (size_t)b * nb * 2, s));
+    }
+    CTX_CHECK(c, d2h(part.data(), bt.part.p, (size_t)B * nb * 2 * 8, s));
+    for (int b = 0; b < B; ++b) {
+        double cnt = 0.0, err2 = 0.0;
+        for (int64_t q = 0; q < nb; ++q) {
+            cnt += part[((size_t)b * nb + q) * 2];
+            err2 += part[((size_t)b * nb + q) * 2 + 1];
+        }
+        std::memcpy(T_out + 16 * (size_t)b, &T[(size_t)b * 16], 16 * sizeof(double));
+        if (fitness_out) fitness_out[b] = cnt > 0 ? cnt / (double)n : 0.0;
+        if (rmse_out) rmse_out[b] = cnt > 0 ? std::sqrt(err2 / cnt) : 0.0;
+        if (ncorr_out) ncorr_out[b] = (int64_t)cnt;
+        if (n_mutual_out) {
+            n_mutual_out[2 * b] = (int64_t)corres[b].size();
+            n_mutual_out[2 * b + 1] = K[b];
+        }
+    }
+    return ORPCD_OK;
 }
 
 int orpcd_set_option(orpcd_ctx* c, const char* key, double value) {
@@ -1833,12 +2145,13 @@ int orpcd_profiling(orpcd_ctx* c, int32_t enable) {
 
 int orpcd_stats(orpcd_ctx* c, double* out, int32_t n) {
     if (!c || !out) return ORPCD_EINVAL;
-    const double v[19] = {c->stats.launches, c->stats.ms,       c->stats.pairs,          c->stats.iterations,
+    const double v[20] = {c->stats.launches, c->stats.ms,       c->stats.pairs,          c->stats.iterations,
                           c->stats.passes,   c->stats.tiles,    c->stats.accum_ms,       c->stats.sched_launches,
                           c->stats.exact_filed, c->stats.exact_queries, c->stats.host_batch_ms,
                           c->stats.host_launch_ms, c->stats.host_sync_ms, c->stats.host_batches,
-                          c->stats.feat[0], c->stats.feat[1], c->stats.feat[2], c->stats.feat[3], c->stats.feat[4]};
-    for (int i = 0; i < n && i < 19; ++i) out[i] = v[i];
+                          c->stats.feat[0], c->stats.feat[1], c->stats.feat[2], c->stats.feat[3], c->stats.feat[4],
+                          c->stats.tie_gaps};
+    for (int i = 0; i < n && i < 20; ++i) out[i] = v[i];
     return ORPCD_OK;
 }
 

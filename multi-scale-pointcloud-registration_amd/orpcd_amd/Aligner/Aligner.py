@@ -257,17 +257,27 @@ class Aligner:
 
     def _select(self, table, draw):
         """Aligner.py:178-202 over a finished table, in attempt order: strict <,
-        ValueError (RNG left after the failing attempt's draw) on rmse == 0."""
+        and the exception optimize() raises for a failed attempt (the
+        optimizer's batch_error: GeneralizedICP's ValueError on rmse == 0,
+        FastGlobalOptimizer's Warning without correspondences), with the RNG
+        left after the failing attempt's draw."""
         R0s, t0s, states = draw
         metric = np.inf
         best_transformation = np.eye(4)
+        batch_error = getattr(self._optimizer, "batch_error", None)
         for n in range(self._attempts):
             current_metric = float(table["rmse"][n])
-            if current_metric == 0 and hasattr(self._optimizer, "zero_rmse_message"):
+            if batch_error is not None:
+                err = batch_error(table, n)
+            elif current_metric == 0 and hasattr(self._optimizer, "zero_rmse_message"):
+                err = ValueError(self._optimizer.zero_rmse_message)
+            else:
+                err = None
+            if err is not None:
                 # the reference raises inside optimize() of attempt n, before
                 # drawing attempt n+1: leave the RNG exactly there
                 np.random.set_state(states[n])
-                raise ValueError(self._optimizer.zero_rmse_message)
+                raise err
             if current_metric < metric:
                 metric = current_metric
                 best_transformation = self._compose(R0s[n], t0s[n], table["T"][n])

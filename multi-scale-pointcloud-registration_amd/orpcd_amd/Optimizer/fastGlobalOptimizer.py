@@ -18,6 +18,14 @@ reference would index past the source's features otherwise, so this build
 raises ``ValueError`` there.  Set it to False for the evidently intended
 behaviour (features of each cloud).
 
+``optimize_batch`` / ``optimize_batch_multi`` are the batched entries the
+build's ``Aligner`` uses (as for GeneralizedICP): all attempts of a
+multistart, or of the speculative compass's candidate scales, run as ONE
+``orpcd_fgr_optimize_batch`` call -- per start the same normals, FPFH,
+matching, tuple test, IRLS and evaluation as ``optimize`` on the posed copy
+``source @ R0 + t0``, bit for bit, with the IRLS problems of all starts in
+one launch and the tuple tests on host threads.
+
 ``seed`` seeds the tuple test's mt19937.  Open3D draws it from its global
 engine, which is not seeded by the reference, so the reference's FGR result
 varies run to run; here it is reproducible.
@@ -131,6 +139,59 @@ class FastGlobalOptimizer(IOptimizer):
             self._LOG.error(_NO_CORR_MSG)
             raise Warning(_NO_CORR_MSG)
         return roto_translation, r["rmse"]
+
+    def _kw(self):
+        return dict(normal_radius=self._normal_estimate_radius, normal_knn=self._normal_estimate_knn,
+                    fpfh_radius=self._fpfh_radius, fpfh_knn=self._fpfh_knn,
+                    target_features_from_source=self._target_features_from_source,
+                    division_factor=self._division_factor, tuple_scale=self._tuple_scale,
+                    maximum_correspondence_distance=self._maximum_correspondence_distance,
+                    iteration_number=self._iteration_number, decrease_mu=self._decrease_mu,
+                    maximum_tuple_count=self._maximum_tuple_count, seed=self._seed)
+
+    def _table(self, r):
+        """Per-start records in the Aligner's table form (T with R transposed,
+        as optimize returns it; iters = the IRLS iterations run, 0 when
+        fewer than 10 tuple correspondences leave T at the identity)."""
+        T = r["T"].copy()
+        T[:, :3, :3] = np.transpose(T[:, :3, :3], (0, 2, 1))
+        iters = np.where(r["n_tuple_corr"] >= 10, self._iteration_number, 0).astype(np.int64)
+        return dict(T=T, rmse=r["rmse"], fitness=r["fitness"], iters=iters, ncorr=r["ncorr"],
+                    n_mutual=r["n_mutual"], n_tuple_corr=r["n_tuple_corr"])
+
+    def optimize_batch(self, source: np.ndarray, target: np.ndarray, R0: np.ndarray, t0: np.ndarray) -> dict:
+        """``optimize(source @ R0[b] + t0[b], target)`` for every start b as one
+        device call.  Does not raise on a start without correspondences: the
+        caller replays the reference's per-attempt error order (batch_error)."""
+        r = self._table(self.context.fgr_optimize_batch(source, [target], R0, t0, **self._kw()))
+        self.last_result = r
+        return r
+
+    def optimize_batch_multi(self, source: np.ndarray, targets, R0s, t0s) -> list:
+        """``optimize_batch`` for several targets (the speculative compass's
+        candidate scales) as one call per 16 targets."""
+        out = []
+        for g in range(0, len(targets), 16):
+            tg, Rg, tg0 = targets[g:g + 16], R0s[g:g + 16], t0s[g:g + 16]
+            sizes = [len(np.asarray(x).reshape(-1, 9)) for x in Rg]
+            tids = np.repeat(np.arange(len(tg), dtype=np.int32), sizes)
+            r = self._table(self.context.fgr_optimize_batch(
+                source, tg, np.concatenate([np.asarray(x).reshape(-1, 3, 3) for x in Rg]),
+                np.concatenate([np.asarray(x).reshape(-1, 3) for x in tg0]), target_of_start=tids, **self._kw()))
+            lo = 0
+            for k in sizes:
+                out.append({key: v[lo:lo + k] for key, v in r.items()})
+                lo += k
+        self.last_result = out[-1]
+        return out
+
+    def batch_error(self, table: dict, n: int):
+        """The exception optimize() would have raised for attempt n of a
+        batched table (fastGlobalOptimizer.py:181-188), or None."""
+        if int(table["ncorr"][n]) == 0:
+            self._LOG.error(_NO_CORR_MSG)
+            return Warning(_NO_CORR_MSG)
+        return None
 
     def __repr__(self):
         return f"""{self.__class__.__name__}

@@ -85,6 +85,7 @@ class GeneralizedICP(IOptimizer):
         self._calls_key, self._calls, self._calls_ok = None, 0, False
         self._ended = None  # how the last confirmed chain ended: "switch" (new cloud / target) or "miss"
         self.spec_stats = dict(served=0, batches=0, missed=0, batch_s=0.0, serve_s=0.0, tie_reruns=0)
+        self._tie_gaps_seen = 0  # context tie_gaps already reported (_note_tie_gaps)
         self._base = None
         self._tie_rows = None  # (base, rows of its KNN-20 boundary ties or None): _base_ties
         self._ctx = None
@@ -131,6 +132,21 @@ class GeneralizedICP(IOptimizer):
             return None
         return R, t
 
+    def _note_tie_gaps(self, ctx):
+        """Warn once per new gap: starts whose source boundary ties could not
+        all be re-decided from their posed copy (orpcd_stats [19]); their
+        covariances keep the rotated unposed ones (parity unpinned there)."""
+        stats = getattr(ctx, "stats", None)  # a stand-in context (tests) may not count
+        if stats is None:
+            return
+        g = int(stats().get("tie_gaps", 0))
+        if g < self._tie_gaps_seen:  # the context's statistics were reset
+            self._tie_gaps_seen = 0
+        if g > self._tie_gaps_seen:
+            self._LOG.warning(f"{g - self._tie_gaps_seen} GICP start(s) with source KNN-20 boundary ties not "
+                              "re-decided per pose (tie table full or pose far outside the cloud's extent)")
+        self._tie_gaps_seen = g
+
     def _base_ties(self, ctx):
         """Rows of the base cloud's KNN-20 boundary ties (orpcd_source_ties;
         None when it has none).  The device re-decides those points' neighbour
@@ -149,6 +165,7 @@ class GeneralizedICP(IOptimizer):
         if rows is not None:
             ctx.set_posed_tie_rows(src[rows][None])
         r = ctx.gicp_batch(pose[0][None], pose[1][None], **self._params())
+        self._note_tie_gaps(ctx)
         self.last_result = r
         return r["T"][0], float(r["rmse"][0])
 
@@ -308,6 +325,7 @@ class GeneralizedICP(IOptimizer):
             posed[0] = src[rows]
             ctx.set_posed_tie_rows(posed)
         r = ctx.gicp_batch(np.array(Rs), np.array(ts), **self._params())
+        self._note_tie_gaps(ctx)
         sets = [None if rows is None else ctx.tie_sets(k) for k in range(len(Rs))]
         self.spec_stats["batch_s"] += time.perf_counter() - t_0
         self.last_result = r
@@ -326,6 +344,7 @@ class GeneralizedICP(IOptimizer):
         ctx.set_target(target, self._epsilon)
         ctx.set_source(source)
         r = ctx.gicp_batch(R0, t0, **self._params())
+        self._note_tie_gaps(ctx)
         T = r["T"].copy()
         T[:, :3, :3] = np.transpose(T[:, :3, :3], (0, 2, 1))
         r["T"] = T
@@ -349,6 +368,7 @@ class GeneralizedICP(IOptimizer):
             r = ctx.gicp_batch_targets(np.concatenate([np.asarray(x).reshape(-1, 3, 3) for x in Rg]),
                                        np.concatenate([np.asarray(x).reshape(-1, 3) for x in tg0]), tids,
                                        **self._params())
+            self._note_tie_gaps(ctx)
             T = r["T"].copy()
             T[:, :3, :3] = np.transpose(T[:, :3, :3], (0, 2, 1))
             lo = 0
@@ -359,6 +379,14 @@ class GeneralizedICP(IOptimizer):
         return out
 
     zero_rmse_message = _ZERO_RMSE_MSG
+
+    def batch_error(self, table: dict, n: int):
+        """The exception optimize() would have raised for attempt n of a
+        batched table (generalizedICP.py:77-81), or None."""
+        if float(table["rmse"][n]) == 0:
+            self._LOG.error(_ZERO_RMSE_MSG)
+            return ValueError(_ZERO_RMSE_MSG)
+        return None
 
     def __repr__(self):
         return f"""{self.__class__.__name__}

@@ -100,6 +100,23 @@ def test_feature_nn_matches_brute_force(ctx):
     assert len(ctx.feature_nn(np.zeros((0, 33)), t)) == 0
 
 
+def test_feature_nn_rejects_overflowing_rows(ctx):
+    """A finite row whose squared norm overflows the expansion (|f| ~ 1e154)
+    would give an inf distance and a NaN key: the entry point
+    refuses it; rows up to |f|^2 = 1e150 are still answered exactly."""
+    rng = np.random.default_rng(5)
+    q, t = rng.random((40, 33)), rng.random((70, 33))
+    big = t.copy()
+    big[3, 7] = 1e160
+    with pytest.raises(Exception, match="squared norm"):
+        ctx.feature_nn(q, big)
+    with pytest.raises(Exception, match="squared norm"):
+        ctx.feature_nn(big, t)
+    ok = t.copy()
+    ok[3] *= 1e70  # |f|^2 ~ 1e140: far from every query, never the answer
+    assert _certify_feature_nn(q, ok, ctx.feature_nn(q, ok)) == 0
+
+
 def test_feature_nn_near_duplicates_resolved_exactly(ctx):
     """Rows equal up to the last bits: |q|^2+|t|^2-2q.t cannot order them, the
     exact re-decision must (oracle distance: sum of squared differences)."""
@@ -215,3 +232,85 @@ def test_aligner_with_fgr_matches_oracle_aligner(ctx, oracle):
     oT, om, osf, oerr = oal.align(src.copy(), tgt.copy())
     assert np.array_equal(gsf, osf)
     assert np.allclose(gT, oT, atol=1e-8) and abs(gm - om) <= 1e-9
+
+
+def _starts(B, seed):
+    """B initialize_rotation() draws (Aligner.py:125-162) from a seeded RandomState."""
+    from orpcd_amd.Aligner.Aligner import draw_block
+    R0, t0 = draw_block(B, np.pi / 2, 0.0, 0.1, np.random.RandomState(seed))
+    return np.array(R0), np.array(t0)
+
+
+def _same(a, b):
+    return all(np.array_equal(np.asarray(a[k]), np.asarray(b[k]))
+               for k in ("T", "rmse", "fitness", "ncorr", "n_mutual", "n_tuple_corr"))
+
+
+@pytest.mark.parametrize("case", ["q4_equal", "q4_fewer_target_points", "own_features", "two_targets"])
+def test_fgr_batch_is_the_per_call_path_bit_for_bit(ctx, case):
+    """orpcd_fgr_optimize_batch: every start's (T, rmse, fitness, ncorr,
+    mutual and tuple counts) identical to orpcd_fgr_optimize on the posed copy
+    np.dot(src, R0) + t0 that the reference's Aligner forms (Aligner.py:
+    183-190).  Q4's batched matching takes no feature search (each row's
+    nearest is its lowest exact duplicate); the per-call path searches."""
+    src, tgt = _pair(2500, noise=1e-3)
+    kw = dict(maximum_correspondence_distance=0.05, fpfh_radius=0.25, fpfh_knn=40, seed=3)
+    targets, tos = [tgt], None
+    if case == "q4_fewer_target_points":
+        targets = [tgt[:1900]]
+    elif case == "own_features":
+        kw["target_features_from_source"] = False
+    elif case == "two_targets":
+        targets = [tgt, tgt * np.array([1.1, 1.0, 0.9])]
+    B = 6
+    R0, t0 = _starts(B, 21)
+    if case == "two_targets":
+        tos = np.array([1, 0, 1, 1, 0, 0], np.int32)
+    got = ctx.fgr_optimize_batch(src, targets, R0, t0, target_of_start=tos, **kw)
+    for b in range(B):
+        tg = targets[0 if tos is None else tos[b]]
+        one = ctx.fgr_optimize(np.dot(src, R0[b]) + t0[b], tg, **kw)
+        row = {k: (got[k][b]) for k in got}
+        assert _same(row, one), f"start {b}: {row['rmse']} vs {one['rmse']}, {row['n_mutual']} vs {one['n_mutual']}"
+    assert (got["n_tuple_corr"] >= 10).all() and (got["ncorr"] > 0).all()
+
+
+def test_fgr_batch_rejects_bad_arguments(ctx):
+    src, tgt = _pair(600)
+    R0, t0 = _starts(2, 1)
+    with pytest.raises(ValueError, match="m <= n"):       # Q4 with more target points
+        ctx.fgr_optimize_batch(src[:500], [tgt], R0, t0)
+    with pytest.raises(ValueError, match="target index"):
+        ctx.fgr_optimize_batch(src, [tgt], R0, t0, target_of_start=np.array([0, 1], np.int32))
+    bad = t0.copy()
+    bad[1, 2] = np.nan
+    with pytest.raises(ValueError, match="non-finite"):
+        ctx.fgr_optimize_batch(src, [tgt], R0, bad)
+
+
+def test_aligner_with_fgr_batched_equals_sequential_aligner(ctx):
+    """The README's usage (Aligner + FastGlobalOptimizer) through the batched
+    speculative compass equals the reference-shaped sequential Aligner that
+    calls optimize() per attempt (Aligner.py:164-317): scale factors, every
+    compass error, T, metric and the RNG position afterwards, bit for bit."""
+    from orpcd_amd import Aligner, FastGlobalOptimizer, Preprocessor
+    from orpcd_amd.Optimizer.iOptimizer import IOptimizer
+
+    class PerCall(IOptimizer):  # optimize() only: the Aligner runs it attempt by attempt
+        def __init__(self, inner):
+            self.inner = inner
+
+        def optimize(self, source, target, **kwargs):
+            return self.inner.optimize(source, target)
+
+    src, tgt = _pair(1500, noise=1e-3)
+    kw = dict(maximum_correspondence_distance=0.05, fpfh_radius=0.25, fpfh_knn=40, seed=2)
+    out = []
+    for opt in (FastGlobalOptimizer(**kw), PerCall(FastGlobalOptimizer(**kw))):
+        np.random.seed(9)
+        al = Aligner(Preprocessor([]), Preprocessor([]), opt, attempts=5, max_iter=3)
+        T, metric, sf, errors = al.align(src.copy(), tgt.copy(), refine_registration=False)
+        out.append((T, metric, sf, errors, np.random.uniform(size=3)))
+    (T1, m1, s1, e1, r1), (T2, m2, s2, e2, r2) = out
+    assert np.array_equal(s1, s2) and np.array_equal(e1, e2) and m1 == m2
+    assert np.array_equal(T1, T2) and np.array_equal(r1, r2)

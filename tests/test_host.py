@@ -133,6 +133,57 @@ def test_batched_zero_rmse_raises_like_reference():
     assert np.array_equal(after, np.random.uniform(size=3))
 
 
+def test_batched_error_hook_raises_the_optimizers_exception():
+    """An optimizer's own failure (FastGlobalOptimizer raises Warning when an
+    attempt finds no correspondence, fastGlobalOptimizer.py:181-188) replays
+    through batch_error: the same exception at attempt n, with the RNG right
+    after attempt n's draws; earlier attempts' failures come first."""
+    from orpcd_amd import Aligner, Preprocessor
+
+    class NoCorr(BatchedScripted):
+        def __init__(self):
+            self.batches = []
+
+        def optimize_batch(self, source, target, R0, t0):
+            n = len(R0)
+            nc = np.full(n, 7, np.int64)
+            nc[3] = nc[5] = 0
+            return dict(T=np.tile(np.eye(4), (n, 1, 1)), rmse=np.linspace(1, 2, n), fitness=np.ones(n),
+                        iters=np.ones(n), ncorr=nc)
+
+        def batch_error(self, table, n):
+            return Warning("no correspondences") if table["ncorr"][n] == 0 else None
+
+    al = Aligner(Preprocessor([]), Preprocessor([]), NoCorr(), attempts=8)
+    src = np.random.default_rng(1).normal(size=(20, 3))
+    np.random.seed(5)
+    with pytest.raises(Warning, match="no correspondences"):
+        al.multistart_registration(src, src)
+    after = np.random.uniform(size=3)
+    np.random.seed(5)
+    for _ in range(4):
+        al.initialize_rotation()
+    assert np.array_equal(after, np.random.uniform(size=3))
+
+
+def test_fgr_batch_table_follows_optimize_conventions():
+    """FastGlobalOptimizer's batched records: T with R transposed (as optimize
+    returns it), IRLS iterations (0 below 10 tuple correspondences), and
+    batch_error's Warning exactly where optimize() would raise (no device)."""
+    from orpcd_amd import FastGlobalOptimizer
+    opt = FastGlobalOptimizer(iteration_number=64)
+    R = np.array([[0.0, -1.0, 0.0], [1.0, 0.0, 0.0], [0.0, 0.0, 1.0]])
+    T = np.tile(np.eye(4), (2, 1, 1))
+    T[0, :3, :3] = R
+    T[0, :3, 3] = [1.0, 2.0, 3.0]
+    r = dict(T=T, rmse=np.array([0.1, 0.0]), fitness=np.array([0.5, 0.0]), ncorr=np.array([40, 0]),
+             n_mutual=np.array([90, 3]), n_tuple_corr=np.array([60, 6]))
+    tb = opt._table(r)
+    assert np.array_equal(tb["T"][0, :3, :3], R.T) and np.array_equal(tb["T"][0, :3, 3], [1.0, 2.0, 3.0])
+    assert list(tb["iters"]) == [64, 0]
+    assert opt.batch_error(tb, 0) is None and isinstance(opt.batch_error(tb, 1), Warning)
+
+
 def test_refine_registration_behaviour():
     from orpcd_amd import Aligner, Preprocessor
     al = Aligner(Preprocessor([]), Preprocessor([]), None)
