@@ -45,6 +45,9 @@
  *       the feature matching inside registration_fgr_based_on_feature_matching
  *   orpcd_fgr_optimize
  *       FastGlobalOptimizer.optimize       Optimizer/fastGlobalOptimizer.py:146-190
+ *   orpcd_comm_*, orpcd_gicp_shard_run
+ *       the same call over several GPUs, its per-pass all-reduce on device
+ *                                          generalizedICP.py:59-70 (C5)
  *   orpcd_fgr_optimize_batch
  *       the B optimize() calls of one multistart (or of several scale
  *       candidates)                        Aligner/Aligner.py:178-202, 263-298
@@ -248,6 +251,20 @@ int orpcd_gicp_shard_pass(orpcd_ctx* ctx, double* sums_out, int32_t* active);
 int orpcd_gicp_shard_update(orpcd_ctx* ctx, const double* sums_in, int32_t* done_out);
 int orpcd_gicp_shard_result(orpcd_ctx* ctx, double* T_out, double* rmse_out, double* fitness_out,
                             int32_t* iters_out, int64_t* ncorr_out);
+
+/* The same start with the collective on the device (RCCL over xGMI, librccl
+ * loaded at run time).  orpcd_comm_unique_id makes a 128-byte RCCL id on one
+ * rank; the caller hands it to the others over any host channel; every rank's
+ * context joins with orpcd_comm_init(nranks, rank, id).  orpcd_gicp_shard_run
+ * then runs every pass after orpcd_gicp_shard_begin: local sums, their
+ * all-reduce and the solve are queued on the library's stream (no host round
+ * trip per pass; the done flag is read every "sync_every" passes);
+ * orpcd_gicp_shard_result reads the answer.  One rank: bit-identical to
+ * orpcd_gicp_batch with one start.                                          */
+int orpcd_comm_unique_id(uint8_t* id_out);
+int orpcd_comm_init(orpcd_ctx* ctx, int32_t nranks, int32_t rank, const uint8_t* id);
+int orpcd_comm_destroy(orpcd_ctx* ctx);
+int orpcd_gicp_shard_run(orpcd_ctx* ctx, int32_t* passes_out);
 
 /* Nearest feature row (squared Euclidean, ties -> lowest index) of every
  * query row: the KDTreeFlann SearchKNN(feature, 1) calls of Open3D's

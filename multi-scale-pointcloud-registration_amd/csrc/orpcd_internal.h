@@ -597,6 +597,10 @@ struct orpcd_ctx {
         int64_t n_total = 0;
         orpcd_gicp_params p{};
     } shard;
+    // RCCL communicator of the row-sharded start (orpcd_comm_init; an
+    // ncclComm_t, librccl loaded at run time)
+    void* comm = nullptr;
+    int comm_ranks = 0, comm_rank = 0;
 };
 
 namespace orpcd {

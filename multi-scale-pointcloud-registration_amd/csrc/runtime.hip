@@ -1,6 +1,8 @@
 // runtime.hip — the C-ABI (include/orpcd.h): context, device-resident clouds
 // and the batched GICP driver.  Host orchestration only; all arithmetic on
 // the hot path runs in the kernels of knn_kernels.hip / gicp_kernels.hip.
+#include <dlfcn.h>
+
 #include <algorithm>
 #include <cmath>
 #include <chrono>
@@ -11,6 +13,8 @@
 #include <random>
 #include <thread>
 #include <utility>
+
+#include <rccl/rccl.h>  // types only: librccl is loaded at run time (rccl_api)
 
 #include "orpcd_internal.h"
 
@@ -871,6 +875,41 @@ void host_parallel(int n, Fn f) {
     for (auto& x : th) x.join();
 }
 
+// RCCL entry points, resolved from librccl.so at first use: the library
+// itself links no collective library, so a host without RCCL still loads it
+// (only orpcd_comm_* then fail, with ORPCD_EDEVICE).
+struct RcclApi {
+    bool ok = false;
+    std::string err;
+    ncclResult_t (*get_unique_id)(ncclUniqueId*) = nullptr;
+    ncclResult_t (*comm_init_rank)(ncclComm_t*, int, ncclUniqueId, int) = nullptr;
+    ncclResult_t (*all_reduce)(const void*, void*, size_t, ncclDataType_t, ncclRedOp_t, ncclComm_t,
+                               hipStream_t) = nullptr;
+    ncclResult_t (*comm_destroy)(ncclComm_t) = nullptr;
+    const char* (*error_string)(ncclResult_t) = nullptr;
+};
+const RcclApi& rccl_api() {
+    static const RcclApi api = [] {
+        RcclApi a;
+        void* h = dlopen("librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
+        if (!h) h = dlopen("librccl.so", RTLD_NOW | RTLD_GLOBAL);
+        if (!h) {
+            const char* e = dlerror();
+            a.err = std::string("librccl.so not loadable: ") + (e ? e : "?");
+            return a;
+        }
+        a.get_unique_id = (decltype(a.get_unique_id))dlsym(h, "ncclGetUniqueId");
+        a.comm_init_rank = (decltype(a.comm_init_rank))dlsym(h, "ncclCommInitRank");
+        a.all_reduce = (decltype(a.all_reduce))dlsym(h, "ncclAllReduce");
+        a.comm_destroy = (decltype(a.comm_destroy))dlsym(h, "ncclCommDestroy");
+        a.error_string = (decltype(a.error_string))dlsym(h, "ncclGetErrorString");
+        a.ok = a.get_unique_id && a.comm_init_rank && a.all_reduce && a.comm_destroy && a.error_string;
+        if (!a.ok) a.err = "librccl.so lacks an nccl* entry point";
+        return a;
+    }();
+    return api;
+}
+
 }  // namespace
 
 extern "C" {
@@ -911,6 +950,7 @@ int orpcd_ctx_destroy(orpcd_ctx* c) {
     if (!c) return ORPCD_EINVAL;
     (void)hipSetDevice(c->device);
     (void)hipStreamSynchronize(c->stream);
+    (void)orpcd_comm_destroy(c);
     for (int k = 0; k < kMaxTargets; ++k) {
         c->tgts[k].release();
         c->tcovs[k].release();
@@ -1649,6 +1689,90 @@ int orpcd_gicp_shard_result(orpcd_ctx* c, double* T_out, double* rmse_out, doubl
     if (iters_out) *iters_out = iters;
     if (ncorr_out) *ncorr_out = nc;
     c->stats.iterations += iters;
+    return ORPCD_OK;
+}
+
+#define CTX_RCCL(ctx, call)                                                                         \
+    do {                                                                                            \
+        const ncclResult_t r_ = (call);                                                             \
+        if (r_ != ncclSuccess) {                                                                    \
+            (ctx)->err = std::string(#call) + ": " + rccl_api().error_string(r_);                   \
+            return ORPCD_EDEVICE;                                                                   \
+        }                                                                                           \
+    } while (0)
+
+int orpcd_comm_unique_id(uint8_t* id_out) {
+    if (!id_out) return ORPCD_EINVAL;
+    const RcclApi& api = rccl_api();
+    if (!api.ok) return ORPCD_EDEVICE;
+    ncclUniqueId id;
+    if (api.get_unique_id(&id) != ncclSuccess) return ORPCD_EDEVICE;
+    std::memcpy(id_out, id.internal, NCCL_UNIQUE_ID_BYTES);
+    return ORPCD_OK;
+}
+
+int orpcd_comm_init(orpcd_ctx* c, int32_t nranks, int32_t rank, const uint8_t* id) {
+    if (!c) return ORPCD_EINVAL;
+    CTX_REQUIRE(c, id && nranks >= 1 && rank >= 0 && rank < nranks, "comm_init: bad arguments");
+    const RcclApi& api = rccl_api();
+    CTX_REQUIRE(c, api.ok, "comm_init: " + api.err);
+    CTX_CHECK(c, hipSetDevice(c->device));
+    (void)orpcd_comm_destroy(c);
+    ncclUniqueId uid;
+    std::memcpy(uid.internal, id, NCCL_UNIQUE_ID_BYTES);
+    ncclComm_t comm = nullptr;
+    CTX_RCCL(c, api.comm_init_rank(&comm, nranks, uid, rank));
+    c->comm = comm;
+    c->comm_ranks = nranks;
+    c->comm_rank = rank;
+    return ORPCD_OK;
+}
+
+int orpcd_comm_destroy(orpcd_ctx* c) {
+    if (!c) return ORPCD_EINVAL;
+    if (c->comm) {
+        (void)hipStreamSynchronize(c->stream);
+        (void)rccl_api().comm_destroy((ncclComm_t)c->comm);
+    }
+    c->comm = nullptr;
+    c->comm_ranks = c->comm_rank = 0;
+    return ORPCD_OK;
+}
+
+// The row-sharded start's pass loop with the collective on the device: per
+// pass the local partials are reduced to the 29 sums (the same fixed-order
+// kernel as orpcd_gicp_shard_pass), all-reduced by RCCL on the library's
+// stream, and solved from the global sums (as orpcd_gicp_shard_update); the
+// host reads the done flag only every sync_every passes.  Every rank computes
+// the same global sums, hence the same done pass, so all ranks enqueue the
+// same collectives; passes enqueued after the start finished are no-ops (every
+// kernel skips a done start; their sums go unused).
+int orpcd_gicp_shard_run(orpcd_ctx* c, int32_t* passes_out) {
+    if (!c) return ORPCD_EINVAL;
+    CTX_REQUIRE(c, c->shard.begun, "gicp_shard_run: call orpcd_gicp_shard_begin first");
+    CTX_REQUIRE(c, c->comm, "gicp_shard_run: no communicator (orpcd_comm_init)");
+    CTX_CHECK(c, hipSetDevice(c->device));
+    const RcclApi& api = rccl_api();
+    const auto& p = c->shard.p;
+    const double r2 = p.max_correspondence_distance * p.max_correspondence_distance;
+    hipStream_t s = c->stream;
+    c->count_tiles = false;
+    const int every = std::max(1, c->opt.sync_every);
+    int32_t done = 0;
+    CTX_CHECK(c, d2h(&done, c->done.p, 4, s));
+    while (!done) {
+        for (int k = 0; k < every; ++k) {
+            CTX_CHECK(c, launch_gicp_pass(c, 1, c->shard.pass, r2, s, nullptr, one_target()));
+            CTX_CHECK(c, launch_reduce_partials(c, 0, c->scratch64c.p, s));
+            CTX_RCCL(c, api.all_reduce(c->scratch64c.p, c->scratch64c.p, kNacc, ncclFloat64, ncclSum,
+                                       (ncclComm_t)c->comm, s));
+            CTX_CHECK(c, launch_gicp_solve_sums(c, c->scratch64c.p, c->shard.n_total, c->shard.pass, p, s));
+            c->shard.pass += 1;
+            c->stats.passes += 1;
+        }
+        CTX_CHECK(c, d2h(&done, c->done.p, 4, s));  // drains the stream
+    }
+    if (passes_out) *passes_out = c->shard.pass;
     return ORPCD_OK;
 }
 

@@ -55,7 +55,8 @@ _lib_lock = threading.Lock()
 EXPORTED = ("orpcd_abi_version", "orpcd_build_id", "orpcd_build_flags", "orpcd_device_count", "orpcd_ctx_create", "orpcd_ctx_destroy",
             "orpcd_last_error", "orpcd_set_target", "orpcd_set_source", "orpcd_gicp_batch",
             "orpcd_set_source_rows", "orpcd_gicp_shard_begin", "orpcd_gicp_shard_pass", "orpcd_gicp_shard_update",
-            "orpcd_gicp_shard_result",
+            "orpcd_gicp_shard_result", "orpcd_comm_unique_id", "orpcd_comm_init", "orpcd_comm_destroy",
+            "orpcd_gicp_shard_run",
             "orpcd_nn1_radius", "orpcd_estimate_normals", "orpcd_fpfh", "orpcd_fpfh_from_normals", "orpcd_fgr", "orpcd_feature_nn",
             "orpcd_fgr_optimize", "orpcd_fgr_optimize_batch", "orpcd_set_source_points", "orpcd_icp_p2p_batch",
             "orpcd_sor", "orpcd_voxel_down_sample", "orpcd_farthest_downsample",
@@ -127,6 +128,11 @@ def load_library():
         L.orpcd_gicp_shard_pass.argtypes = [vp, _f64p, _i32p]
         L.orpcd_gicp_shard_update.argtypes = [vp, _f64p, _i32p]
         L.orpcd_gicp_shard_result.argtypes = [vp, _f64p, _f64p, _f64p, _i32p, _i64p]
+        _u8p = np.ctypeslib.ndpointer(dtype=np.uint8, flags="C_CONTIGUOUS")
+        L.orpcd_comm_unique_id.argtypes = [_u8p]
+        L.orpcd_comm_init.argtypes = [vp, ctypes.c_int32, ctypes.c_int32, _u8p]
+        L.orpcd_comm_destroy.argtypes = [vp]
+        L.orpcd_gicp_shard_run.argtypes = [vp, _i32p]
         L.orpcd_nn1_radius.argtypes = [vp, _f64p, c_i64, _f64p, c_i64, c_dbl, _i32p, _f64p]
         L.orpcd_estimate_normals.argtypes = [vp, _f64p, c_i64, ctypes.c_int32, c_dbl, c_dbl, vp, vp, vp]
         L.orpcd_fpfh.argtypes = [vp, _f64p, c_i64, c_dbl, ctypes.c_int32, c_dbl, ctypes.c_int32, _f64p, _f64p]
@@ -518,6 +524,30 @@ class Context:
         self._check(self._L.orpcd_gicp_shard_result(self._h, T, rmse, fit, it, nc), "orpcd_gicp_shard_result")
         return dict(T=T.reshape(4, 4), rmse=float(rmse[0]), fitness=float(fit[0]), iters=int(it[0]),
                     ncorr=int(nc[0]))
+
+    # ------------------------------------------- device collectives (RCCL)
+    def comm_unique_id(self) -> bytes:
+        """A new RCCL unique id (128 bytes) for orpcd_comm_init on every rank."""
+        uid = np.zeros(128, np.uint8)
+        if self._L.orpcd_comm_unique_id(uid) != ORPCD_OK:
+            raise NativeError("orpcd_comm_unique_id failed (librccl.so missing or no device)")
+        return uid.tobytes()
+
+    def comm_init(self, nranks: int, rank: int, uid: bytes):
+        buf = np.frombuffer(bytes(uid), np.uint8).copy()
+        if buf.size != 128:
+            raise ValueError("comm_init: the RCCL id is 128 bytes")
+        self._check(self._L.orpcd_comm_init(self._h, int(nranks), int(rank), buf), "orpcd_comm_init")
+
+    def comm_destroy(self):
+        self._check(self._L.orpcd_comm_destroy(self._h), "orpcd_comm_destroy")
+
+    def shard_run(self) -> int:
+        """Every pass of the begun row-sharded start, the per-pass all-reduce
+        on the device (orpcd_gicp_shard_run); returns the passes enqueued."""
+        n = np.zeros(1, np.int32)
+        self._check(self._L.orpcd_gicp_shard_run(self._h, n), "orpcd_gicp_shard_run")
+        return int(n[0])
 
     # -------------------------------------------------------- kernel level
     def nn1_radius(self, q: np.ndarray, t: np.ndarray, radius: float):

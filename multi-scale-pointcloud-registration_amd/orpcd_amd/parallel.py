@@ -14,7 +14,11 @@ exists.
 a contiguous block of source rows (covariances still from the full cloud's
 neighbourhoods) and the whole target; per ICP pass it computes the 29 local
 normal-equation sums, one all-reduce(sum) of 232 bytes combines them, and
-every rank solves the same 6x6 system (gicp_rows_sharded).
+every rank solves the same 6x6 system (gicp_rows_sharded).  With
+``device_collectives=True`` that all-reduce is the library's own RCCL
+communicator on its stream (orpcd_comm_init / orpcd_gicp_shard_run): no host
+round trip per pass; torch.distributed only hands the 128-byte RCCL id
+around.
 
 Backend: ``torch.distributed`` — "nccl" (= RCCL over
 xGMI on ROCm) on GPUs, "gloo" for CPU tests.
@@ -103,12 +107,39 @@ def allreduce_sum(v: np.ndarray) -> np.ndarray:
     return t.cpu().numpy()
 
 
+def broadcast_bytes(data: bytes, src: int = 0) -> bytes:
+    """`data` of rank `src` on every rank of the default group (identity on one rank)."""
+    rank, ws = world()
+    if ws == 1:
+        return data
+    import torch.distributed as dist
+    obj = [data if rank == src else None]
+    dist.broadcast_object_list(obj, src=src)
+    return obj[0]
+
+
+def device_comm(ctx):
+    """Join ``ctx`` to an RCCL communicator over the default group's ranks
+    (once per context and group size): rank 0 makes the id, the group
+    broadcasts it."""
+    rank, ws = world()
+    key = (rank, ws)
+    if getattr(ctx, "_orpcd_comm", None) == key:
+        return
+    uid = broadcast_bytes(ctx.comm_unique_id() if rank == 0 else b"", 0)
+    ctx.comm_init(ws, rank, uid)
+    ctx._orpcd_comm = key
+
+
 def gicp_rows_sharded(ctx, source: np.ndarray, target: np.ndarray, R0=None, t0=None, epsilon: float = 1e-3,
-                      **params) -> dict:
+                      device_collectives: bool = False, **params) -> dict:
     """One GICP (pose ``source @ R0 + t0``) with the source rows split over the
     ranks of the default process group.  ``ctx`` is this rank's device
     context (``_native.Context`` or any object with the same shard_* calls).
-    Returns the Open3D-convention result (T column convention)."""
+    ``device_collectives``: the per-pass all-reduce runs on the device through
+    the library's RCCL communicator (device_comm); else on the host through
+    torch.distributed.  Returns the Open3D-convention result (T column
+    convention)."""
     rank, ws = world()
     n = len(source)
     if n < ws:
@@ -122,6 +153,10 @@ def gicp_rows_sharded(ctx, source: np.ndarray, target: np.ndarray, R0=None, t0=N
     ctx.set_target(target, epsilon)
     ctx.set_source_rows(source, lo, hi)
     ctx.shard_begin(R0, t0, n_total=n, epsilon=epsilon, **params)
+    if device_collectives:
+        device_comm(ctx)
+        ctx.shard_run()
+        return ctx.shard_result()
     while True:
         sums, active = ctx.shard_pass()
         if not active:

@@ -3,6 +3,8 @@
 shard_result), built from the oracle's pieces, so that the multi-rank driver
 orpcd_amd.parallel.gicp_rows_sharded can be tested with gloo on CPU.  Test
 infrastructure only (it calls the oracle)."""
+import os
+
 import numpy as np
 
 import oracle
@@ -59,3 +61,22 @@ class FakeShardContext:
 
     def shard_result(self):
         return dict(T=self.T, rmse=self.rmse, fitness=self.fit, iters=self.pass_, ncorr=self.ncorr)
+
+    # device collectives (orpcd_comm_* / orpcd_gicp_shard_run): the same loop,
+    # its all-reduce over the process group; the id is recorded to check that
+    # every rank joined rank 0's communicator
+    def comm_unique_id(self):
+        return os.urandom(128)
+
+    def comm_init(self, nranks, rank, uid):
+        self.comm = (nranks, rank, bytes(uid))
+
+    def shard_run(self):
+        from orpcd_amd import parallel
+        n = 0
+        while True:
+            sums, act = self.shard_pass()
+            if not act or self.shard_update(parallel.allreduce_sum(sums)):
+                return n
+            n += 1
+

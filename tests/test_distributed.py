@@ -84,7 +84,7 @@ def test_record_pack_roundtrip():
         assert np.array_equal(np.asarray(u[k]), np.asarray(r[k]))
 
 
-def _rows_worker(rank, world, port, out_dir):
+def _rows_worker(rank, world, port, out_dir, device_collectives=False):
     sys.path[:0] = [PKG, os.path.join(REPO, "tests"), os.path.join(REPO, "oracle"), REPO]
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     import torch.distributed as dist
@@ -93,9 +93,13 @@ def _rows_worker(rank, world, port, out_dir):
     from shard_fake import FakeShardContext
     from workloads import small_pair
     src, tgt = small_pair(1501, 1400, seed=4)
-    r = parallel.gicp_rows_sharded(FakeShardContext(), src, tgt, max_correspondence_distance=0.3)
+    ctx = FakeShardContext()
+    r = parallel.gicp_rows_sharded(ctx, src, tgt, max_correspondence_distance=0.3,
+                                   device_collectives=device_collectives)
+    comm = np.frombuffer(ctx.comm[2], np.uint8) if device_collectives else np.zeros(0, np.uint8)
     np.savez(os.path.join(out_dir, f"rows{rank}.npz"), T=r["T"], rmse=r["rmse"], fitness=r["fitness"],
-             iters=r["iters"], ncorr=r["ncorr"])
+             iters=r["iters"], ncorr=r["ncorr"], comm=comm,
+             comm_ranks=ctx.comm[0] if device_collectives else 0, comm_rank=ctx.comm[1] if device_collectives else -1)
     dist.destroy_process_group()
 
 
@@ -130,14 +134,20 @@ def test_row_sharded_fewer_rows_than_ranks_raises_everywhere(tmp_path):
         assert (tmp_path / f"few{r}.txt").read_text() == "ValueError"
 
 
-@pytest.mark.parametrize("world", [2, 3])
-def test_row_sharded_gicp_matches_single_process_oracle(tmp_path, world, oracle):
+@pytest.mark.parametrize("world,device_collectives", [(2, False), (3, False), (2, True), (3, True)])
+def test_row_sharded_gicp_matches_single_process_oracle(tmp_path, world, device_collectives, oracle):
     """C5's multi-GPU path: source rows split over ranks, one all-reduce of
     the 29 normal-equation sums per pass; every rank ends with the result of
-    one un-sharded GICP (up to the summation order of the sums)."""
+    one un-sharded GICP (up to the summation order of the sums).  With
+    device_collectives the pass loop is the context's own (orpcd_gicp_shard_run)
+    and every rank joins rank 0's communicator id."""
     import torch.multiprocessing as mp
-    mp.start_processes(_rows_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True,
-                       start_method="spawn")
+    mp.start_processes(_rows_worker, args=(world, _free_port(), str(tmp_path), device_collectives), nprocs=world,
+                       join=True, start_method="spawn")
+    if device_collectives:
+        ids = [np.load(tmp_path / f"rows{r}.npz")["comm"] for r in range(world)]
+        assert all(len(i) == 128 and np.array_equal(i, ids[0]) for i in ids)
+        assert [int(np.load(tmp_path / f"rows{r}.npz")["comm_rank"]) for r in range(world)] == list(range(world))
     from workloads import small_pair
     src, tgt = small_pair(1501, 1400, seed=4)
     ref = oracle.gicp(src, tgt, 0.3)

@@ -30,6 +30,27 @@ def test_shard_single_rank_is_bitwise_gicp_batch(ctx):
     assert r["iters"] == b["iters"][0] and r["ncorr"] == b["ncorr"][0] and r["fitness"] == b["fitness"][0]
 
 
+def test_shard_device_collectives_single_rank_is_bitwise_gicp_batch():
+    """The pass loop with the all-reduce on the device (RCCL communicator of
+    one rank, orpcd_gicp_shard_run): bit-identical to orpcd_gicp_batch B = 1
+    and to the host-collective row path; a second run on the same
+    communicator as well (a context of its own: comm state per context)."""
+    from orpcd_amd import _native, parallel
+    src, tgt = _pair()
+    c = _native.Context(0)
+    r = parallel.gicp_rows_sharded(c, src, tgt, max_correspondence_distance=0.3, device_collectives=True)
+    h = parallel.gicp_rows_sharded(c, src, tgt, max_correspondence_distance=0.3)
+    r2 = parallel.gicp_rows_sharded(c, src, tgt, max_correspondence_distance=0.3, device_collectives=True)
+    c.set_target(tgt, 1e-3, cache=False)
+    c.set_source(src, cache=False)
+    b = c.gicp_batch(np.eye(3)[None], np.zeros((1, 3)), max_correspondence_distance=0.3)
+    for x in (r, h, r2):
+        assert np.array_equal(x["T"], b["T"][0]) and x["rmse"] == b["rmse"][0]
+        assert x["iters"] == b["iters"][0] and x["ncorr"] == b["ncorr"][0] and x["fitness"] == b["fitness"][0]
+    c.comm_destroy()
+    c.close()
+
+
 @pytest.mark.parametrize("splits", [2, 3])
 def test_shard_emulated_ranks_match_unsharded(ctx, oracle, splits):
     from orpcd_amd import _native, parallel
