@@ -14,6 +14,7 @@ import json
 import os
 import subprocess
 import sys
+import time
 from concurrent.futures import ThreadPoolExecutor
 
 HERE = os.path.dirname(os.path.abspath(__file__))
@@ -80,29 +81,46 @@ OBJ_DIR = OBJ + ("_" + "".join(c if c.isalnum() else "_" for c in "".join(EXTRA)
 
 
 def _compile(src, force):
+    """(object path, whether it was compiled now)"""
     obj = os.path.join(OBJ_DIR, os.path.basename(src) + ".o")
     if force or _stale(obj, [src] + _headers()):
         cmd = [HIPCC] + CXXFLAGS + ["-c", src, "-o", obj]
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
             raise RuntimeError(f"hipcc failed on {src}:\n{r.stdout}\n{r.stderr}")
-    return obj
+        return obj, True
+    return obj, False
 
 
 def build(force: bool = False, verbose: bool = False) -> str:
+    """Compile what is stale, relink if needed.  Every call records what it
+    did (units recompiled, relinked or not, source id, seconds) in
+    build/last_build.json and, with verbose, prints it: the build is observed,
+    not assumed."""
+    t0 = time.perf_counter()
     os.makedirs(OBJ_DIR, exist_ok=True)
     os.makedirs(LIBDIR, exist_ok=True)
     srcs = sorted(glob.glob(os.path.join(CSRC, "*.hip")))
     with ThreadPoolExecutor(max_workers=min(8, len(srcs))) as ex:
-        objs = list(ex.map(lambda s: _compile(s, force), srcs))
+        res = list(ex.map(lambda s: _compile(s, force), srcs))
+    objs = [o for o, _ in res]
     objs.append(_build_id_object(force))
-    if force or _stale(LIB, objs):
+    linked = force or _stale(LIB, objs)
+    if linked:
         cmd = [HIPCC, "-shared", f"--offload-arch={ARCH}", "-fPIC", "-o", LIB] + objs
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
             raise RuntimeError(f"link failed:\n{r.stdout}\n{r.stderr}")
+    rec = {"library": os.path.relpath(LIB, REPO), "source_id": source_id(), "extra_flags": " ".join(EXTRA),
+           "units": len(srcs), "recompiled": [os.path.basename(s) for s, (_, c) in zip(srcs, res) if c],
+           "relinked": bool(linked), "seconds": round(time.perf_counter() - t0, 1),
+           "when": time.strftime("%Y-%m-%dT%H:%M:%S")}
+    with open(os.path.join(OBJ_DIR, "last_build.json"), "w") as fh:
+        json.dump(rec, fh, indent=1)
     if verbose:
-        print("built", LIB)
+        print(f"built {LIB}: {len(rec['recompiled'])} of {rec['units']} units recompiled "
+              f"({', '.join(rec['recompiled']) or 'none'}), relinked: {'yes' if linked else 'no'}, "
+              f"source id {rec['source_id']}, {rec['seconds']} s")
     return LIB
 
 

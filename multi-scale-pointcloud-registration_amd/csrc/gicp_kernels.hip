@@ -1005,8 +1005,12 @@ __device__ __forceinline__ void nn_search_body(
 // class-major list, heaviest class first; the wave's duration is added to its
 // group's cost and to the pass total for the next pass's schedule.
 // Waves per workgroup of the ordered dispatch (A/B macro ORPCD_SCHED_WAVES).
+// One: a wave's slot is refilled as soon as it exits, without waiting for
+// three sibling waves of different length (round 5, tools/r5_s1.sh: C2 exact
+// 30 starts 15.6 -> 15.2 ms, 64 starts 24.9 -> 24.1 ms, 2 waves per block in
+// between; identical result hashes).
 #ifndef ORPCD_SCHED_WAVES
-#define ORPCD_SCHED_WAVES 4
+#define ORPCD_SCHED_WAVES 1
 #endif
 constexpr int kSWaves = ORPCD_SCHED_WAVES;
 template <bool kExact>
@@ -1840,46 +1844,75 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 2))) void
 int seed_stride_for(int64_t ntiles, int reps = 512);
 
 // The seed grid of a target (CloudLayout::sgrid): cell i of kSeedGrid^3 over
-// the target's bounding box holds the Morton index of the target nearest to
-// its centre (fp32 culled search as nn1_kernel's, strided representative
-// seeds).  Only a bound seed: any target would do, the nearest is the best.
-// One launch builds the grids of several targets (grid.y = target, layouts
-// from their TargetDesc): a single grid is a latency-bound launch of ~860
-// waves (~0.4 ms), so six of them in sequence cost 2.4 ms per set_targets.
-__global__ __launch_bounds__(kCBlock) void seed_grid_kernel(const TargetDesc* __restrict__ tdesc, int first) {
-    __shared__ float4 stage[kCWaves][kTile];
-    constexpr int nq = kSeedGrid * kSeedGrid * kSeedGrid;
+// the target's bounding box holds the Morton index of a target near its
+// centre.  Only a bound seed: any real target would do (a bound never changes
+// an answer, tests/test_gpu_seed.py), the nearest is the best.
+//
+// Built by jump flooding (round 5): every target point offers itself to its
+// own cell (64-bit atomicMin on (fp32 d^2 to the centre, index)), then rounds
+// with steps 32, 16, 8, 4, 2, 1, 1 let each cell take the best of the seeds of
+// its 26 neighbours at that step (JFA+1: the nearest point to the centre for
+// nearly every cell, a near one otherwise).  Rounds 1-4 searched every cell
+// centre with the culled 1-NN search instead: exact, but its 110,592 centres
+// in raster order make loose wave boxes, and cells far from the surface have
+// large bounds -- 0.38 ms per 50k-point target, 6.3 ms per 1M-point target
+// (C5's set-up, profiles/r05_c5_kernel_stats.csv); these ten launches are
+// independent of the cloud size but for the scatter.
+__device__ __forceinline__ int seed_axis(float x, float lo, float inv) {
+    return min(kSeedGrid - 1, max(0, (int)((x - lo) * inv)));  // the query transform's clamp
+}
+__device__ __forceinline__ float seed_centre(float lo, float inv, int c) {
+    return lo + ((float)c + 0.5f) * (1.0f / inv);
+}
+__device__ __forceinline__ unsigned long long seed_key(float d2, int j) {
+    return ((unsigned long long)__float_as_uint(d2) << 32) | (unsigned)j;
+}
+__global__ __launch_bounds__(256) void seed_scatter_kernel(const TargetDesc* __restrict__ tdesc, int first) {
     const TargetDesc& tg = tdesc[first + blockIdx.y];
-    const float4* __restrict__ p4 = tg.p4;
-    const int ntiles = tg.ntiles, nsuper = tg.nsuper;
-    const int seed_stride = max(1, (ntiles + 511) / 512);  // ~512 representatives
-    const float cxs = 1.0f / tg.sg_inv[0], cys = 1.0f / tg.sg_inv[1], czs = 1.0f / tg.sg_inv[2];
-    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    const int i0 = blockIdx.x * kCBlockQ + wid * (64 * kCQPT) + lane;
-    float qx[kCQPT], qy[kCQPT], qz[kCQPT], bound[kCQPT], bd[kCQPT];
-    int bj[kCQPT];
-#pragma unroll
-    for (int k = 0; k < kCQPT; ++k) {
-        const int i = i0 + 64 * k;
-        const bool valid = i < nq;
-        qx[k] = tg.sg_lo[0] + ((float)(i / (kSeedGrid * kSeedGrid)) + 0.5f) * cxs;
-        qy[k] = tg.sg_lo[1] + ((float)((i / kSeedGrid) % kSeedGrid) + 0.5f) * cys;
-        qz[k] = tg.sg_lo[2] + ((float)(i % kSeedGrid) + 0.5f) * czs;
-        float b = valid ? 3.0e38f : 0.0f;
-        if (valid)
-            for (int t = 0; t < ntiles; t += seed_stride)
-                b = fminf(b, seed_bound(d2f(qx[k], qy[k], qz[k], p4[t * kTile])));
-        bound[k] = b;
+    const int j = blockIdx.x * 256 + threadIdx.x;
+    if (j >= tg.npts) return;
+    const float4 p = tg.p4[j];
+    const int cx = seed_axis(p.x, tg.sg_lo[0], tg.sg_inv[0]), cy = seed_axis(p.y, tg.sg_lo[1], tg.sg_inv[1]),
+              cz = seed_axis(p.z, tg.sg_lo[2], tg.sg_inv[2]);
+    const float d2 = d2f(seed_centre(tg.sg_lo[0], tg.sg_inv[0], cx), seed_centre(tg.sg_lo[1], tg.sg_inv[1], cy),
+                         seed_centre(tg.sg_lo[2], tg.sg_inv[2], cz), p);
+    atomicMin(tg.sgk + (cx * kSeedGrid + cy) * kSeedGrid + cz, seed_key(d2, j));
+}
+// one flooding round: key_out[c] = the best of key_in over c and its 26
+// neighbours at `step` (out = 0xFF.. fill when nothing reached c yet);
+// last != 0: the grid's indices are written instead of the next keys
+__global__ __launch_bounds__(256) void seed_jfa_kernel(const TargetDesc* __restrict__ tdesc, int first, int step,
+                                                       int in_half, int last) {
+    constexpr int G = kSeedGrid, G3 = G * G * G;
+    const TargetDesc& tg = tdesc[first + blockIdx.y];
+    const int c = blockIdx.x * 256 + threadIdx.x;
+    if (c >= G3) return;
+    const int cx = c / (G * G), cy = (c / G) % G, cz = c % G;
+    const float qx = seed_centre(tg.sg_lo[0], tg.sg_inv[0], cx), qy = seed_centre(tg.sg_lo[1], tg.sg_inv[1], cy),
+                qz = seed_centre(tg.sg_lo[2], tg.sg_inv[2], cz);
+    const unsigned long long* in = tg.sgk + (size_t)in_half * G3;
+    unsigned long long best = in[c];
+    for (int dx = -1; dx <= 1; ++dx) {
+        const int nx = cx + dx * step;
+        if (nx < 0 || nx >= G) continue;
+        for (int dy = -1; dy <= 1; ++dy) {
+            const int ny = cy + dy * step;
+            if (ny < 0 || ny >= G) continue;
+            for (int dz = -1; dz <= 1; ++dz) {
+                const int nz = cz + dz * step;
+                if (nz < 0 || nz >= G || (dx | dy | dz) == 0) continue;
+                const unsigned long long k = in[(nx * G + ny) * G + nz];
+                if (k == ~0ull) continue;
+                const int j = (int)(unsigned)k;
+                const unsigned long long cand = seed_key(d2f(qx, qy, qz, tg.p4[j]), j);
+                best = cand < best ? cand : best;
+            }
+        }
     }
-    culled_search<false>(stage[wid], p4, tg.tlo, tg.thi, tg.qbox, ntiles, tg.slo, tg.shi, nsuper, 1, 1, 0, qx, qy, qz,
-                         bound, bd, bj, lane < nsuper ? tg.slo[lane] : make_float4(0.f, 0.f, 0.f, 0.f),
-                         lane < nsuper ? tg.shi[lane] : make_float4(0.f, 0.f, 0.f, 0.f));
-    int32_t* grid = const_cast<int32_t*>(tg.sgrid);
-#pragma unroll
-    for (int k = 0; k < kCQPT; ++k) {
-        const int i = i0 + 64 * k;
-        if (i < nq) grid[i] = bj[k] >= 0 ? bj[k] : 0;
-    }
+    if (last)
+        const_cast<int32_t*>(tg.sgrid)[c] = best == ~0ull ? 0 : (int)(unsigned)best;
+    else
+        tg.sgk[(size_t)(in_half ^ 1) * G3 + c] = best;
 }
 
 // The grid's buffer and frame (host side; the build is launch_seed_grids).
@@ -1887,6 +1920,7 @@ hipError_t prepare_seed_grid(CloudLayout& L) {
     constexpr int nq = kSeedGrid * kSeedGrid * kSeedGrid;
     hipError_t e = L.sgrid.ensure(nq);
     if (e != hipSuccess) return e;
+    if ((e = L.sgk.ensure((size_t)2 * nq)) != hipSuccess) return e;
     for (int a = 0; a < 3; ++a) {
         // the grid in the fp32 frame, a hair larger than the box; a
         // degenerate axis gets a tiny cell (every query clamps into a cell)
@@ -1899,11 +1933,23 @@ hipError_t prepare_seed_grid(CloudLayout& L) {
 }
 
 // The grids of targets [first, first + count) (their descriptors uploaded).
-hipError_t launch_seed_grids(const TargetDesc* tdesc, int first, int count, hipStream_t s) {
+hipError_t launch_seed_grids(const TargetDesc* tdesc, int first, int count, int max_points,
+                             unsigned long long* const* sgk, hipStream_t s) {
     constexpr int nq = kSeedGrid * kSeedGrid * kSeedGrid;
-    seed_grid_kernel<<<dim3((unsigned)((nq + kCBlockQ - 1) / kCBlockQ), (unsigned)count), kCBlock, 0, s>>>(tdesc,
-                                                                                                         first);
-    return hipGetLastError();
+    hipError_t e;
+    for (int k = 0; k < count; ++k)  // every cell empty (0xFF.. keys) in the first half
+        if ((e = hipMemsetAsync(sgk[k], 0xFF, (size_t)nq * 8, s)) != hipSuccess) return e;
+    seed_scatter_kernel<<<dim3((unsigned)((max_points + 255) / 256), (unsigned)count), 256, 0, s>>>(tdesc, first);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    const int steps[] = {32, 16, 8, 4, 2, 1, 1};
+    constexpr int nsteps = sizeof(steps) / sizeof(steps[0]);
+    static_assert(kSeedGrid <= 64, "the first flooding step must reach across the grid");
+    for (int r = 0; r < nsteps; ++r) {
+        seed_jfa_kernel<<<dim3((unsigned)((nq + 255) / 256), (unsigned)count), 256, 0, s>>>(tdesc, first, steps[r],
+                                                                                            r & 1, r == nsteps - 1);
+        if ((e = hipGetLastError()) != hipSuccess) return e;
+    }
+    return hipSuccess;
 }
 
 // Kernel-level 1-NN (orpcd_nn1_radius, FGR's EvaluateRegistration): the same
@@ -2074,6 +2120,8 @@ void write_target_desc(const CloudLayout& L, const double* tcov, int seed_reps, 
     d.oy = L.org[1];
     d.oz = L.org[2];
     d.sgrid = L.sgrid.n ? L.sgrid.p : nullptr;
+    d.sgk = L.sgk.n ? L.sgk.p : nullptr;
+    d.npts = (int)L.n;
     for (int a = 0; a < 3; ++a) {
         d.sg_lo[a] = L.sg_lo[a];
         d.sg_inv[a] = L.sg_inv[a];

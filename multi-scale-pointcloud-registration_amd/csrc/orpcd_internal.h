@@ -6,6 +6,7 @@
 #include <algorithm>
 #include <cstring>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/orpcd.h"
@@ -91,6 +92,38 @@ struct HostBuf {  // pinned
     }
 };
 
+// f(b) for b in [0, n) on up to 16 host threads (the GPU box grants 16 cores;
+// every b writes only its own outputs)
+template <typename Fn>
+void host_parallel(int n, Fn f) {
+    const int nt = std::max(1, std::min({n, 16, (int)std::max(1u, std::thread::hardware_concurrency())}));
+    if (nt <= 1) {
+        for (int b = 0; b < n; ++b) f(b);
+        return;
+    }
+    std::vector<std::thread> th;
+    for (int t = 0; t < nt; ++t)
+        th.emplace_back([&, t] {
+            for (int b = t; b < n; b += nt) f(b);
+        });
+    for (auto& x : th) x.join();
+}
+
+// memcpy of a large block split over host threads (staging copies of 1M-point clouds)
+inline void host_memcpy(void* dst, const void* src, size_t bytes) {
+    constexpr size_t kPiece = (size_t)2 << 20;
+    if (bytes <= 2 * kPiece) {
+        std::memcpy(dst, src, bytes);
+        return;
+    }
+    const int np = (int)((bytes + kPiece - 1) / kPiece);
+    host_parallel(np, [&](int k) {
+        const size_t o = (size_t)k * kPiece;
+        std::memcpy(static_cast<unsigned char*>(dst) + o, static_cast<const unsigned char*>(src) + o,
+                    std::min(kPiece, bytes - o));
+    });
+}
+
 // ------------------------------------------------ host <-> device copies
 // Every copy between the device and host memory the library does not own as
 // pinned (the caller's arrays, std::vector buffers, stack scalars) goes
@@ -150,7 +183,7 @@ inline hipError_t h2d(void* dst, const void* src, size_t bytes, hipStream_t s) {
         const size_t n = std::min(kStageChunk, bytes - off);
         hipError_t e = staging_reserve(st, n);
         if (e != hipSuccess) return e;
-        std::memcpy(st.buf.p, static_cast<const unsigned char*>(src) + off, n);
+        host_memcpy(st.buf.p, static_cast<const unsigned char*>(src) + off, n);
         if ((e = hipMemcpyAsync(static_cast<unsigned char*>(dst) + off, st.buf.p, n, hipMemcpyHostToDevice, s)) !=
             hipSuccess)
             return e;
@@ -188,7 +221,7 @@ inline hipError_t d2h(void* dst, const void* src, size_t bytes, hipStream_t s) {
                                 s)) != hipSuccess)
             return e;
         if ((e = hipStreamSynchronize(s)) != hipSuccess) return e;
-        std::memcpy(static_cast<unsigned char*>(dst) + off, st.buf.p, n);
+        host_memcpy(static_cast<unsigned char*>(dst) + off, st.buf.p, n);
     }
     return hipSuccess;
 }
@@ -230,6 +263,7 @@ struct CloudLayout {
     // seed grid (targets): kSeedGrid^3 cells over the bounding box, per cell the
     // Morton index of the target nearest to its centre (a search bound seed)
     DevBuf<int32_t> sgrid;
+    DevBuf<unsigned long long> sgk;  // its build's ping-pong cell keys (2 x kSeedGrid^3: d^2 bits << 32 | index)
     float sg_lo[3] = {0.f, 0.f, 0.f}, sg_inv[3] = {0.f, 0.f, 0.f};  // fp32 frame: cell = (x - lo) * inv
     DevBuf<uint32_t> codes;   // scratch (2n)
     DevBuf<int32_t> ids;      // scratch
@@ -244,6 +278,7 @@ struct CloudLayout {
         slo.release();
         shi.release();
         sgrid.release();
+        sgk.release();
         codes.release();
         ids.release();
         sort_tmp.release();
@@ -366,6 +401,8 @@ struct TargetDesc {
     int ntiles, nsuper, seed_stride, sg_on;            // sg_on: queries seeded by the seed grid (opt.seed_grid)
     double ox, oy, oz;                                 // fp32 frame origin (CloudLayout::org)
     const int32_t* sgrid;                              // seed grid (CloudLayout::sgrid; built with the target)
+    unsigned long long* sgk;                           // its build's scratch (CloudLayout::sgk)
+    int npts;                                          // real points (p4 holds ntiles x 64, padded far)
     float sg_lo[3], sg_inv[3];
 };
 
@@ -615,7 +652,9 @@ hipError_t launch_gather_rows(const double* in, const int32_t* idx, int64_t offs
 #endif
 constexpr int kSeedGrid = ORPCD_SEED_GRID;  // cells per axis
 hipError_t prepare_seed_grid(CloudLayout& L);
-hipError_t launch_seed_grids(const TargetDesc* tdesc, int first, int count, hipStream_t s);
+// sgk[k]: target first + k's CloudLayout::sgk (host copy of the pointer); max_points: the largest of their n
+hipError_t launch_seed_grids(const TargetDesc* tdesc, int first, int count, int max_points,
+                             unsigned long long* const* sgk, hipStream_t s);
 hipError_t launch_morton(const double* xyz, int64_t n, const double lo[3], double scale, uint32_t* code,
                          int32_t* idx, hipStream_t s);
 hipError_t build_layout(const double* dev_in64, int64_t n, const double bbox_lo[3], double bbox_ext,

@@ -11,7 +11,6 @@
 #include <cstring>
 #include <new>
 #include <random>
-#include <thread>
 #include <utility>
 
 #include <rccl/rccl.h>  // types only: librccl is loaded at run time (rccl_api)
@@ -40,11 +39,48 @@ using namespace orpcd;
 
 namespace {
 
-bool finite_cloud(const double* xyz, int64_t n) {
-    for (int64_t i = 0; i < 3 * n; ++i)
-        if (!std::isfinite(xyz[i])) return false;
-    return true;
+// Every coordinate finite, and the bounding box: one pass over the cloud,
+// split over host threads for large clouds (C5's 1M points: 3.5 -> 0.6 ms).
+struct CloudScan {
+    bool finite = true;
+    double lo[3] = {0.0, 0.0, 0.0}, hi[3] = {0.0, 0.0, 0.0};
+};
+CloudScan scan_cloud(const double* xyz, int64_t n) {
+    CloudScan r;
+    if (n <= 0) return r;
+    constexpr int64_t kChunk = 1 << 16;
+    const int nch = (int)((n + kChunk - 1) / kChunk);
+    std::vector<CloudScan> part((size_t)nch);
+    host_parallel(nch, [&](int ch) {
+        CloudScan& p = part[(size_t)ch];
+        const int64_t i0 = ch * kChunk, i1 = std::min(n, i0 + kChunk);
+        bool fin = true;
+        double lo[3] = {xyz[3 * i0], xyz[3 * i0 + 1], xyz[3 * i0 + 2]}, hi[3] = {lo[0], lo[1], lo[2]};
+        for (int64_t i = i0; i < i1; ++i)
+            for (int a = 0; a < 3; ++a) {
+                const double v = xyz[3 * i + a];
+                fin &= std::isfinite(v);
+                lo[a] = std::min(lo[a], v);
+                hi[a] = std::max(hi[a], v);
+            }
+        p.finite = fin;
+        for (int a = 0; a < 3; ++a) {
+            p.lo[a] = lo[a];
+            p.hi[a] = hi[a];
+        }
+    });
+    r = part[0];
+    for (const CloudScan& p : part) {
+        r.finite &= p.finite;
+        for (int a = 0; a < 3; ++a) {
+            r.lo[a] = std::min(r.lo[a], p.lo[a]);
+            r.hi[a] = std::max(r.hi[a], p.hi[a]);
+        }
+    }
+    return r;
 }
+
+bool finite_cloud(const double* xyz, int64_t n) { return scan_cloud(xyz, n).finite; }
 
 // Feature rows the matrix-core search can order: finite entries and a squared
 // norm <= 1e150, so every expansion |q|^2 + |t|^2 - 2 q.t stays finite and far
@@ -65,15 +101,11 @@ bool feature_rows_ok(const double* f, int64_t rows, int dim) {
 }
 
 void host_bbox(const double* xyz, int64_t n, double lo[3], double hi[3], double* ext) {
+    const CloudScan r = scan_cloud(xyz, n);  // min / max are exact: the same box in any order
     for (int a = 0; a < 3; ++a) {
-        lo[a] = xyz[a];
-        hi[a] = xyz[a];
+        lo[a] = r.lo[a];
+        hi[a] = r.hi[a];
     }
-    for (int64_t i = 1; i < n; ++i)
-        for (int a = 0; a < 3; ++a) {
-            lo[a] = std::min(lo[a], xyz[3 * i + a]);
-            hi[a] = std::max(hi[a], xyz[3 * i + a]);
-        }
     *ext = std::max(hi[0] - lo[0], std::max(hi[1] - lo[1], hi[2] - lo[2]));
 }
 
@@ -134,10 +166,21 @@ int upload_target_k(orpcd_ctx* c, int k, const double* xyz, int64_t m, double ep
     return ORPCD_OK;
 }
 
+// the seed grids of targets [first, first + count) (descriptors uploaded)
+hipError_t seed_grids(orpcd_ctx* c, int first, int count) {
+    unsigned long long* sgk[kMaxTargets];
+    int64_t mx = 0;
+    for (int k = 0; k < count; ++k) {
+        sgk[k] = c->tgts[first + k].sgk.p;
+        mx = std::max(mx, c->tgts[first + k].n);
+    }
+    return launch_seed_grids(c->tdesc.p, first, count, (int)mx, sgk, c->stream);
+}
+
 int upload_target(orpcd_ctx* c, const double* xyz, int64_t m, double eps) {
     int rc = upload_target_k(c, 0, xyz, m, eps);
     if (rc) return rc;
-    CTX_CHECK(c, launch_seed_grids(c->tdesc.p, 0, 1, c->stream));
+    CTX_CHECK(c, seed_grids(c, 0, 1));
     return ORPCD_OK;
 }
 
@@ -148,7 +191,7 @@ int targets_for_epsilon(orpcd_ctx* c, int ntgt, double eps) {
         std::vector<double> host = c->tgt_host[k];
         int rc = upload_target_k(c, k, host.data(), c->tgts[k].n, eps);
         if (rc) return rc;
-        CTX_CHECK(c, launch_seed_grids(c->tdesc.p, k, 1, c->stream));
+        CTX_CHECK(c, seed_grids(c, k, 1));
     }
     return ORPCD_OK;
 }
@@ -858,23 +901,6 @@ int run_passes(orpcd_ctx* c, int B, const orpcd_gicp_params* p, double* T_out, d
 int read_outputs(orpcd_ctx* c, int B, unsigned long long tiles_before, double* T_out, double* rmse_out,
                  double* fitness_out, int32_t* iters_out, int64_t* ncorr_out);
 
-// f(b) for b in [0, n) on up to 16 host threads (the GPU box grants 16 cores;
-// every b writes only its own outputs)
-template <typename Fn>
-void host_parallel(int n, Fn f) {
-    const int nt = std::max(1, std::min({n, 16, (int)std::max(1u, std::thread::hardware_concurrency())}));
-    if (nt <= 1) {
-        for (int b = 0; b < n; ++b) f(b);
-        return;
-    }
-    std::vector<std::thread> th;
-    for (int t = 0; t < nt; ++t)
-        th.emplace_back([&, t] {
-            for (int b = t; b < n; b += nt) f(b);
-        });
-    for (auto& x : th) x.join();
-}
-
 // RCCL entry points, resolved from librccl.so at first use: the library
 // itself links no collective library, so a host without RCCL still loads it
 // (only orpcd_comm_* then fail, with ORPCD_EDEVICE).
@@ -1024,7 +1050,7 @@ int orpcd_set_targets(orpcd_ctx* c, const double* xyz, const int64_t* m, int32_t
         if (rc) return rc;
         off += m[k];
     }
-    CTX_CHECK(c, launch_seed_grids(c->tdesc.p, 0, ntargets, c->stream));  // every target's grid, one launch
+    CTX_CHECK(c, seed_grids(c, 0, ntargets));  // every target's grid, one set of launches
     CTX_CHECK(c, hipStreamSynchronize(c->stream));
     c->ntgt = ntargets;
     return ORPCD_OK;

@@ -96,6 +96,33 @@ class LegacyDraws:
         return ("MT19937", self._key.copy(), int(self._pos[0]), int(self._hg[0]), float(self._g[0]))
 
 
+class _MissingSymbol:
+    """An entry point a variant library (ORPCD_HIP_LIB: another commit's build,
+    for A/B runs) does not export: its ctypes set-up is accepted, a call raises."""
+
+    def __init__(self, name):
+        self.__dict__["name"] = name
+
+    def __setattr__(self, key, value):
+        pass
+
+    def __call__(self, *args):
+        raise NativeError(f"{self.name} is not exported by the variant library {LIB_PATH}")
+
+
+class _VariantLib:
+    def __init__(self, lib):
+        self.__dict__["_lib"] = lib
+
+    def __getattr__(self, name):
+        try:
+            return getattr(self._lib, name)
+        except AttributeError:
+            m = _MissingSymbol(name)
+            self.__dict__[name] = m
+            return m
+
+
 def load_library():
     """Load liborpcd_hip.so (raises NativeError if it is not built)."""
     global _lib
@@ -107,6 +134,8 @@ def load_library():
                               "`python multi-scale-pointcloud-registration_amd/build_native.py` "
                               "(or __graft_entry__.build()).  There is no CPU fallback.")
         L = ctypes.CDLL(LIB_PATH)
+        if "ORPCD_HIP_LIB" in os.environ:  # a variant of another commit may lack newer entry points
+            L = _VariantLib(L)
         vp, c_int, c_i64, c_dbl = ctypes.c_void_p, ctypes.c_int, ctypes.c_int64, ctypes.c_double
         L.orpcd_abi_version.restype = c_int
         L.orpcd_device_count.argtypes = [ctypes.POINTER(c_int)]

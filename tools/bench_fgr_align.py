@@ -108,7 +108,7 @@ def main():
                                    seconds_per_call=round(per, 4),
                                    align_seconds_extrapolated=round(per * len(seq_opt.calls), 1),
                                    speedup_batched=round(per * len(seq_opt.calls) / bat["seconds"], 1),
-                                   parity_calls_within_1e-8=f"{match}/{k}")
+                                   parity_calls_within_1e8=f"{match}/{k}")
     print(json.dumps(out, indent=1))
     if a.out:
         json.dump(out, open(a.out, "w"), indent=1)
