@@ -77,9 +77,16 @@ __device__ __forceinline__ int fpfh_bin(double x) {
 }
 
 // SPFH: one thread per point, histogram in LDS (64 threads x 33 doubles).
+// blockIdx.y: cloud y of a batch (every array at its per-cloud stride,
+// neighbour indices within the cloud); one cloud: y = 0.
 __global__ __launch_bounds__(64) void spfh_kernel(const double* __restrict__ pts, const double* __restrict__ nrm,
                                                   int n, const int32_t* __restrict__ nbr,
                                                   const int32_t* __restrict__ cnt, int k, double* __restrict__ spfh) {
+    pts += (size_t)blockIdx.y * 3 * n;
+    nrm += (size_t)blockIdx.y * 3 * n;
+    nbr += (size_t)blockIdx.y * n * k;
+    cnt += (size_t)blockIdx.y * n;
+    spfh += (size_t)blockIdx.y * 33 * n;
     __shared__ double h[64][33];
     const int i = blockIdx.x * 64 + threadIdx.x;
     for (int j = 0; j < 33; ++j) h[threadIdx.x][j] = 0.0;
@@ -111,6 +118,11 @@ __global__ __launch_bounds__(256) void fpfh_kernel(const double* __restrict__ sp
                                                    const int32_t* __restrict__ nbr, const double* __restrict__ d2,
                                                    const int32_t* __restrict__ cnt, int k, double* __restrict__ feat) {
 #pragma clang fp contract(off)
+    spfh += (size_t)blockIdx.y * 33 * n;  // cloud y of a batch
+    nbr += (size_t)blockIdx.y * n * k;
+    d2 += (size_t)blockIdx.y * n * k;
+    cnt += (size_t)blockIdx.y * n;
+    feat += (size_t)blockIdx.y * kFD * n;
     const int i = blockIdx.x * 256 + threadIdx.x;
     if (i >= n) return;
     double f[33];
@@ -478,10 +490,13 @@ __global__ void row_hash_kernel(const double* __restrict__ F, int n, unsigned lo
     val[i] = i;
 }
 
-__global__ void run_start_kernel(const unsigned long long* __restrict__ ks, int n, int32_t* __restrict__ hv) {
+// seg: rows per segment (a batch's clouds sorted segment by segment; a run
+// never crosses a segment); one cloud: seg = n
+__global__ void run_start_kernel(const unsigned long long* __restrict__ ks, int n, int32_t* __restrict__ hv,
+                                 int seg) {
     const int p = blockIdx.x * blockDim.x + threadIdx.x;
     if (p >= n) return;
-    hv[p] = (p == 0 || ks[p] != ks[p - 1]) ? p : 0;
+    hv[p] = (p % seg == 0 || ks[p] != ks[p - 1]) ? p : 0;
 }
 
 __global__ void representative_kernel(const double* __restrict__ F, const int32_t* __restrict__ vs,
@@ -829,8 +844,14 @@ __global__ __launch_bounds__(256) void fgr_irls_kernel(const double* __restrict_
 }
 
 // ---------------------------------------------------------- small helpers
+// Each takes blockIdx.y as the cloud of a batch (orpcd_fgr_optimize_batch:
+// cloud y at the given strides; a single cloud launches one row, strides 0):
+// every cloud's blocks do the single-cloud arithmetic unchanged.
 // Per-block fixed-order partial sums of x, y, z (normalisation means).
-__global__ __launch_bounds__(256) void sum3_kernel(const double* __restrict__ xyz, int n, double* __restrict__ part) {
+__global__ __launch_bounds__(256) void sum3_kernel(const double* __restrict__ xyz, int n, double* __restrict__ part,
+                                                   int64_t xyz_stride, int64_t part_stride) {
+    xyz += blockIdx.y * xyz_stride;
+    part += blockIdx.y * part_stride;
     __shared__ double red[4][3];
     const int i = blockIdx.x * 256 + threadIdx.x;
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
@@ -852,7 +873,16 @@ __global__ __launch_bounds__(256) void sum3_kernel(const double* __restrict__ xy
 
 // Per-block max of |p - mean|.
 __global__ __launch_bounds__(256) void maxnorm_kernel(const double* __restrict__ xyz, int n, double mx, double my,
-                                                      double mz, double* __restrict__ part) {
+                                                      double mz, double* __restrict__ part,
+                                                      const double* __restrict__ means, int64_t xyz_stride,
+                                                      int64_t part_stride) {
+    if (means) {  // batch: cloud y's mean
+        mx = means[3 * blockIdx.y];
+        my = means[3 * blockIdx.y + 1];
+        mz = means[3 * blockIdx.y + 2];
+    }
+    xyz += blockIdx.y * xyz_stride;
+    part += blockIdx.y * part_stride;
     __shared__ double red[4];
     const int i = blockIdx.x * 256 + threadIdx.x;
     double v = 0.0;
@@ -869,7 +899,10 @@ __global__ __launch_bounds__(256) void maxnorm_kernel(const double* __restrict__
 
 // q = T p (homogeneous, fp64) for EvaluateRegistration.
 __global__ void transform_points_kernel(const double* __restrict__ in, int n, const double* __restrict__ T,
-                                        double* __restrict__ out) {
+                                        double* __restrict__ out, int64_t stride) {
+    in += blockIdx.y * stride;
+    out += blockIdx.y * stride;
+    T += 16 * blockIdx.y;
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     const double x = in[3 * i], y = in[3 * i + 1], z = in[3 * i + 2];
@@ -881,7 +914,11 @@ __global__ void transform_points_kernel(const double* __restrict__ in, int n, co
 // Per-block (count, sum d^2) of nn1 results (EvaluateRegistration).
 __global__ __launch_bounds__(256) void corr_stats_kernel(const int32_t* __restrict__ idx,
                                                          const double* __restrict__ d2, int n,
-                                                         double* __restrict__ part) {
+                                                         double* __restrict__ part, int64_t stride,
+                                                         int64_t part_stride) {
+    idx += blockIdx.y * stride;
+    d2 += blockIdx.y * stride;
+    part += blockIdx.y * part_stride;
     __shared__ double red[4][2];
     const int i = blockIdx.x * 256 + threadIdx.x;
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
@@ -904,12 +941,13 @@ __global__ __launch_bounds__(256) void corr_stats_kernel(const int32_t* __restri
 
 // ---------------------------------------------------------------- launchers
 hipError_t launch_fpfh(const double* pts, const double* nrm, int64_t n, const int32_t* nbr, const double* d2,
-                       const int32_t* cnt, int k, double* spfh, double* feat36, hipStream_t s) {
+                       const int32_t* cnt, int k, double* spfh, double* feat36, hipStream_t s, int clouds) {
     if (n <= 0) return hipSuccess;
-    spfh_kernel<<<(unsigned)((n + 63) / 64), 64, 0, s>>>(pts, nrm, (int)n, nbr, cnt, k, spfh);
+    spfh_kernel<<<dim3((unsigned)((n + 63) / 64), (unsigned)clouds), 64, 0, s>>>(pts, nrm, (int)n, nbr, cnt, k, spfh);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
-    fpfh_kernel<<<(unsigned)((n + 255) / 256), 256, 0, s>>>(spfh, (int)n, nbr, d2, cnt, k, feat36);
+    fpfh_kernel<<<dim3((unsigned)((n + 255) / 256), (unsigned)clouds), 256, 0, s>>>(spfh, (int)n, nbr, d2, cnt, k,
+                                                                                   feat36);
     return hipGetLastError();
 }
 
@@ -1094,7 +1132,7 @@ hipError_t dedup_rows(const double* F, const double* n2, int64_t n, DedupBufs& b
         return e;
     if ((e = b.tmp.ensure(std::max(t1, std::max(t2, t3)))) != hipSuccess) return e;
     if ((e = hipcub::DeviceRadixSort::SortPairs(b.tmp.p, t1, k0, k1, v0, v1, (int)n, 0, 64, s)) != hipSuccess) return e;
-    run_start_kernel<<<g, 256, 0, s>>>(k1, (int)n, v0);
+    run_start_kernel<<<g, 256, 0, s>>>(k1, (int)n, v0, (int)n);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     if ((e = hipcub::DeviceScan::InclusiveScan(b.tmp.p, t2, v0, b.head.p, hipcub::Max(), (int)n, s)) != hipSuccess)
         return e;
@@ -1113,25 +1151,48 @@ hipError_t dedup_rows(const double* F, const double* n2, int64_t n, DedupBufs& b
 }
 
 // dedup_rows' representative flags only (no count, no gather, no host
-// sync): uflag_out[i] = 1 iff row i is the lowest index of its exact-equal
-// rows.  Scratch in b (reused in stream order by the next call).
-hipError_t dedup_flags(const double* F, int64_t n, DedupBufs& b, unsigned char* uflag_out, hipStream_t s) {
+// sync), for `clouds` row sets of n rows each (F and uflag_out back to back):
+// uflag_out[i] = 1 iff row i is the lowest index of the exact-equal rows of
+// its set.  Several sets sort segment by segment (stable, as the single
+// sort); scratch in b (reused in stream order by the next call).
+__global__ void segment_offsets_kernel(int32_t* __restrict__ off, int nseg, int n) {
+    const int k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k <= nseg) off[k] = k * n;
+}
+hipError_t dedup_flags(const double* F, int64_t n, DedupBufs& b, unsigned char* uflag_out, hipStream_t s,
+                       int clouds) {
     hipError_t e;
     if (n <= 0) return hipSuccess;
-    if ((e = b.key.ensure((size_t)n * 2)) != hipSuccess) return e;
-    if ((e = b.val.ensure((size_t)n * 2)) != hipSuccess) return e;
-    if ((e = b.head.ensure((size_t)n + 1)) != hipSuccess) return e;
-    const unsigned g = (unsigned)((n + 255) / 256);
-    unsigned long long *k0 = b.key.p, *k1 = b.key.p + n;
-    int32_t *v0 = b.val.p, *v1 = b.val.p + n;
-    row_hash_kernel<<<g, 256, 0, s>>>(F, (int)n, k0, v0);
+    const int64_t N = n * clouds;
+    if ((e = b.key.ensure((size_t)N * 2)) != hipSuccess) return e;
+    if ((e = b.val.ensure((size_t)N * 2)) != hipSuccess) return e;
+    if ((e = b.head.ensure((size_t)N + clouds + 2)) != hipSuccess) return e;
+    const unsigned g = (unsigned)((N + 255) / 256);
+    unsigned long long *k0 = b.key.p, *k1 = b.key.p + N;
+    int32_t *v0 = b.val.p, *v1 = b.val.p + N, *off = b.head.p + N;
+    row_hash_kernel<<<g, 256, 0, s>>>(F, (int)N, k0, v0);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     size_t t1 = 0, t2 = 0;
-    if ((e = hipcub::DeviceRadixSort::SortPairs(nullptr, t1, k0, k1, v0, v1, (int)n, 0, 64, s)) != hipSuccess) return e;
-    if ((e = hipcub::DeviceScan::InclusiveScan(nullptr, t2, v0, v0, hipcub::Max(), (int)n, s)) != hipSuccess) return e;
+    if (clouds > 1) {
+        segment_offsets_kernel<<<(unsigned)((clouds + 256) / 256), 256, 0, s>>>(off, clouds, (int)n);
+        if ((e = hipGetLastError()) != hipSuccess) return e;
+        if ((e = hipcub::DeviceSegmentedRadixSort::SortPairs(nullptr, t1, k0, k1, v0, v1, (int)N, clouds, off,
+                                                             off + 1, 0, 64, s)) != hipSuccess)
+            return e;
+    } else if ((e = hipcub::DeviceRadixSort::SortPairs(nullptr, t1, k0, k1, v0, v1, (int)n, 0, 64, s)) != hipSuccess) {
+        return e;
+    }
+    if ((e = hipcub::DeviceScan::InclusiveScan(nullptr, t2, v0, v0, hipcub::Max(), (int)N, s)) != hipSuccess) return e;
     if ((e = b.tmp.ensure(std::max(t1, t2))) != hipSuccess) return e;
-    if ((e = hipcub::DeviceRadixSort::SortPairs(b.tmp.p, t1, k0, k1, v0, v1, (int)n, 0, 64, s)) != hipSuccess) return e;
-    run_start_kernel<<<g, 256, 0, s>>>(k1, (int)n, v0);
+    if (clouds > 1) {
+        if ((e = hipcub::DeviceSegmentedRadixSort::SortPairs(b.tmp.p, t1, k0, k1, v0, v1, (int)N, clouds, off,
+                                                             off + 1, 0, 64, s)) != hipSuccess)
+            return e;
+    } else if ((e = hipcub::DeviceRadixSort::SortPairs(b.tmp.p, t1, k0, k1, v0, v1, (int)n, 0, 64, s)) != hipSuccess) {
+        return e;
+    }
+    n = N;
+    run_start_kernel<<<g, 256, 0, s>>>(k1, (int)n, v0, (int)(N / clouds));
     if ((e = hipGetLastError()) != hipSuccess) return e;
     if ((e = hipcub::DeviceScan::InclusiveScan(b.tmp.p, t2, v0, b.head.p, hipcub::Max(), (int)n, s)) != hipSuccess)
         return e;
@@ -1166,24 +1227,33 @@ hipError_t launch_fgr_irls_batch(const double* pq, const int64_t* meta_reg, int 
     return hipGetLastError();
 }
 
-hipError_t launch_sum3(const double* xyz, int64_t n, double* part, hipStream_t s) {
-    sum3_kernel<<<(unsigned)((n + 255) / 256), 256, 0, s>>>(xyz, (int)n, part);
+hipError_t launch_sum3(const double* xyz, int64_t n, double* part, hipStream_t s, int clouds) {
+    // partials: cloud y's ceil(n / 256) x 3 at part + 3 ceil(n / 256) y
+    const int64_t nb = (n + 255) / 256;
+    sum3_kernel<<<dim3((unsigned)nb, (unsigned)clouds), 256, 0, s>>>(xyz, (int)n, part, 3 * n, 3 * nb);
     return hipGetLastError();
 }
 
-hipError_t launch_maxnorm(const double* xyz, int64_t n, const double mean[3], double* part, hipStream_t s) {
-    maxnorm_kernel<<<(unsigned)((n + 255) / 256), 256, 0, s>>>(xyz, (int)n, mean[0], mean[1], mean[2], part);
+hipError_t launch_maxnorm(const double* xyz, int64_t n, const double mean[3], double* part, hipStream_t s,
+                          int clouds, const double* dev_means) {
+    const int64_t nb = (n + 255) / 256;
+    maxnorm_kernel<<<dim3((unsigned)nb, (unsigned)clouds), 256, 0, s>>>(
+        xyz, (int)n, mean ? mean[0] : 0.0, mean ? mean[1] : 0.0, mean ? mean[2] : 0.0, part, dev_means, 3 * n, nb);
     return hipGetLastError();
 }
 
-hipError_t launch_transform_points(const double* in, int64_t n, const double* T, double* out, hipStream_t s) {
+hipError_t launch_transform_points(const double* in, int64_t n, const double* T, double* out, hipStream_t s,
+                                   int clouds) {
     if (n <= 0) return hipSuccess;
-    transform_points_kernel<<<(unsigned)((n + 255) / 256), 256, 0, s>>>(in, (int)n, T, out);
+    transform_points_kernel<<<dim3((unsigned)((n + 255) / 256), (unsigned)clouds), 256, 0, s>>>(in, (int)n, T, out,
+                                                                                              3 * n);
     return hipGetLastError();
 }
 
-hipError_t launch_corr_stats(const int32_t* idx, const double* d2, int64_t n, double* part, hipStream_t s) {
-    corr_stats_kernel<<<(unsigned)((n + 255) / 256), 256, 0, s>>>(idx, d2, (int)n, part);
+hipError_t launch_corr_stats(const int32_t* idx, const double* d2, int64_t n, double* part, hipStream_t s,
+                             int clouds) {
+    const int64_t nb = (n + 255) / 256;
+    corr_stats_kernel<<<dim3((unsigned)nb, (unsigned)clouds), 256, 0, s>>>(idx, d2, (int)n, part, n, 2 * nb);
     return hipGetLastError();
 }
 

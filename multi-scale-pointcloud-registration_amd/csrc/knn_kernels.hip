@@ -325,8 +325,26 @@ __global__ __launch_bounds__(256) void knn_wave_kernel(
     const float4* __restrict__ thi, int ntiles, const float4* __restrict__ slo, const float4* __restrict__ shi,
     int nsuper, const double* __restrict__ in64, double r2, float margin, double ox, double oy, double oz, int K,
     int out_input_order, double* __restrict__ rawcov6, int32_t* __restrict__ nbr_idx, double* __restrict__ nbr_d2,
-    int32_t* __restrict__ nbr_cnt, double* __restrict__ mean_dist, int KC, KnnTieOut ties) {
+    int32_t* __restrict__ nbr_cnt, double* __restrict__ mean_dist, int KC, KnnTieOut ties,
+    const double* __restrict__ orgs = nullptr, const float* __restrict__ margins = nullptr) {
 #pragma clang fp contract(off)
+    if (orgs) {  // copy y of a BatchLayout: its frame, points, boxes and outputs
+        const size_t y = blockIdx.y;
+        ox = orgs[3 * y];
+        oy = orgs[3 * y + 1];
+        oz = orgs[3 * y + 2];
+        margin = margins[y];
+        xyz64 += y * 3 * n;
+        in64 += y * 3 * n;
+        tlo += y * ntiles;
+        thi += y * ntiles;
+        slo += y * nsuper;
+        shi += y * nsuper;
+        if (rawcov6) rawcov6 += y * 6 * n;
+        if (nbr_idx) nbr_idx += y * (size_t)n * KC;
+        if (nbr_d2) nbr_d2 += y * (size_t)n * KC;
+        if (nbr_cnt) nbr_cnt += y * n;
+    }
     const int lane = threadIdx.x & 63;
     const int q = blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     if (q >= n) return;  // wave-uniform
@@ -745,6 +763,18 @@ hipError_t launch_knn_tiles(const CloudLayout& L, const double* in64, int k, dou
     else
         return hipErrorInvalidValue;
 #undef ORPCD_KNN_TILES
+    return hipGetLastError();
+}
+
+hipError_t launch_knn_batch(const BatchLayout& L, const int32_t* perm, const double* in64, const double* orgs,
+                            const float* margins, int k, double radius, double* rawcov6, int32_t* nbr_idx,
+                            double* nbr_d2, int32_t* nbr_cnt, hipStream_t s) {
+    if (L.n <= 0 || L.B <= 0) return hipSuccess;
+    if (k < 1 || k > 64) return hipErrorInvalidValue;
+    const double r2 = radius > 0 ? radius * radius : __builtin_huge_val();
+    knn_wave_kernel<<<dim3((unsigned)((L.n + 3) / 4), (unsigned)L.B), 256, 0, s>>>(
+        L.xyz64.p, perm, (int)L.n, L.tlo.p, L.thi.p, (int)L.ntiles, L.slo.p, L.shi.p, (int)L.nsuper, in64, r2, 0.0f,
+        0.0, 0.0, 0.0, k, 1, rawcov6, nbr_idx, nbr_d2, nbr_cnt, nullptr, k, KnnTieOut{}, orgs, margins);
     return hipGetLastError();
 }
 

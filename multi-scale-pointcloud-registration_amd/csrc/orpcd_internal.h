@@ -285,6 +285,20 @@ struct CloudLayout {
     }
 };
 
+// B rigid copies of one cloud in its Morton order (build_batch_layout): the
+// copies' fp64 points, fp32 frames and tile / super-tile boxes, copy b at
+// b x (3n | npad | ntiles | nsuper).
+struct BatchLayout {
+    int64_t n = 0, npad = 0, ntiles = 0, nsuper = 0;
+    int B = 0;
+    DevBuf<double> xyz64;
+    DevBuf<float4> p4, tlo, thi, qbox, slo, shi;
+    void release() {
+        xyz64.release();
+        for (auto* b : {&p4, &tlo, &thi, &qbox, &slo, &shi}) b->release();
+    }
+};
+
 // Morton order of a query batch (launch_nn1): codes, identity ids, the
 // sorted order and the sort's scratch.
 struct QueryOrder {
@@ -558,12 +572,26 @@ struct orpcd_ctx {
         // evaluation layouts, and the per-start reduction partials, tuples,
         // IRLS problem table and transforms
         struct Batch {
-            orpcd::DevBuf<double> X, FB, part, pq, Tn, T, Q, txyz[orpcd::kMaxTargets], tfeat[orpcd::kMaxTargets];
+            orpcd::DevBuf<double> X, FB, part, pq, Tn, T, Q, mean, txyz[orpcd::kMaxTargets],
+                tfeat[orpcd::kMaxTargets];
             orpcd::DevBuf<int64_t> meta;
             orpcd::DevBuf<unsigned char> uflag;
             orpcd::CloudLayout tlay[orpcd::kMaxTargets];
+            // every start's features at once: the base's Morton order, the
+            // copies' layouts and frames, their KNN / normals / SPFH scratch
+            orpcd::CloudLayout base;
+            orpcd::BatchLayout bl;
+            orpcd::DevBuf<double> src, orgs, raw, nd2, nrm, spfh;
+            orpcd::DevBuf<float> margins;
+            orpcd::DevBuf<int32_t> nbr, cnt;
             void release() {
-                for (auto* b : {&X, &FB, &part, &pq, &Tn, &T, &Q}) b->release();
+                for (auto* b : {&X, &FB, &part, &pq, &Tn, &T, &Q, &mean, &src, &orgs, &raw, &nd2, &nrm, &spfh})
+                    b->release();
+                base.release();
+                bl.release();
+                margins.release();
+                nbr.release();
+                cnt.release();
                 for (int k = 0; k < orpcd::kMaxTargets; ++k) {
                     txyz[k].release();
                     tfeat[k].release();
@@ -659,6 +687,8 @@ hipError_t launch_morton(const double* xyz, int64_t n, const double lo[3], doubl
                          int32_t* idx, hipStream_t s);
 hipError_t build_layout(const double* dev_in64, int64_t n, const double bbox_lo[3], double bbox_ext,
                         const double origin[3], CloudLayout& L, bool with_tiles, hipStream_t s);
+hipError_t build_batch_layout(const double* in64, int64_t n, int B, const int32_t* perm, const double* orgs,
+                              BatchLayout& L, hipStream_t s);
 
 // knn_kernels.hip
 constexpr int kMaxKnn = 1024;  // largest neighbourhood the device KNN keeps (16 sorted chunks of 64 per wave)
@@ -674,6 +704,12 @@ hipError_t launch_normals_cov(const double* rawcov6, int64_t n, const double* Rc
 constexpr int kTieExtra = 4;
 hipError_t launch_knn_cov_ties(const CloudLayout& L, const double* in64, int kcov, double margin, bool out_input_order,
                                double* rawcov6, const KnnTieOut& ties, hipStream_t s);
+// the same KNN (k <= 64) for every copy of a BatchLayout: perm its common
+// Morton order, in64 the copies in input order (B x n x 3), orgs / margins
+// per copy on the device; outputs at copy b x (6n | n k | n k | n), input order
+hipError_t launch_knn_batch(const BatchLayout& L, const int32_t* perm, const double* in64, const double* orgs,
+                            const float* margins, int k, double radius, double* rawcov6, int32_t* nbr_idx,
+                            double* nbr_d2, int32_t* nbr_cnt, hipStream_t s);
 hipError_t launch_cov_override(const double* ent, int count, int64_t n, double eps, double* cov6, hipStream_t s);
 
 // prep_kernels.hip
@@ -708,8 +744,10 @@ hipError_t launch_solve6_test(const double* sums, int n, double* out_serial, dou
 
 // fgr_kernels.hip
 constexpr int kFeatDim = 36;  // 33 FPFH bins padded for the 16x16x4 f64 MFMA
+// clouds > 1: that many clouds of n points back to back (every array at its
+// per-cloud stride; neighbour indices within their cloud)
 hipError_t launch_fpfh(const double* pts, const double* nrm, int64_t n, const int32_t* nbr, const double* d2,
-                       const int32_t* cnt, int k, double* spfh, double* feat36, hipStream_t s);
+                       const int32_t* cnt, int k, double* spfh, double* feat36, hipStream_t s, int clouds = 1);
 hipError_t launch_pad_features(const double* in33, int64_t n, double* out36, hipStream_t s);
 hipError_t launch_feat_norm(const double* F36, int64_t n, double* nrm2, hipStream_t s);
 int feat_nn_parts(int64_t blocks, int64_t nt, int maxp);
@@ -732,10 +770,16 @@ hipError_t launch_fgr_irls_batch(const double* pq, const int64_t* meta_reg, int 
                                  int nmem, double par0, int iters, double division_factor, double max_corr,
                                  int decrease_mu, double* T_out, hipStream_t s);
 // representative flags of dedup_rows (uflag_out[i] = row i is the lowest index of its equal rows)
-hipError_t dedup_flags(const double* F, int64_t n, DedupBufs& b, unsigned char* uflag_out, hipStream_t s);
-hipError_t launch_sum3(const double* xyz, int64_t n, double* part, hipStream_t s);
-hipError_t launch_maxnorm(const double* xyz, int64_t n, const double mean[3], double* part, hipStream_t s);
-hipError_t launch_transform_points(const double* in, int64_t n, const double* T, double* out, hipStream_t s);
-hipError_t launch_corr_stats(const int32_t* idx, const double* d2, int64_t n, double* part, hipStream_t s);
+hipError_t dedup_flags(const double* F, int64_t n, DedupBufs& b, unsigned char* uflag_out, hipStream_t s,
+                       int clouds = 1);
+// clouds > 1: that many clouds of n points back to back (xyz, T, idx / d2 and
+// partials at their natural strides; maxnorm's means from dev_means, 3 per cloud)
+hipError_t launch_sum3(const double* xyz, int64_t n, double* part, hipStream_t s, int clouds = 1);
+hipError_t launch_maxnorm(const double* xyz, int64_t n, const double mean[3], double* part, hipStream_t s,
+                          int clouds = 1, const double* dev_means = nullptr);
+hipError_t launch_transform_points(const double* in, int64_t n, const double* T, double* out, hipStream_t s,
+                                   int clouds = 1);
+hipError_t launch_corr_stats(const int32_t* idx, const double* d2, int64_t n, double* part, hipStream_t s,
+                             int clouds = 1);
 
 }  // namespace orpcd

@@ -2040,6 +2040,11 @@ int orpcd_fgr_optimize_batch(orpcd_ctx* c, const double* src, int64_t n, const d
     for (int64_t i = 0; i < 9 * (int64_t)B; ++i) CTX_REQUIRE(c, std::isfinite(R0[i]), "fgr_optimize_batch: non-finite R0");
     for (int64_t i = 0; i < 3 * (int64_t)B; ++i) CTX_REQUIRE(c, std::isfinite(t0[i]), "fgr_optimize_batch: non-finite t0");
     CTX_CHECK(c, hipSetDevice(c->device));
+    FgrTrace tr;  // ORPCD_FGR_TRACE=1: the batch's phases on stderr
+    g_fgr_trace = &tr;
+    struct Reset {
+        ~Reset() { g_fgr_trace = nullptr; }
+    } reset;
     auto& F = c->fgr;
     auto& bt = F.bt;
     hipStream_t s = c->stream;
@@ -2074,6 +2079,7 @@ int orpcd_fgr_optimize_batch(orpcd_ctx* c, const double* src, int64_t n, const d
         rc = layout_from_device(c, tg, bt.txyz[k].p, mk, bt.tlay[k], true);
         if (rc) return rc;
     }
+    fgr_mark(s, "batch: targets");
     // --- the posed sources source @ R0[b] + t0[b], rounded as numpy forms
     // them (pose_row), and their normals + FPFH, queued start after start
     std::vector<double> P((size_t)B * n * 3);
@@ -2083,26 +2089,71 @@ int orpcd_fgr_optimize_batch(orpcd_ctx* c, const double* src, int64_t n, const d
     CTX_CHECK(c, bt.X.ensure((size_t)B * n * 3));
     CTX_CHECK(c, bt.FB.ensure((size_t)B * n * kFeatDim));
     CTX_CHECK(c, h2d(bt.X.p, P.data(), P.size() * 8, s));
-    rc = fpfh_buffers(c, 0, n, fpfh_knn);
-    if (rc) return rc;
-    for (int b = 0; b < B; ++b) {
-        rc = fpfh_at(c, &P[(size_t)b * n * 3], bt.X.p + (size_t)b * n * 3, n, normal_radius, normal_knn, fpfh_radius,
-                     fpfh_knn, bt.FB.p + (size_t)b * n * kFeatDim);
+    if (normal_knn <= 64 && fpfh_knn <= 64) {
+        // every copy at once: the copies are rigid images of `src`, so they
+        // share its Morton order (BatchLayout; each copy its own frame and
+        // boxes, as its own layout would have them), and the exact KNN, the
+        // normals and FPFH are those of a per-copy layout (the neighbour
+        // lists do not depend on the order): one launch per stage
+        CTX_CHECK(c, bt.src.ensure((size_t)n * 3));
+        CTX_CHECK(c, h2d(bt.src.p, src, (size_t)n * 24, s));
+        rc = layout_from_device(c, src, bt.src.p, n, bt.base, false);
         if (rc) return rc;
+        std::vector<double> orgs((size_t)B * 3);
+        std::vector<float> margins((size_t)B);
+        host_parallel(B, [&](int b) {  // each copy's frame: its box centre, and the fp32 margin of that frame
+            const CloudScan cs = scan_cloud(&P[(size_t)b * n * 3], n);
+            double org[3];
+            for (int a = 0; a < 3; ++a) org[a] = orgs[3 * b + a] = 0.5 * (cs.lo[a] + cs.hi[a]);
+            margins[b] = (float)coord_margin(cs.lo, cs.hi, org);
+        });
+        CTX_CHECK(c, bt.orgs.ensure(orgs.size()));
+        CTX_CHECK(c, bt.margins.ensure(margins.size()));
+        CTX_CHECK(c, h2d(bt.orgs.p, orgs.data(), orgs.size() * 8, s));
+        CTX_CHECK(c, h2d(bt.margins.p, margins.data(), margins.size() * 4, s));
+        CTX_CHECK(c, build_batch_layout(bt.X.p, n, B, bt.base.perm.p, bt.orgs.p, bt.bl, s));
+        const int kk = std::max(normal_knn, fpfh_knn);
+        CTX_CHECK(c, bt.raw.ensure((size_t)B * n * 6));
+        CTX_CHECK(c, bt.nrm.ensure((size_t)B * n * 3));
+        CTX_CHECK(c, bt.nbr.ensure((size_t)B * n * kk));
+        CTX_CHECK(c, bt.nd2.ensure((size_t)B * n * kk));
+        CTX_CHECK(c, bt.cnt.ensure((size_t)B * n));
+        CTX_CHECK(c, bt.spfh.ensure((size_t)B * n * 33));
+        const bool shared = normal_knn == fpfh_knn && normal_radius == fpfh_radius;
+        CTX_CHECK(c, launch_knn_batch(bt.bl, bt.base.perm.p, bt.X.p, bt.orgs.p, bt.margins.p, normal_knn,
+                                      normal_radius, bt.raw.p, shared ? bt.nbr.p : nullptr,
+                                      shared ? bt.nd2.p : nullptr, shared ? bt.cnt.p : nullptr, s));
+        CTX_CHECK(c, launch_normals_cov(bt.raw.p, (int64_t)B * n, nullptr, 1, -1.0, bt.nrm.p, nullptr, s));
+        if (!shared)
+            CTX_CHECK(c, launch_knn_batch(bt.bl, bt.base.perm.p, bt.X.p, bt.orgs.p, bt.margins.p, fpfh_knn,
+                                          fpfh_radius, nullptr, bt.nbr.p, bt.nd2.p, bt.cnt.p, s));
+        CTX_CHECK(c, launch_fpfh(bt.X.p, bt.nrm.p, n, bt.nbr.p, bt.nd2.p, bt.cnt.p, fpfh_knn, bt.spfh.p, bt.FB.p, s,
+                                 B));
+    } else {  // neighbourhoods above 64 (chunked KNN lists): copy by copy
+        rc = fpfh_buffers(c, 0, n, fpfh_knn);
+        if (rc) return rc;
+        for (int b = 0; b < B; ++b) {
+            rc = fpfh_at(c, &P[(size_t)b * n * 3], bt.X.p + (size_t)b * n * 3, n, normal_radius, normal_knn,
+                         fpfh_radius, fpfh_knn, bt.FB.p + (size_t)b * n * kFeatDim);
+            if (rc) return rc;
+        }
     }
+    fgr_mark(s, "batch: pose + normals + fpfh");
     // --- normalisation of every posed source (fixed-order partials, one read-back per phase)
     const int64_t nb = (n + 255) / 256;
     CTX_CHECK(c, bt.part.ensure((size_t)B * nb * 3));
     std::vector<double> part((size_t)B * nb * 3), smean((size_t)B * 3), scale((size_t)B);
-    for (int b = 0; b < B; ++b) CTX_CHECK(c, launch_sum3(bt.X.p + (size_t)b * n * 3, n, bt.part.p + (size_t)b * nb * 3, s));
+    CTX_CHECK(c, launch_sum3(bt.X.p, n, bt.part.p, s, B));  // every start's partials, one launch
     CTX_CHECK(c, d2h(part.data(), bt.part.p, part.size() * 8, s));
     for (int b = 0; b < B; ++b) {
         double sum[3] = {0.0, 0.0, 0.0};
         for (int64_t q = 0; q < nb; ++q)
             for (int a = 0; a < 3; ++a) sum[a] += part[((size_t)b * nb + q) * 3 + a];
         for (int a = 0; a < 3; ++a) smean[3 * b + a] = sum[a] / (double)n;
-        CTX_CHECK(c, launch_maxnorm(bt.X.p + (size_t)b * n * 3, n, &smean[3 * b], bt.part.p + (size_t)b * nb, s));
     }
+    CTX_CHECK(c, bt.mean.ensure((size_t)B * 3));
+    CTX_CHECK(c, h2d(bt.mean.p, smean.data(), smean.size() * 8, s));
+    CTX_CHECK(c, launch_maxnorm(bt.X.p, n, nullptr, bt.part.p, s, B, bt.mean.p));
     CTX_CHECK(c, d2h(part.data(), bt.part.p, (size_t)B * nb * 8, s));
     for (int b = 0; b < B; ++b) {
         double mx = 0.0;
@@ -2110,6 +2161,7 @@ int orpcd_fgr_optimize_batch(orpcd_ctx* c, const double* src, int64_t n, const d
         scale[b] = std::max(std::max(0.0, mx), tmax[tk[b]]);
         CTX_REQUIRE(c, scale[b] > 0.0, "fgr: degenerate clouds (all points at their mean)");
     }
+    fgr_mark(s, "batch: normalisation");
     // --- initial matching + cross check per start
     std::vector<std::vector<std::pair<int, int>>> corres((size_t)B);
     if (q4) {
@@ -2121,8 +2173,7 @@ int orpcd_fgr_optimize_batch(orpcd_ctx* c, const double* src, int64_t n, const d
         // searches return (fgr_match; for i >= m the target-side answer
         // rep(j) <= j < m <= i can never point back).  No search is needed.
         CTX_CHECK(c, bt.uflag.ensure((size_t)B * n));
-        for (int b = 0; b < B; ++b)
-            CTX_CHECK(c, dedup_flags(bt.FB.p + (size_t)b * n * kFeatDim, n, F.dedup, bt.uflag.p + (size_t)b * n, s));
+        CTX_CHECK(c, dedup_flags(bt.FB.p, n, F.dedup, bt.uflag.p, s, B));  // every start's rows, segment by segment
         std::vector<unsigned char> fl((size_t)B * n);
         CTX_CHECK(c, d2h(fl.data(), bt.uflag.p, fl.size(), s));
         for (int b = 0; b < B; ++b)
@@ -2134,6 +2185,7 @@ int orpcd_fgr_optimize_batch(orpcd_ctx* c, const double* src, int64_t n, const d
             if (rc) return rc;
         }
     }
+    fgr_mark(s, "batch: matching");
     // --- tuple tests (host, one mt19937 per start, in parallel)
     std::vector<std::vector<double>> pqs((size_t)B);
     std::vector<int> K((size_t)B);
@@ -2148,6 +2200,7 @@ int orpcd_fgr_optimize_batch(orpcd_ctx* c, const double* src, int64_t n, const d
         const int fi = m[tk[b]] > n ? 1 : 0;
         K[b] = fgr_tuples(corres[b], *p, cl, scale[b], fi, 1 - fi, pqs[b]);
     });
+    fgr_mark(s, "batch: tuple tests");
     // --- IRLS: every start's problem in one launch (one workgroup each)
     std::vector<int64_t> meta_reg, meta_mem;
     int64_t off = 0;
@@ -2174,19 +2227,30 @@ int orpcd_fgr_optimize_batch(orpcd_ctx* c, const double* src, int64_t n, const d
     CTX_CHECK(c, d2h(Tn.data(), bt.Tn.p, Tn.size() * 8, s));
     for (int b = 0; b < B; ++b)
         fgr_original_scale(&Tn[(size_t)b * 16], &smean[3 * b], &tmean[3 * tk[b]], scale[b], &T[(size_t)b * 16]);
+    fgr_mark(s, "batch: irls");
     // --- EvaluateRegistration per start against its target's layout
+    // every start's queries T_b x (one launch), one nn1 per run of starts on
+    // the same target (a query's answer does not depend on its batch mates:
+    // per-query bounds, tiles visited in one fixed order), the per-start
+    // (count, sum d^2) partials in one launch
     CTX_CHECK(c, bt.T.ensure((size_t)B * 16));
-    CTX_CHECK(c, bt.Q.ensure((size_t)n * 3));
+    CTX_CHECK(c, bt.Q.ensure((size_t)B * n * 3));
     CTX_CHECK(c, h2d(bt.T.p, T.data(), T.size() * 8, s));
-    CTX_CHECK(c, c->scratch32.ensure((size_t)n));
-    CTX_CHECK(c, c->scratch64c.ensure((size_t)n));
+    CTX_CHECK(c, c->scratch32.ensure((size_t)B * n));
+    CTX_CHECK(c, c->scratch64c.ensure((size_t)B * n));
+    CTX_CHECK(c, launch_transform_points(bt.X.p, n, bt.T.p, bt.Q.p, s, B));
     const double r = p->maximum_correspondence_distance;
-    for (int b = 0; b < B; ++b) {
-        CTX_CHECK(c, launch_transform_points(bt.X.p + (size_t)b * n * 3, n, bt.T.p + 16 * (size_t)b, bt.Q.p, s));
-        CTX_CHECK(c, launch_nn1(bt.Q.p, n, bt.tlay[tk[b]], r * r, c->scratch32.p, c->scratch64c.p, c->qorder, s));
-        CTX_CHECK(c, launch_corr_stats(c->scratch32.p, c->scratch64c.p, n, bt.part.p + (size_t)b * nb * 2, s));
+    for (int b0 = 0; b0 < B;) {
+        int b1 = b0 + 1;
+        while (b1 < B && tk[b1] == tk[b0]) ++b1;
+        const size_t o = (size_t)b0 * n;
+        CTX_CHECK(c, launch_nn1(bt.Q.p + 3 * o, (int64_t)(b1 - b0) * n, bt.tlay[tk[b0]], r * r, c->scratch32.p + o,
+                                c->scratch64c.p + o, c->qorder, s));
+        b0 = b1;
     }
+    CTX_CHECK(c, launch_corr_stats(c->scratch32.p, c->scratch64c.p, n, bt.part.p, s, B));
     CTX_CHECK(c, d2h(part.data(), bt.part.p, (size_t)B * nb * 2 * 8, s));
+    fgr_mark(s, "batch: evaluation");
     for (int b = 0; b < B; ++b) {
         double cnt = 0.0, err2 = 0.0;
         for (int64_t q = 0; q < nb; ++q) {

@@ -38,9 +38,19 @@ __global__ void morton_kernel(const double* __restrict__ xyz, int n, double lox,
 
 // out64[k] = in64[perm[k]], out4[k] = (float (xyz - origin), orig index bits);
 // padding far.
+// blockIdx.y: cloud y of a batch of rigid copies sharing one Morton order
+// (orgs: its origin; in64 / out64 at y 3n, out4 at y npad); one cloud: y = 0.
 __global__ void gather_points_kernel(const double* __restrict__ in64, const int32_t* __restrict__ perm, int n,
                                      int npad, double ox, double oy, double oz, double* __restrict__ out64,
-                                     float4* __restrict__ out4) {
+                                     float4* __restrict__ out4, const double* __restrict__ orgs) {
+    if (orgs) {
+        ox = orgs[3 * blockIdx.y];
+        oy = orgs[3 * blockIdx.y + 1];
+        oz = orgs[3 * blockIdx.y + 2];
+    }
+    in64 += (size_t)blockIdx.y * 3 * n;
+    out64 += (size_t)blockIdx.y * 3 * n;
+    if (out4) out4 += (size_t)blockIdx.y * npad;
     const int k = blockIdx.x * blockDim.x + threadIdx.x;
     if (k >= npad) return;
     if (k < n) {
@@ -60,6 +70,10 @@ __global__ void gather_points_kernel(const double* __restrict__ in64, const int3
 // qbox[2 kNQ t + kNQ + k] = hi; a quarter without real points gets a point box at 3e38).
 __global__ void tile_aabb_kernel(const float4* __restrict__ p4, int n, int ntiles, float4* __restrict__ lo,
                                  float4* __restrict__ hi, float4* __restrict__ qbox) {
+    p4 += (size_t)blockIdx.y * ntiles * kTile;  // cloud y of a batch (npad = ntiles x 64)
+    lo += (size_t)blockIdx.y * ntiles;
+    hi += (size_t)blockIdx.y * ntiles;
+    qbox += (size_t)blockIdx.y * ntiles * 2 * kNQ;
     const int t = blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= ntiles) return;
     float mnx = 3.0e38f, mny = 3.0e38f, mnz = 3.0e38f, mxx = -3.0e38f, mxy = -3.0e38f, mxz = -3.0e38f;
@@ -94,6 +108,10 @@ __global__ void tile_aabb_kernel(const float4* __restrict__ p4, int n, int ntile
 // One thread per super-tile (64 tiles): AABB of the tile AABBs.
 __global__ void super_aabb_kernel(const float4* __restrict__ tlo, const float4* __restrict__ thi, int ntiles,
                                   int nsuper, float4* __restrict__ slo, float4* __restrict__ shi) {
+    tlo += (size_t)blockIdx.y * ntiles;  // cloud y of a batch
+    thi += (size_t)blockIdx.y * ntiles;
+    slo += (size_t)blockIdx.y * nsuper;
+    shi += (size_t)blockIdx.y * nsuper;
     const int u = blockIdx.x * blockDim.x + threadIdx.x;
     if (u >= nsuper) return;
     float4 lo = make_float4(3.0e38f, 3.0e38f, 3.0e38f, 0.f), hi = make_float4(-3.0e38f, -3.0e38f, -3.0e38f, 0.f);
@@ -168,7 +186,7 @@ hipError_t build_layout(const double* dev_in64, int64_t n, const double bbox_lo[
     if (e != hipSuccess) return e;
     const unsigned gp = (unsigned)((L.npad + 255) / 256);
     gather_points_kernel<<<gp, 256, 0, s>>>(dev_in64, L.perm.p, (int)n, (int)L.npad, origin[0], origin[1],
-                                            origin[2], L.xyz64.p, with_tiles ? L.p4.p : nullptr);
+                                            origin[2], L.xyz64.p, with_tiles ? L.p4.p : nullptr, nullptr);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     if (with_tiles) {
         tile_aabb_kernel<<<(unsigned)((L.ntiles + 255) / 256), 256, 0, s>>>(L.p4.p, (int)n, (int)L.ntiles, L.tlo.p,
@@ -179,6 +197,37 @@ hipError_t build_layout(const double* dev_in64, int64_t n, const double bbox_lo[
         if ((e = hipGetLastError()) != hipSuccess) return e;
     }
     return hipSuccess;
+}
+
+// B rigid copies (input order, B x n x 3 at in64) laid out in the Morton
+// order `perm` of their common base cloud (BatchLayout): a rigid motion keeps
+// Morton neighbours spatially coherent, and the culled searches' answers do
+// not depend on the order, only their speed.  Per copy its own fp32 frame
+// (orgs, B x 3 on the device), tiles and super-tiles.
+hipError_t build_batch_layout(const double* in64, int64_t n, int B, const int32_t* perm, const double* orgs,
+                              BatchLayout& L, hipStream_t s) {
+    L.n = n;
+    L.B = B;
+    L.npad = std::max<int64_t>(kTile, ((n + kTile - 1) / kTile) * kTile);
+    L.ntiles = (n + kTile - 1) / kTile;
+    L.nsuper = (L.ntiles + kSuper - 1) / kSuper;
+    hipError_t e;
+    if ((e = L.xyz64.ensure((size_t)B * n * 3)) != hipSuccess) return e;
+    if ((e = L.p4.ensure((size_t)B * L.npad)) != hipSuccess) return e;
+    if ((e = L.tlo.ensure((size_t)B * L.ntiles)) != hipSuccess) return e;
+    if ((e = L.thi.ensure((size_t)B * L.ntiles)) != hipSuccess) return e;
+    if ((e = L.qbox.ensure((size_t)B * L.ntiles * 2 * kNQ)) != hipSuccess) return e;
+    if ((e = L.slo.ensure((size_t)B * L.nsuper)) != hipSuccess) return e;
+    if ((e = L.shi.ensure((size_t)B * L.nsuper)) != hipSuccess) return e;
+    gather_points_kernel<<<dim3((unsigned)((L.npad + 255) / 256), (unsigned)B), 256, 0, s>>>(
+        in64, perm, (int)n, (int)L.npad, 0.0, 0.0, 0.0, L.xyz64.p, L.p4.p, orgs);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    tile_aabb_kernel<<<dim3((unsigned)((L.ntiles + 255) / 256), (unsigned)B), 256, 0, s>>>(
+        L.p4.p, (int)n, (int)L.ntiles, L.tlo.p, L.thi.p, L.qbox.p);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    super_aabb_kernel<<<dim3((unsigned)((L.nsuper + 255) / 256), (unsigned)B), 256, 0, s>>>(
+        L.tlo.p, L.thi.p, (int)L.ntiles, (int)L.nsuper, L.slo.p, L.shi.p);
+    return hipGetLastError();
 }
 
 }  // namespace orpcd
