@@ -315,6 +315,8 @@ int orpcd_fgr_optimize_batch(orpcd_ctx* ctx, const double* src, int64_t n, const
  *                   previous pass's measured cost (ordered dispatch)
  *   "sched_items", "sched_min_starts"  its split granularity, and the batch
  *                   size from which it is used
+ *   "sched_cap_us"  ordered dispatch: plan no split longer than this many us
+ *                   of the previous pass's measured cost (0: no cap)
  *   "seed_grid"     1 (default) / 0: every query's search bound is also
  *                   seeded by the target nearest its cell of the target's
  *                   48^3 seed grid (built at set_target / set_targets)

@@ -652,6 +652,7 @@ struct SchedX {                          // query transform side (pass p + 1)
     unsigned long long* list;            // class-major items, cap per class
     int cap, NG, have_cost, S0;          // S0: the host's uniform split (no cost known)
     float inv_want;                      // 1 / sched_items
+    float max_target;                    // cap on a split's planned cost (10 ns ticks; 0: none), opt.sched_cap_us
 };
 struct SchedS {                          // search side (pass p)
     const unsigned* cnt;                 // this pass's items per class
@@ -683,7 +684,13 @@ __device__ __forceinline__ void plan_start_items(const SchedX& sx, int slot, int
 #pragma unroll
             for (int o = 32; o >= 1; o >>= 1) t += __shfl_xor(t, o);
         }
-        if (lane == 0) s_target = fmaxf(t * sx.inv_want, 1.0f);
+        float tg = fmaxf(t * sx.inv_want, 1.0f);
+        // early passes: the pass total / sched_items is long (~80 us at C2
+        // pass 5) and a group's cost can double from one pass to the next, so
+        // an unsplit group became the launch's critical wave (r05 wave dumps);
+        // the cap splits heavy groups further there
+        if (sx.max_target > 0.0f) tg = fminf(tg, sx.max_target);
+        if (lane == 0) s_target = tg;
     }
     __syncthreads();
     const int NG = sx.NG;
@@ -2062,6 +2069,7 @@ static SchedX sched_x(const orpcd_ctx* c, int nact, int pass) {
     sx.have_cost = pass > 0;
     sx.S0 = uniform_splits(c, nact);
     sx.inv_want = 1.0f / (float)c->opt.sched_items;
+    sx.max_target = (float)c->opt.sched_cap_us * 100.0f;  // us -> s_memrealtime ticks (10 ns)
     return sx;
 }
 

@@ -639,6 +639,7 @@ struct orpcd_ctx {
         int sched_items = 10240;  // ordered dispatch: split a group until its waves cost <= pass total / this
                                   // (C2 sweep 5120 / 10240 / 20480: 15.4 / 15.0 / 16.6 ms at 30 starts)
         int sched_min_starts = 16;  // ordered dispatch only for batches of at least this many starts
+        int sched_cap_us = 0;     // ordered dispatch: a split's planned cost at most this many us (0: no cap)
         int exact_nn = 1;         // 1 (default): every correspondence is the fp64 nearest target (the
                                   // oracle's lexicographic (d^2, input index) minimum): fp32 search +
                                   // runner-up band test + fp64 re-search of the uncertified queries;

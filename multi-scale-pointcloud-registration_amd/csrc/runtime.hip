@@ -2294,6 +2294,7 @@ int orpcd_set_option(orpcd_ctx* c, const char* key, double value) {
     else if (k == "sched" && (v == 0 || v == 1)) c->opt.sched = v;
     else if (k == "sched_items" && v >= 64 && v <= (1 << 22)) c->opt.sched_items = v;
     else if (k == "sched_min_starts" && v >= 1) c->opt.sched_min_starts = v;
+    else if (k == "sched_cap_us" && v >= 0 && v <= 100000) c->opt.sched_cap_us = v;
     else if (k == "exact_nn" && (v == 0 || v == 1)) c->opt.exact_nn = v;
     else if (k == "exact_blocks" && v >= 1 && v <= 65536) c->opt.exact_blocks = v;
     else if (k == "exact_fused" && v >= 0 && v <= 4096) c->opt.exact_fused = v;

@@ -11,7 +11,12 @@ set -e
 echo "tests rc=$rc" >> $O/steps.log
 if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
 step fgr_align
-timeout -k 10 400 python3 tools/bench_fgr_align.py --out $O/fgr_align.json > $O/fgr_align.log 2>&1 || echo "fgr_align rc=$?" >> $O/steps.log
+set +e
+timeout -k 10 400 python3 tools/bench_fgr_align.py --out $O/fgr_align.json > $O/fgr_align.log 2>&1
+rc=$?
+set -e
+echo "fgr_align rc=$rc" >> $O/steps.log
+if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
 step c5
 timeout -k 10 400 python3 tools/bench_c5.py --out $O/c5.json > $O/c5.log 2>&1
 ORPCD_KNN_TILES=1 timeout -k 10 400 python3 tools/bench_c5.py --cpu-iters 0 --parity 0 --out $O/c5_knntiles.json > $O/c5_knntiles.log 2>&1
@@ -28,6 +33,17 @@ for rep in 1 2; do
     done
   done
 done
+step fgr_trace
+set +e
+ORPCD_FGR_TRACE=1 timeout -k 10 300 python3 tools/bench_fgr_align.py --cpu-seconds 0 > $O/fgr_trace.log 2>&1
+rc=$?
+set -e
+echo "fgr_trace rc=$rc" >> $O/steps.log
+if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
+step wavetime
+ORPCD_HIP_LIB=abl/wt.so ORPCD_WAVETIME=/tmp/wt.bin timeout -k 10 120 python3 tools/one_batch.py '{}' --reps 1 --starts 30 > $O/wt.run.log 2>&1
+python3 tools/wavetime.py /tmp/wt.bin --every 5 --dump $O/wt_dump.npz > $O/wt.txt 2>&1
+rm -f /tmp/wt.bin
 step bench
 timeout -k 10 500 python3 bench.py > $O/bench.json 2> $O/bench.err
 step done
