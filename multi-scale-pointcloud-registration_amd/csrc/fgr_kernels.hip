@@ -13,9 +13,14 @@
 //   * OptimizePairwiseRegistration (GNC / Geman-McClure IRLS, 100 iterations)
 //     in one workgroup, fixed-order reductions, fp64;
 //   * the normalisation means / radius and EvaluateRegistration's reduction.
-// The tuple test (100 x ncorr draws of Open3D's global mt19937, stopping at
-// maximum_tuple_count) is RNG-sequential by construction and runs on the host
-// in runtime.hip.
+//   * AdvancedMatching's tuple test: 100 x ncorr trials of three draws of a
+//     seeded mt19937 through uniform_int_distribution, kept in trial order up
+//     to maximum_tuple_count.  The draws are sequential, the trials are not:
+//     the raw word stream depends only on the seed (generated once on the
+//     host and cached), uniform_int_distribution's mapping of a word only on
+//     ncorr (Lemire's method: the rare rejected words are listed per start),
+//     so every trial of every start is evaluated at once and the accepted
+//     ones are compacted in order.
 #include <cstdio>
 #include <cstdlib>
 
@@ -628,9 +633,9 @@ __device__ __forceinline__ double wave_sum_dpp(double v) {
 __device__ __forceinline__ void irls_problem(const int64_t* meta, const double*& p, double*& q, int& K,
                                              double*& T_out) {
     if (!meta) return;
-    const int64_t* m = meta + 3 * blockIdx.x;
+    const int64_t* m = meta + 4 * blockIdx.x;
     K = (int)m[1];
-    q = const_cast<double*>(p) + m[0] + 3 * (int64_t)K;
+    q = const_cast<double*>(p) + m[3];
     p = p + m[0];
     T_out = T_out + 16 * m[2];
 }
@@ -1199,6 +1204,213 @@ hipError_t dedup_flags(const double* F, int64_t n, DedupBufs& b, unsigned char* 
     representative_kernel<<<g, 256, 0, s>>>(F, v1, b.head.p, (int)n, uflag_out);
     return hipGetLastError();
 }
+
+// ------------------------------------------------------------- tuple test
+// O3D FastGlobalRegistration.cpp AdvancedMatching (tuple part), as restated
+// sequentially by fgr_tuples (runtime.hip) and oracle/orpcd_oracle.cpp: trial t
+// draws r0, r1, r2 = dis(gen) x 3 (dis = uniform_int_distribution<int>(0,
+// ncorr - 1) over std::mt19937(seed)); the trial is accepted when the three
+// side lengths of the fi-side triangle li and of the fj-side triangle lj
+// satisfy li * s < lj < li / s; the accepted trials' pairs, in trial order,
+// are the tuples, and the loop ends after maximum_tuple_count acceptances.
+//
+// libstdc++'s uniform_int_distribution (32-bit engine, range n) takes a word
+// x, forms x * n in 64 bits, and rejects the word when the low half is below
+// (2^32 - n) mod n; otherwise the draw is the high half.  Draw d of a window
+// therefore reads word d + #{rejected words before it}: with the window's
+// rejected positions r_j sorted, key_j = r_j - word0 - j is non-decreasing and
+// the word is word0 + d + #{j : key_j <= d}.
+//
+// Arithmetic: no contraction; IEEE division and square root on both sides
+// (the device's f64 sqrt and division are correctly rounded), so each length
+// and each comparison is the host's, bit for bit.
+__device__ __forceinline__ int64_t tuple_word(const TupleJob& J, const int64_t* __restrict__ keys, int64_t d) {
+    int lo = 0, hi = J.nrej;
+    while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if (keys[J.rej + mid] <= d)
+            lo = mid + 1;
+        else
+            hi = mid;
+    }
+    return J.word0 + d + lo;
+}
+
+__device__ __forceinline__ int tuple_draw(const TupleJob& J, const uint32_t* __restrict__ words,
+                                          const int64_t* __restrict__ keys, int64_t d) {
+    const uint64_t x = (uint64_t)words[tuple_word(J, keys, d)] * (uint64_t)(uint32_t)J.ncorr;
+    return (int)(x >> 32);
+}
+
+__device__ __forceinline__ double tuple_side(const double* a, const double* b) {
+#pragma clang fp contract(off)
+    const double d0 = a[0] - b[0], d1 = a[1] - b[1], d2 = a[2] - b[2];
+    return sqrt(d0 * d0 + d1 * d1 + d2 * d2);
+}
+
+__global__ __launch_bounds__(256) void tuple_points_kernel(const TupleJob* __restrict__ jobs,
+                                                           const int32_t* __restrict__ pairs, double* __restrict__ A,
+                                                           double* __restrict__ Bv) {
+    const TupleJob& J = jobs[blockIdx.y];
+    const int64_t k = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (k >= J.ncorr) return;
+    const int64_t g = J.corr + k;
+    const int i = pairs[2 * g], j = pairs[2 * g + 1];
+    for (int a = 0; a < 3; ++a) {
+        A[3 * g + a] = (J.xi[3 * (int64_t)i + a] - J.mi[a]) / J.scale;
+        Bv[3 * g + a] = (J.xj[3 * (int64_t)j + a] - J.mj[a]) / J.scale;
+    }
+}
+
+__global__ __launch_bounds__(256) void tuple_reject_kernel(const TupleJob* __restrict__ jobs,
+                                                           const uint32_t* __restrict__ words,
+                                                           int64_t* __restrict__ rej, int32_t* __restrict__ nrej,
+                                                           int64_t rcap) {
+    const TupleJob& J = jobs[blockIdx.y];
+    if (J.tw == 0 || J.threshold == 0) return;
+    const int64_t span = 3 * J.tw + rcap;
+    const uint32_t n = (uint32_t)J.ncorr;
+    for (int64_t k = (int64_t)blockIdx.x * 256 + threadIdx.x; k < span; k += (int64_t)gridDim.x * 256) {
+        const int64_t w = J.word0 + k;
+        const uint32_t low = (uint32_t)((uint64_t)words[w] * (uint64_t)n);
+        if (low < J.threshold) {
+            const int slot = atomicAdd(&nrej[blockIdx.y], 1);
+            if (slot < rcap) rej[(int64_t)blockIdx.y * rcap + slot] = w;
+        }
+    }
+}
+
+constexpr int kTupleChunk = 4096;  // trials per eval workgroup: 4 waves x 16 rounds x 64 lanes
+
+__global__ __launch_bounds__(256) void tuple_eval_kernel(const TupleJob* __restrict__ jobs,
+                                                         const uint32_t* __restrict__ words,
+                                                         const int64_t* __restrict__ keys,
+                                                         const double* __restrict__ A, const double* __restrict__ Bv,
+                                                         double sc, uint64_t* __restrict__ mask,
+                                                         int32_t* __restrict__ chunk_cnt) {
+#pragma clang fp contract(off)
+    const int b = blockIdx.y;
+    const TupleJob& J = jobs[b];
+    const int64_t base = (int64_t)blockIdx.x * kTupleChunk;
+    if (base >= J.tw) return;
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    __shared__ int part[4];
+    int acc_count = 0;
+    for (int it = 0; it < 16; ++it) {
+        const int64_t t0 = base + (int64_t)(wid * 16 + it) * 64;
+        if (t0 >= J.tw) break;  // wave-uniform
+        const int64_t t = t0 + lane;
+        bool acc = false;
+        if (t < J.tw) {
+            int r[3];
+            for (int e = 0; e < 3; ++e) r[e] = tuple_draw(J, words, keys, 3 * t + e);
+            double pi[3][3], pj[3][3];
+            for (int e = 0; e < 3; ++e)
+                for (int a = 0; a < 3; ++a) {
+                    pi[e][a] = A[3 * (J.corr + r[e]) + a];
+                    pj[e][a] = Bv[3 * (J.corr + r[e]) + a];
+                }
+            acc = true;
+            for (int e = 0; e < 3; ++e) {
+                const int f = (e + 1) % 3;
+                const double li = tuple_side(pi[e], pi[f]), lj = tuple_side(pj[e], pj[f]);
+                acc = acc && (li * sc < lj) && (lj < li / sc);
+            }
+        }
+        const uint64_t m = __ballot(acc);
+        if (lane == 0) mask[(int64_t)b * (kTupleWindow / 64) + t0 / 64] = m;
+        acc_count += __popcll(m);
+    }
+    if (lane == 0) part[wid] = acc_count;
+    __syncthreads();
+    if (threadIdx.x == 0)
+        chunk_cnt[(int64_t)b * (kTupleWindow / kTupleChunk) + blockIdx.x] = part[0] + part[1] + part[2] + part[3];
+}
+
+// one workgroup per start; the first wave walks the window's chunks in order,
+// lane k taking the chunk's k-th mask word, and writes each accepted trial's
+// three pairs at its rank among all of the start's tuples
+__global__ __launch_bounds__(64) void tuple_select_kernel(const TupleJob* __restrict__ jobs,
+                                                          const uint32_t* __restrict__ words,
+                                                          const int64_t* __restrict__ keys,
+                                                          const uint64_t* __restrict__ mask,
+                                                          const int32_t* __restrict__ chunk_cnt,
+                                                          const double* __restrict__ A,
+                                                          const double* __restrict__ Bv, int maxc,
+                                                          int32_t* __restrict__ cnt, double* __restrict__ rows) {
+    const int b = blockIdx.x;
+    const TupleJob& J = jobs[b];
+    if (J.tw == 0) return;
+    const int lane = threadIdx.x;
+    int have = cnt[b];
+    const int64_t nch = (J.tw + kTupleChunk - 1) / kTupleChunk;
+    const double* src = J.fi == 0 ? A : Bv;  // source rows: cloud 0
+    const double* tgt = J.fi == 0 ? Bv : A;
+    for (int64_t ch = 0; ch < nch && have < maxc; ++ch) {
+        const int cc = chunk_cnt[(int64_t)b * (kTupleWindow / kTupleChunk) + ch];
+        if (cc == 0) continue;
+        const int64_t t0 = ch * kTupleChunk + (int64_t)lane * 64;
+        uint64_t m = t0 < J.tw ? mask[(int64_t)b * (kTupleWindow / 64) + t0 / 64] : 0ull;
+        // exclusive prefix of the lanes' popcounts
+        const int pc = __popcll(m);
+        int incl = pc;
+        for (int off = 1; off < 64; off <<= 1) {
+            const int v = __shfl_up(incl, off, 64);
+            if (lane >= off) incl += v;
+        }
+        int rank = have + incl - pc;
+        while (m && rank < maxc) {
+            const int bit = __ffsll((unsigned long long)m) - 1;
+            m &= m - 1;
+            const int64_t t = t0 + bit;
+            for (int e = 0; e < 3; ++e) {
+                const int64_t g = J.corr + tuple_draw(J, words, keys, 3 * t + e);
+                const int64_t row = 3 * (int64_t)rank + e;
+                for (int a = 0; a < 3; ++a) {
+                    rows[J.out + 3 * row + a] = src[3 * g + a];
+                    rows[J.out + 3 * J.cap + 3 * row + a] = tgt[3 * g + a];
+                }
+            }
+            ++rank;
+        }
+        have = min(maxc, have + cc);
+    }
+    if (lane == 0) cnt[b] = have;
+}
+
+hipError_t launch_tuple_points(const TupleJob* jobs, int B, int max_ncorr, const int32_t* pairs, double* A,
+                               double* Bv, hipStream_t s) {
+    if (B <= 0 || max_ncorr <= 0) return hipSuccess;
+    tuple_points_kernel<<<dim3((unsigned)((max_ncorr + 255) / 256), (unsigned)B), 256, 0, s>>>(jobs, pairs, A, Bv);
+    return hipGetLastError();
+}
+
+hipError_t launch_tuple_reject(const TupleJob* jobs, int B, int64_t max_span, const uint32_t* words, int64_t* rej,
+                               int32_t* nrej, int64_t rcap, hipStream_t s) {
+    if (B <= 0 || max_span <= 0) return hipSuccess;
+    // 16 words per thread: a window's span (<= 6.3M words) in <= 1536 blocks per start
+    const int64_t blocks = std::min<int64_t>((max_span + 4095) / 4096, 1536);
+    tuple_reject_kernel<<<dim3((unsigned)blocks, (unsigned)B), 256, 0, s>>>(jobs, words, rej, nrej, rcap);
+    return hipGetLastError();
+}
+
+hipError_t launch_tuple_eval(const TupleJob* jobs, int B, int64_t max_tw, const uint32_t* words, const int64_t* keys,
+                             const double* A, const double* Bv, double tuple_scale, uint64_t* mask,
+                             int32_t* chunk_cnt, hipStream_t s) {
+    if (B <= 0 || max_tw <= 0) return hipSuccess;
+    const unsigned nch = (unsigned)((max_tw + kTupleChunk - 1) / kTupleChunk);
+    tuple_eval_kernel<<<dim3(nch, (unsigned)B), 256, 0, s>>>(jobs, words, keys, A, Bv, tuple_scale, mask, chunk_cnt);
+    return hipGetLastError();
+}
+
+hipError_t launch_tuple_select(const TupleJob* jobs, int B, const uint32_t* words, const int64_t* keys,
+                               const uint64_t* mask, const int32_t* chunk_cnt, const double* A, const double* Bv,
+                               int maxc, int32_t* cnt, double* rows, hipStream_t s) {
+    if (B <= 0) return hipSuccess;
+    tuple_select_kernel<<<(unsigned)B, 64, 0, s>>>(jobs, words, keys, mask, chunk_cnt, A, Bv, maxc, cnt, rows);
+    return hipGetLastError();
+}
+
 
 hipError_t launch_fgr_irls(const double* p, double* q, int K, double par0, int iters, double division_factor,
                            double max_corr, int decrease_mu, double* T_out, hipStream_t s) {

@@ -653,6 +653,7 @@ struct SchedX {                          // query transform side (pass p + 1)
     int cap, NG, have_cost, S0;          // S0: the host's uniform split (no cost known)
     float inv_want;                      // 1 / sched_items
     float max_target;                    // cap on a split's planned cost (10 ns ticks; 0: none), opt.sched_cap_us
+    float inv_max_items;                 // 1 / the item budget sched_capacity holds room for
 };
 struct SchedS {                          // search side (pass p)
     const unsigned* cnt;                 // this pass's items per class
@@ -689,7 +690,8 @@ __device__ __forceinline__ void plan_start_items(const SchedX& sx, int slot, int
         // pass 5) and a group's cost can double from one pass to the next, so
         // an unsplit group became the launch's critical wave (r05 wave dumps);
         // the cap splits heavy groups further there
-        if (sx.max_target > 0.0f) tg = fminf(tg, sx.max_target);
+        // the cap, within the list's room: at most ~1 / inv_max_items items
+        if (sx.max_target > 0.0f) tg = fmaxf(fminf(tg, sx.max_target), fmaxf(t * sx.inv_max_items, 1.0f));
         if (lane == 0) s_target = tg;
     }
     __syncthreads();
@@ -2044,11 +2046,15 @@ bool sched_wanted(const orpcd_ctx* c, int B) { return c->opt.sched && B >= c->op
 
 // items per class: every item of a pass may fall in one class.  Pass 0:
 // S0 * groups <= search_waves + groups (search_splits rounds up); later
-// passes: sum ceil(cost / (total / sched_items)) <= sched_items + groups,
+// passes: sum ceil(cost / target) <= total / target + groups with target >=
+// total / sched_items, or >= total / sched_item_budget under sched_cap_us,
 // doubled against float rounding of the per-group quotients.
+static int64_t sched_item_budget(const orpcd_ctx* c) {
+    return c->opt.sched_cap_us > 0 ? (int64_t)c->opt.sched_items * c->opt.sched_cap_mult : c->opt.sched_items;
+}
 int sched_capacity(const orpcd_ctx* c, int B) {
     const int64_t NG = (c->src.n + 127) / 128;
-    return (int)(std::max<int64_t>(c->opt.sched_items, c->opt.search_waves) + 2 * (int64_t)B * NG + 64);
+    return (int)(std::max<int64_t>(sched_item_budget(c), c->opt.search_waves) + 2 * (int64_t)B * NG + 64);
 }
 
 // the ordered dispatch's planner arguments for the queries of `pass` (none
@@ -2070,6 +2076,7 @@ static SchedX sched_x(const orpcd_ctx* c, int nact, int pass) {
     sx.S0 = uniform_splits(c, nact);
     sx.inv_want = 1.0f / (float)c->opt.sched_items;
     sx.max_target = (float)c->opt.sched_cap_us * 100.0f;  // us -> s_memrealtime ticks (10 ns)
+    sx.inv_max_items = 1.0f / (float)sched_item_budget(c);
     return sx;
 }
 
@@ -2176,7 +2183,7 @@ hipError_t launch_gicp_pass(const orpcd_ctx* c, int nact, int pass, double r2, h
         // the grid covers their upper bound (surplus waves exit at once)
         const int64_t NG = (N + 127) / 128;
         const int64_t items = pass == 0 ? (int64_t)uniform_splits(c, nact) * nact * NG
-                                        : (int64_t)c->opt.sched_items + 2 * (int64_t)nact * NG + 64;
+                                        : sched_item_budget(c) + 2 * (int64_t)nact * NG + 64;
         const int64_t B = c->sched_B;
         const int par = pass & 1;
         SchedS sa{};

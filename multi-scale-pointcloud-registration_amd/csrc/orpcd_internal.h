@@ -7,6 +7,7 @@
 #include <cstring>
 #include <string>
 #include <thread>
+#include <random>
 #include <vector>
 
 #include "../../include/orpcd.h"
@@ -283,6 +284,26 @@ struct CloudLayout {
         ids.release();
         sort_tmp.release();
     }
+};
+
+// AdvancedMatching's tuple test on the device (fgr_kernels.hip, "tuple
+// test"): one job per start, trials processed in windows of kTupleWindow.
+constexpr int64_t kTupleWindow = (int64_t)1 << 21;  // trials per start and window
+struct TupleJob {
+    const double* xi = nullptr;  // cloud fi (the one with more points; the source on a tie), device, input order
+    const double* xj = nullptr;  // cloud fj
+    double mi[3] = {0, 0, 0}, mj[3] = {0, 0, 0};  // their means (NormalizePointCloud)
+    double scale = 1.0;          // the common radius
+    int64_t corr = 0;            // offset of the start's (i, j) pairs in the pair and point arrays
+    int64_t rej = 0;             // offset of its rejection keys (window-relative, sorted)
+    int64_t out = 0;             // offset of its tuple rows: cap source rows (x3), then cap target rows
+    int64_t cap = 0;             // tuple rows reserved: 3 * min(maximum_tuple_count, trials)
+    int64_t trials = 0;          // 100 * ncorr
+    int64_t tw = 0;              // trials in this window (0: the start has finished)
+    int64_t word0 = 0;           // stream index of the window's first draw
+    int32_t ncorr = 0, fi = 0;
+    uint32_t threshold = 0;      // (2^32 - ncorr) mod ncorr: the Lemire rejection bound of uniform_int_distribution
+    int32_t nrej = 0;            // rejection keys of this window
 };
 
 // B rigid copies of one cloud in its Morton order (build_batch_layout): the
@@ -601,8 +622,34 @@ struct orpcd_ctx {
                 uflag.release();
             }
         } bt;
+        // the device tuple test (fgr_tuples_device): the seed's mt19937 word
+        // stream (host copy extended on demand, mirrored on the device), jobs,
+        // pairs, normalised pair points, rejection keys, accept bits, tuple rows
+        struct Tuples {
+            bool valid = false;
+            uint32_t seed = 0;
+            std::mt19937 gen;
+            std::vector<uint32_t> host;
+            size_t on_dev = 0;
+            orpcd::DevBuf<uint32_t> words;
+            orpcd::DevBuf<orpcd::TupleJob> jobs;
+            orpcd::DevBuf<int32_t> pairs, nrej, chunk, cnt;
+            orpcd::DevBuf<double> A, Bv, rows;
+            orpcd::DevBuf<int64_t> rej;
+            orpcd::DevBuf<uint64_t> mask;
+            void release() {
+                words.release();
+                on_dev = 0;
+                jobs.release();
+                for (auto* b : {&pairs, &nrej, &chunk, &cnt}) b->release();
+                for (auto* b : {&A, &Bv, &rows}) b->release();
+                rej.release();
+                mask.release();
+            }
+        } tup;
         void release() {
             bt.release();
+            tup.release();
             for (int k = 0; k < 2; ++k) {
                 xyz[k].release();
                 feat[k].release();
@@ -640,6 +687,7 @@ struct orpcd_ctx {
                                   // (C2 sweep 5120 / 10240 / 20480: 15.4 / 15.0 / 16.6 ms at 30 starts)
         int sched_min_starts = 16;  // ordered dispatch only for batches of at least this many starts
         int sched_cap_us = 0;     // ordered dispatch: a split's planned cost at most this many us (0: no cap)
+        int sched_cap_mult = 4;   // ... within an item budget of this many times sched_items
         int exact_nn = 1;         // 1 (default): every correspondence is the fp64 nearest target (the
                                   // oracle's lexicographic (d^2, input index) minimum): fp32 search +
                                   // runner-up band test + fp64 re-search of the uncertified queries;
@@ -766,10 +814,28 @@ hipError_t expand_dup_answers(const DedupBufs& b, int64_t n, int64_t nu, const i
 hipError_t launch_fgr_irls(const double* p, double* q, int K, double par0, int iters, double division_factor,
                            double max_corr, int decrease_mu, double* T_out, hipStream_t s);
 // several IRLS problems in one launch each for the register- and the
-// memory-resident form: meta = {offset of p in pq (doubles), K, output slot} per problem
+// memory-resident form: meta = {offset of p in pq (doubles), K, output slot,
+// offset of q in pq} per problem
 hipError_t launch_fgr_irls_batch(const double* pq, const int64_t* meta_reg, int nreg, const int64_t* meta_mem,
                                  int nmem, double par0, int iters, double division_factor, double max_corr,
                                  int decrease_mu, double* T_out, hipStream_t s);
+// the device tuple test (TupleJob)
+// normalised points of every pair: A[k] = (xi[pair.x] - mi) / scale, Bv[k] likewise on cloud fj
+hipError_t launch_tuple_points(const TupleJob* jobs, int B, int max_ncorr, const int32_t* pairs, double* A,
+                               double* Bv, hipStream_t s);
+// stream positions in [word0, word0 + 3 tw + rcap) whose draw uniform_int_distribution rejects (unordered)
+hipError_t launch_tuple_reject(const TupleJob* jobs, int B, int64_t max_span, const uint32_t* words, int64_t* rej,
+                               int32_t* nrej, int64_t rcap, hipStream_t s);
+// every trial of the window: accept bits (mask, kTupleWindow / 64 words per
+// start) and accepted trials per 4096 (chunk_cnt, kTupleWindow / 4096 per start)
+hipError_t launch_tuple_eval(const TupleJob* jobs, int B, int64_t max_tw, const uint32_t* words, const int64_t* keys,
+                             const double* A, const double* Bv, double tuple_scale, uint64_t* mask,
+                             int32_t* chunk_cnt, hipStream_t s);
+// the window's first accepted trials in order, up to maximum_tuple_count in
+// all, as (source, target) rows; cnt[b] = tuples so far
+hipError_t launch_tuple_select(const TupleJob* jobs, int B, const uint32_t* words, const int64_t* keys,
+                               const uint64_t* mask, const int32_t* chunk_cnt, const double* A, const double* Bv,
+                               int maxc, int32_t* cnt, double* rows, hipStream_t s);
 // representative flags of dedup_rows (uflag_out[i] = row i is the lowest index of its equal rows)
 hipError_t dedup_flags(const double* F, int64_t n, DedupBufs& b, unsigned char* uflag_out, hipStream_t s,
                        int clouds = 1);

@@ -356,6 +356,209 @@ int fgr_tuples(const std::vector<std::pair<int, int>>& corres, const orpcd_fgr_p
     return K;
 }
 
+// One start of the device tuple test: its cross-checked pairs (i in cloud
+// fi, j in cloud fj), the device points of both clouds in input order and the
+// normalisation (means, common scale).
+struct TupleStart {
+    const std::vector<std::pair<int, int>>* corres = nullptr;
+    const double* xi = nullptr;   // device
+    const double* xj = nullptr;
+    const double* hxi = nullptr;  // the same points on the host (ORPCD_FGR_HOST_TUPLES)
+    const double* hxj = nullptr;
+    double mi[3] = {0, 0, 0}, mj[3] = {0, 0, 0};
+    double scale = 1.0;
+    int fi = 0;
+};
+
+// the seed's mt19937 words [0, need) on the device (host copy extended on demand)
+int tuple_stream(orpcd_ctx* c, uint32_t seed, size_t need) {
+    auto& T = c->fgr.tup;
+    if (!T.valid || T.seed != seed) {
+        T.gen.seed(seed);
+        T.host.clear();
+        T.on_dev = 0;
+        T.seed = seed;
+        T.valid = true;
+    }
+    if (T.host.size() < need) {
+        const size_t want = std::max(need, T.host.size() * 2);
+        T.host.reserve(want);
+        while (T.host.size() < want) T.host.push_back((uint32_t)T.gen());
+    }
+    if (T.on_dev < need) {
+        if (T.words.n < T.host.size()) {
+            CTX_CHECK(c, T.words.ensure(T.host.size()));
+            T.on_dev = 0;
+        }
+        CTX_CHECK(c, h2d(T.words.p + T.on_dev, T.host.data() + T.on_dev, (T.host.size() - T.on_dev) * 4, c->stream));
+        T.on_dev = T.host.size();
+    }
+    return ORPCD_OK;
+}
+
+// fgr_tuples for every start at once on the device (fgr_kernels.hip, "tuple
+// test"); the same tuples, bit for bit.  Start b's K[b] rows are at
+// c->fgr.tup.rows + out[b]: cap[b] source rows (x, y, z), then cap[b] target
+// rows.  ORPCD_FGR_HOST_TUPLES=1 runs fgr_tuples on host threads instead and
+// lays its rows out the same way (A/B and the parity test of this path).
+int fgr_tuples_device(orpcd_ctx* c, const std::vector<TupleStart>& st, const orpcd_fgr_params& p,
+                      std::vector<int>& K, std::vector<int64_t>& out, std::vector<int64_t>& cap) {
+    auto& T = c->fgr.tup;
+    hipStream_t s = c->stream;
+    const int B = (int)st.size();
+    const int maxc = p.maximum_tuple_count;
+    K.assign((size_t)B, 0);
+    out.assign((size_t)B, 0);
+    cap.assign((size_t)B, 0);
+    std::vector<TupleJob> jobs((size_t)B);
+    int64_t npairs = 0, nrows = 0;
+    int max_ncorr = 0;
+    for (int b = 0; b < B; ++b) {
+        TupleJob& J = jobs[b];
+        J.ncorr = (int)st[b].corres->size();
+        J.trials = (int64_t)J.ncorr * 100;
+        J.cap = 3 * std::min<int64_t>(maxc, J.trials);
+        J.corr = npairs;
+        J.out = nrows;
+        J.xi = st[b].xi;
+        J.xj = st[b].xj;
+        for (int a = 0; a < 3; ++a) {
+            J.mi[a] = st[b].mi[a];
+            J.mj[a] = st[b].mj[a];
+        }
+        J.scale = st[b].scale;
+        J.fi = st[b].fi;
+        J.threshold = J.ncorr > 0 ? (0u - (uint32_t)J.ncorr) % (uint32_t)J.ncorr : 0u;
+        out[b] = nrows;
+        cap[b] = J.cap;
+        npairs += J.ncorr;
+        nrows += 6 * std::max<int64_t>(J.cap, 1);
+        max_ncorr = std::max(max_ncorr, J.ncorr);
+    }
+    CTX_CHECK(c, T.rows.ensure((size_t)std::max<int64_t>(nrows, 6)));
+    if (getenv("ORPCD_FGR_HOST_TUPLES")) {
+        std::vector<double> rows((size_t)nrows, 0.0);
+        host_parallel(B, [&](int b) {
+            const TupleStart& S = st[b];
+            FgrCloud cl[2];
+            cl[S.fi].xyz = S.hxi;
+            cl[1 - S.fi].xyz = S.hxj;
+            for (int a = 0; a < 3; ++a) {
+                cl[S.fi].mean[a] = S.mi[a];
+                cl[1 - S.fi].mean[a] = S.mj[a];
+            }
+            std::vector<double> pq;
+            K[b] = fgr_tuples(*S.corres, p, cl, S.scale, S.fi, 1 - S.fi, pq);
+            for (int64_t r = 0; r < K[b]; ++r)
+                for (int a = 0; a < 3; ++a) {
+                    rows[(size_t)(out[b] + 3 * r + a)] = pq[(size_t)(3 * r + a)];
+                    rows[(size_t)(out[b] + 3 * cap[b] + 3 * r + a)] = pq[(size_t)(3 * K[b] + 3 * r + a)];
+                }
+        });
+        CTX_CHECK(c, h2d(T.rows.p, rows.data(), rows.size() * 8, s));
+        return ORPCD_OK;
+    }
+    if (npairs == 0) return ORPCD_OK;
+    // pairs and their normalised points
+    std::vector<int32_t> pairs((size_t)npairs * 2);
+    for (int b = 0; b < B; ++b) {
+        int64_t o = jobs[b].corr;
+        for (const auto& pr : *st[b].corres) {
+            pairs[(size_t)(2 * o)] = pr.first;
+            pairs[(size_t)(2 * o + 1)] = pr.second;
+            ++o;
+        }
+    }
+    CTX_CHECK(c, T.pairs.ensure(pairs.size()));
+    CTX_CHECK(c, T.A.ensure((size_t)npairs * 3));
+    CTX_CHECK(c, T.Bv.ensure((size_t)npairs * 3));
+    CTX_CHECK(c, T.jobs.ensure((size_t)B));
+    CTX_CHECK(c, T.nrej.ensure((size_t)B));
+    CTX_CHECK(c, T.cnt.ensure((size_t)B));
+    CTX_CHECK(c, h2d(T.pairs.p, pairs.data(), pairs.size() * 4, s));
+    CTX_CHECK(c, h2d(T.jobs.p, jobs.data(), jobs.size() * sizeof(TupleJob), s));
+    CTX_CHECK(c, launch_tuple_points(T.jobs.p, B, max_ncorr, T.pairs.p, T.A.p, T.Bv.p, s));
+    CTX_CHECK(c, hipMemsetAsync(T.cnt.p, 0, (size_t)B * 4, s));
+    std::vector<int64_t> t0((size_t)B, 0);
+    std::vector<int32_t> cnt((size_t)B, 0), nrej((size_t)B);
+    std::vector<int64_t> lists;
+    for (;;) {
+        // --- this window's trials per start
+        int64_t max_tw = 0, max_span = 0;
+        double expect = 0.0;
+        for (int b = 0; b < B; ++b) {
+            TupleJob& J = jobs[b];
+            J.tw = (cnt[b] >= maxc || t0[b] >= J.trials) ? 0 : std::min(kTupleWindow, J.trials - t0[b]);
+            J.nrej = 0;
+            max_tw = std::max(max_tw, J.tw);
+            expect = std::max(expect, 3.0 * (double)J.tw * (double)J.threshold / 4294967296.0);
+        }
+        if (max_tw == 0) break;
+        // --- the words uniform_int_distribution rejects (rcap per start;
+        // a window with more is scanned again with room for all of them)
+        int64_t rcap = (int64_t)(2.0 * expect) + 64;
+        for (;;) {
+            size_t need = 0;
+            for (int b = 0; b < B; ++b)
+                if (jobs[b].tw > 0) {
+                    max_span = std::max(max_span, 3 * jobs[b].tw + rcap);
+                    need = std::max(need, (size_t)(jobs[b].word0 + 3 * jobs[b].tw + rcap));
+                }
+            int rc = tuple_stream(c, (uint32_t)p.seed, need);
+            if (rc) return rc;
+            CTX_CHECK(c, T.rej.ensure((size_t)B * rcap));
+            CTX_CHECK(c, h2d(T.jobs.p, jobs.data(), jobs.size() * sizeof(TupleJob), s));
+            CTX_CHECK(c, hipMemsetAsync(T.nrej.p, 0, (size_t)B * 4, s));
+            CTX_CHECK(c, launch_tuple_reject(T.jobs.p, B, max_span, T.words.p, T.rej.p, T.nrej.p, rcap, s));
+            CTX_CHECK(c, d2h(nrej.data(), T.nrej.p, (size_t)B * 4, s));
+            CTX_CHECK(c, hipStreamSynchronize(s));
+            int32_t most = 0;
+            for (int b = 0; b < B; ++b) most = std::max(most, nrej[b]);
+            if (most <= rcap) break;
+            rcap = (int64_t)most + 64;
+        }
+        // --- sorted rejection keys, window-relative: key_j = r_j - word0 - j
+        bool any = false;
+        for (int b = 0; b < B; ++b) any = any || nrej[b] > 0;
+        if (any) {
+            lists.resize((size_t)B * rcap);
+            CTX_CHECK(c, d2h(lists.data(), T.rej.p, lists.size() * 8, s));
+            CTX_CHECK(c, hipStreamSynchronize(s));
+            for (int b = 0; b < B; ++b) {
+                int64_t* L = &lists[(size_t)b * rcap];
+                std::sort(L, L + nrej[b]);
+                for (int j = 0; j < nrej[b]; ++j) L[j] = L[j] - jobs[b].word0 - j;
+                jobs[b].nrej = nrej[b];
+                jobs[b].rej = (int64_t)b * rcap;
+            }
+            CTX_CHECK(c, h2d(T.rej.p, lists.data(), lists.size() * 8, s));
+            CTX_CHECK(c, h2d(T.jobs.p, jobs.data(), jobs.size() * sizeof(TupleJob), s));
+        }
+        // --- every trial of the window, then the accepted ones in order
+        CTX_CHECK(c, T.mask.ensure((size_t)B * (kTupleWindow / 64)));
+        CTX_CHECK(c, T.chunk.ensure((size_t)B * (kTupleWindow / 4096)));
+        CTX_CHECK(c, launch_tuple_eval(T.jobs.p, B, max_tw, T.words.p, T.rej.p, T.A.p, T.Bv.p, p.tuple_scale,
+                                       T.mask.p, T.chunk.p, s));
+        CTX_CHECK(c, launch_tuple_select(T.jobs.p, B, T.words.p, T.rej.p, T.mask.p, T.chunk.p, T.A.p, T.Bv.p, maxc,
+                                         T.cnt.p, T.rows.p, s));
+        CTX_CHECK(c, d2h(cnt.data(), T.cnt.p, (size_t)B * 4, s));
+        CTX_CHECK(c, hipStreamSynchronize(s));
+        // --- the next window starts at the word after the last one read
+        for (int b = 0; b < B; ++b) {
+            TupleJob& J = jobs[b];
+            if (J.tw == 0) continue;
+            const int64_t* L = any ? &lists[(size_t)b * rcap] : nullptr;
+            int64_t used = 0;
+            for (int j = 0; j < J.nrej; ++j)
+                if (L[j] <= 3 * J.tw - 1) ++used;
+            J.word0 += 3 * J.tw + used;
+            t0[b] += J.tw;
+        }
+    }
+    for (int b = 0; b < B; ++b) K[b] = 3 * cnt[b];
+    return ORPCD_OK;
+}
+
 // GetInvTransformationOriginalScale: the normalised-frame Tn back to the
 // clouds' own frames (Open3D's column convention).
 void fgr_original_scale(const double Tn[16], const double mean_src[3], const double mean_tgt[3], double scale,
@@ -481,11 +684,6 @@ int fgr_device(orpcd_ctx* c, const double* src, int64_t n, const double* tgt, in
         scale = std::max(scale, mx);
     }
     CTX_REQUIRE(c, scale > 0.0, "fgr: degenerate clouds (all points at their mean)");
-    FgrCloud cl[2];
-    for (int k = 0; k < 2; ++k) {
-        cl[k].xyz = host[k];
-        for (int a = 0; a < 3; ++a) cl[k].mean[a] = mean[k][a];
-    }
     fgr_mark(s, "normalisation");
     // --- initial matching on the matrix cores, both directions
     int fi = 0, fj = 1;
@@ -493,16 +691,30 @@ int fgr_device(orpcd_ctx* c, const double* src, int64_t n, const double* tgt, in
     std::vector<std::pair<int, int>> corres;
     int rc = fgr_match(c, F.feat[0].p, n, F.feat[1].p, m, same_features, corres);
     if (rc) return rc;
-    // --- tuple test: Open3D's sequential mt19937 draws (RNG-bound, host)
+    // --- tuple test: Open3D's mt19937 draws, every trial at once (fgr_tuples_device)
     const int ncorr = (int)corres.size();
-    std::vector<double> pq;
-    const int K = fgr_tuples(corres, p, cl, scale, fi, fj, pq);
+    std::vector<TupleStart> ts(1);
+    ts[0].corres = &corres;
+    ts[0].xi = F.xyz[fi].p;
+    ts[0].xj = F.xyz[fj].p;
+    ts[0].hxi = host[fi];
+    ts[0].hxj = host[fj];
+    for (int a = 0; a < 3; ++a) {
+        ts[0].mi[a] = mean[fi][a];
+        ts[0].mj[a] = mean[fj][a];
+    }
+    ts[0].scale = scale;
+    ts[0].fi = fi;
+    std::vector<int> Ks;
+    std::vector<int64_t> outs, caps;
+    rc = fgr_tuples_device(c, ts, p, Ks, outs, caps);
+    if (rc) return rc;
+    const int K = Ks[0];
     fgr_mark(s, "cross check + tuple test");
     // --- GNC / Geman-McClure IRLS in one workgroup (fp64)
-    CTX_CHECK(c, F.pq.ensure(pq.size()));
     CTX_CHECK(c, F.Tn.ensure(16));
-    if (K > 0) CTX_CHECK(c, h2d(F.pq.p, pq.data(), (size_t)K * 48, s));
-    CTX_CHECK(c, launch_fgr_irls(F.pq.p, F.pq.p + (size_t)3 * K, K, 1.0, p.iteration_number, p.division_factor,
+    double* rows = c->fgr.tup.rows.p + outs[0];
+    CTX_CHECK(c, launch_fgr_irls(rows, rows + 3 * caps[0], K, 1.0, p.iteration_number, p.division_factor,
                                  p.maximum_correspondence_distance, p.decrease_mu ? 1 : 0, F.Tn.p, s));
     double Tn[16];
     CTX_CHECK(c, d2h(Tn, F.Tn.p, sizeof(Tn), s));
@@ -2186,41 +2398,44 @@ int orpcd_fgr_optimize_batch(orpcd_ctx* c, const double* src, int64_t n, const d
         }
     }
     fgr_mark(s, "batch: matching");
-    // --- tuple tests (host, one mt19937 per start, in parallel)
-    std::vector<std::vector<double>> pqs((size_t)B);
-    std::vector<int> K((size_t)B);
-    host_parallel(B, [&](int b) {
-        FgrCloud cl[2];
-        cl[0].xyz = &P[(size_t)b * n * 3];
-        cl[1].xyz = tgts + 3 * toff[tk[b]];
-        for (int a = 0; a < 3; ++a) {
-            cl[0].mean[a] = smean[3 * b + a];
-            cl[1].mean[a] = tmean[3 * tk[b] + a];
-        }
+    // --- tuple tests: every trial of every start at once (fgr_tuples_device)
+    std::vector<TupleStart> ts((size_t)B);
+    for (int b = 0; b < B; ++b) {
         const int fi = m[tk[b]] > n ? 1 : 0;
-        K[b] = fgr_tuples(corres[b], *p, cl, scale[b], fi, 1 - fi, pqs[b]);
-    });
+        const double* dev[2] = {bt.X.p + (size_t)b * n * 3, bt.txyz[tk[b]].p};
+        const double* hst[2] = {&P[(size_t)b * n * 3], tgts + 3 * toff[tk[b]]};
+        const double* mn[2] = {&smean[3 * b], &tmean[3 * tk[b]]};
+        TupleStart& S = ts[b];
+        S.corres = &corres[b];
+        S.xi = dev[fi];
+        S.xj = dev[1 - fi];
+        S.hxi = hst[fi];
+        S.hxj = hst[1 - fi];
+        for (int a = 0; a < 3; ++a) {
+            S.mi[a] = mn[fi][a];
+            S.mj[a] = mn[1 - fi][a];
+        }
+        S.scale = scale[b];
+        S.fi = fi;
+    }
+    std::vector<int> K;
+    std::vector<int64_t> outs, caps;
+    rc = fgr_tuples_device(c, ts, *p, K, outs, caps);
+    if (rc) return rc;
     fgr_mark(s, "batch: tuple tests");
     // --- IRLS: every start's problem in one launch (one workgroup each)
     std::vector<int64_t> meta_reg, meta_mem;
-    int64_t off = 0;
     for (int b = 0; b < B; ++b) {
         auto& mt = K[b] <= 512 * 6 ? meta_reg : meta_mem;  // kIrlsThreads x kIrlsPer: launch_fgr_irls's split
-        mt.insert(mt.end(), {off, (int64_t)K[b], (int64_t)b});
-        off += 6 * (int64_t)std::max(K[b], 1);
+        mt.insert(mt.end(), {outs[b], (int64_t)K[b], (int64_t)b, outs[b] + 3 * caps[b]});
     }
-    std::vector<double> pq((size_t)off);
-    for (int b = 0, o = 0; b < B; o += 6 * std::max(K[b], 1), ++b)
-        std::memcpy(&pq[(size_t)o], pqs[b].data(), (size_t)6 * std::max(K[b], 1) * 8);
     std::vector<int64_t> meta(meta_reg);
     meta.insert(meta.end(), meta_mem.begin(), meta_mem.end());
-    CTX_CHECK(c, bt.pq.ensure(pq.size()));
     CTX_CHECK(c, bt.meta.ensure(meta.size()));
     CTX_CHECK(c, bt.Tn.ensure((size_t)B * 16));
-    CTX_CHECK(c, h2d(bt.pq.p, pq.data(), pq.size() * 8, s));
     CTX_CHECK(c, h2d(bt.meta.p, meta.data(), meta.size() * 8, s));
-    const int nreg = (int)meta_reg.size() / 3, nmem = (int)meta_mem.size() / 3;
-    CTX_CHECK(c, launch_fgr_irls_batch(bt.pq.p, bt.meta.p, nreg, bt.meta.p + 3 * (size_t)nreg, nmem, 1.0,
+    const int nreg = (int)meta_reg.size() / 4, nmem = (int)meta_mem.size() / 4;
+    CTX_CHECK(c, launch_fgr_irls_batch(c->fgr.tup.rows.p, bt.meta.p, nreg, bt.meta.p + 4 * (size_t)nreg, nmem, 1.0,
                                        p->iteration_number, p->division_factor, p->maximum_correspondence_distance,
                                        p->decrease_mu ? 1 : 0, bt.Tn.p, s));
     std::vector<double> Tn((size_t)B * 16), T((size_t)B * 16);
@@ -2295,6 +2510,7 @@ int orpcd_set_option(orpcd_ctx* c, const char* key, double value) {
     else if (k == "sched_items" && v >= 64 && v <= (1 << 22)) c->opt.sched_items = v;
     else if (k == "sched_min_starts" && v >= 1) c->opt.sched_min_starts = v;
     else if (k == "sched_cap_us" && v >= 0 && v <= 100000) c->opt.sched_cap_us = v;
+    else if (k == "sched_cap_mult" && v >= 1 && v <= 16) c->opt.sched_cap_mult = v;
     else if (k == "exact_nn" && (v == 0 || v == 1)) c->opt.exact_nn = v;
     else if (k == "exact_blocks" && v >= 1 && v <= 65536) c->opt.exact_blocks = v;
     else if (k == "exact_fused" && v >= 0 && v <= 4096) c->opt.exact_fused = v;

@@ -12,6 +12,8 @@ Tolerances:
     counts (so the same tuples), T elementwise <= 1e-9, fitness identical,
     RMSE <= 1e-9 relative.
 """
+import os
+
 import numpy as np
 import pytest
 
@@ -314,3 +316,43 @@ def test_aligner_with_fgr_batched_equals_sequential_aligner(ctx):
     (T1, m1, s1, e1, r1), (T2, m2, s2, e2, r2) = out
     assert np.array_equal(s1, s2) and np.array_equal(e1, e2) and m1 == m2
     assert np.array_equal(T1, T2) and np.array_equal(r1, r2)
+
+
+def _host_and_device_tuples(fn):
+    """fn() with the tuple test on host threads (fgr_tuples, Open3D's loop as
+    written) and on the device (every trial at once), in that order."""
+    os.environ["ORPCD_FGR_HOST_TUPLES"] = "1"
+    try:
+        host = fn()
+    finally:
+        del os.environ["ORPCD_FGR_HOST_TUPLES"]
+    return host, fn()
+
+
+@pytest.mark.parametrize("case", ["batch_two_targets", "batch_stop_early", "two_windows_rejections"])
+def test_device_tuple_test_is_the_sequential_loop_bit_for_bit(ctx, case):
+    """The device tuple test (fgr_kernels.hip "tuple test") against the host
+    loop of the same draws: every result bit for bit.  two_windows_rejections:
+    ~25k mutual pairs, so ~2.5M trials run in two windows (2^21 trials each)
+    and uniform_int_distribution rejects dozens of the ~7.5M words (for
+    ncorr = n, 2^32 mod n of every 2^32 word values); the tight tuple scale
+    keeps the acceptances (~3%) below the tuple limit, so every trial runs."""
+    kw = dict(maximum_correspondence_distance=0.05, fpfh_radius=0.25, fpfh_knn=40, seed=4)
+    if case == "two_windows_rejections":
+        src, tgt = _pair(30000, noise=1e-3)
+        kw.update(maximum_tuple_count=10 ** 6, tuple_scale=0.9995)
+        h, d = _host_and_device_tuples(lambda: ctx.fgr_optimize(src, tgt, **kw))
+        assert _same(h, d) and d["n_mutual"] > 2 ** 21 // 100
+        assert 10 <= d["n_tuple_corr"] < 3 * 10 ** 6      # no early stop: every trial was drawn
+        return
+    src, tgt = _pair(2500, noise=1e-3)
+    if case == "batch_stop_early":
+        kw["maximum_tuple_count"] = 7
+    targets = [tgt, tgt[:2100] * np.array([1.1, 1.0, 0.9])]
+    R0, t0 = _starts(6, 5)
+    tos = np.array([1, 0, 1, 1, 0, 0], np.int32)
+    h, d = _host_and_device_tuples(lambda: ctx.fgr_optimize_batch(src, targets, R0, t0, target_of_start=tos, **kw))
+    for b in range(6):
+        assert _same({k: h[k][b] for k in h}, {k: d[k][b] for k in d}), f"start {b}"
+    if case == "batch_stop_early":
+        assert (d["n_tuple_corr"] == 21).all()
