@@ -789,7 +789,13 @@ __global__ __launch_bounds__(256) void xform_queries_kernel(const double* __rest
         xform(Q, p, q);
         x = (float)(q[0] - tg.ox), y = (float)(q[1] - tg.oy), z = (float)(q[2] - tg.oz);
         bound = r2s;
-        const int jp = prevnn[(size_t)slot * N + i];
+        int jp = prevnn[(size_t)slot * N + i];
+#ifdef ORPCD_BOUNDS_CHECK
+        if (jp >= tg.npts) {
+            printf("[chk] xform slot %d i %d prevnn %d npts %d\n", slot, i, jp, tg.npts);
+            jp = kNoSeed;
+        }
+#endif
         if (jp >= 0) bound = fminf(bound, seed_bound(d2f(x, y, z, p4[jp])));
         if (tg.sgrid && tg.sg_on) {
             // the target nearest to the centre of the query's seed-grid cell
@@ -800,7 +806,13 @@ __global__ __launch_bounds__(256) void xform_queries_kernel(const double* __rest
             const int cx = min(kSeedGrid - 1, max(0, (int)((x - tg.sg_lo[0]) * tg.sg_inv[0])));
             const int cy = min(kSeedGrid - 1, max(0, (int)((y - tg.sg_lo[1]) * tg.sg_inv[1])));
             const int cz = min(kSeedGrid - 1, max(0, (int)((z - tg.sg_lo[2]) * tg.sg_inv[2])));
-            const int g = tg.sgrid[(cx * kSeedGrid + cy) * kSeedGrid + cz];
+            int g = tg.sgrid[(cx * kSeedGrid + cy) * kSeedGrid + cz];
+#ifdef ORPCD_BOUNDS_CHECK
+            if (g < 0 || g >= tg.npts) {
+                printf("[chk] xform slot %d i %d seed cell %d,%d,%d -> %d npts %d\n", slot, i, cx, cy, cz, g, tg.npts);
+                g = 0;
+            }
+#endif
             bound = fminf(bound, seed_bound(d2f(x, y, z, p4[g])));
         } else if (jp < 0 && (jp == kNoSeed || reseed)) {
             for (int t = 0; t < tg.ntiles; t += tg.seed_stride)
@@ -1154,6 +1166,13 @@ __device__ __forceinline__ int exact_entry(unsigned long long ent, const double*
 #pragma clang fp contract(off)
     const int lane = threadIdx.x & 63;
     const int slot = (int)(ent >> 40), tk = (int)((ent >> 32) & 0xFFu), i = (int)(unsigned)ent;
+#ifdef ORPCD_BOUNDS_CHECK
+    if (slot >= 4096 || tk >= kMaxTargets || i >= N || i < 0) {
+        if (lane == 0) printf("[chk] exact entry %llx: slot %d tk %d i %d N %d\n", ent, slot, tk, i, N);
+        bv = kNone;
+        return -1;
+    }
+#endif
     const size_t qi = (size_t)slot * N + i;
     const TargetDesc& tg = tdesc[tk];
     // the entry's independent loads, one round
@@ -1192,10 +1211,14 @@ __device__ __forceinline__ int exact_entry(unsigned long long ent, const double*
             for (int u4 = 0; u4 < 4; ++u4) {
                 kk[u4] = c + u4 < nt ? tl[c + u4] * kTile + lane : -1;
                 const int k = kk[u4] >= 0 ? kk[u4] : 0;
-                in[u4] = __float_as_int(ldg_f32(&tg.p4[k].w));
-                tx[u4] = ldg_f64(t64 + 3 * (size_t)k);
-                ty[u4] = ldg_f64(t64 + 3 * (size_t)k + 1);
-                tz[u4] = ldg_f64(t64 + 3 * (size_t)k + 2);
+                in[u4] = __float_as_int(ldg_f32(&tg.p4[k].w));  // p4 holds the padded tiles: -1 past the points
+                // the fp64 points stop at npts: a padding lane reads point 0
+                // (and is skipped below).  Reading past them faulted whenever
+                // the buffer's end met an unmapped page (round 5).
+                const size_t kx = k < tg.npts ? (size_t)k : 0;
+                tx[u4] = ldg_f64(t64 + 3 * kx);
+                ty[u4] = ldg_f64(t64 + 3 * kx + 1);
+                tz[u4] = ldg_f64(t64 + 3 * kx + 2);
             }
 #pragma unroll
             for (int u4 = 0; u4 < 4; ++u4) {
@@ -1620,7 +1643,14 @@ __device__ __forceinline__ void gicp_block_terms(int slot, int ablk, const doubl
 #pragma unroll
     for (int k = 0; k < kQ; ++k) {
         const int i = (ablk * kQ + k) * 256 + threadIdx.x;
-        const int j = bv[k] == kNone ? -1 : (int)(unsigned)(bv[k] & 0xffffffffu);
+        int j = bv[k] == kNone ? -1 : (int)(unsigned)(bv[k] & 0xffffffffu);
+#ifdef ORPCD_BOUNDS_CHECK
+        if (j >= (1 << 26) || j < -1) {
+            printf("[chk] accum slot %d i %d best %llx\n", slot, i, bv[k]);
+            j = -1;
+            bv[k] = kNone;
+        }
+#endif
         if (i < N) prevnn[(size_t)slot * N + i] = j >= 0 ? j : kNoMatch;
         const int jj = j >= 0 ? j : 0;
 #pragma unroll
@@ -2092,13 +2122,25 @@ static ExactArgs exact_args(const orpcd_ctx* c, int pass) {
     return ex;
 }
 
+// ORPCD_SYNC_LAUNCH=1 (debugging only): drain the stream after every launch
+// of the pass loop and name the kernel whose execution failed
+static hipError_t launched(const char* name, hipStream_t s) {
+    hipError_t e = hipGetLastError();
+    static const bool sync = getenv("ORPCD_SYNC_LAUNCH") != nullptr;
+    if (e == hipSuccess && sync) {
+        e = hipStreamSynchronize(s);
+        if (e != hipSuccess) fprintf(stderr, "[orpcd] %s failed: %s\n", name, hipGetErrorString(e));
+    }
+    return e;
+}
+
 hipError_t launch_xform(const orpcd_ctx* c, int nact, int pass, double r2, hipStream_t s, const TgtBounds& tb) {
     const int N = (int)c->src.n;
     const SchedX sx = sched_x(c, nact, pass);
     xform_queries_kernel<<<dim3((unsigned)((N + 255) / 256) + (sx.list ? 1u : 0u), (unsigned)nact), 256, 0, s>>>(
         c->src.xyz64.p, N, c->active.p, c->Q.p, c->done.p, c->tdesc.p, tb, c->prevnn.p, search_r2(r2),
         c->opt.reseed, c->q32.p, c->best.p, c->gbox.p, sx, exact_args(c, pass));
-    return hipGetLastError();
+    return launched("xform_queries_kernel", s);
 }
 
 TgtBounds one_target() {
@@ -2218,13 +2260,13 @@ hipError_t launch_gicp_pass(const orpcd_ctx* c, int nact, int pass, double r2, h
             return e;
 #endif
     }
-    if ((e = hipGetLastError()) != hipSuccess) return e;
+    if ((e = launched("nn_search(_sched)_kernel", s)) != hipSuccess) return e;
     const int ablk = accum_blocks(N);
     const bool fused = c->exact_live && c->est != kEstP2P && c->opt.exact_fused;
     if (c->exact_live && !fused) {  // fp64 re-search of the queries the search could not certify
         nn_exact_kernel<<<(unsigned)c->opt.exact_blocks, 256, 0, s>>>(c->src.xyz64.p, N, c->Q.p, c->tdesc.p, c->q32.p,
                                                      exact_args(c, pass), c->best.p);
-        if ((e = hipGetLastError()) != hipSuccess) return e;
+        if ((e = launched("nn_exact_kernel", s)) != hipSuccess) return e;
     }
     if (mid && (e = hipEventRecord(mid, s)) != hipSuccess) return e;
     if (fused) {
@@ -2233,18 +2275,18 @@ hipError_t launch_gicp_pass(const orpcd_ctx* c, int nact, int pass, double r2, h
         gicp_accum_exact_kernel<<<(unsigned)(nexact + ablk * nact), 256, 0, s>>>(
             c->src.xyz64.p, c->scov.p, N, c->tdesc.p, tb, c->active.p, c->Q.p, c->R.p, c->done.p, r2, c->best.p,
             c->prevnn.p, c->partial.p, ablk, nexact, c->q32.p, exact_args(c, pass), 1.0 - c->batch_eps);
-        return hipGetLastError();
+        return launched("gicp_accum_exact_kernel", s);
     }
     if (c->est == kEstP2P) {
         p2p_accum_kernel<<<dim3((unsigned)ablk, (unsigned)nact), 256, 0, s>>>(
             c->src.xyz64.p, N, c->tdesc.p, tb, c->active.p, c->Q.p, c->done.p, r2, c->best.p, c->prevnn.p,
             c->partial.p, ablk);
-        return hipGetLastError();
+        return launched("p2p_accum_kernel", s);
     }
     gicp_accum_kernel<<<dim3((unsigned)ablk, (unsigned)nact), 256, 0, s>>>(
         c->src.xyz64.p, c->scov.p, N, c->tdesc.p, tb, c->active.p, c->Q.p, c->R.p, c->done.p, r2, c->best.p,
         c->prevnn.p, c->partial.p, ablk, 1.0 - c->batch_eps);
-    return hipGetLastError();
+    return launched("gicp_accum_kernel", s);
 }
 
 hipError_t launch_gicp_solve(const orpcd_ctx* c, int nact, int pass, const orpcd_gicp_params& p, hipStream_t s,
@@ -2254,7 +2296,7 @@ hipError_t launch_gicp_solve(const orpcd_ctx* c, int nact, int pass, const orpcd
     solve<<<(unsigned)nact, 64, 0, s>>>(c->active.p, c->partial.p, accum_blocks(c->src.n), nullptr,
                                                     c->src.n, pass, p.max_iteration, p.relative_fitness,
                                                     p.relative_rmse, a);
-    hipError_t e = hipGetLastError();
+    hipError_t e = launched("icp_solve_kernel", s);
     if (e != hipSuccess) return e;
     const double r2 = p.max_correspondence_distance * p.max_correspondence_distance;
     return launch_xform(c, nact, pass + 1, r2, s, tb);  // queries of the next pass (done starts skip)

@@ -93,7 +93,7 @@ __global__ __launch_bounds__(256) void knn_tiles_kernel(
     const float4* __restrict__ thi, int ntiles, const float4* __restrict__ slo, const float4* __restrict__ shi,
     int nsuper, const double* __restrict__ in64, double r2, float margin, double ox, double oy, double oz, int kout,
     int out_input_order, double* __restrict__ rawcov6, int32_t* __restrict__ nbr_idx, double* __restrict__ nbr_d2,
-    int32_t* __restrict__ nbr_cnt, double* __restrict__ mean_dist) {
+    int32_t* __restrict__ nbr_cnt, double* __restrict__ mean_dist, KnnTieOut ties) {
     __shared__ double sx[4][kTile], sy[4][kTile], sz[4][kTile];
     __shared__ int32_t sid[4][kTile];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -220,6 +220,31 @@ __global__ __launch_bounds__(256) void knn_tiles_kernel(
 #pragma unroll
     for (int s = 0; s < K; ++s) c += (s < kout && bi[s] >= 0) ? 1 : 0;
     const int o = out_input_order ? perm[q] : q;
+    if (ties.cnt && kout < K) {
+        // boundary tie (as knn_wave_kernel): the (kout+1)-th neighbour within
+        // the band of the kout-th; the entry lists the kout + kTieExtra nearest
+        const int Kt = kout + kTieExtra;
+        double dk = r2, dk1 = r2;
+#pragma unroll
+        for (int s = 0; s < K; ++s) {
+            if (s == kout) dk = bi[s] >= 0 ? bd[s] : r2;
+            if (s == kout - 1) dk1 = bi[s] >= 0 ? bd[s] : r2;
+        }
+        if (dk < 3.0e38 && dk - dk1 <= ties.rel * dk + ties.abs_coef * sqrt(dk)) {
+            const int e = atomicAdd(ties.cnt, 1);
+            if (e < ties.cap) {
+                int32_t* row = ties.rows + (size_t)e * (Kt + 2);
+                row[0] = q;
+                row[1] = perm[q];
+#pragma unroll
+                for (int s = 0; s < K; ++s)
+                    if (s < Kt) {
+                        row[2 + s] = bi[s];
+                        ties.d2[(size_t)e * Kt + s] = bi[s] >= 0 ? bd[s] : __builtin_huge_val();
+                    }
+            }
+        }
+    }
     if (nbr_idx) {
 #pragma unroll
         for (int s = 0; s < K; ++s)
@@ -714,13 +739,43 @@ __global__ __launch_bounds__(256) void knn_wave_multi_kernel(
     }
 }
 
+// lane-per-query (knn_tiles_kernel, K <= 64): kout neighbours kept in a
+// register list of the template's K >= kout; ties as launch_knn_cov_ties
+static hipError_t launch_knn_lanes(const CloudLayout& L, const double* in64, int K, int kout, double r2,
+                                   double margin, bool out_input_order, double* rawcov6, int32_t* nbr_idx,
+                                   double* nbr_d2, int32_t* nbr_cnt, double* mean_dist, const KnnTieOut& ties,
+                                   hipStream_t s) {
+    const dim3 grid((unsigned)((L.ntiles + 3) / 4));
+#define ORPCD_KNN_LANES(KK)                                                                                       \
+    knn_tiles_kernel<KK><<<grid, 256, 0, s>>>(L.xyz64.p, L.perm.p, (int)L.n, L.tlo.p, L.thi.p, (int)L.ntiles,    \
+                                              L.slo.p, L.shi.p, (int)L.nsuper, in64, r2, (float)margin,          \
+                                              L.org[0], L.org[1], L.org[2], kout, out_input_order ? 1 : 0, rawcov6, \
+                                              nbr_idx, nbr_d2, nbr_cnt, mean_dist, ties)
+    if (K <= 8)
+        ORPCD_KNN_LANES(8);
+    else if (K <= 20)
+        ORPCD_KNN_LANES(20);
+    else if (K <= 24)
+        ORPCD_KNN_LANES(24);
+    else if (K <= 32)
+        ORPCD_KNN_LANES(32);
+    else if (K <= 64)
+        ORPCD_KNN_LANES(64);
+    else
+        return hipErrorInvalidValue;
+#undef ORPCD_KNN_LANES
+    return hipGetLastError();
+}
+
 hipError_t launch_knn_tiles(const CloudLayout& L, const double* in64, int k, double radius, double margin,
                             bool out_input_order, double* rawcov6, int32_t* nbr_idx, double* nbr_d2,
-                            int32_t* nbr_cnt, hipStream_t s, double* mean_dist) {
+                            int32_t* nbr_cnt, hipStream_t s, double* mean_dist, bool lane_per_query) {
     if (L.n <= 0) return hipSuccess;
     const double r2 = radius > 0 ? radius * radius : __builtin_huge_val();
-    static const bool lane_per_query = getenv("ORPCD_KNN_TILES") != nullptr;  // A/B: the lane-per-query kernel
-    if (!lane_per_query && k >= 1 && k <= 64) {
+    if (lane_per_query && k >= 1 && k <= 64)
+        return launch_knn_lanes(L, in64, k, k, r2, margin, out_input_order, rawcov6, nbr_idx, nbr_d2, nbr_cnt,
+                                mean_dist, KnnTieOut{}, s);
+    if (k >= 1 && k <= 64) {
         knn_wave_kernel<<<(unsigned)((L.n + 3) / 4), 256, 0, s>>>(
             L.xyz64.p, L.perm.p, (int)L.n, L.tlo.p, L.thi.p, (int)L.ntiles, L.slo.p, L.shi.p, (int)L.nsuper, in64, r2,
             (float)margin, L.org[0], L.org[1], L.org[2], k, out_input_order ? 1 : 0, rawcov6, nbr_idx, nbr_d2, nbr_cnt,
@@ -746,24 +801,7 @@ hipError_t launch_knn_tiles(const CloudLayout& L, const double* in64, int k, dou
 #undef ORPCD_KNN_MULTI
         return hipGetLastError();
     }
-    const dim3 grid((unsigned)((L.ntiles + 3) / 4));
-#define ORPCD_KNN_TILES(KK)                                                                                      \
-    knn_tiles_kernel<KK><<<grid, 256, 0, s>>>(L.xyz64.p, L.perm.p, (int)L.n, L.tlo.p, L.thi.p, (int)L.ntiles,   \
-                                              L.slo.p, L.shi.p, (int)L.nsuper, in64, r2, (float)margin,         \
-                                              L.org[0], L.org[1], L.org[2], k, out_input_order ? 1 : 0, rawcov6, \
-                                              nbr_idx, nbr_d2, nbr_cnt, mean_dist)
-    if (k <= 8)
-        ORPCD_KNN_TILES(8);
-    else if (k <= 20)
-        ORPCD_KNN_TILES(20);
-    else if (k <= 32)
-        ORPCD_KNN_TILES(32);
-    else if (k <= 64)
-        ORPCD_KNN_TILES(64);
-    else
-        return hipErrorInvalidValue;
-#undef ORPCD_KNN_TILES
-    return hipGetLastError();
+    return hipErrorInvalidValue;
 }
 
 hipError_t launch_knn_batch(const BatchLayout& L, const int32_t* perm, const double* in64, const double* orgs,
@@ -779,10 +817,13 @@ hipError_t launch_knn_batch(const BatchLayout& L, const int32_t* perm, const dou
 }
 
 hipError_t launch_knn_cov_ties(const CloudLayout& L, const double* in64, int kcov, double margin, bool out_input_order,
-                               double* rawcov6, const KnnTieOut& ties, hipStream_t s) {
+                               double* rawcov6, const KnnTieOut& ties, hipStream_t s, bool lane_per_query) {
     if (L.n <= 0) return hipSuccess;
     const int K = kcov + kTieExtra;
     if (kcov < 1 || K > 64) return hipErrorInvalidValue;
+    if (lane_per_query)
+        return launch_knn_lanes(L, in64, K, kcov, __builtin_huge_val(), margin, out_input_order, rawcov6, nullptr,
+                                nullptr, nullptr, nullptr, ties, s);
     knn_wave_kernel<<<(unsigned)((L.n + 3) / 4), 256, 0, s>>>(
         L.xyz64.p, L.perm.p, (int)L.n, L.tlo.p, L.thi.p, (int)L.ntiles, L.slo.p, L.shi.p, (int)L.nsuper, in64,
         __builtin_huge_val(), (float)margin, L.org[0], L.org[1], L.org[2], K, out_input_order ? 1 : 0, rawcov6, nullptr,

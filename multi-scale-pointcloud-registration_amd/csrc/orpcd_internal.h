@@ -686,8 +686,11 @@ struct orpcd_ctx {
         int sched_items = 10240;  // ordered dispatch: split a group until its waves cost <= pass total / this
                                   // (C2 sweep 5120 / 10240 / 20480: 15.4 / 15.0 / 16.6 ms at 30 starts)
         int sched_min_starts = 16;  // ordered dispatch only for batches of at least this many starts
-        int sched_cap_us = 0;     // ordered dispatch: a split's planned cost at most this many us (0: no cap)
-        int sched_cap_mult = 4;   // ... within an item budget of this many times sched_items
+        int sched_cap_us = 30;    // ordered dispatch: a split's planned cost at most this many us (0: no cap;
+                                  // C2 30 / 64 starts 15.50 -> 15.37 / 24.44 -> 24.23 ms, identical hashes,
+                                  // profiles/r05_sched_cap_sweep*.log)
+        int sched_cap_mult = 2;   // ... within an item budget of this many times sched_items
+        int knn_lane_min = 262144;  // clouds of at least this many points: lane-per-query KNN (0: never)
         int exact_nn = 1;         // 1 (default): every correspondence is the fp64 nearest target (the
                                   // oracle's lexicographic (d^2, input index) minimum): fp32 search +
                                   // runner-up band test + fp64 re-search of the uncertified queries;
@@ -743,7 +746,8 @@ hipError_t build_batch_layout(const double* in64, int64_t n, int B, const int32_
 constexpr int kMaxKnn = 1024;  // largest neighbourhood the device KNN keeps (16 sorted chunks of 64 per wave)
 hipError_t launch_knn_tiles(const CloudLayout& L, const double* in64, int k, double radius, double margin,
                             bool out_input_order, double* rawcov6, int32_t* nbr_idx, double* nbr_d2,
-                            int32_t* nbr_cnt, hipStream_t s, double* mean_dist = nullptr);
+                            int32_t* nbr_cnt, hipStream_t s, double* mean_dist = nullptr,
+                            bool lane_per_query = false);
 hipError_t launch_normals_cov(const double* rawcov6, int64_t n, const double* Rc9, int nslots, double eps,
                               double* normals3, double* cov6, hipStream_t s, double* enorm3 = nullptr);
 // KNN-kcov covariances (pure KNN, as launch_knn_tiles) whose search also keeps
@@ -752,7 +756,7 @@ hipError_t launch_normals_cov(const double* rawcov6, int64_t n, const double* Rc
 // raw covariance (6)} -> GICP covariance of that slot's point
 constexpr int kTieExtra = 4;
 hipError_t launch_knn_cov_ties(const CloudLayout& L, const double* in64, int kcov, double margin, bool out_input_order,
-                               double* rawcov6, const KnnTieOut& ties, hipStream_t s);
+                               double* rawcov6, const KnnTieOut& ties, hipStream_t s, bool lane_per_query = false);
 // the same KNN (k <= 64) for every copy of a BatchLayout: perm its common
 // Morton order, in64 the copies in input order (B x n x 3), orgs / margins
 // per copy on the device; outputs at copy b x (6n | n k | n k | n), input order

@@ -142,6 +142,12 @@ int upload_layout(orpcd_ctx* c, const double* xyz, int64_t n, CloudLayout& L, bo
     return layout_from_device(c, xyz, c->scratch64a.p, n, L, tiles, margin);
 }
 
+// The KNN kernel for a cloud of n points: lane-per-query (knn_tiles_kernel)
+// from knn_lane_min points on, where its n / 256 workgroups fill the chip (C5
+// target, 1M points: 8.0 -> 5.5 ms per set-up, profiles/r05_c5_jfa*.json);
+// wave-per-query below.  Both return the same exact neighbour lists.
+bool knn_lane(const orpcd_ctx* c, int64_t n) { return c->opt.knn_lane_min > 0 && n >= c->opt.knn_lane_min; }
+
 // Target k: Morton layout + tiles + GICP covariances (KNN-20 normals), and
 // its device descriptor (TargetDesc, read by the kernels of every batch).
 int upload_target_k(orpcd_ctx* c, int k, const double* xyz, int64_t m, double eps) {
@@ -153,7 +159,7 @@ int upload_target_k(orpcd_ctx* c, int k, const double* xyz, int64_t m, double ep
     CTX_CHECK(c, c->scratch64b.ensure((size_t)m * 6));
     if (eps >= 0.0) {
         CTX_CHECK(c, launch_knn_tiles(c->tgts[k], c->scratch64a.p, 20, -1.0, margin, false, c->scratch64b.p, nullptr,
-                                      nullptr, nullptr, c->stream));
+                                      nullptr, nullptr, c->stream, nullptr, knn_lane(c, m)));
         CTX_CHECK(c, launch_normals_cov(c->scratch64b.p, m, nullptr, 1, eps, nullptr,
                                         ORPCD_NORMAL_COV ? nullptr : c->tcovs[k].p, c->stream,
                                         ORPCD_NORMAL_COV ? c->tcovs[k].p : nullptr));
@@ -258,11 +264,11 @@ int fpfh_at(orpcd_ctx* c, const double* host_xyz, const double* pts, int64_t n, 
     const bool shared = normal_knn == fpfh_knn && normal_radius == fpfh_radius;
     CTX_CHECK(c, launch_knn_tiles(c->aux, pts, normal_knn, normal_radius, margin, true, F.raw.p,
                                   shared ? F.nbr.p : nullptr, shared ? F.nd2.p : nullptr, shared ? F.cnt.p : nullptr,
-                                  c->stream));
+                                  c->stream, nullptr, knn_lane(c, n)));
     CTX_CHECK(c, launch_normals_cov(F.raw.p, n, nullptr, 1, -1.0, F.nrm.p, nullptr, c->stream));
     if (!shared)  // compute_fpfh_feature's own neighbourhoods
         CTX_CHECK(c, launch_knn_tiles(c->aux, pts, fpfh_knn, fpfh_radius, margin, true, nullptr, F.nbr.p, F.nd2.p,
-                                      F.cnt.p, c->stream));
+                                      F.cnt.p, c->stream, nullptr, knn_lane(c, n)));
     CTX_CHECK(c, launch_fpfh(pts, F.nrm.p, n, F.nbr.p, F.nd2.p, F.cnt.p, fpfh_knn, F.spfh.p, feat_out, c->stream));
     return ORPCD_OK;
 }
@@ -290,7 +296,7 @@ int features_device(orpcd_ctx* c, const double* host_xyz, int k, int64_t n, doub
         if (rc) return rc;
     }
     CTX_CHECK(c, launch_knn_tiles(c->aux, pts, fpfh_knn, fpfh_radius, margin, true, nullptr, F.nbr.p, F.nd2.p,
-                                  F.cnt.p, c->stream));
+                                  F.cnt.p, c->stream, nullptr, knn_lane(c, n)));
     CTX_CHECK(c, launch_fpfh(pts, F.nrm.p, n, F.nbr.p, F.nd2.p, F.cnt.p, fpfh_knn, F.spfh.p, F.feat[k].p, c->stream));
     return ORPCD_OK;
 }
@@ -814,7 +820,8 @@ int source_ties_detect(orpcd_ctx* c, const CloudLayout& L, const double* dev_in6
     to.cap = kTieCap;
     to.rel = kTieRel;
     to.abs_coef = abs_coef;
-    CTX_CHECK(c, launch_knn_cov_ties(L, dev_in64, kcov, margin, input_order, rawcov6, to, c->stream));
+    CTX_CHECK(c, launch_knn_cov_ties(L, dev_in64, kcov, margin, input_order, rawcov6, to, c->stream,
+                                     knn_lane(c, L.n)));
     int cnt = 0;
     CTX_CHECK(c, d2h(&cnt, c->tie_cnt.p, 4, c->stream));
     CTX_CHECK(c, hipStreamSynchronize(c->stream));
@@ -1101,6 +1108,11 @@ int batch_setup(orpcd_ctx* c, const double* R0, const double* t0, int B, const o
                                         ORPCD_NORMAL_COV ? c->scov.p : nullptr));
         int rc = source_ties_apply(c, R0, t0, B, p->epsilon);  // boundary ties decided on the posed copies
         if (rc) return rc;
+    }
+    if (getenv("ORPCD_SYNC_LAUNCH")) {  // debugging: the set-up's kernels, apart from the pass loop's
+        const hipError_t e = hipStreamSynchronize(s);
+        if (e != hipSuccess) fprintf(stderr, "[orpcd] batch set-up kernels failed: %s\n", hipGetErrorString(e));
+        CTX_CHECK(c, e);
     }
     CTX_CHECK(c, launch_xform(c, B, 0, p->max_correspondence_distance * p->max_correspondence_distance, s,
                               target_bounds(c, hAct, B)));
@@ -1703,7 +1715,7 @@ int orpcd_sor(orpcd_ctx* c, const double* xyz, int64_t n, int32_t nb_neighbors, 
     CTX_CHECK(c, c->vox.flag.ensure((size_t)n));
     double* avg = c->scratch64b.p;
     CTX_CHECK(c, launch_knn_tiles(c->aux, c->scratch64a.p, nb_neighbors, -1.0, margin, true, nullptr, nullptr,
-                                  nullptr, nullptr, s, avg));
+                                  nullptr, nullptr, s, avg, knn_lane(c, n)));
     CTX_CHECK(c, launch_sor_select(avg, n, std_ratio, c->scratch64c.p, c->vox.flag.p, c->scratch32.p,
                                    c->scratch32.p + n, c->vox.tmp, s));
     int32_t k = 0;
@@ -2054,7 +2066,7 @@ int orpcd_estimate_normals(orpcd_ctx* c, const double* xyz, int64_t n, int32_t k
     double* unrm = uraw + 6 * n;
     double* ucov = unrm + 3 * n;
     CTX_CHECK(c, launch_knn_tiles(c->aux, c->scratch64a.p, knn, radius, margin, true, uraw, nullptr, nullptr, nullptr,
-                                  c->stream));
+                                  c->stream, nullptr, knn_lane(c, n)));
     CTX_CHECK(c, launch_normals_cov(uraw, n, nullptr, 1, epsilon, unrm, epsilon >= 0 ? ucov : nullptr, c->stream));
     std::vector<double> raw6((size_t)n * 6), cov6;
     CTX_CHECK(c, d2h(raw6.data(), uraw, (size_t)n * 48, c->stream));
@@ -2511,6 +2523,7 @@ int orpcd_set_option(orpcd_ctx* c, const char* key, double value) {
     else if (k == "sched_min_starts" && v >= 1) c->opt.sched_min_starts = v;
     else if (k == "sched_cap_us" && v >= 0 && v <= 100000) c->opt.sched_cap_us = v;
     else if (k == "sched_cap_mult" && v >= 1 && v <= 16) c->opt.sched_cap_mult = v;
+    else if (k == "knn_lane_min" && v >= 0) c->opt.knn_lane_min = v;
     else if (k == "exact_nn" && (v == 0 || v == 1)) c->opt.exact_nn = v;
     else if (k == "exact_blocks" && v >= 1 && v <= 65536) c->opt.exact_blocks = v;
     else if (k == "exact_fused" && v >= 0 && v <= 4096) c->opt.exact_fused = v;

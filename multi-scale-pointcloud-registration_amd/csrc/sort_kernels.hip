@@ -159,7 +159,10 @@ hipError_t build_layout(const double* dev_in64, int64_t n, const double bbox_lo[
     L.npad = std::max<int64_t>(kTile, ((n + kTile - 1) / kTile) * kTile);
     L.ntiles = (n + kTile - 1) / kTile;
     hipError_t e;
-    if ((e = L.xyz64.ensure((size_t)n * 3)) != hipSuccess) return e;
+    // xyz64 is sized to the padded tiles (its padding is never written nor
+    // used): a kernel that loads a whole tile's fp64 points before testing
+    // which lanes are real then stays inside the allocation
+    if ((e = L.xyz64.ensure((size_t)L.npad * 3)) != hipSuccess) return e;
     if ((e = L.perm.ensure((size_t)n)) != hipSuccess) return e;
     if ((e = L.codes.ensure((size_t)n * 2)) != hipSuccess) return e;
     if ((e = L.ids.ensure((size_t)n)) != hipSuccess) return e;
