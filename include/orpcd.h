@@ -48,6 +48,9 @@
  *   orpcd_comm_*, orpcd_gicp_shard_run
  *       the same call over several GPUs, its per-pass all-reduce on device
  *                                          generalizedICP.py:59-70 (C5)
+ *   orpcd_set_target_rows, orpcd_target_cov_rows, orpcd_set_target_cov
+ *       the target's KNN-20 covariances (generalizedICP.py:59-70) split by
+ *       rows over the same GPUs, one all-gather
  *   orpcd_fgr_optimize_batch
  *       the B optimize() calls of one multistart (or of several scale
  *       candidates)                        Aligner/Aligner.py:178-202, 263-298
@@ -265,6 +268,23 @@ int orpcd_comm_unique_id(uint8_t* id_out);
 int orpcd_comm_init(orpcd_ctx* ctx, int32_t nranks, int32_t rank, const uint8_t* id);
 int orpcd_comm_destroy(orpcd_ctx* ctx);
 int orpcd_gicp_shard_run(orpcd_ctx* ctx, int32_t* passes_out);
+
+/* The target side of the same split: every rank builds the whole target's
+ * search layout and seed grid (the search needs them) but runs the KNN-20
+ * covariance pass only over its slice of Morton rows [row_begin, row_end)
+ * (ceil(m / nranks) rounded up to whole 64-point tiles).  With a communicator
+ * of nranks ranks (orpcd_comm_init) one RCCL all-gather on the library's
+ * stream completes the covariances and the target is set as by
+ * orpcd_set_target (bit for bit).  Without one (or nranks == 1 trivially
+ * complete), the caller completes it: orpcd_target_cov_rows reads this rank's
+ * rows (orpcd_target_cov_width() doubles per row, Morton order), and
+ * orpcd_set_target_cov takes the concatenation of every rank's rows (m rows).
+ * The GICP calls refuse an incomplete target.                               */
+int orpcd_set_target_rows(orpcd_ctx* ctx, const double* xyz, int64_t m, double epsilon, int32_t rank,
+                          int32_t nranks, int64_t* row_begin, int64_t* row_end);
+int32_t orpcd_target_cov_width(void);
+int orpcd_target_cov_rows(orpcd_ctx* ctx, int64_t row_begin, int64_t row_end, double* out);
+int orpcd_set_target_cov(orpcd_ctx* ctx, const double* cov);
 
 /* Nearest feature row (squared Euclidean, ties -> lowest index) of every
  * query row: the KDTreeFlann SearchKNN(feature, 1) calls of Open3D's

@@ -93,12 +93,12 @@ __global__ __launch_bounds__(256) void knn_tiles_kernel(
     const float4* __restrict__ thi, int ntiles, const float4* __restrict__ slo, const float4* __restrict__ shi,
     int nsuper, const double* __restrict__ in64, double r2, float margin, double ox, double oy, double oz, int kout,
     int out_input_order, double* __restrict__ rawcov6, int32_t* __restrict__ nbr_idx, double* __restrict__ nbr_d2,
-    int32_t* __restrict__ nbr_cnt, double* __restrict__ mean_dist, KnnTieOut ties) {
+    int32_t* __restrict__ nbr_cnt, double* __restrict__ mean_dist, KnnTieOut ties, int t0, int t1) {
     __shared__ double sx[4][kTile], sy[4][kTile], sz[4][kTile];
     __shared__ int32_t sid[4][kTile];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    const int own = blockIdx.x * 4 + w;  // the wave's own tile
-    if (own >= ntiles) return;           // wave-uniform
+    const int own = t0 + blockIdx.x * 4 + w;  // the wave's own tile (queries: tiles [t0, t1))
+    if (own >= t1) return;                    // wave-uniform
     const int q = own * kTile + lane;
     const bool valid = q < n;
     const double qx = valid ? xyz64[3 * q] : 0.0, qy = valid ? xyz64[3 * q + 1] : 0.0,
@@ -351,7 +351,8 @@ __global__ __launch_bounds__(256) void knn_wave_kernel(
     int nsuper, const double* __restrict__ in64, double r2, float margin, double ox, double oy, double oz, int K,
     int out_input_order, double* __restrict__ rawcov6, int32_t* __restrict__ nbr_idx, double* __restrict__ nbr_d2,
     int32_t* __restrict__ nbr_cnt, double* __restrict__ mean_dist, int KC, KnnTieOut ties,
-    const double* __restrict__ orgs = nullptr, const float* __restrict__ margins = nullptr) {
+    const double* __restrict__ orgs = nullptr, const float* __restrict__ margins = nullptr,
+    const int32_t* __restrict__ qlist = nullptr, int nq = 0, int q0 = 0, int q1 = 0x7fffffff) {
 #pragma clang fp contract(off)
     if (orgs) {  // copy y of a BatchLayout: its frame, points, boxes and outputs
         const size_t y = blockIdx.y;
@@ -371,7 +372,14 @@ __global__ __launch_bounds__(256) void knn_wave_kernel(
         if (nbr_cnt) nbr_cnt += y * n;
     }
     const int lane = threadIdx.x & 63;
-    const int q = blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    int q = blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    if (qlist) {  // only the listed Morton positions query (a row shard's points)
+        if (q >= nq) return;  // wave-uniform
+        q = __builtin_amdgcn_readfirstlane(qlist[q]);
+    } else {      // Morton positions [q0, q1)
+        q += q0;
+        if (q >= q1) return;
+    }
     if (q >= n) return;  // wave-uniform
     const double qx = xyz64[3 * q], qy = xyz64[3 * q + 1], qz = xyz64[3 * q + 2];
     const float fx = (float)(qx - ox), fy = (float)(qy - oy), fz = (float)(qz - oz);  // the boxes' fp32 frame
@@ -744,13 +752,15 @@ __global__ __launch_bounds__(256) void knn_wave_multi_kernel(
 static hipError_t launch_knn_lanes(const CloudLayout& L, const double* in64, int K, int kout, double r2,
                                    double margin, bool out_input_order, double* rawcov6, int32_t* nbr_idx,
                                    double* nbr_d2, int32_t* nbr_cnt, double* mean_dist, const KnnTieOut& ties,
-                                   hipStream_t s) {
-    const dim3 grid((unsigned)((L.ntiles + 3) / 4));
+                                   hipStream_t s, int t0 = 0, int t1 = -1) {
+    if (t1 < 0) t1 = (int)L.ntiles;
+    if (t1 <= t0) return hipSuccess;
+    const dim3 grid((unsigned)((t1 - t0 + 3) / 4));
 #define ORPCD_KNN_LANES(KK)                                                                                       \
     knn_tiles_kernel<KK><<<grid, 256, 0, s>>>(L.xyz64.p, L.perm.p, (int)L.n, L.tlo.p, L.thi.p, (int)L.ntiles,    \
                                               L.slo.p, L.shi.p, (int)L.nsuper, in64, r2, (float)margin,          \
                                               L.org[0], L.org[1], L.org[2], kout, out_input_order ? 1 : 0, rawcov6, \
-                                              nbr_idx, nbr_d2, nbr_cnt, mean_dist, ties)
+                                              nbr_idx, nbr_d2, nbr_cnt, mean_dist, ties, t0, t1)
     if (K <= 8)
         ORPCD_KNN_LANES(8);
     else if (K <= 20)
@@ -817,10 +827,19 @@ hipError_t launch_knn_batch(const BatchLayout& L, const int32_t* perm, const dou
 }
 
 hipError_t launch_knn_cov_ties(const CloudLayout& L, const double* in64, int kcov, double margin, bool out_input_order,
-                               double* rawcov6, const KnnTieOut& ties, hipStream_t s, bool lane_per_query) {
+                               double* rawcov6, const KnnTieOut& ties, hipStream_t s, bool lane_per_query,
+                               const int32_t* qlist, int64_t nq) {
     if (L.n <= 0) return hipSuccess;
     const int K = kcov + kTieExtra;
     if (kcov < 1 || K > 64) return hipErrorInvalidValue;
+    if (qlist) {  // listed queries only: one wave each
+        if (nq <= 0) return hipSuccess;
+        knn_wave_kernel<<<(unsigned)((nq + 3) / 4), 256, 0, s>>>(
+            L.xyz64.p, L.perm.p, (int)L.n, L.tlo.p, L.thi.p, (int)L.ntiles, L.slo.p, L.shi.p, (int)L.nsuper, in64,
+            __builtin_huge_val(), (float)margin, L.org[0], L.org[1], L.org[2], K, out_input_order ? 1 : 0, rawcov6,
+            nullptr, nullptr, nullptr, nullptr, kcov, ties, nullptr, nullptr, qlist, (int)nq);
+        return hipGetLastError();
+    }
     if (lane_per_query)
         return launch_knn_lanes(L, in64, K, kcov, __builtin_huge_val(), margin, out_input_order, rawcov6, nullptr,
                                 nullptr, nullptr, nullptr, ties, s);
@@ -828,6 +847,38 @@ hipError_t launch_knn_cov_ties(const CloudLayout& L, const double* in64, int kco
         L.xyz64.p, L.perm.p, (int)L.n, L.tlo.p, L.thi.p, (int)L.ntiles, L.slo.p, L.shi.p, (int)L.nsuper, in64,
         __builtin_huge_val(), (float)margin, L.org[0], L.org[1], L.org[2], K, out_input_order ? 1 : 0, rawcov6, nullptr,
         nullptr, nullptr, nullptr, kcov, ties);
+    return hipGetLastError();
+}
+
+hipError_t launch_knn_cov_range(const CloudLayout& L, const double* in64, int k, double margin, double* rawcov6,
+                                int64_t lo, int64_t hi, bool lane_per_query, hipStream_t s) {
+    hi = std::min<int64_t>(hi, L.n);
+    if (hi <= lo) return hipSuccess;
+    if (k < 1 || k > 64) return hipErrorInvalidValue;
+    if (lane_per_query) {  // whole tiles of queries: lo on a tile boundary, hi too unless it is the end
+        if (lo % kTile || (hi % kTile && hi != L.n)) return hipErrorInvalidValue;
+        return launch_knn_lanes(L, in64, k, k, __builtin_huge_val(), margin, false, rawcov6, nullptr, nullptr,
+                                nullptr, nullptr, KnnTieOut{}, s, (int)(lo / kTile), (int)((hi + kTile - 1) / kTile));
+    }
+    knn_wave_kernel<<<(unsigned)((hi - lo + 3) / 4), 256, 0, s>>>(
+        L.xyz64.p, L.perm.p, (int)L.n, L.tlo.p, L.thi.p, (int)L.ntiles, L.slo.p, L.shi.p, (int)L.nsuper, in64,
+        __builtin_huge_val(), (float)margin, L.org[0], L.org[1], L.org[2], k, 0, rawcov6, nullptr, nullptr, nullptr,
+        nullptr, k, KnnTieOut{}, nullptr, nullptr, nullptr, 0, (int)lo, (int)hi);
+    return hipGetLastError();
+}
+
+// qlist[k] = Morton position of input row row_begin + k (inv: the layout's perm inverted)
+__global__ void rows_to_positions_kernel(const int32_t* __restrict__ perm, int n, int64_t row_begin, int64_t nrows,
+                                         int32_t* __restrict__ qlist) {
+    const int k = blockIdx.x * 256 + threadIdx.x;
+    if (k >= n) return;
+    const int64_t r = (int64_t)perm[k] - row_begin;
+    if (r >= 0 && r < nrows) qlist[r] = k;
+}
+hipError_t launch_rows_to_positions(const int32_t* perm, int64_t n, int64_t row_begin, int64_t nrows, int32_t* qlist,
+                                    hipStream_t s) {
+    if (n <= 0) return hipSuccess;
+    rows_to_positions_kernel<<<(unsigned)((n + 255) / 256), 256, 0, s>>>(perm, (int)n, row_begin, nrows, qlist);
     return hipGetLastError();
 }
 

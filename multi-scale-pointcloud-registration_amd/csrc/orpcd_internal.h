@@ -469,6 +469,7 @@ struct orpcd_ctx {
                                           -1.0, -1.0, -1.0, -1.0, -1.0, -1.0, -1.0, -1.0};
     std::vector<double> tgt_host[orpcd::kMaxTargets];  // input-order copies (epsilon re-derivation)
     int ntgt = 0;                                      // targets set (orpcd_set_target: 1)
+    int64_t tgt_rows[2] = {0, 0};                      // orpcd_set_target_rows: the Morton rows computed here
     orpcd::CloudLayout& tgt = tgts[0];
     orpcd::DevBuf<double>& tcov = tcovs[0];
     orpcd::DevBuf<orpcd::TargetDesc> tdesc;  // kMaxTargets device descriptors of the targets
@@ -756,7 +757,15 @@ hipError_t launch_normals_cov(const double* rawcov6, int64_t n, const double* Rc
 // raw covariance (6)} -> GICP covariance of that slot's point
 constexpr int kTieExtra = 4;
 hipError_t launch_knn_cov_ties(const CloudLayout& L, const double* in64, int kcov, double margin, bool out_input_order,
-                               double* rawcov6, const KnnTieOut& ties, hipStream_t s, bool lane_per_query = false);
+                               double* rawcov6, const KnnTieOut& ties, hipStream_t s, bool lane_per_query = false,
+                               const int32_t* qlist = nullptr, int64_t nq = 0);
+// KNN-k raw covariances of the queries at Morton positions [lo, hi) only
+// (rawcov6 in Morton order; lane_per_query needs lo and hi on tile bounds)
+hipError_t launch_knn_cov_range(const CloudLayout& L, const double* in64, int k, double margin, double* rawcov6,
+                                int64_t lo, int64_t hi, bool lane_per_query, hipStream_t s);
+// qlist[k] = the Morton position (perm inverted) of input row row_begin + k, k < nrows
+hipError_t launch_rows_to_positions(const int32_t* perm, int64_t n, int64_t row_begin, int64_t nrows, int32_t* qlist,
+                                    hipStream_t s);
 // the same KNN (k <= 64) for every copy of a BatchLayout: perm its common
 // Morton order, in64 the copies in input order (B x n x 3), orgs / margins
 // per copy on the device; outputs at copy b x (6n | n k | n k | n), input order

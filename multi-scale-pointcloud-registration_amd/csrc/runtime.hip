@@ -801,7 +801,8 @@ double tie_d2(const double* a, const double* b) {
 }
 
 int source_ties_detect(orpcd_ctx* c, const CloudLayout& L, const double* dev_in64, const double* host_xyz, int64_t n,
-                       double margin, bool input_order, double* rawcov6) {
+                       double margin, bool input_order, double* rawcov6, const int32_t* qlist = nullptr,
+                       int64_t nq = 0) {
     auto& T = c->ties;
     T.clear();
     const int kcov = T.kcov, K = kcov + kTieExtra;
@@ -821,7 +822,7 @@ int source_ties_detect(orpcd_ctx* c, const CloudLayout& L, const double* dev_in6
     to.rel = kTieRel;
     to.abs_coef = abs_coef;
     CTX_CHECK(c, launch_knn_cov_ties(L, dev_in64, kcov, margin, input_order, rawcov6, to, c->stream,
-                                     knn_lane(c, L.n)));
+                                     knn_lane(c, L.n), qlist, nq));
     int cnt = 0;
     CTX_CHECK(c, d2h(&cnt, c->tie_cnt.p, 4, c->stream));
     CTX_CHECK(c, hipStreamSynchronize(c->stream));
@@ -1135,6 +1136,7 @@ struct RcclApi {
     ncclResult_t (*comm_init_rank)(ncclComm_t*, int, ncclUniqueId, int) = nullptr;
     ncclResult_t (*all_reduce)(const void*, void*, size_t, ncclDataType_t, ncclRedOp_t, ncclComm_t,
                                hipStream_t) = nullptr;
+    ncclResult_t (*all_gather)(const void*, void*, size_t, ncclDataType_t, ncclComm_t, hipStream_t) = nullptr;
     ncclResult_t (*comm_destroy)(ncclComm_t) = nullptr;
     const char* (*error_string)(ncclResult_t) = nullptr;
 };
@@ -1151,9 +1153,10 @@ const RcclApi& rccl_api() {
         a.get_unique_id = (decltype(a.get_unique_id))dlsym(h, "ncclGetUniqueId");
         a.comm_init_rank = (decltype(a.comm_init_rank))dlsym(h, "ncclCommInitRank");
         a.all_reduce = (decltype(a.all_reduce))dlsym(h, "ncclAllReduce");
+        a.all_gather = (decltype(a.all_gather))dlsym(h, "ncclAllGather");
         a.comm_destroy = (decltype(a.comm_destroy))dlsym(h, "ncclCommDestroy");
         a.error_string = (decltype(a.error_string))dlsym(h, "ncclGetErrorString");
-        a.ok = a.get_unique_id && a.comm_init_rank && a.all_reduce && a.comm_destroy && a.error_string;
+        a.ok = a.get_unique_id && a.comm_init_rank && a.all_reduce && a.all_gather && a.comm_destroy && a.error_string;
         if (!a.ok) a.err = "librccl.so lacks an nccl* entry point";
         return a;
     }();
@@ -1809,12 +1812,16 @@ int orpcd_set_source_rows(orpcd_ctx* c, const double* xyz, int64_t n, int64_t ro
     CTX_REQUIRE(c, row_begin >= 0 && row_begin < row_end && row_end <= n, "set_source_rows: bad row range");
     CTX_REQUIRE(c, finite_cloud(xyz, n), "set_source_rows: non-finite coordinates");
     CTX_CHECK(c, hipSetDevice(c->device));
-    // KNN-20 covariances of every point against the full cloud (input order)
+    // KNN-20 covariances of this shard's rows against the full cloud (input
+    // order; the other rows' are not computed: each rank computes its own)
     double margin = 0.0;
     int rc = upload_layout(c, xyz, n, c->aux, true, &margin);
     if (rc) return rc;
+    const int64_t nrows = row_end - row_begin;
     CTX_CHECK(c, c->scratch64b.ensure((size_t)n * 6));
-    rc = source_ties_detect(c, c->aux, c->scratch64a.p, xyz, n, margin, true, c->scratch64b.p);
+    CTX_CHECK(c, c->scratch32.ensure((size_t)nrows));
+    CTX_CHECK(c, launch_rows_to_positions(c->aux.perm.p, n, row_begin, nrows, c->scratch32.p, c->stream));
+    rc = source_ties_detect(c, c->aux, c->scratch64a.p, xyz, n, margin, true, c->scratch64b.p, c->scratch32.p, nrows);
     if (rc) return rc;
     // the shard's rows in their own Morton layout, covariances gathered to it
     const int64_t ns = row_end - row_begin;
@@ -1997,6 +2004,93 @@ int orpcd_comm_destroy(orpcd_ctx* c) {
 // the same global sums, hence the same done pass, so all ranks enqueue the
 // same collectives; passes enqueued after the start finished are no-ops (every
 // kernel skips a done start; their sums go unused).
+// Target covariances split by Morton rows (SURVEY.md §8(e), C5's row split):
+// every rank builds the whole target's layout and seed grid (the search needs
+// them), but runs the KNN-20 covariance pass only over its slice of
+// kTile-aligned Morton rows; one all-gather assembles the rest -- in place on
+// the device through the context's RCCL communicator when it has one of
+// nranks ranks, otherwise by the caller (orpcd_target_cov_rows on every rank,
+// orpcd_set_target_cov with the concatenation: a host all-gather).
+static int64_t target_slice(int64_t m, int nranks) {
+    return ((m + nranks - 1) / nranks + kTile - 1) / kTile * kTile;
+}
+
+int orpcd_set_target_rows(orpcd_ctx* c, const double* xyz, int64_t m, double epsilon, int32_t rank, int32_t nranks,
+                          int64_t* row_begin, int64_t* row_end) {
+    if (!c) return ORPCD_EINVAL;
+    CTX_REQUIRE(c, xyz && m > 0, "set_target_rows: empty target cloud");
+    CTX_REQUIRE(c, m < kMaxPoints, "set_target_rows: too many points");
+    CTX_REQUIRE(c, nranks >= 1 && nranks <= 65536 && rank >= 0 && rank < nranks, "set_target_rows: bad rank");
+    CTX_REQUIRE(c, epsilon >= 0, "set_target_rows: epsilon must be >= 0");
+    CTX_REQUIRE(c, finite_cloud(xyz, m), "set_target_rows: non-finite coordinates");
+    const bool device_gather = nranks > 1 && c->comm;
+    CTX_REQUIRE(c, !device_gather || (c->comm_ranks == nranks && c->comm_rank == rank),
+                "set_target_rows: rank / nranks differ from the communicator's (orpcd_comm_init)");
+    CTX_CHECK(c, hipSetDevice(c->device));
+    c->ntgt = 0;
+    c->last_B = 0;
+    double margin = 0.0;
+    int rc = upload_layout(c, xyz, m, c->tgts[0], true, &margin);
+    if (rc) return rc;
+    CTX_CHECK(c, prepare_seed_grid(c->tgts[0]));
+    const int64_t slice = target_slice(m, nranks);
+    const int64_t lo = std::min(m, (int64_t)rank * slice), hi = std::min(m, lo + slice);
+    CTX_CHECK(c, c->tcovs[0].ensure((size_t)(slice * nranks) * kCovW));
+    CTX_CHECK(c, c->scratch64b.ensure((size_t)m * 6));
+    double* tcov = c->tcovs[0].p;
+    if (hi > lo) {
+        CTX_CHECK(c, launch_knn_cov_range(c->tgts[0], c->scratch64a.p, 20, margin, c->scratch64b.p, lo, hi,
+                                          knn_lane(c, m), c->stream));
+        CTX_CHECK(c, launch_normals_cov(c->scratch64b.p + lo * 6, hi - lo, nullptr, 1, epsilon, nullptr,
+                                        ORPCD_NORMAL_COV ? nullptr : tcov + lo * kCovW, c->stream,
+                                        ORPCD_NORMAL_COV ? tcov + lo * kCovW : nullptr));
+    }
+    if (device_gather) {
+        const RcclApi& api = rccl_api();
+        CTX_RCCL(c, api.all_gather(tcov + (size_t)rank * slice * kCovW, tcov, (size_t)slice * kCovW, ncclFloat64,
+                                   (ncclComm_t)c->comm, c->stream));
+    }
+    c->tgt_eps[0] = epsilon;
+    c->tgt_host[0].assign(xyz, xyz + 3 * m);
+    CTX_CHECK(c, c->tdesc.ensure(kMaxTargets));
+    write_target_desc(c->tgts[0], tcov, c->opt.seed_reps, c->opt.seed_grid != 0, c->tdesc_h[0]);
+    CTX_CHECK(c, h2d(c->tdesc.p, &c->tdesc_h[0], sizeof(TargetDesc), c->stream));
+    CTX_CHECK(c, seed_grids(c, 0, 1));
+    CTX_CHECK(c, hipStreamSynchronize(c->stream));
+    c->tgt_rows[0] = lo;
+    c->tgt_rows[1] = hi;
+    if (row_begin) *row_begin = lo;
+    if (row_end) *row_end = hi;
+    // complete (usable by the GICP calls) once every row is there
+    if (nranks == 1 || device_gather) c->ntgt = 1;
+    return ORPCD_OK;
+}
+
+int32_t orpcd_target_cov_width(void) { return kCovW; }
+
+int orpcd_target_cov_rows(orpcd_ctx* c, int64_t row_begin, int64_t row_end, double* out) {
+    if (!c) return ORPCD_EINVAL;
+    CTX_REQUIRE(c, out && c->tgt.n > 0 && c->tcov.n >= (size_t)c->tgt.n * kCovW, "target_cov_rows: no target");
+    const bool whole = c->ntgt > 0;
+    CTX_REQUIRE(c, row_begin >= (whole ? 0 : c->tgt_rows[0]) && row_end <= (whole ? c->tgt.n : c->tgt_rows[1]) &&
+                       row_begin <= row_end,
+                "target_cov_rows: rows outside those computed here");
+    CTX_CHECK(c, hipSetDevice(c->device));
+    CTX_CHECK(c, d2h(out, c->tcov.p + row_begin * kCovW, (size_t)(row_end - row_begin) * kCovW * 8, c->stream));
+    return ORPCD_OK;
+}
+
+int orpcd_set_target_cov(orpcd_ctx* c, const double* cov) {
+    if (!c) return ORPCD_EINVAL;
+    CTX_REQUIRE(c, cov && c->tgt.n > 0 && c->tcov.n >= (size_t)c->tgt.n * kCovW,
+                "set_target_cov: no target layout (orpcd_set_target_rows)");
+    CTX_CHECK(c, hipSetDevice(c->device));
+    CTX_CHECK(c, h2d(c->tcov.p, cov, (size_t)c->tgt.n * kCovW * 8, c->stream));
+    CTX_CHECK(c, hipStreamSynchronize(c->stream));
+    c->ntgt = 1;
+    return ORPCD_OK;
+}
+
 int orpcd_gicp_shard_run(orpcd_ctx* c, int32_t* passes_out) {
     if (!c) return ORPCD_EINVAL;
     CTX_REQUIRE(c, c->shard.begun, "gicp_shard_run: call orpcd_gicp_shard_begin first");

@@ -56,7 +56,8 @@ EXPORTED = ("orpcd_abi_version", "orpcd_build_id", "orpcd_build_flags", "orpcd_d
             "orpcd_last_error", "orpcd_set_target", "orpcd_set_source", "orpcd_gicp_batch",
             "orpcd_set_source_rows", "orpcd_gicp_shard_begin", "orpcd_gicp_shard_pass", "orpcd_gicp_shard_update",
             "orpcd_gicp_shard_result", "orpcd_comm_unique_id", "orpcd_comm_init", "orpcd_comm_destroy",
-            "orpcd_gicp_shard_run",
+            "orpcd_gicp_shard_run", "orpcd_set_target_rows", "orpcd_target_cov_width", "orpcd_target_cov_rows",
+            "orpcd_set_target_cov",
             "orpcd_nn1_radius", "orpcd_estimate_normals", "orpcd_fpfh", "orpcd_fpfh_from_normals", "orpcd_fgr", "orpcd_feature_nn",
             "orpcd_fgr_optimize", "orpcd_fgr_optimize_batch", "orpcd_set_source_points", "orpcd_icp_p2p_batch",
             "orpcd_sor", "orpcd_voxel_down_sample", "orpcd_farthest_downsample",
@@ -162,6 +163,11 @@ def load_library():
         L.orpcd_comm_init.argtypes = [vp, ctypes.c_int32, ctypes.c_int32, _u8p]
         L.orpcd_comm_destroy.argtypes = [vp]
         L.orpcd_gicp_shard_run.argtypes = [vp, _i32p]
+        L.orpcd_set_target_rows.argtypes = [vp, _f64p, c_i64, c_dbl, ctypes.c_int32, ctypes.c_int32, _i64p, _i64p]
+        L.orpcd_target_cov_width.restype = ctypes.c_int32
+        L.orpcd_target_cov_width.argtypes = []
+        L.orpcd_target_cov_rows.argtypes = [vp, c_i64, c_i64, _f64p]
+        L.orpcd_set_target_cov.argtypes = [vp, _f64p]
         L.orpcd_nn1_radius.argtypes = [vp, _f64p, c_i64, _f64p, c_i64, c_dbl, _i32p, _f64p]
         L.orpcd_estimate_normals.argtypes = [vp, _f64p, c_i64, ctypes.c_int32, c_dbl, c_dbl, vp, vp, vp]
         L.orpcd_fpfh.argtypes = [vp, _f64p, c_i64, c_dbl, ctypes.c_int32, c_dbl, ctypes.c_int32, _f64p, _f64p]
@@ -553,6 +559,34 @@ class Context:
         self._check(self._L.orpcd_gicp_shard_result(self._h, T, rmse, fit, it, nc), "orpcd_gicp_shard_result")
         return dict(T=T.reshape(4, 4), rmse=float(rmse[0]), fitness=float(fit[0]), iters=int(it[0]),
                     ncorr=int(nc[0]))
+
+    def set_target_rows(self, xyz: np.ndarray, rank: int, nranks: int, epsilon: float = 1e-3):
+        """This rank's share of the target's covariance pass (orpcd_set_target_rows);
+        returns its Morton rows (lo, hi).  Complete at once with a communicator
+        of nranks ranks; otherwise complete it with set_target_cov."""
+        xyz = _c3(xyz)
+        lo, hi = np.zeros(1, np.int64), np.zeros(1, np.int64)
+        self._check(self._L.orpcd_set_target_rows(self._h, xyz, len(xyz), float(epsilon), int(rank), int(nranks),
+                                                  lo, hi), "orpcd_set_target_rows")
+        self._target_key = None
+        self._target_rows_n = len(xyz)
+        return int(lo[0]), int(hi[0])
+
+    def target_cov_rows(self, lo: int, hi: int) -> np.ndarray:
+        """The target's covariance rows [lo, hi) in Morton order, (hi - lo, width)."""
+        w = int(self._L.orpcd_target_cov_width())
+        out = np.zeros((max(int(hi) - int(lo), 0), w))
+        self._check(self._L.orpcd_target_cov_rows(self._h, int(lo), int(hi), out.reshape(-1) if out.size else
+                                                  np.zeros(1)), "orpcd_target_cov_rows")
+        return out
+
+    def set_target_cov(self, cov: np.ndarray):
+        """Complete a target begun with set_target_rows: every rank's rows, in order (m, width)."""
+        cov = np.ascontiguousarray(cov, dtype=np.float64)
+        n = getattr(self, "_target_rows_n", None)
+        if n is None or cov.size != n * int(self._L.orpcd_target_cov_width()):
+            raise ValueError("set_target_cov: needs set_target_rows first and (m, width) rows")
+        self._check(self._L.orpcd_set_target_cov(self._h, cov.reshape(-1)), "orpcd_set_target_cov")
 
     # ------------------------------------------- device collectives (RCCL)
     def comm_unique_id(self) -> bytes:

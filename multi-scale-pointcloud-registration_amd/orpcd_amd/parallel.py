@@ -11,8 +11,10 @@ block spans one or two candidate targets.  No other data-path collective
 exists.
 
 2. Row sharding of one start (C5: one GICP over 1M points).  Each rank owns
-a contiguous block of source rows (covariances still from the full cloud's
-neighbourhoods) and the whole target; per ICP pass it computes the 29 local
+a contiguous block of source rows (their covariances from the full cloud's
+neighbourhoods, computed for its rows only) and the whole target, whose
+covariance pass is split by rows too (target_rows_sharded: each rank 1/ws of
+the KNN-20 pass, one all-gather); per ICP pass it computes the 29 local
 normal-equation sums, one all-reduce(sum) of 232 bytes combines them, and
 every rank solves the same 6x6 system (gicp_rows_sharded).  With
 ``device_collectives=True`` that all-reduce is the library's own RCCL
@@ -131,6 +133,36 @@ def device_comm(ctx):
     ctx._orpcd_comm = key
 
 
+def allgather_arrays(a: np.ndarray) -> list:
+    """Every rank's array (shapes may differ), in rank order (identity on one rank)."""
+    rank, ws = world()
+    if ws == 1:
+        return [a]
+    import torch.distributed as dist
+    out = [None] * ws
+    dist.all_gather_object(out, np.ascontiguousarray(a))
+    return out
+
+
+def target_rows_sharded(ctx, target: np.ndarray, epsilon: float = 1e-3, device_collectives: bool = False):
+    """Set ``target`` on every rank's ``ctx`` with its KNN-20 covariance pass
+    split by rows (orpcd_set_target_rows): each rank computes 1/ws of the rows;
+    one all-gather completes them -- on the device through the context's RCCL
+    communicator with ``device_collectives``, else through torch.distributed
+    on the host (orpcd_target_cov_rows / orpcd_set_target_cov).  The result is
+    the target orpcd_set_target makes, bit for bit."""
+    rank, ws = world()
+    if ws == 1:
+        ctx.set_target(target, epsilon)
+        return
+    if device_collectives:
+        device_comm(ctx)
+        ctx.set_target_rows(target, rank, ws, epsilon)
+        return
+    lo, hi = ctx.set_target_rows(target, rank, ws, epsilon)
+    ctx.set_target_cov(np.concatenate(allgather_arrays(ctx.target_cov_rows(lo, hi))))
+
+
 def gicp_rows_sharded(ctx, source: np.ndarray, target: np.ndarray, R0=None, t0=None, epsilon: float = 1e-3,
                       device_collectives: bool = False, **params) -> dict:
     """One GICP (pose ``source @ R0 + t0``) with the source rows split over the
@@ -150,7 +182,7 @@ def gicp_rows_sharded(ctx, source: np.ndarray, target: np.ndarray, R0=None, t0=N
     lo, hi = shard(n, rank, ws)
     R0 = np.eye(3) if R0 is None else R0
     t0 = np.zeros(3) if t0 is None else t0
-    ctx.set_target(target, epsilon)
+    target_rows_sharded(ctx, target, epsilon, device_collectives)
     ctx.set_source_rows(source, lo, hi)
     ctx.shard_begin(R0, t0, n_total=n, epsilon=epsilon, **params)
     if device_collectives:

@@ -15,6 +15,27 @@ class FakeShardContext:
         self.tgt = np.ascontiguousarray(target, dtype=np.float64)
         self.tcov = oracle.estimate_normals(self.tgt, 20, -1.0, epsilon)[2]
 
+    # the target's covariance pass by rows (orpcd_set_target_rows): the fake's
+    # rows are input rows; a rank keeps its slice only until set_target_cov
+    def set_target_rows(self, target, rank, nranks, epsilon):
+        self.tgt = np.ascontiguousarray(target, dtype=np.float64)
+        m = len(self.tgt)
+        slice_ = -(-m // nranks)
+        lo, hi = min(m, rank * slice_), min(m, rank * slice_ + slice_)
+        self.tcov = np.full((m, 3, 3), np.nan)
+        self.tcov[lo:hi] = oracle.estimate_normals(self.tgt, 20, -1.0, epsilon)[2][lo:hi]
+        if getattr(self, "comm", None) and self.comm[0] == nranks:  # the device all-gather, over the group
+            from orpcd_amd import parallel
+            self.set_target_cov(np.concatenate(parallel.allgather_arrays(self.target_cov_rows(lo, hi))))
+        return lo, hi
+
+    def target_cov_rows(self, lo, hi):
+        assert not np.isnan(self.tcov[lo:hi]).any()
+        return self.tcov[lo:hi].reshape(hi - lo, 9)
+
+    def set_target_cov(self, cov):
+        self.tcov = np.asarray(cov).reshape(len(self.tgt), 3, 3)
+
     def set_source_rows(self, source, lo, hi):
         self.src_full = np.ascontiguousarray(source, dtype=np.float64)
         self.lo, self.hi = lo, hi

@@ -119,3 +119,48 @@ def test_shard_c5_size_two_ranks_match_oracle(oracle):
     print(f"C5 2 ranks: |dT| {np.abs(res[0]['T'] - o['T']).max():.1e} |d rmse| {abs(res[0]['rmse'] - o['rmse']):.1e}")
     for c in ctxs:
         c.close()
+
+
+@pytest.mark.parametrize("lane_min", [0, 1])
+def test_target_rows_emulated_ranks_assemble_the_full_target(lane_min):
+    """orpcd_set_target_rows over 3 emulated ranks (3 contexts; both KNN
+    kernels): each rank's Morton rows are the full orpcd_set_target's, bit for
+    bit; their concatenation through orpcd_set_target_cov gives a target on
+    which a GICP batch returns the same bits; an incomplete target is refused
+    by the GICP calls; one rank alone is complete at once."""
+    from orpcd_amd import _native
+    src, tgt = _pair()
+    full = _native.Context(0)
+    full.set_option("knn_lane_min", lane_min)
+    full.set_target(tgt, 1e-3, cache=False)
+    want = full.target_cov_rows(0, len(tgt))
+    ctxs = [_native.Context(0) for _ in range(3)]
+    parts, rows = [], []
+    for r, c in enumerate(ctxs):
+        c.set_option("knn_lane_min", lane_min)
+        lo, hi = c.set_target_rows(tgt, r, 3, 1e-3)
+        assert lo % 64 == 0 and (hi % 64 == 0 or hi == len(tgt))
+        rows.append((lo, hi))
+        parts.append(c.target_cov_rows(lo, hi))
+        assert np.array_equal(parts[-1], want[lo:hi])
+    assert rows[0][0] == 0 and rows[-1][1] == len(tgt) and all(rows[k][1] == rows[k + 1][0] for k in range(2))
+    with pytest.raises(ValueError, match="no target"):
+        ctxs[1].set_source(src, cache=False)
+        ctxs[1].gicp_batch(np.eye(3)[None], np.zeros((1, 3)))
+    with pytest.raises(ValueError):
+        ctxs[1].target_cov_rows(0, len(tgt))       # rows another rank computed
+    ctxs[0].set_target_cov(np.concatenate(parts))
+    ctxs[0].set_source(src, cache=False)
+    full.set_source(src, cache=False)
+    R0 = np.array([np.eye(3), np.eye(3)[[1, 2, 0]]])
+    t0 = np.zeros((2, 3))
+    a, b = ctxs[0].gicp_batch(R0, t0, max_correspondence_distance=0.3), full.gicp_batch(R0, t0,
+                                                                                       max_correspondence_distance=0.3)
+    for k in ("T", "rmse", "iters", "ncorr"):
+        assert np.array_equal(a[k], b[k]), k
+    one = _native.Context(0)
+    one.set_option("knn_lane_min", lane_min)
+    assert one.set_target_rows(tgt, 0, 1, 1e-3) == (0, len(tgt))
+    assert np.array_equal(one.target_cov_rows(0, len(tgt)), want)
+    for c in ctxs + [full, one]:
+        c.close()

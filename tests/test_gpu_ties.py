@@ -15,7 +15,8 @@ np.random.seed(0)) has 8 points whose 20th and 21st neighbours are within
 * 30 C1 starts through orpcd_gicp_batch against oracle GICP on the posed
   copies: identical iteration counts, RMSE within 1e-10, T within 1e-9;
 * the same starts with the source rows split over 2 emulated ranks
-  (orpcd_set_source_rows, C5's path): the same gates;
+  (orpcd_set_source_rows, C5's path; each rank lists its own rows' ties):
+  the same gates;
 * the zero-code-change drop-in path (the reference-shaped sequential Aligner,
   one optimize() per attempt) through a complete C1 align() against the
   complete-oracle fixture (g7_align_c1): every call's RMSE within 1e-10.
@@ -108,8 +109,8 @@ def test_c1_starts_row_sharded_match_oracle(oracle, c1):
         lo, hi = parallel.shard(len(s), k, 2)
         c.set_target(t, 1e-3)
         c.set_source_rows(s, lo, hi)
-    n_on = sum(c.source_ties()["n_ties"] for c in ctxs[:1])
-    assert n_on == 8
+    # each rank lists the ties among its own rows (its KNN runs for its rows only)
+    assert sum(c.source_ties()["n_ties"] for c in ctxs) == 8
     for b in range(0, 30, 6):
         R0, t0 = z["R0"][b], z["t0"][b]
         for c in ctxs:
