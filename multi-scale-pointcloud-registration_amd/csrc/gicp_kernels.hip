@@ -644,6 +644,11 @@ __host__ __device__ __forceinline__ unsigned long long sched_item(int slot, int 
     return ((unsigned long long)slot << 48) | ((unsigned long long)k << 44) | ((unsigned long long)wg << 20) |
            ((unsigned long long)split << 8) | (unsigned long long)S;
 }
+// most splits of one 128-query group (item fields: 8 bits each for S and split)
+#ifndef ORPCD_SCHED_SMAX
+#define ORPCD_SCHED_SMAX 64
+#endif
+static_assert(ORPCD_SCHED_SMAX >= 1 && ORPCD_SCHED_SMAX <= 255, "split count must fit the item's 8-bit fields");
 struct SchedX {                          // query transform side (pass p + 1)
     const unsigned* wcost_prev;          // the previous pass's per-group costs (B x NG)
     unsigned* wcost_cur;                 // this pass's: zeroed for the search
@@ -702,7 +707,7 @@ __device__ __forceinline__ void plan_start_items(const SchedX& sx, int slot, int
         cls = kSchedClasses - 1;
         if (sx.have_cost) {
             const unsigned C = cost[g];
-            S = min(64, max(1, (int)ceilf((float)C / s_target)));
+            S = min(ORPCD_SCHED_SMAX, max(1, (int)ceilf((float)C / s_target)));
             const unsigned per = C / (unsigned)S + 1u;
             cls = max(0, kSchedClasses - 1 - (31 - __builtin_clz(per)));  // log2 of a split's cost, heaviest first
         }
@@ -1074,7 +1079,7 @@ __global__ __launch_bounds__(64 * kSWaves) __attribute__((amdgpu_waves_per_eu(kE
     const int slot = (int)(it >> 48), tk = (int)((it >> 44) & 15u), wg = (int)((it >> 20) & 0xFFFFFFu);
     const int split = (int)((it >> 8) & 0xFFu), S = (int)(it & 0xFFu);
 #ifdef ORPCD_SCHED_CHECK
-    if (slot >= sa.B || wg >= sa.NG || tk >= kMaxTargets || S < 1 || S > 64 || split >= S || wg * 128 >= N) {
+    if (slot >= sa.B || wg >= sa.NG || tk >= kMaxTargets || S < 1 || S > ORPCD_SCHED_SMAX || split >= S || wg * 128 >= N) {
         if (lane == 0) printf("[sched] bad item w %u cls %d off %u: slot %d tk %d wg %d split %d S %d\n", w, cls, off, slot, tk, wg, split, S);
         return;
     }

@@ -103,9 +103,10 @@ def main():
     # of every multistart (a multistart the 1-GPU run never evaluated was
     # speculated past the reference's path: its rows are never selected and
     # are filled with rmse = inf)
-    rank_wall, rank_calls, rank_gathers = [], [], []
+    rank_wall, rank_calls, rank_gathers, rank_iters = [], [], [], []
     for r in range(a.ranks):
         k = [0]
+        its = []  # per call: (max, sum) of this rank's starts' iterations
 
         def replay(local, B, r=r):
             full = np.zeros((B, parallel.REC))
@@ -117,6 +118,7 @@ def main():
                 else:
                     full[p, 0] = np.inf
             lo, hi = parallel.shard(B, r, a.ranks)
+            its.append((int(local[:, 2].max()) if len(local) else 0, int(local[:, 2].sum())))
             m = known[lo:hi]
             assert np.array_equal(local[m], full[lo:hi][m]), f"rank {r} call {k[0]}: sharded rows differ"
             full[lo:hi] = local
@@ -138,6 +140,7 @@ def main():
         rank_wall.append(w)
         rank_calls.append(c)
         rank_gathers.append(k[0])
+        rank_iters.append(its)
     parallel.world, parallel.allgather_records = real_world, real_gather
     Aligner._run_tables = orig_run_tables
     ncalls = len(rank_calls[0])
@@ -146,6 +149,16 @@ def main():
     host_outside = max(w - sum(c) for w, c in zip(rank_wall, rank_calls))
     ag = rank_gathers[0] * a.allgather_us * 1e-6
     tG = sum(per_call_max) + ag + host_outside
+    # the same projection if every call's work were spread evenly over the
+    # ranks (the bound a perfect re-deal could reach)
+    per_call_mean = [float(np.mean([rc[i] for rc in rank_calls])) for i in range(ncalls)]
+    t_bal = sum(per_call_mean) + ag + host_outside
+    # what sets a rank's call time: its starts' largest iteration count (the
+    # passes it runs) or their summed iterations (its work)
+    xs = np.array([[rank_iters[r][i][0], rank_iters[r][i][1], rank_calls[r][i]] for r in range(a.ranks)
+                   for i in range(min(ncalls, len(rank_iters[r])))], float)
+    corr = {"max_iters": round(float(np.corrcoef(xs[:, 0], xs[:, 2])[0, 1]), 3) if len(xs) > 2 else None,
+            "sum_iters": round(float(np.corrcoef(xs[:, 1], xs[:, 2])[0, 1]), 3) if len(xs) > 2 else None}
     out = {
         "metric": f"C4 Aligner.align() pattern search wall-clock, {a.attempts} starts/multistart, "
                   f"{a.points // 1000}k<->{a.points // 1000}k (1-GPU measurement + {a.ranks}-rank projection)",
@@ -161,7 +174,10 @@ def main():
         "per_call_1gpu_s": [round(x, 5) for x in calls1],
         "per_call_rank_s": [[round(x, 5) for x in c] for c in rank_calls],
 
+        "per_call_rank_iters_max_sum": rank_iters,
+        "call_time_correlation": corr,
         "projected_speedup": round(t1 / tG, 2),
+        "projected_speedup_balanced": round(t1 / t_bal, 2),
         "speculative_depth": {"1gpu": "auto", "ranks": a.depth or "auto"}, "shard_interleave": a.interleave,
         "result": res1,
         "note": "every rank's shard timed alone on one MI355X (same seed, same control flow); its rows were "

@@ -1,0 +1,20 @@
+# Round 5, GPU session 12: persistent ordered dispatch A/B (5 and 4 waves per SIMD), then the GPU suite with it forced on.
+set -e
+O=gpurun_out/r5s12; mkdir -p $O
+cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
+step() { echo "$(date +%T) $1" >> $O/steps.log; }
+step sweep
+for rep in 1 2; do
+  for cfg in 'head|{}' 'head|{"sched_persist": 1}' 'head|{"sched_persist": 1, "persist_waves": 10240}' 'abl/peu4.so|{"sched_persist": 1, "persist_waves": 4096}' 'abl/peu4.so|{"sched_persist": 1, "persist_waves": 8192}'; do
+    lib=${cfg%%|*}; opt=${cfg#*|}
+    for ST in 30 64 8; do
+      echo "== $lib $opt starts=$ST" >> $O/sweep.log
+      if [ $lib = head ]; then
+        timeout -k 10 120 python3 tools/one_batch.py "$opt" --reps 5 --starts $ST >> $O/sweep.log 2>&1
+      else
+        ORPCD_HIP_LIB=$lib timeout -k 10 120 python3 tools/one_batch.py "$opt" --reps 5 --starts $ST >> $O/sweep.log 2>&1
+      fi
+    done
+  done
+done
+step done
