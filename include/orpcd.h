@@ -135,6 +135,19 @@ int orpcd_gicp_batch_targets(orpcd_ctx* ctx, const double* R0, const double* t0,
                              int32_t B, const orpcd_gicp_params* params, double* T_out, double* rmse_out,
                              double* fitness_out, int32_t* iters_out, int64_t* ncorr_out);
 
+/* orpcd_gicp_batch_targets over passes [pass_begin, pass_end) only: a window
+ * of the same loop.  state_in (B x 18 doubles, caller order: T row-major 4x4
+ * as the solve keeps it, then the previous pass's fitness and rmse) is where
+ * the starts stand at pass_begin (NULL at pass_begin 0).  After the window,
+ * done_out[b] = 1 for the starts that finished (their outputs are set) and
+ * state_out holds the others' state at pass_end; resuming them from it, in
+ * any batch and on any context with the same source and targets, continues
+ * them bit for bit (the multi-GPU re-deal of running starts).  */
+int orpcd_gicp_batch_window(orpcd_ctx* ctx, const double* R0, const double* t0, const int32_t* target_of_start,
+                            int32_t B, const orpcd_gicp_params* params, int32_t pass_begin, int32_t pass_end,
+                            const double* state_in, double* state_out, int32_t* done_out, double* T_out,
+                            double* rmse_out, double* fitness_out, int32_t* iters_out, int64_t* ncorr_out);
+
 /* ------------------------------------ source KNN-20 boundary ties (per pose)
  * Open3D recomputes the source's KNN-20 covariances on every posed copy
  * source_initialized = source @ R0 + t0 (Aligner.py:183-185; the PointCloud

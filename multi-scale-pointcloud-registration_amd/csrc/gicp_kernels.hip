@@ -2107,7 +2107,7 @@ static SchedX sched_x(const orpcd_ctx* c, int nact, int pass) {
     sx.list = c->wlist.p;
     sx.cap = c->sched_cap;
     sx.NG = (int)NG;
-    sx.have_cost = pass > 0;
+    sx.have_cost = pass > c->pass_base;  // costs exist from the batch's second pass on
     sx.S0 = uniform_splits(c, nact);
     sx.inv_want = 1.0f / (float)c->opt.sched_items;
     sx.max_target = (float)c->opt.sched_cap_us * 100.0f;  // us -> s_memrealtime ticks (10 ns)
@@ -2229,7 +2229,7 @@ hipError_t launch_gicp_pass(const orpcd_ctx* c, int nact, int pass, double r2, h
         // ordered dispatch: the items were filed by this pass's query transform;
         // the grid covers their upper bound (surplus waves exit at once)
         const int64_t NG = (N + 127) / 128;
-        const int64_t items = pass == 0 ? (int64_t)uniform_splits(c, nact) * nact * NG
+        const int64_t items = pass == c->pass_base ? (int64_t)uniform_splits(c, nact) * nact * NG
                                         : sched_item_budget(c) + 2 * (int64_t)nact * NG + 64;
         const int64_t B = c->sched_B;
         const int par = pass & 1;

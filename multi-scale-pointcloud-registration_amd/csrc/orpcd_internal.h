@@ -288,6 +288,7 @@ struct CloudLayout {
 
 // AdvancedMatching's tuple test on the device (fgr_kernels.hip, "tuple
 // test"): one job per start, trials processed in windows of kTupleWindow.
+constexpr int kStateW = 18;  // a running GICP start's state (orpcd_gicp_batch_window): T (16), prev fitness, rmse
 constexpr int64_t kTupleWindow = (int64_t)1 << 21;  // trials per start and window
 struct TupleJob {
     const double* xi = nullptr;  // cloud fi (the one with more points; the source on a tie), device, input order
@@ -470,6 +471,7 @@ struct orpcd_ctx {
     std::vector<double> tgt_host[orpcd::kMaxTargets];  // input-order copies (epsilon re-derivation)
     int ntgt = 0;                                      // targets set (orpcd_set_target: 1)
     int64_t tgt_rows[2] = {0, 0};                      // orpcd_set_target_rows: the Morton rows computed here
+    int pass_base = 0;                                 // the running batch's first pass (orpcd_gicp_batch_window)
     orpcd::CloudLayout& tgt = tgts[0];
     orpcd::DevBuf<double>& tcov = tcovs[0];
     orpcd::DevBuf<orpcd::TargetDesc> tdesc;  // kMaxTargets device descriptors of the targets

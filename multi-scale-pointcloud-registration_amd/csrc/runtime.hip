@@ -996,7 +996,7 @@ int source_ties_apply(orpcd_ctx* c, const double* R0, const double* t0, int B, d
 // init16 != null (PointToPoint refinement): base pose G_b = init16[b] (column
 // convention, as registration_icp applies `init`), no covariances.
 int batch_setup(orpcd_ctx* c, const double* R0, const double* t0, int B, const orpcd_gicp_params* p,
-                const double* init16 = nullptr) {
+                const double* init16 = nullptr, const double* state_in = nullptr, int pass_begin = 0) {
     const int64_t N = c->src.n;
     const int nblk = accum_blocks(N);
     c->last_B = 0;  // set once the batch is set up
@@ -1081,6 +1081,22 @@ int batch_setup(orpcd_ctx* c, const double* R0, const double* t0, int B, const o
         for (int t = 0; t < 12; ++t) hQ[12 * b + t] = hG[12 * b + t];
         for (int t = 0; t < 9; ++t) hR[9 * b + t] = (t % 4 == 0) ? 1.0 : 0.0;
         hPrev[2 * b] = hPrev[2 * b + 1] = 0.0;
+        if (state_in) {  // resumed at pass_begin: the pose and previous metrics the solve left there
+#pragma clang fp contract(off)  // Q as icp_solve_kernel forms it (solve_start), bit for bit
+            const double* S = state_in + (size_t)kStateW * b;
+            const double* G = &hG[12 * b];
+            for (int t = 0; t < 16; ++t) hT[16 * b + t] = S[t];
+            for (int r = 0; r < 3; ++r) {
+                for (int cc = 0; cc < 4; ++cc) {
+                    double v = S[4 * r + 0] * G[cc] + S[4 * r + 1] * G[4 + cc] + S[4 * r + 2] * G[8 + cc];
+                    if (cc == 3) v += S[4 * r + 3];
+                    hQ[12 * b + 4 * r + cc] = v;
+                }
+                for (int cc = 0; cc < 3; ++cc) hR[9 * b + 3 * r + cc] = S[4 * r + cc];
+            }
+            hPrev[2 * b] = S[16];
+            hPrev[2 * b + 1] = S[17];
+        }
     }
     int32_t* hAct = c->h32.p;
     int32_t* hDone = hAct + B;
@@ -1115,14 +1131,16 @@ int batch_setup(orpcd_ctx* c, const double* R0, const double* t0, int B, const o
         if (e != hipSuccess) fprintf(stderr, "[orpcd] batch set-up kernels failed: %s\n", hipGetErrorString(e));
         CTX_CHECK(c, e);
     }
-    CTX_CHECK(c, launch_xform(c, B, 0, p->max_correspondence_distance * p->max_correspondence_distance, s,
+    c->pass_base = pass_begin;
+    CTX_CHECK(c, launch_xform(c, B, pass_begin, p->max_correspondence_distance * p->max_correspondence_distance, s,
                               target_bounds(c, hAct, B)));
     c->gaps_setup_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_setup).count();
     return ORPCD_OK;
 }
 
 int run_passes(orpcd_ctx* c, int B, const orpcd_gicp_params* p, double* T_out, double* rmse_out,
-               double* fitness_out, int32_t* iters_out, int64_t* ncorr_out);
+               double* fitness_out, int32_t* iters_out, int64_t* ncorr_out, int pass_begin = 0,
+               int pass_end = 0x7fffffff);
 int read_outputs(orpcd_ctx* c, int B, unsigned long long tiles_before, double* T_out, double* rmse_out,
                  double* fitness_out, int32_t* iters_out, int64_t* ncorr_out);
 
@@ -1307,10 +1325,33 @@ int orpcd_gicp_batch(orpcd_ctx* c, const double* R0, const double* t0, int32_t B
     return orpcd_gicp_batch_targets(c, R0, t0, nullptr, B, p, T_out, rmse_out, fitness_out, iters_out, ncorr_out);
 }
 
+int orpcd_gicp_batch_window(orpcd_ctx* c, const double* R0, const double* t0, const int32_t* target_of_start,
+                            int32_t B, const orpcd_gicp_params* p, int32_t pass_begin, int32_t pass_end,
+                            const double* state_in, double* state_out, int32_t* done_out, double* T_out,
+                            double* rmse_out, double* fitness_out, int32_t* iters_out, int64_t* ncorr_out);
+
 int orpcd_gicp_batch_targets(orpcd_ctx* c, const double* R0, const double* t0, const int32_t* target_of_start,
                              int32_t B, const orpcd_gicp_params* p, double* T_out, double* rmse_out,
                              double* fitness_out, int32_t* iters_out, int64_t* ncorr_out) {
+    return orpcd_gicp_batch_window(c, R0, t0, target_of_start, B, p, 0, 0x7fffffff, nullptr, nullptr, nullptr, T_out,
+                                   rmse_out, fitness_out, iters_out, ncorr_out);
+}
+
+// The same batch run over passes [pass_begin, pass_end) only (DESIGN.md §7,
+// the C4 re-deal): state_in (B x kStateW, caller order: T row-major 4x4, the
+// previous pass's fitness and rmse) is where the starts stand at pass_begin
+// (required when pass_begin > 0); after the window, done_out[b] tells which
+// starts finished (their outputs are set) and state_out holds the others'
+// state at pass_end.  Resuming a start from that state -- in any batch, on
+// any context -- continues it bit for bit: a start's passes depend only on
+// its pose, its covariances (from R0, t0) and the target.
+int orpcd_gicp_batch_window(orpcd_ctx* c, const double* R0, const double* t0, const int32_t* target_of_start,
+                            int32_t B, const orpcd_gicp_params* p, int32_t pass_begin, int32_t pass_end,
+                            const double* state_in, double* state_out, int32_t* done_out, double* T_out,
+                            double* rmse_out, double* fitness_out, int32_t* iters_out, int64_t* ncorr_out) {
     if (!c) return ORPCD_EINVAL;
+    CTX_REQUIRE(c, pass_begin >= 0 && pass_end > pass_begin && (pass_begin == 0 || state_in),
+                "gicp_batch_window: bad pass window (pass_begin > 0 needs state_in)");
     // the caller's posed tie rows (orpcd_set_posed_tie_rows) belong to this
     // call only: taken before any validation, so a rejected batch never
     // leaves them for the next one
@@ -1358,21 +1399,42 @@ int orpcd_gicp_batch_targets(orpcd_ctx* c, const double* R0, const double* t0, c
     if (rc) return rc;
     c->batch_ntgt = ntg;
     for (int k = 0; k <= ntg; ++k) c->batch_first[k] = first[k];
-    std::vector<double> sR((size_t)B * 9), st((size_t)B * 3);
+    std::vector<double> sR((size_t)B * 9), st((size_t)B * 3), sS;
     for (int b = 0; b < B; ++b) {
         std::memcpy(&sR[(size_t)pos[b] * 9], R0 + 9 * b, 9 * sizeof(double));
         std::memcpy(&st[(size_t)pos[b] * 3], t0 + 3 * b, 3 * sizeof(double));
     }
+    if (state_in) {
+        sS.resize((size_t)B * kStateW);
+        for (int b = 0; b < B; ++b)
+            std::memcpy(&sS[(size_t)pos[b] * kStateW], state_in + (size_t)kStateW * b, kStateW * sizeof(double));
+    }
     const auto t_batch = std::chrono::steady_clock::now();
-    rc = batch_setup(c, sR.data(), st.data(), B, p);
+    rc = batch_setup(c, sR.data(), st.data(), B, p, nullptr, state_in ? sS.data() : nullptr, pass_begin);
     if (rc) return rc;
     std::vector<double> oT((size_t)B * 16), orm((size_t)B), ofit((size_t)B);
     std::vector<int32_t> oit((size_t)B);
     std::vector<int64_t> onc((size_t)B);
-    rc = run_passes(c, B, p, oT.data(), orm.data(), ofit.data(), oit.data(), onc.data());
+    rc = run_passes(c, B, p, oT.data(), orm.data(), ofit.data(), oit.data(), onc.data(), pass_begin, pass_end);
     c->batch_ntgt = 1;
     c->batch_first[1] = 0;
+    c->pass_base = 0;
     if (rc) return rc;
+    if (done_out || state_out) {  // which starts finished in the window, and where the others stand
+        std::vector<int32_t> dn((size_t)B);
+        std::vector<double> hT((size_t)B * 16), hP((size_t)B * 2);
+        CTX_CHECK(c, d2h(dn.data(), c->done.p, (size_t)B * 4, c->stream));
+        CTX_CHECK(c, d2h(hT.data(), c->T.p, hT.size() * 8, c->stream));
+        CTX_CHECK(c, d2h(hP.data(), c->prev.p, hP.size() * 8, c->stream));
+        for (int b = 0; b < B; ++b) {
+            const int q = pos[b];
+            if (done_out) done_out[b] = dn[q] ? 1 : 0;
+            if (state_out) {
+                std::memcpy(state_out + (size_t)kStateW * b, &hT[(size_t)q * 16], 16 * sizeof(double));
+                std::memcpy(state_out + (size_t)kStateW * b + 16, &hP[(size_t)q * 2], 2 * sizeof(double));
+            }
+        }
+    }
     c->stats.host_batch_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_batch).count();
     c->stats.host_batches += 1;
     c->last_slot = pos;
@@ -1527,7 +1589,7 @@ int read_outputs(orpcd_ctx* c, int B, unsigned long long tiles_before, double* T
 // posed source); PointToPoint outputs T * G (registration_icp's result, init
 // included).
 int run_passes(orpcd_ctx* c, int B, const orpcd_gicp_params* p, double* T_out, double* rmse_out,
-               double* fitness_out, int32_t* iters_out, int64_t* ncorr_out) {
+               double* fitness_out, int32_t* iters_out, int64_t* ncorr_out, int pass_begin, int pass_end) {
     const int64_t N = c->src.n;
     (void)N;
     double* hT = c->h64.p + (size_t)B * 12;
@@ -1571,7 +1633,7 @@ int run_passes(orpcd_ctx* c, int B, const orpcd_gicp_params* p, double* T_out, d
     const double sync_before = c->stats.host_sync_ms;
     int nsync = 0;
     double sync_max = 0.0;
-    for (int pass = 0; pass <= p->max_iteration && nact > 0; ++pass) {
+    for (int pass = pass_begin; pass <= p->max_iteration && pass < pass_end && nact > 0; ++pass) {
         hipEvent_t* ev = timed ? &c->ev_pool[3 * pending] : nullptr;
         const auto tl = clk::now();
         hipEvent_t* ge = gaps ? &gev[(size_t)4 * pass] : nullptr;
@@ -1589,7 +1651,7 @@ int run_passes(orpcd_ctx* c, int B, const orpcd_gicp_params* p, double* T_out, d
         if (c->exact_live) c->stats.exact_queries += (double)nact * (double)c->src.n;
         // the host learns which starts finished only every few passes; a
         // finished start's blocks exit at once in the passes in between
-        const bool sync = (pass % every) == every - 1 || pass == p->max_iteration;
+        const bool sync = ((pass - pass_begin) % every) == every - 1 || pass == p->max_iteration || pass == pass_end - 1;
         if (!sync) continue;
         CTX_CHECK(c, hipMemcpyAsync(hDone, c->done.p, (size_t)B * 4, hipMemcpyDeviceToHost, s));
         unsigned long long tiles_now[2] = {0, 0};

@@ -56,7 +56,7 @@ EXPORTED = ("orpcd_abi_version", "orpcd_build_id", "orpcd_build_flags", "orpcd_d
             "orpcd_last_error", "orpcd_set_target", "orpcd_set_source", "orpcd_gicp_batch",
             "orpcd_set_source_rows", "orpcd_gicp_shard_begin", "orpcd_gicp_shard_pass", "orpcd_gicp_shard_update",
             "orpcd_gicp_shard_result", "orpcd_comm_unique_id", "orpcd_comm_init", "orpcd_comm_destroy",
-            "orpcd_gicp_shard_run", "orpcd_set_target_rows", "orpcd_target_cov_width", "orpcd_target_cov_rows",
+            "orpcd_gicp_shard_run", "orpcd_gicp_batch_window", "orpcd_set_target_rows", "orpcd_target_cov_width", "orpcd_target_cov_rows",
             "orpcd_set_target_cov",
             "orpcd_nn1_radius", "orpcd_estimate_normals", "orpcd_fpfh", "orpcd_fpfh_from_normals", "orpcd_fgr", "orpcd_feature_nn",
             "orpcd_fgr_optimize", "orpcd_fgr_optimize_batch", "orpcd_set_source_points", "orpcd_icp_p2p_batch",
@@ -163,6 +163,9 @@ def load_library():
         L.orpcd_comm_init.argtypes = [vp, ctypes.c_int32, ctypes.c_int32, _u8p]
         L.orpcd_comm_destroy.argtypes = [vp]
         L.orpcd_gicp_shard_run.argtypes = [vp, _i32p]
+        L.orpcd_gicp_batch_window.argtypes = [vp, _f64p, _f64p, vp, ctypes.c_int32, ctypes.POINTER(GicpParams),
+                                              ctypes.c_int32, ctypes.c_int32, vp, _f64p, _i32p, _f64p, _f64p, _f64p,
+                                              _i32p, _i64p]
         L.orpcd_set_target_rows.argtypes = [vp, _f64p, c_i64, c_dbl, ctypes.c_int32, ctypes.c_int32, _i64p, _i64p]
         L.orpcd_target_cov_width.restype = ctypes.c_int32
         L.orpcd_target_cov_width.argtypes = []
@@ -458,6 +461,35 @@ class Context:
                                                      ctypes.byref(p), T.reshape(-1), rmse, fit, iters, ncorr),
                     "orpcd_gicp_batch_targets")
         return dict(T=T, rmse=rmse, fitness=fit, iters=iters, ncorr=ncorr)
+
+    STATE_W = 18  # a running start's state: T (4x4, row-major), previous fitness and rmse
+
+    def gicp_batch_window(self, R0: np.ndarray, t0: np.ndarray, target_of_start=None, pass_begin: int = 0,
+                          pass_end: int = 1 << 30, state=None, max_correspondence_distance=0.5, max_iteration=100,
+                          relative_fitness=1e-6, relative_rmse=1e-6, epsilon=1e-3) -> dict:
+        """gicp_batch_targets over passes [pass_begin, pass_end) (orpcd_gicp_batch_window):
+        `done` marks the starts that finished (their outputs are set); `state`
+        (B, 18) is where the others stand at pass_end, to resume them from
+        (pass_begin = pass_end, state) in any batch."""
+        R0 = np.ascontiguousarray(R0, dtype=np.float64).reshape(-1, 3, 3)
+        B = R0.shape[0]
+        t0 = np.ascontiguousarray(t0, dtype=np.float64).reshape(B, 3)
+        tids = None if target_of_start is None else np.ascontiguousarray(target_of_start, dtype=np.int32).reshape(B)
+        st_in = None if state is None else np.ascontiguousarray(state, dtype=np.float64).reshape(B, self.STATE_W)
+        p = GicpParams(float(max_correspondence_distance), int(max_iteration), float(relative_fitness),
+                       float(relative_rmse), float(epsilon))
+        T = np.zeros((B, 4, 4))
+        rmse, fit = np.zeros(B), np.zeros(B)
+        iters = np.zeros(B, np.int32)
+        ncorr = np.zeros(B, np.int64)
+        done = np.zeros(B, np.int32)
+        st_out = np.zeros((B, self.STATE_W))
+        ptr = lambda a: None if a is None else a.ctypes.data_as(ctypes.c_void_p)  # noqa: E731
+        self._check(self._L.orpcd_gicp_batch_window(self._h, R0.reshape(-1), t0.reshape(-1), ptr(tids), B,
+                                                    ctypes.byref(p), int(pass_begin), int(pass_end), ptr(st_in),
+                                                    st_out.reshape(-1), done, T.reshape(-1), rmse, fit, iters,
+                                                    ncorr), "orpcd_gicp_batch_window")
+        return dict(T=T, rmse=rmse, fitness=fit, iters=iters, ncorr=ncorr, done=done.astype(bool), state=st_out)
 
     def gicp_correspondences(self, B: int, N: int) -> np.ndarray:
         """(B, N) input index of each source point's nearest target in the
