@@ -1032,7 +1032,7 @@ __device__ __forceinline__ void nn_search_body(
 // group's cost and to the pass total for the next pass's schedule.
 // Waves per workgroup of the ordered dispatch (A/B macro ORPCD_SCHED_WAVES).
 // One: a wave's slot is refilled as soon as it exits, without waiting for
-// three sibling waves of different length (round 5, tools/r5_s1.sh: C2 exact
+// three sibling waves of different length (round 5, profiles/r05_sched_waves_ab.txt: C2 exact
 // 30 starts 15.6 -> 15.2 ms, 64 starts 24.9 -> 24.1 ms, 2 waves per block in
 // between; identical result hashes).
 #ifndef ORPCD_SCHED_WAVES
