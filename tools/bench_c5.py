@@ -34,6 +34,8 @@ def main():
                     help="rows: the row-sharded pass API (a host all-reduce every pass); batch: orpcd_gicp_batch "
                          "with one start (host sync every sync_every passes; bit-identical at one rank); "
                          "auto: batch on one GPU, rows on several")
+    ap.add_argument("--device-collectives", type=int, default=0,
+                    help="rows path: target all-gather and per-pass all-reduce on the library's RCCL communicator")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -41,12 +43,14 @@ def main():
     if world > 1:
         import torch
         import torch.distributed as dist
-        torch.cuda.set_device(int(os.environ.get("LOCAL_RANK", "0")))
-        dist.init_process_group("nccl")
+        # ORPCD_BENCH_BACKEND=gloo / ORPCD_BENCH_DEVICE=0: rehearsal of the multi-rank path on a one-GPU box
+        torch.cuda.set_device(int(os.environ.get("ORPCD_BENCH_DEVICE", os.environ.get("LOCAL_RANK", "0"))))
+        dist.init_process_group(os.environ.get("ORPCD_BENCH_BACKEND", "nccl"))
     from orpcd_amd import _native, parallel
     from workloads import c5_pair
     src, tgt = c5_pair(args.points)
-    ctx = _native.Context()
+    ctx = _native.Context(int(os.environ.get("ORPCD_BENCH_DEVICE", os.environ.get("LOCAL_RANK", "0"))) if world > 1
+                          else None)
     for k, v in json.loads(args.opt).items():
         ctx.set_option(k, v)
     params = dict(max_correspondence_distance=0.5, max_iteration=args.iters)
@@ -62,7 +66,10 @@ def main():
         the call): target and source uploaded, laid out, KNN-20 covariances.
         Returns (target s, source s)."""
         t_0 = time.perf_counter()
-        ctx.set_target(tgt, 1e-3, cache=False)
+        if path == "rows":  # the target's covariance pass split by rows, one all-gather
+            parallel.target_rows_sharded(ctx, tgt, 1e-3, device_collectives=bool(args.device_collectives))
+        else:
+            ctx.set_target(tgt, 1e-3, cache=False)
         t_1 = time.perf_counter()
         if path == "batch":
             ctx.set_source(src, cache=False)
@@ -75,6 +82,10 @@ def main():
 
     def run_rows(prm):
         ctx.shard_begin(np.eye(3), np.zeros(3), n_total=len(src), **prm)
+        if args.device_collectives:
+            parallel.device_comm(ctx)
+            ctx.shard_run()
+            return ctx.shard_result()
         while True:
             sums, act = ctx.shard_pass()
             if not act or ctx.shard_update(parallel.allreduce_sum(sums)):
