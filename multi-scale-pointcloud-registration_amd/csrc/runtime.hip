@@ -494,7 +494,12 @@ int fgr_tuples_device(orpcd_ctx* c, const std::vector<TupleStart>& st, const orp
         double expect = 0.0;
         for (int b = 0; b < B; ++b) {
             TupleJob& J = jobs[b];
-            J.tw = (cnt[b] >= maxc || t0[b] >= J.trials) ? 0 : std::min(kTupleWindow, J.trials - t0[b]);
+            // the first window is short when the tuple limit is small (most
+            // calls reach it within a few hundred trials per tuple): fewer
+            // words drawn, rejections scanned and trials evaluated for nothing
+            const int64_t win = t0[b] == 0 ? std::min<int64_t>(kTupleWindow, std::max<int64_t>(65536, 256 * (int64_t)maxc))
+                                           : kTupleWindow;
+            J.tw = (cnt[b] >= maxc || t0[b] >= J.trials) ? 0 : std::min(win, J.trials - t0[b]);
             J.nrej = 0;
             max_tw = std::max(max_tw, J.tw);
             expect = std::max(expect, 3.0 * (double)J.tw * (double)J.threshold / 4294967296.0);
