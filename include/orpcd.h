@@ -359,10 +359,6 @@ int orpcd_fgr_optimize_batch(orpcd_ctx* ctx, const double* src, int64_t n, const
  *                   at most exact_blocks blocks, exact_fused per running
  *                   start inside the accumulation launch (0: a launch of
  *                   its own before the accumulation)
- *   "solve_tail"    1 (default) / 0: a GeneralizedICP batch's per-start
- *                   reduction, convergence test and 6x6 solve run in the
- *                   accumulation launch (its last block per start) instead
- *                   of a launch of their own; the same results bit for bit
  *   "count_tiles"   1 (default) / 0: while profiling (orpcd_profiling), the
  *                   search also counts the quarters it scans (stats [2], [5]);
  *                   0 keeps only the hipEvent timing (the counters' atomics

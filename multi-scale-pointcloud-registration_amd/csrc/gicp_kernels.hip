@@ -1385,11 +1385,9 @@ __device__ __forceinline__ double wave_sum_fixed(double v) {
 }
 
 // Block reduction of NV per-thread values into partial[slot, block][slot_of(v)].
-// coherent: the partial is stored past this XCD's L2 (agent-scope atomic
-// stores), for a solve tail that reads it in the same launch (SolveTail)
 template <int NV, typename SlotOf>
 __device__ __forceinline__ void block_partial(const double* acc, double (*red)[NV], SlotOf slot_of,
-                                              double* __restrict__ out, bool coherent = false) {
+                                              double* __restrict__ out) {
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
 #pragma unroll
     for (int v = 0; v < NV; ++v) {
@@ -1402,34 +1400,17 @@ __device__ __forceinline__ void block_partial(const double* acc, double (*red)[N
 #pragma unroll
         for (int v = 0; v < NV; ++v)
             if (slot_of(v) == (int)threadIdx.x) s = ((red[0][v] + red[1][v]) + red[2][v]) + red[3][v];
-        if (coherent)
-            __hip_atomic_store(out + threadIdx.x, s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        else
-            out[threadIdx.x] = s;
+        out[threadIdx.x] = s;
     }
 }
 
 // Fixed-order reduction of one start's block partials (lane-strided, then
-// the wave).  coherent: the partials were written in this launch (agent-scope
-// atomic loads: the same sums, read past this XCD's L2).
+// the wave).
 __device__ __forceinline__ void reduce_partials(const double* __restrict__ partial, int slot, int nblk,
-                                                double s[kNacc], bool coherent = false) {
+                                                double s[kNacc]) {
     const int lane = threadIdx.x & 63;
 #pragma unroll
     for (int v = 0; v < kNacc; ++v) s[v] = 0.0;
-    if (coherent) {
-        for (int b = lane; b < nblk; b += 64) {
-            double* pp = const_cast<double*>(partial) + ((size_t)slot * nblk + b) * kPartialStride;
-            double t[kNacc];
-#pragma unroll
-            for (int v = 0; v < kNacc; ++v) t[v] = __hip_atomic_load(pp + v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-#pragma unroll
-            for (int v = 0; v < kNacc; ++v) s[v] += t[v];
-        }
-#pragma unroll
-        for (int v = 0; v < kNacc; ++v) s[v] = wave_sum_fixed(s[v]);
-        return;
-    }
     for (int b = lane; b < nblk; b += 64) {
         const double* pp = partial + ((size_t)slot * nblk + b) * kPartialStride;
         // every 16 B load of the partial issued before the first add: one
@@ -1556,39 +1537,6 @@ __device__ bool solve_start(int slot, const double s[kNacc], int64_t N, int pass
             for (int c = 0; c < 3; ++c) a.R[9 * slot + 3 * r + c] = Tn[4 * r + c];
     }
     return false;
-}
-
-// Solve tail (opt.solve_tail, GeneralizedICP batches): the accumulation
-// launch's last block of a start to finish reduces that start's partials and
-// runs its solve, in place of a launch of icp_solve_kernel after the grid
-// drains -- the same reduction order and solve, so the same bits.  Each block
-// stores its partial past its XCD's L2 (coherent block_partial) and waits for
-// the stores before its agent-scope count; the block that counts last reads
-// the partials with agent-scope loads and resets the count for the next pass.
-struct SolveTail {
-    unsigned* cnt;  // B: the start's blocks counted this pass (null: no tail)
-    SolveArgs a;
-    int64_t N;
-    int pass, max_iter;
-    double rel_fit, rel_rmse;
-};
-
-__device__ __forceinline__ void solve_tail(const SolveTail& t, int slot, const double* __restrict__ partial, int nblk,
-                                           unsigned* last) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");  // this thread's partial store has completed
-    __syncthreads();
-    if (threadIdx.x == 0)
-        *last = __hip_atomic_fetch_add(t.cnt + slot, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
-                (unsigned)nblk - 1u;
-    __syncthreads();
-    if (!*last || threadIdx.x >= 64) return;
-    if (threadIdx.x == 0) __hip_atomic_store(t.cnt + slot, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const double pose = pose_lane_load(slot, t.a);  // written by an earlier launch
-    double s[kNacc];
-    reduce_partials(partial, slot, nblk, s, true);
-    PoseIn pin;
-    pose_from_lanes(pose, pin);
-    solve_start<0>(slot, s, t.N, t.pass, t.max_iter, t.rel_fit, t.rel_rmse, t.a, pin);
 }
 
 // Test entry (orpcd_test_solve6): for each of n systems (21 upper JTJ + 6 JTr),
@@ -1784,29 +1732,26 @@ __device__ __forceinline__ void gicp_block_terms(int slot, int ablk, const doubl
     }
 }
 
-// ORPCD_ACCUM_WAVES: the accumulation's register budget (waves per SIMD).  3:
-// the terms alone fit it (166 VGPRs); the inlined solve tail's uniform
-// values would otherwise push the compiler's choice to 170 VGPRs, 2 waves
-#ifndef ORPCD_ACCUM_WAVES
-#define ORPCD_ACCUM_WAVES 3
-#endif
+// ORPCD_ACCUM_WAVES: a register budget for the accumulation (A/B builds); unset,
+// the compiler's choice (214 VGPRs, 2 waves/SIMD)
+#ifdef ORPCD_ACCUM_WAVES
 #define ORPCD_ACCUM_ATTR __attribute__((amdgpu_waves_per_eu(ORPCD_ACCUM_WAVES, 8)))
+#else
+#define ORPCD_ACCUM_ATTR
+#endif
 __global__ __launch_bounds__(256) ORPCD_ACCUM_ATTR void gicp_accum_kernel(
     const double* __restrict__ src, const double* __restrict__ scov, int N, const TargetDesc* __restrict__ tdesc,
     TgtBounds tb, const int32_t* __restrict__ active, const double* __restrict__ Qm,
     const double* __restrict__ Rm, const int32_t* __restrict__ done, double r2,
     unsigned long long* __restrict__ best, int32_t* __restrict__ prevnn, double* __restrict__ partial,
-    int nblk, double om, SolveTail tail) {
+    int nblk, double om) {
     const int slot = active[blockIdx.y];
     if (done[slot]) return;
     const TargetDesc& tg = tdesc[target_of_row(tb, blockIdx.y)];
     __shared__ double red[4][kNacc];
-    __shared__ unsigned last;
     double acc[kNacc];
     gicp_block_terms(slot, blockIdx.x, src, scov, N, tg.xyz64, tg.tcov, Qm, Rm, r2, best, prevnn, acc, om);
-    block_partial<kNacc>(acc, red, [](int v) { return v; }, partial + ((size_t)slot * nblk + blockIdx.x) * kPartialStride,
-                         tail.cnt != nullptr);
-    if (tail.cnt) solve_tail(tail, slot, partial, nblk, &last);
+    block_partial<kNacc>(acc, red, [](int v) { return v; }, partial + ((size_t)slot * nblk + blockIdx.x) * kPartialStride);
 }
 
 // Exact mode, fused: the re-search of the listed queries and the
@@ -1824,10 +1769,9 @@ __global__ __launch_bounds__(256) ORPCD_ACCUM_ATTR void gicp_accum_exact_kernel(
     TgtBounds tb, const int32_t* __restrict__ active, const double* __restrict__ Qm,
     const double* __restrict__ Rm, const int32_t* __restrict__ done, double r2,
     unsigned long long* __restrict__ best, int32_t* __restrict__ prevnn, double* __restrict__ partial,
-    int nblk, int nexact, const float4* __restrict__ q32, ExactArgs ex, double om, SolveTail tail) {
+    int nblk, int nexact, const float4* __restrict__ q32, ExactArgs ex, double om) {
     __shared__ double red[4][kNacc];
     __shared__ int tlist[4][kExactList];
-    __shared__ unsigned last;
     if ((int)blockIdx.x < nexact) {
         exact_entries<true>(blockIdx.x * 4 + (threadIdx.x >> 6), (unsigned)nexact * 4, src, N, Qm, tdesc, q32, ex,
                             best, tlist[threadIdx.x >> 6]);
@@ -1839,9 +1783,7 @@ __global__ __launch_bounds__(256) ORPCD_ACCUM_ATTR void gicp_accum_exact_kernel(
     const TargetDesc& tg = tdesc[target_of_row(tb, row)];
     double acc[kNacc];
     gicp_block_terms(slot, bx, src, scov, N, tg.xyz64, tg.tcov, Qm, Rm, r2, best, prevnn, acc, om, ex.sec, ex.total);
-    block_partial<kNacc>(acc, red, [](int v) { return v; }, partial + ((size_t)slot * nblk + bx) * kPartialStride,
-                         tail.cnt != nullptr);
-    if (tail.cnt) solve_tail(tail, slot, partial, nblk, &last);
+    block_partial<kNacc>(acc, red, [](int v) { return v; }, partial + ((size_t)slot * nblk + bx) * kPartialStride);
 }
 
 // PointToPoint accumulation (TransformationEstimationPointToPoint, Eigen::
@@ -2278,21 +2220,9 @@ static hipError_t dump_wavetime(int pass, int nact, int S, unsigned n, hipStream
 }
 #endif
 
-bool solve_tail_on(const orpcd_ctx* c) { return c->opt.solve_tail != 0 && c->est != kEstP2P; }
-
 hipError_t launch_gicp_pass(const orpcd_ctx* c, int nact, int pass, double r2, hipStream_t s, hipEvent_t mid,
-                            const TgtBounds& tb, const orpcd_gicp_params* tail_p) {
+                            const TgtBounds& tb) {
     const int N = (int)c->src.n;
-    SolveTail tail{};
-    if (tail_p && solve_tail_on(c)) {
-        tail.cnt = c->tailcnt.p;
-        tail.a = solve_args(c);
-        tail.N = c->src.n;
-        tail.pass = pass;
-        tail.max_iter = tail_p->max_iteration;
-        tail.rel_fit = tail_p->relative_fitness;
-        tail.rel_rmse = tail_p->relative_rmse;
-    }
     const int sblk = (N + kCBlockQ - 1) / kCBlockQ;
     hipError_t e;
     if (c->sched_live) {
@@ -2349,7 +2279,7 @@ hipError_t launch_gicp_pass(const orpcd_ctx* c, int nact, int pass, double r2, h
         const int nexact = std::max(8, std::min(c->opt.exact_blocks, c->opt.exact_fused * nact));
         gicp_accum_exact_kernel<<<(unsigned)(nexact + ablk * nact), 256, 0, s>>>(
             c->src.xyz64.p, c->scov.p, N, c->tdesc.p, tb, c->active.p, c->Q.p, c->R.p, c->done.p, r2, c->best.p,
-            c->prevnn.p, c->partial.p, ablk, nexact, c->q32.p, exact_args(c, pass), 1.0 - c->batch_eps, tail);
+            c->prevnn.p, c->partial.p, ablk, nexact, c->q32.p, exact_args(c, pass), 1.0 - c->batch_eps);
         return launched("gicp_accum_exact_kernel", s);
     }
     if (c->est == kEstP2P) {
@@ -2360,20 +2290,19 @@ hipError_t launch_gicp_pass(const orpcd_ctx* c, int nact, int pass, double r2, h
     }
     gicp_accum_kernel<<<dim3((unsigned)ablk, (unsigned)nact), 256, 0, s>>>(
         c->src.xyz64.p, c->scov.p, N, c->tdesc.p, tb, c->active.p, c->Q.p, c->R.p, c->done.p, r2, c->best.p,
-        c->prevnn.p, c->partial.p, ablk, 1.0 - c->batch_eps, tail);
+        c->prevnn.p, c->partial.p, ablk, 1.0 - c->batch_eps);
     return launched("gicp_accum_kernel", s);
 }
 
 hipError_t launch_gicp_solve(const orpcd_ctx* c, int nact, int pass, const orpcd_gicp_params& p, hipStream_t s,
-                             const TgtBounds& tb, bool tail) {
-    if (!(tail && solve_tail_on(c))) {  // else solved by the accumulation's solve tail
-        const SolveArgs a = solve_args(c);
-        auto solve = c->est == kEstP2P ? icp_solve_kernel<1> : icp_solve_kernel<0>;
-        solve<<<(unsigned)nact, 64, 0, s>>>(c->active.p, c->partial.p, accum_blocks(c->src.n), nullptr, c->src.n,
-                                            pass, p.max_iteration, p.relative_fitness, p.relative_rmse, a);
-        const hipError_t e = launched("icp_solve_kernel", s);
-        if (e != hipSuccess) return e;
-    }
+                             const TgtBounds& tb) {
+    const SolveArgs a = solve_args(c);
+    auto solve = c->est == kEstP2P ? icp_solve_kernel<1> : icp_solve_kernel<0>;
+    solve<<<(unsigned)nact, 64, 0, s>>>(c->active.p, c->partial.p, accum_blocks(c->src.n), nullptr,
+                                                    c->src.n, pass, p.max_iteration, p.relative_fitness,
+                                                    p.relative_rmse, a);
+    hipError_t e = launched("icp_solve_kernel", s);
+    if (e != hipSuccess) return e;
     const double r2 = p.max_correspondence_distance * p.max_correspondence_distance;
     return launch_xform(c, nact, pass + 1, r2, s, tb);  // queries of the next pass (done starts skip)
 }

@@ -545,7 +545,6 @@ struct orpcd_ctx {
     orpcd::DevBuf<double> prev;     // B*2 previous (fitness, rmse)
     orpcd::DevBuf<double> partial;  // B*nblk*32
     orpcd::DevBuf<int32_t> done;    // B
-    orpcd::DevBuf<unsigned> tailcnt;  // B: accumulation blocks counted this pass (SolveTail; zero between passes)
     orpcd::DevBuf<int32_t> active;  // B
     orpcd::DevBuf<double> out_fit, out_rmse;
     orpcd::DevBuf<int32_t> out_iters;
@@ -707,8 +706,6 @@ struct orpcd_ctx {
                                   // hipStreamSynchronize
         int exact_fused = 64;     // > 0: the re-search runs in the accumulation's launch (GICP), this many
                                   // blocks per running start (at most exact_blocks); 0: a launch of its own
-        int solve_tail = 1;       // 1: a GICP batch's solve runs in its accumulation launch (the last block of
-                                  // each start); 0: icp_solve_kernel, a launch of its own
     } opt;
     std::vector<hipEvent_t> ev_pool;
     orpcd::KernelStats stats;
@@ -798,13 +795,10 @@ TgtBounds one_target();
 // bounds of the launch rows act[0..nact) (increasing slots) over the batch's targets
 TgtBounds target_bounds(const orpcd_ctx* c, const int32_t* act, int nact);
 void write_target_desc(const CloudLayout& L, const double* tcov, int seed_reps, bool seed_grid, TargetDesc& d);
-// tail_p != null: the accumulation also solves each start (SolveTail, when
-// solve_tail_on), and launch_gicp_solve(tail = true) only transforms the queries
-bool solve_tail_on(const orpcd_ctx* c);
 hipError_t launch_gicp_pass(const orpcd_ctx* c, int nact, int pass, double r2, hipStream_t s, hipEvent_t mid,
-                            const TgtBounds& tb, const orpcd_gicp_params* tail_p = nullptr);
+                            const TgtBounds& tb);
 hipError_t launch_gicp_solve(const orpcd_ctx* c, int nact, int pass, const orpcd_gicp_params& p, hipStream_t s,
-                             const TgtBounds& tb, bool tail = false);
+                             const TgtBounds& tb);
 hipError_t launch_reduce_partials(const orpcd_ctx* c, int slot, double* sums29, hipStream_t s);
 hipError_t launch_gicp_solve_sums(const orpcd_ctx* c, const double* sums29, int64_t n_total, int pass,
                                   const orpcd_gicp_params& p, hipStream_t s);

@@ -1049,8 +1049,6 @@ int batch_setup(orpcd_ctx* c, const double* R0, const double* t0, int B, const o
         CTX_CHECK(c, hipMemsetAsync(c->wcnt.p, 0, 2 * (size_t)kSchedClasses * 4, c->stream));
     }
     CTX_CHECK(c, c->done.ensure((size_t)B));
-    CTX_CHECK(c, c->tailcnt.ensure((size_t)B));
-    CTX_CHECK(c, hipMemsetAsync(c->tailcnt.p, 0, (size_t)B * 4, c->stream));
     CTX_CHECK(c, c->active.ensure((size_t)B));
     CTX_CHECK(c, c->out_fit.ensure((size_t)B));
     CTX_CHECK(c, c->out_rmse.ensure((size_t)B));
@@ -1647,10 +1645,10 @@ int run_passes(orpcd_ctx* c, int B, const orpcd_gicp_params* p, double* T_out, d
         if (timed) CTX_CHECK(c, hipEventRecord(ev[0], s));
         if (gaps) CTX_CHECK(c, hipEventRecord(ge[0], s));
         const TgtBounds tb = target_bounds(c, hAct, nact);
-        CTX_CHECK(c, launch_gicp_pass(c, nact, pass, r2, s, timed ? ev[1] : (gaps ? ge[1] : nullptr), tb, p));
+        CTX_CHECK(c, launch_gicp_pass(c, nact, pass, r2, s, timed ? ev[1] : (gaps ? ge[1] : nullptr), tb));
         if (trace) CTX_CHECK(c, hipEventRecord(ev[2], s));  // accumulation time: traced runs only
         if (gaps) CTX_CHECK(c, hipEventRecord(ge[2], s));
-        CTX_CHECK(c, launch_gicp_solve(c, nact, pass, *p, s, tb, true));
+        CTX_CHECK(c, launch_gicp_solve(c, nact, pass, *p, s, tb));
         if (gaps) CTX_CHECK(c, hipEventRecord(ge[3], s));
         c->stats.host_launch_ms += ms_since(tl);
         ++pending;
@@ -2690,7 +2688,6 @@ int orpcd_set_option(orpcd_ctx* c, const char* key, double value) {
     else if (k == "exact_nn" && (v == 0 || v == 1)) c->opt.exact_nn = v;
     else if (k == "exact_blocks" && v >= 1 && v <= 65536) c->opt.exact_blocks = v;
     else if (k == "exact_fused" && v >= 0 && v <= 4096) c->opt.exact_fused = v;
-    else if (k == "solve_tail" && (v == 0 || v == 1)) c->opt.solve_tail = v;
     else if (k == "count_tiles" && (v == 0 || v == 1)) c->opt.count_tiles = v;
     else if (k == "sync_poll" && (v == 0 || v == 1)) c->opt.sync_poll = v;
     else {

@@ -85,35 +85,3 @@ def test_sched_many_groups_single_start(ctx):
     ref = _run(ctx, {"sched": 0}, lambda: ctx.gicp_batch(R0, t0, max_iteration=6))
     got = _run(ctx, {"sched": 1, "sched_min_starts": 1}, lambda: ctx.gicp_batch(R0, t0, max_iteration=6))
     _same(got, ref)
-
-
-@pytest.mark.parametrize("exact_nn", [1, 0])
-def test_solve_tail_matches_solve_launch(ctx, exact_nn):
-    """The solve run by each start's last accumulation block (opt
-    "solve_tail", default) against icp_solve_kernel's launch of its own: the
-    same partials in the same order through the same solve, so bit-identical
-    results -- including starts finishing at different passes, the maximum
-    iteration reached, and a batch of one start."""
-    src, tgt = small_pair(6000, 5500, seed=43)
-    rng = np.random.default_rng(14)
-    R0 = np.array([rot_xyz(*rng.uniform(-90, 90, 3)) for _ in range(24)])
-    t0 = rng.normal(size=(24, 3)) * 0.1
-    ctx.set_target(tgt)
-    ctx.set_source(src)
-
-    def run():
-        return [ctx.gicp_batch(R0, t0), ctx.gicp_batch(R0[:5], t0[:5], max_iteration=7),
-                ctx.gicp_batch(R0[:1], t0[:1])]
-
-    ctx.set_option("exact_nn", exact_nn)
-    try:
-        ctx.set_option("solve_tail", 0)
-        ref = run()
-        ctx.set_option("solve_tail", 1)
-        got = run()
-        assert len(set(got[0]["iters"].tolist())) > 3
-        for g, r in zip(got, ref):
-            _same(g, r)
-    finally:
-        ctx.set_option("exact_nn", 1)
-        ctx.set_option("solve_tail", 1)
