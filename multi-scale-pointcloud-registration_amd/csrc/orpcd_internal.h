@@ -678,7 +678,8 @@ struct orpcd_ctx {
     struct Options {
         int search_waves = 32768;  // split a start's tiles until ~this many waves run (A/B: tools/ab_search.py)
         int small_batch = 8;      // at most this many running starts: half the search_waves target
-        int sync_every = 8;       // passes between host checks of the done flags (C2 sweep: 4 17.6 ms, 8-16 17.3)
+        int sync_every = 16;      // passes between host checks of the done flags (round 5 sweep, C2 batches of
+                                  // 1/8/30/64 starts, 8 -> 16: -2/+0.3/-1.2/-0.6 %; r05_sync_every_ab.txt)
         int super_cull = 1;       // first culling level over 64-tile super-tiles
         int reseed = 0;           // representative seeding also after pass 0
         int seed_reps = 64;       // pass-0 seed without a seed grid: nearest of ~this many tile representatives

@@ -240,7 +240,7 @@ def test_sync_interval_identical(ctx, every):
         got, gidx = run(every)
         ref, ridx = run(64)
     finally:
-        ctx.set_option("sync_every", 8)
+        ctx.set_option("sync_every", 16)  # the default
         ctx.set_option("exact_nn", 1)
     assert len(set(got[0]["iters"].tolist())) > 5
     assert (got[1]["iters"] == 7).any()
