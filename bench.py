@@ -53,7 +53,9 @@ FLOP_PER_PAIR = 8           # 3 sub + 3 mul/fma(=5) per query-target distance (S
 
 def parse():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="ranks (one process per GPU); N > 1 without WORLD_SIZE spawns the N rank processes "
+                         "itself (default: WORLD_SIZE when launched by torch.distributed.run, else 1)")
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--points", type=int, default=50_000)
@@ -67,38 +69,113 @@ def parse():
     return ap.parse_args()
 
 
+def _free_port():
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_ranks(n):
+    """`--gpus N` (N > 1) started without a launcher: start the N rank
+    processes here, one per GPU (RANK = LOCAL_RANK = r, WORLD_SIZE = N,
+    rendezvous on 127.0.0.1), exactly as `python -m torch.distributed.run
+    --nproc-per-node N bench.py --gpus N ...` would.  This parent never
+    imports torch or touches a GPU; it forwards nothing but waits, and exits
+    with the first non-zero rank status (the other ranks are then stopped), so
+    a failed rank fails the run.  Rank 0 prints the JSON line."""
+    import signal
+    import subprocess
+    port = os.environ.get("MASTER_PORT") or str(_free_port())
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=port)
+        procs.append(subprocess.Popen([sys.executable, "-u", os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    status = 0
+    live = list(procs)
+    while live:
+        for p in list(live):
+            rc = p.poll()
+            if rc is None:
+                continue
+            live.remove(p)
+            if rc != 0 and status == 0:
+                status = rc if rc > 0 else 128 - rc
+                print(f"bench.py: rank {procs.index(p)} exited with {rc}; stopping the other ranks",
+                      file=sys.stderr, flush=True)
+                for q in live:
+                    q.send_signal(signal.SIGTERM)
+        if live:
+            time.sleep(0.05)
+    return status
+
+
+def _bench_optimizer(device):
+    """The optimizer the bench drives: the build's GeneralizedICP (HIP) -- or,
+    for the CPU rehearsal of the multi-rank launch only (tests/test_bench_launch.py),
+    the class named by ORPCD_BENCH_OPTIMIZER="file.py:Class", which must
+    provide the same optimize_batch / context surface."""
+    spec = os.environ.get("ORPCD_BENCH_OPTIMIZER")
+    if not spec:
+        from orpcd_amd import GeneralizedICP
+        return GeneralizedICP(device=device)
+    import importlib.util
+    path, cls = spec.rsplit(":", 1)
+    m = importlib.util.spec_from_file_location("orpcd_bench_optimizer", path)
+    mod = importlib.util.module_from_spec(m)
+    m.loader.exec_module(mod)
+    return getattr(mod, cls)(device=device)
+
+
 def main():
     args = parse()
-    world = int(os.environ.get("WORLD_SIZE", "1"))
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None and args.gpus is not None and args.gpus > 1:
+        sys.exit(launch_ranks(args.gpus))
+    world = int(env_world or "1")
+    if args.gpus is not None and args.gpus != world:
+        print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}: launch one rank per GPU "
+              f"(--nproc-per-node {args.gpus}) or drop --gpus", file=sys.stderr)
+        sys.exit(2)
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    # ORPCD_BENCH_BACKEND=gloo / ORPCD_BENCH_DEVICE=0: rehearsal of the
+    # multi-rank path on a one-GPU box (production: nccl = RCCL, GPU = LOCAL_RANK)
+    device = int(os.environ.get("ORPCD_BENCH_DEVICE", local_rank))
+    on_gpu = not os.environ.get("ORPCD_BENCH_OPTIMIZER")
     dist = None
     if world > 1:
         import torch
         import torch.distributed as dist
 
-        # ORPCD_BENCH_BACKEND=gloo / ORPCD_BENCH_DEVICE=0: rehearsal of the
-        # multi-rank path on a one-GPU box (production: nccl = RCCL, GPU = LOCAL_RANK)
-        local_rank = int(os.environ.get("ORPCD_BENCH_DEVICE", local_rank))
-        torch.cuda.set_device(local_rank)
+        if on_gpu:
+            torch.cuda.set_device(device)
         dist.init_process_group(os.environ.get("ORPCD_BENCH_BACKEND", "nccl"), init_method="env://")
 
-    from orpcd_amd import Aligner, GeneralizedICP, Preprocessor
+    from orpcd_amd import Aligner, Preprocessor
     from workloads import c2_pair
 
     src_raw, tgt_raw = c2_pair(args.points)
     source = Preprocessor([]).preprocess(src_raw)
     target = Preprocessor([]).preprocess(tgt_raw)
 
-    opt = GeneralizedICP(device=local_rank)
+    opt = _bench_optimizer(device)
     ctx = opt.context
+    devices = [device]
+    if dist is not None:
+        devices = [None] * world
+        dist.all_gather_object(devices, device)
     total_attempts = args.attempts * world
     aligner = Aligner(Preprocessor([]), Preprocessor([]), opt, attempts=total_attempts)
 
     def barrier():
         if dist is not None:
             import torch
-            torch.cuda.synchronize()
+            if on_gpu:
+                torch.cuda.synchronize()
             dist.barrier()
 
     def step(k, al=aligner):
@@ -166,7 +243,7 @@ def main():
     parity = None
     fast = None
     setup = None
-    if rank == 0 and world == 1:
+    if rank == 0 and world == 1 and on_gpu:
         setup = setup_inclusive_run(ctx, step, args)
         o = o_iters = None
         if args.cpu_seconds > 0:
@@ -208,6 +285,7 @@ def main():
             "value": round(value, 3),
             "unit": "GICP iterations/s",
             "n_gpus": world,
+            "devices": devices,
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(elapsed / args.steps * 1e3, 3),

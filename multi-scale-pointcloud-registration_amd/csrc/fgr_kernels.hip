@@ -1056,7 +1056,6 @@ hipError_t launch_feat_nn(const double* Fq, const double* nq2, int64_t nq, const
     if (timing) {
         timing[0] += ms1;
         timing[2] += (double)nq * (double)nt;
-        timing[3] += (double)nflag * (double)nt;
         timing[4] += 1;
     }
     if (nflag == 0) return hipSuccess;
@@ -1081,37 +1080,28 @@ hipError_t launch_feat_nn(const double* Fq, const double* nq2, int64_t nq, const
         if ((e = hipEventSynchronize(b.ev[3])) != hipSuccess) return e;
         if ((e = hipEventElapsedTime(&ms2, b.ev[2], b.ev[3])) != hipSuccess) return e;
         timing[1] += ms2;
+        // the pairs pass 2 evaluates: a block's real rows x its sub-part's
+        // targets, for the (block, sub-part) tiles the need masks do not skip
+        // (the kernel's own skip rule, over the sorted masks)
+        std::vector<uint32_t> nk((size_t)nflag);
+        if ((e = d2h(nk.data(), b.nkey.p + nq, (size_t)nflag * 4, s)) != hipSuccess) return e;
+        if ((e = hipStreamSynchronize(s)) != hipSuccess) return e;
+        double pairs2 = 0.0;
+        for (int y = 0; y < parts2; ++y) {
+            const int t_begin = y * len2, t_end = (int)std::min<int64_t>(nt, (int64_t)t_begin + len2);
+            if (t_begin >= t_end) continue;
+            const int p_lo = t_begin / len1, p_hi = (t_end - 1) / len1;
+            const uint32_t range = (p_hi >= 31 ? 0xFFFFFFFFu : ((1u << (p_hi + 1)) - 1u)) & ~((1u << p_lo) - 1u);
+            for (int r0 = 0; r0 < nflag; r0 += 256) {
+                const int r1 = std::min(nflag, r0 + 256);
+                bool run = false;
+                for (int j = r0; j < r1 && !run; ++j) run = (nk[(size_t)j] & range) != 0;
+                if (run) pairs2 += (double)(r1 - r0) * (double)(t_end - t_begin);
+            }
+        }
+        timing[3] += pairs2;
     }
     merge_exact_kernel<<<g2, 256, 0, s>>>(b.part_d.p, b.part_i.p, (int)nq, parts2, b.qsort.p, nsel, tmap, out);
-    return hipGetLastError();
-}
-
-// Answers of duplicate rows from their representatives' (dedup_rows' runs:
-// sorted position p holds row vs[p]; a row that is not its own
-// representative (uflag 0) equals the row at its run head).
-__global__ void unique_pos_kernel(const int32_t* __restrict__ uidx, int nu, int32_t* __restrict__ pos) {
-    const int k = blockIdx.x * blockDim.x + threadIdx.x;
-    if (k < nu) pos[uidx[k]] = k;
-}
-
-__global__ void expand_dup_kernel(const int32_t* __restrict__ vs, const int32_t* __restrict__ head,
-                                  const unsigned char* __restrict__ uflag, int n, const int32_t* __restrict__ pos,
-                                  const int32_t* __restrict__ out_u, int32_t* __restrict__ out) {
-    const int p = blockIdx.x * blockDim.x + threadIdx.x;
-    if (p >= n) return;
-    const int i = vs[p];
-    const int r = uflag[i] ? i : vs[head[p]];
-    out[i] = out_u[pos[r]];
-}
-
-hipError_t expand_dup_answers(const DedupBufs& b, int64_t n, int64_t nu, const int32_t* out_u, int32_t* pos,
-                              int32_t* out, hipStream_t s) {
-    if (n <= 0) return hipSuccess;
-    unique_pos_kernel<<<(unsigned)((nu + 255) / 256), 256, 0, s>>>(b.uidx.p, (int)nu, pos);
-    hipError_t e = hipGetLastError();
-    if (e != hipSuccess) return e;
-    expand_dup_kernel<<<(unsigned)((n + 255) / 256), 256, 0, s>>>(b.val.p + n, b.head.p, b.uflag.p, (int)n, pos,
-                                                                  out_u, out);
     return hipGetLastError();
 }
 

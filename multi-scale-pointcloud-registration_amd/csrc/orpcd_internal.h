@@ -588,7 +588,7 @@ struct orpcd_ctx {
         orpcd::DevBuf<double> feat[2];    // n x 36 padded features
         orpcd::DevBuf<double> fn2[2];     // |f|^2
         orpcd::DevBuf<double> nrm, raw, nd2, spfh, red, pq, Tn;
-        orpcd::DevBuf<int32_t> nbr, cnt, nn[2], dpos;
+        orpcd::DevBuf<int32_t> nbr, cnt, nn[2];
         orpcd::DedupBufs dedup;
         orpcd::FeatNNBufs fnn;
         // orpcd_fgr_optimize_batch: the batch's posed sources (B x n x 3) and
@@ -823,10 +823,6 @@ hipError_t launch_feat_nn(const double* Fq, const double* nq2, int64_t nq, const
 // Representatives (lowest index) of the distinct rows of F (n x 36): b.uidx
 // (increasing), b.Fu / b.n2u their rows and norms; *nu_out their count.
 hipError_t dedup_rows(const double* F, const double* n2, int64_t n, DedupBufs& b, int64_t* nu_out, hipStream_t s);
-// out[i] = out_u[position of row i's representative in b.uidx] for the n rows
-// b was built from (pos: n ints of scratch)
-hipError_t expand_dup_answers(const DedupBufs& b, int64_t n, int64_t nu, const int32_t* out_u, int32_t* pos,
-                              int32_t* out, hipStream_t s);
 hipError_t launch_fgr_irls(const double* p, double* q, int K, double par0, int iters, double division_factor,
                            double max_corr, int decrease_mu, double* T_out, hipStream_t s);
 // several IRLS problems in one launch each for the register- and the

@@ -621,6 +621,24 @@ int fgr_match(orpcd_ctx* c, const double* fsrc, int64_t n, const double* ftgt, i
     int fi = 0, fj = 1;
     if (np[1] > np[0]) std::swap(fi, fj);
     const int64_t nPti = np[fi], nPtj = np[fj];
+    if (same_features) {
+        // the two sets are the same rows (n == m): every row's nearest feature
+        // row is the lowest index of its exact duplicates (distance 0; any
+        // other row is strictly farther), in both directions, so the mutual
+        // pairs are (i, i) for the rows that are their own representative --
+        // the answer both exact searches would return (the batch path's Q4
+        // rule, orpcd_fgr_optimize_batch).  No search runs.
+        corres.clear();
+        CTX_CHECK(c, F.dedup.uflag.ensure((size_t)nPti));
+        CTX_CHECK(c, dedup_flags(feat[fi], nPti, F.dedup, F.dedup.uflag.p, s, 1));
+        std::vector<unsigned char> fl((size_t)nPti);
+        CTX_CHECK(c, d2h(fl.data(), F.dedup.uflag.p, fl.size(), s));
+        CTX_CHECK(c, hipStreamSynchronize(s));
+        for (int64_t i = 0; i < nPti; ++i)
+            if (fl[(size_t)i]) corres.push_back({(int)i, (int)i});
+        fgr_mark(s, "feature matching (same rows)");
+        return ORPCD_OK;
+    }
     for (int k = 0; k < 2; ++k) {
         CTX_CHECK(c, F.fn2[k].ensure((size_t)np[k]));
         CTX_CHECK(c, launch_feat_norm(feat[k], np[k], F.fn2[k].p, s));
@@ -629,23 +647,11 @@ int fgr_match(orpcd_ctx* c, const double* fsrc, int64_t n, const double* ftgt, i
     CTX_CHECK(c, F.nn[1].ensure((size_t)nPti));
     int64_t nu = 0;
     CTX_CHECK(c, dedup_rows(feat[fi], F.fn2[fi].p, nPti, F.dedup, &nu, s));
-    if (same_features) {
-        // the second direction is the first one's problem input for input,
-        // and identical query rows have identical answers, so one search
-        // runs, over the distinct rows against themselves (F.nn[1] as its
-        // output), and every row takes its representative's answer
-        CTX_CHECK(c, F.dpos.ensure((size_t)nPti));
-        CTX_CHECK(c, launch_feat_nn(F.dedup.Fu.p, F.dedup.n2u.p, nu, F.dedup.Fu.p, F.dedup.n2u.p, nu, F.dedup.uidx.p,
-                                    33, F.fnn, F.nn[1].p, s, c->profiling ? c->stats.feat : nullptr));
-        CTX_CHECK(c, expand_dup_answers(F.dedup, nPti, nu, F.nn[1].p, F.dpos.p, F.nn[0].p, s));
-        CTX_CHECK(c, hipMemcpyAsync(F.nn[1].p, F.nn[0].p, (size_t)nPti * 4, hipMemcpyDeviceToDevice, s));
-    } else {
-        CTX_CHECK(c, launch_feat_nn(feat[fj], F.fn2[fj].p, nPtj, F.dedup.Fu.p, F.dedup.n2u.p, nu, F.dedup.uidx.p, 33,
-                                    F.fnn, F.nn[0].p, s, c->profiling ? c->stats.feat : nullptr));
-        CTX_CHECK(c, dedup_rows(feat[fj], F.fn2[fj].p, nPtj, F.dedup, &nu, s));
-        CTX_CHECK(c, launch_feat_nn(feat[fi], F.fn2[fi].p, nPti, F.dedup.Fu.p, F.dedup.n2u.p, nu, F.dedup.uidx.p, 33,
-                                    F.fnn, F.nn[1].p, s, c->profiling ? c->stats.feat : nullptr));
-    }
+    CTX_CHECK(c, launch_feat_nn(feat[fj], F.fn2[fj].p, nPtj, F.dedup.Fu.p, F.dedup.n2u.p, nu, F.dedup.uidx.p, 33,
+                                F.fnn, F.nn[0].p, s, c->profiling ? c->stats.feat : nullptr));
+    CTX_CHECK(c, dedup_rows(feat[fj], F.fn2[fj].p, nPtj, F.dedup, &nu, s));
+    CTX_CHECK(c, launch_feat_nn(feat[fi], F.fn2[fi].p, nPti, F.dedup.Fu.p, F.dedup.n2u.p, nu, F.dedup.uidx.p, 33,
+                                F.fnn, F.nn[1].p, s, c->profiling ? c->stats.feat : nullptr));
     fgr_mark(s, "feature matching");
     std::vector<int32_t> j_to_i((size_t)nPtj), i_to_j((size_t)nPti);
     CTX_CHECK(c, d2h(j_to_i.data(), F.nn[0].p, (size_t)nPtj * 4, s));
@@ -949,7 +955,7 @@ void tie_posed_rows(const orpcd_ctx::SourceTies& T, int b, const double* R0, con
 
 // Slot-ordered starts (R0 row-major: source @ R0 + t0): every tie's
 // covariance re-decided per start, written over the rotated one in c->scov.
-int source_ties_apply(orpcd_ctx* c, const double* R0, const double* t0, int B, double eps) {
+int source_ties_apply(orpcd_ctx* c, const double* R0, const double* t0, int B, double eps, bool count_gaps) {
     auto& T = c->ties;
     T.last_sets.clear();
     if (T.on) {
@@ -958,8 +964,10 @@ int source_ties_apply(orpcd_ctx* c, const double* R0, const double* t0, int B, d
         // (kTieCap / the brute-force budget), or the posed copy's coordinates
         // exceed what the band's absolute term assumes: posing rounds a
         // coordinate by ~u |x R0 + t0| <= u (sqrt(3) A + |t0|), and kTieAbs
-        // (1 + A) holds ~2000x that for |x R0 + t0| <= 1000 (1 + A)
-        for (int b = 0; b < B; ++b) {
+        // (1 + A) holds ~2000x that for |x R0 + t0| <= 1000 (1 + A).  A start
+        // is counted once: when it begins (pass 0), not again when a pass
+        // window resumes it
+        for (int b = 0; b < B && count_gaps; ++b) {
             double tb = 0.0;
             for (int k = 0; k < 3; ++k) tb = std::max(tb, std::fabs(t0[3 * b + k]));
             if (!T.complete || std::sqrt(3.0) * T.band_A + tb > 1000.0 * (1.0 + T.band_A)) c->stats.tie_gaps += 1;
@@ -1128,7 +1136,7 @@ int batch_setup(orpcd_ctx* c, const double* R0, const double* t0, int B, const o
         CTX_CHECK(c, launch_normals_cov(c->sraw.p, N, c->scratch64c.p, B, p->epsilon, nullptr,
                                         ORPCD_NORMAL_COV ? nullptr : c->scov.p, s,
                                         ORPCD_NORMAL_COV ? c->scov.p : nullptr));
-        int rc = source_ties_apply(c, R0, t0, B, p->epsilon);  // boundary ties decided on the posed copies
+        int rc = source_ties_apply(c, R0, t0, B, p->epsilon, pass_begin == 0);  // boundary ties decided on the posed copies
         if (rc) return rc;
     }
     if (getenv("ORPCD_SYNC_LAUNCH")) {  // debugging: the set-up's kernels, apart from the pass loop's
@@ -1355,8 +1363,6 @@ int orpcd_gicp_batch_window(orpcd_ctx* c, const double* R0, const double* t0, co
                             const double* state_in, double* state_out, int32_t* done_out, double* T_out,
                             double* rmse_out, double* fitness_out, int32_t* iters_out, int64_t* ncorr_out) {
     if (!c) return ORPCD_EINVAL;
-    CTX_REQUIRE(c, pass_begin >= 0 && pass_end > pass_begin && (pass_begin == 0 || state_in),
-                "gicp_batch_window: bad pass window (pass_begin > 0 needs state_in)");
     // the caller's posed tie rows (orpcd_set_posed_tie_rows) belong to this
     // call only: taken before any validation, so a rejected batch never
     // leaves them for the next one
@@ -1366,6 +1372,8 @@ int orpcd_gicp_batch_window(orpcd_ctx* c, const double* R0, const double* t0, co
     const int posed_B = TS.posed_B;
     TS.posed_B = 0;
     TS.posed_slot.clear();
+    CTX_REQUIRE(c, pass_begin >= 0 && pass_end > pass_begin && (pass_begin == 0 || state_in),
+                "gicp_batch_window: bad pass window (pass_begin > 0 needs state_in)");
     CTX_REQUIRE(c, R0 && t0 && p && T_out && rmse_out, "gicp_batch: null argument");
     CTX_REQUIRE(c, B > 0, "gicp_batch: B must be > 0");
     CTX_REQUIRE(c, c->src.n > 0, "gicp_batch: no source (call orpcd_set_source)");

@@ -6,10 +6,15 @@ feature_matching``).  Same constructor, defaults, validation (log + fall back
 to the default), R-transposed return (:176-178) and ``Warning`` raised when
 the evaluation finds no correspondence (:181-188).
 
-One call = one ``orpcd_fgr_optimize``: FPFH of both clouds, the fp64-MFMA
-mutual feature matching, the tuple test, the GNC IRLS and the evaluation all
-run against device-resident clouds; only the tuple test's sequential
-mt19937 draws run on the host.
+One call = one ``orpcd_fgr_optimize``: FPFH of both clouds, the mutual
+feature matching, the tuple test, the GNC IRLS and the evaluation all run
+against device-resident clouds.  The tuple test's mt19937 word stream is
+generated on the host; every trial is evaluated and the accepted tuples
+selected on the device.  Matching: with each cloud's own features it is the
+fp64-MFMA 33-D nearest-row search in both directions; under Q4 on equal-size
+clouds the two feature sets are the same rows, so every row's nearest row is
+the lowest index of its exact duplicates and the mutual pairs come from the
+dedup pass alone (no search).
 
 Quirk Q4 (fastGlobalOptimizer.py:137-142): the reference computes the TARGET
 features from the SOURCE cloud.  ``target_features_from_source=True`` (the
@@ -23,8 +28,8 @@ build's ``Aligner`` uses (as for GeneralizedICP): all attempts of a
 multistart, or of the speculative compass's candidate scales, run as ONE
 ``orpcd_fgr_optimize_batch`` call -- per start the same normals, FPFH,
 matching, tuple test, IRLS and evaluation as ``optimize`` on the posed copy
-``source @ R0 + t0``, bit for bit, with the IRLS problems of all starts in
-one launch and the tuple tests on host threads.
+``source @ R0 + t0``, bit for bit, with the tuple tests of all starts and
+the IRLS problems of all starts each in one device launch.
 
 ``seed`` seeds the tuple test's mt19937.  Open3D draws it from its global
 engine, which is not seeded by the reference, so the reference's FGR result

@@ -133,9 +133,12 @@ class GeneralizedICP(IOptimizer):
         return R, t
 
     def _note_tie_gaps(self, ctx):
-        """Warn once per new gap: starts whose source boundary ties could not
-        all be re-decided from their posed copy (orpcd_stats [19]); their
-        covariances keep the rotated unposed ones (parity unpinned there)."""
+        """Warn about starts whose source boundary ties could not all be
+        re-decided from their posed copy (orpcd_stats [19]); their covariances
+        keep the rotated unposed ones (parity unpinned there).  One warning per
+        source cloud (a source whose tie table overflowed would otherwise warn
+        on every multistart); later gaps of the same source are logged at
+        debug level and still counted in spec_stats["tie_gaps"]."""
         stats = getattr(ctx, "stats", None)  # a stand-in context (tests) may not count
         if stats is None:
             return
@@ -143,8 +146,16 @@ class GeneralizedICP(IOptimizer):
         if g < self._tie_gaps_seen:  # the context's statistics were reset
             self._tie_gaps_seen = 0
         if g > self._tie_gaps_seen:
-            self._LOG.warning(f"{g - self._tie_gaps_seen} GICP start(s) with source KNN-20 boundary ties not "
-                              "re-decided per pose (tie table full or pose far outside the cloud's extent)")
+            new = g - self._tie_gaps_seen
+            self.spec_stats["tie_gaps"] = self.spec_stats.get("tie_gaps", 0) + new
+            source = getattr(ctx, "_source_key", None)
+            msg = (f"{new} GICP start(s) with source KNN-20 boundary ties not re-decided per pose "
+                   "(tie table full or pose far outside the cloud's extent)")
+            if source is None or source != getattr(self, "_tie_gap_source", None):
+                self._LOG.warning(msg + "; further gaps of this source are logged at debug level")
+                self._tie_gap_source = source
+            else:
+                self._LOG.debug(msg)
         self._tie_gaps_seen = g
 
     def _base_ties(self, ctx):

@@ -15,18 +15,34 @@ class FakeShardContext:
         self.tgt = np.ascontiguousarray(target, dtype=np.float64)
         self.tcov = oracle.estimate_normals(self.tgt, 20, -1.0, epsilon)[2]
 
-    # the target's covariance pass by rows (orpcd_set_target_rows): the fake's
-    # rows are input rows; a rank keeps its slice only until set_target_cov
+    # the target's covariance pass by rows (orpcd_set_target_rows), with the
+    # library's slicing: blocks of target_slice(m, n) rows (a multiple of the
+    # 64-row tile), rank r's block at r * slice, the in-place all-gather into
+    # a buffer of slice * n rows whose first m rows are the target's.  The
+    # fake's rows are input rows (the library's are Morton rows); a rank keeps
+    # its slice only until set_target_cov
+    TILE = 64
+
+    @classmethod
+    def target_slice(cls, m, nranks):
+        return -(-(-(-m // nranks)) // cls.TILE) * cls.TILE
+
     def set_target_rows(self, target, rank, nranks, epsilon):
         self.tgt = np.ascontiguousarray(target, dtype=np.float64)
         m = len(self.tgt)
-        slice_ = -(-m // nranks)
-        lo, hi = min(m, rank * slice_), min(m, rank * slice_ + slice_)
+        sl = self.target_slice(m, nranks)
+        lo, hi = min(m, rank * sl), min(m, rank * sl + sl)
         self.tcov = np.full((m, 3, 3), np.nan)
         self.tcov[lo:hi] = oracle.estimate_normals(self.tgt, 20, -1.0, epsilon)[2][lo:hi]
         if getattr(self, "comm", None) and self.comm[0] == nranks:  # the device all-gather, over the group
             from orpcd_amd import parallel
-            self.set_target_cov(np.concatenate(parallel.allgather_arrays(self.target_cov_rows(lo, hi))))
+            send = np.full((sl, 9), np.nan)                # this rank's block of the gather buffer
+            send[: hi - lo] = self.tcov[lo:hi].reshape(hi - lo, 9)
+            blocks = parallel.allgather_arrays(send)
+            assert all(b.shape == (sl, 9) for b in blocks)
+            gathered = np.concatenate(blocks)              # slice * nranks rows, block r at r * slice
+            assert len(gathered) == sl * nranks >= m and not np.isnan(gathered[:m]).any()
+            self.set_target_cov(gathered[:m])
         return lo, hi
 
     def target_cov_rows(self, lo, hi):

@@ -6,7 +6,7 @@ CPU oracle:
   Q4 target features from the source; fastGlobalOptimizer.py:23-34,
   :137-142, :158-174).  Gate: the same mutual-match and tuple counts (so the
   same tuples), T elementwise <= 1e-9, inlier RMSE <= 1e-9 relative, the same
-  inlier count.
+  inlier count.  Also with each cloud's own features (the 33-D contraction).
 * C4 (configs[3]): the C2 pair with attempts=64, sharded over 8 ranks in
   contiguous blocks of 8 starts (parallel.shard, Aligner.py:178-202).  A
   start's result never depends on its batch mates, so every rank's block run
@@ -44,6 +44,29 @@ def test_c3_fgr_defaults_match_oracle(ctx, oracle):
     To[:3, :3] = To[:3, :3].T                          # the plugin's row convention (Q1)
     assert np.abs(T - To).max() <= 1e-9 and rmse == g["rmse"]
     print(f"C3: n_mutual {g['n_mutual']} tuples {g['n_tuple_corr']} rmse {rmse:.9g} "
+          f"|dT| {np.abs(g['T'] - o['T']).max():.1e}")
+
+
+def test_c3_fgr_own_features_match_oracle(ctx, oracle):
+    """C3 with each cloud's OWN FPFH (target_features_from_source=False, the
+    evidently intended fastGlobalOptimizer.py:130-142 behaviour): the genuine
+    100k x 100k 33-D feature contraction on the matrix cores, both directions.
+    Gate: the oracle's mutual and tuple counts, T <= 1e-9, the same inliers."""
+    from orpcd_amd import FastGlobalOptimizer
+    from workloads import c3_pair
+    src, tgt = c3_pair(100_000)
+    src, tgt = _radius_scale(src), _radius_scale(tgt)
+    opt = FastGlobalOptimizer(seed=0, target_features_from_source=False)
+    T, rmse = opt.optimize(src, tgt)
+    g = opt.last_result
+    _, fs = oracle.fpfh(src, 0.1, 20, 0.1, 20)
+    _, ft = oracle.fpfh(tgt, 0.1, 20, 0.1, 20)
+    o = oracle.fgr(src, tgt, fs, ft, seed=0)
+    assert g["n_mutual"] == o["n_mutual"] and g["n_tuple_corr"] == o["n_tuple_corr"], (g, o)
+    assert np.abs(g["T"] - o["T"]).max() <= 1e-9, np.abs(g["T"] - o["T"]).max()
+    assert g["ncorr"] == o["ncorr"]
+    assert abs(g["rmse"] - o["rmse"]) <= 1e-9 * o["rmse"] + 1e-15
+    print(f"C3 own features: n_mutual {g['n_mutual']} tuples {g['n_tuple_corr']} rmse {rmse:.9g} "
           f"|dT| {np.abs(g['T'] - o['T']).max():.1e}")
 
 

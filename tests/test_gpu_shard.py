@@ -129,6 +129,7 @@ def test_target_rows_emulated_ranks_assemble_the_full_target(lane_min):
     which a GICP batch returns the same bits; an incomplete target is refused
     by the GICP calls; one rank alone is complete at once."""
     from orpcd_amd import _native
+    from shard_fake import FakeShardContext
     src, tgt = _pair()
     full = _native.Context(0)
     full.set_option("knn_lane_min", lane_min)
@@ -140,6 +141,8 @@ def test_target_rows_emulated_ranks_assemble_the_full_target(lane_min):
         c.set_option("knn_lane_min", lane_min)
         lo, hi = c.set_target_rows(tgt, r, 3, 1e-3)
         assert lo % 64 == 0 and (hi % 64 == 0 or hi == len(tgt))
+        sl = FakeShardContext.target_slice(len(tgt), 3)    # the layout the CPU gloo tests' fake uses
+        assert (lo, hi) == (min(len(tgt), r * sl), min(len(tgt), r * sl + sl))
         rows.append((lo, hi))
         parts.append(c.target_cov_rows(lo, hi))
         assert np.array_equal(parts[-1], want[lo:hi])

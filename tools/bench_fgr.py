@@ -2,12 +2,15 @@
 
     python tools/bench_fgr.py [--points 100000] [--repeat 5] [--cpu 1] [--out profiles/r01_fgr_c3.json]
 
-Times the build's plugin (FPFH of both clouds + fp64-MFMA mutual matching +
-tuple test + GNC IRLS + evaluation, one orpcd_fgr_optimize call) with inputs
-on the host, as the Aligner hands them over, and the feature-NN kernel alone
-with HIP events per pass (orpcd_profiling / orpcd_stats) for its roofline:
-2*33 FLOP per query-target pair over the pairs pass 1
-evaluates, priced against the fp64 matrix peak.  The CPU oracle (same seed, same Q4 choice) is timed once on the host
+Times the build's plugin (FPFH of both clouds + mutual matching + tuple test
++ GNC IRLS + evaluation, one orpcd_fgr_optimize call) with inputs on the host,
+as the Aligner hands them over: the C3 default (Q4: no feature search, the
+mutual pairs come from the dedup pass) and the own-features path
+(target_features_from_source=False: two fp64-MFMA 33-D searches per call).
+The feature-NN roofline is taken on the own-features path with HIP events per
+pass (orpcd_profiling / orpcd_stats): 2*33 FLOP per query-target pair
+ over the pairs each pass evaluates, priced against the fp64
+matrix peak.  The CPU oracle (same seed, same Q4 choice) is timed once on the host
 cores as the baseline and its result compared.
 """
 import argparse
@@ -51,35 +54,64 @@ def main():
         times.append(time.perf_counter() - t0)
     r = opt.last_result
 
-    # the feature search the C3 call itself runs (Q4 on equal sizes: ONE
-    # search over the distinct rows against themselves, fgr_match), timed by
-    # hipEvents inside optimize() calls
-    ctx = opt.context
-    ctx.profiling(True)
-    ctx.reset_stats()
-    for _ in range(args.repeat):
-        opt.optimize(src, tgt)
-    so = ctx.stats()
-    ctx.profiling(False)
-    k = max(so["feat_calls"], 1)
-    o1_ms, o2_ms = so["feat_pass1_ms"] / k, so["feat_pass2_ms"] / k
-    o1_pairs, o2_pairs = so["feat_pass1_pairs"] / k, so["feat_pass2_pairs"] / k
+    # The C3 call itself (Q4 on equal sizes) runs NO feature search: the two
+    # feature sets are the same rows, so the mutual pairs come from the dedup
+    # pass (fgr_match).  The genuine 33-D contraction is the own-features
+    # path (target_features_from_source=False): two exact searches per call,
+    # timed here by hipEvents inside optimize() calls.
+    def search_stats(o, reps):
+        ctx = o.context
+        ctx.profiling(True)
+        ctx.reset_stats()
+        t = []
+        for _ in range(reps):
+            t0 = time.perf_counter()
+            o.optimize(src, tgt)
+            t.append(time.perf_counter() - t0)
+        so = ctx.stats()
+        ctx.profiling(False)
+        calls = so["feat_calls"]
+        k = max(calls, 1)
+        p1_ms, p2_ms = so["feat_pass1_ms"] / k, so["feat_pass2_ms"] / k
+        p1, p2 = so["feat_pass1_pairs"] / k, so["feat_pass2_pairs"] / k
+        out = {"searches_per_call": round(calls / reps, 2), "optimize_ms_median_profiled": round(
+            1e3 * float(np.median(t)), 3)}
+        if calls:
+            a1 = flop_pair * p1 / max(p1_ms * 1e-3, 1e-12) / 1e12
+            a12 = flop_pair * (p1 + p2) / max((p1_ms + p2_ms) * 1e-3, 1e-12) / 1e12
+            out.update(pass1_ms=round(p1_ms, 4), pass2_ms=round(p2_ms, 4), pass1_pairs=p1, pass2_pairs=p2,
+                       achieved_tflops_pass1=round(a1, 3), frac_pass1=round(a1 / FP64_MATRIX_PEAK_TF, 4),
+                       achieved_tflops_both_passes=round(a12, 3),
+                       frac_both_passes=round(a12 / FP64_MATRIX_PEAK_TF, 4))
+        return out
 
-    # feature-NN kernels alone (one direction: the source features against
-    # themselves, as Q4 pairs them), hipEvent-timed per pass (orpcd_stats)
-    _, fs = ctx.fpfh(src, 0.1, 20, 0.1, 20)
-    ctx.feature_nn(fs[:4096], fs)                       # warm-up
+    n = len(src)
+    flop_pair = 2 * 33                                  # per query-target pair (SURVEY.md §8d)
+    in_q4 = search_stats(opt, args.repeat)
+
+    own = FastGlobalOptimizer(seed=0, target_features_from_source=False)
+    T_own, rmse_own = own.optimize(src, tgt)           # warm-up
+    own_times = []
+    for _ in range(args.repeat):
+        t0 = time.perf_counter()
+        T_own, rmse_own = own.optimize(src, tgt)
+        own_times.append(time.perf_counter() - t0)
+    r_own = own.last_result
+    in_own = search_stats(own, args.repeat)
+
+    # one direction alone (source features against the target's), hipEvent-timed per pass
+    ctx = own.context
+    fs, ft = own.get_fpfh_features(src, tgt)
+    ctx.feature_nn(fs[:4096], ft)                       # warm-up
     reps = 3
     ctx.profiling(True)
     ctx.reset_stats()
     t0 = time.perf_counter()
     for _ in range(reps):
-        ctx.feature_nn(fs, fs)
+        ctx.feature_nn(fs, ft)
     nn_s = (time.perf_counter() - t0) / reps
     st = ctx.stats()
     ctx.profiling(False)
-    n = len(src)
-    flop_pair = 2 * 33                                  # per query-target pair (SURVEY.md §8d)
     p1_ms, p2_ms = st["feat_pass1_ms"] / reps, st["feat_pass2_ms"] / reps
     p1_pairs, p2_pairs = st["feat_pass1_pairs"] / reps, st["feat_pass2_pairs"] / reps
     achieved = flop_pair * p1_pairs / (p1_ms * 1e-3) / 1e12
@@ -92,23 +124,25 @@ def main():
                    "points": n},
         "result": {"rmse": float(rmse), "fitness": r["fitness"], "n_mutual": r["n_mutual"],
                    "n_tuple_corr": r["n_tuple_corr"]},
+        "in_optimize_q4": in_q4,
+        "own_features": {
+            "workload": "C3 pair, FastGlobalOptimizer(target_features_from_source=False): each cloud's own FPFH",
+            "value": round(1e3 * float(np.median(own_times)), 3), "unit": "ms",
+            "result": {"rmse": float(rmse_own), "fitness": r_own["fitness"], "n_mutual": r_own["n_mutual"],
+                       "n_tuple_corr": r_own["n_tuple_corr"]},
+            "in_optimize": in_own},
         "feature_nn": {
             "kernel": "feat_nn_kernel (pass 1: every query; pass 2: flagged near-ties, exact re-measure)",
+            "what": "one direction of the own-features search: source FPFH rows against the target's",
             "pass1_ms": round(p1_ms, 4), "pass2_ms": round(p2_ms, 4),
             "pass1_pairs": p1_pairs, "pass2_pairs": p2_pairs, "flop_per_pair": flop_pair,
             "achieved_tflops": round(achieved, 3), "peak_tflops": FP64_MATRIX_PEAK_TF,
             "frac": round(achieved / FP64_MATRIX_PEAK_TF, 4),
             "pass2_achieved_tflops": round(flop_pair * p2_pairs / max(p2_ms * 1e-3, 1e-12) / 1e12, 3),
             "seconds_per_direction_incl_upload": round(nn_s, 5),
-            # the search inside the timed optimize() calls: queries = targets = the distinct rows
-            "in_optimize": {"searches_per_call": round(so["feat_calls"] / args.repeat, 2),
-                            "pass1_ms": round(o1_ms, 4), "pass2_ms": round(o2_ms, 4),
-                            "pass1_pairs": o1_pairs, "pass2_pairs": o2_pairs,
-                            "achieved_tflops": round(flop_pair * o1_pairs / max(o1_ms * 1e-3, 1e-12) / 1e12, 3),
-                            "frac": round(flop_pair * o1_pairs / max(o1_ms * 1e-3, 1e-12) / 1e12
-                                          / FP64_MATRIX_PEAK_TF, 4)},
-            "note": "pairs = queries x distinct target rows (exact duplicate rows are collapsed first); "
-                    "brute-force equivalent N x N = %.3g pairs" % (float(n) * n)},
+            "note": "pass-1 pairs = queries x distinct target rows (exact duplicate rows are collapsed first); "
+                    "pass-2 pairs = the (256-query block, sub-part) tiles the need masks do not skip, real rows "
+                    "only; brute-force equivalent N x N = %.3g pairs" % (float(n) * n)},
     }
     if args.cpu:
         sys.path.insert(0, os.path.join(REPO, "oracle"))
@@ -119,6 +153,13 @@ def main():
         line["cpu_baseline"] = {"value": round(cpu_s * 1e3, 1), "unit": "ms", "cores": oracle.num_threads(),
                                 "kind": "port", "sample": "the same optimize call, full size"}
         line["parity"] = {"max_abs_dT": float(np.abs(oT - T).max()), "d_rmse": float(abs(ormse - rmse))}
+        t0 = time.perf_counter()
+        oT, ormse = oracle.OracleFastGlobalOptimizer(seed=0, compat_q4=False).optimize(src, tgt)
+        line["own_features"]["cpu_baseline"] = {"value": round((time.perf_counter() - t0) * 1e3, 1), "unit": "ms",
+                                                "cores": oracle.num_threads(), "kind": "port",
+                                                "sample": "the same own-features optimize call, full size"}
+        line["own_features"]["parity"] = {"max_abs_dT": float(np.abs(oT - T_own).max()),
+                                          "d_rmse": float(abs(ormse - rmse_own))}
     s = json.dumps(line)
     print(s)
     if args.out:
