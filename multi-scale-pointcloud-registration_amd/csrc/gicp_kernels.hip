@@ -406,10 +406,17 @@ __device__ __forceinline__ int culled_search(float4* stage, const float4* __rest
         const unsigned long long t0 = __builtin_readcyclecounter();
         const int r = next_candidate_impl(lbk);
         ph_cull += __builtin_readcyclecounter() - t0;
-        return r;
 #else
-        return next_candidate_impl(lbk);
+        const int r = next_candidate_impl(lbk);
 #endif
+#ifdef ORPCD_BOUNDS_CHECK
+        // the candidate's whole-tile loads (p4: npad = ntiles x 64 points, qbox)
+        if (r >= ntiles) {
+            if ((threadIdx.x & 63) == 0) printf("[chk] culled_search tile %d >= ntiles %d\n", r, ntiles);
+            return -1;
+        }
+#endif
+        return r;
     };
     // software pipeline: the next candidate's 1 KiB tile load is in flight
     // while the current tile is scanned out of LDS
@@ -1215,6 +1222,12 @@ __device__ __forceinline__ int exact_entry(unsigned long long ent, const double*
 #pragma unroll
             for (int u4 = 0; u4 < 4; ++u4) {
                 kk[u4] = c + u4 < nt ? tl[c + u4] * kTile + lane : -1;
+#ifdef ORPCD_BOUNDS_CHECK
+                if (kk[u4] >= tg.ntiles * kTile) {
+                    printf("[chk] scan_listed tile %d >= ntiles %d\n", tl[c + u4], tg.ntiles);
+                    kk[u4] = -1;
+                }
+#endif
                 const int k = kk[u4] >= 0 ? kk[u4] : 0;
                 in[u4] = __float_as_int(ldg_f32(&tg.p4[k].w));  // p4 holds the padded tiles: -1 past the points
                 // the fp64 points stop at npts: a padding lane reads point 0
@@ -2356,6 +2369,12 @@ hipError_t launch_nn1(const double* q, int64_t nq, const CloudLayout& t, double 
                                         (int)t.nsuper, seed_stride_for(t.ntiles), t.xyz64.p, t.perm.p, r2,
                                         search_r2(r2), idx, d2, org_of(t));
     return hipGetLastError();
+}
+
+// this unit's code object loaded now (orpcd_ctx_create), not at its first launch
+hipError_t preload_code_object_gicp() {
+    hipFuncAttributes attr;
+    return hipFuncGetAttributes(&attr, reinterpret_cast<const void*>(&seed_scatter_kernel));
 }
 
 }  // namespace orpcd

@@ -933,4 +933,10 @@ hipError_t launch_normals_cov(const double* rawcov6, int64_t n, const double* Rc
     return hipGetLastError();
 }
 
+// this unit's code object loaded now (orpcd_ctx_create), not at its first launch
+hipError_t preload_code_object_knn() {
+    hipFuncAttributes attr;
+    return hipFuncGetAttributes(&attr, reinterpret_cast<const void*>(&normals_cov_kernel));
+}
+
 }  // namespace orpcd

@@ -849,6 +849,13 @@ hipError_t launch_tuple_select(const TupleJob* jobs, int B, const uint32_t* word
                                const uint64_t* mask, const int32_t* chunk_cnt, const double* A, const double* Bv,
                                int maxc, int32_t* cnt, double* rows, hipStream_t s);
 // representative flags of dedup_rows (uflag_out[i] = row i is the lowest index of its equal rows)
+// The GICP path's device code objects (one per translation unit: sort,
+// KNN, GICP), loaded at context creation instead of at the first launch of
+// each unit's kernels (hipFuncGetAttributes on one kernel loads the unit's
+// code object): the one-time cost moves out of the first call.
+hipError_t preload_code_object_sort();
+hipError_t preload_code_object_knn();
+hipError_t preload_code_object_gicp();
 hipError_t dedup_flags(const double* F, int64_t n, DedupBufs& b, unsigned char* uflag_out, hipStream_t s,
                        int clouds = 1);
 // clouds > 1: that many clouds of n points back to back (xyz, T, idx / d2 and

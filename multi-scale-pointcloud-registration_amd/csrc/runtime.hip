@@ -118,12 +118,31 @@ double coord_margin(const double lo[3], const double hi[3], const double org[3])
     return m * 0x1p-21;
 }
 
+// ORPCD_SETUP_TRACE=1: the set-up phases of set_target / set_source on
+// stderr (each mark drains the stream first: the phases' own times)
+struct SetupTrace {
+    bool on = getenv("ORPCD_SETUP_TRACE") != nullptr;
+    std::chrono::steady_clock::time_point t0 = std::chrono::steady_clock::now();
+    void mark(hipStream_t s, const char* what) {
+        if (!on) return;
+        (void)hipStreamSynchronize(s);
+        const auto t = std::chrono::steady_clock::now();
+        fprintf(stderr, "[orpcd setup] %-28s %8.3f ms\n", what, std::chrono::duration<double, std::milli>(t - t0).count());
+        t0 = t;
+    }
+};
+thread_local SetupTrace* g_setup_trace = nullptr;
+static void setup_mark(hipStream_t s, const char* what) {
+    if (g_setup_trace) g_setup_trace->mark(s, what);
+}
+
 // Lay out a device-resident (input-order) cloud in Morton order with tiles;
 // its fp32 frame is centred on the bounding box (CloudLayout::org).
 int layout_from_device(orpcd_ctx* c, const double* host_xyz, const double* dev_xyz, int64_t n, CloudLayout& L,
                        bool tiles, double* margin = nullptr) {
     double lo[3], hi[3], org[3], ext;
     host_bbox(host_xyz, n, lo, hi, &ext);
+    setup_mark(c->stream, "upload + host bbox");
     for (int a = 0; a < 3; ++a) {
         org[a] = 0.5 * (lo[a] + hi[a]);
         L.lo[a] = lo[a];
@@ -131,6 +150,7 @@ int layout_from_device(orpcd_ctx* c, const double* host_xyz, const double* dev_x
     }
     if (margin) *margin = coord_margin(lo, hi, org);
     CTX_CHECK(c, build_layout(dev_xyz, n, lo, ext, org, L, tiles, c->stream));
+    setup_mark(c->stream, "Morton layout");
     return ORPCD_OK;
 }
 
@@ -166,6 +186,7 @@ int upload_target_k(orpcd_ctx* c, int k, const double* xyz, int64_t m, double ep
     }
     c->tgt_eps[k] = eps;
     c->tgt_host[k].assign(xyz, xyz + 3 * m);
+    setup_mark(c->stream, "KNN-20 covariances + host copy");
     CTX_CHECK(c, c->tdesc.ensure(kMaxTargets));
     write_target_desc(c->tgts[k], c->tcovs[k].p, c->opt.seed_reps, c->opt.seed_grid != 0, c->tdesc_h[k]);
     CTX_CHECK(c, h2d(c->tdesc.p + k, &c->tdesc_h[k], sizeof(TargetDesc), c->stream));
@@ -377,6 +398,7 @@ struct TupleStart {
 };
 
 // the seed's mt19937 words [0, need) on the device (host copy extended on demand)
+constexpr size_t kTupleCacheWords = size_t(16) << 20;  // 64 MB host + 64 MB device kept between calls
 int tuple_stream(orpcd_ctx* c, uint32_t seed, size_t need) {
     auto& T = c->fgr.tup;
     if (!T.valid || T.seed != seed) {
@@ -567,6 +589,17 @@ int fgr_tuples_device(orpcd_ctx* c, const std::vector<TupleStart>& st, const orp
         }
     }
     for (int b = 0; b < B; ++b) K[b] = 3 * cnt[b];
+    // the seed's word stream stays cached for the next call (the same seed
+    // every call), up to kTupleCacheWords: a call that needed more (a very
+    // long tuple test) releases it, host and device, and the next call
+    // regenerates what it needs
+    if (T.host.size() > kTupleCacheWords) {
+        CTX_CHECK(c, hipStreamSynchronize(s));
+        std::vector<uint32_t>().swap(T.host);
+        T.words.release();
+        T.on_dev = 0;
+        T.valid = false;
+    }
     return ORPCD_OK;
 }
 
@@ -837,6 +870,7 @@ int source_ties_detect(orpcd_ctx* c, const CloudLayout& L, const double* dev_in6
     int cnt = 0;
     CTX_CHECK(c, d2h(&cnt, c->tie_cnt.p, 4, c->stream));
     CTX_CHECK(c, hipStreamSynchronize(c->stream));
+    setup_mark(c->stream, "KNN-20 covariances (ties listed)");
     T.on = true;
     if (cnt == 0) return ORPCD_OK;
     const int m = std::min(cnt, kTieCap);
@@ -1208,6 +1242,47 @@ int orpcd_device_count(int* count) {
     return ORPCD_OK;
 }
 
+// Context creation runs the set-up path once on a synthetic cloud of
+// kWarmPoints points (>= knn_lane_min: the kernels a large cloud takes), so
+// that a fresh context's first set_target / set_source does not pay the
+// process's one-time GPU runtime costs: code-object loads, the first launch
+// of every kernel (rocprim's sort kernels alone cost ~13 ms at their first
+// 1M-point sort), the blit kernels of the first copies.  Measured on MI355X
+// (profiles/r06_c5_cold.md): allocations are not the cost (33 hipMalloc,
+// 0.56 ms in all).  ORPCD_LAZY_CODE_OBJECTS=1 skips it.
+constexpr int64_t kWarmPoints = 262144;
+static int warm_setup(orpcd_ctx* c) {
+    std::vector<double> pts((size_t)kWarmPoints * 3);
+    uint64_t x = 0x9E3779B97F4A7C15ull;  // splitmix64: a fixed pseudo-random cube, no ties
+    for (auto& v : pts) {
+        uint64_t z = (x += 0x9E3779B97F4A7C15ull);
+        z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+        z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+        v = (double)((z ^ (z >> 31)) >> 11) * 0x1p-53;
+    }
+    int rc = upload_target(c, pts.data(), kWarmPoints, 1e-3);
+    if (rc) return rc;
+    double margin = 0.0;
+    rc = upload_layout(c, pts.data(), kWarmPoints, c->src, true, &margin);
+    if (rc) return rc;
+    CTX_CHECK(c, c->sraw.ensure((size_t)kWarmPoints * 6));
+    rc = source_ties_detect(c, c->src, c->scratch64a.p, pts.data(), kWarmPoints, margin, false, c->sraw.p);
+    if (rc) return rc;
+    std::vector<double> back(64);
+    CTX_CHECK(c, d2h(back.data(), c->scratch64a.p, back.size() * 8, c->stream));
+    CTX_CHECK(c, hipStreamSynchronize(c->stream));
+    // nothing of the synthetic clouds stays usable
+    c->ties.clear();
+    c->tgt_host[0].clear();
+    c->tgt_eps[0] = -1.0;
+    c->ntgt = 0;
+    c->src_cov = false;
+    c->last_B = 0;
+    c->tgts[0].n = 0;  // the buffers stay allocated (sized for the next cloud of this size)
+    c->src.n = 0;
+    return ORPCD_OK;
+}
+
 int orpcd_ctx_create(int device, orpcd_ctx** out) {
     if (!out) return ORPCD_EINVAL;
     *out = nullptr;
@@ -1220,10 +1295,20 @@ int orpcd_ctx_create(int device, orpcd_ctx** out) {
     if (hipSetDevice(device) != hipSuccess ||
         hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
         c->counters.ensure(kCounterSlots * kCounterStride) != hipSuccess ||
-        hipMemset(c->counters.p, 0, kCounterSlots * kCounterStride * 8) != hipSuccess) {
+        hipMemset(c->counters.p, 0, kCounterSlots * kCounterStride * 8) != hipSuccess ||
+        (!getenv("ORPCD_LAZY_CODE_OBJECTS") &&
+         (preload_code_object_sort() != hipSuccess || preload_code_object_knn() != hipSuccess ||
+          preload_code_object_gicp() != hipSuccess ||
+          // the creating thread's pinned staging buffer at its full size
+          // (a 1M-point cloud's first upload would otherwise pin it: ~4 ms)
+          staging_reserve(staging(), kStageChunk) != hipSuccess))) {
         if (c->stream) (void)hipStreamDestroy(c->stream);
         c->counters.release();
         delete c;
+        return ORPCD_EDEVICE;
+    }
+    if (!getenv("ORPCD_LAZY_CODE_OBJECTS") && warm_setup(c) != ORPCD_OK) {
+        orpcd_ctx_destroy(c);
         return ORPCD_EDEVICE;
     }
     *out = c;
@@ -1282,9 +1367,15 @@ int orpcd_set_target(orpcd_ctx* c, const double* xyz, int64_t m, double epsilon)
     CTX_CHECK(c, hipSetDevice(c->device));
     c->ntgt = 0;
     c->last_B = 0;  // the last batch's correspondences refer to the old targets
+    SetupTrace tr;
+    g_setup_trace = &tr;
+    struct Reset {
+        ~Reset() { g_setup_trace = nullptr; }
+    } reset;
     int rc = upload_target(c, xyz, m, epsilon);
     if (rc) return rc;
     CTX_CHECK(c, hipStreamSynchronize(c->stream));
+    setup_mark(c->stream, "target: seed grid");
     c->ntgt = 1;
     return ORPCD_OK;
 }
@@ -1322,6 +1413,11 @@ int orpcd_set_source(orpcd_ctx* c, const double* xyz, int64_t n) {
     CTX_CHECK(c, hipSetDevice(c->device));
     c->src_cov = false;
     c->last_B = 0;
+    SetupTrace tr;
+    g_setup_trace = &tr;
+    struct Reset {
+        ~Reset() { g_setup_trace = nullptr; }
+    } reset;
     double margin = 0.0;
     int rc = upload_layout(c, xyz, n, c->src, true, &margin);
     if (rc) return rc;
@@ -1329,6 +1425,7 @@ int orpcd_set_source(orpcd_ctx* c, const double* xyz, int64_t n) {
     rc = source_ties_detect(c, c->src, c->scratch64a.p, xyz, n, margin, false, c->sraw.p);
     if (rc) return rc;
     CTX_CHECK(c, hipStreamSynchronize(c->stream));
+    setup_mark(c->stream, "source: KNN-20 + ties");
     c->src_cov = true;
     return ORPCD_OK;
 }
@@ -2432,6 +2529,30 @@ int orpcd_fgr_optimize_batch(orpcd_ctx* c, const double* src, int64_t n, const d
     CTX_REQUIRE(c, finite_cloud(src, n) && finite_cloud(tgts, toff[ntgt]), "fgr_optimize_batch: non-finite coordinates");
     for (int64_t i = 0; i < 9 * (int64_t)B; ++i) CTX_REQUIRE(c, std::isfinite(R0[i]), "fgr_optimize_batch: non-finite R0");
     for (int64_t i = 0; i < 3 * (int64_t)B; ++i) CTX_REQUIRE(c, std::isfinite(t0[i]), "fgr_optimize_batch: non-finite t0");
+    {
+        // the per-start buffers (posed copy, padded features, SPFH, KNN
+        // lists, normals; host copy) scale with B x n: a batch above the
+        // budget (ORPCD_FGR_BATCH_BYTES, default 16 GiB) runs in chunks of
+        // starts, each start's result being independent of its batch mates
+        const int kk = std::max(normal_knn, fpfh_knn);
+        const double per_start = (double)n * (3 * 8 + kFeatDim * 8 + 33 * 8 + 6 * 8 + 3 * 8 + 8.0 * kk + 4 + 3 * 8);
+        const char* env = getenv("ORPCD_FGR_BATCH_BYTES");
+        const double budget = env ? std::max(1.0, atof(env)) : 16.0 * (1ull << 30);
+        const int32_t chunk = (int32_t)std::max(1.0, std::min((double)B, std::floor(budget / per_start)));
+        if (chunk < B) {
+            for (int32_t b0 = 0; b0 < B; b0 += chunk) {
+                const int32_t nb = std::min(chunk, B - b0);
+                rc = orpcd_fgr_optimize_batch(c, src, n, tgts, m, ntgt, R0 + 9 * (size_t)b0, t0 + 3 * (size_t)b0,
+                                              target_of_start ? target_of_start + b0 : nullptr, nb, normal_radius,
+                                              normal_knn, fpfh_radius, fpfh_knn, target_features_from_source, p,
+                                              T_out + 16 * (size_t)b0, fitness_out ? fitness_out + b0 : nullptr,
+                                              rmse_out ? rmse_out + b0 : nullptr, ncorr_out ? ncorr_out + b0 : nullptr,
+                                              n_mutual_out ? n_mutual_out + 2 * (size_t)b0 : nullptr);
+                if (rc) return rc;
+            }
+            return ORPCD_OK;
+        }
+    }
     CTX_CHECK(c, hipSetDevice(c->device));
     FgrTrace tr;  // ORPCD_FGR_TRACE=1: the batch's phases on stderr
     g_fgr_trace = &tr;

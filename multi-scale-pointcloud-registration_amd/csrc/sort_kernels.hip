@@ -152,6 +152,20 @@ hipError_t launch_morton(const double* xyz, int64_t n, const double lo[3], doubl
     return hipGetLastError();
 }
 
+// Every buffer a kernel loads whole tiles of holds the padded tiles (the
+// round-5 fault was a whole-tile load past an n-point buffer): checked on the
+// host after each layout build, always on (a few integer compares).
+static hipError_t check_layout_sizes(const char* what, size_t copies, size_t n, size_t npad, size_t ntiles,
+                                     size_t nsuper, size_t xyz64, size_t p4, size_t tlo, size_t thi, size_t qbox,
+                                     size_t slo, size_t shi, bool xyz_padded) {
+    const bool ok = npad == std::max<size_t>(kTile, ntiles * kTile) && npad >= n &&
+                    xyz64 >= copies * 3 * (xyz_padded ? npad : n) && (p4 == 0 || (p4 >= copies * npad &&
+                    tlo >= copies * ntiles && thi >= copies * ntiles && qbox >= copies * ntiles * 2 * kNQ &&
+                    slo >= copies * nsuper && shi >= copies * nsuper));
+    if (!ok) fprintf(stderr, "[orpcd] %s: layout buffers smaller than the padded tiles\n", what);
+    return ok ? hipSuccess : hipErrorInvalidValue;
+}
+
 hipError_t build_layout(const double* dev_in64, int64_t n, const double bbox_lo[3], double bbox_ext,
                         const double origin[3], CloudLayout& L, bool with_tiles, hipStream_t s) {
     L.n = n;
@@ -199,7 +213,8 @@ hipError_t build_layout(const double* dev_in64, int64_t n, const double bbox_lo[
                                                                             (int)L.nsuper, L.slo.p, L.shi.p);
         if ((e = hipGetLastError()) != hipSuccess) return e;
     }
-    return hipSuccess;
+    return check_layout_sizes("build_layout", 1, (size_t)n, (size_t)L.npad, (size_t)L.ntiles, (size_t)L.nsuper,
+                              L.xyz64.n, with_tiles ? L.p4.n : 0, L.tlo.n, L.thi.n, L.qbox.n, L.slo.n, L.shi.n, true);
 }
 
 // B rigid copies (input order, B x n x 3 at in64) laid out in the Morton
@@ -230,7 +245,17 @@ hipError_t build_batch_layout(const double* in64, int64_t n, int B, const int32_
     if ((e = hipGetLastError()) != hipSuccess) return e;
     super_aabb_kernel<<<dim3((unsigned)((L.nsuper + 255) / 256), (unsigned)B), 256, 0, s>>>(
         L.tlo.p, L.thi.p, (int)L.ntiles, (int)L.nsuper, L.slo.p, L.shi.p);
-    return hipGetLastError();
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    // the copies' fp64 points are n each (no whole-tile fp64 loads on them:
+    // the batched KNN tests k < n before every load)
+    return check_layout_sizes("build_batch_layout", (size_t)B, (size_t)n, (size_t)L.npad, (size_t)L.ntiles,
+                              (size_t)L.nsuper, L.xyz64.n, L.p4.n, L.tlo.n, L.thi.n, L.qbox.n, L.slo.n, L.shi.n, false);
+}
+
+// this unit's code object loaded now (orpcd_ctx_create), not at its first launch
+hipError_t preload_code_object_sort() {
+    hipFuncAttributes attr;
+    return hipFuncGetAttributes(&attr, reinterpret_cast<const void*>(&morton_kernel));
 }
 
 }  // namespace orpcd

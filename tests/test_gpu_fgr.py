@@ -277,6 +277,24 @@ def test_fgr_batch_is_the_per_call_path_bit_for_bit(ctx, case):
     assert (got["n_tuple_corr"] >= 10).all() and (got["ncorr"] > 0).all()
 
 
+def test_fgr_batch_chunked_by_memory_budget_is_bit_identical(ctx):
+    """A batch whose per-start buffers exceed the budget (ORPCD_FGR_BATCH_BYTES)
+    runs in chunks of starts: every output (T, rmse, fitness, ncorr, mutual
+    and tuple counts) equals the one-chunk batch bit for bit."""
+    src, tgt = _pair(2500, noise=1e-3)
+    kw = dict(maximum_correspondence_distance=0.05, fpfh_radius=0.25, fpfh_knn=40, seed=3)
+    targets = [tgt, tgt[:2100] * np.array([1.1, 1.0, 0.9])]
+    R0, t0 = _starts(7, 17)
+    tos = np.array([1, 0, 1, 1, 0, 0, 1], np.int32)
+    whole = ctx.fgr_optimize_batch(src, targets, R0, t0, target_of_start=tos, **kw)
+    os.environ["ORPCD_FGR_BATCH_BYTES"] = str(2500 * 1500 * 3)   # about 3 starts per chunk
+    try:
+        chunked = ctx.fgr_optimize_batch(src, targets, R0, t0, target_of_start=tos, **kw)
+    finally:
+        del os.environ["ORPCD_FGR_BATCH_BYTES"]
+    assert _same(whole, chunked)
+
+
 def test_fgr_batch_rejects_bad_arguments(ctx):
     src, tgt = _pair(600)
     R0, t0 = _starts(2, 1)

@@ -49,8 +49,10 @@ def main():
     from orpcd_amd import _native, parallel
     from workloads import c5_pair
     src, tgt = c5_pair(args.points)
+    t_ctx = time.perf_counter()
     ctx = _native.Context(int(os.environ.get("ORPCD_BENCH_DEVICE", os.environ.get("LOCAL_RANK", "0"))) if world > 1
                           else None)
+    ctx_create_s = time.perf_counter() - t_ctx  # the process's first context: GPU runtime init + warm-up
     for k, v in json.loads(args.opt).items():
         ctx.set_option(k, v)
     params = dict(max_correspondence_distance=0.5, max_iteration=args.iters)
@@ -151,7 +153,11 @@ def main():
                    "warm_iterations": round(warm_call - warm_setup, 4),
                    "cold": round(setup_s + cold_first_run_s + elapsed, 4), "cold_setup": round(setup_s, 4),
                    "cold_setup_target": round(cold_target_s, 4), "cold_setup_source": round(cold_source_s, 4),
-                   "note": "cold = first set-up + the 1-iteration warm-up run + the timed run"},
+                   "ctx_create": round(ctx_create_s, 4),
+                   "lazy_code_objects": bool(os.environ.get("ORPCD_LAZY_CODE_OBJECTS")),
+                   "note": "cold = first set-up + the 1-iteration warm-up run + the timed run, on a fresh context; "
+                           "ctx_create = the process's first orpcd_ctx_create (HIP runtime init, code-object "
+                           "loads and the synthetic set-up warm-up, profiles/r06_c5_cold.md)"},
         "value_end_to_end": round(r["iters"] / warm_call, 3),
         "result": {"rmse": r["rmse"], "fitness": r["fitness"], "iters": r["iters"], "ncorr": r["ncorr"]},
     }
