@@ -676,6 +676,7 @@ struct SchedS {                          // search side (pass p)
     unsigned long long* wtot_next;       // the next pass's: zeroed here (block 0; read by this
                                          // pass's transform, which ran before)
     int cap, NG, B;
+    int xcd;                             // item order XCD-aware (option sched_xcd)
 };
 
 // The ordered dispatch's work items of start `slot` (one block per start,
@@ -1059,7 +1060,7 @@ __global__ __launch_bounds__(64 * kSWaves) __attribute__((amdgpu_waves_per_eu(kE
         sa.wtot_next[lane] = 0ull;  // kSchedTot == 64
     }
     const unsigned w = __builtin_amdgcn_readfirstlane(blockIdx.x * kSWaves + wid);
-    unsigned base = 0, off = 0;
+    unsigned base = 0, off = 0, ncls = 0;
     int cls = -1;
 #pragma unroll
     for (int c = 0; c < kSchedClasses; ++c) {
@@ -1067,10 +1068,21 @@ __global__ __launch_bounds__(64 * kSWaves) __attribute__((amdgpu_waves_per_eu(kE
         if (cls < 0 && w < base + n) {
             cls = c;
             off = w - base;
+            ncls = n;
         }
         base += n;
     }
     if (cls < 0) return;  // past the pass's items
+    if (sa.xcd) {
+        // one-wave workgroups go to the XCDs round-robin (workgroup w on XCD
+        // w % 8): waves w, w + 8, ... of a class take one contiguous chunk of
+        // its items (adjacent query groups and their splits, which read the
+        // same target tiles) instead of every 8th item, so each XCD's L2
+        // holds one region's tiles (profiles/r06_pmc_waves.json: one-wave
+        // workgroups raised the L2 misses 37%)
+        const unsigned n8 = ncls >> 3;
+        if (off < 8 * n8) off = (off & 7u) * n8 + (off >> 3);
+    }
 #ifdef ORPCD_SCHED_CHECK
     if (base > (unsigned)sa.cap || off >= (unsigned)sa.cap) {
         if (lane == 0 && w < 4) printf("[sched] counts %u exceed cap %d (w %u cls %d off %u)\n", base, sa.cap, w, cls, off);
@@ -1488,18 +1500,24 @@ __device__ __forceinline__ void pose_from_lanes(double v, PoseIn& p) {
     for (int t = 0; t < 12; ++t) p.G[t] = rl64(v, 18 + t);
 }
 
+// ldlt_x: null, or (two-wave solve: every caller's block is two waves holding
+// the same sums) an LDS slot for x -- wave 1 runs the LDLT while wave 0
+// evaluates the determinant check, joined through LDS (the two are
+// independent: the LDLT's x is used only when the check passes).  Wave 0
+// alone stores; the values are those of the one-wave solve bit for bit.
 template <int kEst>  // kEst 0: GeneralizedICP, 1: PointToPoint
 __device__ bool solve_start(int slot, const double s[kNacc], int64_t N, int pass, int max_iter, double rel_fit,
-                            double rel_rmse, const SolveArgs& a, const PoseIn& pin) {
+                            double rel_rmse, const SolveArgs& a, const PoseIn& pin, double* ldlt_x = nullptr) {
 #pragma clang fp contract(off)  // no fused multiply-add: the same rounding in every caller
     const int lane = threadIdx.x & 63;
+    const bool store = ldlt_x == nullptr || (threadIdx.x >> 6) == 0;  // the storing wave
     const double cnt = s[28];
     const double fit = cnt > 0 ? cnt / (double)N : 0.0;
     const double rmse = cnt > 0 ? sqrt(s[27] / cnt) : 0.0;
     const double pf = pin.pf, pr = pin.pr;
     const bool converged = pass >= 1 && fabs(pf - fit) < rel_fit && fabs(pr - rmse) < rel_rmse;
     if (converged || pass >= max_iter) {
-        if (lane == 0) {
+        if (lane == 0 && store) {
             a.out_fit[slot] = fit;
             a.out_rmse[slot] = rmse;
             a.out_iters[slot] = pass;
@@ -1508,7 +1526,7 @@ __device__ bool solve_start(int slot, const double s[kNacc], int64_t N, int pass
         }
         return true;
     }
-    if (lane == 0) {
+    if (lane == 0 && store) {
         a.prev[2 * slot] = fit;
         a.prev[2 * slot + 1] = rmse;
     }
@@ -1516,6 +1534,27 @@ __device__ bool solve_start(int slot, const double s[kNacc], int64_t N, int pass
     double upd[16] = {1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1};
     if (cnt > 0 && kEst == 1) {
         umeyama_from_moments(s, cnt, upd);  // every lane, the same values
+    } else if (cnt > 0 && ldlt_x) {
+        double det = 0.0;
+        if (!store) {  // wave 1: the LDLT (as below), x to LDS
+            double JTJ[36], b[6], x[6];
+            for (int r = 0; r < 6; ++r) b[r] = -s[21 + r];
+            for (int i = 0, k = 0; i < 6; ++i)
+                for (int j = i; j < 6; ++j, ++k) JTJ[6 * i + j] = JTJ[6 * j + i] = s[k];
+            ldlt_solve6(JTJ, b, x);
+            if (lane < 6) ldlt_x[lane] = x[lane];
+        } else {       // wave 0: the determinant check
+            double row[6];
+            sym6_row(s, lane, row);
+            det = det6_wave(row, lane);
+        }
+        __syncthreads();
+        if (!store) return false;
+        if (!(fabs(det) < 1e-6 || isnan(det) || isinf(det))) {
+            double x[6];
+            for (int r = 0; r < 6; ++r) x[r] = ldlt_x[r];
+            vec6_to_m4_wave(x, upd, lane);
+        }
     } else if (cnt > 0) {
         double row[6], b[6];
         sym6_row(s, lane, row);
@@ -1875,11 +1914,19 @@ __global__ __launch_bounds__(64) void reduce_partials_kernel(const double* __res
         for (int v = 0; v < kNacc; ++v) sums[v] = s[v];
 }
 
+// kSolveWaves: one, or two for the GeneralizedICP solve (the determinant
+// check and the LDLT in separate waves, solve_start; ORPCD_SOLVE_WAVES A/B).
+#ifndef ORPCD_SOLVE_WAVES
+#define ORPCD_SOLVE_WAVES 2
+#endif
+template <int kEst>
+constexpr int solve_waves() { return kEst == 0 ? ORPCD_SOLVE_WAVES : 1; }
 template <int kEst>  // 0: GeneralizedICP, 1: PointToPoint
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 2))) void icp_solve_kernel(const int32_t* __restrict__ active,
+__global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(1, 2))) void icp_solve_kernel(const int32_t* __restrict__ active,
                                                         const double* __restrict__ partial, int nblk,
                                                         const double* __restrict__ sums_in, int64_t N, int pass,
                                                         int max_iter, double rel_fit, double rel_rmse, SolveArgs a) {
+    __shared__ double ldlt_x[8];
     const int slot = active[blockIdx.x];
     // the done flag, the partials and the pose are loaded together (one memory
     // round trip after active[]); a finished start only wasted the loads
@@ -1895,7 +1942,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 2))) void
     if (finished) return;
     PoseIn pin;
     pose_from_lanes(pose, pin);
-    solve_start<kEst>(slot, s, N, pass, max_iter, rel_fit, rel_rmse, a, pin);
+    solve_start<kEst>(slot, s, N, pass, max_iter, rel_fit, rel_rmse, a, pin,
+                      solve_waves<kEst>() == 2 ? ldlt_x : nullptr);
 }
 
 int seed_stride_for(int64_t ntiles, int reps = 512);
@@ -2256,6 +2304,7 @@ hipError_t launch_gicp_pass(const orpcd_ctx* c, int nact, int pass, double r2, h
         sa.cap = c->sched_cap;
         sa.NG = (int)NG;
         sa.B = (int)B;
+        sa.xcd = kSWaves == 1 ? c->opt.sched_xcd : 0;
         const int64_t grid = (std::min<int64_t>(items, c->sched_cap) + kSWaves - 1) / kSWaves;
         auto kern = c->exact_live ? nn_search_sched_kernel<true> : nn_search_sched_kernel<false>;
         kern<<<dim3((unsigned)grid), 64 * kSWaves, 0, s>>>(c->q32.p, N, c->tdesc.p, c->opt.super_cull, c->best.p,
@@ -2311,7 +2360,8 @@ hipError_t launch_gicp_solve(const orpcd_ctx* c, int nact, int pass, const orpcd
                              const TgtBounds& tb) {
     const SolveArgs a = solve_args(c);
     auto solve = c->est == kEstP2P ? icp_solve_kernel<1> : icp_solve_kernel<0>;
-    solve<<<(unsigned)nact, 64, 0, s>>>(c->active.p, c->partial.p, accum_blocks(c->src.n), nullptr,
+    const int solve_threads = 64 * (c->est == kEstP2P ? solve_waves<1>() : solve_waves<0>());
+    solve<<<(unsigned)nact, solve_threads, 0, s>>>(c->active.p, c->partial.p, accum_blocks(c->src.n), nullptr,
                                                     c->src.n, pass, p.max_iteration, p.relative_fitness,
                                                     p.relative_rmse, a);
     hipError_t e = launched("icp_solve_kernel", s);
@@ -2328,7 +2378,7 @@ hipError_t launch_reduce_partials(const orpcd_ctx* c, int slot, double* sums29, 
 hipError_t launch_gicp_solve_sums(const orpcd_ctx* c, const double* sums29, int64_t n_total, int pass,
                                   const orpcd_gicp_params& p, hipStream_t s) {
     const SolveArgs a = solve_args(c);
-    icp_solve_kernel<0><<<1, 64, 0, s>>>(c->active.p, nullptr, 0, sums29, n_total, pass, p.max_iteration,
+    icp_solve_kernel<0><<<1, 64 * solve_waves<0>(), 0, s>>>(c->active.p, nullptr, 0, sums29, n_total, pass, p.max_iteration,
                                        p.relative_fitness, p.relative_rmse, a);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;

@@ -690,6 +690,7 @@ struct orpcd_ctx {
         int sched_items = 10240;  // ordered dispatch: split a group until its waves cost <= pass total / this
                                   // (C2 sweep 5120 / 10240 / 20480: 15.4 / 15.0 / 16.6 ms at 30 starts)
         int sched_min_starts = 16;  // ordered dispatch only for batches of at least this many starts
+        int sched_xcd = 0;          // ordered dispatch: each XCD takes a contiguous chunk of a class's items
         int sched_cap_us = 30;    // ordered dispatch: a split's planned cost at most this many us (0: no cap;
                                   // C2 30 / 64 starts 15.50 -> 15.37 / 24.44 -> 24.23 ms, identical hashes,
                                   // profiles/r05_sched_cap_sweep*.log)

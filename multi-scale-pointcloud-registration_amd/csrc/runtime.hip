@@ -2811,6 +2811,7 @@ int orpcd_set_option(orpcd_ctx* c, const char* key, double value) {
     else if (k == "sched" && (v == 0 || v == 1)) c->opt.sched = v;
     else if (k == "sched_items" && v >= 64 && v <= (1 << 22)) c->opt.sched_items = v;
     else if (k == "sched_min_starts" && v >= 1) c->opt.sched_min_starts = v;
+    else if (k == "sched_xcd" && (v == 0 || v == 1)) c->opt.sched_xcd = v;
     else if (k == "sched_cap_us" && v >= 0 && v <= 100000) c->opt.sched_cap_us = v;
     else if (k == "sched_cap_mult" && v >= 1 && v <= 16) c->opt.sched_cap_mult = v;
     else if (k == "knn_lane_min" && v >= 0) c->opt.knn_lane_min = v;
