@@ -148,6 +148,22 @@ int orpcd_gicp_batch_window(orpcd_ctx* ctx, const double* R0, const double* t0, 
                             const double* state_in, double* state_out, int32_t* done_out, double* T_out,
                             double* rmse_out, double* fitness_out, int32_t* iters_out, int64_t* ncorr_out);
 
+/* A target's device state -- Morton layout, tile / quarter / super-tile
+ * boxes, seed grid and GICP covariances -- as one device buffer, and its
+ * adoption by another context (on this or another GPU): the multi-GPU
+ * re-deal of running starts moves target layouts between
+ * ranks (an RCCL all-gather of these buffers) instead of building them again.
+ * orpcd_target_layout_bytes: the buffer size for target k (< the targets set);
+ * orpcd_get_target_layout: writes it to device memory dev_out (>= that size,
+ * on this context's device, 256-byte aligned);
+ * orpcd_set_target_layouts: makes ntargets (<= 16) such buffers the targets
+ * 0..ntargets-1 of ctx, as orpcd_set_targets would have made them from the
+ * same clouds and epsilon (bit for bit: batches on them return the same
+ * results).  Replaces orpcd_set_targets.                                    */
+int64_t orpcd_target_layout_bytes(orpcd_ctx* ctx, int32_t k);
+int orpcd_get_target_layout(orpcd_ctx* ctx, int32_t k, void* dev_out, int64_t bytes);
+int orpcd_set_target_layouts(orpcd_ctx* ctx, const void* const* dev_in, int32_t ntargets);
+
 /* ------------------------------------ source KNN-20 boundary ties (per pose)
  * Open3D recomputes the source's KNN-20 covariances on every posed copy
  * source_initialized = source @ R0 + t0 (Aligner.py:183-185; the PointCloud

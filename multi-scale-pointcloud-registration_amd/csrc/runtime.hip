@@ -215,6 +215,19 @@ int upload_target(orpcd_ctx* c, const double* xyz, int64_t m, double eps) {
 int targets_for_epsilon(orpcd_ctx* c, int ntgt, double eps) {
     for (int k = 0; k < ntgt; ++k) {
         if (c->tgt_eps[k] == eps) continue;
+        if (c->tgt_host[k].empty()) {
+            // an adopted layout (orpcd_set_target_layouts): the input-order
+            // points from its Morton-order fp64 points and permutation
+            const CloudLayout& L = c->tgts[k];
+            std::vector<double> mz((size_t)L.n * 3);
+            std::vector<int32_t> perm((size_t)L.n);
+            CTX_CHECK(c, d2h(mz.data(), L.xyz64.p, mz.size() * 8, c->stream));
+            CTX_CHECK(c, d2h(perm.data(), L.perm.p, perm.size() * 4, c->stream));
+            CTX_CHECK(c, hipStreamSynchronize(c->stream));
+            c->tgt_host[k].resize(mz.size());
+            for (int64_t i = 0; i < L.n; ++i)
+                for (int a = 0; a < 3; ++a) c->tgt_host[k][3 * (size_t)perm[(size_t)i] + a] = mz[3 * (size_t)i + a];
+        }
         std::vector<double> host = c->tgt_host[k];
         int rc = upload_target_k(c, k, host.data(), c->tgts[k].n, eps);
         if (rc) return rc;
@@ -2235,6 +2248,143 @@ int orpcd_set_target_rows(orpcd_ctx* c, const double* xyz, int64_t m, double eps
     if (row_end) *row_end = hi;
     // complete (usable by the GICP calls) once every row is there
     if (nranks == 1 || device_gather) c->ntgt = 1;
+    return ORPCD_OK;
+}
+
+// ---------------------------------------------- target layouts as buffers
+// One device buffer per target: a header, then the layout's arrays at
+// 256-byte aligned offsets (orpcd_target_layout_bytes / get / set).
+namespace {
+constexpr uint64_t kLayoutMagic = 0x31304c4443505230ull;  // "0RPCDL01"
+enum { kLayXyz, kLayPerm, kLayP4, kLayTlo, kLayThi, kLayQbox, kLaySlo, kLayShi, kLaySgrid, kLayTcov, kLaySections };
+struct LayoutHeader {
+    uint64_t magic;
+    int64_t n, npad, ntiles, nsuper;
+    double org[3], lo[3], hi[3], eps;
+    float sg_lo[3], sg_inv[3];
+    int32_t has_sgrid, cov_w;
+    uint64_t off[kLaySections], len[kLaySections];  // bytes
+    uint64_t total;
+};
+LayoutHeader layout_header(const CloudLayout& L, double eps) {
+    LayoutHeader h{};
+    h.magic = kLayoutMagic;
+    h.n = L.n;
+    h.npad = L.npad;
+    h.ntiles = L.ntiles;
+    h.nsuper = L.nsuper;
+    for (int a = 0; a < 3; ++a) {
+        h.org[a] = L.org[a];
+        h.lo[a] = L.lo[a];
+        h.hi[a] = L.hi[a];
+        h.sg_lo[a] = L.sg_lo[a];
+        h.sg_inv[a] = L.sg_inv[a];
+    }
+    h.eps = eps;
+    h.has_sgrid = L.sgrid.n > 0;
+    h.cov_w = kCovW;
+    const uint64_t len[kLaySections] = {
+        (uint64_t)L.npad * 3 * 8,  (uint64_t)L.n * 4,
+        (uint64_t)L.npad * 16,     (uint64_t)L.ntiles * 16,
+        (uint64_t)L.ntiles * 16,   (uint64_t)L.ntiles * 2 * kNQ * 16,
+        (uint64_t)L.nsuper * 16,   (uint64_t)L.nsuper * 16,
+        h.has_sgrid ? (uint64_t)kSeedGrid * kSeedGrid * kSeedGrid * 4 : 0,
+        (uint64_t)L.n * kCovW * 8};
+    uint64_t at = (sizeof(LayoutHeader) + 255) / 256 * 256;
+    for (int i = 0; i < kLaySections; ++i) {
+        h.off[i] = at;
+        h.len[i] = len[i];
+        at += (len[i] + 255) / 256 * 256;
+    }
+    h.total = at;
+    return h;
+}
+}  // namespace
+
+int64_t orpcd_target_layout_bytes(orpcd_ctx* c, int32_t k) {
+    if (!c) return -1;
+    if (k < 0 || k >= c->ntgt) {
+        c->err = "target_layout_bytes: no such target";
+        return -1;
+    }
+    return (int64_t)layout_header(c->tgts[k], c->tgt_eps[k]).total;
+}
+
+int orpcd_get_target_layout(orpcd_ctx* c, int32_t k, void* dev_out, int64_t bytes) {
+    if (!c) return ORPCD_EINVAL;
+    CTX_REQUIRE(c, k >= 0 && k < c->ntgt, "get_target_layout: no such target");
+    const CloudLayout& L = c->tgts[k];
+    const LayoutHeader h = layout_header(L, c->tgt_eps[k]);
+    CTX_REQUIRE(c, dev_out && bytes >= (int64_t)h.total && ((uintptr_t)dev_out & 255) == 0,
+                "get_target_layout: the buffer is smaller than orpcd_target_layout_bytes or not 256-byte aligned");
+    CTX_CHECK(c, hipSetDevice(c->device));
+    hipStream_t s = c->stream;
+    unsigned char* o = static_cast<unsigned char*>(dev_out);
+    const void* src[kLaySections] = {L.xyz64.p, L.perm.p, L.p4.p, L.tlo.p, L.thi.p, L.qbox.p, L.slo.p, L.shi.p,
+                                     L.sgrid.p, c->tcovs[k].p};
+    CTX_CHECK(c, h2d(o, &h, sizeof(h), s));
+    for (int i = 0; i < kLaySections; ++i)
+        if (h.len[i]) CTX_CHECK(c, hipMemcpyAsync(o + h.off[i], src[i], h.len[i], hipMemcpyDeviceToDevice, s));
+    CTX_CHECK(c, hipStreamSynchronize(s));
+    return ORPCD_OK;
+}
+
+int orpcd_set_target_layouts(orpcd_ctx* c, const void* const* dev_in, int32_t ntargets) {
+    if (!c) return ORPCD_EINVAL;
+    CTX_REQUIRE(c, dev_in && ntargets >= 1 && ntargets <= kMaxTargets, "set_target_layouts: 1 to 16 layouts");
+    CTX_CHECK(c, hipSetDevice(c->device));
+    hipStream_t s = c->stream;
+    c->ntgt = 0;
+    c->last_B = 0;  // the last batch's correspondences refer to the old targets
+    for (int k = 0; k < ntargets; ++k) {
+        CTX_REQUIRE(c, dev_in[k], "set_target_layouts: null buffer");
+        LayoutHeader h;
+        CTX_CHECK(c, d2h(&h, dev_in[k], sizeof(h), s));
+        CTX_CHECK(c, hipStreamSynchronize(s));
+        CTX_REQUIRE(c, h.magic == kLayoutMagic && h.cov_w == kCovW && h.n > 0 && h.n < kMaxPoints,
+                    "set_target_layouts: not a target layout of this library (orpcd_get_target_layout)");
+        CloudLayout& L = c->tgts[k];
+        L.n = h.n;
+        L.npad = h.npad;
+        L.ntiles = h.ntiles;
+        L.nsuper = h.nsuper;
+        for (int a = 0; a < 3; ++a) {
+            L.org[a] = h.org[a];
+            L.lo[a] = h.lo[a];
+            L.hi[a] = h.hi[a];
+        }
+        const LayoutHeader want = layout_header(L, h.eps);  // the sizes this layout implies
+        for (int i = 0; i < kLaySections; ++i)
+            CTX_REQUIRE(c, i == kLaySgrid ? (h.len[i] == 0 || h.len[i] == want.len[i]) : h.len[i] == want.len[i],
+                        "set_target_layouts: inconsistent layout header");
+        CTX_CHECK(c, L.xyz64.ensure((size_t)L.npad * 3));
+        CTX_CHECK(c, L.perm.ensure((size_t)L.n));
+        CTX_CHECK(c, L.p4.ensure((size_t)L.npad));
+        CTX_CHECK(c, L.tlo.ensure((size_t)L.ntiles));
+        CTX_CHECK(c, L.thi.ensure((size_t)L.ntiles));
+        CTX_CHECK(c, L.qbox.ensure((size_t)L.ntiles * 2 * kNQ));
+        CTX_CHECK(c, L.slo.ensure((size_t)L.nsuper));
+        CTX_CHECK(c, L.shi.ensure((size_t)L.nsuper));
+        CTX_CHECK(c, prepare_seed_grid(L));  // sgrid / its scratch, sg_lo / sg_inv from the box
+        for (int a = 0; a < 3; ++a) {
+            L.sg_lo[a] = h.sg_lo[a];
+            L.sg_inv[a] = h.sg_inv[a];
+        }
+        CTX_CHECK(c, c->tcovs[k].ensure((size_t)L.n * kCovW));
+        void* dst[kLaySections] = {L.xyz64.p, L.perm.p, L.p4.p, L.tlo.p, L.thi.p, L.qbox.p, L.slo.p, L.shi.p,
+                                   L.sgrid.p, c->tcovs[k].p};
+        const unsigned char* in = static_cast<const unsigned char*>(dev_in[k]);
+        for (int i = 0; i < kLaySections; ++i)
+            if (h.len[i]) CTX_CHECK(c, hipMemcpyAsync(dst[i], in + h.off[i], h.len[i], hipMemcpyDeviceToDevice, s));
+        c->tgt_eps[k] = h.eps;
+        c->tgt_host[k].clear();  // rebuilt from the device layout if another epsilon is asked for
+        CTX_CHECK(c, c->tdesc.ensure(kMaxTargets));
+        write_target_desc(L, c->tcovs[k].p, c->opt.seed_reps, c->opt.seed_grid != 0, c->tdesc_h[k]);
+        CTX_CHECK(c, h2d(c->tdesc.p + k, &c->tdesc_h[k], sizeof(TargetDesc), s));
+        if (!h.has_sgrid) CTX_CHECK(c, seed_grids(c, k, 1));
+    }
+    CTX_CHECK(c, hipStreamSynchronize(s));
+    c->ntgt = ntargets;
     return ORPCD_OK;
 }
 

@@ -57,7 +57,7 @@ EXPORTED = ("orpcd_abi_version", "orpcd_build_id", "orpcd_build_flags", "orpcd_d
             "orpcd_set_source_rows", "orpcd_gicp_shard_begin", "orpcd_gicp_shard_pass", "orpcd_gicp_shard_update",
             "orpcd_gicp_shard_result", "orpcd_comm_unique_id", "orpcd_comm_init", "orpcd_comm_destroy",
             "orpcd_gicp_shard_run", "orpcd_gicp_batch_window", "orpcd_set_target_rows", "orpcd_target_cov_width", "orpcd_target_cov_rows",
-            "orpcd_set_target_cov",
+            "orpcd_set_target_cov", "orpcd_target_layout_bytes", "orpcd_get_target_layout", "orpcd_set_target_layouts",
             "orpcd_nn1_radius", "orpcd_estimate_normals", "orpcd_fpfh", "orpcd_fpfh_from_normals", "orpcd_fgr", "orpcd_feature_nn",
             "orpcd_fgr_optimize", "orpcd_fgr_optimize_batch", "orpcd_set_source_points", "orpcd_icp_p2p_batch",
             "orpcd_sor", "orpcd_voxel_down_sample", "orpcd_farthest_downsample",
@@ -171,6 +171,10 @@ def load_library():
         L.orpcd_target_cov_width.argtypes = []
         L.orpcd_target_cov_rows.argtypes = [vp, c_i64, c_i64, _f64p]
         L.orpcd_set_target_cov.argtypes = [vp, _f64p]
+        L.orpcd_target_layout_bytes.argtypes = [vp, ctypes.c_int32]
+        L.orpcd_target_layout_bytes.restype = c_i64
+        L.orpcd_get_target_layout.argtypes = [vp, ctypes.c_int32, vp, c_i64]
+        L.orpcd_set_target_layouts.argtypes = [vp, ctypes.POINTER(vp), ctypes.c_int32]
         L.orpcd_nn1_radius.argtypes = [vp, _f64p, c_i64, _f64p, c_i64, c_dbl, _i32p, _f64p]
         L.orpcd_estimate_normals.argtypes = [vp, _f64p, c_i64, ctypes.c_int32, c_dbl, c_dbl, vp, vp, vp]
         L.orpcd_fpfh.argtypes = [vp, _f64p, c_i64, c_dbl, ctypes.c_int32, c_dbl, ctypes.c_int32, _f64p, _f64p]
@@ -363,6 +367,29 @@ class Context:
             xyz = np.ascontiguousarray(np.concatenate(ts, axis=0))
         self._check(self._L.orpcd_set_targets(self._h, xyz, m, len(ts), float(epsilon)), "orpcd_set_targets")
         self._target_key = key if len(ts) > 1 else (self._key(ts[0]), float(epsilon))
+
+    # ------------------------------- target layouts as device buffers (re-deal)
+    def target_layout_bytes(self, k: int = 0) -> int:
+        """Size of target k's device-state buffer (orpcd_target_layout_bytes)."""
+        n = int(self._L.orpcd_target_layout_bytes(self._h, int(k)))
+        if n < 0:
+            msg = self._L.orpcd_last_error(self._h)
+            raise ValueError(f"orpcd_target_layout_bytes: {msg.decode() if msg else ''}")
+        return n
+
+    def get_target_layout(self, k: int, dev_ptr: int, nbytes: int):
+        """Write target k's device state to device memory at dev_ptr (>= target_layout_bytes(k), 256-byte
+        aligned, on this context's device; e.g. a torch uint8 tensor's data_ptr())."""
+        self._check(self._L.orpcd_get_target_layout(self._h, int(k), ctypes.c_void_p(int(dev_ptr)), int(nbytes)),
+                    "orpcd_get_target_layout")
+
+    def set_target_layouts(self, dev_ptrs, key=None):
+        """Adopt up to 16 target buffers written by get_target_layout (on any context) as targets 0..n-1, as
+        set_targets would have built them.  `key`: the set_targets cache key of the same clouds, if known."""
+        arr = (ctypes.c_void_p * len(dev_ptrs))(*[ctypes.c_void_p(int(p)) for p in dev_ptrs])
+        self._target_key = None
+        self._check(self._L.orpcd_set_target_layouts(self._h, arr, len(dev_ptrs)), "orpcd_set_target_layouts")
+        self._target_key = key
 
     def set_target_points(self, xyz: np.ndarray, cache: bool = True):
         """The target's search layout (covariances skipped) for PointToPoint ICP."""

@@ -19,6 +19,11 @@
    (max over ranks of phase 1 + max of phase 2 + one more all-gather at
    --allgather-us); both plus the host time outside the batches from
    profiles (--host-s).  Reported against T1 (--t1-s, the 1-GPU align()).
+4. --move-layouts 1 (round 6): in phase 2 a rank ADOPTS the device layouts of
+   the targets its share needs (orpcd_set_target_layouts, written once by
+   their phase-1 owner with orpcd_get_target_layout) instead of building them
+   again; the layouts it did not own are charged at --xgmi-gbps, and each
+   owner's serialisation time is added to its phase 1.
 A projection from one GPU, not an 8-GPU measurement.
 """
 import argparse
@@ -41,6 +46,9 @@ def main():
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--passes", default="16,24,32")
     ap.add_argument("--allgather-us", type=float, default=50.0)
+    ap.add_argument("--move-layouts", type=int, default=1)
+    ap.add_argument("--xgmi-gbps", type=float, default=50.0,
+                    help="point-to-point rate charged for a moved layout (one xGMI link, conservative)")
     ap.add_argument("--out", default=None)
     a = ap.parse_args()
     from orpcd_amd import Aligner, GeneralizedICP, Preprocessor, _native, parallel
@@ -114,6 +122,38 @@ def main():
                                   state=state, **prm)
         return time.perf_counter() - t0, r
 
+    builder = _native.Context(0)  # the phase-1 owners' contexts, as far as their layouts go
+
+    def layouts_for(call):
+        """Every target's device layout of one batch, as its phase-1 owner writes it: (tensor, ptr, bytes,
+        seconds to write)."""
+        if "lay" not in call:
+            import torch
+            builder.set_targets(call["targets"], 1e-3, cache=False)
+            lay = []
+            for k in range(len(call["targets"])):
+                n = builder.target_layout_bytes(k)
+                t = torch.empty(n + 256, dtype=torch.uint8, device="cuda")
+                ptr = t.data_ptr() + (-t.data_ptr()) % 256
+                t0 = time.perf_counter()
+                builder.get_target_layout(k, ptr, n)
+                lay.append((t, ptr, n, time.perf_counter() - t0))
+            call["lay"] = lay
+        return call["lay"]
+
+    def run_adopt(call, idx, owned, pass_begin, state):
+        """Phase 2 of one rank with moved layouts: adopt, then resume; plus the charged transfer."""
+        flat_k, flat_R, flat_t = call["flat"]
+        ks = sorted(set(flat_k[idx].tolist()))
+        lay = layouts_for(call)
+        moved = sum(lay[k][2] for k in ks if k not in owned)
+        t0 = time.perf_counter()
+        ctx.set_target_layouts([lay[k][1] for k in ks])
+        ctx.set_source(call["source"])
+        tids = np.searchsorted(ks, flat_k[idx]).astype(np.int32)
+        r = ctx.gicp_batch_window(flat_R[idx], flat_t[idx], tids, pass_begin=pass_begin, state=state, **prm)
+        return time.perf_counter() - t0 + moved / (a.xgmi_gbps * 1e9), r, moved
+
     for call in calls:
         K = len(call["draws"])
         B = a.attempts
@@ -146,13 +186,17 @@ def main():
            "no_redeal": {"sum_batch_max_s": round(sum(max(t) for t in base), 4),
                          "rank_s": [[round(x, 5) for x in t] for t in base]}}
     for P in [int(x) for x in a.passes.split(",")]:
-        ph1, ph2, moved, identical = [], [], [], True
+        ph1, ph2, moved, identical, moved_bytes = [], [], [], True, []
         for call, rec in zip(calls, ref):
             n = len(call["flat"][0])
-            t_1, done, state = [], np.zeros(n, bool), np.zeros((n, 18))
+            t_1, done, state, owned = [], np.zeros(n, bool), np.zeros((n, 18)), []
             for r in range(G):
                 lo, hi = parallel.shard(n, r, G)
                 dt, res = run(call, np.arange(lo, hi), pass_end=P)
+                own = set(call["flat"][0][lo:hi].tolist())
+                owned.append(own)
+                if a.move_layouts:  # the owner writes its targets' layouts for the others
+                    dt += sum(layouts_for(call)[k][3] for k in own)
                 t_1.append(dt)
                 done[lo:hi] = res["done"]
                 state[lo:hi] = res["state"]
@@ -167,7 +211,11 @@ def main():
                 if len(idx) == 0:
                     t_2.append(0.0)
                     continue
-                dt, res = run(call, idx, pass_begin=P, state=state[idx])
+                if a.move_layouts:
+                    dt, res, mb = run_adopt(call, idx, owned[r], P, state[idx])
+                    moved_bytes.append(mb)
+                else:
+                    dt, res = run(call, idx, pass_begin=P, state=state[idx])
                 t_2.append(dt)
                 for i, f in enumerate(idx):
                     identical &= rec[f] == tuple(np.asarray(res[k][i]).tobytes() for k in ("T", "rmse", "iters"))
@@ -177,7 +225,8 @@ def main():
         tot = sum(max(x) for x in ph1) + sum(max(x) for x in ph2) + len(calls) * a.allgather_us * 1e-6
         out[f"redeal_P{P}"] = {"sum_s": round(tot, 4), "phase1_max_s": [round(max(x), 5) for x in ph1],
                                "phase2_max_s": [round(max(x), 5) for x in ph2], "running_at_P": moved,
-                               "bit_identical": bool(identical)}
+                               "bit_identical": bool(identical), "move_layouts": bool(a.move_layouts),
+                               "moved_layout_mb_per_rank_max": round(max(moved_bytes, default=0) / 1e6, 2)}
         print(f"P={P}: {tot:.4f} s vs {out['no_redeal']['sum_batch_max_s']:.4f} s, identical {identical}",
               file=sys.stderr, flush=True)
     s = json.dumps(out)
