@@ -161,6 +161,10 @@ int orpcd_gicp_batch_window(orpcd_ctx* ctx, const double* R0, const double* t0, 
  * same clouds and epsilon (bit for bit: batches on them return the same
  * results).  Replaces orpcd_set_targets.                                    */
 int64_t orpcd_target_layout_bytes(orpcd_ctx* ctx, int32_t k);
+/* device memory on ctx's device for such buffers, for callers without an
+ * allocator of their own (256-byte aligned); freed by orpcd_device_free.    */
+int orpcd_device_alloc(orpcd_ctx* ctx, int64_t bytes, void** dev_out);
+int orpcd_device_free(orpcd_ctx* ctx, void* dev);
 int orpcd_get_target_layout(orpcd_ctx* ctx, int32_t k, void* dev_out, int64_t bytes);
 int orpcd_set_target_layouts(orpcd_ctx* ctx, const void* const* dev_in, int32_t ntargets);
 

@@ -2310,6 +2310,24 @@ int64_t orpcd_target_layout_bytes(orpcd_ctx* c, int32_t k) {
     return (int64_t)layout_header(c->tgts[k], c->tgt_eps[k]).total;
 }
 
+int orpcd_device_alloc(orpcd_ctx* c, int64_t bytes, void** dev_out) {
+    if (!c) return ORPCD_EINVAL;
+    CTX_REQUIRE(c, dev_out && bytes > 0, "device_alloc: bad arguments");
+    *dev_out = nullptr;
+    CTX_CHECK(c, hipSetDevice(c->device));
+    CTX_CHECK(c, hipMalloc(dev_out, (size_t)bytes));  // hipMalloc: 256-byte aligned at least
+    return ORPCD_OK;
+}
+
+int orpcd_device_free(orpcd_ctx* c, void* dev) {
+    if (!c) return ORPCD_EINVAL;
+    if (!dev) return ORPCD_OK;
+    CTX_CHECK(c, hipSetDevice(c->device));
+    CTX_CHECK(c, hipStreamSynchronize(c->stream));
+    CTX_CHECK(c, hipFree(dev));
+    return ORPCD_OK;
+}
+
 int orpcd_get_target_layout(orpcd_ctx* c, int32_t k, void* dev_out, int64_t bytes) {
     if (!c) return ORPCD_EINVAL;
     CTX_REQUIRE(c, k >= 0 && k < c->ntgt, "get_target_layout: no such target");
@@ -2355,7 +2373,8 @@ int orpcd_set_target_layouts(orpcd_ctx* c, const void* const* dev_in, int32_t nt
         }
         const LayoutHeader want = layout_header(L, h.eps);  // the sizes this layout implies
         for (int i = 0; i < kLaySections; ++i)
-            CTX_REQUIRE(c, i == kLaySgrid ? (h.len[i] == 0 || h.len[i] == want.len[i]) : h.len[i] == want.len[i],
+            CTX_REQUIRE(c, i == kLaySgrid ? (h.len[i] == 0 || h.len[i] == (uint64_t)kSeedGrid * kSeedGrid * kSeedGrid * 4)
+                                          : h.len[i] == want.len[i],
                         "set_target_layouts: inconsistent layout header");
         CTX_CHECK(c, L.xyz64.ensure((size_t)L.npad * 3));
         CTX_CHECK(c, L.perm.ensure((size_t)L.n));

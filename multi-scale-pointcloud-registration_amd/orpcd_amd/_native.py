@@ -58,6 +58,7 @@ EXPORTED = ("orpcd_abi_version", "orpcd_build_id", "orpcd_build_flags", "orpcd_d
             "orpcd_gicp_shard_result", "orpcd_comm_unique_id", "orpcd_comm_init", "orpcd_comm_destroy",
             "orpcd_gicp_shard_run", "orpcd_gicp_batch_window", "orpcd_set_target_rows", "orpcd_target_cov_width", "orpcd_target_cov_rows",
             "orpcd_set_target_cov", "orpcd_target_layout_bytes", "orpcd_get_target_layout", "orpcd_set_target_layouts",
+            "orpcd_device_alloc", "orpcd_device_free",
             "orpcd_nn1_radius", "orpcd_estimate_normals", "orpcd_fpfh", "orpcd_fpfh_from_normals", "orpcd_fgr", "orpcd_feature_nn",
             "orpcd_fgr_optimize", "orpcd_fgr_optimize_batch", "orpcd_set_source_points", "orpcd_icp_p2p_batch",
             "orpcd_sor", "orpcd_voxel_down_sample", "orpcd_farthest_downsample",
@@ -175,6 +176,8 @@ def load_library():
         L.orpcd_target_layout_bytes.restype = c_i64
         L.orpcd_get_target_layout.argtypes = [vp, ctypes.c_int32, vp, c_i64]
         L.orpcd_set_target_layouts.argtypes = [vp, ctypes.POINTER(vp), ctypes.c_int32]
+        L.orpcd_device_alloc.argtypes = [vp, c_i64, ctypes.POINTER(vp)]
+        L.orpcd_device_free.argtypes = [vp, vp]
         L.orpcd_nn1_radius.argtypes = [vp, _f64p, c_i64, _f64p, c_i64, c_dbl, _i32p, _f64p]
         L.orpcd_estimate_normals.argtypes = [vp, _f64p, c_i64, ctypes.c_int32, c_dbl, c_dbl, vp, vp, vp]
         L.orpcd_fpfh.argtypes = [vp, _f64p, c_i64, c_dbl, ctypes.c_int32, c_dbl, ctypes.c_int32, _f64p, _f64p]
@@ -376,6 +379,15 @@ class Context:
             msg = self._L.orpcd_last_error(self._h)
             raise ValueError(f"orpcd_target_layout_bytes: {msg.decode() if msg else ''}")
         return n
+
+    def device_alloc(self, nbytes: int) -> int:
+        """Device memory on this context's device (orpcd_device_alloc); free with device_free."""
+        p = ctypes.c_void_p()
+        self._check(self._L.orpcd_device_alloc(self._h, int(nbytes), ctypes.byref(p)), "orpcd_device_alloc")
+        return int(p.value)
+
+    def device_free(self, dev_ptr: int):
+        self._check(self._L.orpcd_device_free(self._h, ctypes.c_void_p(int(dev_ptr))), "orpcd_device_free")
 
     def get_target_layout(self, k: int, dev_ptr: int, nbytes: int):
         """Write target k's device state to device memory at dev_ptr (>= target_layout_bytes(k), 256-byte

@@ -74,7 +74,6 @@ def test_target_layouts_moved_between_contexts_bit_identical():
     the same batch results bit for bit (the re-deal moves layouts between
     ranks instead of building them again); a foreign buffer is refused;
     another epsilon rebuilds the covariances from the adopted layout."""
-    import torch
     from orpcd_amd import _native
     src, tgt = small_pair(6007, 5003, seed=11)
     targets = [tgt, tgt * np.array([1.1, 1.0, 0.9]), tgt * np.array([0.95, 1.05, 1.0])]
@@ -83,10 +82,11 @@ def test_target_layouts_moved_between_contexts_bit_identical():
     bufs = []
     for k in range(len(targets)):
         n = a.target_layout_bytes(k)
-        t = torch.empty(n + 256, dtype=torch.uint8, device="cuda")
-        ptr = t.data_ptr() + (-t.data_ptr()) % 256
+        ptr = a.device_alloc(n)
         a.get_target_layout(k, ptr, n)
-        bufs.append((t, ptr))
+        bufs.append((n, ptr))
+    with pytest.raises(ValueError):                   # smaller than the layout
+        a.get_target_layout(0, bufs[0][1], bufs[0][0] - 1)
     b.set_target_layouts([p for _, p in bufs[::-1]])  # another order: targets 2, 1, 0
     R0, t0 = _starts(12, 5)
     tos = (np.arange(12) % 3).astype(np.int32)
@@ -97,14 +97,15 @@ def test_target_layouts_moved_between_contexts_bit_identical():
     rb = b.gicp_batch_window(R0, t0, (2 - tos).astype(np.int32), **prm)
     for k in KEYS:
         assert np.array_equal(ra[k], rb[k]), k
-    junk = torch.zeros(4096, dtype=torch.uint8, device="cuda")
-    with pytest.raises(ValueError):
-        b.set_target_layouts([junk.data_ptr()])
+    with pytest.raises(ValueError):                   # not a layout: a layout's point section
+        b.set_target_layouts([bufs[0][1] + 256 * ((bufs[0][0] // 2) // 256)])
     b.set_target_layouts([p for _, p in bufs])
     prm = dict(max_correspondence_distance=0.3, epsilon=1e-2)  # covariances for another epsilon
     ra = a.gicp_batch_window(R0, t0, tos, **prm)
     rb = b.gicp_batch_window(R0, t0, tos, **prm)
     for k in KEYS:
         assert np.array_equal(ra[k], rb[k]), k
+    for _, p in bufs:
+        a.device_free(p)
     a.close()
     b.close()
