@@ -1105,6 +1105,96 @@ hipError_t launch_feat_nn(const double* Fq, const double* nq2, int64_t nq, const
     return hipGetLastError();
 }
 
+// Answers of duplicate rows from their representatives' (dedup_rows' runs:
+// sorted position p holds row vs[p]; a row that is not its own
+// representative (uflag 0) equals the row at its run head): identical query
+// rows have identical answers, so a search runs over the distinct rows only.
+__global__ void unique_pos_kernel(const int32_t* __restrict__ uidx, int nu, int32_t* __restrict__ pos) {
+    const int k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k < nu) pos[uidx[k]] = k;
+}
+
+__global__ void expand_dup_kernel(const int32_t* __restrict__ vs, const int32_t* __restrict__ head,
+                                  const unsigned char* __restrict__ uflag, int n, const int32_t* __restrict__ pos,
+                                  const int32_t* __restrict__ out_u, int32_t* __restrict__ out) {
+    const int p = blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= n) return;
+    const int i = vs[p];
+    const int r = uflag[i] ? i : vs[head[p]];
+    out[i] = out_u[pos[r]];
+}
+
+hipError_t expand_dup_answers(const DedupBufs& b, int64_t n, int64_t nu, const int32_t* out_u, int32_t* pos,
+                              int32_t* out, hipStream_t s) {
+    if (n <= 0) return hipSuccess;
+    unique_pos_kernel<<<(unsigned)((nu + 255) / 256), 256, 0, s>>>(b.uidx.p, (int)nu, pos);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    expand_dup_kernel<<<(unsigned)((n + 255) / 256), 256, 0, s>>>(b.val.p + n, b.head.p, b.uflag.p, (int)n, pos,
+                                                                  out_u, out);
+    return hipGetLastError();
+}
+
+// AdvancedMatching's cross check keeps (i, i_to_j[i]) only when
+// j_to_i[i_to_j[i]] == i, so the second direction's search matters only for
+// the rows i that some j chose: they are compacted here (needed_rows) and
+// their answers scattered back (scatter_answers); every other i keeps -1,
+// which the cross check rejects as it rejects a non-mutual match.
+__global__ void need_flags_kernel(const int32_t* __restrict__ j_to_i, int nj, int ni, unsigned char* __restrict__ flag) {
+    const int j = blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= nj) return;
+    const int i = j_to_i[j];
+    if (i >= 0 && i < ni) flag[i] = 1;  // racing writers store the same byte
+}
+
+__global__ void scatter_answers_kernel(const int32_t* __restrict__ idx, int n, const int32_t* __restrict__ ans,
+                                       int32_t* __restrict__ out) {
+    const int k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k < n) out[idx[k]] = ans[k];
+}
+
+hipError_t needed_rows(const int32_t* j_to_i, int64_t nj, const double* F, const double* n2, int64_t ni,
+                       NeedBufs& b, int64_t* nq_out, hipStream_t s) {
+    hipError_t e;
+    *nq_out = 0;
+    if (ni <= 0) return hipSuccess;
+    if ((e = b.flag.ensure((size_t)ni)) != hipSuccess) return e;
+    if ((e = b.idx.ensure((size_t)ni + 1)) != hipSuccess) return e;
+    if ((e = b.out.ensure((size_t)ni)) != hipSuccess) return e;
+    if ((e = hipMemsetAsync(b.flag.p, 0, (size_t)ni, s)) != hipSuccess) return e;
+    if (nj > 0) {
+        need_flags_kernel<<<(unsigned)((nj + 255) / 256), 256, 0, s>>>(j_to_i, (int)nj, (int)ni, b.flag.p);
+        if ((e = hipGetLastError()) != hipSuccess) return e;
+    }
+    int32_t* nsel = b.idx.p + ni;
+    size_t tmp = 0;
+    if ((e = hipcub::DeviceSelect::Flagged(nullptr, tmp, hipcub::CountingInputIterator<int32_t>(0), b.flag.p, b.idx.p,
+                                           nsel, (int)ni, s)) != hipSuccess)
+        return e;
+    if ((e = b.tmp.ensure(tmp)) != hipSuccess) return e;
+    if ((e = hipcub::DeviceSelect::Flagged(b.tmp.p, tmp, hipcub::CountingInputIterator<int32_t>(0), b.flag.p, b.idx.p,
+                                           nsel, (int)ni, s)) != hipSuccess)
+        return e;
+    int32_t nq = 0;
+    if ((e = d2h(&nq, nsel, 4, s)) != hipSuccess) return e;
+    if ((e = hipStreamSynchronize(s)) != hipSuccess) return e;
+    if (nq > 0) {
+        if ((e = b.F.ensure((size_t)nq * kFD)) != hipSuccess) return e;
+        if ((e = b.n2.ensure((size_t)nq)) != hipSuccess) return e;
+        gather_rows_kernel<<<(unsigned)(((int64_t)nq * kFD + 255) / 256), 256, 0, s>>>(F, n2, b.idx.p, nq, b.F.p,
+                                                                                       b.n2.p);
+        if ((e = hipGetLastError()) != hipSuccess) return e;
+    }
+    *nq_out = nq;
+    return hipSuccess;
+}
+
+hipError_t scatter_answers(const int32_t* idx, int64_t n, const int32_t* ans, int32_t* out, hipStream_t s) {
+    if (n <= 0) return hipSuccess;
+    scatter_answers_kernel<<<(unsigned)((n + 255) / 256), 256, 0, s>>>(idx, (int)n, ans, out);
+    return hipGetLastError();
+}
+
 hipError_t dedup_rows(const double* F, const double* n2, int64_t n, DedupBufs& b, int64_t* nu_out, hipStream_t s) {
     hipError_t e;
     if ((e = b.key.ensure((size_t)n * 2)) != hipSuccess) return e;

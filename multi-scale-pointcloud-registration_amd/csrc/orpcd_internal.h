@@ -329,6 +329,24 @@ struct QueryOrder {
     DevBuf<unsigned char> tmp;
 };
 
+// The query rows the second direction of the mutual feature matching needs
+// (needed_rows): flags, their indices, the gathered rows and norms, the
+// search's answers for them.
+struct NeedBufs {
+    DevBuf<unsigned char> flag, tmp;
+    DevBuf<int32_t> idx, out, pos;
+    DevBuf<double> F, n2;
+    void release() {
+        flag.release();
+        tmp.release();
+        idx.release();
+        out.release();
+        pos.release();
+        F.release();
+        n2.release();
+    }
+};
+
 struct DedupBufs {
     DevBuf<unsigned long long> key;
     DevBuf<int32_t> val, head, uidx;
@@ -589,7 +607,8 @@ struct orpcd_ctx {
         orpcd::DevBuf<double> fn2[2];     // |f|^2
         orpcd::DevBuf<double> nrm, raw, nd2, spfh, red, pq, Tn;
         orpcd::DevBuf<int32_t> nbr, cnt, nn[2];
-        orpcd::DedupBufs dedup;
+        orpcd::DedupBufs dedup, dedup2;  // the two clouds' distinct feature rows (matching)
+        orpcd::NeedBufs need;
         orpcd::FeatNNBufs fnn;
         // orpcd_fgr_optimize_batch: the batch's posed sources (B x n x 3) and
         // their features (B x n x 36), per-target points / features /
@@ -662,6 +681,8 @@ struct orpcd_ctx {
             for (auto* b : {&nrm, &raw, &nd2, &spfh, &red, &pq, &Tn}) b->release();
             for (auto* b : {&nbr, &cnt}) b->release();
             dedup.release();
+            dedup2.release();
+            need.release();
             fnn.release();
         }
     } fgr;
@@ -824,6 +845,17 @@ hipError_t launch_feat_nn(const double* Fq, const double* nq2, int64_t nq, const
 // Representatives (lowest index) of the distinct rows of F (n x 36): b.uidx
 // (increasing), b.Fu / b.n2u their rows and norms; *nu_out their count.
 hipError_t dedup_rows(const double* F, const double* n2, int64_t n, DedupBufs& b, int64_t* nu_out, hipStream_t s);
+// the rows i of F (ni rows) that some j chose (j_to_i[j] == i, nj entries):
+// their indices in b.idx, the rows and norms gathered into b.F / b.n2, their
+// count in *nq_out (the stream drains once)
+hipError_t needed_rows(const int32_t* j_to_i, int64_t nj, const double* F, const double* n2, int64_t ni,
+                       NeedBufs& b, int64_t* nq_out, hipStream_t s);
+// out[i] = out_u[position of row i's representative in b.uidx] for the n rows
+// b was built from (pos: n ints of scratch)
+hipError_t expand_dup_answers(const DedupBufs& b, int64_t n, int64_t nu, const int32_t* out_u, int32_t* pos,
+                              int32_t* out, hipStream_t s);
+// out[idx[k]] = ans[k], k < n
+hipError_t scatter_answers(const int32_t* idx, int64_t n, const int32_t* ans, int32_t* out, hipStream_t s);
 hipError_t launch_fgr_irls(const double* p, double* q, int K, double par0, int iters, double division_factor,
                            double max_corr, int decrease_mu, double* T_out, hipStream_t s);
 // several IRLS problems in one launch each for the register- and the

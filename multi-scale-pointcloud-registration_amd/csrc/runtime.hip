@@ -691,13 +691,32 @@ int fgr_match(orpcd_ctx* c, const double* fsrc, int64_t n, const double* ftgt, i
     }
     CTX_CHECK(c, F.nn[0].ensure((size_t)nPtj));
     CTX_CHECK(c, F.nn[1].ensure((size_t)nPti));
-    int64_t nu = 0;
+    fgr_mark(s, "  feature norms");
+    // the distinct rows of both sets: direction 1 searches the distinct j
+    // rows against the distinct i rows (duplicates take their
+    // representative's answer: identical rows, identical answers), direction
+    // 2 the chosen i rows against the distinct j rows
+    int64_t nu = 0, nuj = 0;
     CTX_CHECK(c, dedup_rows(feat[fi], F.fn2[fi].p, nPti, F.dedup, &nu, s));
-    CTX_CHECK(c, launch_feat_nn(feat[fj], F.fn2[fj].p, nPtj, F.dedup.Fu.p, F.dedup.n2u.p, nu, F.dedup.uidx.p, 33,
-                                F.fnn, F.nn[0].p, s, c->profiling ? c->stats.feat : nullptr));
-    CTX_CHECK(c, dedup_rows(feat[fj], F.fn2[fj].p, nPtj, F.dedup, &nu, s));
-    CTX_CHECK(c, launch_feat_nn(feat[fi], F.fn2[fi].p, nPti, F.dedup.Fu.p, F.dedup.n2u.p, nu, F.dedup.uidx.p, 33,
-                                F.fnn, F.nn[1].p, s, c->profiling ? c->stats.feat : nullptr));
+    CTX_CHECK(c, dedup_rows(feat[fj], F.fn2[fj].p, nPtj, F.dedup2, &nuj, s));
+    fgr_mark(s, "  dedup (both sets)");
+    CTX_CHECK(c, F.need.out.ensure((size_t)std::max(nPti, nPtj)));
+    CTX_CHECK(c, F.need.pos.ensure((size_t)nPtj));
+    CTX_CHECK(c, launch_feat_nn(F.dedup2.Fu.p, F.dedup2.n2u.p, nuj, F.dedup.Fu.p, F.dedup.n2u.p, nu, F.dedup.uidx.p,
+                                33, F.fnn, F.need.out.p, s, c->profiling ? c->stats.feat : nullptr));
+    CTX_CHECK(c, expand_dup_answers(F.dedup2, nPtj, nuj, F.need.out.p, F.need.pos.p, F.nn[0].p, s));
+    fgr_mark(s, "  search j -> i (distinct rows)");
+    // the second direction for the rows i some j chose only: any other i
+    // fails the cross check whatever its answer (needed_rows)
+    int64_t nq = 0;
+    CTX_CHECK(c, needed_rows(F.nn[0].p, nPtj, feat[fi], F.fn2[fi].p, nPti, F.need, &nq, s));
+    CTX_CHECK(c, hipMemsetAsync(F.nn[1].p, 0xFF, (size_t)nPti * 4, s));
+    if (nq > 0) {
+        CTX_CHECK(c, launch_feat_nn(F.need.F.p, F.need.n2.p, nq, F.dedup2.Fu.p, F.dedup2.n2u.p, nuj, F.dedup2.uidx.p,
+                                    33, F.fnn, F.need.out.p, s, c->profiling ? c->stats.feat : nullptr));
+        CTX_CHECK(c, scatter_answers(F.need.idx.p, nq, F.need.out.p, F.nn[1].p, s));
+    }
+    fgr_mark(s, "  search i -> j (chosen rows)");
     fgr_mark(s, "feature matching");
     std::vector<int32_t> j_to_i((size_t)nPtj), i_to_j((size_t)nPti);
     CTX_CHECK(c, d2h(j_to_i.data(), F.nn[0].p, (size_t)nPtj * 4, s));
