@@ -232,7 +232,9 @@ __global__ __launch_bounds__(256) void knn_tiles_kernel(
         }
         if (dk < 3.0e38 && dk - dk1 <= ties.rel * dk + ties.abs_coef * sqrt(dk)) {
             const int e = atomicAdd(ties.cnt, 1);
-            if (e < ties.cap) {
+            if (ties.detect) {
+                if (e < ties.cap) ties.detect[e] = q;
+            } else if (e < ties.cap) {
                 int32_t* row = ties.rows + (size_t)e * (Kt + 2);
                 row[0] = q;
                 row[1] = perm[q];
@@ -475,7 +477,9 @@ __global__ __launch_bounds__(256) void knn_wave_kernel(
             int e = 0;
             if (lane == 0) e = atomicAdd(ties.cnt, 1);
             e = __builtin_amdgcn_readfirstlane(e);
-            if (e < ties.cap) {
+            if (ties.detect) {
+                if (lane == 0 && e < ties.cap) ties.detect[e] = q;
+            } else if (e < ties.cap) {
                 int32_t* row = ties.rows + (size_t)e * (K + 2);
                 if (lane == 0) {
                     row[0] = q;
@@ -765,6 +769,8 @@ static hipError_t launch_knn_lanes(const CloudLayout& L, const double* in64, int
         ORPCD_KNN_LANES(8);
     else if (K <= 20)
         ORPCD_KNN_LANES(20);
+    else if (K <= 21)
+        ORPCD_KNN_LANES(21);  // KNN-20 with its tie detection (the 21st neighbour)
     else if (K <= 24)
         ORPCD_KNN_LANES(24);
     else if (K <= 32)
@@ -830,7 +836,8 @@ hipError_t launch_knn_cov_ties(const CloudLayout& L, const double* in64, int kco
                                double* rawcov6, const KnnTieOut& ties, hipStream_t s, bool lane_per_query,
                                const int32_t* qlist, int64_t nq) {
     if (L.n <= 0) return hipSuccess;
-    const int K = kcov + kTieExtra;
+    // detect-only: the kcov + 1 nearest decide a tie; the listed pass keeps kcov + kTieExtra
+    const int K = ties.detect ? kcov + 1 : kcov + kTieExtra;
     if (kcov < 1 || K > 64) return hipErrorInvalidValue;
     if (qlist) {  // listed queries only: one wave each
         if (nq <= 0) return hipSuccess;

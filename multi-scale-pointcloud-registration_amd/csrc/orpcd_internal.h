@@ -436,6 +436,10 @@ struct KnnTieOut {
     double* d2 = nullptr;
     int cap = 0;
     double rel = 0.0, abs_coef = 0.0;
+    // detect-only mode (non-null): a tie point appends its Morton position
+    // here (at most cap) instead of its row, so the search needs only the
+    // kout + 1 nearest; its rows come from a second, listed pass
+    int32_t* detect = nullptr;
 };
 
 // ------------------------------------------------- several targets per batch
@@ -545,7 +549,8 @@ struct orpcd_ctx {
     orpcd::DevBuf<double> tie_ent;    // per batch: override entries {slot, position, raw covariance (6)}
     orpcd::DevBuf<int32_t> tie_rows;  // knn tie table (KnnTieOut)
     orpcd::DevBuf<double> tie_d2;
-    orpcd::DevBuf<int> tie_cnt;
+    orpcd::DevBuf<int> tie_cnt;       // [0] rows written, [1] tie points detected
+    orpcd::DevBuf<int32_t> tie_q;     // the detected points (Morton positions)
 
     // batch state (per start slot)
     orpcd::DevBuf<double> scov;     // B*N*kCovW posed-frame source covariance
