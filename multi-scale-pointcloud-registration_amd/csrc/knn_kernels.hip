@@ -473,7 +473,7 @@ __global__ __launch_bounds__(256) void knn_wave_kernel(
             return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
         };
         const double dk = lane_d(KC), dk1 = lane_d(KC - 1);
-        if (dk < INF && dk - dk1 <= ties.rel * dk + ties.abs_coef * sqrt(dk)) {
+        if (ties.force || (dk < INF && dk - dk1 <= ties.rel * dk + ties.abs_coef * sqrt(dk))) {
             int e = 0;
             if (lane == 0) e = atomicAdd(ties.cnt, 1);
             e = __builtin_amdgcn_readfirstlane(e);

@@ -440,6 +440,9 @@ struct KnnTieOut {
     // here (at most cap) instead of its row, so the search needs only the
     // kout + 1 nearest; its rows come from a second, listed pass
     int32_t* detect = nullptr;
+    // listed pass over detected points (knn_wave_kernel with a query list):
+    // every listed point writes its row, without testing the band again
+    int force = 0;
 };
 
 // ------------------------------------------------- several targets per batch

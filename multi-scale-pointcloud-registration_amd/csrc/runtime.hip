@@ -911,9 +911,12 @@ int source_ties_detect(orpcd_ctx* c, const CloudLayout& L, const double* dev_in6
     int ndet = 0;
     CTX_CHECK(c, d2h(&ndet, c->tie_cnt.p + 1, 4, c->stream));
     CTX_CHECK(c, hipStreamSynchronize(c->stream));
-    if (ndet > 0)
-        CTX_CHECK(c, launch_knn_cov_ties(L, dev_in64, kcov, margin, input_order, nullptr, to, c->stream, false,
+    if (ndet > 0) {
+        KnnTieOut rows = to;
+        rows.force = 1;  // detected already: every listed point writes its row
+        CTX_CHECK(c, launch_knn_cov_ties(L, dev_in64, kcov, margin, input_order, nullptr, rows, c->stream, false,
                                          c->tie_q.p, std::min(ndet, kTieCap)));
+    }
     int cnt = 0;
     CTX_CHECK(c, d2h(&cnt, c->tie_cnt.p, 4, c->stream));
     CTX_CHECK(c, hipStreamSynchronize(c->stream));
