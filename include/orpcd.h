@@ -368,6 +368,9 @@ int orpcd_fgr_optimize_batch(orpcd_ctx* ctx, const double* src, int64_t n, const
  *                   previous pass's measured cost (ordered dispatch)
  *   "sched_items", "sched_min_starts"  its split granularity, and the batch
  *                   size from which it is used
+ *   "sched_xcd"     0 (default) / 1: ordered dispatch, each XCD takes one
+ *                   contiguous chunk of a cost class's items (measured: no
+ *                   gain)
  *   "sched_cap_us"  ordered dispatch: plan no split longer than this many us
  *                   of the previous pass's measured cost (0: no cap)
  *   "seed_grid"     1 (default) / 0: every query's search bound is also
