@@ -88,10 +88,11 @@ def allgather_records(local: np.ndarray, B: int) -> np.ndarray:
     t = torch.from_numpy(buf).to(dev)
     outs = [torch.empty_like(t) for _ in range(ws)]
     dist.all_gather(outs, t)
+    allr = torch.stack(outs).cpu().numpy()  # one device-to-host copy for every rank's block
     table = np.zeros((B, REC))
     for r in range(ws):
         lo, hi = shard(B, r, ws)
-        table[lo:hi] = outs[r][: hi - lo].cpu().numpy()
+        table[lo:hi] = allr[r, : hi - lo]
     return table
 
 
