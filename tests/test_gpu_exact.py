@@ -305,3 +305,47 @@ def test_exact_correspondences_ragged_target_sizes(exact, oracle, m):
             assert np.all(d2 <= od2 * (1 + 2e-5) + 1e-30)
     finally:
         exact.set_option("exact_nn", 1)
+
+
+@pytest.mark.parametrize("extent", [1.0, 100.0])
+@pytest.mark.parametrize("rel", [0.0, 1e-9, 6e-8, 5e-7, 1e-5])
+def test_exact_adversarial_near_ties(exact, oracle, extent, rel):
+    """Near-ties at and below fp32's resolution: every posed query gets two
+    targets on opposite sides at distances r and r (1 + rel s) (s uniform in
+    [-1, 1], r in [1e-3, 1e-2] of the extent), among as many random decoys.
+    With rel below 2^-24 the fp32 keys cannot order the pair, and with the
+    extent at 100 the band's cloud-frame term (4.04 u A) is ~1e4 times the
+    distance term: the runner-up tracking, the band test and the fp64
+    re-search must still return the oracle's lexicographic (d^2, index)
+    minimum, index for index."""
+    rng = np.random.default_rng(int(rel * 1e12) + int(extent))
+    n = 2500
+    src = rng.uniform(-0.5, 0.5, size=(n, 3)) * extent
+    R0, t0 = rot_xyz(17.0, -23.0, 41.0)[None], np.array([[0.01, -0.02, 0.03]]) * extent
+    q = _posed(src, R0[0], t0[0])
+    u = rng.normal(size=(n, 3))
+    u /= np.linalg.norm(u, axis=1, keepdims=True)
+    r = rng.uniform(1e-3, 1e-2, size=(n, 1)) * extent
+    s = rng.uniform(-1.0, 1.0, size=(n, 1))
+    near = np.concatenate([q + r * u, q - r * (1.0 + rel * s) * u])
+    decoys = rng.uniform(-0.6, 0.6, size=(n, 3)) * extent
+    tgt = np.concatenate([near, decoys])
+    tgt = tgt[rng.permutation(len(tgt))]
+    exact.set_target(tgt)
+    exact.set_source(src)
+    exact.reset_stats()
+    exact.gicp_batch(R0, t0, max_correspondence_distance=0.05 * extent, max_iteration=0)
+    st = exact.stats()
+    _check_corr(exact, oracle, src, tgt, R0, t0, 0.05 * extent)
+    if rel <= 6e-8:  # pairs fp32 cannot order: most queries go to the fp64 re-search
+        assert st["exact_filed"] >= n // 2, st
+        # ... and the fp32 answers (exact_nn 0) differ from the oracle's for many of
+        # them: the case the exact mode exists for
+        exact.set_option("exact_nn", 0)
+        try:
+            exact.gicp_batch(R0, t0, max_correspondence_distance=0.05 * extent, max_iteration=0)
+            g = exact.gicp_correspondences(1, n)[0]
+        finally:
+            exact.set_option("exact_nn", 1)
+        oi, _ = oracle.nn1_radius(q, tgt, 0.05 * extent)
+        assert (g != oi).sum() >= n // 10, (g != oi).sum()
