@@ -185,8 +185,10 @@ int upload_target_k(orpcd_ctx* c, int k, const double* xyz, int64_t m, double ep
                                         ORPCD_NORMAL_COV ? c->tcovs[k].p : nullptr));
     }
     c->tgt_eps[k] = eps;
-    c->tgt_host[k].assign(xyz, xyz + 3 * m);
-    setup_mark(c->stream, "KNN-20 covariances + host copy");
+    // no host copy of the points: another epsilon rebuilds them from the
+    // device layout (targets_for_epsilon); a 1M-point copy cost ~1 ms per set-up
+    c->tgt_host[k].clear();
+    setup_mark(c->stream, "KNN-20 covariances");
     CTX_CHECK(c, c->tdesc.ensure(kMaxTargets));
     write_target_desc(c->tgts[k], c->tcovs[k].p, c->opt.seed_reps, c->opt.seed_grid != 0, c->tdesc_h[k]);
     CTX_CHECK(c, h2d(c->tdesc.p + k, &c->tdesc_h[k], sizeof(TargetDesc), c->stream));
@@ -216,8 +218,8 @@ int targets_for_epsilon(orpcd_ctx* c, int ntgt, double eps) {
     for (int k = 0; k < ntgt; ++k) {
         if (c->tgt_eps[k] == eps) continue;
         if (c->tgt_host[k].empty()) {
-            // an adopted layout (orpcd_set_target_layouts): the input-order
-            // points from its Morton-order fp64 points and permutation
+            // the input-order points from the layout's Morton-order fp64
+            // points and permutation (the set-up keeps no host copy)
             const CloudLayout& L = c->tgts[k];
             std::vector<double> mz((size_t)L.n * 3);
             std::vector<int32_t> perm((size_t)L.n);
@@ -228,7 +230,7 @@ int targets_for_epsilon(orpcd_ctx* c, int ntgt, double eps) {
             for (int64_t i = 0; i < L.n; ++i)
                 for (int a = 0; a < 3; ++a) c->tgt_host[k][3 * (size_t)perm[(size_t)i] + a] = mz[3 * (size_t)i + a];
         }
-        std::vector<double> host = c->tgt_host[k];
+        const std::vector<double> host = std::move(c->tgt_host[k]);
         int rc = upload_target_k(c, k, host.data(), c->tgts[k].n, eps);
         if (rc) return rc;
         CTX_CHECK(c, seed_grids(c, k, 1));
@@ -2282,7 +2284,7 @@ int orpcd_set_target_rows(orpcd_ctx* c, const double* xyz, int64_t m, double eps
                                    (ncclComm_t)c->comm, c->stream));
     }
     c->tgt_eps[0] = epsilon;
-    c->tgt_host[0].assign(xyz, xyz + 3 * m);
+    c->tgt_host[0].clear();  // rebuilt from the device layout if another epsilon is asked for
     CTX_CHECK(c, c->tdesc.ensure(kMaxTargets));
     write_target_desc(c->tgts[0], tcov, c->opt.seed_reps, c->opt.seed_grid != 0, c->tdesc_h[0]);
     CTX_CHECK(c, h2d(c->tdesc.p, &c->tdesc_h[0], sizeof(TargetDesc), c->stream));

@@ -496,3 +496,28 @@ def test_wave_solve_bit_identical(ctx, oracle):
     assert np.array_equal(ser.view(np.int64), wav.view(np.int64)), np.argwhere(ser.view(np.int64) != wav.view(np.int64))[:5]
     accepted = ~(np.abs(ser[:, 0]) < 1e-6) & np.isfinite(ser[:, 0])
     assert accepted.sum() > 1000 and (~accepted).sum() > 50  # both branches exercised
+
+
+def test_epsilon_change_rebuilds_target_bit_identical(ctx):
+    """A batch asking for another epsilon than the target was set up with
+    re-derives its covariances from the device layout's points (the set-up
+    keeps no host copy of the cloud): bit for bit a fresh set-up with that
+    epsilon, and back again."""
+    from orpcd_amd import _native
+    src, tgt = small_pair(3000, 3500, seed=21)
+    rng = np.random.default_rng(4)
+    R0 = np.array([rot_xyz(*rng.uniform(-20, 20, 3)) for _ in range(4)])
+    t0 = rng.normal(size=(4, 3)) * 0.05
+    fresh = _native.Context(0)
+    try:
+        for eps in (1e-2, 1e-3):
+            ctx.set_target(tgt, epsilon=1e-3 if eps == 1e-2 else 1e-2)
+            ctx.set_source(src)
+            r = ctx.gicp_batch(R0, t0, epsilon=eps)
+            fresh.set_target(tgt, epsilon=eps)
+            fresh.set_source(src)
+            f = fresh.gicp_batch(R0, t0, epsilon=eps)
+            for k in ("T", "rmse", "fitness", "iters", "ncorr"):
+                assert np.array_equal(r[k], f[k]), (eps, k)
+    finally:
+        fresh.close()
