@@ -67,3 +67,27 @@ def test_bench_failed_rank_fails_the_launch(tmp_path):
     r = _run(["--gpus", "2"] + COMMON, tmp_path, extra_env=dict(ORPCD_BENCH_OPTIMIZER="/nonexistent.py:X"),
              timeout=120)
     assert r.returncode != 0
+
+
+def test_bench_under_torch_distributed_run(tmp_path):
+    """The driver's own multi-GPU form: `python -m torch.distributed.run
+    --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port P
+    bench.py --gpus 2 ...` (WORLD_SIZE set by the launcher, so bench.py starts
+    no processes itself): one JSON line, from rank 0, with n_gpus 2."""
+    import socket
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    env = dict(os.environ, ORPCD_BENCH_OPTIMIZER=FAKE, ORPCD_BENCH_BACKEND="gloo",
+               ORPCD_FAKE_LOG=str(tmp_path / "calls.jsonl"), OMP_NUM_THREADS="1")
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT"):
+        env.pop(k, None)
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+                        "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.join(REPO, "bench.py"),
+                        "--gpus", "2"] + COMMON, env=env, cwd=str(tmp_path), capture_output=True, text=True,
+                       timeout=240)
+    assert r.returncode == 0, r.stderr[-3000:]
+    line = _line(r.stdout)
+    assert line["n_gpus"] == 2 and line["devices"] == [0, 1]
+    assert line["config"]["attempts_per_step"] == 60 and line["c4"]["n_gpus"] == 2
