@@ -87,8 +87,22 @@ __device__ __forceinline__ float gapf(float lo, float hi, float x, float margin)
     return fmaxf(0.0f, fmaxf(lo - x, x - hi) - margin);
 }
 
+// the packed lane-per-query network (knn_tiles_kernel): on by default
+#ifndef ORPCD_KNN_PACKED
+#define ORPCD_KNN_PACKED 1
+#endif
+constexpr int kKnnSlack = 3;        // keys kept beyond K (a boundary run of equal buckets up to this long)
+constexpr int kKnnPackedMaxK = 24;  // larger lists keep the exact network (their registers: 235-256 VGPRs)
+
+// waves per SIMD asked of the lane-per-query kernel for K <= 24 (the GICP
+// covariance lists): 3 (168 VGPRs; the packed network's state fits, the
+// spills are in the exact fallback and the final resolution) measured faster
+// than the compiler's 2 at C5; larger K keep the compiler's choice
+#ifndef ORPCD_KNN_LANE_WAVES
+#define ORPCD_KNN_LANE_WAVES 3
+#endif
 template <int K>
-__global__ __launch_bounds__(256) void knn_tiles_kernel(
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(K <= 24 ? ORPCD_KNN_LANE_WAVES : 1, 8))) void knn_tiles_kernel(
     const double* __restrict__ xyz64, const int32_t* __restrict__ perm, int n, const float4* __restrict__ tlo,
     const float4* __restrict__ thi, int ntiles, const float4* __restrict__ slo, const float4* __restrict__ shi,
     int nsuper, const double* __restrict__ in64, double r2, float margin, double ox, double oy, double oz, int kout,
@@ -105,17 +119,13 @@ __global__ __launch_bounds__(256) void knn_tiles_kernel(
                  qz = valid ? xyz64[3 * q + 2] : 0.0;
     double bd[K];
     int bi[K];
-#pragma unroll
-    for (int s = 0; s < K; ++s) {
-        bd[s] = r2;
-        bi[s] = -1;
-    }
-    // Two phases per staged tile: (1) every lane marks the candidates that
-    // beat its bound at tile start (the bound only shrinks, so this is a
-    // superset); (2) each lane walks only its own marks.  The wave then pays
-    // the insertion network max_lane(marks) times instead of once for every
-    // candidate that ANY lane takes.
-    auto scan_tile = [&](int t) {
+    const float inf = 3.0e38f;
+    const float fx = (float)(qx - ox), fy = (float)(qy - oy), fz = (float)(qz - oz);  // the boxes' fp32 frame
+    const float lox = wave_fmin(valid ? fx : inf), hix = wave_fmax(valid ? fx : -inf);
+    const float loy = wave_fmin(valid ? fy : inf), hiy = wave_fmax(valid ? fy : -inf);
+    const float loz = wave_fmin(valid ? fz : inf), hiz = wave_fmax(valid ? fz : -inf);
+    // stage tile t in LDS as fp64 SoA (+ input indices)
+    auto stage = [&](int t) {
         const int k = t * kTile + lane;
         const bool real = k < n;
         sx[w][lane] = real ? xyz64[3 * k] : 1e300;
@@ -125,95 +135,213 @@ __global__ __launch_bounds__(256) void knn_tiles_kernel(
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        auto dist = [&](int c) {
+    };
+    auto dist = [&](int c) {
 #pragma clang fp contract(off)
-            const double dx = qx - sx[w][c], dy = qy - sy[w][c], dz = qz - sz[w][c];
-            return dx * dx + dy * dy + dz * dz;
+        const double dx = qx - sx[w][c], dy = qy - sy[w][c], dz = qz - sz[w][c];
+        return dx * dx + dy * dy + dz * dz;
+    };
+    // The walk: own tile, then its Morton neighbours (a near-final bound
+    // before the culled walk), then the super-tiles / tiles whose boxes can
+    // still hold a point below some lane's bound.  visit(t) scans tile t;
+    // bound() is the lane's fp32 culling bound.
+    constexpr int kWin = 2;
+    auto walk = [&](auto&& visit, auto&& bound) {
+        visit(own);
+        for (int dt = 1; dt <= kWin; ++dt) {
+            if (own - dt >= 0) visit(own - dt);
+            if (own + dt < ntiles) visit(own + dt);
+        }
+        for (int sb = 0; sb < nsuper; sb += 64) {
+            float Wb = wave_fmax(bound());
+            const int u = sb + lane;
+            float sl = inf;
+            if (u < nsuper) {
+                const float4 c = slo[u], d = shi[u];
+                const float dx = fmaxf(0.0f, fmaxf(c.x - hix, lox - d.x) - margin);
+                const float dy = fmaxf(0.0f, fmaxf(c.y - hiy, loy - d.y) - margin);
+                const float dz = fmaxf(0.0f, fmaxf(c.z - hiz, loz - d.z) - margin);
+                sl = dx * dx + dy * dy + dz * dz;
+            }
+            unsigned long long smask = __ballot(sl < Wb);
+            while (smask) {
+                const int su = sb + __builtin_ctzll(smask);
+                smask &= smask - 1;
+                Wb = wave_fmax(bound());
+                const int t = su * kSuper + lane;
+                float lb = inf;
+                float4 a = make_float4(0.f, 0.f, 0.f, 0.f), b = a;
+                if (t < ntiles && (t < own - kWin || t > own + kWin)) {
+                    a = tlo[t];
+                    b = thi[t];
+                    const float dx = fmaxf(0.0f, fmaxf(a.x - hix, lox - b.x) - margin);
+                    const float dy = fmaxf(0.0f, fmaxf(a.y - hiy, loy - b.y) - margin);
+                    const float dz = fmaxf(0.0f, fmaxf(a.z - hiz, loz - b.z) - margin);
+                    lb = dx * dx + dy * dy + dz * dz;
+                }
+                unsigned long long mask = __ballot(lb < Wb);
+                while (mask) {
+                    const int k = __builtin_ctzll(mask);
+                    mask &= mask - 1;
+                    const float ax = __shfl(a.x, k, 64), ay = __shfl(a.y, k, 64), az = __shfl(a.z, k, 64);
+                    const float bx = __shfl(b.x, k, 64), by = __shfl(b.y, k, 64), bz = __shfl(b.z, k, 64);
+                    const float gx = gapf(ax, bx, fx, margin), gy = gapf(ay, by, fy, margin),
+                                gz = gapf(az, bz, fz, margin);
+                    const bool need = valid && gx * gx + gy * gy + gz * gz < bound();
+                    if (__ballot(need) == 0ull) continue;
+                    visit(su * kSuper + k);
+                }
+            }
+        }
+    };
+    auto to_bound = [&](double b) -> float {  // fp32 upper bound of a d^2 bound
+        return b >= 3.0e38 ? inf : (float)b * 1.0000003f + 1e-37f;
+    };
+    // The exact network: the K best (d^2, input index) so far, sorted.  Two
+    // phases per staged tile: (1) every lane marks the candidates that beat
+    // its bound at tile start (the bound only shrinks, so this is a
+    // superset); (2) each lane walks only its own marks.  The wave then pays
+    // the insertion network max_lane(marks) times instead of once for every
+    // candidate that ANY lane takes.
+    auto exact_walk = [&]() {
+#pragma unroll
+        for (int s = 0; s < K; ++s) {
+            bd[s] = r2;
+            bi[s] = -1;
+        }
+        auto visit = [&](int t) {
+            stage(t);
+            const double b0 = bd[K - 1];
+            unsigned long long marks = 0;
+#pragma unroll 8
+            for (int c = 0; c < kTile; ++c) marks |= (unsigned long long)(dist(c) <= b0) << c;
+            if (!valid) marks = 0;
+            while (marks) {
+                const int c = __builtin_ctzll(marks);
+                marks &= marks - 1;
+                const double d = dist(c);
+                const int id = sid[w][c];
+                if (d < bd[K - 1] || (d == bd[K - 1] && bi[K - 1] >= 0 && id < bi[K - 1])) {
+                    double cd = d;
+                    int ci = id;
+#pragma unroll
+                    for (int s = 0; s < K; ++s) {
+                        const bool sw = cd < bd[s] || (cd == bd[s] && (unsigned)ci < (unsigned)bi[s]);
+                        const double td = bd[s];
+                        const int ti = bi[s];
+                        bd[s] = sw ? cd : td;
+                        bi[s] = sw ? ci : ti;
+                        cd = sw ? td : cd;
+                        ci = sw ? ti : ci;
+                    }
+                }
+            }
+            __builtin_amdgcn_wave_barrier();  // the stage is rewritten by the next tile
         };
-        const double b0 = bd[K - 1];
+        walk(visit, [&]() -> float { return valid ? to_bound(bd[K - 1]) : 0.0f; });
+    };
+    if constexpr (ORPCD_KNN_PACKED && K <= kKnnPackedMaxK) {
+    // The packed network (default for K <= kKnnPackedMaxK): one 64-bit key per kept candidate, the
+    // fp64 d^2 bits truncated to their top 37 (a bucket of relative width
+    // 2^-25) over the 27-bit input index (kMaxPoints = 2^27).  Keys are
+    // unique, and their order is (bucket, index): a compare-exchange is one
+    // 64-bit compare and four selects instead of the exact pair's three
+    // compares and six selects.  The list keeps KL = K + kKnnSlack keys;
+    // culling uses the upper end of the K-th key's bucket, so every point in a
+    // bucket at most the K-th's is scanned.  At the end the keys whose bucket
+    // is at most the K-th's are a superset of the exact K nearest (a point
+    // outside it has a larger bucket, hence a larger d^2, than K kept ones)
+    // whenever the list's last key lies in a larger bucket than the K-th;
+    // their fp64 d^2 is recomputed (the same expression) and equal-bucket runs
+    // are put in (d^2, index) order.  Otherwise a run of equal buckets may
+    // continue past the list and the wave re-runs the exact network.
+    constexpr int KL = K + kKnnSlack;
+    constexpr unsigned long long kIdxMask = (1ull << 27) - 1ull, kBucketMask = ~kIdxMask, kEmpty = ~0ull;
+    static_assert(kMaxPoints <= (int64_t)(1ull << 27), "the key's index field holds every input index");
+    auto bucket_hi = [&](unsigned long long key) -> double {  // the largest d^2 of key's bucket (r2 if empty)
+        return key == kEmpty ? r2 : fmin(r2, __longlong_as_double((long long)(key | kIdxMask)));
+    };
+    unsigned long long bk[KL];
+#pragma unroll
+    for (int s = 0; s < KL; ++s) bk[s] = kEmpty;
+    auto visit = [&](int t) {
+        stage(t);
+        // marks: below r2 and in a bucket at most the K-th key's (at tile start).
+        // A point left out -- unmarked, or marked when KL smaller keys were
+        // already kept -- has a key above the final list's last one, so the
+        // overflow test below sees any such point in the K-th key's bucket
+        const double b0 = bucket_hi(bk[K - 1]);
         unsigned long long marks = 0;
 #pragma unroll 8
-        for (int c = 0; c < kTile; ++c) marks |= (unsigned long long)(dist(c) <= b0) << c;
+        for (int c = 0; c < kTile; ++c) {
+            const double d = dist(c);
+            marks |= (unsigned long long)(d <= b0 && d < r2) << c;
+        }
         if (!valid) marks = 0;
         while (marks) {
             const int c = __builtin_ctzll(marks);
             marks &= marks - 1;
-            const double d = dist(c);
-            const int id = sid[w][c];
-            if (d < bd[K - 1] || (d == bd[K - 1] && bi[K - 1] >= 0 && id < bi[K - 1])) {
-                double cd = d;
-                int ci = id;
+            const unsigned long long key =
+                ((unsigned long long)__double_as_longlong(dist(c)) & kBucketMask) | (unsigned long long)sid[w][c];
+            if (key < bk[KL - 1]) {
+                unsigned long long ck = key;
 #pragma unroll
-                for (int s = 0; s < K; ++s) {
-                    const bool sw = cd < bd[s] || (cd == bd[s] && (unsigned)ci < (unsigned)bi[s]);
-                    const double td = bd[s];
-                    const int ti = bi[s];
-                    bd[s] = sw ? cd : td;
-                    bi[s] = sw ? ci : ti;
-                    cd = sw ? td : cd;
-                    ci = sw ? ti : ci;
+                for (int s = 0; s < KL; ++s) {
+                    const bool sw = ck < bk[s];
+                    const unsigned long long t2 = bk[s];
+                    bk[s] = sw ? ck : t2;
+                    ck = sw ? t2 : ck;
                 }
             }
         }
         __builtin_amdgcn_wave_barrier();  // the stage is rewritten by the next tile
     };
-    // own tile, then its Morton neighbours: a near-final bound before the walk
-    constexpr int kWin = 2;
-    scan_tile(own);
-    for (int dt = 1; dt <= kWin; ++dt) {
-        if (own - dt >= 0) scan_tile(own - dt);
-        if (own + dt < ntiles) scan_tile(own + dt);
+    walk(visit, [&]() -> float { return valid ? to_bound(bucket_hi(bk[K - 1])) : 0.0f; });
+    const unsigned long long tK = bk[K - 1] & kBucketMask;
+    const bool overflow = valid && bk[K - 1] != kEmpty && (bk[KL - 1] & kBucketMask) == tK;
+    if (__ballot(overflow) != 0ull) {
+        exact_walk();
+    } else {
+        double cd[KL];
+        int ci[KL];
+#pragma unroll
+        for (int s = 0; s < KL; ++s) {
+            const bool use = bk[s] != kEmpty && (bk[s] & kBucketMask) <= tK;
+            ci[s] = use ? (int)(bk[s] & kIdxMask) : -1;
+            double d = r2;
+            if (use) {
+#pragma clang fp contract(off)
+                const int j = ci[s];
+                const double dx = qx - in64[3 * j], dy = qy - in64[3 * j + 1], dz = qz - in64[3 * j + 2];
+                d = dx * dx + dy * dy + dz * dz;
+            }
+            cd[s] = d;
+        }
+        // equal-bucket runs into (d^2, index) order: adjacent exchanges until
+        // none is needed (keys already order different buckets correctly)
+        for (;;) {
+            bool moved = false;
+#pragma unroll
+            for (int s = 0; s + 1 < KL; ++s) {
+                const bool sw = ci[s + 1] >= 0 && (cd[s + 1] < cd[s] || (cd[s + 1] == cd[s] && ci[s + 1] < ci[s]));
+                const double td = cd[s];
+                const int ti = ci[s];
+                cd[s] = sw ? cd[s + 1] : td;
+                ci[s] = sw ? ci[s + 1] : ti;
+                cd[s + 1] = sw ? td : cd[s + 1];
+                ci[s + 1] = sw ? ti : ci[s + 1];
+                moved |= sw;
+            }
+            if (__ballot(moved) == 0ull) break;
+        }
+#pragma unroll
+        for (int s = 0; s < K; ++s) {
+            bd[s] = ci[s] >= 0 ? cd[s] : r2;
+            bi[s] = ci[s];
+        }
     }
-
-    const float inf = 3.0e38f;
-    const float fx = (float)(qx - ox), fy = (float)(qy - oy), fz = (float)(qz - oz);  // the boxes' fp32 frame
-    const float lox = wave_fmin(valid ? fx : inf), hix = wave_fmax(valid ? fx : -inf);
-    const float loy = wave_fmin(valid ? fy : inf), hiy = wave_fmax(valid ? fy : -inf);
-    const float loz = wave_fmin(valid ? fz : inf), hiz = wave_fmax(valid ? fz : -inf);
-    auto lane_bound = [&]() -> float {  // fp32 upper bound of the lane's K-th distance
-        if (!valid) return 0.0f;
-        const double b = bd[K - 1];
-        return b >= 3.0e38 ? inf : (float)b * 1.0000003f + 1e-37f;
-    };
-    for (int sb = 0; sb < nsuper; sb += 64) {
-        float Wb = wave_fmax(lane_bound());
-        const int u = sb + lane;
-        float sl = inf;
-        if (u < nsuper) {
-            const float4 c = slo[u], d = shi[u];
-            const float dx = fmaxf(0.0f, fmaxf(c.x - hix, lox - d.x) - margin);
-            const float dy = fmaxf(0.0f, fmaxf(c.y - hiy, loy - d.y) - margin);
-            const float dz = fmaxf(0.0f, fmaxf(c.z - hiz, loz - d.z) - margin);
-            sl = dx * dx + dy * dy + dz * dz;
-        }
-        unsigned long long smask = __ballot(sl < Wb);
-        while (smask) {
-            const int su = sb + __builtin_ctzll(smask);
-            smask &= smask - 1;
-            Wb = wave_fmax(lane_bound());
-            const int t = su * kSuper + lane;
-            float lb = inf;
-            float4 a = make_float4(0.f, 0.f, 0.f, 0.f), b = a;
-            if (t < ntiles && (t < own - kWin || t > own + kWin)) {
-                a = tlo[t];
-                b = thi[t];
-                const float dx = fmaxf(0.0f, fmaxf(a.x - hix, lox - b.x) - margin);
-                const float dy = fmaxf(0.0f, fmaxf(a.y - hiy, loy - b.y) - margin);
-                const float dz = fmaxf(0.0f, fmaxf(a.z - hiz, loz - b.z) - margin);
-                lb = dx * dx + dy * dy + dz * dz;
-            }
-            unsigned long long mask = __ballot(lb < Wb);
-            while (mask) {
-                const int k = __builtin_ctzll(mask);
-                mask &= mask - 1;
-                const float ax = __shfl(a.x, k, 64), ay = __shfl(a.y, k, 64), az = __shfl(a.z, k, 64);
-                const float bx = __shfl(b.x, k, 64), by = __shfl(b.y, k, 64), bz = __shfl(b.z, k, 64);
-                const float gx = gapf(ax, bx, fx, margin), gy = gapf(ay, by, fy, margin), gz = gapf(az, bz, fz, margin);
-                const bool need = valid && gx * gx + gy * gy + gz * gz < lane_bound();
-                if (__ballot(need) == 0ull) continue;
-                scan_tile(su * kSuper + k);
-            }
-        }
+    } else {
+        exact_walk();
     }
     if (!valid) return;
     int c = 0;

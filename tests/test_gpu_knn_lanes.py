@@ -74,3 +74,28 @@ def test_source_ties_and_gicp_identical(pair, oracle):
     ra, rb = wave.gicp_batch(R0, t0), lane.gicp_batch(R0, t0)
     for k in ("T", "rmse", "iters"):
         assert np.array_equal(ra[k], rb[k]), k
+
+
+@pytest.mark.parametrize("kind", ["duplicates", "bucket_ties", "mixed"])
+@pytest.mark.parametrize("knn,radius", [(20, -1.0), (8, -1.0), (24, 0.2)])
+def test_packed_network_ties_identical(pair, kind, knn, radius):
+    """The lane kernel's packed network (64-bit keys: d^2 truncated to a
+    bucket of relative width 2^-25 over the input index) on clouds built to
+    stress it: exact duplicates (every point 2-7 times: equal-d^2 runs past
+    the list's slack, the exact fallback), copies displaced by ~1e-9 of the
+    extent (distinct fp64 d^2 in one bucket: the in-bucket exact re-order), and
+    both.  Normals / covariances identical to the wave kernel's, bit for bit."""
+    wave, lane = pair
+    rng = np.random.default_rng({"duplicates": 7, "bucket_ties": 8, "mixed": 9}[kind])
+    base = _cloud(3001, 4)
+    reps = rng.integers(2, 8, size=len(base))
+    x = np.repeat(base, reps, axis=0)
+    if kind != "duplicates":
+        tiny = rng.normal(size=x.shape) * 1e-9
+        if kind == "mixed":
+            tiny[rng.random(len(x)) < 0.5] = 0.0
+        x = x + tiny
+    x = x[rng.permutation(len(x))]
+    a, b = wave.estimate_normals(x, knn, radius), lane.estimate_normals(x, knn, radius)
+    for u, v in zip(a, b):
+        assert np.array_equal(u, v)
