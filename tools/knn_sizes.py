@@ -1,7 +1,12 @@
 """Set-up time (set_target / set_source) of the wave- and lane-per-query KNN at several cloud sizes:
     python tools/knn_sizes.py"""
+import os
+import sys
+import time
+
 import numpy as np
-REPO = "/root/repo"
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [os.path.join(REPO, "multi-scale-pointcloud-registration_amd"), REPO]
 from orpcd_amd import _native, Preprocessor
 from workloads import c2_pair, bumpy_sphere
