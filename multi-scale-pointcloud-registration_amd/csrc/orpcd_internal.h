@@ -724,7 +724,7 @@ struct orpcd_ctx {
                                   // C2 30 / 64 starts 15.50 -> 15.37 / 24.44 -> 24.23 ms, identical hashes,
                                   // profiles/r05_sched_cap_sweep*.log)
         int sched_cap_mult = 2;   // ... within an item budget of this many times sched_items
-        int knn_lane_min = 262144;  // clouds of at least this many points: lane-per-query KNN (0: never)
+        int knn_lane_min = 65536;   // clouds of at least this many points: lane-per-query KNN (0: never)
         int exact_nn = 1;         // 1 (default): every correspondence is the fp64 nearest target (the
                                   // oracle's lexicographic (d^2, input index) minimum): fp32 search +
                                   // runner-up band test + fp64 re-search of the uncertified queries;

@@ -1,5 +1,5 @@
 """GPU: the lane-per-query KNN (knn_tiles_kernel: one query per lane, the
-default from knn_lane_min = 262144 points on, i.e. C5's 1M-point clouds)
+default from knn_lane_min = 65536 points on: C3's 100k and C5's 1M-point clouds)
 returns what the wave-per-query KNN (knn_wave_kernel) returns, bit for bit, on
 every path that runs a KNN: raw covariances / normals / GICP covariances
 (pure KNN and hybrid radius), FPFH, SOR's mean distances, and the source's
