@@ -350,7 +350,8 @@ class Context:
 
     def set_target(self, xyz: np.ndarray, epsilon: float = 1e-3, cache: bool = True):
         xyz = _c3(xyz)
-        key = (self._key(xyz), float(epsilon))
+        # cache=False: no fingerprint (xxh3 reads the whole cloud: ~0.6 ms at 1M points)
+        key = (self._key(xyz), float(epsilon)) if cache else None
         if cache and key == self._target_key:
             return
         self._target_key = None
@@ -410,10 +411,11 @@ class Context:
         if cache and self._target_key is not None and self._target_key[0] == k:
             return  # any current layout of the same points serves
         self.set_target(xyz, -1.0, cache=False)
+        self._target_key = (k, -1.0)
 
     def set_source(self, xyz: np.ndarray, cache: bool = True):
         xyz = _c3(xyz)
-        key = (self._key(xyz), "cov")
+        key = (self._key(xyz), "cov") if cache else None
         if cache and key == self._source_key:
             return
         self._source_key = None
